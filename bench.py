@@ -1,0 +1,180 @@
+#!/usr/bin/env python3
+"""bench.py -- SGD updates/s of SVD k=100 on a MovieLens-1M-shaped set (BASELINE.json configs[1]).
+
+One step = one fast-mode SGD epoch (core/svd.go:92-130) over all 1,000,209 ratings, inputs resident
+in HBM (user-CSR + factors uploaded before the timed region).  N>1 GPUs: one process per GPU
+(torch.distributed, backend nccl = RCCL over xGMI); each rank owns its own item-range shard of
+ML-1M size (weak scaling, users replicated) and the user-factor / user-bias / global-bias deltas are
+all-reduced once per epoch (north_star item sharding).
+
+Prints ONE JSON line on rank 0 (contract in the task statement).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(REPO, "recommend-sys_amd"))
+
+METRIC = "SGD updates/sec, SVD k=100 MovieLens-1M, 1/2/4/8 GPU; % HBM roofline"
+K = 100
+LR, REG = 0.005, 0.02
+HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md chip table: 8.0 TB/s spec
+
+
+def algorithmic_bytes(nnz, n_users, k):
+    """nnz*(16 + 8k) + U*(16 + 8k) per epoch (fp32 factors, int32 idx, fp32 rating)."""
+    return nnz * (16 + 8 * k) + n_users * (16 + 8 * k)
+
+
+def cpu_baseline(u, i, r, n_users, n_items, budget_s=10.0):
+    """Times the C restatement of core/svd.go:63-132 (oracle, fp64, single thread) on whole epochs
+    of the same workload until ~budget_s of CPU work has run."""
+    sys.path.insert(0, os.path.join(REPO, "oracle"))
+    import oracle as O
+    rng = np.random.default_rng(0)
+    P, Q = rng.normal(0, 0.1, (n_users, K)), rng.normal(0, 0.1, (n_items, K))
+    bu, bi, gb = np.zeros(n_users), np.zeros(n_items), 0.0
+    epochs, t_total = 0, 0.0
+    while t_total < budget_s and epochs < 100:
+        t0 = time.perf_counter()
+        P, Q, bu, bi, gb = O.svd_fit(u, i, r, P, Q, bu, bi, gb, epochs=1, lr=LR, reg=REG)
+        t_total += time.perf_counter() - t0
+        epochs += 1
+    return {"value": len(r) * epochs / t_total, "unit": "updates/s", "cores": 1, "kind": "port",
+            "sample": f"{epochs} full epoch(s) of the same {len(r)}-rating set, C fp64 restatement "
+                      f"of core/svd.go:92-130 (oracle/), single thread, {t_total:.1f} s"}
+
+
+def load_traffic():
+    """HBM bytes per SGD launch measured by rocprofv3 --pmc (separate pass, committed summary)."""
+    p = os.path.join(REPO, "profiles", "sgd_traffic.json")
+    if os.path.exists(p):
+        try:
+            return json.load(open(p)).get("hbm_bytes_per_launch")
+        except Exception:
+            return None
+    return None
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-budget", type=float, default=10.0)
+    args = ap.parse_args()
+
+    import torch
+    import rsgpu
+    from rsgpu import synth
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl")
+    dev = local if world > 1 else 0
+    torch.cuda.set_device(dev)
+
+    # Weak scaling: each rank owns an ML-1M-sized item shard; users are shared (replicated).
+    u, i, r, n_users, n_items = synth.ml1m_like(seed=20250824 + rank)
+    nnz = len(r)
+    ctx = rsgpu.Context(dev)
+    plan = ctx.svd_plan(rsgpu.Ratings(u, i, r, n_users, n_items), K)
+    rng = np.random.default_rng(1)
+    P0 = rng.normal(0, 0.1, (n_users, K))  # identical on every rank (replicated user factors)
+    Q0 = np.random.default_rng(100 + rank).normal(0, 0.1, (n_items, K))
+    plan.upload(P0, Q0, np.zeros(n_users), np.zeros(n_items), 0.0)
+    stream = torch.cuda.current_stream(dev).cuda_stream
+
+    if world > 1:
+        import rsgpu.multi as multi
+        step = multi.ItemShardedStep(plan, ctx, dist, stream, total_nnz=nnz * world)
+        run = lambda n: step.run(n, LR, REG)
+    else:
+        run = lambda n: plan.epochs(n, LR, REG, stream)
+
+    for _ in range(args.warmup):
+        run(1)
+    torch.cuda.synchronize()
+    if dist:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    run(args.steps)
+    torch.cuda.synchronize()
+    if dist:
+        dist.barrier()
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    if dist:
+        t = torch.tensor([dt], dtype=torch.float64, device=f"cuda:{dev}")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        dt = float(t.item())
+
+    # kernel-only timing of the SGD kernel (HIP events on the launch stream), separate pass
+    plan.set_timing(True)
+    if world > 1:
+        step.run(5, LR, REG)
+    else:
+        plan.epochs(5, LR, REG, stream)
+    kms, nl = plan.last_kernel_ms()
+    plan.set_timing(False)
+    avg_kernel_s = kms / 1e3 / nl
+    P, Q, bu, bi, gb = plan.download()
+    finite = bool(np.isfinite(P).all() and np.isfinite(Q).all() and np.isfinite(gb))
+
+    if rank == 0:
+        total_updates = nnz * world * args.steps
+        ab = algorithmic_bytes(nnz, n_users, K)
+        achieved = ab / avg_kernel_s / 1e9
+        traffic = load_traffic() if world == 1 else None
+        line = {
+            "metric": METRIC,
+            "value": total_updates / dt,
+            "unit": "updates/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": dt / args.steps * 1e3,
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "f32",
+            "data": "synthetic ML-1M-shaped ratings (rsgpu/synth.py: 6040 users x 3706 items, "
+                    "1,000,209 ratings per rank, seed 20250824+rank); random-init factors N(0,0.1)",
+            "config": {"workload": "SVD nFactors=100 fast-mode SGD, 1 epoch over ML-1M-shaped set "
+                                   "per step (BASELINE configs[1])",
+                       "n_users": n_users, "n_items_per_rank": n_items, "nnz_per_rank": nnz,
+                       "n_factors": K, "lr": LR, "reg": REG,
+                       "parallelism": f"item-sharded x{world}" if world > 1 else "single GPU"},
+            "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS,
+                         "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
+                         "traffic": traffic,
+                         "kernel": "svd_epoch_fast_kernel<16,2>",
+                         "avg_kernel_us": avg_kernel_s * 1e6,
+                         "algorithmic_bytes_per_launch": ab},
+            "finite": finite,
+        }
+        if not args.no_cpu_baseline and world == 1:
+            line["cpu_baseline"] = cpu_baseline(u, i, r, n_users, n_items, args.cpu_budget)
+        print(json.dumps(line), flush=True)
+    plan.close()
+    ctx.close()
+    if dist:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

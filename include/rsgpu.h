@@ -1,0 +1,151 @@
+/*
+ * rsgpu.h -- C-ABI of the MI355X (gfx950) hot path for Oneaccount1/recommend-sys.
+ *
+ * This is the drop-in boundary: the entry points a cgo binding behind the reference's Go
+ * `core.Estimator` types would call (INTEGRATION.md shows the binding).  Plain pointers and sizes
+ * only; no torch or HIP types in the signatures (`stream` arguments are `hipStream_t` passed as
+ * `void*`, NULL = the context's own stream).
+ *
+ * Reference interfaces replaced (all paths relative to the reference repository root):
+ *   rs_svd_fit        <- core/svd.go:63-132    (*SVD).Fit            (per-epoch SGD, K1)
+ *   rs_svdpp_fit      <- core/svd.go:316-427   (*SVDPP).Fit          (K2)
+ *   rs_nmf_fit        <- core/svd.go:158-251   (*NMF).Fit            (K3)
+ *   rs_knn_sims       <- core/knn.go:224-298   (*KNN).Fit pair loop  (K4 Cosine/MSD, K5 Pearson)
+ *                        with core/sim.go:10-81 Cosine / MSD / Pearson as the pair function
+ *   rs_sim_pair       <- core/sim.go:7-81      Sim func(a, b SortedIdRatings) float64
+ *   rs_svd_predict    <- core/svd.go:32-51     (*SVD).Predict (batched; next-row §8f)
+ *   rs_baseline_fit   <- core/base.go:433-461  (*BaseLine).Fit (used by KNN-baseline knn.go:260)
+ *
+ * Conventions
+ *   - Ratings arrive as the TrainSet's COO triples (core/data.go:109-127) in TRAIN-SET ORDER with
+ *     INNER ids (core/data.go:131-154: ids assigned by first appearance).  The library builds the
+ *     user-CSR it needs itself and never retains a caller pointer after a call returns (cgo rule).
+ *   - Model state is float64 on the host side (the reference's [][]float64 rows, flattened row-major
+ *     with row stride = n_factors) and float32 on the device, converted at the boundary.
+ *   - Every call returns an int status: RS_OK (0) or a negative RS_ERR_*; the message is available
+ *     from rs_last_error(ctx) (thread-local when ctx is NULL).
+ *   - Re-entrant: no global mutable state; each rs_ctx owns one HIP stream on one device and every
+ *     entry point calls hipSetDevice(ctx->device) first (goroutines migrate OS threads).  A ctx must
+ *     not be used by two threads at once; use one ctx per goroutine / CrossValidate fold.
+ */
+#ifndef RSGPU_H
+#define RSGPU_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define RS_OK 0
+#define RS_ERR_INVALID (-1)     /* bad argument (null pointer, id out of range, bad size)        */
+#define RS_ERR_HIP (-2)         /* a HIP runtime call failed (message names it)                   */
+#define RS_ERR_NOMEM (-3)       /* host or device allocation failed                               */
+#define RS_ERR_UNSUPPORTED (-4) /* valid request this build does not implement                    */
+#define RS_ERR_NO_DEVICE (-5)   /* no gfx950 device visible                                       */
+
+/* SGD visit schedule (SURVEY §8a parity contract P1/P2) */
+#define RS_SGD_FAST 0    /* user-CSR, one 16-lane group per user, Hogwild q_i, deferred global bias */
+#define RS_SGD_ORDERED 1 /* single group, exact train-set order and update order of svd.go:93-129 */
+
+/* Similarity kinds: core/sim.go Cosine (10-25), MSD (28-44), Pearson (47-81) */
+#define RS_SIM_COSINE 0
+#define RS_SIM_MSD 1
+#define RS_SIM_PEARSON 2
+
+typedef struct rs_ctx rs_ctx;
+
+/* COO ratings of a TrainSet in train-set order, inner ids (core/data.go:21-25, 109-127). */
+typedef struct {
+    int64_t nnz;
+    int32_t n_users; /* TrainSet.UserCount */
+    int32_t n_items; /* TrainSet.ItemCount */
+    const int32_t* users;
+    const int32_t* items;
+    const double* ratings;
+} rs_ratings;
+
+/* Hyper-parameters read by SVD/SVD++ Fit (core/svd.go:65-71, 317-324). */
+typedef struct {
+    int32_t n_factors; /* "nFactors" */
+    int32_t n_epochs;  /* "nEpochs"  */
+    double lr;         /* "lr"       */
+    double reg;        /* "reg"      */
+    int32_t mode;      /* RS_SGD_FAST or RS_SGD_ORDERED */
+    int32_t reserved;
+} rs_sgd_params;
+
+/* ---- context -------------------------------------------------------------------------------- */
+int32_t rs_version(void);
+int rs_device_count(int32_t* n);
+int rs_open(int32_t device, rs_ctx** out);
+void rs_close(rs_ctx* ctx);
+const char* rs_last_error(const rs_ctx* ctx);
+int rs_synchronize(rs_ctx* ctx);
+
+/* ---- estimators (host buffers in/out) ------------------------------------------------------- */
+
+/* core/svd.go:63-132.  P (n_users x n_factors), Q (n_items x n_factors): injected initial factors
+ * in (svd.go:80-85 draws them; the draw is unseeded in the reference, Q4), fitted factors out.
+ * bu, bi, gb: in/out (the reference starts them at zero). */
+int rs_svd_fit(rs_ctx* ctx, const rs_ratings* r, const rs_sgd_params* p, double* P, double* Q,
+               double* bu, double* bi, double* gb);
+
+/* core/svd.go:32-51 for n (inner user, inner item) pairs; -1 = unknown id (data.go:129). */
+int rs_svd_predict(rs_ctx* ctx, int64_t n, const int32_t* users, const int32_t* items,
+                   int32_t n_users, int32_t n_items, int32_t n_factors, const double* P,
+                   const double* Q, const double* bu, const double* bi, double gb, double* out);
+
+/* core/svd.go:316-427.  Y (n_items x n_factors) = ImplFactor.  RS_SGD_ORDERED runs the literal
+ * per-rating y-update of svd.go:399-422; RS_SGD_FAST runs the user-CSR kernel with the lazy
+ * per-user y-update. */
+int rs_svdpp_fit(rs_ctx* ctx, const rs_ratings* r, const rs_sgd_params* p, double* P, double* Q,
+                 double* Y, double* bu, double* bi, double* gb);
+
+/* core/svd.go:158-251.  as_written=1 reproduces svd.go:243-249 (Q5), 0 the intended update. */
+int rs_nmf_fit(rs_ctx* ctx, const rs_ratings* r, int32_t n_factors, int32_t n_epochs, double reg,
+               int32_t as_written, double* P, double* Q);
+
+/* core/base.go:433-461 BaseLine.Fit (bias-only SGD, ORDERED semantics). */
+int rs_baseline_fit(rs_ctx* ctx, const rs_ratings* r, int32_t n_epochs, double lr, double reg,
+                    double* bu, double* bi, double* gb);
+
+/* core/knn.go:224-298 pair loop: sims (n_left x n_left, row-major float64) = sim(left_a, left_b)
+ * over the co-rated right ids, NaN where nothing is co-rated and on the diagonal (knn.go:238,283).
+ * Rows are CSR (rowptr[n_left+1], ids in [0, n_right), ratings) in any order within a row. */
+int rs_knn_sims(rs_ctx* ctx, int32_t kind, int32_t n_left, int32_t n_right, const int64_t* rowptr,
+                const int32_t* ids, const double* ratings, double* sims);
+
+/* core/sim.go one pair (ID-ascending inputs), computed on the device by the K5 merge kernel. */
+int rs_sim_pair(rs_ctx* ctx, int32_t kind, int64_t na, const int32_t* a_ids, const double* a_r,
+                int64_t nb, const int32_t* b_ids, const double* b_r, double* out);
+
+/* ---- device-resident SVD plan (bench / multi-GPU hosts; device pointers) -------------------- */
+/* A plan uploads the user-CSR once and keeps P, Q, bu, bi, gb resident in HBM (float32, row
+ * stride ld = round_up(n_factors, 4)).  Epochs are enqueued on `stream` without host syncs. */
+typedef struct rs_svd_plan rs_svd_plan;
+
+int rs_svd_plan_create(rs_ctx* ctx, const rs_ratings* r, int32_t n_factors, rs_svd_plan** out);
+void rs_svd_plan_destroy(rs_svd_plan* plan);
+/* host f64 -> device f32 (any of the pointers may be NULL = leave unchanged) */
+int rs_svd_plan_upload(rs_svd_plan* plan, const double* P, const double* Q, const double* bu,
+                       const double* bi, const double* gb);
+int rs_svd_plan_download(rs_svd_plan* plan, double* P, double* Q, double* bu, double* bi,
+                         double* gb);
+/* Enqueue n_epochs fast-mode epochs (one SGD kernel + one global-bias fold per epoch). */
+int rs_svd_plan_epochs(rs_svd_plan* plan, int32_t n_epochs, float lr, float reg, void* stream);
+/* Device pointers of the resident state (float32 unless noted); ld = row stride in floats. */
+int rs_svd_plan_device_ptrs(rs_svd_plan* plan, void** P, void** Q, void** bu, void** bi,
+                            void** gb_f64, int32_t* ld);
+/* Per-launch timing: when on, rs_svd_plan_epochs brackets every SGD kernel with HIP events on
+ * the stream it runs on (adds one event pair per epoch; leave off for throughput runs). */
+int rs_svd_plan_set_timing(rs_svd_plan* plan, int32_t on);
+/* Device time of the last rs_svd_plan_epochs call in milliseconds (HIP events on the launch
+ * stream).  Timing on: sum over the SGD kernels only, n_launches = epochs.  Timing off: the whole
+ * enqueued span (SGD + global-bias fold kernels), n_launches = 2 * epochs. */
+int rs_svd_plan_last_kernel_ms(rs_svd_plan* plan, double* ms, int32_t* n_launches);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* RSGPU_H */

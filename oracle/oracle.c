@@ -1,0 +1,651 @@
+/*
+ * oracle.c -- CPU restatement of the reference hot path.  TEST INFRASTRUCTURE ONLY: loaded by
+ * tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg, never by the product path.
+ * See oracle.h for what each function restates and how the restatement is pinned.
+ *
+ * Built with -O2 -ffp-contract=off: Go on amd64 never fuses a*b+c, so neither may the oracle.
+ */
+#include "oracle.h"
+
+#include <math.h>
+#include <stdlib.h>
+#include <string.h>
+
+/* ------------------------------------------------------------------------------------------ */
+/* open-addressing map int64 -> int32 for first-appearance inner ids (data.go:137-151)          */
+
+typedef struct {
+    int64_t* keys;
+    int32_t* vals;
+    uint8_t* used;
+    int64_t cap;
+} idmap;
+
+static uint64_t mix64(uint64_t x) {
+    x ^= x >> 33;
+    x *= 0xff51afd7ed558ccdULL;
+    x ^= x >> 33;
+    x *= 0xc4ceb9fe1a85ec53ULL;
+    x ^= x >> 33;
+    return x;
+}
+
+static int idmap_init(idmap* m, int64_t n) {
+    int64_t cap = 16;
+    while (cap < 2 * n + 16) cap <<= 1;
+    m->cap = cap;
+    m->keys = (int64_t*)malloc((size_t)cap * sizeof(int64_t));
+    m->vals = (int32_t*)malloc((size_t)cap * sizeof(int32_t));
+    m->used = (uint8_t*)calloc((size_t)cap, 1);
+    return (m->keys && m->vals && m->used) ? 0 : -1;
+}
+
+static void idmap_free(idmap* m) {
+    free(m->keys);
+    free(m->vals);
+    free(m->used);
+}
+
+/* returns the inner id of key, inserting next_id if absent */
+static int32_t idmap_get_or_put(idmap* m, int64_t key, int32_t* next_id) {
+    uint64_t h = mix64((uint64_t)key) & (uint64_t)(m->cap - 1);
+    while (m->used[h]) {
+        if (m->keys[h] == key) return m->vals[h];
+        h = (h + 1) & (uint64_t)(m->cap - 1);
+    }
+    m->used[h] = 1;
+    m->keys[h] = key;
+    m->vals[h] = (*next_id)++;
+    return m->vals[h];
+}
+
+int or_trainset_ids(int64_t n, const int64_t* users, const int64_t* items, int32_t* inner_u,
+                    int32_t* inner_i, int32_t* n_users, int32_t* n_items) {
+    idmap mu, mi;
+    if (idmap_init(&mu, n) || idmap_init(&mi, n)) return -1;
+    int32_t nu = 0, ni = 0;
+    /* data.go:138-143: all users first ... */
+    for (int64_t t = 0; t < n; t++) inner_u[t] = idmap_get_or_put(&mu, users[t], &nu);
+    /* data.go:146-151: ... then all items */
+    for (int64_t t = 0; t < n; t++) inner_i[t] = idmap_get_or_put(&mi, items[t], &ni);
+    *n_users = nu;
+    *n_items = ni;
+    idmap_free(&mu);
+    idmap_free(&mi);
+    return 0;
+}
+
+/* gonum floats.Dot restated as a sequential sum (see oracle.h) */
+static double dot(const double* a, const double* b, int32_t k) {
+    double s = 0.0;
+    for (int32_t f = 0; f < k; f++) s += a[f] * b[f];
+    return s;
+}
+
+/* ------------------------------------------------------------------------------------------ */
+/* SVD                                                                                         */
+
+void or_svd_fit(int64_t n, const int32_t* u, const int32_t* i, const double* r, int32_t k,
+                int32_t epochs, double lr, double reg, double* P, double* Q, double* bu,
+                double* bi, double* gb) {
+    double GB = *gb;
+    for (int32_t epoch = 0; epoch < epochs; epoch++) {      /* svd.go:92 */
+        for (int64_t t = 0; t < n; t++) {                   /* svd.go:93: train-set order (Q3) */
+            const int32_t uu = u[t], ii = i[t];
+            const double rating = r[t];
+            const double userBias = bu[uu];                 /* svd.go:97-98: pre-update copies */
+            const double itemBias = bi[ii];
+            double* pu = P + (int64_t)uu * k;               /* svd.go:99-100: ALIASES (Q1) */
+            double* qi = Q + (int64_t)ii * k;
+            /* svd.go:102 -> Predict svd.go:35-48: ((gb + bu) + bi) + dot(p, q) */
+            double pred = GB;
+            pred += bu[uu];
+            pred += bi[ii];
+            pred += dot(pu, qi, k);
+            const double diff = pred - rating;
+            GB -= lr * diff;                                /* svd.go:105-106 (Q2) */
+            bu[uu] -= lr * (diff + reg * userBias);         /* svd.go:108-109 */
+            bi[ii] -= lr * (diff + reg * itemBias);         /* svd.go:111-112 */
+            /* svd.go:114-120: a = q*diff; b = p*reg; a += b; a *= lr; p -= a */
+            for (int32_t f = 0; f < k; f++) {
+                double a = qi[f] * diff;
+                double b = pu[f] * reg;
+                a = a + b;
+                a = a * lr;
+                pu[f] = pu[f] - a;
+            }
+            /* svd.go:122-128: same with the ALREADY UPDATED p (Q1) */
+            for (int32_t f = 0; f < k; f++) {
+                double a = pu[f] * diff;
+                double b = qi[f] * reg;
+                a = a + b;
+                a = a * lr;
+                qi[f] = qi[f] - a;
+            }
+        }
+    }
+    *gb = GB;
+}
+
+void or_svd_predict(int64_t n, const int32_t* u, const int32_t* i, int32_t k, const double* P,
+                    const double* Q, const double* bu, const double* bi, double gb, double* out) {
+    for (int64_t t = 0; t < n; t++) {
+        const int32_t uu = u[t], ii = i[t];
+        double ret = gb;                                    /* svd.go:35 */
+        if (uu >= 0) ret += bu[uu];                         /* svd.go:37-39 */
+        if (ii >= 0) ret += bi[ii];                         /* svd.go:41-43 */
+        if (uu >= 0 && ii >= 0) ret += dot(P + (int64_t)uu * k, Q + (int64_t)ii * k, k);
+        out[t] = ret;
+    }
+}
+
+/* ------------------------------------------------------------------------------------------ */
+/* SVD++                                                                                       */
+
+/* data.go:185-199 UserRatings: per inner user, (item, position) in data order -> CSR */
+static void build_user_csr(int64_t n, const int32_t* u, int32_t n_users, int64_t** rowptr_out,
+                           int64_t** pos_out) {
+    int64_t* rowptr = (int64_t*)calloc((size_t)n_users + 1, sizeof(int64_t));
+    int64_t* pos = (int64_t*)malloc((size_t)(n > 0 ? n : 1) * sizeof(int64_t));
+    for (int64_t t = 0; t < n; t++) rowptr[u[t] + 1]++;
+    for (int32_t x = 0; x < n_users; x++) rowptr[x + 1] += rowptr[x];
+    int64_t* fill = (int64_t*)malloc(((size_t)n_users + 1) * sizeof(int64_t));
+    memcpy(fill, rowptr, ((size_t)n_users + 1) * sizeof(int64_t));
+    for (int64_t t = 0; t < n; t++) pos[fill[u[t]]++] = t;
+    free(fill);
+    *rowptr_out = rowptr;
+    *pos_out = pos;
+}
+
+/* svd.go:271-282 ensembleImplFactors: e = (sum_j Y[j]) / sqrt(|N(u)|), floats.Add in N(u) order */
+static void ensemble(const int64_t* rowptr, const int64_t* pos, const int32_t* items, int32_t uu,
+                     int32_t k, const double* Y, double* e) {
+    for (int32_t f = 0; f < k; f++) e[f] = 0.0;
+    int64_t count = 0;
+    for (int64_t x = rowptr[uu]; x < rowptr[uu + 1]; x++) {
+        const double* y = Y + (int64_t)items[pos[x]] * k;
+        for (int32_t f = 0; f < k; f++) e[f] = e[f] + y[f];
+        count++;
+    }
+    const double s = sqrt((double)count);
+    for (int32_t f = 0; f < k; f++) e[f] /= s;              /* utils.go:63-67 divConst */
+}
+
+void or_svdpp_fit(int64_t n, const int32_t* u, const int32_t* i, const double* r,
+                  int32_t n_users, int32_t k, int32_t epochs, double lr, double reg, double* P,
+                  double* Q, double* Y, double* bu, double* bi, double* gb) {
+    int64_t *rowptr, *pos;
+    build_user_csr(n, u, n_users, &rowptr, &pos);           /* svd.go:342 */
+    double* e = (double*)malloc((size_t)k * sizeof(double));
+    double GB = *gb;
+    for (int32_t epoch = 0; epoch < epochs; epoch++) {      /* svd.go:350 */
+        for (int64_t t = 0; t < n; t++) {                   /* svd.go:352 */
+            const int32_t uu = u[t], ii = i[t];
+            const double rating = r[t];
+            const double userBias = bu[uu];                 /* svd.go:358-361 (aliases) */
+            const double itemBias = bi[ii];
+            double* pu = P + (int64_t)uu * k;
+            double* qi = Q + (int64_t)ii * k;
+            /* svd.go:363 internalPredict svd.go:290-305 */
+            double pred = GB;
+            pred += bu[uu];
+            pred += bi[ii];
+            ensemble(rowptr, pos, i, uu, k, Y, e);
+            double s = 0.0;                                 /* tmp = 0 + p + e; dot(tmp, q) */
+            for (int32_t f = 0; f < k; f++) {
+                double tmp = 0.0;
+                tmp = tmp + pu[f];
+                tmp = tmp + e[f];
+                s += tmp * qi[f];
+            }
+            pred += s;
+            const double diff = pred - rating;              /* svd.go:364 */
+            GB -= lr * diff;                                /* svd.go:366-367 */
+            bu[uu] -= lr * (diff + reg * userBias);         /* svd.go:370-371 */
+            bi[ii] -= lr * (diff + reg * itemBias);         /* svd.go:374-375 */
+            for (int32_t f = 0; f < k; f++) {               /* svd.go:378-384, old q */
+                double a = qi[f] * diff;
+                double b = pu[f] * reg;
+                a = a + b;
+                a = a * lr;
+                pu[f] = pu[f] - a;
+            }
+            for (int32_t f = 0; f < k; f++) {               /* svd.go:387-396, NEW p plus e */
+                double a = pu[f];
+                a = a + e[f];                               /* len(emImpFactor) > 0 (L388) */
+                a = a * diff;
+                double b = qi[f] * reg;
+                a = a + b;
+                a = a * lr;
+                qi[f] = qi[f] - a;
+            }
+            /* svd.go:399-422: every j in N(u), with the NEW q_i (alias) */
+            const double sq = sqrt((double)(rowptr[uu + 1] - rowptr[uu]));
+            for (int64_t x = rowptr[uu]; x < rowptr[uu + 1]; x++) {
+                double* y = Y + (int64_t)i[pos[x]] * k;
+                for (int32_t f = 0; f < k; f++) {
+                    double a = qi[f] * diff;                /* L410-411 */
+                    a = a / sq;                             /* L412 divConst */
+                    double b = y[f] * reg;                  /* L413-414 */
+                    a = a + b;                              /* L415 */
+                    a = a * lr;                             /* L416 */
+                    y[f] = y[f] - a;                        /* L417 */
+                }
+            }
+        }
+    }
+    *gb = GB;
+    free(e);
+    free(rowptr);
+    free(pos);
+}
+
+void or_svdpp_predict(int64_t n_train, const int32_t* tu, const int32_t* ti, int32_t n_users,
+                      int64_t n, const int32_t* u, const int32_t* i, int32_t k, const double* P,
+                      const double* Q, const double* Y, const double* bu, const double* bi,
+                      double gb, double* out) {
+    int64_t *rowptr, *pos;
+    build_user_csr(n_train, tu, n_users, &rowptr, &pos);
+    double* e = (double*)malloc((size_t)k * sizeof(double));
+    for (int64_t t = 0; t < n; t++) {
+        const int32_t uu = u[t], ii = i[t];
+        double ret = gb;
+        if (uu >= 0) ret += bu[uu];
+        if (ii >= 0) ret += bi[ii];
+        if (uu >= 0 && ii >= 0) {
+            ensemble(rowptr, pos, ti, uu, k, Y, e);
+            const double* pu = P + (int64_t)uu * k;
+            const double* qi = Q + (int64_t)ii * k;
+            double s = 0.0;
+            for (int32_t f = 0; f < k; f++) {
+                double tmp = 0.0;
+                tmp = tmp + pu[f];
+                tmp = tmp + e[f];
+                s += tmp * qi[f];
+            }
+            ret += s;
+        }
+        out[t] = ret;
+    }
+    free(e);
+    free(rowptr);
+    free(pos);
+}
+
+/* ------------------------------------------------------------------------------------------ */
+/* NMF                                                                                         */
+
+void or_nmf_fit(int64_t n, const int32_t* u, const int32_t* i, const double* r, int32_t n_users,
+                int32_t n_items, int32_t k, int32_t epochs, double reg, int32_t as_written,
+                double* P, double* Q) {
+    const size_t su = (size_t)n_users * k, si = (size_t)n_items * k;
+    double* userUp = (double*)malloc(su * sizeof(double));  /* svd.go:173-176 */
+    double* userDown = (double*)malloc(su * sizeof(double));
+    double* itemUp = (double*)malloc(si * sizeof(double));
+    double* itemDown = (double*)malloc(si * sizeof(double));
+    double* buffer = (double*)malloc((size_t)k * sizeof(double));
+    for (int32_t epoch = 0; epoch < epochs; epoch++) {      /* svd.go:178 */
+        memset(userUp, 0, su * sizeof(double));             /* svd.go:180-183 */
+        memset(userDown, 0, su * sizeof(double));
+        memset(itemUp, 0, si * sizeof(double));
+        memset(itemDown, 0, si * sizeof(double));
+        for (int64_t t = 0; t < n; t++) {                   /* svd.go:186 */
+            const int32_t uu = u[t], ii = i[t];
+            const double rating = r[t];
+            const double* pu = P + (int64_t)uu * k;
+            const double* qi = Q + (int64_t)ii * k;
+            const double prediction = dot(pu, qi, k);       /* svd.go:190 -> 144 */
+            double* uup = userUp + (int64_t)uu * k;
+            double* udn = userDown + (int64_t)uu * k;
+            double* iup = itemUp + (int64_t)ii * k;
+            double* idn = itemDown + (int64_t)ii * k;
+            for (int32_t f = 0; f < k; f++) uup[f] = uup[f] + qi[f] * rating;      /* L193-197 */
+            for (int32_t f = 0; f < k; f++) udn[f] = udn[f] + qi[f] * prediction;  /* L200-204 */
+            for (int32_t f = 0; f < k; f++) udn[f] = udn[f] + pu[f] * reg;         /* L206-210 */
+            for (int32_t f = 0; f < k; f++) iup[f] = iup[f] + pu[f] * rating;      /* L214-218 */
+            for (int32_t f = 0; f < k; f++) idn[f] = idn[f] + pu[f] * prediction;  /* L221-225 */
+            for (int32_t f = 0; f < k; f++) idn[f] = idn[f] + qi[f] * reg;         /* L227-231 */
+        }
+        for (int32_t x = 0; x < n_users; x++) {             /* svd.go:236-241 */
+            double* pu = P + (int64_t)x * k;
+            for (int32_t f = 0; f < k; f++) {
+                buffer[f] = userUp[(int64_t)x * k + f];
+                buffer[f] = buffer[f] / userDown[(int64_t)x * k + f];
+                pu[f] = pu[f] * buffer[f];
+            }
+        }
+        for (int32_t x = 0; x < n_items; x++) {             /* svd.go:243-249 */
+            double* qi = Q + (int64_t)x * k;
+            for (int32_t f = 0; f < k; f++) {
+                const int64_t o = (int64_t)x * k + f;
+                buffer[f] = itemUp[o];                      /* L244: copy BEFORE the divide */
+                itemUp[o] = itemUp[o] / itemDown[o];        /* L246: divides itemUp in place */
+                qi[f] = qi[f] * (as_written ? buffer[f] : itemUp[o]); /* L248 (Q5) */
+            }
+        }
+    }
+    free(userUp);
+    free(userDown);
+    free(itemUp);
+    free(itemDown);
+    free(buffer);
+}
+
+void or_nmf_predict(int64_t n, const int32_t* u, const int32_t* i, int32_t k, const double* P,
+                    const double* Q, double* out) {
+    for (int64_t t = 0; t < n; t++) {                       /* svd.go:140-147 */
+        if (u[t] >= 0 && i[t] >= 0)
+            out[t] = dot(P + (int64_t)u[t] * k, Q + (int64_t)i[t] * k, k);
+        else
+            out[t] = 0.0;
+    }
+}
+
+/* ------------------------------------------------------------------------------------------ */
+/* Similarities                                                                                */
+
+static double sim_cosine(int64_t na, const int32_t* a_id, const double* a_r, int64_t nb,
+                         const int32_t* b_id, const double* b_r) {
+    double m = 0.0, n = 0.0, l = 0.0;                       /* sim.go:11 */
+    int64_t ptr = 0;
+    for (int64_t x = 0; x < na; x++) {                      /* sim.go:13 */
+        while (ptr < nb && b_id[ptr] < a_id[x]) ptr++;      /* sim.go:14-16 */
+        if (ptr < nb && b_id[ptr] == a_id[x]) {             /* sim.go:17 */
+            const double ra = a_r[x], rb = b_r[ptr];
+            m += ra * ra;                                   /* sim.go:19-21 */
+            n += rb * rb;
+            l += ra * rb;
+        }
+    }
+    return l / (sqrt(m) * sqrt(n));                         /* sim.go:24 */
+}
+
+static double sim_msd(int64_t na, const int32_t* a_id, const double* a_r, int64_t nb,
+                      const int32_t* b_id, const double* b_r) {
+    double count = 0.0, sum = 0.0;                          /* sim.go:29 */
+    int64_t ptr = 0;
+    for (int64_t x = 0; x < na; x++) {
+        while (ptr < nb && b_id[ptr] < a_id[x]) ptr++;
+        if (ptr < nb && b_id[ptr] == a_id[x]) {
+            const double d = a_r[x] - b_r[ptr];
+            sum += d * d;                                   /* sim.go:37 */
+            count++;
+        }
+    }
+    return 1.0 / (sum / count + 1.0);                       /* sim.go:43 */
+}
+
+static double sim_pearson(int64_t na, const int32_t* a_id, const double* a_r, int64_t nb,
+                          const int32_t* b_id, const double* b_r) {
+    double count = 0.0, sum = 0.0;                          /* sim.go:49-54: mean over ALL of a */
+    for (int64_t x = 0; x < na; x++) {
+        sum += a_r[x];
+        count += 1;
+    }
+    const double meanA = sum / count;
+    count = 0.0;                                            /* sim.go:57-62 */
+    sum = 0.0;
+    for (int64_t x = 0; x < nb; x++) {
+        sum += b_r[x];
+        count += 1;
+    }
+    const double meanB = sum / count;
+    double m = 0.0, n = 0.0, l = 0.0;                       /* sim.go:65-79 */
+    int64_t ptr = 0;
+    for (int64_t x = 0; x < na; x++) {
+        while (ptr < nb && b_id[ptr] < a_id[x]) ptr++;
+        if (ptr < nb && b_id[ptr] == a_id[x]) {
+            const double ra = a_r[x] - meanA;
+            const double rb = b_r[ptr] - meanB;
+            m += ra * ra;
+            n += rb * rb;
+            l += ra * rb;
+        }
+    }
+    return l / (sqrt(m) * sqrt(n));                         /* sim.go:80 */
+}
+
+double or_sim(int32_t kind, int64_t na, const int32_t* a_id, const double* a_r, int64_t nb,
+              const int32_t* b_id, const double* b_r) {
+    switch (kind) {
+        case 0: return sim_cosine(na, a_id, a_r, nb, b_id, b_r);
+        case 1: return sim_msd(na, a_id, a_r, nb, b_id, b_r);
+        default: return sim_pearson(na, a_id, a_r, nb, b_id, b_r);
+    }
+}
+
+typedef struct {
+    int32_t id;
+    double r;
+} idr;
+
+static int cmp_idr(const void* x, const void* y) {
+    const idr* a = (const idr*)x;
+    const idr* b = (const idr*)y;
+    return (a->id > b->id) - (a->id < b->id);
+}
+
+void or_knn_sims(int32_t kind, int32_t L, const int64_t* rowptr, const int32_t* ids,
+                 const double* ratings, double* sims) {
+    const int64_t nnz = rowptr[L];
+    int32_t* sid = (int32_t*)malloc((size_t)(nnz > 0 ? nnz : 1) * sizeof(int32_t));
+    double* sr = (double*)malloc((size_t)(nnz > 0 ? nnz : 1) * sizeof(double));
+    idr* tmp = (idr*)malloc((size_t)(nnz > 0 ? nnz : 1) * sizeof(idr));
+    /* data.go:236-243 sorts(): each row sorted by ID (unique IDs: any sort gives this order) */
+    for (int32_t x = 0; x < L; x++) {
+        const int64_t b = rowptr[x], e = rowptr[x + 1];
+        for (int64_t t = b; t < e; t++) {
+            tmp[t - b].id = ids[t];
+            tmp[t - b].r = ratings[t];
+        }
+        qsort(tmp, (size_t)(e - b), sizeof(idr), cmp_idr);
+        for (int64_t t = b; t < e; t++) {
+            sid[t] = tmp[t - b].id;
+            sr[t] = tmp[t - b].r;
+        }
+    }
+    free(tmp);
+    const int64_t LL = (int64_t)L * L;
+    for (int64_t t = 0; t < LL; t++) sims[t] = NAN;         /* knn.go:238/242 newNanMatrix */
+    for (int32_t a = 0; a < L; a++) {                       /* knn.go:280 (nJobs = 1) */
+        for (int32_t b = 0; b < L; b++) {                   /* knn.go:282 */
+            if (a == b) continue;                           /* knn.go:283: diagonal stays NaN */
+            if (!isnan(sims[(int64_t)a * L + b])) continue; /* knn.go:284 */
+            const double v = or_sim(kind, rowptr[a + 1] - rowptr[a], sid + rowptr[a],
+                                    sr + rowptr[a], rowptr[b + 1] - rowptr[b], sid + rowptr[b],
+                                    sr + rowptr[b]);
+            if (!isnan(v)) {                                /* knn.go:286-289 */
+                sims[(int64_t)a * L + b] = v;
+                sims[(int64_t)b * L + a] = v;
+            }
+        }
+    }
+    free(sid);
+    free(sr);
+}
+
+/* ------------------------------------------------------------------------------------------ */
+/* KNN.Predict                                                                                 */
+
+static const double* g_sim_row; /* comparator context (single-threaded oracle) */
+
+typedef struct {
+    int32_t id;
+    double r;
+    int64_t pos;
+} cand;
+
+static int cmp_cand(const void* x, const void* y) {
+    const cand* a = (const cand*)x;
+    const cand* b = (const cand*)y;
+    const double sa = g_sim_row[a->id], sb = g_sim_row[b->id];
+    if (sa > sb) return -1;                                 /* knn.go:124-126: desc by sim */
+    if (sa < sb) return 1;
+    return (a->pos > b->pos) - (a->pos < b->pos);           /* documented tie rule */
+}
+
+void or_knn_predict(int32_t type, int32_t L, const double* sims, const int64_t* right_rowptr,
+                    const int32_t* right_ids, const double* right_r, const double* means,
+                    const double* stddevs, const double* bias, double global_mean, int32_t k,
+                    int32_t min_k, int64_t n, const int32_t* left, const int32_t* right,
+                    double* out) {
+    int64_t maxdeg = 1;
+    for (int64_t x = 0; x < n; x++) {
+        if (right[x] < 0) continue;
+        const int64_t d = right_rowptr[right[x] + 1] - right_rowptr[right[x]];
+        if (d > maxdeg) maxdeg = d;
+    }
+    cand* c = (cand*)malloc((size_t)maxdeg * sizeof(cand));
+    for (int64_t x = 0; x < n; x++) {
+        const int32_t li = left[x], ri = right[x];
+        if (li < 0 || ri < 0) {                             /* knn.go:170-172 */
+            out[x] = global_mean;
+            continue;
+        }
+        const double* srow = sims + (int64_t)li * L;
+        int64_t nc = 0;
+        for (int64_t t = right_rowptr[ri]; t < right_rowptr[ri + 1]; t++) { /* knn.go:176-180 */
+            if (!isnan(srow[right_ids[t]])) {
+                c[nc].id = right_ids[t];
+                c[nc].r = right_r[t];
+                c[nc].pos = nc;
+                nc++;
+            }
+        }
+        if (nc <= min_k) {                                  /* knn.go:183-185 */
+            out[x] = global_mean;
+            continue;
+        }
+        g_sim_row = srow;
+        qsort(c, (size_t)nc, sizeof(cand), cmp_cand);       /* knn.go:188-189 */
+        const int64_t nn = nc < k ? nc : k;                 /* knn.go:192-195 */
+        double weightSum = 0.0, weightRating = 0.0;
+        for (int64_t t = 0; t < nn; t++) {                  /* knn.go:199-211 */
+            weightSum += srow[c[t].id];
+            double rating = c[t].r;
+            if (type == 1) rating -= means[c[t].id];
+            else if (type == 2) rating = (rating - means[c[t].id]) / stddevs[c[t].id];
+            else if (type == 3) rating -= bias[c[t].id];
+            weightRating += srow[c[t].id] * rating;
+        }
+        double prediction = weightRating / weightSum;       /* knn.go:212-220 */
+        if (type == 1) prediction += means[li];
+        else if (type == 3) prediction += bias[li];
+        else if (type == 2) {
+            prediction *= stddevs[li];
+            prediction += means[li];
+        }
+        out[x] = prediction;
+    }
+    free(c);
+}
+
+void or_baseline_fit(int64_t n, const int32_t* u, const int32_t* i, const double* r,
+                     int32_t epochs, double lr, double reg, double* bu, double* bi, double* gb) {
+    double GB = *gb;
+    for (int32_t epoch = 0; epoch < epochs; epoch++) {      /* base.go:443 */
+        for (int64_t t = 0; t < n; t++) {
+            const int32_t uu = u[t], ii = i[t];
+            const double userBias = bu[uu], itemBias = bi[ii];
+            double pred = GB;                               /* base.go:420-431 */
+            pred += bu[uu];
+            pred += bi[ii];
+            const double diff = pred - r[t];
+            GB -= lr * diff;                                /* base.go:456-458 */
+            bu[uu] -= lr * (diff + reg * userBias);
+            bi[ii] -= lr * (diff + reg * itemBias);
+        }
+    }
+    *gb = GB;
+}
+
+/* ------------------------------------------------------------------------------------------ */
+/* Restatement of the GPU fast-mode schedule (sgd.hip), see oracle.h                           */
+
+void or_svd_fit_chunked(int32_t n_users, const int64_t* rowptr, const int32_t* items,
+                        const double* r, int32_t chunk, int32_t k, int32_t epochs, double lr,
+                        double reg, double* P, double* Q, double* bu, double* bi, double* gb) {
+    /* work items: each user row split into ceil(deg / chunk) near-equal pieces */
+    int64_t nw = 0;
+    for (int32_t x = 0; x < n_users; x++) {
+        const int64_t d = rowptr[x + 1] - rowptr[x];
+        nw += d > 0 ? (d + chunk - 1) / chunk : 0;
+    }
+    int32_t* wu = (int32_t*)malloc((size_t)(nw > 0 ? nw : 1) * sizeof(int32_t));
+    int64_t* wb = (int64_t*)malloc((size_t)(nw > 0 ? nw : 1) * sizeof(int64_t));
+    int64_t* we = (int64_t*)malloc((size_t)(nw > 0 ? nw : 1) * sizeof(int64_t));
+    int32_t* wsplit = (int32_t*)malloc((size_t)(nw > 0 ? nw : 1) * sizeof(int32_t));
+    int64_t w = 0, maxlen = 0;
+    for (int32_t x = 0; x < n_users; x++) {
+        const int64_t d = rowptr[x + 1] - rowptr[x];
+        if (d == 0) continue;
+        const int64_t pieces = (d + chunk - 1) / chunk;
+        for (int64_t p = 0; p < pieces; p++) {
+            wu[w] = x;
+            wb[w] = rowptr[x] + d * p / pieces;
+            we[w] = rowptr[x] + d * (p + 1) / pieces;
+            wsplit[w] = pieces > 1;
+            if (we[w] - wb[w] > maxlen) maxlen = we[w] - wb[w];
+            w++;
+        }
+    }
+    double* lp = (double*)malloc((size_t)(nw > 0 ? nw : 1) * k * sizeof(double));
+    double* lp0 = (double*)malloc((size_t)(nw > 0 ? nw : 1) * k * sizeof(double));
+    double* lbu = (double*)malloc((size_t)(nw > 0 ? nw : 1) * sizeof(double));
+    double* lbu0 = (double*)malloc((size_t)(nw > 0 ? nw : 1) * sizeof(double));
+    double* lgb = (double*)malloc((size_t)(nw > 0 ? nw : 1) * sizeof(double));
+    int64_t nnz = rowptr[n_users];
+    double GB = *gb;
+    for (int32_t epoch = 0; epoch < epochs; epoch++) {
+        for (int64_t x = 0; x < nw; x++) {
+            memcpy(lp + x * k, P + (int64_t)wu[x] * k, (size_t)k * sizeof(double));
+            memcpy(lp0 + x * k, P + (int64_t)wu[x] * k, (size_t)k * sizeof(double));
+            lbu[x] = lbu0[x] = bu[wu[x]];
+            lgb[x] = GB;
+        }
+        for (int64_t t = 0; t < maxlen; t++) {
+            for (int64_t x = 0; x < nw; x++) {
+                const int64_t pos = wb[x] + t;
+                if (pos >= we[x]) continue;
+                const int32_t ii = items[pos];
+                double* pu = lp + x * k;
+                double* qi = Q + (int64_t)ii * k;
+                const double ub = lbu[x], ib = bi[ii];
+                double pred = lgb[x];
+                pred += ub;
+                pred += ib;
+                pred += dot(pu, qi, k);
+                const double diff = pred - r[pos];
+                lgb[x] -= lr * diff;
+                lbu[x] = ub - lr * (diff + reg * ub);
+                bi[ii] = ib - lr * (diff + reg * ib);
+                for (int32_t f = 0; f < k; f++) pu[f] = pu[f] - (qi[f] * diff + pu[f] * reg) * lr;
+                for (int32_t f = 0; f < k; f++) qi[f] = qi[f] - (pu[f] * diff + qi[f] * reg) * lr;
+            }
+        }
+        double gsum = 0.0;
+        for (int64_t x = 0; x < nw; x++) {
+            const int32_t uu = wu[x];
+            if (!wsplit[x]) {
+                memcpy(P + (int64_t)uu * k, lp + x * k, (size_t)k * sizeof(double));
+                bu[uu] = lbu[x];
+            } else {
+                for (int32_t f = 0; f < k; f++)
+                    P[(int64_t)uu * k + f] += lp[x * k + f] - lp0[x * k + f];
+                bu[uu] += lbu[x] - lbu0[x];
+            }
+            gsum += (double)(we[x] - wb[x]) * (lgb[x] - GB);
+        }
+        if (nnz > 0) GB += gsum / (double)nnz;
+    }
+    *gb = GB;
+    free(wu);
+    free(wb);
+    free(we);
+    free(wsplit);
+    free(lp);
+    free(lp0);
+    free(lbu);
+    free(lbu0);
+    free(lgb);
+}

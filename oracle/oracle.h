@@ -1,0 +1,106 @@
+/*
+ * oracle.h -- CPU restatement of the reference hot path (TEST INFRASTRUCTURE ONLY).
+ *
+ * Reference: Oneaccount1/recommend-sys @ 2025-08-24, pure Go, package core/.
+ * The reference cannot be compiled here (no Go toolchain, gonum v0.9.1 absent, and the package has
+ * compile errors at this snapshot: core/eval.go:40,107).  This file restates, in plain C and fp64,
+ * the exact arithmetic order of the functions on the hot path.  Every function cites the reference
+ * file:line it follows.
+ *
+ * Pinning (see DESIGN.md "Oracle"):
+ *   - Cosine/MSD/Pearson are pinned by the reference's own known-answer tests core/sim_test.go:10-59
+ *     (tests/golden/sim_kat.json, exact values 14/sqrt(205), 1/10, 0).
+ *   - SVD / NMF / KNN fits are pinned by the reference's accuracy regressions core/base_test.go:35,43,51
+ *     (5-fold CV on ML-100K, RMSE/MAE <= expected + 0.008), evaluated on the restatement.
+ *   - SVD++ has no active reference test (core/base_test.go:38-40 is commented out): parity unpinned.
+ *   - gonum floats.Dot (third-party, gonum.org/v1/gonum v0.9.1, go.mod:7, not vendored) is restated as
+ *     a sequential left-to-right sum; its amd64 asm summation order is unverified (few-ulp effect).
+ *
+ * Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg may load this library.
+ */
+#ifndef RS_ORACLE_H
+#define RS_ORACLE_H
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* data.go:131-154 NewTrainSet: inner ids by first appearance over Users, then over Items. */
+int or_trainset_ids(int64_t n, const int64_t* users, const int64_t* items,
+                    int32_t* inner_u, int32_t* inner_i, int32_t* n_users, int32_t* n_items);
+
+/* svd.go:63-132 SVD.Fit epoch loop, ratings visited in the given (train-set) order.
+ * P (U*k), Q (I*k) carry the injected initial factors in and the fitted factors out
+ * (svd.go:80-85 draws them; Q4: the draw is unseeded in the reference so parity injects it).
+ * bu, bi, gb are in/out (reference starts them at 0: svd.go:77-78, GlobalBias zero value). */
+void or_svd_fit(int64_t n, const int32_t* u, const int32_t* i, const double* r,
+                int32_t k, int32_t epochs, double lr, double reg,
+                double* P, double* Q, double* bu, double* bi, double* gb);
+
+/* svd.go:32-51 SVD.Predict for inner ids (-1 = unknown, data.go:129 newID). */
+void or_svd_predict(int64_t n, const int32_t* u, const int32_t* i, int32_t k,
+                    const double* P, const double* Q, const double* bu, const double* bi,
+                    double gb, double* out);
+
+/* svd.go:316-427 SVDPP.Fit, literal O(sum |N(u)|^2 k) form.  N(u) = TrainSet.UserRatings()
+ * (data.go:185-199: data order).  n_users needed to build N(u). */
+void or_svdpp_fit(int64_t n, const int32_t* u, const int32_t* i, const double* r,
+                  int32_t n_users, int32_t k, int32_t epochs, double lr, double reg,
+                  double* P, double* Q, double* Y, double* bu, double* bi, double* gb);
+
+/* svd.go:271-310 SVDPP.Predict for inner ids. */
+void or_svdpp_predict(int64_t n_train, const int32_t* tu, const int32_t* ti, int32_t n_users,
+                      int64_t n, const int32_t* u, const int32_t* i, int32_t k,
+                      const double* P, const double* Q, const double* Y, const double* bu,
+                      const double* bi, double gb, double* out);
+
+/* svd.go:158-251 NMF.Fit.  as_written=1 reproduces svd.go:243-249 literally (Q5: q_i *= itemUp[i]
+ * undivided); as_written=0 applies the intended q_i *= itemUp[i]/itemDown[i] (svd.go:242 comment). */
+void or_nmf_fit(int64_t n, const int32_t* u, const int32_t* i, const double* r,
+                int32_t n_users, int32_t n_items, int32_t k, int32_t epochs, double reg,
+                int32_t as_written, double* P, double* Q);
+
+/* svd.go:140-147 NMF.Predict. */
+void or_nmf_predict(int64_t n, const int32_t* u, const int32_t* i, int32_t k,
+                    const double* P, const double* Q, double* out);
+
+/* sim.go:10-81 Cosine (kind 0), MSD (kind 1), Pearson (kind 2) over ID-ascending lists. */
+double or_sim(int32_t kind, int64_t na, const int32_t* a_id, const double* a_r,
+              int64_t nb, const int32_t* b_id, const double* b_r);
+
+/* knn.go:270-297 (KNN.Fit pair loop) with nJobs = 1: Sims L x L, NaN where no co-rating, NaN
+ * diagonal.  Rows are given as CSR (rowptr int64[L+1], ids, ratings) in data order and sorted by
+ * ID here (data.go:236-243 sorts). */
+void or_knn_sims(int32_t kind, int32_t L, const int64_t* rowptr, const int32_t* ids,
+                 const double* ratings, double* sims);
+
+/* knn.go:156-222 KNN.Predict with ties broken by (sim desc, position asc) -- the reference uses
+ * Go's unstable sort.Sort (knn.go:189), so tie order is the one documented deviation.
+ * type: 0 basic, 1 centered, 2 zscore, 3 baseline.  right_* is RightRatings CSR in data order. */
+void or_knn_predict(int32_t type, int32_t L, const double* sims, const int64_t* right_rowptr,
+                    const int32_t* right_ids, const double* right_r, const double* means,
+                    const double* stddevs, const double* bias, double global_mean,
+                    int32_t k, int32_t min_k, int64_t n, const int32_t* left, const int32_t* right,
+                    double* out);
+
+/* base.go:433-461 BaseLine.Fit (bias-only SGD, used by KNN baseline knn.go:260-268). */
+void or_baseline_fit(int64_t n, const int32_t* u, const int32_t* i, const double* r,
+                     int32_t epochs, double lr, double reg, double* bu, double* bi, double* gb);
+
+/* ---- restatements of THIS build's own GPU schedules (not of the reference) ---- */
+
+/* Fast-mode SGD schedule of recommend-sys_amd/csrc/sgd.hip, single-threaded: work items are
+ * (user, CSR range) chunks; all chunks advance in lock-step rounds (round t processes the t-th
+ * rating of every live chunk in chunk order), which is the schedule the GPU runs when every chunk
+ * is resident; per-chunk local GlobalBias, folded at epoch end as gb += sum(n_w * dgb_w) / nnz.
+ * P deltas of split users are summed in chunk order.  Used for RMSE-parity studies and for the
+ * race-free factor parity test (inputs where no two chunks share an item). */
+void or_svd_fit_chunked(int32_t n_users, const int64_t* rowptr, const int32_t* items,
+                        const double* r, int32_t chunk, int32_t k, int32_t epochs, double lr,
+                        double reg, double* P, double* Q, double* bu, double* bi, double* gb);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -1,0 +1,108 @@
+// common.hpp -- shared host/device helpers of librsgpu (gfx950 only).
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+#include <cstdio>
+#include <string>
+#include <vector>
+
+#include "rsgpu.h"
+
+struct rs_ctx {
+    int device = 0;
+    hipStream_t stream = nullptr;
+    std::string err;
+};
+
+namespace rs {
+
+// Thread-local error slot for calls made with a NULL ctx (or that fail before a ctx exists).
+std::string& tls_error();
+
+int set_error(rs_ctx* ctx, int code, const std::string& msg);
+
+struct HipError {
+    hipError_t code;
+    std::string what;
+};
+
+#define RS_HIP(call)                                                                          \
+    do {                                                                                      \
+        hipError_t _e = (call);                                                               \
+        if (_e != hipSuccess)                                                                 \
+            throw ::rs::HipError{_e, std::string(#call) + ": " + hipGetErrorString(_e)};     \
+    } while (0)
+
+// Owning device buffer (RAII); frees on scope exit so error paths never leak HBM.
+template <typename T>
+struct DevBuf {
+    T* p = nullptr;
+    size_t n = 0;
+    DevBuf() = default;
+    explicit DevBuf(size_t count) { alloc(count); }
+    DevBuf(const DevBuf&) = delete;
+    DevBuf& operator=(const DevBuf&) = delete;
+    DevBuf(DevBuf&& o) noexcept : p(o.p), n(o.n) { o.p = nullptr; o.n = 0; }
+    DevBuf& operator=(DevBuf&& o) noexcept {
+        if (this != &o) { release(); p = o.p; n = o.n; o.p = nullptr; o.n = 0; }
+        return *this;
+    }
+    ~DevBuf() { release(); }
+    void alloc(size_t count) {
+        release();
+        n = count;
+        if (count) RS_HIP(hipMalloc(reinterpret_cast<void**>(&p), count * sizeof(T)));
+    }
+    void release() {
+        if (p) (void)hipFree(p);
+        p = nullptr;
+        n = 0;
+    }
+    void upload(const T* h, size_t count, hipStream_t s) {
+        if (count) RS_HIP(hipMemcpyAsync(p, h, count * sizeof(T), hipMemcpyHostToDevice, s));
+    }
+    void download(T* h, size_t count, hipStream_t s) const {
+        if (count) RS_HIP(hipMemcpyAsync(h, p, count * sizeof(T), hipMemcpyDeviceToHost, s));
+    }
+};
+
+inline int32_t round_up4(int32_t k) { return (k + 3) & ~3; }
+
+// f64 host rows (stride k) <-> f32 padded rows (stride ld) with zero padding.
+void pack_rows_f32(const double* src, int64_t rows, int32_t k, int32_t ld, std::vector<float>& dst);
+void unpack_rows_f64(const std::vector<float>& src, int64_t rows, int32_t k, int32_t ld, double* dst);
+
+// Stable user-CSR of COO ratings (core/data.go:185-199 order: data order within a user).
+struct UserCSR {
+    std::vector<int64_t> rowptr;  // n_rows + 1
+    std::vector<int32_t> cols;
+    std::vector<float> vals;
+};
+void build_csr(int64_t nnz, int32_t n_rows, const int32_t* rows, const int32_t* cols,
+               const double* vals, UserCSR& out);
+
+// Validates a rs_ratings block; returns RS_OK or an error (message set on ctx).
+int check_ratings(rs_ctx* ctx, const rs_ratings* r);
+
+}  // namespace rs
+
+// Entry-point wrapper: sets the device, converts exceptions into status codes.
+template <typename F>
+int rs_guard(rs_ctx* ctx, F&& body) {
+    try {
+        if (ctx) {
+            hipError_t e = hipSetDevice(ctx->device);
+            if (e != hipSuccess)
+                return rs::set_error(ctx, RS_ERR_HIP, std::string("hipSetDevice: ") + hipGetErrorString(e));
+        }
+        return body();
+    } catch (const rs::HipError& e) {
+        return rs::set_error(ctx, e.code == hipErrorOutOfMemory ? RS_ERR_NOMEM : RS_ERR_HIP, e.what);
+    } catch (const std::bad_alloc&) {
+        return rs::set_error(ctx, RS_ERR_NOMEM, "host allocation failed");
+    } catch (const std::exception& e) {
+        return rs::set_error(ctx, RS_ERR_INVALID, e.what());
+    }
+}

@@ -1,0 +1,128 @@
+// rsgpu.cpp -- context management and host-side helpers of the C-ABI (include/rsgpu.h).
+#include <hip/hip_runtime.h>
+
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "common.hpp"
+
+namespace rs {
+
+std::string& tls_error() {
+    static thread_local std::string e;
+    return e;
+}
+
+int set_error(rs_ctx* ctx, int code, const std::string& msg) {
+    if (ctx) ctx->err = msg;
+    tls_error() = msg;
+    return code;
+}
+
+void pack_rows_f32(const double* src, int64_t rows, int32_t k, int32_t ld, std::vector<float>& dst) {
+    dst.assign(static_cast<size_t>(rows) * ld, 0.f);
+    for (int64_t r = 0; r < rows; ++r)
+        for (int32_t f = 0; f < k; ++f) dst[r * ld + f] = static_cast<float>(src[r * k + f]);
+}
+
+void unpack_rows_f64(const std::vector<float>& src, int64_t rows, int32_t k, int32_t ld, double* dst) {
+    for (int64_t r = 0; r < rows; ++r)
+        for (int32_t f = 0; f < k; ++f) dst[r * k + f] = static_cast<double>(src[r * ld + f]);
+}
+
+void build_csr(int64_t nnz, int32_t n_rows, const int32_t* rows, const int32_t* cols,
+               const double* vals, UserCSR& out) {
+    out.rowptr.assign(static_cast<size_t>(n_rows) + 1, 0);
+    for (int64_t t = 0; t < nnz; ++t) out.rowptr[rows[t] + 1]++;
+    for (int32_t x = 0; x < n_rows; ++x) out.rowptr[x + 1] += out.rowptr[x];
+    std::vector<int64_t> fill(out.rowptr.begin(), out.rowptr.end() - 1);
+    out.cols.resize(static_cast<size_t>(nnz));
+    out.vals.resize(static_cast<size_t>(nnz));
+    for (int64_t t = 0; t < nnz; ++t) {  // stable: data order within a row
+        const int64_t d = fill[rows[t]]++;
+        out.cols[d] = cols[t];
+        out.vals[d] = static_cast<float>(vals[t]);
+    }
+}
+
+int check_ratings(rs_ctx* ctx, const rs_ratings* r) {
+    if (!r) return set_error(ctx, RS_ERR_INVALID, "ratings is NULL");
+    if (r->nnz < 0 || r->n_users < 0 || r->n_items < 0)
+        return set_error(ctx, RS_ERR_INVALID, "negative size");
+    if (r->nnz > 0 && (!r->users || !r->items || !r->ratings))
+        return set_error(ctx, RS_ERR_INVALID, "ratings arrays are NULL");
+    for (int64_t t = 0; t < r->nnz; ++t) {
+        if (r->users[t] < 0 || r->users[t] >= r->n_users)
+            return set_error(ctx, RS_ERR_INVALID, "user id out of range at " + std::to_string(t));
+        if (r->items[t] < 0 || r->items[t] >= r->n_items)
+            return set_error(ctx, RS_ERR_INVALID, "item id out of range at " + std::to_string(t));
+    }
+    return RS_OK;
+}
+
+}  // namespace rs
+
+extern "C" int32_t rs_version(void) { return 1; }
+
+extern "C" int rs_device_count(int32_t* n) {
+    return rs_guard(nullptr, [&]() -> int {
+        if (!n) return rs::set_error(nullptr, RS_ERR_INVALID, "n is NULL");
+        int c = 0;
+        hipError_t e = hipGetDeviceCount(&c);
+        if (e != hipSuccess) {
+            *n = 0;
+            return rs::set_error(nullptr, RS_ERR_NO_DEVICE, std::string("hipGetDeviceCount: ") + hipGetErrorString(e));
+        }
+        *n = c;
+        return RS_OK;
+    });
+}
+
+extern "C" int rs_open(int32_t device, rs_ctx** out) {
+    return rs_guard(nullptr, [&]() -> int {
+        if (!out) return rs::set_error(nullptr, RS_ERR_INVALID, "out is NULL");
+        *out = nullptr;
+        int c = 0;
+        if (hipGetDeviceCount(&c) != hipSuccess || c == 0)
+            return rs::set_error(nullptr, RS_ERR_NO_DEVICE, "no HIP device visible");
+        if (device < 0 || device >= c) return rs::set_error(nullptr, RS_ERR_INVALID, "device out of range");
+        hipDeviceProp_t prop;
+        RS_HIP(hipGetDeviceProperties(&prop, device));
+        if (std::strncmp(prop.gcnArchName, "gfx950", 6) != 0)
+            return rs::set_error(nullptr, RS_ERR_NO_DEVICE,
+                                 std::string("librsgpu is built for gfx950 only; device is ") + prop.gcnArchName);
+        RS_HIP(hipSetDevice(device));
+        auto* ctx = new rs_ctx();
+        ctx->device = device;
+        hipError_t e = hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking);
+        if (e != hipSuccess) {
+            delete ctx;
+            return rs::set_error(nullptr, RS_ERR_HIP, std::string("hipStreamCreate: ") + hipGetErrorString(e));
+        }
+        *out = ctx;
+        return RS_OK;
+    });
+}
+
+extern "C" void rs_close(rs_ctx* ctx) {
+    if (!ctx) return;
+    (void)hipSetDevice(ctx->device);
+    if (ctx->stream) {
+        (void)hipStreamSynchronize(ctx->stream);
+        (void)hipStreamDestroy(ctx->stream);
+    }
+    delete ctx;
+}
+
+extern "C" const char* rs_last_error(const rs_ctx* ctx) {
+    return ctx ? ctx->err.c_str() : rs::tls_error().c_str();
+}
+
+extern "C" int rs_synchronize(rs_ctx* ctx) {
+    if (!ctx) return rs::set_error(ctx, RS_ERR_INVALID, "ctx is NULL");
+    return rs_guard(ctx, [&]() -> int {
+        RS_HIP(hipStreamSynchronize(ctx->stream));
+        return RS_OK;
+    });
+}

@@ -1,0 +1,244 @@
+"""ctypes binding of librsgpu.so (include/rsgpu.h) -- the host side used by tests and bench.py.
+
+This module is plumbing over the C-ABI: every compute call goes to the HIP library and fails
+loudly (RsError) when the library or a gfx950 device is missing.  There is no CPU fallback.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+import numpy as np
+
+from . import _build
+
+LIB_PATH = _build.LIB
+_lib = None
+
+RS_OK = 0
+RS_ERR_INVALID, RS_ERR_HIP, RS_ERR_NOMEM, RS_ERR_UNSUPPORTED, RS_ERR_NO_DEVICE = -1, -2, -3, -4, -5
+SGD_FAST, SGD_ORDERED = 0, 1
+SIM_COSINE, SIM_MSD, SIM_PEARSON = 0, 1, 2
+
+HEADER_SYMBOLS = (
+    "rs_version", "rs_device_count", "rs_open", "rs_close", "rs_last_error", "rs_synchronize",
+    "rs_svd_fit", "rs_svd_predict", "rs_svdpp_fit", "rs_nmf_fit", "rs_baseline_fit",
+    "rs_knn_sims", "rs_sim_pair", "rs_svd_plan_create", "rs_svd_plan_destroy",
+    "rs_svd_plan_upload", "rs_svd_plan_download", "rs_svd_plan_epochs",
+    "rs_svd_plan_device_ptrs", "rs_svd_plan_set_timing", "rs_svd_plan_last_kernel_ms",
+)
+
+
+class RsError(RuntimeError):
+    def __init__(self, code, msg):
+        super().__init__(f"librsgpu error {code}: {msg}")
+        self.code = code
+
+
+class _Ratings(C.Structure):
+    _fields_ = [("nnz", C.c_int64), ("n_users", C.c_int32), ("n_items", C.c_int32),
+                ("users", C.c_void_p), ("items", C.c_void_p), ("ratings", C.c_void_p)]
+
+
+class _SgdParams(C.Structure):
+    _fields_ = [("n_factors", C.c_int32), ("n_epochs", C.c_int32), ("lr", C.c_double),
+                ("reg", C.c_double), ("mode", C.c_int32), ("reserved", C.c_int32)]
+
+
+_vp = C.c_void_p
+_i32, _i64, _dbl, _flt = C.c_int32, C.c_int64, C.c_double, C.c_float
+
+
+def lib():
+    """Loads librsgpu.so (building it first when the sources are newer)."""
+    global _lib
+    if _lib is None:
+        if os.path.exists(os.path.join(_build.CSRC, "sgd.hip")):
+            _build.build()
+        if not os.path.exists(LIB_PATH):
+            raise ImportError(f"librsgpu.so missing at {LIB_PATH}; run __graft_entry__.build()")
+        L = C.CDLL(LIB_PATH)
+        sig = {
+            "rs_version": (_i32, []),
+            "rs_device_count": (C.c_int, [C.POINTER(_i32)]),
+            "rs_open": (C.c_int, [_i32, C.POINTER(_vp)]),
+            "rs_close": (None, [_vp]),
+            "rs_last_error": (C.c_char_p, [_vp]),
+            "rs_synchronize": (C.c_int, [_vp]),
+            "rs_svd_fit": (C.c_int, [_vp, C.POINTER(_Ratings), C.POINTER(_SgdParams), _vp, _vp,
+                                     _vp, _vp, _vp]),
+            "rs_svd_predict": (C.c_int, [_vp, _i64, _vp, _vp, _i32, _i32, _i32, _vp, _vp, _vp,
+                                         _vp, _dbl, _vp]),
+            "rs_svdpp_fit": (C.c_int, [_vp, C.POINTER(_Ratings), C.POINTER(_SgdParams), _vp, _vp,
+                                       _vp, _vp, _vp, _vp]),
+            "rs_nmf_fit": (C.c_int, [_vp, C.POINTER(_Ratings), _i32, _i32, _dbl, _i32, _vp, _vp]),
+            "rs_baseline_fit": (C.c_int, [_vp, C.POINTER(_Ratings), _i32, _dbl, _dbl, _vp, _vp,
+                                          _vp]),
+            "rs_knn_sims": (C.c_int, [_vp, _i32, _i32, _i32, _vp, _vp, _vp, _vp]),
+            "rs_sim_pair": (C.c_int, [_vp, _i32, _i64, _vp, _vp, _i64, _vp, _vp, _vp]),
+            "rs_svd_plan_create": (C.c_int, [_vp, C.POINTER(_Ratings), _i32, C.POINTER(_vp)]),
+            "rs_svd_plan_destroy": (None, [_vp]),
+            "rs_svd_plan_upload": (C.c_int, [_vp, _vp, _vp, _vp, _vp, _vp]),
+            "rs_svd_plan_download": (C.c_int, [_vp, _vp, _vp, _vp, _vp, _vp]),
+            "rs_svd_plan_epochs": (C.c_int, [_vp, _i32, _flt, _flt, _vp]),
+            "rs_svd_plan_device_ptrs": (C.c_int, [_vp, C.POINTER(_vp), C.POINTER(_vp),
+                                                  C.POINTER(_vp), C.POINTER(_vp), C.POINTER(_vp),
+                                                  C.POINTER(_i32)]),
+            "rs_svd_plan_set_timing": (C.c_int, [_vp, _i32]),
+            "rs_svd_plan_last_kernel_ms": (C.c_int, [_vp, C.POINTER(_dbl), C.POINTER(_i32)]),
+        }
+        for name, (res, args) in sig.items():
+            f = getattr(L, name)
+            f.restype = res
+            f.argtypes = args
+        _lib = L
+    return _lib
+
+
+def _ptr(a):
+    return None if a is None else a.ctypes.data_as(C.c_void_p)
+
+
+def _check(code, ctx=None):
+    if code != RS_OK:
+        msg = lib().rs_last_error(ctx)
+        raise RsError(code, msg.decode() if msg else "")
+
+
+def device_count() -> int:
+    n = _i32(0)
+    code = lib().rs_device_count(C.byref(n))
+    return n.value if code == RS_OK else 0
+
+
+class Ratings:
+    """COO TrainSet ratings in train-set order with inner ids (core/data.go:109-127)."""
+
+    def __init__(self, users, items, ratings, n_users=None, n_items=None):
+        self.users = np.ascontiguousarray(users, dtype=np.int32)
+        self.items = np.ascontiguousarray(items, dtype=np.int32)
+        self.ratings = np.ascontiguousarray(ratings, dtype=np.float64)
+        self.n_users = int(self.users.max() + 1 if n_users is None and len(self.users) else (n_users or 0))
+        self.n_items = int(self.items.max() + 1 if n_items is None and len(self.items) else (n_items or 0))
+
+    def c(self):
+        return _Ratings(len(self.ratings), self.n_users, self.n_items, _ptr(self.users),
+                        _ptr(self.items), _ptr(self.ratings))
+
+
+class Context:
+    """One HIP stream on one gfx950 device (rs_open / rs_close)."""
+
+    def __init__(self, device: int = 0):
+        h = C.c_void_p()
+        code = lib().rs_open(device, C.byref(h))
+        if code != RS_OK:
+            raise RsError(code, lib().rs_last_error(None).decode())
+        self.h = h
+        self.device = device
+
+    def close(self):
+        if self.h:
+            lib().rs_close(self.h)
+            self.h = None
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        self.close()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def check(self, code):
+        _check(code, self.h)
+
+    # ---- estimators --------------------------------------------------------------------------
+
+    def svd_fit(self, r: Ratings, P, Q, bu=None, bi=None, gb=0.0, n_epochs=20, lr=0.005,
+                reg=0.02, mode=SGD_FAST):
+        P = np.array(P, dtype=np.float64, order="C")
+        Q = np.array(Q, dtype=np.float64, order="C")
+        bu = np.zeros(r.n_users) if bu is None else np.array(bu, dtype=np.float64)
+        bi = np.zeros(r.n_items) if bi is None else np.array(bi, dtype=np.float64)
+        g = np.array([gb], dtype=np.float64)
+        assert P.shape == (r.n_users, P.shape[1]) and Q.shape == (r.n_items, P.shape[1])
+        prm = _SgdParams(P.shape[1], n_epochs, lr, reg, mode, 0)
+        rc = r.c()
+        self.check(lib().rs_svd_fit(self.h, C.byref(rc), C.byref(prm), _ptr(P), _ptr(Q),
+                                    _ptr(bu), _ptr(bi), _ptr(g)))
+        return P, Q, bu, bi, float(g[0])
+
+    def svd_plan(self, r: Ratings, n_factors: int) -> "SvdPlan":
+        return SvdPlan(self, r, n_factors)
+
+
+class SvdPlan:
+    """Device-resident user-CSR + factors (rs_svd_plan_*)."""
+
+    def __init__(self, ctx: Context, r: Ratings, n_factors: int):
+        self.ctx = ctx
+        self.n_users, self.n_items, self.k = r.n_users, r.n_items, n_factors
+        self.nnz = len(r.ratings)
+        h = C.c_void_p()
+        rc = r.c()
+        ctx.check(lib().rs_svd_plan_create(ctx.h, C.byref(rc), n_factors, C.byref(h)))
+        self.h = h
+
+    def upload(self, P=None, Q=None, bu=None, bi=None, gb=None):
+        arrs = [None if a is None else np.ascontiguousarray(a, dtype=np.float64)
+                for a in (P, Q, bu, bi)]
+        g = None if gb is None else np.array([gb], dtype=np.float64)
+        self.ctx.check(lib().rs_svd_plan_upload(self.h, *[_ptr(a) for a in arrs], _ptr(g)))
+
+    def download(self):
+        P = np.empty((self.n_users, self.k))
+        Q = np.empty((self.n_items, self.k))
+        bu, bi, g = np.empty(self.n_users), np.empty(self.n_items), np.empty(1)
+        self.ctx.check(lib().rs_svd_plan_download(self.h, _ptr(P), _ptr(Q), _ptr(bu), _ptr(bi),
+                                                  _ptr(g)))
+        return P, Q, bu, bi, float(g[0])
+
+    def epochs(self, n, lr=0.005, reg=0.02, stream=None):
+        self.ctx.check(lib().rs_svd_plan_epochs(self.h, n, lr, reg, stream))
+
+    def device_ptrs(self):
+        ps = [C.c_void_p() for _ in range(5)]
+        ld = _i32(0)
+        self.ctx.check(lib().rs_svd_plan_device_ptrs(self.h, *[C.byref(p) for p in ps],
+                                                     C.byref(ld)))
+        return [p.value for p in ps], ld.value
+
+    def set_timing(self, on: bool):
+        self.ctx.check(lib().rs_svd_plan_set_timing(self.h, int(on)))
+
+    def last_kernel_ms(self):
+        ms, n = _dbl(0), _i32(0)
+        self.ctx.check(lib().rs_svd_plan_last_kernel_ms(self.h, C.byref(ms), C.byref(n)))
+        return ms.value, n.value
+
+    def close(self):
+        if self.h:
+            lib().rs_svd_plan_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+def svd_predict(users, items, P, Q, bu, bi, gb):
+    u = np.ascontiguousarray(users, dtype=np.int32)
+    i = np.ascontiguousarray(items, dtype=np.int32)
+    P, Q = np.ascontiguousarray(P, np.float64), np.ascontiguousarray(Q, np.float64)
+    bu, bi = np.ascontiguousarray(bu, np.float64), np.ascontiguousarray(bi, np.float64)
+    out = np.empty(len(u))
+    _check(lib().rs_svd_predict(None, len(u), _ptr(u), _ptr(i), P.shape[0], Q.shape[0],
+                                P.shape[1], _ptr(P), _ptr(Q), _ptr(bu), _ptr(bi), gb, _ptr(out)))
+    return out

@@ -1,0 +1,74 @@
+"""Builds librsgpu.so (gfx950 only) in-tree with hipcc.
+
+Objects go to recommend-sys_amd/build/, the shared library to recommend-sys_amd/rsgpu/librsgpu.so
+(git-ignored, but shipped to the GPU box by gpurun).  Incremental: a source is recompiled when it or
+any header is newer than its object.
+"""
+from __future__ import annotations
+
+import concurrent.futures as cf
+import glob
+import os
+import subprocess
+
+PKG_DIR = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(PKG_DIR)                 # recommend-sys_amd/
+REPO = os.path.dirname(ROOT)
+CSRC = os.path.join(ROOT, "csrc")
+BUILD = os.path.join(ROOT, "build")
+INCLUDE = os.path.join(REPO, "include")
+LIB = os.path.join(PKG_DIR, "librsgpu.so")
+HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
+ARCH = "gfx950"
+
+# -ffp-contract=off: parity kernels must not fuse a*b+c (the Go reference never does);
+# fast kernels opt back in locally with `#pragma clang fp contract(fast)`.
+CFLAGS = ["-O3", "-std=c++17", "-fPIC", "-ffp-contract=off", f"--offload-arch={ARCH}",
+          "-Wall", "-Wno-unused-result", f"-I{INCLUDE}", f"-I{CSRC}"]
+
+
+def _sources():
+    return sorted(glob.glob(os.path.join(CSRC, "*.hip")) + glob.glob(os.path.join(CSRC, "*.cpp")))
+
+
+def _headers():
+    return glob.glob(os.path.join(CSRC, "*.hpp")) + glob.glob(os.path.join(INCLUDE, "*.h"))
+
+
+def _compile(src: str, obj: str) -> None:
+    cmd = [HIPCC] + CFLAGS + ["-c", src, "-o", obj]
+    if src.endswith(".cpp"):
+        cmd = [HIPCC, "-x", "hip"] + CFLAGS + ["-c", src, "-o", obj]
+    r = subprocess.run(cmd, capture_output=True, text=True)
+    if r.returncode != 0:
+        raise RuntimeError(f"hipcc failed for {src}:\n{r.stderr}")
+
+
+def build(verbose: bool = False, jobs: int = 8) -> str:
+    os.makedirs(BUILD, exist_ok=True)
+    srcs = _sources()
+    hdr_time = max((os.path.getmtime(h) for h in _headers()), default=0.0)
+    todo = []
+    objs = []
+    for s in srcs:
+        o = os.path.join(BUILD, os.path.basename(s) + ".o")
+        objs.append(o)
+        if not os.path.exists(o) or os.path.getmtime(o) < max(os.path.getmtime(s), hdr_time):
+            todo.append((s, o))
+    if todo:
+        with cf.ThreadPoolExecutor(max_workers=min(jobs, len(todo))) as ex:
+            for f in [ex.submit(_compile, s, o) for s, o in todo]:
+                f.result()
+            if verbose:
+                print(f"compiled {len(todo)} sources")
+    newest = max(os.path.getmtime(o) for o in objs)
+    if todo or not os.path.exists(LIB) or os.path.getmtime(LIB) < newest:
+        cmd = [HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", LIB] + objs
+        r = subprocess.run(cmd, capture_output=True, text=True)
+        if r.returncode != 0:
+            raise RuntimeError(f"link failed:\n{r.stderr}")
+    return LIB
+
+
+if __name__ == "__main__":
+    print(build(verbose=True))
