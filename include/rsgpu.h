@@ -45,8 +45,12 @@ extern "C" {
 #define RS_ERR_NO_DEVICE (-5)   /* no gfx950 device visible                                       */
 
 /* SGD visit schedule (SURVEY §8a parity contract P1/P2) */
-#define RS_SGD_FAST 0    /* user-CSR, one 16-lane group per user, Hogwild q_i, deferred global bias */
+#define RS_SGD_FAST 0    /* user-CSR, one wave per user, atomic q_i deltas, deferred global bias */
 #define RS_SGD_ORDERED 1 /* single group, exact train-set order and update order of svd.go:93-129 */
+
+/* FAST-mode write-back of the item rows (rs_svd_plan_set_mode) */
+#define RS_SGD_WB_ATOMIC 0 /* float-atomic deltas at the memory side: no lost updates (default) */
+#define RS_SGD_WB_STORE 1  /* write-through stores: Hogwild, concurrent updates of a row can be lost */
 
 /* Similarity kinds: core/sim.go Cosine (10-25), MSD (28-44), Pearson (47-81) */
 #define RS_SIM_COSINE 0
@@ -72,7 +76,7 @@ typedef struct {
     double lr;         /* "lr"       */
     double reg;        /* "reg"      */
     int32_t mode;      /* RS_SGD_FAST or RS_SGD_ORDERED */
-    int32_t reserved;
+    int32_t write_back; /* FAST only: RS_SGD_WB_ATOMIC (0, default) or RS_SGD_WB_STORE */
 } rs_sgd_params;
 
 /* ---- context -------------------------------------------------------------------------------- */
@@ -121,8 +125,10 @@ int rs_sim_pair(rs_ctx* ctx, int32_t kind, int64_t na, const int32_t* a_ids, con
                 int64_t nb, const int32_t* b_ids, const double* b_r, double* out);
 
 /* ---- device-resident SVD plan (bench / multi-GPU hosts; device pointers) -------------------- */
-/* A plan uploads the user-CSR once and keeps P, Q, bu, bi, gb resident in HBM (float32, row
- * stride ld = round_up(n_factors, 4)).  Epochs are enqueued on `stream` without host syncs. */
+/* A plan uploads the user-CSR once and keeps the model resident in HBM: P (n_users x ld) and
+ * Q (n_items x ld) float32 with ld = 64 * ceil((n_factors + 1) / 64); columns [0, n_factors) hold
+ * the factors, column ld - 1 the bias (b_u in P, b_i in Q), the rest is zero; GlobalBias is one
+ * float64.  Epochs are enqueued on `stream` without host syncs. */
 typedef struct rs_svd_plan rs_svd_plan;
 
 int rs_svd_plan_create(rs_ctx* ctx, const rs_ratings* r, int32_t n_factors, rs_svd_plan** out);
@@ -134,9 +140,11 @@ int rs_svd_plan_download(rs_svd_plan* plan, double* P, double* Q, double* bu, do
                          double* gb);
 /* Enqueue n_epochs fast-mode epochs (one SGD kernel + one global-bias fold per epoch). */
 int rs_svd_plan_epochs(rs_svd_plan* plan, int32_t n_epochs, float lr, float reg, void* stream);
-/* Device pointers of the resident state (float32 unless noted); ld = row stride in floats. */
-int rs_svd_plan_device_ptrs(rs_svd_plan* plan, void** P, void** Q, void** bu, void** bi,
-                            void** gb_f64, int32_t* ld);
+/* write_back: RS_SGD_WB_ATOMIC (default) or RS_SGD_WB_STORE; ring_depth: item-row prefetch distance
+ * in ratings (4, 8 = default, 16). */
+int rs_svd_plan_set_mode(rs_svd_plan* plan, int32_t write_back, int32_t ring_depth);
+/* Device pointers of the resident state (layout above); ld = row stride in floats. */
+int rs_svd_plan_device_ptrs(rs_svd_plan* plan, void** P, void** Q, void** gb_f64, int32_t* ld);
 /* Per-launch timing: when on, rs_svd_plan_epochs brackets every SGD kernel with HIP events on
  * the stream it runs on (adds one event pair per epoch; leave off for throughput runs). */
 int rs_svd_plan_set_timing(rs_svd_plan* plan, int32_t on);

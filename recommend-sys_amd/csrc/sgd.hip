@@ -1,20 +1,33 @@
 // sgd.hip -- K1: SGD epoch of the Funk-SVD model (reference core/svd.go:63-132), gfx950.
 //
 // Two schedules (SURVEY §8a parity contract):
-//   FAST    user-CSR; one G-lane group per user; p_u and b_u live in VGPRs for the whole user row;
-//           q_i / b_i are gathered (prefetched one rating ahead) and written back Hogwild-style;
-//           GlobalBias (Q2) is a per-group local SGD copy folded at epoch end as
-//           gb += sum_w n_w * (gb_w - gb) / nnz (deterministic fixed-order fold).
-//           Users are dispatched heaviest-first (LPT) so the serial chain of the heaviest user starts
-//           at t=0.  RMSE parity with the reference (P2).
-//   ORDERED one group walks the ratings in train-set order with the exact update order of
+//   FAST    user-CSR, one wave per user row (heaviest user first, LPT); p_u in VGPRs for the whole
+//           row; q_i rows gathered D ratings ahead into a register ring; q_i updates written back
+//           as float-atomic deltas (RS_SGD_WB_ATOMIC, default: no lost updates) or as write-through
+//           stores (RS_SGD_WB_STORE: Hogwild, loses concurrent updates of hot items).  GlobalBias
+//           (Q2) is a per-wave local SGD copy folded at epoch end as gb += sum_w n_w (gb_w - gb)/nnz
+//           (fixed-order, deterministic).  RMSE parity with the reference (P2).
+//   ORDERED one 16-lane group walks the ratings in train-set order with the exact update order of
 //           svd.go:93-129 (aliasing Q1: q_i is updated with the NEW p_u) -- factor parity (P1).
+//
+// Device layout of the FAST plan (HBM, fp32): P is n_users x ld, Q is n_items x ld with
+// ld = 64 * ceil((k + 1) / 64); columns [0, k) hold the factors, column ld - 1 holds the bias
+// (b_u in P, b_i in Q), the rest is zero padding.  Lane l of the wave owns columns l + 64 x, so one
+// row is E = ld / 64 fully coalesced 256-byte wave instructions and the bias sits in lane 63.
+//
+// Cross-XCD visibility (MI355X_MICROARCH.md "Workgroup dispatch, XCD placement & inter-workgroup
+// visibility"): per-CU L1s and per-XCD L2s are not coherent inside a launch.  q_i loads carry sc1
+// (bypass L1) and updates go to the memory side (atomics) or write through (sc1 stores); with plain
+// accesses every XCD trains its own stale copy of the hot rows (measured: ML-100K RMSE 0.972 vs
+// 0.937 for the reference order).
 //
 // Algorithmic bytes per epoch: nnz*(16 + 8k) + U*(16 + 8k)  (fp32 factors).
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cstdlib>
 #include <numeric>
+#include <stdexcept>
 #include <vector>
 
 #include "common.hpp"
@@ -22,134 +35,134 @@
 
 namespace rs {
 
-// --------------------------------------------------------------------------------------------
-// FAST epoch kernel
+constexpr int32_t kOutOfRange = 0x7FFFFFF0;  // buffer offset past num_records: load 0 / drop store
+constexpr int kSgdAux = 16;                  // sc1
 
-template <int G, int V>
+// Sum over the 64 lanes of a wave: DPP inside each 16-lane row, then the gfx950 permlane swaps
+// across rows.  Every lane ends with the bitwise-identical total.
+__device__ __forceinline__ float wave_sum(float x) {
+    x = group_sum<16>(x);
+    auto r16 = __builtin_amdgcn_permlane16_swap(__float_as_uint(x), __float_as_uint(x), false, false);
+    x = __uint_as_float(r16[0]) + __uint_as_float(r16[1]);
+    auto r32 = __builtin_amdgcn_permlane32_swap(__float_as_uint(x), __float_as_uint(x), false, false);
+    return __uint_as_float(r32[0]) + __uint_as_float(r32[1]);
+}
+
+__device__ __forceinline__ float lane63(float x) {
+    return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(x), 63));
+}
+
+// FAST epoch kernel (K1).  Item ids and ratings are wave-uniform: read 16 at a time with scalar
+// loads one batch ahead, so row addresses are SGPR arithmetic.  The 16-rating batch loop is
+// unrolled so every ring index is a compile-time constant.
+template <int E, int D, int WB>
 __global__ __launch_bounds__(256) void svd_epoch_fast_kernel(
     const int32_t* __restrict__ work, int32_t n_work, const int64_t* __restrict__ rowptr,
     const int32_t* __restrict__ items, const float* __restrict__ ratings, float* __restrict__ P,
-    float* Q, float* __restrict__ bu, float* bi, int32_t ld, const double* __restrict__ gb_in,
-    double* __restrict__ gb_partial, float lr, float reg) {
+    float* Q, int32_t q_bytes, const double* __restrict__ gb_in, double* __restrict__ gb_partial,
+    float lr, float reg) {
 #pragma clang fp contract(fast)
-    constexpr int GPB = 256 / G;  // groups per block
-    __shared__ double s_contrib[GPB];
-    const int gl = threadIdx.x & (G - 1);
-    const int grp = threadIdx.x / G;
-    const int w = blockIdx.x * GPB + grp;
+    constexpr int LD = 64 * E, B = 16;
+    static_assert(B % D == 0 && D <= B, "ring depth must divide the 16-rating batch");
+    __shared__ double s_contrib[4];
+    const int lane = threadIdx.x & 63;
+    const int wib = threadIdx.x >> 6;
+    const int w = __builtin_amdgcn_readfirstlane(static_cast<int>(blockIdx.x) * 4 + wib);
     const float gb0 = static_cast<float>(gb_in[0]);
+    const __amdgpu_buffer_rsrc_t rq = __builtin_amdgcn_make_buffer_rsrc(Q, 0, q_bytes, 0x00020000);
+    const int32_t lane4 = lane * 4;
+    const bool bias_lane = lane == 63;
+    const float a = 1.f - lr * reg;
     double contrib = 0.0;
 
     if (w < n_work) {
         const int32_t u = work[w];
         const int64_t b = rowptr[u], e = rowptr[u + 1];
-        bool act[V];
-        float4 p[V];
-        const float* prow = P + static_cast<int64_t>(u) * ld;
+        float p[E];
+        float* prow = P + static_cast<int64_t>(u) * LD;
 #pragma unroll
-        for (int v = 0; v < V; ++v) {
-            const int c = gl + G * v;
-            act[v] = 4 * c < ld;
-            p[v] = act[v] ? *reinterpret_cast<const float4*>(prow + 4 * c) : make_float4(0, 0, 0, 0);
-        }
-        float ub = bu[u];
+        for (int x = 0; x < E; ++x) p[x] = prow[lane + 64 * x];
+        float ub = lane63(p[E - 1]);
         float gb = gb0;
-        if (b < e) {
-            int32_t it = items[b];
-            float rr = ratings[b];
-            float4 q[V];
-            {
-                const float* qrow = Q + static_cast<int64_t>(it) * ld;
+
+        auto load_row = [&](float (&q)[E], int32_t valid, int32_t item) {
+            const int32_t row = valid ? item * (LD * 4) : kOutOfRange;  // SGPR arithmetic
 #pragma unroll
-                for (int v = 0; v < V; ++v)
-                    q[v] = act[v] ? *reinterpret_cast<const float4*>(qrow + 4 * (gl + G * v))
-                                  : make_float4(0, 0, 0, 0);
+            for (int x = 0; x < E; ++x)
+                q[x] = __uint_as_float(
+                    __builtin_amdgcn_raw_buffer_load_b32(rq, row + lane4 + 256 * x, 0, kSgdAux));
+        };
+
+        int32_t it_cur[B], it_nxt[B];
+#pragma unroll
+        for (int j = 0; j < B; ++j) it_cur[j] = items[b + j];  // arrays padded by 64 entries
+#pragma unroll
+        for (int j = 0; j < B; ++j) it_nxt[j] = items[b + B + j];
+        const int32_t deg = static_cast<int32_t>(e - b);
+        float ring[D][E];
+#pragma unroll
+        for (int s = 0; s < D; ++s) load_row(ring[s], s < deg, it_cur[s]);
+
+        for (int64_t base = b; base < e; base += B) {
+            const int32_t rem = static_cast<int32_t>(e - base);  // wave-uniform, SALU compares
+            float rt[B];
+#pragma unroll
+            for (int j = 0; j < B; ++j) rt[j] = ratings[base + j];
+#pragma unroll
+            for (int j = 0; j < B; ++j) {
+                constexpr int kD = D;
+                const int slot = j % kD;
+                if (j < rem) {
+                    float* q = ring[slot];
+                    const float bq = lane63(q[E - 1]);
+                    float s = 0.f;
+#pragma unroll
+                    for (int x = 0; x < E - 1; ++x) s += p[x] * q[x];
+                    s += p[E - 1] * (bias_lane ? 0.f : q[E - 1]);
+                    s = wave_sum(s);
+                    // svd.go:102-128 in FMA form: a = 1 - lr*reg, c = lr*diff:
+                    // p <- a p - c q ; q <- a q - c p_new ; b <- a b - c ; gb <- gb - c
+                    const float diff = ((gb + ub) + bq) + s - rt[j];
+                    const float c = lr * diff;
+                    gb -= c;
+                    ub = __builtin_fmaf(ub, a, -c);
+                    const float bq_new = __builtin_fmaf(bq, a, -c);
+                    float qn[E];
+#pragma unroll
+                    for (int x = 0; x < E; ++x) {
+                        p[x] = __builtin_fmaf(-c, q[x], p[x] * a);
+                        qn[x] = __builtin_fmaf(-c, p[x], q[x] * a);
+                    }
+                    p[E - 1] = bias_lane ? ub : p[E - 1];
+                    qn[E - 1] = bias_lane ? bq_new : qn[E - 1];
+                    const int32_t row = it_cur[j] * (LD * 4);
+#pragma unroll
+                    for (int x = 0; x < E; ++x) {
+                        if constexpr (WB == 1)
+                            __builtin_amdgcn_raw_ptr_buffer_atomic_fadd_f32(qn[x] - q[x], rq,
+                                                                           row + lane4 + 256 * x, 0, 0);
+                        else
+                            __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(qn[x]), rq,
+                                                                  row + lane4 + 256 * x, 0, kSgdAux);
+                    }
+                }
+                // refill this slot with the rating D ahead
+                const int jn = j + D;
+                load_row(ring[slot], jn < rem, jn < B ? it_cur[jn % B] : it_nxt[jn % B]);
             }
-            float bq = bi[it];
-            int32_t itn = it;
-            float rn = 0.f;
-            if (b + 1 < e) {
-                itn = items[b + 1];
-                rn = ratings[b + 1];
-            }
-            for (int64_t pos = b; pos < e; ++pos) {
-                // prefetch rating pos+1's item row and rating pos+2's (item, rating)
-                const bool more = pos + 1 < e;
-                float4 qn[V];
-                float bqn = 0.f;
-                if (more) {
-                    const float* qrow = Q + static_cast<int64_t>(itn) * ld;
 #pragma unroll
-                    for (int v = 0; v < V; ++v)
-                        qn[v] = act[v] ? *reinterpret_cast<const float4*>(qrow + 4 * (gl + G * v))
-                                       : make_float4(0, 0, 0, 0);
-                    bqn = bi[itn];
-                } else {
+            for (int j = 0; j < B; ++j) it_cur[j] = it_nxt[j];
 #pragma unroll
-                    for (int v = 0; v < V; ++v) qn[v] = make_float4(0, 0, 0, 0);
-                }
-                int32_t itnn = 0;
-                float rnn = 0.f;
-                if (pos + 2 < e) {
-                    itnn = items[pos + 2];
-                    rnn = ratings[pos + 2];
-                }
-                // svd.go:102 -> Predict: ((gb + b_u) + b_i) + <p_u, q_i>
-                float s = 0.f;
-#pragma unroll
-                for (int v = 0; v < V; ++v) s += dot4(p[v], q[v]);
-                s = group_sum<G>(s);
-                const float diff = ((gb + ub) + bq) + s - rr;
-                gb -= lr * diff;                                   // svd.go:106 (local copy)
-                const float ub_new = ub - lr * (diff + reg * ub);  // svd.go:108-109
-                const float bq_new = bq - lr * (diff + reg * bq);  // svd.go:111-112
-#pragma unroll
-                for (int v = 0; v < V; ++v) {  // svd.go:114-120 then 122-128 with the new p (Q1)
-                    p[v].x = p[v].x - (q[v].x * diff + p[v].x * reg) * lr;
-                    p[v].y = p[v].y - (q[v].y * diff + p[v].y * reg) * lr;
-                    p[v].z = p[v].z - (q[v].z * diff + p[v].z * reg) * lr;
-                    p[v].w = p[v].w - (q[v].w * diff + p[v].w * reg) * lr;
-                    q[v].x = q[v].x - (p[v].x * diff + q[v].x * reg) * lr;
-                    q[v].y = q[v].y - (p[v].y * diff + q[v].y * reg) * lr;
-                    q[v].z = q[v].z - (p[v].z * diff + q[v].z * reg) * lr;
-                    q[v].w = q[v].w - (p[v].w * diff + q[v].w * reg) * lr;
-                }
-                {
-                    float* qrow = Q + static_cast<int64_t>(it) * ld;
-#pragma unroll
-                    for (int v = 0; v < V; ++v)
-                        if (act[v]) *reinterpret_cast<float4*>(qrow + 4 * (gl + G * v)) = q[v];
-                }
-                bi[it] = bq_new;  // every lane of the group stores the same bits
-                ub = ub_new;
-                if (itn == it) {  // repeated (u, i): use the value just written, not the prefetch
-#pragma unroll
-                    for (int v = 0; v < V; ++v) qn[v] = q[v];
-                    bqn = bq_new;
-                }
-#pragma unroll
-                for (int v = 0; v < V; ++v) q[v] = qn[v];
-                bq = bqn;
-                it = itn;
-                rr = rn;
-                itn = itnn;
-                rn = rnn;
-            }
+            for (int j = 0; j < B; ++j) it_nxt[j] = items[base + 2 * B + j];
         }
-        float* pw = P + static_cast<int64_t>(u) * ld;
 #pragma unroll
-        for (int v = 0; v < V; ++v)
-            if (act[v]) *reinterpret_cast<float4*>(pw + 4 * (gl + G * v)) = p[v];
-        bu[u] = ub;
-        contrib = static_cast<double>(e - b) * (static_cast<double>(gb) - static_cast<double>(gb0));
+        for (int x = 0; x < E; ++x) prow[lane + 64 * x] = p[x];
+        contrib = static_cast<double>(deg) * (static_cast<double>(gb) - static_cast<double>(gb0));
     }
-    if (gl == 0) s_contrib[grp] = contrib;
+    if (lane == 0) s_contrib[wib] = contrib;
     __syncthreads();
-    if (threadIdx.x == 0) {
-        double t = 0.0;
-        for (int g = 0; g < GPB; ++g) t += s_contrib[g];
-        gb_partial[blockIdx.x] = t;
-    }
+    if (threadIdx.x == 0)
+        gb_partial[blockIdx.x] = ((s_contrib[0] + s_contrib[1]) + s_contrib[2]) + s_contrib[3];
 }
 
 // gb += (sum of block partials in fixed order) / nnz  -- one block, deterministic tree.
@@ -257,15 +270,17 @@ struct rs_svd_plan {
     rs::DevBuf<int32_t> items;
     rs::DevBuf<float> ratings;
     rs::DevBuf<int32_t> work;
-    rs::DevBuf<float> P, Q, bu, bi;
+    rs::DevBuf<float> P, Q;  // bias in column ld - 1
     rs::DevBuf<double> gb, partial;
     int32_t n_blocks = 0;
+    int32_t write_back = RS_SGD_WB_ATOMIC;
+    int32_t ring_depth = 8;
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
     double last_ms = 0.0;
     int32_t last_launches = 0;
     bool timing = false;
     hipStream_t last_stream = nullptr;  // stream of the last enqueued epochs (synced before copies)
-    std::vector<hipEvent_t> tev;  // timing mode: [2 * epoch] start, [2 * epoch + 1] end
+    std::vector<hipEvent_t> tev;        // timing mode: [2 * epoch] start, [2 * epoch + 1] end
     int32_t tev_used = 0;
     ~rs_svd_plan() {
         if (ev0) (void)hipEventDestroy(ev0);
@@ -276,22 +291,42 @@ struct rs_svd_plan {
 
 namespace rs {
 
-static int fast_groups(int32_t ld) { return ld <= 32 ? 8 : 16; }
+constexpr int32_t kMaxFactors = 511;
 
-template <int G, int V>
+template <int E, int D, int WB>
 static void launch_fast_t(rs_svd_plan* pl, float lr, float reg, hipStream_t s) {
-    hipLaunchKernelGGL((svd_epoch_fast_kernel<G, V>), dim3(pl->n_blocks), dim3(256), 0, s,
+    const int32_t q_bytes = static_cast<int32_t>(pl->Q.n * sizeof(float));
+    hipLaunchKernelGGL((svd_epoch_fast_kernel<E, D, WB>), dim3(pl->n_blocks), dim3(256), 0, s,
                        pl->work.p, pl->n_work, pl->rowptr.p, pl->items.p, pl->ratings.p, pl->P.p,
-                       pl->Q.p, pl->bu.p, pl->bi.p, pl->ld, pl->gb.p, pl->partial.p, lr, reg);
+                       pl->Q.p, q_bytes, pl->gb.p, pl->partial.p, lr, reg);
+}
+
+template <int D, int WB>
+static void launch_fast_e(rs_svd_plan* pl, float lr, float reg, hipStream_t s) {
+    switch (pl->ld / 64) {
+        case 1: launch_fast_t<1, D, WB>(pl, lr, reg, s); break;
+        case 2: launch_fast_t<2, D, WB>(pl, lr, reg, s); break;
+        case 3: launch_fast_t<3, D, WB>(pl, lr, reg, s); break;
+        case 4: launch_fast_t<4, D, WB>(pl, lr, reg, s); break;
+        case 5: launch_fast_t<5, D, WB>(pl, lr, reg, s); break;
+        case 6: launch_fast_t<6, D, WB>(pl, lr, reg, s); break;
+        case 7: launch_fast_t<7, D, WB>(pl, lr, reg, s); break;
+        default: launch_fast_t<8, D, WB>(pl, lr, reg, s); break;
+    }
+}
+
+template <int WB>
+static void launch_fast_d(rs_svd_plan* pl, float lr, float reg, hipStream_t s) {
+    switch (pl->ring_depth) {
+        case 4: launch_fast_e<4, WB>(pl, lr, reg, s); break;
+        case 16: launch_fast_e<16, WB>(pl, lr, reg, s); break;
+        default: launch_fast_e<8, WB>(pl, lr, reg, s); break;
+    }
 }
 
 static void launch_fast(rs_svd_plan* pl, float lr, float reg, hipStream_t s) {
-    const int32_t ld = pl->ld;
-    if (ld <= 32) launch_fast_t<8, 1>(pl, lr, reg, s);
-    else if (ld <= 64) launch_fast_t<16, 1>(pl, lr, reg, s);
-    else if (ld <= 128) launch_fast_t<16, 2>(pl, lr, reg, s);
-    else if (ld <= 256) launch_fast_t<16, 4>(pl, lr, reg, s);
-    else launch_fast_t<16, 8>(pl, lr, reg, s);
+    if (pl->write_back == RS_SGD_WB_STORE) launch_fast_d<0>(pl, lr, reg, s);  // template WB: 0 store
+    else launch_fast_d<1>(pl, lr, reg, s);                                    //             1 atomic
     RS_HIP(hipGetLastError());
 }
 
@@ -309,7 +344,7 @@ static void launch_ordered(int64_t nnz, const int32_t* u, const int32_t* i, cons
     RS_HIP(hipGetLastError());
 }
 
-constexpr int32_t kMaxFactors = 512;
+int32_t fast_ld(int32_t k) { return 64 * ((k + 1 + 63) / 64); }
 
 static void plan_build(rs_ctx* ctx, const rs_ratings* r, int32_t k, rs_svd_plan* pl) {
     hipStream_t s = ctx->stream;
@@ -317,8 +352,10 @@ static void plan_build(rs_ctx* ctx, const rs_ratings* r, int32_t k, rs_svd_plan*
     pl->n_users = r->n_users;
     pl->n_items = r->n_items;
     pl->k = k;
-    pl->ld = round_up4(k);
+    pl->ld = fast_ld(k);
     pl->nnz = r->nnz;
+    if (static_cast<int64_t>(std::max(1, r->n_items)) * pl->ld * 4 >= (int64_t{1} << 31) - 64)
+        throw std::invalid_argument("n_items * n_factors too large for 32-bit buffer offsets");
     UserCSR csr;
     build_csr(r->nnz, r->n_users, r->users, r->items, r->ratings, csr);
     // LPT dispatch order: heaviest user first (ties by user id), empty users dropped.
@@ -330,11 +367,13 @@ static void plan_build(rs_ctx* ctx, const rs_ratings* r, int32_t k, rs_svd_plan*
         return csr.rowptr[a + 1] - csr.rowptr[a] > csr.rowptr[b + 1] - csr.rowptr[b];
     });
     pl->n_work = static_cast<int32_t>(order.size());
-    const int gpb = 256 / fast_groups(pl->ld);
-    pl->n_blocks = std::max<int32_t>(1, (pl->n_work + gpb - 1) / gpb);
+    pl->n_blocks = std::max<int32_t>(1, (pl->n_work + 3) / 4);  // one wave per user, 4 per block
+    // items / ratings padded by 64 entries: the kernel reads whole 16-entry batches (two ahead)
+    csr.cols.resize(csr.cols.size() + 64, 0);
+    csr.vals.resize(csr.vals.size() + 64, 0.f);
     pl->rowptr.alloc(csr.rowptr.size());
-    pl->items.alloc(std::max<size_t>(1, csr.cols.size()));
-    pl->ratings.alloc(std::max<size_t>(1, csr.vals.size()));
+    pl->items.alloc(csr.cols.size());
+    pl->ratings.alloc(csr.vals.size());
     pl->work.alloc(std::max<size_t>(1, order.size()));
     pl->rowptr.upload(csr.rowptr.data(), csr.rowptr.size(), s);
     pl->items.upload(csr.cols.data(), csr.cols.size(), s);
@@ -342,14 +381,10 @@ static void plan_build(rs_ctx* ctx, const rs_ratings* r, int32_t k, rs_svd_plan*
     pl->work.upload(order.data(), order.size(), s);
     pl->P.alloc(static_cast<size_t>(std::max(1, r->n_users)) * pl->ld);
     pl->Q.alloc(static_cast<size_t>(std::max(1, r->n_items)) * pl->ld);
-    pl->bu.alloc(std::max(1, r->n_users));
-    pl->bi.alloc(std::max(1, r->n_items));
     pl->gb.alloc(1);
     pl->partial.alloc(pl->n_blocks);
     RS_HIP(hipMemsetAsync(pl->P.p, 0, pl->P.n * sizeof(float), s));
     RS_HIP(hipMemsetAsync(pl->Q.p, 0, pl->Q.n * sizeof(float), s));
-    RS_HIP(hipMemsetAsync(pl->bu.p, 0, pl->bu.n * sizeof(float), s));
-    RS_HIP(hipMemsetAsync(pl->bi.p, 0, pl->bi.n * sizeof(float), s));
     RS_HIP(hipMemsetAsync(pl->gb.p, 0, sizeof(double), s));
     RS_HIP(hipEventCreate(&pl->ev0));
     RS_HIP(hipEventCreate(&pl->ev1));
@@ -360,31 +395,36 @@ static void plan_sync_last(rs_svd_plan* pl) {
     if (pl->last_stream) RS_HIP(hipStreamSynchronize(pl->last_stream));
 }
 
+// f64 factor rows (stride k) + bias -> f32 rows of ld floats with the bias in column ld - 1
+static void pack_with_bias(const double* F, const double* bias, int64_t rows, int32_t k, int32_t ld,
+                           const std::vector<float>& old, std::vector<float>& dst) {
+    dst.assign(static_cast<size_t>(rows) * ld, 0.f);
+    for (int64_t r = 0; r < rows; ++r) {
+        float* d = dst.data() + r * ld;
+        if (F) for (int32_t f = 0; f < k; ++f) d[f] = static_cast<float>(F[r * k + f]);
+        else for (int32_t f = 0; f < k; ++f) d[f] = old[r * ld + f];
+        d[ld - 1] = bias ? static_cast<float>(bias[r]) : old[r * ld + ld - 1];
+    }
+}
+
 static void plan_upload(rs_svd_plan* pl, const double* P, const double* Q, const double* bu,
                         const double* bi, const double* gb) {
     plan_sync_last(pl);
     hipStream_t s = pl->ctx->stream;
-    std::vector<float> tmp;
-    if (P) {
-        pack_rows_f32(P, pl->n_users, pl->k, pl->ld, tmp);
-        pl->P.upload(tmp.data(), tmp.size(), s);
+    std::vector<float> old, tmp;
+    auto put = [&](DevBuf<float>& d, int64_t rows, const double* F, const double* bias) {
+        if (!F && !bias) return;
+        if (!F || !bias) {  // partial update: keep the other half of the row
+            old.resize(static_cast<size_t>(rows) * pl->ld);
+            d.download(old.data(), old.size(), s);
+            RS_HIP(hipStreamSynchronize(s));
+        }
+        pack_with_bias(F, bias, rows, pl->k, pl->ld, old, tmp);
+        d.upload(tmp.data(), tmp.size(), s);
         RS_HIP(hipStreamSynchronize(s));
-    }
-    if (Q) {
-        pack_rows_f32(Q, pl->n_items, pl->k, pl->ld, tmp);
-        pl->Q.upload(tmp.data(), tmp.size(), s);
-        RS_HIP(hipStreamSynchronize(s));
-    }
-    if (bu) {
-        pack_rows_f32(bu, pl->n_users, 1, 1, tmp);
-        pl->bu.upload(tmp.data(), tmp.size(), s);
-        RS_HIP(hipStreamSynchronize(s));
-    }
-    if (bi) {
-        pack_rows_f32(bi, pl->n_items, 1, 1, tmp);
-        pl->bi.upload(tmp.data(), tmp.size(), s);
-        RS_HIP(hipStreamSynchronize(s));
-    }
+    };
+    put(pl->P, pl->n_users, P, bu);
+    put(pl->Q, pl->n_items, Q, bi);
     if (gb) {
         pl->gb.upload(gb, 1, s);
         RS_HIP(hipStreamSynchronize(s));
@@ -396,16 +436,18 @@ static void plan_download(rs_svd_plan* pl, double* P, double* Q, double* bu, dou
     plan_sync_last(pl);
     hipStream_t s = pl->ctx->stream;
     std::vector<float> tmp;
-    auto get = [&](const DevBuf<float>& d, int64_t rows, int32_t k, int32_t ld, double* out) {
-        tmp.resize(static_cast<size_t>(rows) * ld);
+    auto get = [&](const DevBuf<float>& d, int64_t rows, double* F, double* bias) {
+        if (!F && !bias) return;
+        tmp.resize(static_cast<size_t>(rows) * pl->ld);
         d.download(tmp.data(), tmp.size(), s);
         RS_HIP(hipStreamSynchronize(s));
-        unpack_rows_f64(tmp, rows, k, ld, out);
+        for (int64_t r = 0; r < rows; ++r) {
+            if (F) for (int32_t f = 0; f < pl->k; ++f) F[r * pl->k + f] = tmp[r * pl->ld + f];
+            if (bias) bias[r] = tmp[r * pl->ld + pl->ld - 1];
+        }
     };
-    if (P) get(pl->P, pl->n_users, pl->k, pl->ld, P);
-    if (Q) get(pl->Q, pl->n_items, pl->k, pl->ld, Q);
-    if (bu) get(pl->bu, pl->n_users, 1, 1, bu);
-    if (bi) get(pl->bi, pl->n_items, 1, 1, bi);
+    get(pl->P, pl->n_users, P, bu);
+    get(pl->Q, pl->n_items, Q, bi);
     if (gb) {
         pl->gb.download(gb, 1, s);
         RS_HIP(hipStreamSynchronize(s));
@@ -442,7 +484,7 @@ static int check_sgd(rs_ctx* ctx, const rs_ratings* r, const rs_sgd_params* p) {
     if (st != RS_OK) return st;
     if (!p) return set_error(ctx, RS_ERR_INVALID, "params is NULL");
     if (p->n_factors < 1 || p->n_factors > kMaxFactors)
-        return set_error(ctx, RS_ERR_UNSUPPORTED, "n_factors must be in [1, 512]");
+        return set_error(ctx, RS_ERR_UNSUPPORTED, "n_factors must be in [1, 511]");
     if (p->n_epochs < 0) return set_error(ctx, RS_ERR_INVALID, "n_epochs < 0");
     if (p->mode != RS_SGD_FAST && p->mode != RS_SGD_ORDERED)
         return set_error(ctx, RS_ERR_INVALID, "unknown SGD mode");
@@ -463,7 +505,7 @@ extern "C" int rs_svd_plan_create(rs_ctx* ctx, const rs_ratings* r, int32_t n_fa
         int st = rs::check_ratings(ctx, r);
         if (st != RS_OK) return st;
         if (n_factors < 1 || n_factors > rs::kMaxFactors)
-            return rs::set_error(ctx, RS_ERR_UNSUPPORTED, "n_factors must be in [1, 512]");
+            return rs::set_error(ctx, RS_ERR_UNSUPPORTED, "n_factors must be in [1, 511]");
         auto* pl = new rs_svd_plan();
         try {
             rs::plan_build(ctx, r, n_factors, pl);
@@ -478,10 +520,21 @@ extern "C" int rs_svd_plan_create(rs_ctx* ctx, const rs_ratings* r, int32_t n_fa
 
 extern "C" void rs_svd_plan_destroy(rs_svd_plan* pl) {
     if (!pl) return;
+    // Destroy before closing the owning ctx (its stream may be the last one used).
     (void)hipSetDevice(pl->ctx->device);
     if (pl->last_stream) (void)hipStreamSynchronize(pl->last_stream);
-    (void)hipStreamSynchronize(pl->ctx->stream);
     delete pl;
+}
+
+extern "C" int rs_svd_plan_set_mode(rs_svd_plan* pl, int32_t write_back, int32_t ring_depth) {
+    if (!pl) return rs::set_error(nullptr, RS_ERR_INVALID, "plan is NULL");
+    if (write_back != RS_SGD_WB_ATOMIC && write_back != RS_SGD_WB_STORE)
+        return rs::set_error(pl->ctx, RS_ERR_INVALID, "unknown write-back mode");
+    if (ring_depth != 4 && ring_depth != 8 && ring_depth != 16)
+        return rs::set_error(pl->ctx, RS_ERR_INVALID, "ring depth must be 4, 8 or 16");
+    pl->write_back = write_back;
+    pl->ring_depth = ring_depth;
+    return RS_OK;
 }
 
 extern "C" int rs_svd_plan_upload(rs_svd_plan* pl, const double* P, const double* Q,
@@ -513,13 +566,11 @@ extern "C" int rs_svd_plan_epochs(rs_svd_plan* pl, int32_t n_epochs, float lr, f
     });
 }
 
-extern "C" int rs_svd_plan_device_ptrs(rs_svd_plan* pl, void** P, void** Q, void** bu, void** bi,
-                                       void** gb, int32_t* ld) {
+extern "C" int rs_svd_plan_device_ptrs(rs_svd_plan* pl, void** P, void** Q, void** gb,
+                                       int32_t* ld) {
     if (!pl) return rs::set_error(nullptr, RS_ERR_INVALID, "plan is NULL");
     if (P) *P = pl->P.p;
     if (Q) *Q = pl->Q.p;
-    if (bu) *bu = pl->bu.p;
-    if (bi) *bi = pl->bi.p;
     if (gb) *gb = pl->gb.p;
     if (ld) *ld = pl->ld;
     return RS_OK;
@@ -567,6 +618,7 @@ extern "C" int rs_svd_fit(rs_ctx* ctx, const rs_ratings* r, const rs_sgd_params*
         if (p->mode == RS_SGD_FAST) {
             rs_svd_plan pl;
             rs::plan_build(ctx, r, p->n_factors, &pl);
+            pl.write_back = p->write_back == RS_SGD_WB_STORE ? RS_SGD_WB_STORE : RS_SGD_WB_ATOMIC;
             rs::plan_upload(&pl, P, Q, bu, bi, gb);
             rs::plan_epochs(&pl, p->n_epochs, lr, reg, ctx->stream);
             rs::plan_download(&pl, P, Q, bu, bi, gb);

@@ -7,6 +7,7 @@ from __future__ import annotations
 
 import ctypes as C
 import os
+import weakref
 
 import numpy as np
 
@@ -18,6 +19,7 @@ _lib = None
 RS_OK = 0
 RS_ERR_INVALID, RS_ERR_HIP, RS_ERR_NOMEM, RS_ERR_UNSUPPORTED, RS_ERR_NO_DEVICE = -1, -2, -3, -4, -5
 SGD_FAST, SGD_ORDERED = 0, 1
+WB_ATOMIC, WB_STORE = 0, 1
 SIM_COSINE, SIM_MSD, SIM_PEARSON = 0, 1, 2
 
 HEADER_SYMBOLS = (
@@ -25,7 +27,7 @@ HEADER_SYMBOLS = (
     "rs_svd_fit", "rs_svd_predict", "rs_svdpp_fit", "rs_nmf_fit", "rs_baseline_fit",
     "rs_knn_sims", "rs_sim_pair", "rs_svd_plan_create", "rs_svd_plan_destroy",
     "rs_svd_plan_upload", "rs_svd_plan_download", "rs_svd_plan_epochs",
-    "rs_svd_plan_device_ptrs", "rs_svd_plan_set_timing", "rs_svd_plan_last_kernel_ms",
+    "rs_svd_plan_device_ptrs", "rs_svd_plan_set_mode", "rs_svd_plan_set_timing", "rs_svd_plan_last_kernel_ms",
 )
 
 
@@ -42,7 +44,7 @@ class _Ratings(C.Structure):
 
 class _SgdParams(C.Structure):
     _fields_ = [("n_factors", C.c_int32), ("n_epochs", C.c_int32), ("lr", C.c_double),
-                ("reg", C.c_double), ("mode", C.c_int32), ("reserved", C.c_int32)]
+                ("reg", C.c_double), ("mode", C.c_int32), ("write_back", C.c_int32)]
 
 
 _vp = C.c_void_p
@@ -82,8 +84,8 @@ def lib():
             "rs_svd_plan_download": (C.c_int, [_vp, _vp, _vp, _vp, _vp, _vp]),
             "rs_svd_plan_epochs": (C.c_int, [_vp, _i32, _flt, _flt, _vp]),
             "rs_svd_plan_device_ptrs": (C.c_int, [_vp, C.POINTER(_vp), C.POINTER(_vp),
-                                                  C.POINTER(_vp), C.POINTER(_vp), C.POINTER(_vp),
-                                                  C.POINTER(_i32)]),
+                                                  C.POINTER(_vp), C.POINTER(_i32)]),
+            "rs_svd_plan_set_mode": (C.c_int, [_vp, _i32, _i32]),
             "rs_svd_plan_set_timing": (C.c_int, [_vp, _i32]),
             "rs_svd_plan_last_kernel_ms": (C.c_int, [_vp, C.POINTER(_dbl), C.POINTER(_i32)]),
         }
@@ -136,9 +138,12 @@ class Context:
             raise RsError(code, lib().rs_last_error(None).decode())
         self.h = h
         self.device = device
+        self._plans = weakref.WeakSet()
 
     def close(self):
         if self.h:
+            for pl in list(self._plans):
+                pl.close()
             lib().rs_close(self.h)
             self.h = None
 
@@ -160,14 +165,14 @@ class Context:
     # ---- estimators --------------------------------------------------------------------------
 
     def svd_fit(self, r: Ratings, P, Q, bu=None, bi=None, gb=0.0, n_epochs=20, lr=0.005,
-                reg=0.02, mode=SGD_FAST):
+                reg=0.02, mode=SGD_FAST, write_back=WB_ATOMIC):
         P = np.array(P, dtype=np.float64, order="C")
         Q = np.array(Q, dtype=np.float64, order="C")
         bu = np.zeros(r.n_users) if bu is None else np.array(bu, dtype=np.float64)
         bi = np.zeros(r.n_items) if bi is None else np.array(bi, dtype=np.float64)
         g = np.array([gb], dtype=np.float64)
         assert P.shape == (r.n_users, P.shape[1]) and Q.shape == (r.n_items, P.shape[1])
-        prm = _SgdParams(P.shape[1], n_epochs, lr, reg, mode, 0)
+        prm = _SgdParams(P.shape[1], n_epochs, lr, reg, mode, write_back)
         rc = r.c()
         self.check(lib().rs_svd_fit(self.h, C.byref(rc), C.byref(prm), _ptr(P), _ptr(Q),
                                     _ptr(bu), _ptr(bi), _ptr(g)))
@@ -186,8 +191,10 @@ class SvdPlan:
         self.nnz = len(r.ratings)
         h = C.c_void_p()
         rc = r.c()
+        self.h = None
         ctx.check(lib().rs_svd_plan_create(ctx.h, C.byref(rc), n_factors, C.byref(h)))
         self.h = h
+        ctx._plans.add(self)
 
     def upload(self, P=None, Q=None, bu=None, bi=None, gb=None):
         arrs = [None if a is None else np.ascontiguousarray(a, dtype=np.float64)
@@ -206,8 +213,11 @@ class SvdPlan:
     def epochs(self, n, lr=0.005, reg=0.02, stream=None):
         self.ctx.check(lib().rs_svd_plan_epochs(self.h, n, lr, reg, stream))
 
+    def set_mode(self, write_back=WB_ATOMIC, ring_depth=8):
+        self.ctx.check(lib().rs_svd_plan_set_mode(self.h, write_back, ring_depth))
+
     def device_ptrs(self):
-        ps = [C.c_void_p() for _ in range(5)]
+        ps = [C.c_void_p() for _ in range(3)]
         ld = _i32(0)
         self.ctx.check(lib().rs_svd_plan_device_ptrs(self.h, *[C.byref(p) for p in ps],
                                                      C.byref(ld)))

@@ -23,7 +23,10 @@ ARCH = "gfx950"
 
 # -ffp-contract=off: parity kernels must not fuse a*b+c (the Go reference never does);
 # fast kernels opt back in locally with `#pragma clang fp contract(fast)`.
-CFLAGS = ["-O3", "-std=c++17", "-fPIC", "-ffp-contract=off", f"--offload-arch={ARCH}",
+# -fno-slp-vectorize: hipcc's SLP pass packs independent f32 FMAs into v_pk_* plus v_mov
+# shuffles, which costs issue slots on the latency chain of the SGD kernels.
+CFLAGS = ["-O3", "-std=c++17", "-fPIC", "-ffp-contract=off", "-fno-slp-vectorize",
+          f"--offload-arch={ARCH}",
           "-Wall", "-Wno-unused-result", f"-I{INCLUDE}", f"-I{CSRC}"]
 
 

@@ -70,8 +70,9 @@ def _disjoint_input(n_users=300, per_user=12, k=64, seed=4, ragged=True):
     return users, items, r, n_users, len(users)
 
 
-@pytest.mark.parametrize("k", [8, 20, 64, 100, 128, 256])
-def test_fast_matches_own_schedule_race_free(ctx, k):
+@pytest.mark.parametrize("wb", [rsgpu.WB_ATOMIC, rsgpu.WB_STORE])
+@pytest.mark.parametrize("k", [8, 20, 63, 64, 100, 128, 256, 511])
+def test_fast_matches_own_schedule_race_free(ctx, k, wb):
     u, i, r, nu, ni = _disjoint_input(k=k)
     rng = np.random.default_rng(k)
     P0, Q0 = rng.normal(0, 0.1, (nu, k)), rng.normal(0, 0.1, (ni, k))
@@ -79,7 +80,7 @@ def test_fast_matches_own_schedule_race_free(ctx, k):
     for epochs in (1, 3):
         ref = O.svd_fit_chunked(rowptr, items, rr, P0, Q0, 1 << 30, epochs=epochs)
         got = ctx.svd_fit(rsgpu.Ratings(u, i, r, nu, ni), P0, Q0, n_epochs=epochs,
-                          mode=rsgpu.SGD_FAST)
+                          mode=rsgpu.SGD_FAST, write_back=wb)
         assert _maxdiff(ref[:4], got[:4]) <= TOL, (k, epochs)
         assert abs(ref[4] - got[4]) <= TOL
 
@@ -143,7 +144,7 @@ def test_bad_arguments(ctx):
         ctx.svd_fit(rsgpu.Ratings([0, 5], [0, 0], [1.0, 2.0], 2, 1), np.zeros((2, 4)),
                     np.zeros((1, 4)))
     with pytest.raises(rsgpu.RsError):
-        ctx.svd_fit(rsgpu.Ratings([0], [0], [1.0], 1, 1), np.zeros((1, 600)), np.zeros((1, 600)))
+        ctx.svd_fit(rsgpu.Ratings([0], [0], [1.0], 1, 1), np.zeros((1, 512)), np.zeros((1, 512)))
 
 
 def test_empty_and_tiny_inputs(ctx):
