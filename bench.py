@@ -162,7 +162,7 @@ def main():
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
                          "traffic": traffic,
-                         "kernel": "svd_epoch_fast_kernel<16,2>",
+                         "kernel": "svd_epoch_fast_kernel<E=2,D=8,atomic>",
                          "avg_kernel_us": avg_kernel_s * 1e6,
                          "algorithmic_bytes_per_launch": ab},
             "finite": finite,
