@@ -13,11 +13,3 @@ extern "C" int rs_baseline_fit(rs_ctx* ctx, const rs_ratings*, int32_t, double, 
                                double*, double*) {
     return rs::set_error(ctx, RS_ERR_UNSUPPORTED, "rs_baseline_fit: not built yet");
 }
-extern "C" int rs_knn_sims(rs_ctx* ctx, int32_t, int32_t, int32_t, const int64_t*, const int32_t*,
-                           const double*, double*) {
-    return rs::set_error(ctx, RS_ERR_UNSUPPORTED, "rs_knn_sims: not built yet");
-}
-extern "C" int rs_sim_pair(rs_ctx* ctx, int32_t, int64_t, const int32_t*, const double*, int64_t,
-                           const int32_t*, const double*, double*) {
-    return rs::set_error(ctx, RS_ERR_UNSUPPORTED, "rs_sim_pair: not built yet");
-}

@@ -1,0 +1,419 @@
+// sim.hip -- K4 / K5: all-pairs similarity of KNN.Fit (reference core/knn.go:224-298 with
+// core/sim.go:10-81 as the pair function), gfx950.
+//
+// K4 (Cosine, MSD; bit-exact): when every rating is r = x / s with integer x, s in {1, 2} and
+// |x| <= 11 (ML-100K/1M integer stars: s = 1; ML-20M half stars: s = 2), the co-rated sums of
+// sim.go are exact integers times 1/s^2.  They are computed as int8 x int8 -> int32 MFMA
+// contractions over the dense (left x right) matrices X (x), X2 (x^2) and M (1 where rated):
+//     l = X X^T,   m = X2 M^T,   n = M X2^T,   count = M M^T  (MSD only)
+// and the float64 epilogue evaluates exactly the reference expressions
+//     Cosine  l / (sqrt(m) * sqrt(n))            (sim.go:24)
+//     MSD     1 / (sum / count + 1), sum = m + n - 2 l  (sim.go:43)
+// on the exactly-representable sums, so every similarity (and the NaN pattern: 0/0 where nothing
+// is co-rated, knn.go:286) is bitwise equal to the reference's sorted-merge result.
+// Only tiles of the upper triangle are computed; each writes S[a][b] and S[b][a] (knn.go:287-288)
+// and the diagonal stays NaN (knn.go:283).
+//
+// K5 (Pearson, and Cosine/MSD when ratings are not of that form): one workgroup per left row a,
+// row a scattered densely into LDS (or a global scratch row), one thread per partner b > a walking
+// b's ID-sorted list; the co-rated IDs are therefore visited in ascending order exactly like the
+// sorted merge of sim.go, with the same float64 operations in the same order -> bitwise equal.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstdlib>
+#include <limits>
+#include <numeric>
+#include <vector>
+
+#include "common.hpp"
+
+namespace rs {
+
+typedef int i32x4 __attribute__((ext_vector_type(4)));
+typedef int i32x16 __attribute__((ext_vector_type(16)));
+
+constexpr int kTile = 128;   // block tile (a x b)
+constexpr int kKBlock = 64;  // bytes of the contraction dimension per iteration
+
+// ---------------------------------------------------------------------------------------------
+// dense operands: X[a][k] = x, X2 = x^2, M = 1 (rows padded to kTile, k padded to kKBlock)
+
+__global__ void knn_scatter_kernel(int32_t L, const int64_t* __restrict__ rowptr,
+                                   const int32_t* __restrict__ ids, const int8_t* __restrict__ x,
+                                   int64_t ldk, int8_t* __restrict__ X, int8_t* __restrict__ X2,
+                                   int8_t* __restrict__ M) {
+    const int32_t a = blockIdx.x;
+    if (a >= L) return;
+    for (int64_t t = rowptr[a] + threadIdx.x; t < rowptr[a + 1]; t += blockDim.x) {
+        const int64_t o = static_cast<int64_t>(a) * ldk + ids[t];
+        const int8_t v = x[t];
+        X[o] = v;
+        X2[o] = static_cast<int8_t>(v * v);
+        M[o] = 1;
+    }
+}
+
+__device__ __forceinline__ void tri_tile(int32_t t, int32_t& ta, int32_t& tb) {
+    // t enumerates (ta, tb), ta <= tb, column-major over tb: t = tb (tb + 1) / 2 + ta
+    int32_t b = static_cast<int32_t>((sqrt(8.0 * t + 1.0) - 1.0) * 0.5);
+    while (static_cast<int64_t>(b) * (b + 1) / 2 > t) --b;
+    while (static_cast<int64_t>(b + 1) * (b + 2) / 2 <= t) ++b;
+    tb = b;
+    ta = t - b * (b + 1) / 2;
+}
+
+// KIND 0 = Cosine (3 contractions), 1 = MSD (4 contractions)
+template <int KIND>
+__global__ __launch_bounds__(256) void knn_sims_mfma_kernel(
+    const int8_t* __restrict__ X, const int8_t* __restrict__ X2, const int8_t* __restrict__ M,
+    int64_t ldk, int32_t L, double inv_s2, double* __restrict__ S) {
+    constexpr int NC = KIND == 0 ? 3 : 4;
+    int32_t ta, tb;
+    tri_tile(static_cast<int32_t>(blockIdx.x), ta, tb);
+    const int lane = threadIdx.x & 63;
+    const int wave = threadIdx.x >> 6;
+    const int wa = wave >> 1, wb = wave & 1;
+    if (ta == tb && wa > wb) return;  // strictly below the diagonal: covered by its mirror
+    const int32_t r0 = ta * kTile + 64 * wa;  // left rows (a)
+    const int32_t c0 = tb * kTile + 64 * wb;  // partner rows (b)
+    const int row = lane & 31, half = lane >> 5;
+
+    i32x16 acc[NC][2][2];
+#pragma unroll
+    for (int c = 0; c < NC; ++c)
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+#pragma unroll
+            for (int j = 0; j < 2; ++j) acc[c][i][j] = i32x16{};
+
+    // Lane (row, half) reads bytes [32 half, 32 half + 32) of each 64-byte K block of its row: the
+    // same bijection k <-> (lane, element) for both operands, so sum_k A[a][k] B[b][k] is exact
+    // whatever the MFMA's internal k order.
+    const int8_t* pa[3][2];
+    const int8_t* pb[3][2];
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+        const int64_t oa = static_cast<int64_t>(r0 + 32 * i + row) * ldk + 32 * half;
+        const int64_t ob = static_cast<int64_t>(c0 + 32 * i + row) * ldk + 32 * half;
+        pa[0][i] = X + oa;  pa[1][i] = X2 + oa;  pa[2][i] = M + oa;
+        pb[0][i] = X + ob;  pb[1][i] = X2 + ob;  pb[2][i] = M + ob;
+    }
+    for (int64_t k0 = 0; k0 < ldk; k0 += kKBlock) {
+        i32x4 fa[3][2][2], fb[3][2][2];  // [matrix][tile][k-half of the 32 bytes]
+#pragma unroll
+        for (int m = 0; m < 3; ++m)
+#pragma unroll
+            for (int i = 0; i < 2; ++i) {
+                const i32x4* qa = reinterpret_cast<const i32x4*>(pa[m][i] + k0);
+                const i32x4* qb = reinterpret_cast<const i32x4*>(pb[m][i] + k0);
+                fa[m][i][0] = qa[0];
+                fa[m][i][1] = qa[1];
+                fb[m][i][0] = qb[0];
+                fb[m][i][1] = qb[1];
+            }
+#pragma unroll
+        for (int s = 0; s < 2; ++s)
+#pragma unroll
+            for (int i = 0; i < 2; ++i)
+#pragma unroll
+                for (int j = 0; j < 2; ++j) {
+                    acc[0][i][j] = __builtin_amdgcn_mfma_i32_32x32x32_i8(fa[0][i][s], fb[0][j][s], acc[0][i][j], 0, 0, 0);
+                    acc[1][i][j] = __builtin_amdgcn_mfma_i32_32x32x32_i8(fa[1][i][s], fb[2][j][s], acc[1][i][j], 0, 0, 0);
+                    acc[2][i][j] = __builtin_amdgcn_mfma_i32_32x32x32_i8(fa[2][i][s], fb[1][j][s], acc[2][i][j], 0, 0, 0);
+                    if constexpr (NC == 4)
+                        acc[3][i][j] = __builtin_amdgcn_mfma_i32_32x32x32_i8(fa[2][i][s], fb[2][j][s], acc[3][i][j], 0, 0, 0);
+                }
+    }
+    // epilogue: C/D layout of 32x32 MFMA: col = lane & 31, row = (q & 3) + 8 (q >> 2) + 4 (lane >> 5)
+    const double nan = __builtin_nan("");
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+#pragma unroll
+            for (int q = 0; q < 16; ++q) {
+                const int32_t a = r0 + 32 * i + (q & 3) + 8 * (q >> 2) + 4 * half;
+                const int32_t b = c0 + 32 * j + row;
+                if (a >= L || b >= L) continue;
+                if (a == b) {
+                    S[static_cast<int64_t>(a) * L + b] = nan;
+                    continue;
+                }
+                if (ta == tb && a > b) continue;
+                const int64_t li = acc[0][i][j][q], mi = acc[1][i][j][q], ni = acc[2][i][j][q];
+                double v;
+                if constexpr (KIND == 0) {
+                    const double l = static_cast<double>(li) * inv_s2;
+                    const double m = static_cast<double>(mi) * inv_s2;
+                    const double n = static_cast<double>(ni) * inv_s2;
+                    v = l / (sqrt(m) * sqrt(n));
+                } else {
+                    const double sum = static_cast<double>(mi + ni - 2 * li) * inv_s2;
+                    const double count = static_cast<double>(acc[3][i][j][q]);
+                    v = 1.0 / (sum / count + 1.0);
+                }
+                S[static_cast<int64_t>(a) * L + b] = v;
+                S[static_cast<int64_t>(b) * L + a] = v;
+            }
+}
+
+// ---------------------------------------------------------------------------------------------
+// K5: merge-order float64 kernel (any ratings; Pearson always)
+
+// Per-row mean over ALL of the row's ratings in ID order (sim.go:49-62).
+__global__ void row_mean_kernel(int32_t L, const int64_t* __restrict__ rowptr,
+                                const double* __restrict__ r, double* __restrict__ mean) {
+    const int32_t a = blockIdx.x * blockDim.x + threadIdx.x;
+    if (a >= L) return;
+    double count = 0.0, sum = 0.0;
+    for (int64_t t = rowptr[a]; t < rowptr[a + 1]; ++t) {
+        sum += r[t];
+        count += 1;
+    }
+    mean[a] = sum / count;
+}
+
+template <int KIND>  // 0 Cosine, 1 MSD, 2 Pearson
+__device__ __forceinline__ double pair_sim(const double* __restrict__ dense_a, const uint8_t* __restrict__ has_a,
+                                           double mean_a, int64_t bb, int64_t be,
+                                           const int32_t* __restrict__ ids, const double* __restrict__ r,
+                                           double mean_b) {
+    if constexpr (KIND == 0) {
+        double m = 0.0, n = 0.0, l = 0.0;
+        for (int64_t t = bb; t < be; ++t) {
+            const int32_t id = ids[t];
+            if (has_a[id]) {
+                const double ra = dense_a[id], rb = r[t];
+                m += ra * ra;
+                n += rb * rb;
+                l += ra * rb;
+            }
+        }
+        return l / (sqrt(m) * sqrt(n));
+    } else if constexpr (KIND == 1) {
+        double count = 0.0, sum = 0.0;
+        for (int64_t t = bb; t < be; ++t) {
+            const int32_t id = ids[t];
+            if (has_a[id]) {
+                const double d = dense_a[id] - r[t];
+                sum += d * d;
+                count++;
+            }
+        }
+        return 1.0 / (sum / count + 1.0);
+    } else {
+        double m = 0.0, n = 0.0, l = 0.0;
+        for (int64_t t = bb; t < be; ++t) {
+            const int32_t id = ids[t];
+            if (has_a[id]) {
+                const double ra = dense_a[id] - mean_a;
+                const double rb = r[t] - mean_b;
+                m += ra * ra;
+                n += rb * rb;
+                l += ra * rb;
+            }
+        }
+        return l / (sqrt(m) * sqrt(n));
+    }
+}
+
+// Persistent workgroups walk the left rows a = blockIdx.x, blockIdx.x + gridDim.x, ...; row a lives
+// densely in the workgroup's own global scratch row (R doubles + R flags), written and read only by
+// that workgroup between barriers, then cleared.  One thread per partner b > a.
+template <int KIND>
+__global__ __launch_bounds__(256) void sims_merge_kernel(
+    int32_t L, int32_t R, const int64_t* __restrict__ rowptr, const int32_t* __restrict__ ids,
+    const double* __restrict__ r, const double* __restrict__ mean, double* __restrict__ scratch,
+    uint8_t* __restrict__ scratch_has, double* __restrict__ S) {
+    double* dense = scratch + static_cast<int64_t>(blockIdx.x) * R;
+    uint8_t* has = scratch_has + static_cast<int64_t>(blockIdx.x) * R;
+    for (int32_t a = blockIdx.x; a < L; a += gridDim.x) {
+        for (int64_t t = rowptr[a] + threadIdx.x; t < rowptr[a + 1]; t += blockDim.x) {
+            dense[ids[t]] = r[t];
+            has[ids[t]] = 1;
+        }
+        __syncthreads();
+        const double ma = KIND == 2 ? mean[a] : 0.0;
+        if (threadIdx.x == 0) S[static_cast<int64_t>(a) * L + a] = __builtin_nan("");
+        for (int32_t b = a + 1 + threadIdx.x; b < L; b += blockDim.x) {
+            const double v = pair_sim<KIND>(dense, has, ma, rowptr[b], rowptr[b + 1], ids, r,
+                                            KIND == 2 ? mean[b] : 0.0);
+            S[static_cast<int64_t>(a) * L + b] = v;  // NaN stays NaN (knn.go:286)
+            S[static_cast<int64_t>(b) * L + a] = v;
+        }
+        __syncthreads();
+        for (int64_t t = rowptr[a] + threadIdx.x; t < rowptr[a + 1]; t += blockDim.x) has[ids[t]] = 0;
+        __syncthreads();
+    }
+}
+
+// ---------------------------------------------------------------------------------------------
+// host side
+
+struct SortedRows {
+    std::vector<int64_t> rowptr;
+    std::vector<int32_t> ids;
+    std::vector<double> r;
+};
+
+// data.go:236-243 sorts(): each row ID-ascending (stable, so duplicates keep data order)
+static void sort_rows(int32_t L, const int64_t* rowptr, const int32_t* ids, const double* r,
+                      SortedRows& out) {
+    out.rowptr.assign(rowptr, rowptr + L + 1);
+    const int64_t nnz = rowptr[L] - rowptr[0];
+    out.ids.resize(nnz);
+    out.r.resize(nnz);
+    std::vector<int64_t> idx;
+    for (int32_t a = 0; a < L; ++a) {
+        const int64_t b = rowptr[a], e = rowptr[a + 1];
+        idx.resize(e - b);
+        std::iota(idx.begin(), idx.end(), b);
+        std::stable_sort(idx.begin(), idx.end(), [&](int64_t x, int64_t y) { return ids[x] < ids[y]; });
+        for (int64_t t = b; t < e; ++t) {
+            out.ids[t - rowptr[0]] = ids[idx[t - b]];
+            out.r[t - rowptr[0]] = r[idx[t - b]];
+        }
+    }
+    for (auto& p : out.rowptr) p -= rowptr[0];
+}
+
+// ratings exactly x / s, s in {1, 2}, |x| <= 11, and no repeated id inside a row -> MFMA path
+static int int8_scale(const SortedRows& sr) {
+    for (int s = 1; s <= 2; ++s) {
+        bool ok = true;
+        for (double v : sr.r) {
+            const double x = v * s;
+            if (!(x == std::floor(x)) || std::fabs(x) > 11.0) {
+                ok = false;
+                break;
+            }
+        }
+        if (ok) return s;
+    }
+    return 0;
+}
+
+static bool has_repeats(int32_t L, const SortedRows& sr) {
+    for (int32_t a = 0; a < L; ++a)
+        for (int64_t t = sr.rowptr[a] + 1; t < sr.rowptr[a + 1]; ++t)
+            if (sr.ids[t] == sr.ids[t - 1]) return true;
+    return false;
+}
+
+static void sims_device(rs_ctx* ctx, int32_t kind, int32_t L, int32_t R, const SortedRows& sr,
+                        bool allow_mfma, DevBuf<double>& dS) {
+    hipStream_t s = ctx->stream;
+    const int64_t nnz = static_cast<int64_t>(sr.ids.size());
+    dS.alloc(std::max<int64_t>(1, static_cast<int64_t>(L) * L));
+    if (L == 0) return;
+    const int scale = (kind != RS_SIM_PEARSON && allow_mfma && !has_repeats(L, sr)) ? int8_scale(sr) : 0;
+    DevBuf<int64_t> drow(sr.rowptr.size());
+    DevBuf<int32_t> dids(std::max<int64_t>(1, nnz));
+    drow.upload(sr.rowptr.data(), sr.rowptr.size(), s);
+    dids.upload(sr.ids.data(), nnz, s);
+    if (scale) {
+        const int64_t ldk = ((static_cast<int64_t>(R) + kKBlock - 1) / kKBlock) * kKBlock;
+        const int64_t Lp = ((static_cast<int64_t>(L) + kTile - 1) / kTile) * kTile;
+        std::vector<int8_t> hx(nnz);
+        for (int64_t t = 0; t < nnz; ++t) hx[t] = static_cast<int8_t>(sr.r[t] * scale);
+        DevBuf<int8_t> dx(std::max<int64_t>(1, nnz));
+        dx.upload(hx.data(), nnz, s);
+        DevBuf<int8_t> X(Lp * ldk), X2(Lp * ldk), M(Lp * ldk);
+        RS_HIP(hipMemsetAsync(X.p, 0, X.n, s));
+        RS_HIP(hipMemsetAsync(X2.p, 0, X2.n, s));
+        RS_HIP(hipMemsetAsync(M.p, 0, M.n, s));
+        hipLaunchKernelGGL(knn_scatter_kernel, dim3(L), dim3(256), 0, s, L, drow.p, dids.p, dx.p,
+                           ldk, X.p, X2.p, M.p);
+        RS_HIP(hipGetLastError());
+        const int32_t T = static_cast<int32_t>(Lp / kTile);
+        const int64_t n_tiles = static_cast<int64_t>(T) * (T + 1) / 2;
+        const double inv_s2 = 1.0 / static_cast<double>(scale * scale);
+        if (kind == RS_SIM_COSINE)
+            hipLaunchKernelGGL(knn_sims_mfma_kernel<0>, dim3(n_tiles), dim3(256), 0, s, X.p, X2.p,
+                               M.p, ldk, L, inv_s2, dS.p);
+        else
+            hipLaunchKernelGGL(knn_sims_mfma_kernel<1>, dim3(n_tiles), dim3(256), 0, s, X.p, X2.p,
+                               M.p, ldk, L, inv_s2, dS.p);
+        RS_HIP(hipGetLastError());
+        RS_HIP(hipStreamSynchronize(s));
+        return;
+    }
+    DevBuf<double> dr(std::max<int64_t>(1, nnz)), dmean(L);
+    dr.upload(sr.r.data(), nnz, s);
+    hipLaunchKernelGGL(row_mean_kernel, dim3((L + 255) / 256), dim3(256), 0, s, L, drow.p, dr.p,
+                       dmean.p);
+    const int32_t grid = std::min<int32_t>(L, 2048);
+    DevBuf<double> scratch(static_cast<int64_t>(std::max(1, R)) * grid);
+    DevBuf<uint8_t> scratch_has(static_cast<int64_t>(std::max(1, R)) * grid);
+    RS_HIP(hipMemsetAsync(scratch_has.p, 0, scratch_has.n, s));
+    if (kind == RS_SIM_COSINE)
+        hipLaunchKernelGGL(sims_merge_kernel<0>, dim3(grid), dim3(256), 0, s, L, R, drow.p, dids.p, dr.p, dmean.p, scratch.p, scratch_has.p, dS.p);
+    else if (kind == RS_SIM_MSD)
+        hipLaunchKernelGGL(sims_merge_kernel<1>, dim3(grid), dim3(256), 0, s, L, R, drow.p, dids.p, dr.p, dmean.p, scratch.p, scratch_has.p, dS.p);
+    else
+        hipLaunchKernelGGL(sims_merge_kernel<2>, dim3(grid), dim3(256), 0, s, L, R, drow.p, dids.p, dr.p, dmean.p, scratch.p, scratch_has.p, dS.p);
+    RS_HIP(hipGetLastError());
+    RS_HIP(hipStreamSynchronize(s));
+}
+
+}  // namespace rs
+
+extern "C" int rs_knn_sims(rs_ctx* ctx, int32_t kind, int32_t n_left, int32_t n_right,
+                           const int64_t* rowptr, const int32_t* ids, const double* ratings,
+                           double* sims) {
+    if (!ctx) return rs::set_error(ctx, RS_ERR_INVALID, "ctx is NULL");
+    return rs_guard(ctx, [&]() -> int {
+        if (kind < RS_SIM_COSINE || kind > RS_SIM_PEARSON)
+            return rs::set_error(ctx, RS_ERR_INVALID, "unknown similarity kind");
+        if (n_left < 0 || n_right < 0 || !rowptr || (n_left > 0 && !sims))
+            return rs::set_error(ctx, RS_ERR_INVALID, "bad knn arguments");
+        const int64_t nnz = rowptr[n_left] - rowptr[0];
+        if (nnz > 0 && (!ids || !ratings)) return rs::set_error(ctx, RS_ERR_INVALID, "ids/ratings NULL");
+        for (int32_t a = 0; a < n_left; ++a)
+            if (rowptr[a + 1] < rowptr[a]) return rs::set_error(ctx, RS_ERR_INVALID, "rowptr not monotone");
+        for (int64_t t = rowptr[0]; t < rowptr[n_left]; ++t)
+            if (ids[t] < 0 || ids[t] >= n_right) return rs::set_error(ctx, RS_ERR_INVALID, "id out of range");
+        rs::SortedRows sr;
+        rs::sort_rows(n_left, rowptr, ids, ratings, sr);
+        rs::DevBuf<double> dS;
+        const char* env = std::getenv("RSGPU_KNN_NO_MFMA");
+        rs::sims_device(ctx, kind, n_left, n_right, sr, !(env && env[0] == '1'), dS);
+        dS.download(sims, static_cast<int64_t>(n_left) * n_left, ctx->stream);
+        RS_HIP(hipStreamSynchronize(ctx->stream));
+        return RS_OK;
+    });
+}
+
+extern "C" int rs_sim_pair(rs_ctx* ctx, int32_t kind, int64_t na, const int32_t* a_ids,
+                           const double* a_r, int64_t nb, const int32_t* b_ids, const double* b_r,
+                           double* out) {
+    if (!ctx) return rs::set_error(ctx, RS_ERR_INVALID, "ctx is NULL");
+    return rs_guard(ctx, [&]() -> int {
+        if (!out || na < 0 || nb < 0 || (na && (!a_ids || !a_r)) || (nb && (!b_ids || !b_r)))
+            return rs::set_error(ctx, RS_ERR_INVALID, "bad sim_pair arguments");
+        // a two-row KNN problem on the merge kernel: S[0][1] = sim(a, b)
+        int32_t R = 1;
+        for (int64_t t = 0; t < na; ++t) R = std::max(R, a_ids[t] + 1);
+        for (int64_t t = 0; t < nb; ++t) R = std::max(R, b_ids[t] + 1);
+        std::vector<int64_t> rowptr = {0, na, na + nb};
+        std::vector<int32_t> ids(a_ids, a_ids + na);
+        ids.insert(ids.end(), b_ids, b_ids + nb);
+        std::vector<double> r(a_r, a_r + na);
+        r.insert(r.end(), b_r, b_r + nb);
+        for (int32_t t : ids)
+            if (t < 0) return rs::set_error(ctx, RS_ERR_INVALID, "negative id");
+        rs::SortedRows sr;
+        sr.rowptr = rowptr;
+        sr.ids = ids;
+        sr.r = r;  // inputs are ID-ascending already (SortedIdRatings)
+        rs::DevBuf<double> dS;
+        rs::sims_device(ctx, kind, 2, R, sr, false, dS);
+        double S[4];
+        dS.download(S, 4, ctx->stream);
+        RS_HIP(hipStreamSynchronize(ctx->stream));
+        *out = S[1];
+        return RS_OK;
+    });
+}

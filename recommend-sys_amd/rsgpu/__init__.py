@@ -178,6 +178,28 @@ class Context:
                                     _ptr(bu), _ptr(bi), _ptr(g)))
         return P, Q, bu, bi, float(g[0])
 
+    def knn_sims(self, kind, rowptr, ids, ratings, n_right):
+        """core/knn.go:224-298 pair loop -> dense L x L float64 Sims (NaN = no co-rating)."""
+        rowptr = np.ascontiguousarray(rowptr, dtype=np.int64)
+        ids = np.ascontiguousarray(ids, dtype=np.int32)
+        ratings = np.ascontiguousarray(ratings, dtype=np.float64)
+        L = len(rowptr) - 1
+        out = np.empty((L, L))
+        self.check(lib().rs_knn_sims(self.h, kind, L, n_right, _ptr(rowptr), _ptr(ids),
+                                     _ptr(ratings), _ptr(out)))
+        return out
+
+    def sim_pair(self, kind, a_ids, a_r, b_ids, b_r):
+        """core/sim.go Cosine / MSD / Pearson of two ID-ascending lists, on the device."""
+        a_ids = np.ascontiguousarray(a_ids, dtype=np.int32)
+        b_ids = np.ascontiguousarray(b_ids, dtype=np.int32)
+        a_r = np.ascontiguousarray(a_r, dtype=np.float64)
+        b_r = np.ascontiguousarray(b_r, dtype=np.float64)
+        out = np.empty(1)
+        self.check(lib().rs_sim_pair(self.h, kind, len(a_ids), _ptr(a_ids), _ptr(a_r),
+                                     len(b_ids), _ptr(b_ids), _ptr(b_r), _ptr(out)))
+        return float(out[0])
+
     def svd_plan(self, r: Ratings, n_factors: int) -> "SvdPlan":
         return SvdPlan(self, r, n_factors)
 

@@ -1,0 +1,124 @@
+"""GPU parity tests of K4 (int8-MFMA Cosine/MSD) and K5 (merge-order Pearson) through the C-ABI.
+
+P3: Sims bitwise equal to the oracle's restatement of core/knn.go:224-298 + core/sim.go (NaN
+pattern included), and therefore identical top-K neighbour lists under (sim desc, index asc).
+"""
+import json
+import math
+import os
+
+import numpy as np
+import pytest
+
+import oracle as O
+import rsgpu
+
+pytestmark = pytest.mark.gpu
+HERE = os.path.dirname(os.path.abspath(__file__))
+KINDS = {"Cosine": rsgpu.SIM_COSINE, "MSD": rsgpu.SIM_MSD, "Pearson": rsgpu.SIM_PEARSON}
+
+
+def bitwise_equal(a, b):
+    a, b = np.asarray(a), np.asarray(b)
+    return a.shape == b.shape and np.array_equal(a.view(np.uint64), b.view(np.uint64)) or \
+        (np.array_equal(np.isnan(a), np.isnan(b)) and np.array_equal(a[~np.isnan(a)], b[~np.isnan(b)]))
+
+
+def topk(S, k=40):
+    out = []
+    for row in S:
+        idx = np.nonzero(~np.isnan(row))[0]
+        order = np.lexsort((idx, -row[idx]))
+        out.append(idx[order][:k])
+    return out
+
+
+def test_sim_pair_known_answers(ctx):
+    """core/sim_test.go:10-59 on the device: the exact values, bit for bit."""
+    kat = json.load(open(os.path.join(HERE, "golden", "sim_kat.json")))
+    a, b = kat["a"], kat["b"]
+    for case in kat["cases"]:
+        v = ctx.sim_pair(KINDS[case["sim"]], a["ids"], a["ratings"], b["ids"], b["ratings"])
+        assert v == case["exact"], (case["sim"], v)
+        assert abs(v - case["expect"]) <= kat["epsilon"]
+    assert math.isnan(ctx.sim_pair(rsgpu.SIM_COSINE, [1], [2.0], [2], [3.0]))
+
+
+@pytest.fixture(scope="module")
+def ml100k_lists(ml100k):
+    U, I, R = ml100k
+    iu, ii, nu, ni = O.trainset_ids(U, I)
+    return iu, ii, R, nu, ni
+
+
+@pytest.mark.parametrize("user_based", [False, True])
+@pytest.mark.parametrize("kind", [rsgpu.SIM_COSINE, rsgpu.SIM_MSD, rsgpu.SIM_PEARSON])
+def test_knn_sims_ml100k_bitwise(ctx, ml100k_lists, kind, user_based):
+    """Full ML-100K (item- and user-based): every Sims entry bitwise equal, NaN pattern too."""
+    iu, ii, R, nu, ni = ml100k_lists
+    left, right, nl, nr = (iu, ii, nu, ni) if user_based else (ii, iu, ni, nu)
+    rowptr, ids, rr = O.csr_by(left, nl, right, R)
+    ref = O.knn_sims(kind, rowptr, ids, rr)
+    got = ctx.knn_sims(kind, rowptr, ids, rr, nr)
+    assert np.array_equal(np.isnan(ref), np.isnan(got))
+    m = ~np.isnan(ref)
+    assert np.array_equal(ref[m].view(np.uint64), got[m].view(np.uint64))
+    for x, y in zip(topk(ref)[:200], topk(got)[:200]):
+        assert np.array_equal(x, y)
+
+
+def test_knn_merge_path_matches_mfma(ctx, ml100k_lists, monkeypatch):
+    iu, ii, R, nu, ni = ml100k_lists
+    rowptr, ids, rr = O.csr_by(ii, ni, iu, R)
+    a = ctx.knn_sims(rsgpu.SIM_MSD, rowptr, ids, rr, nu)
+    monkeypatch.setenv("RSGPU_KNN_NO_MFMA", "1")
+    b = ctx.knn_sims(rsgpu.SIM_MSD, rowptr, ids, rr, nu)
+    assert np.array_equal(np.isnan(a), np.isnan(b))
+    m = ~np.isnan(a)
+    assert np.array_equal(a[m].view(np.uint64), b[m].view(np.uint64))
+
+
+def _random_lists(L, Rn, density, values, seed):
+    rng = np.random.default_rng(seed)
+    mask = rng.random((L, Rn)) < density
+    rows, cols = np.nonzero(mask)
+    perm = rng.permutation(len(rows))  # data order inside a row is arbitrary (sorts() fixes it)
+    rows, cols = rows[perm], cols[perm]
+    r = rng.choice(values, len(rows))
+    return O.csr_by(rows, L, cols, r)
+
+
+@pytest.mark.parametrize("kind", [rsgpu.SIM_COSINE, rsgpu.SIM_MSD, rsgpu.SIM_PEARSON])
+@pytest.mark.parametrize("L,Rn,values", [
+    (300, 1000, np.arange(1, 11) / 2.0),          # half stars (ML-20M): scale 2 on the MFMA path
+    (129, 70, np.arange(0, 6, dtype=float)),       # zero ratings: rated but x = 0 (M carries them)
+    (1, 5, np.array([3.0])),                        # single row: only the NaN diagonal
+    (257, 300, np.array([1.3, 2.7, 4.1])),          # not x/s representable: merge path
+    (200, 64, np.arange(-5, 6, dtype=float)),       # negative ratings, |x| <= 11
+])
+def test_knn_sims_random_bitwise(ctx, kind, L, Rn, values):
+    rowptr, ids, rr = _random_lists(L, Rn, 0.05, values, seed=L + Rn)
+    ref = O.knn_sims(kind, rowptr, ids, rr)
+    got = ctx.knn_sims(kind, rowptr, ids, rr, Rn)
+    assert np.array_equal(np.isnan(ref), np.isnan(got))
+    m = ~np.isnan(ref)
+    assert np.array_equal(ref[m].view(np.uint64), got[m].view(np.uint64))
+
+
+def test_knn_empty_rows(ctx):
+    rowptr = np.array([0, 0, 2, 2, 3], np.int64)
+    ids = np.array([1, 0, 1], np.int32)
+    rr = np.array([4.0, 5.0, 3.0])
+    for kind in KINDS.values():
+        ref = O.knn_sims(kind, rowptr, ids, rr)
+        got = ctx.knn_sims(kind, rowptr, ids, rr, 2)
+        assert np.array_equal(np.isnan(ref), np.isnan(got))
+        m = ~np.isnan(ref)
+        assert np.array_equal(ref[m], got[m])
+
+
+def test_knn_bad_arguments(ctx):
+    with pytest.raises(rsgpu.RsError):
+        ctx.knn_sims(7, [0, 1], [0], [1.0], 1)
+    with pytest.raises(rsgpu.RsError):
+        ctx.knn_sims(rsgpu.SIM_COSINE, [0, 1], [5], [1.0], 2)
