@@ -178,6 +178,15 @@ class Context:
                                     _ptr(bu), _ptr(bi), _ptr(g)))
         return P, Q, bu, bi, float(g[0])
 
+    def nmf_fit(self, r: Ratings, P, Q, n_epochs=50, reg=0.06, as_written=True):
+        """core/svd.go:158-251 (as_written reproduces svd.go:243-249, Q5)."""
+        P = np.array(P, dtype=np.float64, order="C")
+        Q = np.array(Q, dtype=np.float64, order="C")
+        rc = r.c()
+        self.check(lib().rs_nmf_fit(self.h, C.byref(rc), P.shape[1], n_epochs, reg,
+                                    int(as_written), _ptr(P), _ptr(Q)))
+        return P, Q
+
     def knn_sims(self, kind, rowptr, ids, ratings, n_right):
         """core/knn.go:224-298 pair loop -> dense L x L float64 Sims (NaN = no co-rating)."""
         rowptr = np.ascontiguousarray(rowptr, dtype=np.int64)
