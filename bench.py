@@ -95,7 +95,8 @@ def main():
     rng = np.random.default_rng(1)
     P0 = rng.normal(0, 0.1, (n_users, K))  # identical on every rank (replicated user factors)
     Q0 = np.random.default_rng(100 + rank).normal(0, 0.1, (n_items, K))
-    plan.upload(P0, Q0, np.zeros(n_users), np.zeros(n_items), 0.0)
+    # GlobalBias warm start of the FAST schedule (rs_svd_fit does the same, common.hpp)
+    plan.upload(P0, Q0, np.zeros(n_users), np.zeros(n_items), float(np.mean(r)))
     stream = torch.cuda.current_stream(dev).cuda_stream
 
     if world > 1:

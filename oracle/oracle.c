@@ -649,3 +649,37 @@ void or_svd_fit_chunked(int32_t n_users, const int64_t* rowptr, const int32_t* i
     free(lbu0);
     free(lgb);
 }
+
+void or_svdpp_fit_userwise(int32_t n_users, const int64_t* rowptr, const int32_t* items,
+                           const double* r, int32_t k, int32_t epochs, double lr, double reg,
+                           double* P, double* Q, double* Y, double* bu, double* bi, double* gb) {
+    const int64_t nnz = rowptr[n_users];
+    int32_t* uu = (int32_t*)malloc((size_t)(nnz > 0 ? nnz : 1) * sizeof(int32_t));
+    for (int32_t x = 0; x < n_users; x++)
+        for (int64_t t = rowptr[x]; t < rowptr[x + 1]; t++) uu[t] = x;
+    double GB = *gb;
+    for (int32_t epoch = 0; epoch < epochs; epoch++) {
+        double gsum = 0.0;
+        for (int32_t x = 0; x < n_users; x++) {
+            const int64_t b = rowptr[x], e = rowptr[x + 1];
+            if (e == b) continue;
+            /* the user's row as its own train set: N(x) = the row, in row order */
+            double g = GB;
+            or_svdpp_fit(e - b, uu + b, items + b, r + b, x + 1, k, 1, lr, reg, P, Q, Y, bu, bi, &g);
+            gsum += (double)(e - b) * (g - GB);
+        }
+        if (nnz > 0) GB += gsum / (double)nnz;
+    }
+    *gb = GB;
+    free(uu);
+}
+
+double or_gb_warm_start(int32_t n_users, const int64_t* rowptr, const int32_t* items,
+                        const double* r, const double* bu, const double* bi) {
+    const int64_t nnz = rowptr[n_users];
+    if (nnz <= 0) return 0.0;
+    double s = 0.0;
+    for (int32_t x = 0; x < n_users; x++)
+        for (int64_t t = rowptr[x]; t < rowptr[x + 1]; t++) s += r[t] - bu[x] - bi[items[t]];
+    return s / (double)nnz;
+}

@@ -61,9 +61,14 @@ def lib():
                                      _i32p, _i32p, _f64p]
         L.or_baseline_fit.argtypes = [C.c_int64, _i32p, _i32p, _f64p, C.c_int32, C.c_double,
                                       C.c_double, _f64p, _f64p, _dp]
+        L.or_svdpp_fit_userwise.argtypes = [C.c_int32, _i64p, _i32p, _f64p, C.c_int32, C.c_int32,
+                                            C.c_double, C.c_double, _f64p, _f64p, _f64p, _f64p,
+                                            _f64p, _dp]
         L.or_svd_fit_chunked.argtypes = [C.c_int32, _i64p, _i32p, _f64p, C.c_int32, C.c_int32,
                                          C.c_int32, C.c_double, C.c_double, _f64p, _f64p, _f64p,
                                          _f64p, _dp]
+        L.or_gb_warm_start.argtypes = [C.c_int32, _i64p, _i32p, _f64p, _f64p, _f64p]
+        L.or_gb_warm_start.restype = C.c_double
         _lib = L
     return _lib
 
@@ -143,11 +148,19 @@ def svd_predict(u, i, P, Q, bu, bi, gb):
     return out
 
 
+def gb_warm_start(rowptr, items, r, bu, bi):
+    return lib().or_gb_warm_start(len(rowptr) - 1, _i64(rowptr), _i32(items), _f64(r), _f64(bu),
+                                  _f64(bi))
+
+
 def svd_fit_chunked(rowptr, items, r, P, Q, chunk, bu=None, bi=None, gb=0.0, epochs=20,
-                    lr=0.005, reg=0.02):
+                    lr=0.005, reg=0.02, warm=True):
+    """Restatement of the GPU FAST SVD schedule (with its GlobalBias warm start when warm)."""
     P, Q = _f64(P).copy(), _f64(Q).copy()
     bu = np.zeros(P.shape[0]) if bu is None else _f64(bu).copy()
     bi = np.zeros(Q.shape[0]) if bi is None else _f64(bi).copy()
+    if warm and epochs > 0:
+        gb = gb_warm_start(rowptr, items, r, bu, bi)
     g = C.c_double(gb)
     lib().or_svd_fit_chunked(P.shape[0], _i64(rowptr), _i32(items), _f64(r), chunk, P.shape[1],
                              epochs, lr, reg, P, Q, bu, bi, C.byref(g))
@@ -160,6 +173,16 @@ def svdpp_fit(u, i, r, n_users, P, Q, Y, epochs=20, lr=0.007, reg=0.02):
     g = C.c_double(0.0)
     lib().or_svdpp_fit(len(r), _i32(u), _i32(i), _f64(r), n_users, P.shape[1], epochs, lr, reg,
                        P, Q, Y, bu, bi, C.byref(g))
+    return P, Q, Y, bu, bi, g.value
+
+
+def svdpp_fit_userwise(rowptr, items, r, P, Q, Y, epochs=20, lr=0.007, reg=0.02, warm=True):
+    """Restatement of the GPU FAST SVD++ schedule (with its GlobalBias warm start when warm)."""
+    P, Q, Y = _f64(P).copy(), _f64(Q).copy(), _f64(Y).copy()
+    bu, bi = np.zeros(P.shape[0]), np.zeros(Q.shape[0])
+    g = C.c_double(gb_warm_start(rowptr, items, r, bu, bi) if warm and epochs > 0 else 0.0)
+    lib().or_svdpp_fit_userwise(P.shape[0], _i64(rowptr), _i32(items), _f64(r), P.shape[1], epochs,
+                                lr, reg, P, Q, Y, bu, bi, C.byref(g))
     return P, Q, Y, bu, bi, g.value
 
 

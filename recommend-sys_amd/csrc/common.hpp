@@ -83,6 +83,12 @@ struct UserCSR {
 void build_csr(int64_t nnz, int32_t n_rows, const int32_t* rows, const int32_t* cols,
                const double* vals, UserCSR& out);
 
+// FAST-mode GlobalBias warm start: the least-squares bias given the current b_u, b_i (factors
+// ignored), i.e. mean(r - b_u - b_i).  The sequential reference reaches this value within its first
+// ~1/lr updates (svd.go:105-106); the FAST schedule folds GlobalBias only between epochs, so it starts
+// there instead of at 0 (measured: SVD++ ML-100K RMSE 1.126 without, 0.920 with; reference 0.920).
+double gb_warm_start(const rs_ratings* r, const double* bu, const double* bi);
+
 // Validates a rs_ratings block; returns RS_OK or an error (message set on ctx).
 int check_ratings(rs_ctx* ctx, const rs_ratings* r);
 

@@ -38,7 +38,7 @@ template <int E, int D, bool UPONLY>
 __global__ __launch_bounds__(256) void nmf_pass_kernel(
     int32_t n_rows, const int64_t* __restrict__ rowptr, const int32_t* __restrict__ cols,
     const float* __restrict__ vals, const float* __restrict__ own,
-    const float* __restrict__ partner, float* __restrict__ out, float reg) {
+    const float* __restrict__ partner, float* __restrict__ out, int32_t k, float reg) {
 #pragma clang fp contract(off)
     constexpr int LD = 64 * E, B = 16;
     const int lane = threadIdx.x & 63;
@@ -97,7 +97,7 @@ __global__ __launch_bounds__(256) void nmf_pass_kernel(
         // svd.go:236-241 (users, items intended): buffer = up / down; p *= buffer
         // svd.go:243-249 (items as written, Q5):   q *= up (the undivided copy)
         const float buffer = UPONLY ? up[x] : up[x] / down[x];
-        w[lane + 64 * x] = p[x] * buffer;
+        w[lane + 64 * x] = lane + 64 * x < k ? p[x] * buffer : 0.f;  // padding stays 0 (0/0)
     }
 }
 
@@ -105,17 +105,17 @@ template <int E, int D>
 static void nmf_epoch_t(int32_t n_users, int32_t n_items, const DevBuf<int64_t>& urow,
                         const DevBuf<int32_t>& ucol, const DevBuf<float>& uval,
                         const DevBuf<int64_t>& irow, const DevBuf<int32_t>& icol,
-                        const DevBuf<float>& ival, float* P, float*& Q, float*& Qn, float reg,
-                        bool as_written, hipStream_t s) {
+                        const DevBuf<float>& ival, float* P, float*& Q, float*& Qn, int32_t k,
+                        float reg, bool as_written, hipStream_t s) {
     const dim3 gi((n_items + 3) / 4), gu((n_users + 3) / 4);
     if (n_items > 0) {
         if (as_written)
-            hipLaunchKernelGGL((nmf_pass_kernel<E, D, true>), gi, dim3(256), 0, s, n_items, irow.p, icol.p, ival.p, Q, P, Qn, reg);
+            hipLaunchKernelGGL((nmf_pass_kernel<E, D, true>), gi, dim3(256), 0, s, n_items, irow.p, icol.p, ival.p, Q, P, Qn, k, reg);
         else
-            hipLaunchKernelGGL((nmf_pass_kernel<E, D, false>), gi, dim3(256), 0, s, n_items, irow.p, icol.p, ival.p, Q, P, Qn, reg);
+            hipLaunchKernelGGL((nmf_pass_kernel<E, D, false>), gi, dim3(256), 0, s, n_items, irow.p, icol.p, ival.p, Q, P, Qn, k, reg);
     }
     if (n_users > 0)
-        hipLaunchKernelGGL((nmf_pass_kernel<E, D, false>), gu, dim3(256), 0, s, n_users, urow.p, ucol.p, uval.p, P, Q, P, reg);
+        hipLaunchKernelGGL((nmf_pass_kernel<E, D, false>), gu, dim3(256), 0, s, n_users, urow.p, ucol.p, uval.p, P, Q, P, k, reg);
     RS_HIP(hipGetLastError());
     std::swap(Q, Qn);
 }
@@ -161,10 +161,10 @@ extern "C" int rs_nmf_fit(rs_ctx* ctx, const rs_ratings* r, int32_t n_factors, i
         const float fr = static_cast<float>(reg);
         for (int32_t ep = 0; ep < n_epochs; ++ep) {
             switch (E) {
-                case 1: rs::nmf_epoch_t<1, 8>(r->n_users, r->n_items, urow, ucol, uval, irow, icol, ival, dP.p, q, qn, fr, as_written != 0, s); break;
-                case 2: rs::nmf_epoch_t<2, 8>(r->n_users, r->n_items, urow, ucol, uval, irow, icol, ival, dP.p, q, qn, fr, as_written != 0, s); break;
-                case 4: rs::nmf_epoch_t<4, 8>(r->n_users, r->n_items, urow, ucol, uval, irow, icol, ival, dP.p, q, qn, fr, as_written != 0, s); break;
-                default: rs::nmf_epoch_t<8, 4>(r->n_users, r->n_items, urow, ucol, uval, irow, icol, ival, dP.p, q, qn, fr, as_written != 0, s); break;
+                case 1: rs::nmf_epoch_t<1, 8>(r->n_users, r->n_items, urow, ucol, uval, irow, icol, ival, dP.p, q, qn, k, fr, as_written != 0, s); break;
+                case 2: rs::nmf_epoch_t<2, 8>(r->n_users, r->n_items, urow, ucol, uval, irow, icol, ival, dP.p, q, qn, k, fr, as_written != 0, s); break;
+                case 4: rs::nmf_epoch_t<4, 8>(r->n_users, r->n_items, urow, ucol, uval, irow, icol, ival, dP.p, q, qn, k, fr, as_written != 0, s); break;
+                default: rs::nmf_epoch_t<8, 4>(r->n_users, r->n_items, urow, ucol, uval, irow, icol, ival, dP.p, q, qn, k, fr, as_written != 0, s); break;
             }
         }
         dP.download(hP.data(), hP.size(), s);

@@ -46,6 +46,13 @@ void build_csr(int64_t nnz, int32_t n_rows, const int32_t* rows, const int32_t* 
     }
 }
 
+double gb_warm_start(const rs_ratings* r, const double* bu, const double* bi) {
+    if (r->nnz <= 0) return 0.0;
+    double s = 0.0;
+    for (int64_t t = 0; t < r->nnz; ++t) s += r->ratings[t] - bu[r->users[t]] - bi[r->items[t]];
+    return s / static_cast<double>(r->nnz);
+}
+
 int check_ratings(rs_ctx* ctx, const rs_ratings* r) {
     if (!r) return set_error(ctx, RS_ERR_INVALID, "ratings is NULL");
     if (r->nnz < 0 || r->n_users < 0 || r->n_items < 0)

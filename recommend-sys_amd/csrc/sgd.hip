@@ -619,6 +619,7 @@ extern "C" int rs_svd_fit(rs_ctx* ctx, const rs_ratings* r, const rs_sgd_params*
             rs_svd_plan pl;
             rs::plan_build(ctx, r, p->n_factors, &pl);
             pl.write_back = p->write_back == RS_SGD_WB_STORE ? RS_SGD_WB_STORE : RS_SGD_WB_ATOMIC;
+            if (p->n_epochs > 0) *gb = rs::gb_warm_start(r, bu, bi);
             rs::plan_upload(&pl, P, Q, bu, bi, gb);
             rs::plan_epochs(&pl, p->n_epochs, lr, reg, ctx->stream);
             rs::plan_download(&pl, P, Q, bu, bi, gb);

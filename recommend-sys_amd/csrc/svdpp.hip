@@ -1,0 +1,434 @@
+// svdpp.hip -- K2: SVD++ epoch (reference core/svd.go:259-427), gfx950.
+//
+// ORDERED  one workgroup walks the ratings in train-set order with the literal per-rating work of
+//          the reference: e = (sum_{j in N(u)} y_j) / sqrt|N(u)| recomputed for every rating
+//          (svd.go:271-282, called from 363), then b, p_u, q_i and every y_j of N(u) updated
+//          (svd.go:366-422).  Thread f owns factor column f of every row, so the only cross-thread
+//          step per rating is the prediction's dot product.  Parity target (SVD++ is unpinned by
+//          the reference: core/base_test.go:38-40 is commented out) = the fp64 restatement.
+// FAST     user-CSR, one wave per user, heaviest first.  Within a user row the y-update is the same
+//          affine map for every j in N(u) (y <- a y - (lr diff / sqrt n) q_new, a = 1 - lr reg), so
+//          the wave keeps S0 = sum y_j, the scale A and the offset vector C in registers,
+//              e = (A S0 - n C) / sqrt n,
+//          and applies y_j += (A - 1) y_j - C once per (u, j) at the end of the row (SURVEY §8a
+//          A8: equal to the literal update in user-major order).  q_i and y_j deltas go to the
+//          memory side as float atomics (cross-XCD coherent, no lost updates), like K1.
+//
+// FAST device layout: P, Q, Y are (rows x ld) float32, ld = 64 ceil((k + 1) / 64); the bias (b_u in
+// P, b_i in Q) sits in column ld - 1, Y's column ld - 1 stays 0.
+// Algorithmic bytes per epoch: nnz*(16 + 8k) + U*(16 + 8k) + nnz*(4 + 12k).
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <vector>
+
+#include "common.hpp"
+#include "wave.hpp"
+
+namespace rs {
+
+constexpr int32_t kPPOut = 0x7FFFFFF0;
+constexpr int kPPAux = 16;  // sc1
+
+__device__ __forceinline__ float pp_wave_sum(float x) {
+    x = group_sum<16>(x);
+    auto r16 = __builtin_amdgcn_permlane16_swap(__float_as_uint(x), __float_as_uint(x), false, false);
+    x = __uint_as_float(r16[0]) + __uint_as_float(r16[1]);
+    auto r32 = __builtin_amdgcn_permlane32_swap(__float_as_uint(x), __float_as_uint(x), false, false);
+    return __uint_as_float(r32[0]) + __uint_as_float(r32[1]);
+}
+
+__device__ __forceinline__ float pp_lane63(float x) {
+    return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(x), 63));
+}
+
+// ---------------------------------------------------------------------------------------------
+// FAST (lazy y) epoch kernel
+
+template <int E, int D>
+__global__ __launch_bounds__(256) void svdpp_epoch_fast_kernel(
+    const int32_t* __restrict__ work, int32_t n_work, const int64_t* __restrict__ rowptr,
+    const int32_t* __restrict__ items, const float* __restrict__ ratings, float* __restrict__ P,
+    float* Q, float* Y, int32_t row_bytes_q, int32_t row_bytes_y, const double* __restrict__ gb_in,
+    double* __restrict__ gb_partial, float lr, float reg) {
+#pragma clang fp contract(fast)
+    constexpr int LD = 64 * E, B = 16;
+    __shared__ double s_contrib[4];
+    const int lane = threadIdx.x & 63;
+    const int wib = threadIdx.x >> 6;
+    const int w = __builtin_amdgcn_readfirstlane(static_cast<int>(blockIdx.x) * 4 + wib);
+    const float gb0 = static_cast<float>(gb_in[0]);
+    const __amdgpu_buffer_rsrc_t rq = __builtin_amdgcn_make_buffer_rsrc(Q, 0, row_bytes_q, 0x00020000);
+    const __amdgpu_buffer_rsrc_t ry = __builtin_amdgcn_make_buffer_rsrc(Y, 0, row_bytes_y, 0x00020000);
+    const int32_t lane4 = lane * 4;
+    const bool bias_lane = lane == 63;
+    const float a = 1.f - lr * reg;
+    double contrib = 0.0;
+
+    if (w < n_work) {
+        const int32_t u = work[w];
+        const int64_t b = rowptr[u], e = rowptr[u + 1];
+        const int32_t deg = static_cast<int32_t>(e - b);
+        const float nf = static_cast<float>(deg);
+        const float sq = sqrtf(nf);
+        float p[E];
+        float* prow = P + static_cast<int64_t>(u) * LD;
+#pragma unroll
+        for (int x = 0; x < E; ++x) p[x] = prow[lane + 64 * x];
+        float ub = pp_lane63(p[E - 1]);
+        float gb = gb0;
+        auto load_rowq = [&](__amdgpu_buffer_rsrc_t rs_, float (&q)[E], int32_t valid, int32_t item) {
+            const int32_t row = valid ? item * (LD * 4) : kPPOut;
+#pragma unroll
+            for (int x = 0; x < E; ++x)
+                q[x] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rs_, row + lane4 + 256 * x, 0, kPPAux));
+        };
+
+        // pass 1: S0 = sum_{j in N(u)} y_j   (svd.go:276-278)
+        float S0[E];
+#pragma unroll
+        for (int x = 0; x < E; ++x) S0[x] = 0.f;
+        for (int64_t base = b; base < e; base += 8) {
+            const int32_t rem = static_cast<int32_t>(e - base);
+            float yv[8][E];
+#pragma unroll
+            for (int j = 0; j < 8; ++j) load_rowq(ry, yv[j], j < rem, items[base + j]);
+#pragma unroll
+            for (int j = 0; j < 8; ++j)
+#pragma unroll
+                for (int x = 0; x < E; ++x) S0[x] += yv[j][x];
+        }
+        float A = 1.f;
+        float Cv[E];
+#pragma unroll
+        for (int x = 0; x < E; ++x) Cv[x] = 0.f;
+
+        // pass 2: the ratings of u in data order
+        int32_t it_cur[B], it_nxt[B];
+#pragma unroll
+        for (int j = 0; j < B; ++j) it_cur[j] = items[b + j];
+#pragma unroll
+        for (int j = 0; j < B; ++j) it_nxt[j] = items[b + B + j];
+        float ring[D][E];
+#pragma unroll
+        for (int s = 0; s < D; ++s) load_rowq(rq, ring[s], s < deg, it_cur[s]);
+        for (int64_t base = b; base < e; base += B) {
+            const int32_t rem = static_cast<int32_t>(e - base);
+            float rt[B];
+#pragma unroll
+            for (int j = 0; j < B; ++j) rt[j] = ratings[base + j];
+#pragma unroll
+            for (int j = 0; j < B; ++j) {
+                constexpr int kD = D;
+                const int slot = j % kD;
+                if (j < rem) {
+                    float* q = ring[slot];
+                    const float bq = pp_lane63(q[E - 1]);
+                    float ev[E];
+                    float s = 0.f;
+#pragma unroll
+                    for (int x = 0; x < E; ++x) {
+                        ev[x] = (A * S0[x] - nf * Cv[x]) / sq;            // svd.go:271-282
+                        const float qx = (x == E - 1 && bias_lane) ? 0.f : q[x];
+                        s += (p[x] + ev[x]) * qx;                         // svd.go:302-305
+                    }
+                    s = pp_wave_sum(s);
+                    const float diff = ((gb + ub) + bq) + s - rt[j];      // svd.go:363-364
+                    const float c = lr * diff;
+                    gb -= c;                                              // svd.go:366-367
+                    ub = __builtin_fmaf(ub, a, -c);                       // svd.go:370-371
+                    const float bq_new = __builtin_fmaf(bq, a, -c);       // svd.go:374-375
+                    const float cy = c / sq;                              // svd.go:410-412
+                    A *= a;                                               // svd.go:413-417 (lazy)
+#pragma unroll
+                    for (int x = 0; x < E; ++x) {
+                        const float pn = __builtin_fmaf(-c, q[x], p[x] * a);           // 378-384
+                        const float qn = __builtin_fmaf(-c, pn + ev[x], q[x] * a);     // 387-396
+                        const bool bx = x == E - 1 && bias_lane;
+                        p[x] = bx ? ub : pn;
+                        const float qw = bx ? bq_new : qn;
+                        Cv[x] = bx ? 0.f : __builtin_fmaf(cy, qn, Cv[x] * a);
+                        __builtin_amdgcn_raw_ptr_buffer_atomic_fadd_f32(
+                            qw - q[x], rq, it_cur[j] * (LD * 4) + lane4 + 256 * x, 0, 0);
+                    }
+                }
+                const int jn = j + D;
+                load_rowq(rq, ring[slot], jn < rem, jn < B ? it_cur[jn % B] : it_nxt[jn % B]);
+            }
+#pragma unroll
+            for (int j = 0; j < B; ++j) it_cur[j] = it_nxt[j];
+#pragma unroll
+            for (int j = 0; j < B; ++j) it_nxt[j] = items[base + 2 * B + j];
+        }
+
+        // pass 3: y_j += (A - 1) y_j - C for every j in N(u) (the deferred svd.go:399-422)
+        const float am1 = A - 1.f;
+        for (int64_t base = b; base < e; base += 8) {
+            const int32_t rem = static_cast<int32_t>(e - base);
+            float yv[8][E];
+#pragma unroll
+            for (int j = 0; j < 8; ++j) load_rowq(ry, yv[j], j < rem, items[base + j]);
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+                const int32_t row = j < rem ? items[base + j] * (LD * 4) : kPPOut;
+#pragma unroll
+                for (int x = 0; x < E; ++x)
+                    __builtin_amdgcn_raw_ptr_buffer_atomic_fadd_f32(__builtin_fmaf(am1, yv[j][x], -Cv[x]), ry,
+                                                                   row + lane4 + 256 * x, 0, 0);
+            }
+        }
+#pragma unroll
+        for (int x = 0; x < E; ++x) prow[lane + 64 * x] = p[x];
+        contrib = static_cast<double>(deg) * (static_cast<double>(gb) - static_cast<double>(gb0));
+    }
+    if (lane == 0) s_contrib[wib] = contrib;
+    __syncthreads();
+    if (threadIdx.x == 0)
+        gb_partial[blockIdx.x] = ((s_contrib[0] + s_contrib[1]) + s_contrib[2]) + s_contrib[3];
+}
+
+__global__ __launch_bounds__(256) void pp_gb_fold_kernel(const double* __restrict__ partial,
+                                                         int64_t n, double* __restrict__ gb,
+                                                         double inv_nnz) {
+    __shared__ double s[256];
+    double t = 0.0;
+    for (int64_t x = threadIdx.x; x < n; x += 256) t += partial[x];
+    s[threadIdx.x] = t;
+    __syncthreads();
+    for (int w = 128; w > 0; w >>= 1) {
+        if (static_cast<int>(threadIdx.x) < w) s[threadIdx.x] += s[threadIdx.x + w];
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) gb[0] += s[0] * inv_nnz;
+}
+
+// ---------------------------------------------------------------------------------------------
+// ORDERED (literal) kernel: one workgroup of NT threads, thread f = factor column f (k <= NT).
+
+template <int NT>
+__global__ __launch_bounds__(NT) void svdpp_ordered_kernel(
+    int64_t nnz, const int32_t* __restrict__ users, const int32_t* __restrict__ items,
+    const float* __restrict__ ratings, const int64_t* __restrict__ nrow,
+    const int32_t* __restrict__ ncol, float* P, float* Q, float* Y, float* bu, float* bi,
+    int32_t k, double* gb_io, int32_t epochs, float lr, float reg) {
+#pragma clang fp contract(off)
+    __shared__ float red[NT / 64];
+    const int f = threadIdx.x;
+    const bool act = f < k;
+    const double lrd = lr, regd = reg;
+    double gb = gb_io[0];
+    for (int32_t epoch = 0; epoch < epochs; ++epoch) {       // svd.go:350
+        for (int64_t n = 0; n < nnz; ++n) {                   // svd.go:352
+            const int32_t u = users[n], i = items[n];
+            const float r = ratings[n];
+            const int64_t jb = nrow[u], je = nrow[u + 1];
+            const float ub = bu[u], ib = bi[i];               // svd.go:358-359
+            float p = act ? P[static_cast<int64_t>(u) * k + f] : 0.f;
+            float q = act ? Q[static_cast<int64_t>(i) * k + f] : 0.f;
+            // svd.go:271-282 ensembleImplFactors (column f, N(u) order)
+            float e = 0.f;
+            if (act)
+                for (int64_t x = jb; x < je; ++x) e = e + Y[static_cast<int64_t>(ncol[x]) * k + f];
+            const float sq = static_cast<float>(sqrt(static_cast<double>(je - jb)));
+            e = e / sq;
+            float tmp = 0.f;                                   // svd.go:302-305
+            tmp = tmp + p;
+            tmp = tmp + e;
+            float s = tmp * q;
+            for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o);
+            if ((f & 63) == 0) red[f >> 6] = s;
+            __syncthreads();
+            float dot = 0.f;
+            for (int x = 0; x < NT / 64; ++x) dot += red[x];
+            __syncthreads();
+            double pred = gb;                                  // svd.go:290-305
+            pred += static_cast<double>(ub);
+            pred += static_cast<double>(ib);
+            pred += static_cast<double>(dot);
+            const double diff = pred - static_cast<double>(r);
+            gb -= lrd * diff;                                  // svd.go:366-367
+            const float ub_new = static_cast<float>(ub - lrd * (diff + regd * ub));
+            const float ib_new = static_cast<float>(ib - lrd * (diff + regd * ib));
+            const float df = static_cast<float>(diff);
+            float av = (q * df + p * reg) * lr;                // svd.go:378-384 (old q)
+            p = p - av;
+            av = p;                                            // svd.go:387-396 (new p + e)
+            av = av + e;
+            av = av * df;
+            av = (av + q * reg) * lr;
+            q = q - av;
+            if (act) {
+                P[static_cast<int64_t>(u) * k + f] = p;
+                Q[static_cast<int64_t>(i) * k + f] = q;
+                for (int64_t x = jb; x < je; ++x) {            // svd.go:399-422
+                    float* y = Y + static_cast<int64_t>(ncol[x]) * k + f;
+                    float a2 = q * df;
+                    a2 = a2 / sq;
+                    a2 = (a2 + *y * reg) * lr;
+                    *y = *y - a2;
+                }
+            }
+            bu[u] = ub_new;  // every thread stores the same bits and re-reads its own write
+            bi[i] = ib_new;
+        }
+    }
+    if (f == 0) gb_io[0] = gb;
+}
+
+static void pack_bias_rows(const double* F, const double* bias, int64_t rows, int32_t k, int32_t ld,
+                           std::vector<float>& dst) {
+    dst.assign(static_cast<size_t>(rows) * ld, 0.f);
+    for (int64_t r = 0; r < rows; ++r) {
+        for (int32_t f = 0; f < k; ++f) dst[r * ld + f] = static_cast<float>(F[r * k + f]);
+        if (bias) dst[r * ld + ld - 1] = static_cast<float>(bias[r]);
+    }
+}
+
+static void unpack_bias_rows(const std::vector<float>& src, int64_t rows, int32_t k, int32_t ld,
+                             double* F, double* bias) {
+    for (int64_t r = 0; r < rows; ++r) {
+        for (int32_t f = 0; f < k; ++f) F[r * k + f] = src[r * ld + f];
+        if (bias) bias[r] = src[r * ld + ld - 1];
+    }
+}
+
+template <int E>
+static void launch_pp_fast(int32_t n_blocks, const DevBuf<int32_t>& work, int32_t n_work,
+                           const DevBuf<int64_t>& rowptr, const DevBuf<int32_t>& items,
+                           const DevBuf<float>& ratings, DevBuf<float>& P, DevBuf<float>& Q,
+                           DevBuf<float>& Y, DevBuf<double>& gb, DevBuf<double>& partial, float lr,
+                           float reg, hipStream_t s) {
+    hipLaunchKernelGGL((svdpp_epoch_fast_kernel<E, 8>), dim3(n_blocks), dim3(256), 0, s, work.p,
+                       n_work, rowptr.p, items.p, ratings.p, P.p, Q.p, Y.p,
+                       static_cast<int32_t>(Q.n * 4), static_cast<int32_t>(Y.n * 4), gb.p,
+                       partial.p, lr, reg);
+}
+
+}  // namespace rs
+
+extern "C" int rs_svdpp_fit(rs_ctx* ctx, const rs_ratings* r, const rs_sgd_params* p, double* P,
+                            double* Q, double* Y, double* bu, double* bi, double* gb) {
+    if (!ctx) return rs::set_error(ctx, RS_ERR_INVALID, "ctx is NULL");
+    return rs_guard(ctx, [&]() -> int {
+        int st = rs::check_ratings(ctx, r);
+        if (st != RS_OK) return st;
+        if (!p || !P || !Q || !Y || !bu || !bi || !gb)
+            return rs::set_error(ctx, RS_ERR_INVALID, "NULL argument");
+        const int32_t k = p->n_factors;
+        if (k < 1 || k > 511) return rs::set_error(ctx, RS_ERR_UNSUPPORTED, "n_factors must be in [1, 511]");
+        if (p->n_epochs < 0) return rs::set_error(ctx, RS_ERR_INVALID, "n_epochs < 0");
+        hipStream_t s = ctx->stream;
+        const float lr = static_cast<float>(p->lr), reg = static_cast<float>(p->reg);
+        rs::UserCSR csr;  // N(u) = TrainSet.UserRatings() (data.go:185-199), data order
+        rs::build_csr(r->nnz, r->n_users, r->users, r->items, r->ratings, csr);
+        csr.cols.resize(csr.cols.size() + 64, 0);
+        csr.vals.resize(csr.vals.size() + 64, 0.f);
+        rs::DevBuf<int64_t> drow(csr.rowptr.size());
+        rs::DevBuf<int32_t> dcol(csr.cols.size());
+        rs::DevBuf<float> dval(csr.vals.size());
+        drow.upload(csr.rowptr.data(), csr.rowptr.size(), s);
+        dcol.upload(csr.cols.data(), csr.cols.size(), s);
+        dval.upload(csr.vals.data(), csr.vals.size(), s);
+        rs::DevBuf<double> dgb(1);
+        dgb.upload(gb, 1, s);
+        if (p->mode == RS_SGD_ORDERED) {
+            const int64_t nnz = r->nnz;
+            rs::DevBuf<int32_t> du(std::max<int64_t>(1, nnz)), di(std::max<int64_t>(1, nnz));
+            rs::DevBuf<float> dr(std::max<int64_t>(1, nnz));
+            std::vector<float> rf(nnz);
+            for (int64_t t = 0; t < nnz; ++t) rf[t] = static_cast<float>(r->ratings[t]);
+            du.upload(r->users, nnz, s);
+            di.upload(r->items, nnz, s);
+            dr.upload(rf.data(), nnz, s);
+            std::vector<float> hP, hQ, hY, hbu, hbi;
+            rs::pack_rows_f32(P, r->n_users, k, k, hP);
+            rs::pack_rows_f32(Q, r->n_items, k, k, hQ);
+            rs::pack_rows_f32(Y, r->n_items, k, k, hY);
+            rs::pack_rows_f32(bu, r->n_users, 1, 1, hbu);
+            rs::pack_rows_f32(bi, r->n_items, 1, 1, hbi);
+            rs::DevBuf<float> dP(std::max<size_t>(1, hP.size())), dQ(std::max<size_t>(1, hQ.size())),
+                dY(std::max<size_t>(1, hY.size())), dbu(std::max<size_t>(1, hbu.size())),
+                dbi(std::max<size_t>(1, hbi.size()));
+            dP.upload(hP.data(), hP.size(), s);
+            dQ.upload(hQ.data(), hQ.size(), s);
+            dY.upload(hY.data(), hY.size(), s);
+            dbu.upload(hbu.data(), hbu.size(), s);
+            dbi.upload(hbi.data(), hbi.size(), s);
+            if (nnz > 0 && p->n_epochs > 0) {
+                if (k <= 256)
+                    hipLaunchKernelGGL((rs::svdpp_ordered_kernel<256>), dim3(1), dim3(256), 0, s, nnz, du.p, di.p, dr.p, drow.p, dcol.p, dP.p, dQ.p, dY.p, dbu.p, dbi.p, k, dgb.p, p->n_epochs, lr, reg);
+                else
+                    hipLaunchKernelGGL((rs::svdpp_ordered_kernel<512>), dim3(1), dim3(512), 0, s, nnz, du.p, di.p, dr.p, drow.p, dcol.p, dP.p, dQ.p, dY.p, dbu.p, dbi.p, k, dgb.p, p->n_epochs, lr, reg);
+                RS_HIP(hipGetLastError());
+            }
+            dP.download(hP.data(), hP.size(), s);
+            dQ.download(hQ.data(), hQ.size(), s);
+            dY.download(hY.data(), hY.size(), s);
+            dbu.download(hbu.data(), hbu.size(), s);
+            dbi.download(hbi.data(), hbi.size(), s);
+            dgb.download(gb, 1, s);
+            RS_HIP(hipStreamSynchronize(s));
+            rs::unpack_rows_f64(hP, r->n_users, k, k, P);
+            rs::unpack_rows_f64(hQ, r->n_items, k, k, Q);
+            rs::unpack_rows_f64(hY, r->n_items, k, k, Y);
+            rs::unpack_rows_f64(hbu, r->n_users, 1, 1, bu);
+            rs::unpack_rows_f64(hbi, r->n_items, 1, 1, bi);
+            return RS_OK;
+        }
+        // FAST: heaviest user first; GlobalBias warm start (common.hpp)
+        if (p->n_epochs > 0) {
+            *gb = rs::gb_warm_start(r, bu, bi);
+            dgb.upload(gb, 1, s);
+        }
+        std::vector<int32_t> order;
+        for (int32_t x = 0; x < r->n_users; ++x)
+            if (csr.rowptr[x + 1] > csr.rowptr[x]) order.push_back(x);
+        std::stable_sort(order.begin(), order.end(), [&](int32_t x, int32_t y) {
+            return csr.rowptr[x + 1] - csr.rowptr[x] > csr.rowptr[y + 1] - csr.rowptr[y];
+        });
+        const int32_t E = (k + 1 + 63) / 64, ld = 64 * E;
+        if (static_cast<int64_t>(std::max(1, r->n_items)) * ld * 4 >= (int64_t{1} << 31) - 64)
+            return rs::set_error(ctx, RS_ERR_UNSUPPORTED, "n_items * n_factors too large");
+        const int32_t n_work = static_cast<int32_t>(order.size());
+        const int32_t n_blocks = std::max<int32_t>(1, (n_work + 3) / 4);
+        rs::DevBuf<int32_t> dwork(std::max<size_t>(1, order.size()));
+        dwork.upload(order.data(), order.size(), s);
+        std::vector<float> hP, hQ, hY;
+        rs::pack_bias_rows(P, bu, r->n_users, k, ld, hP);
+        rs::pack_bias_rows(Q, bi, r->n_items, k, ld, hQ);
+        rs::pack_bias_rows(Y, nullptr, r->n_items, k, ld, hY);
+        rs::DevBuf<float> dP(std::max<size_t>(1, hP.size())), dQ(std::max<size_t>(1, hQ.size())),
+            dY(std::max<size_t>(1, hY.size()));
+        rs::DevBuf<double> dpart(n_blocks);
+        dP.upload(hP.data(), hP.size(), s);
+        dQ.upload(hQ.data(), hQ.size(), s);
+        dY.upload(hY.data(), hY.size(), s);
+        const double inv_nnz = r->nnz > 0 ? 1.0 / static_cast<double>(r->nnz) : 0.0;
+        for (int32_t ep = 0; ep < p->n_epochs; ++ep) {
+            switch (E) {
+                case 1: rs::launch_pp_fast<1>(n_blocks, dwork, n_work, drow, dcol, dval, dP, dQ, dY, dgb, dpart, lr, reg, s); break;
+                case 2: rs::launch_pp_fast<2>(n_blocks, dwork, n_work, drow, dcol, dval, dP, dQ, dY, dgb, dpart, lr, reg, s); break;
+                case 3: rs::launch_pp_fast<3>(n_blocks, dwork, n_work, drow, dcol, dval, dP, dQ, dY, dgb, dpart, lr, reg, s); break;
+                case 4: rs::launch_pp_fast<4>(n_blocks, dwork, n_work, drow, dcol, dval, dP, dQ, dY, dgb, dpart, lr, reg, s); break;
+                case 5: rs::launch_pp_fast<5>(n_blocks, dwork, n_work, drow, dcol, dval, dP, dQ, dY, dgb, dpart, lr, reg, s); break;
+                case 6: rs::launch_pp_fast<6>(n_blocks, dwork, n_work, drow, dcol, dval, dP, dQ, dY, dgb, dpart, lr, reg, s); break;
+                case 7: rs::launch_pp_fast<7>(n_blocks, dwork, n_work, drow, dcol, dval, dP, dQ, dY, dgb, dpart, lr, reg, s); break;
+                default: rs::launch_pp_fast<8>(n_blocks, dwork, n_work, drow, dcol, dval, dP, dQ, dY, dgb, dpart, lr, reg, s); break;
+            }
+            RS_HIP(hipGetLastError());
+            hipLaunchKernelGGL(rs::pp_gb_fold_kernel, dim3(1), dim3(256), 0, s, dpart.p,
+                               static_cast<int64_t>(n_blocks), dgb.p, inv_nnz);
+            RS_HIP(hipGetLastError());
+        }
+        dP.download(hP.data(), hP.size(), s);
+        dQ.download(hQ.data(), hQ.size(), s);
+        dY.download(hY.data(), hY.size(), s);
+        dgb.download(gb, 1, s);
+        RS_HIP(hipStreamSynchronize(s));
+        rs::unpack_bias_rows(hP, r->n_users, k, ld, P, bu);
+        rs::unpack_bias_rows(hQ, r->n_items, k, ld, Q, bi);
+        rs::unpack_bias_rows(hY, r->n_items, k, ld, Y, nullptr);
+        return RS_OK;
+    });
+}

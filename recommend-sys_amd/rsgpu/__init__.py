@@ -178,6 +178,21 @@ class Context:
                                     _ptr(bu), _ptr(bi), _ptr(g)))
         return P, Q, bu, bi, float(g[0])
 
+    def svdpp_fit(self, r: Ratings, P, Q, Y, bu=None, bi=None, gb=0.0, n_epochs=20, lr=0.007,
+                  reg=0.02, mode=SGD_FAST):
+        """core/svd.go:316-427 (ORDERED: literal per-rating y updates; FAST: lazy-y user-CSR)."""
+        P = np.array(P, dtype=np.float64, order="C")
+        Q = np.array(Q, dtype=np.float64, order="C")
+        Y = np.array(Y, dtype=np.float64, order="C")
+        bu = np.zeros(r.n_users) if bu is None else np.array(bu, dtype=np.float64)
+        bi = np.zeros(r.n_items) if bi is None else np.array(bi, dtype=np.float64)
+        g = np.array([gb], dtype=np.float64)
+        prm = _SgdParams(P.shape[1], n_epochs, lr, reg, mode, 0)
+        rc = r.c()
+        self.check(lib().rs_svdpp_fit(self.h, C.byref(rc), C.byref(prm), _ptr(P), _ptr(Q), _ptr(Y),
+                                      _ptr(bu), _ptr(bi), _ptr(g)))
+        return P, Q, Y, bu, bi, float(g[0])
+
     def nmf_fit(self, r: Ratings, P, Q, n_epochs=50, reg=0.06, as_written=True):
         """core/svd.go:158-251 (as_written reproduces svd.go:243-249, Q5)."""
         P = np.array(P, dtype=np.float64, order="C")

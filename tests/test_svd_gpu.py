@@ -151,8 +151,10 @@ def test_empty_and_tiny_inputs(ctx):
     P, Q, bu, bi, gb = ctx.svd_fit(rsgpu.Ratings(np.zeros(0), np.zeros(0), np.zeros(0), 2, 2),
                                    np.ones((2, 4)), np.ones((2, 4)))
     assert np.all(P == 1) and gb == 0.0
-    for mode in (rsgpu.SGD_FAST, rsgpu.SGD_ORDERED):
-        ref = O.svd_fit([0], [0], [4.0], np.full((1, 3), 0.1), np.full((1, 3), 0.2), epochs=2)
-        got = ctx.svd_fit(rsgpu.Ratings([0], [0], [4.0], 1, 1), np.full((1, 3), 0.1),
-                          np.full((1, 3), 0.2), n_epochs=2, mode=mode)
-        assert _maxdiff(ref[:4], got[:4]) <= TOL
+    P0, Q0 = np.full((1, 3), 0.1), np.full((1, 3), 0.2)
+    refs = {rsgpu.SGD_ORDERED: O.svd_fit([0], [0], [4.0], P0, Q0, epochs=2),
+            rsgpu.SGD_FAST: O.svd_fit_chunked(np.array([0, 1]), [0], [4.0], P0, Q0, 1 << 30,
+                                              epochs=2)}
+    for mode, ref in refs.items():
+        got = ctx.svd_fit(rsgpu.Ratings([0], [0], [4.0], 1, 1), P0, Q0, n_epochs=2, mode=mode)
+        assert _maxdiff(ref[:4], got[:4]) <= TOL and abs(ref[4] - got[4]) <= TOL
