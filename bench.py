@@ -101,7 +101,8 @@ def main():
 
     if world > 1:
         import rsgpu.multi as multi
-        step = multi.ItemShardedStep(plan, ctx, dist, stream, total_nnz=nnz * world)
+        w, total = multi.user_weights(u, n_users, dist, device=f"cuda:{dev}")
+        step = multi.ItemShardedStep(plan, dist, w, total, device=f"cuda:{dev}", stream=stream)
         run = lambda n: step.run(n, LR, REG)
     else:
         run = lambda n: plan.epochs(n, LR, REG, stream)

@@ -143,6 +143,19 @@ int rs_svd_plan_epochs(rs_svd_plan* plan, int32_t n_epochs, float lr, float reg,
 /* write_back: RS_SGD_WB_ATOMIC (default) or RS_SGD_WB_STORE; ring_depth: item-row prefetch distance
  * in ratings (4, 8 = default, 16). */
 int rs_svd_plan_set_mode(rs_svd_plan* plan, int32_t write_back, int32_t ring_depth);
+/* ---- item-sharded multi-GPU (north_star: Q sharded by item range, users replicated) --------- *
+ * Each rank builds a plan over its item shard.  Per epoch: rs_svd_plan_epoch_delta leaves P at the
+ * epoch start and writes dP[u] = w_u (p_u(end) - p_u(start)) (bias column included) and
+ * gbsum = sum_w n_w (gb_w - gb); the caller all-reduces (sum) dP and gbsum over the ranks (RCCL)
+ * and calls rs_svd_plan_apply_delta(inv_total_nnz = 1 / total ratings over all ranks).
+ * w_u = (ratings of u in this shard) / (ratings of u over all shards): the count-weighted average of
+ * the shards' user deltas (a plain sum of per-shard deltas overshoots for users split over shards).
+ * dP: device buffer of n_users x ld float32; gbsum: device float64. */
+int rs_svd_plan_set_user_weights(rs_svd_plan* plan, const float* w /* host, n_users; NULL clears */);
+int rs_svd_plan_epoch_delta(rs_svd_plan* plan, float lr, float reg, void* dP, void* gbsum,
+                            void* stream);
+int rs_svd_plan_apply_delta(rs_svd_plan* plan, const void* dP, const void* gbsum,
+                            double inv_total_nnz, void* stream);
 /* Device pointers of the resident state (layout above); ld = row stride in floats. */
 int rs_svd_plan_device_ptrs(rs_svd_plan* plan, void** P, void** Q, void** gb_f64, int32_t* ld);
 /* Per-launch timing: when on, rs_svd_plan_epochs brackets every SGD kernel with HIP events on

@@ -60,7 +60,7 @@ __global__ __launch_bounds__(256) void svd_epoch_fast_kernel(
     const int32_t* __restrict__ work, int32_t n_work, const int64_t* __restrict__ rowptr,
     const int32_t* __restrict__ items, const float* __restrict__ ratings, float* __restrict__ P,
     float* Q, int32_t q_bytes, const double* __restrict__ gb_in, double* __restrict__ gb_partial,
-    float lr, float reg) {
+    float lr, float reg, float* __restrict__ dP, const float* __restrict__ uw) {
 #pragma clang fp contract(fast)
     constexpr int LD = 64 * E, B = 16;
     static_assert(B % D == 0 && D <= B, "ring depth must divide the 16-rating batch");
@@ -155,8 +155,15 @@ __global__ __launch_bounds__(256) void svd_epoch_fast_kernel(
 #pragma unroll
             for (int j = 0; j < B; ++j) it_nxt[j] = items[base + 2 * B + j];
         }
+        if (dP) {  // item-sharded multi-GPU: weighted delta, P itself stays at the epoch start
+            const float wu = uw[u];
+            float* drow = dP + static_cast<int64_t>(u) * LD;
 #pragma unroll
-        for (int x = 0; x < E; ++x) prow[lane + 64 * x] = p[x];
+            for (int x = 0; x < E; ++x) drow[lane + 64 * x] = wu * (p[x] - prow[lane + 64 * x]);
+        } else {
+#pragma unroll
+            for (int x = 0; x < E; ++x) prow[lane + 64 * x] = p[x];
+        }
         contrib = static_cast<double>(deg) * (static_cast<double>(gb) - static_cast<double>(gb0));
     }
     if (lane == 0) s_contrib[wib] = contrib;
@@ -178,6 +185,36 @@ __global__ __launch_bounds__(256) void gb_fold_kernel(const double* __restrict__
         __syncthreads();
     }
     if (threadIdx.x == 0) gb[0] += s[0] * inv_nnz;
+}
+
+// Multi-GPU: the all-reduced weighted user deltas and global-bias sum are applied in place.
+__global__ __launch_bounds__(256) void svd_apply_delta_kernel(float4* __restrict__ P,
+                                                              const float4* __restrict__ dP, int64_t n4,
+                                                              double* __restrict__ gb,
+                                                              const double* __restrict__ gbsum,
+                                                              double inv_total) {
+    for (int64_t t = blockIdx.x * 256 + threadIdx.x; t < n4; t += static_cast<int64_t>(gridDim.x) * 256) {
+        float4 a = P[t];
+        const float4 d = dP[t];
+        a.x += d.x; a.y += d.y; a.z += d.z; a.w += d.w;
+        P[t] = a;
+    }
+    if (blockIdx.x == 0 && threadIdx.x == 0) gb[0] += gbsum[0] * inv_total;
+}
+
+// sum of block partials in fixed order (multi-GPU: the ranks' sums are all-reduced, then applied)
+__global__ __launch_bounds__(256) void gb_sum_kernel(const double* __restrict__ partial, int64_t n,
+                                                     double* __restrict__ out) {
+    __shared__ double s[256];
+    double t = 0.0;
+    for (int64_t x = threadIdx.x; x < n; x += 256) t += partial[x];
+    s[threadIdx.x] = t;
+    __syncthreads();
+    for (int w = 128; w > 0; w >>= 1) {
+        if (static_cast<int>(threadIdx.x) < w) s[threadIdx.x] += s[threadIdx.x + w];
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) out[0] = s[0];
 }
 
 // --------------------------------------------------------------------------------------------
@@ -272,6 +309,7 @@ struct rs_svd_plan {
     rs::DevBuf<int32_t> work;
     rs::DevBuf<float> P, Q;  // bias in column ld - 1
     rs::DevBuf<double> gb, partial;
+    rs::DevBuf<float> uw;  // per-user share of this shard (multi-GPU delta mode)
     int32_t n_blocks = 0;
     int32_t write_back = RS_SGD_WB_ATOMIC;
     int32_t ring_depth = 8;
@@ -294,39 +332,39 @@ namespace rs {
 constexpr int32_t kMaxFactors = 511;
 
 template <int E, int D, int WB>
-static void launch_fast_t(rs_svd_plan* pl, float lr, float reg, hipStream_t s) {
+static void launch_fast_t(rs_svd_plan* pl, float lr, float reg, hipStream_t s, float* dP) {
     const int32_t q_bytes = static_cast<int32_t>(pl->Q.n * sizeof(float));
     hipLaunchKernelGGL((svd_epoch_fast_kernel<E, D, WB>), dim3(pl->n_blocks), dim3(256), 0, s,
                        pl->work.p, pl->n_work, pl->rowptr.p, pl->items.p, pl->ratings.p, pl->P.p,
-                       pl->Q.p, q_bytes, pl->gb.p, pl->partial.p, lr, reg);
+                       pl->Q.p, q_bytes, pl->gb.p, pl->partial.p, lr, reg, dP, pl->uw.p);
 }
 
 template <int D, int WB>
-static void launch_fast_e(rs_svd_plan* pl, float lr, float reg, hipStream_t s) {
+static void launch_fast_e(rs_svd_plan* pl, float lr, float reg, hipStream_t s, float* dP) {
     switch (pl->ld / 64) {
-        case 1: launch_fast_t<1, D, WB>(pl, lr, reg, s); break;
-        case 2: launch_fast_t<2, D, WB>(pl, lr, reg, s); break;
-        case 3: launch_fast_t<3, D, WB>(pl, lr, reg, s); break;
-        case 4: launch_fast_t<4, D, WB>(pl, lr, reg, s); break;
-        case 5: launch_fast_t<5, D, WB>(pl, lr, reg, s); break;
-        case 6: launch_fast_t<6, D, WB>(pl, lr, reg, s); break;
-        case 7: launch_fast_t<7, D, WB>(pl, lr, reg, s); break;
-        default: launch_fast_t<8, D, WB>(pl, lr, reg, s); break;
+        case 1: launch_fast_t<1, D, WB>(pl, lr, reg, s, dP); break;
+        case 2: launch_fast_t<2, D, WB>(pl, lr, reg, s, dP); break;
+        case 3: launch_fast_t<3, D, WB>(pl, lr, reg, s, dP); break;
+        case 4: launch_fast_t<4, D, WB>(pl, lr, reg, s, dP); break;
+        case 5: launch_fast_t<5, D, WB>(pl, lr, reg, s, dP); break;
+        case 6: launch_fast_t<6, D, WB>(pl, lr, reg, s, dP); break;
+        case 7: launch_fast_t<7, D, WB>(pl, lr, reg, s, dP); break;
+        default: launch_fast_t<8, D, WB>(pl, lr, reg, s, dP); break;
     }
 }
 
 template <int WB>
-static void launch_fast_d(rs_svd_plan* pl, float lr, float reg, hipStream_t s) {
+static void launch_fast_d(rs_svd_plan* pl, float lr, float reg, hipStream_t s, float* dP) {
     switch (pl->ring_depth) {
-        case 4: launch_fast_e<4, WB>(pl, lr, reg, s); break;
-        case 16: launch_fast_e<16, WB>(pl, lr, reg, s); break;
-        default: launch_fast_e<8, WB>(pl, lr, reg, s); break;
+        case 4: launch_fast_e<4, WB>(pl, lr, reg, s, dP); break;
+        case 16: launch_fast_e<16, WB>(pl, lr, reg, s, dP); break;
+        default: launch_fast_e<8, WB>(pl, lr, reg, s, dP); break;
     }
 }
 
-static void launch_fast(rs_svd_plan* pl, float lr, float reg, hipStream_t s) {
-    if (pl->write_back == RS_SGD_WB_STORE) launch_fast_d<0>(pl, lr, reg, s);  // template WB: 0 store
-    else launch_fast_d<1>(pl, lr, reg, s);                                    //             1 atomic
+static void launch_fast(rs_svd_plan* pl, float lr, float reg, hipStream_t s, float* dP = nullptr) {
+    if (pl->write_back == RS_SGD_WB_STORE) launch_fast_d<0>(pl, lr, reg, s, dP);  // WB 0: store
+    else launch_fast_d<1>(pl, lr, reg, s, dP);                                    // WB 1: atomic
     RS_HIP(hipGetLastError());
 }
 
@@ -524,6 +562,69 @@ extern "C" void rs_svd_plan_destroy(rs_svd_plan* pl) {
     (void)hipSetDevice(pl->ctx->device);
     if (pl->last_stream) (void)hipStreamSynchronize(pl->last_stream);
     delete pl;
+}
+
+extern "C" int rs_svd_plan_set_user_weights(rs_svd_plan* pl, const float* w) {
+    if (!pl) return rs::set_error(nullptr, RS_ERR_INVALID, "plan is NULL");
+    return rs_guard(pl->ctx, [&]() -> int {
+        if (!w) {
+            pl->uw.release();
+            return RS_OK;
+        }
+        pl->uw.alloc(std::max(1, pl->n_users));
+        pl->uw.upload(w, pl->n_users, pl->ctx->stream);
+        RS_HIP(hipStreamSynchronize(pl->ctx->stream));
+        return RS_OK;
+    });
+}
+
+extern "C" int rs_svd_plan_epoch_delta(rs_svd_plan* pl, float lr, float reg, void* dP, void* gbsum,
+                                       void* stream) {
+    if (!pl) return rs::set_error(nullptr, RS_ERR_INVALID, "plan is NULL");
+    return rs_guard(pl->ctx, [&]() -> int {
+        if (!dP || !gbsum) return rs::set_error(pl->ctx, RS_ERR_INVALID, "delta buffers are NULL");
+        if (!pl->uw.p) return rs::set_error(pl->ctx, RS_ERR_INVALID, "user weights not set");
+        hipStream_t s = stream ? static_cast<hipStream_t>(stream) : pl->ctx->stream;
+        RS_HIP(hipMemsetAsync(dP, 0, pl->P.n * sizeof(float), s));  // users absent from the shard
+        if (pl->timing) {
+            if (pl->tev.size() < 2) {
+                for (int x = 0; x < 2; ++x) {
+                    hipEvent_t e;
+                    RS_HIP(hipEventCreate(&e));
+                    pl->tev.push_back(e);
+                }
+            }
+            pl->tev_used = 2;
+            RS_HIP(hipEventRecord(pl->tev[0], s));
+        }
+        RS_HIP(hipEventRecord(pl->ev0, s));
+        rs::launch_fast(pl, lr, reg, s, static_cast<float*>(dP));
+        if (pl->timing) RS_HIP(hipEventRecord(pl->tev[1], s));
+        hipLaunchKernelGGL(rs::gb_sum_kernel, dim3(1), dim3(256), 0, s, pl->partial.p,
+                           static_cast<int64_t>(pl->n_blocks), static_cast<double*>(gbsum));
+        RS_HIP(hipGetLastError());
+        RS_HIP(hipEventRecord(pl->ev1, s));
+        pl->last_launches = pl->timing ? 1 : 2;
+        pl->last_stream = s;
+        pl->last_ms = -1.0;
+        return RS_OK;
+    });
+}
+
+extern "C" int rs_svd_plan_apply_delta(rs_svd_plan* pl, const void* dP, const void* gbsum,
+                                       double inv_total_nnz, void* stream) {
+    if (!pl) return rs::set_error(nullptr, RS_ERR_INVALID, "plan is NULL");
+    return rs_guard(pl->ctx, [&]() -> int {
+        if (!dP || !gbsum) return rs::set_error(pl->ctx, RS_ERR_INVALID, "delta buffers are NULL");
+        hipStream_t s = stream ? static_cast<hipStream_t>(stream) : pl->ctx->stream;
+        const int64_t n4 = static_cast<int64_t>(pl->P.n) / 4;
+        hipLaunchKernelGGL(rs::svd_apply_delta_kernel, dim3(1024), dim3(256), 0, s,
+                           reinterpret_cast<float4*>(pl->P.p), static_cast<const float4*>(dP), n4,
+                           pl->gb.p, static_cast<const double*>(gbsum), inv_total_nnz);
+        RS_HIP(hipGetLastError());
+        pl->last_stream = s;
+        return RS_OK;
+    });
 }
 
 extern "C" int rs_svd_plan_set_mode(rs_svd_plan* pl, int32_t write_back, int32_t ring_depth) {

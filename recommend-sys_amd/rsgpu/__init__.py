@@ -27,7 +27,8 @@ HEADER_SYMBOLS = (
     "rs_svd_fit", "rs_svd_predict", "rs_svdpp_fit", "rs_nmf_fit", "rs_baseline_fit",
     "rs_knn_sims", "rs_sim_pair", "rs_svd_plan_create", "rs_svd_plan_destroy",
     "rs_svd_plan_upload", "rs_svd_plan_download", "rs_svd_plan_epochs",
-    "rs_svd_plan_device_ptrs", "rs_svd_plan_set_mode", "rs_svd_plan_set_timing", "rs_svd_plan_last_kernel_ms",
+    "rs_svd_plan_device_ptrs", "rs_svd_plan_set_mode", "rs_svd_plan_set_timing",
+    "rs_svd_plan_set_user_weights", "rs_svd_plan_epoch_delta", "rs_svd_plan_apply_delta", "rs_svd_plan_last_kernel_ms",
 )
 
 
@@ -86,6 +87,9 @@ def lib():
             "rs_svd_plan_device_ptrs": (C.c_int, [_vp, C.POINTER(_vp), C.POINTER(_vp),
                                                   C.POINTER(_vp), C.POINTER(_i32)]),
             "rs_svd_plan_set_mode": (C.c_int, [_vp, _i32, _i32]),
+            "rs_svd_plan_set_user_weights": (C.c_int, [_vp, _vp]),
+            "rs_svd_plan_epoch_delta": (C.c_int, [_vp, _flt, _flt, _vp, _vp, _vp]),
+            "rs_svd_plan_apply_delta": (C.c_int, [_vp, _vp, _vp, _dbl, _vp]),
             "rs_svd_plan_set_timing": (C.c_int, [_vp, _i32]),
             "rs_svd_plan_last_kernel_ms": (C.c_int, [_vp, C.POINTER(_dbl), C.POINTER(_i32)]),
         }
@@ -202,6 +206,14 @@ class Context:
                                     int(as_written), _ptr(P), _ptr(Q)))
         return P, Q
 
+    def baseline_fit(self, r: Ratings, n_epochs=20, lr=0.005, reg=0.02):
+        """core/base.go:433-461 BaseLine.Fit (exact reference order, float64)."""
+        bu, bi, g = np.zeros(r.n_users), np.zeros(r.n_items), np.zeros(1)
+        rc = r.c()
+        self.check(lib().rs_baseline_fit(self.h, C.byref(rc), n_epochs, lr, reg, _ptr(bu),
+                                         _ptr(bi), _ptr(g)))
+        return bu, bi, float(g[0])
+
     def knn_sims(self, kind, rowptr, ids, ratings, n_right):
         """core/knn.go:224-298 pair loop -> dense L x L float64 Sims (NaN = no co-rating)."""
         rowptr = np.ascontiguousarray(rowptr, dtype=np.int64)
@@ -268,6 +280,29 @@ class SvdPlan:
         self.ctx.check(lib().rs_svd_plan_device_ptrs(self.h, *[C.byref(p) for p in ps],
                                                      C.byref(ld)))
         return [p.value for p in ps], ld.value
+
+    def set_user_weights(self, w):
+        self._w = None if w is None else np.ascontiguousarray(w, dtype=np.float32)
+        self.ctx.check(lib().rs_svd_plan_set_user_weights(self.h, _ptr(self._w)))
+
+    def epoch_delta(self, dP_ptr, gbsum_ptr, lr=0.005, reg=0.02, stream=None):
+        """Device pointers (ints): dP n_users x ld float32, gbsum one float64."""
+        self.ctx.check(lib().rs_svd_plan_epoch_delta(self.h, lr, reg, dP_ptr, gbsum_ptr, stream))
+
+    def apply_delta(self, dP_ptr, gbsum_ptr, inv_total_nnz, stream=None):
+        self.ctx.check(lib().rs_svd_plan_apply_delta(self.h, dP_ptr, gbsum_ptr, inv_total_nnz,
+                                                     stream))
+
+    # torch-tensor forms used by rsgpu.multi.ItemShardedStep
+    def epoch_delta_t(self, dP, gbsum, lr, reg, stream=None):
+        self.epoch_delta(dP.data_ptr(), gbsum.data_ptr(), lr, reg, stream)
+
+    def apply_delta_t(self, dP, gbsum, inv_total_nnz, stream=None):
+        self.apply_delta(dP.data_ptr(), gbsum.data_ptr(), inv_total_nnz, stream)
+
+    @property
+    def ld(self):
+        return self.device_ptrs()[1]
 
     def set_timing(self, on: bool):
         self.ctx.check(lib().rs_svd_plan_set_timing(self.h, int(on)))

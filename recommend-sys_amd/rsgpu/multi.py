@@ -1,0 +1,54 @@
+"""Item-sharded multi-GPU SGD (north_star): one process per GPU, torch.distributed (backend "nccl"
+= RCCL over xGMI on ROCm), Q and b_i sharded by item range, P and b_u replicated.
+
+Per epoch every rank runs its shard's fast SGD kernel in delta mode (rs_svd_plan_epoch_delta), the
+ranks all-reduce the count-weighted user deltas (n_users x ld fp32, one collective) and the
+global-bias sum (one float64), and every rank applies the same sum (rs_svd_plan_apply_delta), so P,
+b_u and GlobalBias stay bitwise identical across ranks.
+"""
+from __future__ import annotations
+
+import numpy as np
+
+
+def item_shard_of(n_items: int, n_shards: int, seed: int = 20250826) -> np.ndarray:
+    """Shard id of every item: contiguous ranges of a seeded permutation of the ids (the survey's
+    'item-ID ranges, nnz-balanced after ID hashing')."""
+    perm = np.random.default_rng(seed).permutation(n_items)
+    return (perm.astype(np.int64) * n_shards // max(1, n_items)).astype(np.int32)
+
+
+def take_shard(users, items, ratings, shard_of_item, rank):
+    m = shard_of_item[np.asarray(items)] == rank
+    return np.asarray(users)[m], np.asarray(items)[m], np.asarray(ratings)[m]
+
+
+def user_weights(local_users, n_users, dist, device=None):
+    """w_u = (ratings of u on this rank) / (ratings of u on all ranks); one all-reduce of counts."""
+    import torch
+    cnt = np.bincount(np.asarray(local_users, dtype=np.int64), minlength=n_users).astype(np.float64)
+    t = torch.tensor(cnt, dtype=torch.float64, device=device)
+    dist.all_reduce(t)
+    tot = t.cpu().numpy()
+    w = np.divide(cnt, tot, out=np.zeros_like(cnt), where=tot > 0)
+    return w.astype(np.float32), float(tot.sum())
+
+
+class ItemShardedStep:
+    """Runs epochs of the item-sharded schedule.  `plan` needs epoch_delta_t(dP, gbsum, lr, reg),
+    apply_delta_t(dP, gbsum, inv_total_nnz), n_users, ld and set_user_weights(w)."""
+
+    def __init__(self, plan, dist, weights, total_nnz, device=None, stream=None):
+        import torch
+        self.plan, self.dist, self.stream = plan, dist, stream
+        self.dP = torch.zeros((plan.n_users, plan.ld), dtype=torch.float32, device=device)
+        self.gbsum = torch.zeros(1, dtype=torch.float64, device=device)
+        self.inv_total = 1.0 / total_nnz if total_nnz > 0 else 0.0
+        plan.set_user_weights(weights)
+
+    def run(self, n_epochs, lr=0.005, reg=0.02):
+        for _ in range(n_epochs):
+            self.plan.epoch_delta_t(self.dP, self.gbsum, lr, reg, self.stream)
+            self.dist.all_reduce(self.dP)
+            self.dist.all_reduce(self.gbsum)
+            self.plan.apply_delta_t(self.dP, self.gbsum, self.inv_total, self.stream)

@@ -122,3 +122,13 @@ def test_knn_bad_arguments(ctx):
         ctx.knn_sims(7, [0, 1], [0], [1.0], 1)
     with pytest.raises(rsgpu.RsError):
         ctx.knn_sims(rsgpu.SIM_COSINE, [0, 1], [5], [1.0], 2)
+
+
+def test_baseline_fit_bitwise(ctx, ml100k):
+    """core/base.go:433-461 BaseLine.Fit (used by KNNBaseLine, knn.go:260-268): float64 serial
+    chain in the reference order -> bitwise equal to the restatement."""
+    from helpers import folds
+    f = folds(*ml100k)[0]
+    ref = O.baseline_fit(f.iu, f.ii, f.r, f.nu, f.ni)
+    got = ctx.baseline_fit(rsgpu.Ratings(f.iu, f.ii, f.r, f.nu, f.ni))
+    assert np.array_equal(ref[0], got[0]) and np.array_equal(ref[1], got[1]) and ref[2] == got[2]

@@ -1,0 +1,131 @@
+"""Item-sharded multi-GPU schedule (rsgpu.multi): world_size-2 gloo tests on CPU with a host model
+of the plan (the shard's epoch is the oracle's restatement of the fast kernel's schedule), checked
+against a single-process computation of the same merge rule."""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+import oracle as O
+from rsgpu import multi
+
+K, EPOCHS = 8, 3
+
+
+class HostPlan:
+    """CPU stand-in for SvdPlan's delta interface (the GPU test covers the kernels themselves)."""
+
+    def __init__(self, users, items, r, n_users, n_items, P0, Q0, gb0):
+        self.k = P0.shape[1]
+        self.n_users, self.ld = n_users, self.k + 1
+        self.rowptr, self.items, self.r = O.csr_by(users, n_users, items, r)
+        self.P, self.Q = P0.copy(), Q0.copy()
+        self.bu, self.bi, self.gb = np.zeros(n_users), np.zeros(n_items), gb0
+        self.w = None
+
+    def set_user_weights(self, w):
+        self.w = np.asarray(w, np.float64)
+
+    def epoch_delta_t(self, dP, gbsum, lr, reg, stream=None):
+        P, Q, bu, bi, g = O.svd_fit_chunked(self.rowptr, self.items, self.r, self.P, self.Q, 1 << 30,
+                                            bu=self.bu, bi=self.bi, gb=self.gb, epochs=1, lr=lr,
+                                            reg=reg, warm=False)
+        self.Q, self.bi = Q, bi
+        d = np.zeros((self.n_users, self.ld))
+        d[:, :self.k] = self.w[:, None] * (P - self.P)
+        d[:, self.k] = self.w * (bu - self.bu)
+        dP.copy_(torch.from_numpy(d.astype(np.float32)))
+        deg = np.diff(self.rowptr).astype(np.float64)
+        nnz = deg.sum()
+        gbsum.copy_(torch.tensor([(g - self.gb) * nnz]))  # fold of the local chains (one fold)
+
+    def apply_delta_t(self, dP, gbsum, inv_total, stream=None):
+        d = dP.numpy().astype(np.float64)
+        self.P = self.P + d[:, :self.k]
+        self.bu = self.bu + d[:, self.k]
+        self.gb = self.gb + float(gbsum.item()) * inv_total
+
+
+def make_data(seed=0, n_users=40, n_items=60, nnz=700):
+    rng = np.random.default_rng(seed)
+    pairs = rng.choice(n_users * n_items, nnz, replace=False)
+    u, i = (pairs // n_items).astype(np.int32), (pairs % n_items).astype(np.int32)
+    return u, i, rng.integers(1, 6, nnz).astype(float), n_users, n_items
+
+
+def reference_merge(u, i, r, nu, ni, P0, Q0, n_shards, epochs=EPOCHS):
+    """Single process: every shard's epoch from the same start, count-weighted user-delta merge."""
+    sh = multi.item_shard_of(ni, n_shards)
+    plans = [HostPlan(*multi.take_shard(u, i, r, sh, s), nu, ni, P0, Q0, 3.0) for s in range(n_shards)]
+    cnt = np.stack([np.bincount(multi.take_shard(u, i, r, sh, s)[0], minlength=nu) for s in range(n_shards)])
+    tot = cnt.sum(0)
+    for s, p in enumerate(plans):
+        p.set_user_weights(np.divide(cnt[s], tot, out=np.zeros(nu), where=tot > 0))
+    for _ in range(epochs):
+        ds, gs = [], []
+        for p in plans:
+            dP, g = torch.zeros((nu, p.ld)), torch.zeros(1, dtype=torch.float64)
+            p.epoch_delta_t(dP, g, 0.005, 0.02)
+            ds.append(dP)
+            gs.append(g)
+        dsum, gsum = sum(ds), sum(gs)
+        for p in plans:
+            p.apply_delta_t(dsum, gsum, 1.0 / len(r))
+    return plans
+
+
+def _worker(rank, world, port, out):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    u, i, r, nu, ni = make_data()
+    rng = np.random.default_rng(1)
+    P0, Q0 = rng.normal(0, 0.1, (nu, K)), rng.normal(0, 0.1, (ni, K))
+    sh = multi.item_shard_of(ni, world)
+    lu, li, lr_ = multi.take_shard(u, i, r, sh, rank)
+    plan = HostPlan(lu, li, lr_, nu, ni, P0, Q0, 3.0)
+    w, total = multi.user_weights(lu, nu, dist)
+    assert total == len(r)
+    step = multi.ItemShardedStep(plan, dist, w, total)
+    step.run(EPOCHS)
+    out[rank] = (plan.P, plan.Q, plan.bu, plan.bi, plan.gb)
+    dist.destroy_process_group()
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def test_item_shards_partition_items():
+    sh = multi.item_shard_of(1000, 4)
+    assert set(np.unique(sh)) == {0, 1, 2, 3}
+    assert max(np.bincount(sh)) - min(np.bincount(sh)) <= 1
+
+
+def test_two_rank_gloo_matches_single_process_merge():
+    port = _free_port()
+    with mp.Manager() as m:
+        out = m.dict()
+        mp.spawn(_worker, args=(2, port, out), nprocs=2, join=True)
+        res = dict(out)
+    u, i, r, nu, ni = make_data()
+    rng = np.random.default_rng(1)
+    P0, Q0 = rng.normal(0, 0.1, (nu, K)), rng.normal(0, 0.1, (ni, K))
+    plans = reference_merge(u, i, r, nu, ni, P0, Q0, 2)
+    for rank in (0, 1):
+        P, Q, bu, bi, gb = res[rank]
+        # replicated state identical on both ranks and equal to the single-process merge
+        np.testing.assert_allclose(P, plans[rank].P, atol=1e-6)
+        np.testing.assert_allclose(bu, plans[rank].bu, atol=1e-6)
+        assert abs(gb - plans[rank].gb) < 1e-9
+        np.testing.assert_array_equal(res[0][0], res[1][0])
+        # each rank's item shard equals the shard trained in the single-process run
+        mine = multi.item_shard_of(ni, 2) == rank
+        np.testing.assert_allclose(Q[mine], plans[rank].Q[mine], atol=1e-6)

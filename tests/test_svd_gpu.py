@@ -158,3 +158,45 @@ def test_empty_and_tiny_inputs(ctx):
     for mode, ref in refs.items():
         got = ctx.svd_fit(rsgpu.Ratings([0], [0], [4.0], 1, 1), P0, Q0, n_epochs=2, mode=mode)
         assert _maxdiff(ref[:4], got[:4]) <= TOL and abs(ref[4] - got[4]) <= TOL
+
+
+def test_item_sharded_delta_mode_two_shards(ctx):
+    """rs_svd_plan_epoch_delta / apply_delta with two item shards on one device and the all-reduce
+    done on the host: equal to the host model of the merge rule (race-free input)."""
+    import torch
+    from rsgpu import multi
+    from test_multi import reference_merge
+    u, i, r, nu, ni = _disjoint_input(n_users=120, k=16)
+    k, epochs = 16, 3
+    rng = np.random.default_rng(8)
+    P0, Q0 = rng.normal(0, 0.1, (nu, k)), rng.normal(0, 0.1, (ni, k))
+    sh = multi.item_shard_of(ni, 2)
+    plans, ws = [], []
+    cnt = np.stack([np.bincount(multi.take_shard(u, i, r, sh, s)[0], minlength=nu) for s in (0, 1)])
+    for s in (0, 1):
+        su, si, sr = multi.take_shard(u, i, r, sh, s)
+        pl = ctx.svd_plan(rsgpu.Ratings(su, si, sr, nu, ni), k)
+        pl.upload(P0, Q0, np.zeros(nu), np.zeros(ni), 3.0)
+        pl.set_user_weights(np.divide(cnt[s], cnt.sum(0), out=np.zeros(nu), where=cnt.sum(0) > 0))
+        plans.append(pl)
+    ld = plans[0].ld
+    dPs = [torch.zeros((nu, ld), dtype=torch.float32, device="cuda") for _ in plans]
+    gss = [torch.zeros(1, dtype=torch.float64, device="cuda") for _ in plans]
+    for _ in range(epochs):
+        for pl, dP, g in zip(plans, dPs, gss):
+            pl.epoch_delta_t(dP, g, 0.005, 0.02)
+        torch.cuda.synchronize()
+        dsum, gsum = dPs[0] + dPs[1], gss[0] + gss[1]
+        for pl in plans:
+            pl.apply_delta_t(dsum, gsum, 1.0 / len(r))
+        torch.cuda.synchronize()
+    ref = reference_merge(u, i, r, nu, ni, P0, Q0, 2, epochs=epochs)
+    for s, pl in enumerate(plans):
+        P, Q, bu, bi, gb = pl.download()
+        np.testing.assert_allclose(P, ref[s].P, atol=TOL)
+        np.testing.assert_allclose(bu, ref[s].bu, atol=TOL)
+        mine = sh == s
+        np.testing.assert_allclose(Q[mine], ref[s].Q[mine], atol=TOL)
+        np.testing.assert_allclose(bi[mine], ref[s].bi[mine], atol=TOL)
+        assert abs(gb - ref[s].gb) < TOL
+        pl.close()
