@@ -86,6 +86,10 @@ int rs_open(int32_t device, rs_ctx** out);
 void rs_close(rs_ctx* ctx);
 const char* rs_last_error(const rs_ctx* ctx);
 int rs_synchronize(rs_ctx* ctx);
+/* Device time (ms, HIP events on the ctx stream) of the kernels of the last estimator call on ctx
+ * (rs_svd_fit, rs_svdpp_fit, rs_nmf_fit, rs_baseline_fit, rs_knn_sims): uploads, host packing and
+ * downloads excluded. */
+int rs_last_kernel_ms(const rs_ctx* ctx, double* ms);
 
 /* ---- estimators (host buffers in/out) ------------------------------------------------------- */
 

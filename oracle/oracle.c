@@ -464,6 +464,16 @@ void or_knn_sims(int32_t kind, int32_t L, const int64_t* rowptr, const int32_t* 
     free(sr);
 }
 
+void or_knn_sims_rows(int32_t kind, int32_t L, const int64_t* rowptr, const int32_t* sid,
+                      const double* sr, int32_t row_begin, int32_t row_end, double* out) {
+    for (int32_t a = row_begin; a < row_end; a++)
+        for (int32_t b = 0; b < L; b++)
+            out[(int64_t)(a - row_begin) * L + b] =
+                a == b ? NAN
+                       : or_sim(kind, rowptr[a + 1] - rowptr[a], sid + rowptr[a], sr + rowptr[a],
+                                rowptr[b + 1] - rowptr[b], sid + rowptr[b], sr + rowptr[b]);
+}
+
 /* ------------------------------------------------------------------------------------------ */
 /* KNN.Predict                                                                                 */
 

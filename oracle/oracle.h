@@ -75,6 +75,10 @@ double or_sim(int32_t kind, int64_t na, const int32_t* a_id, const double* a_r,
 void or_knn_sims(int32_t kind, int32_t L, const int64_t* rowptr, const int32_t* ids,
                  const double* ratings, double* sims);
 
+/* Rows [row_begin, row_end) of the knn.go pair loop against every partner (cpu_baseline sample). */
+void or_knn_sims_rows(int32_t kind, int32_t L, const int64_t* rowptr, const int32_t* sorted_ids,
+                      const double* sorted_r, int32_t row_begin, int32_t row_end, double* out);
+
 /* knn.go:156-222 KNN.Predict with ties broken by (sim desc, position asc) -- the reference uses
  * Go's unstable sort.Sort (knn.go:189), so tie order is the one documented deviation.
  * type: 0 basic, 1 centered, 2 zscore, 3 baseline.  right_* is RightRatings CSR in data order. */

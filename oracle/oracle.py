@@ -67,6 +67,8 @@ def lib():
         L.or_svd_fit_chunked.argtypes = [C.c_int32, _i64p, _i32p, _f64p, C.c_int32, C.c_int32,
                                          C.c_int32, C.c_double, C.c_double, _f64p, _f64p, _f64p,
                                          _f64p, _dp]
+        L.or_knn_sims_rows.argtypes = [C.c_int32, C.c_int32, _i64p, _i32p, _f64p, C.c_int32,
+                                       C.c_int32, _f64p]
         L.or_gb_warm_start.argtypes = [C.c_int32, _i64p, _i32p, _f64p, _f64p, _f64p]
         L.or_gb_warm_start.restype = C.c_double
         _lib = L
@@ -215,6 +217,15 @@ def knn_sims(kind, rowptr, ids, ratings):
     L = len(rowptr) - 1
     out = np.empty((L, L))
     lib().or_knn_sims(kind, L, _i64(rowptr), _i32(ids), _f64(ratings), out)
+    return out
+
+
+def knn_sims_rows(kind, rowptr, sorted_ids, sorted_r, row_begin, row_end):
+    """Rows of the pair loop (rows must already be ID-sorted, data.go:236-243)."""
+    L = len(rowptr) - 1
+    out = np.empty((row_end - row_begin, L))
+    lib().or_knn_sims_rows(kind, L, _i64(rowptr), _i32(sorted_ids), _f64(sorted_r), row_begin,
+                           row_end, out)
     return out
 
 

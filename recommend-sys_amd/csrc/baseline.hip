@@ -89,6 +89,7 @@ extern "C" int rs_baseline_fit(rs_ctx* ctx, const rs_ratings* r, int32_t n_epoch
         dbi.upload(bi, r->n_items, s);
         dgb.upload(gb, 1, s);
         const int64_t nb = static_cast<int64_t>(r->n_users) + r->n_items;
+        rs::kernel_span_begin(ctx);
         if (nnz > 0 && n_epochs > 0) {
             if (nb <= rs::kBaselineLdsDoubles)
                 hipLaunchKernelGGL(rs::baseline_fit_kernel<true>, dim3(1), dim3(64), nb * sizeof(double), s, nnz, du.p, di.p, dr.p, r->n_users, r->n_items, dbu.p, dbi.p, dgb.p, n_epochs, lr, reg);
@@ -96,6 +97,7 @@ extern "C" int rs_baseline_fit(rs_ctx* ctx, const rs_ratings* r, int32_t n_epoch
                 hipLaunchKernelGGL(rs::baseline_fit_kernel<false>, dim3(1), dim3(64), 0, s, nnz, du.p, di.p, dr.p, r->n_users, r->n_items, dbu.p, dbi.p, dgb.p, n_epochs, lr, reg);
             RS_HIP(hipGetLastError());
         }
+        rs::kernel_span_end(ctx);
         dbu.download(bu, r->n_users, s);
         dbi.download(bi, r->n_items, s);
         dgb.download(gb, 1, s);

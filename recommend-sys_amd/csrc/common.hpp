@@ -14,7 +14,20 @@ struct rs_ctx {
     int device = 0;
     hipStream_t stream = nullptr;
     std::string err;
+    hipEvent_t k0 = nullptr, k1 = nullptr;  // bracket the main kernels of the last estimator call
+    double last_kernel_ms = 0.0;
 };
+
+namespace rs {
+// Device-time bracket of an estimator call's kernels (HIP events on the ctx stream).
+inline void kernel_span_begin(rs_ctx* c) { (void)hipEventRecord(c->k0, c->stream); }
+inline void kernel_span_end(rs_ctx* c) {
+    (void)hipEventRecord(c->k1, c->stream);
+    float ms = 0.f;
+    if (hipEventSynchronize(c->k1) == hipSuccess && hipEventElapsedTime(&ms, c->k0, c->k1) == hipSuccess)
+        c->last_kernel_ms = ms;
+}
+}  // namespace rs
 
 namespace rs {
 

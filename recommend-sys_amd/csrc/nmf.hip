@@ -159,6 +159,8 @@ extern "C" int rs_nmf_fit(rs_ctx* ctx, const rs_ratings* r, int32_t n_factors, i
         float* q = dQa.p;
         float* qn = dQb.p;
         const float fr = static_cast<float>(reg);
+        RS_HIP(hipStreamSynchronize(s));
+        rs::kernel_span_begin(ctx);
         for (int32_t ep = 0; ep < n_epochs; ++ep) {
             switch (E) {
                 case 1: rs::nmf_epoch_t<1, 8>(r->n_users, r->n_items, urow, ucol, uval, irow, icol, ival, dP.p, q, qn, k, fr, as_written != 0, s); break;
@@ -167,6 +169,7 @@ extern "C" int rs_nmf_fit(rs_ctx* ctx, const rs_ratings* r, int32_t n_factors, i
                 default: rs::nmf_epoch_t<8, 4>(r->n_users, r->n_items, urow, ucol, uval, irow, icol, ival, dP.p, q, qn, k, fr, as_written != 0, s); break;
             }
         }
+        rs::kernel_span_end(ctx);
         dP.download(hP.data(), hP.size(), s);
         RS_HIP(hipMemcpyAsync(hQ.data(), q, hQ.size() * sizeof(float), hipMemcpyDeviceToHost, s));
         RS_HIP(hipStreamSynchronize(s));

@@ -107,6 +107,11 @@ extern "C" int rs_open(int32_t device, rs_ctx** out) {
             delete ctx;
             return rs::set_error(nullptr, RS_ERR_HIP, std::string("hipStreamCreate: ") + hipGetErrorString(e));
         }
+        if (hipEventCreate(&ctx->k0) != hipSuccess || hipEventCreate(&ctx->k1) != hipSuccess) {
+            (void)hipStreamDestroy(ctx->stream);
+            delete ctx;
+            return rs::set_error(nullptr, RS_ERR_HIP, "hipEventCreate failed");
+        }
         *out = ctx;
         return RS_OK;
     });
@@ -119,11 +124,19 @@ extern "C" void rs_close(rs_ctx* ctx) {
         (void)hipStreamSynchronize(ctx->stream);
         (void)hipStreamDestroy(ctx->stream);
     }
+    if (ctx->k0) (void)hipEventDestroy(ctx->k0);
+    if (ctx->k1) (void)hipEventDestroy(ctx->k1);
     delete ctx;
 }
 
 extern "C" const char* rs_last_error(const rs_ctx* ctx) {
     return ctx ? ctx->err.c_str() : rs::tls_error().c_str();
+}
+
+extern "C" int rs_last_kernel_ms(const rs_ctx* ctx, double* ms) {
+    if (!ctx || !ms) return rs::set_error(nullptr, RS_ERR_INVALID, "NULL argument");
+    *ms = ctx->last_kernel_ms;
+    return RS_OK;
 }
 
 extern "C" int rs_synchronize(rs_ctx* ctx) {

@@ -722,7 +722,9 @@ extern "C" int rs_svd_fit(rs_ctx* ctx, const rs_ratings* r, const rs_sgd_params*
             pl.write_back = p->write_back == RS_SGD_WB_STORE ? RS_SGD_WB_STORE : RS_SGD_WB_ATOMIC;
             if (p->n_epochs > 0) *gb = rs::gb_warm_start(r, bu, bi);
             rs::plan_upload(&pl, P, Q, bu, bi, gb);
+            rs::kernel_span_begin(ctx);
             rs::plan_epochs(&pl, p->n_epochs, lr, reg, ctx->stream);
+            rs::kernel_span_end(ctx);
             rs::plan_download(&pl, P, Q, bu, bi, gb);
             return RS_OK;
         }
@@ -751,9 +753,11 @@ extern "C" int rs_svd_fit(rs_ctx* ctx, const rs_ratings* r, const rs_sgd_params*
         dbu.upload(hbu.data(), hbu.size(), s);
         dbi.upload(hbi.data(), hbi.size(), s);
         dgb.upload(gb, 1, s);
+        rs::kernel_span_begin(ctx);
         if (nnz > 0 && p->n_epochs > 0)
             rs::launch_ordered(nnz, du.p, di.p, dr.p, dP.p, dQ.p, dbu.p, dbi.p, ld, dgb.p,
                                p->n_epochs, lr, reg, s);
+        rs::kernel_span_end(ctx);
         dP.download(hP.data(), hP.size(), s);
         dQ.download(hQ.data(), hQ.size(), s);
         dbu.download(hbu.data(), hbu.size(), s);

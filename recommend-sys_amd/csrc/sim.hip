@@ -327,6 +327,8 @@ static void sims_device(rs_ctx* ctx, int32_t kind, int32_t L, int32_t R, const S
         hipLaunchKernelGGL(knn_scatter_kernel, dim3(L), dim3(256), 0, s, L, drow.p, dids.p, dx.p,
                            ldk, X.p, X2.p, M.p);
         RS_HIP(hipGetLastError());
+        RS_HIP(hipStreamSynchronize(s));
+        kernel_span_begin(ctx);
         const int32_t T = static_cast<int32_t>(Lp / kTile);
         const int64_t n_tiles = static_cast<int64_t>(T) * (T + 1) / 2;
         const double inv_s2 = 1.0 / static_cast<double>(scale * scale);
@@ -337,7 +339,7 @@ static void sims_device(rs_ctx* ctx, int32_t kind, int32_t L, int32_t R, const S
             hipLaunchKernelGGL(knn_sims_mfma_kernel<1>, dim3(n_tiles), dim3(256), 0, s, X.p, X2.p,
                                M.p, ldk, L, inv_s2, dS.p);
         RS_HIP(hipGetLastError());
-        RS_HIP(hipStreamSynchronize(s));
+        kernel_span_end(ctx);
         return;
     }
     DevBuf<double> dr(std::max<int64_t>(1, nnz)), dmean(L);
@@ -348,6 +350,8 @@ static void sims_device(rs_ctx* ctx, int32_t kind, int32_t L, int32_t R, const S
     DevBuf<double> scratch(static_cast<int64_t>(std::max(1, R)) * grid);
     DevBuf<uint8_t> scratch_has(static_cast<int64_t>(std::max(1, R)) * grid);
     RS_HIP(hipMemsetAsync(scratch_has.p, 0, scratch_has.n, s));
+    RS_HIP(hipStreamSynchronize(s));
+    kernel_span_begin(ctx);
     if (kind == RS_SIM_COSINE)
         hipLaunchKernelGGL(sims_merge_kernel<0>, dim3(grid), dim3(256), 0, s, L, R, drow.p, dids.p, dr.p, dmean.p, scratch.p, scratch_has.p, dS.p);
     else if (kind == RS_SIM_MSD)
@@ -355,7 +359,7 @@ static void sims_device(rs_ctx* ctx, int32_t kind, int32_t L, int32_t R, const S
     else
         hipLaunchKernelGGL(sims_merge_kernel<2>, dim3(grid), dim3(256), 0, s, L, R, drow.p, dids.p, dr.p, dmean.p, scratch.p, scratch_has.p, dS.p);
     RS_HIP(hipGetLastError());
-    RS_HIP(hipStreamSynchronize(s));
+    kernel_span_end(ctx);
 }
 
 }  // namespace rs

@@ -355,6 +355,7 @@ extern "C" int rs_svdpp_fit(rs_ctx* ctx, const rs_ratings* r, const rs_sgd_param
             dY.upload(hY.data(), hY.size(), s);
             dbu.upload(hbu.data(), hbu.size(), s);
             dbi.upload(hbi.data(), hbi.size(), s);
+            rs::kernel_span_begin(ctx);
             if (nnz > 0 && p->n_epochs > 0) {
                 if (k <= 256)
                     hipLaunchKernelGGL((rs::svdpp_ordered_kernel<256>), dim3(1), dim3(256), 0, s, nnz, du.p, di.p, dr.p, drow.p, dcol.p, dP.p, dQ.p, dY.p, dbu.p, dbi.p, k, dgb.p, p->n_epochs, lr, reg);
@@ -362,6 +363,7 @@ extern "C" int rs_svdpp_fit(rs_ctx* ctx, const rs_ratings* r, const rs_sgd_param
                     hipLaunchKernelGGL((rs::svdpp_ordered_kernel<512>), dim3(1), dim3(512), 0, s, nnz, du.p, di.p, dr.p, drow.p, dcol.p, dP.p, dQ.p, dY.p, dbu.p, dbi.p, k, dgb.p, p->n_epochs, lr, reg);
                 RS_HIP(hipGetLastError());
             }
+            rs::kernel_span_end(ctx);
             dP.download(hP.data(), hP.size(), s);
             dQ.download(hQ.data(), hQ.size(), s);
             dY.download(hY.data(), hY.size(), s);
@@ -405,6 +407,8 @@ extern "C" int rs_svdpp_fit(rs_ctx* ctx, const rs_ratings* r, const rs_sgd_param
         dQ.upload(hQ.data(), hQ.size(), s);
         dY.upload(hY.data(), hY.size(), s);
         const double inv_nnz = r->nnz > 0 ? 1.0 / static_cast<double>(r->nnz) : 0.0;
+        RS_HIP(hipStreamSynchronize(s));
+        rs::kernel_span_begin(ctx);
         for (int32_t ep = 0; ep < p->n_epochs; ++ep) {
             switch (E) {
                 case 1: rs::launch_pp_fast<1>(n_blocks, dwork, n_work, drow, dcol, dval, dP, dQ, dY, dgb, dpart, lr, reg, s); break;
@@ -421,6 +425,7 @@ extern "C" int rs_svdpp_fit(rs_ctx* ctx, const rs_ratings* r, const rs_sgd_param
                                static_cast<int64_t>(n_blocks), dgb.p, inv_nnz);
             RS_HIP(hipGetLastError());
         }
+        rs::kernel_span_end(ctx);
         dP.download(hP.data(), hP.size(), s);
         dQ.download(hQ.data(), hQ.size(), s);
         dY.download(hY.data(), hY.size(), s);

@@ -24,6 +24,7 @@ SIM_COSINE, SIM_MSD, SIM_PEARSON = 0, 1, 2
 
 HEADER_SYMBOLS = (
     "rs_version", "rs_device_count", "rs_open", "rs_close", "rs_last_error", "rs_synchronize",
+    "rs_last_kernel_ms",
     "rs_svd_fit", "rs_svd_predict", "rs_svdpp_fit", "rs_nmf_fit", "rs_baseline_fit",
     "rs_knn_sims", "rs_sim_pair", "rs_svd_plan_create", "rs_svd_plan_destroy",
     "rs_svd_plan_upload", "rs_svd_plan_download", "rs_svd_plan_epochs",
@@ -68,6 +69,7 @@ def lib():
             "rs_close": (None, [_vp]),
             "rs_last_error": (C.c_char_p, [_vp]),
             "rs_synchronize": (C.c_int, [_vp]),
+            "rs_last_kernel_ms": (C.c_int, [_vp, C.POINTER(_dbl)]),
             "rs_svd_fit": (C.c_int, [_vp, C.POINTER(_Ratings), C.POINTER(_SgdParams), _vp, _vp,
                                      _vp, _vp, _vp]),
             "rs_svd_predict": (C.c_int, [_vp, _i64, _vp, _vp, _i32, _i32, _i32, _vp, _vp, _vp,
@@ -165,6 +167,12 @@ class Context:
 
     def check(self, code):
         _check(code, self.h)
+
+    def last_kernel_ms(self) -> float:
+        """Device time of the kernels of the last estimator call on this context."""
+        ms = _dbl(0)
+        self.check(lib().rs_last_kernel_ms(self.h, C.byref(ms)))
+        return ms.value
 
     # ---- estimators --------------------------------------------------------------------------
 

@@ -101,3 +101,50 @@ def small_like(n_users, n_items, nnz, seed=1, min_deg=5, hist=None):
     ratings = _planted_ratings(rng, users, items, n_users, n_items, hist)
     perm = rng.permutation(nnz)
     return users[perm].astype(np.int32), items[perm].astype(np.int32), ratings[perm], n_users, n_items
+
+
+# Published ML-20M half-star histogram (0.5 .. 5.0), recalled from the MovieLens-20M README era
+# statistics -- the file is not in the reference snapshot, so treat these counts as approximate.
+ML20M_HIST = (239125, 680732, 279252, 1430997, 883398, 4291193, 2200156, 5561926, 1534824, 2898660)
+
+
+def _zipf_items(rng, n, n_items, s, item_of_rank):
+    ranks = np.arange(1, n_items + 1, dtype=np.float64)
+    cdf = np.cumsum(ranks ** -s)
+    cdf /= cdf[-1]
+    return item_of_rank[np.searchsorted(cdf, rng.random(n), side="right").clip(0, n_items - 1)]
+
+
+def ml20m_like(seed: int = 20250825, scale: float = 1.0):
+    """U=138,493, I=26,744, nnz=20,000,263 (x scale on users and nnz); >=20 ratings per user;
+    Zipf(1.0) item popularity over permuted ids; no duplicate (u, i); half-star ratings from user and
+    item biases plus noise, quantile-mapped to ML20M_HIST.  Returns (users, items, ratings, U, I)."""
+    rng = np.random.default_rng(seed)
+    n_users = int(round(138493 * scale))
+    n_items = 26744
+    nnz = int(round(sum(ML20M_HIST) * scale))
+    deg = _degrees(rng, n_users, nnz, 20, 9254)
+    item_of_rank = rng.permutation(n_items)
+    users = np.repeat(np.arange(n_users, dtype=np.int64), deg)
+    items = _zipf_items(rng, nnz, n_items, 1.0, item_of_rank).astype(np.int64)
+    for _ in range(30):  # resolve duplicate (u, i): redraw the later copies (uniformly after 10 rounds)
+        key = users * n_items + items
+        order = np.argsort(key, kind="stable")
+        dup = np.zeros(nnz, bool)
+        dup[order[1:]] = key[order[1:]] == key[order[:-1]]
+        nd = int(dup.sum())
+        if nd == 0:
+            break
+        items[dup] = (_zipf_items(rng, nd, n_items, 1.0, item_of_rank) if _ < 10
+                      else rng.integers(0, n_items, nd))
+    hist = np.array(ML20M_HIST, np.float64)
+    hist = np.floor(hist / hist.sum() * nnz).astype(np.int64)
+    hist[-4] += nnz - hist.sum()
+    score = rng.normal(0, 0.5, n_users)[users] + rng.normal(0, 0.5, n_items)[items] + rng.normal(0, 0.7, nnz)
+    order = np.argsort(score, kind="stable")
+    r = np.empty(nnz)
+    cut = np.concatenate([[0], np.cumsum(hist)])
+    for lvl in range(len(hist)):
+        r[order[cut[lvl]:cut[lvl + 1]]] = 0.5 * (lvl + 1)
+    perm = rng.permutation(nnz)
+    return users[perm].astype(np.int32), items[perm].astype(np.int32), r[perm], n_users, n_items

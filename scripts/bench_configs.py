@@ -1,0 +1,161 @@
+#!/usr/bin/env python3
+"""Measures the BASELINE.json configurations that bench.py does not cover (bench.py = configs[1]):
+
+  config 3  SVD++ nFactors=128 on an ML-1M-shaped set (FAST lazy-y kernel K2)
+  config 4  KNN item-based Cosine on an ML-20M-shaped set (int8-MFMA K4)
+  extra     NMF nFactors=15 on the ML-1M-shaped set (K3; no BASELINE config)
+
+Each line: kernel-only device time (HIP events on the launch stream, rs_last_kernel_ms), the
+roofline fraction against the bound SURVEY §8d names, and a CPU baseline timed on this host on a
+bounded sample of the same workload (the oracle: C fp64 restatement of the reference, 1 thread).
+Writes JSON lines to stdout (and --out).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [os.path.join(REPO, "recommend-sys_amd"), os.path.join(REPO, "oracle")]
+
+HBM_PEAK = 8000.0      # GB/s, MI355X_MICROARCH.md chip table
+I8_PEAK = 5000.0       # dense int8 MFMA TOP/s: 2x the ~2.5 PF dense bf16 rate (microarch: i8 2x bf16)
+
+
+def emit(d, out):
+    line = json.dumps(d)
+    print(line, flush=True)
+    if out:
+        with open(out, "a") as f:
+            f.write(line + "\n")
+
+
+def config3(ctx, out, epochs=5):
+    import oracle as O
+    import rsgpu
+    from rsgpu import synth
+    u, i, r, nu, ni = synth.ml1m_like()
+    k = 128
+    rng = np.random.default_rng(3)
+    P0, Q0, Y0 = (rng.normal(0, 0.1, (m, k)) for m in (nu, ni, ni))
+    R = rsgpu.Ratings(u, i, r, nu, ni)
+    ctx.svdpp_fit(R, P0, Q0, Y0, n_epochs=1)            # warm-up (code objects, allocator)
+    t0 = time.perf_counter()
+    ctx.svdpp_fit(R, P0, Q0, Y0, n_epochs=epochs)
+    wall = time.perf_counter() - t0
+    ms = ctx.last_kernel_ms() / epochs
+    nnz = len(r)
+    ab = nnz * (16 + 8 * k) + nu * (16 + 8 * k) + nnz * (4 + 12 * k)
+    # CPU: literal svd.go:316-427 restatement on the first 3000 ratings (cost per rating depends on
+    # |N(u)| of the rated user; the shuffled prefix is a uniform sample), extrapolated to an epoch
+    m = 3000
+    t0 = time.perf_counter()
+    O.svdpp_fit(u[:m], i[:m], r[:m], nu, P0, Q0, Y0, epochs=1)
+    # the prefix's N(u) are the prefix's own ratings: rescale by the full-set |N(u)| ratio
+    deg_full = np.bincount(u, minlength=nu)[u[:m]].mean()
+    deg_pref = np.bincount(u[:m], minlength=nu)[u[:m]].mean()
+    t_rating = (time.perf_counter() - t0) / m * (deg_full / deg_pref)
+    emit({"config": "SVD++ nFactors=128 ML-1M-shaped (BASELINE configs[2])", "kernel": "svdpp_epoch_fast_kernel<E=3,D=8>",
+          "updates_per_s": nnz / (ms / 1e3), "epoch_ms_kernel": ms, "fit_wall_s": wall,
+          "roofline": {"bound": "hbm", "achieved_GBs": ab / (ms / 1e3) / 1e9, "peak_GBs": HBM_PEAK,
+                       "frac": ab / (ms / 1e3) / 1e9 / HBM_PEAK, "algorithmic_bytes": ab},
+          "cpu_baseline": {"value": 1.0 / t_rating, "unit": "updates/s", "cores": 1, "kind": "port",
+                           "sample": f"literal svd.go:352-424 restatement, {m} ratings, cost scaled to "
+                                     f"full-set |N(u)| (x{deg_full / deg_pref:.1f})"}}, out)
+
+
+def config4(ctx, out):
+    import oracle as O
+    import rsgpu
+    from rsgpu import synth
+    u, i, r, nu, ni = synth.ml20m_like()
+    order = np.argsort(i, kind="stable")
+    rowptr = np.zeros(ni + 1, np.int64)
+    np.add.at(rowptr, i.astype(np.int64) + 1, 1)
+    rowptr = np.cumsum(rowptr)
+    ids, rr = u[order], r[order]
+    L, R = ni, nu
+    t0 = time.perf_counter()
+    S = ctx.knn_sims(rsgpu.SIM_COSINE, rowptr, ids, rr, R)
+    wall = time.perf_counter() - t0
+    ms = ctx.last_kernel_ms()
+    Lp = (L + 127) // 128 * 128
+    T = Lp // 128
+    kpad = (R + 63) // 64 * 64
+    executed = 3 * 2 * (T * (T + 1) // 2) * 128 * 128 * kpad     # 3 int8 contractions, triangle tiles
+    algorithmic = 2 * 2 * L * (L + 1) // 2 * R                    # G=2, unique pairs
+    # CPU: the reference-style merge (sim.go:10-25) for rows [0, 64) against every partner,
+    # extrapolated to the unique pairs of the full matrix (knn.go skips computed mirrors)
+    srt = np.lexsort((ids, np.repeat(np.arange(L), np.diff(rowptr))))
+    sid, sr = ids[srt], rr[srt]
+    rows = 64
+    t0 = time.perf_counter()
+    blk = O.knn_sims_rows(O.COSINE, rowptr, sid, sr, 0, rows)
+    t_blk = time.perf_counter() - t0
+    t_full = t_blk * (L / rows) / 2
+    same = np.array_equal(np.isnan(blk), np.isnan(S[:rows])) and np.array_equal(
+        blk[~np.isnan(blk)].view(np.uint64), S[:rows][~np.isnan(blk)].view(np.uint64))
+    emit({"config": "KNN item-based Cosine ML-20M-shaped (BASELINE configs[3])",
+          "kernel": "knn_sims_mfma_kernel<Cosine> (v_mfma_i32_32x32x32_i8)",
+          "L": L, "R": R, "nnz": int(len(r)), "kernel_ms": ms, "fit_wall_s": wall,
+          "pairs_per_s": L * (L - 1) / 2 / (ms / 1e3),
+          "roofline": {"bound": "mfma", "achieved_TOPs_executed": executed / (ms / 1e3) / 1e12,
+                       "achieved_TOPs_algorithmic": algorithmic / (ms / 1e3) / 1e12,
+                       "peak_TOPs": I8_PEAK, "frac": executed / (ms / 1e3) / 1e12 / I8_PEAK,
+                       "executed_int8_ops": executed, "algorithmic_int8_ops": algorithmic},
+          "parity_rows_0_63_bitwise": bool(same),
+          "cpu_baseline": {"value": L * (L - 1) / 2 / t_full, "unit": "pairs/s", "cores": 1,
+                           "kind": "port", "sample": f"rows 0-{rows - 1} x {L} partners, merge "
+                           f"restatement {t_blk:.1f} s, extrapolated x{L / rows / 2:.0f} to the "
+                           f"unique pairs ({t_full:.0f} s)"}}, out)
+
+
+def nmf(ctx, out, epochs=50):
+    import oracle as O
+    import rsgpu
+    from rsgpu import synth
+    u, i, r, nu, ni = synth.ml1m_like()
+    k = 15
+    rng = np.random.default_rng(5)
+    P0, Q0 = rng.uniform(0, 1, (nu, k)), rng.uniform(0, 1, (ni, k))
+    R = rsgpu.Ratings(u, i, r, nu, ni)
+    ctx.nmf_fit(R, P0, Q0, n_epochs=1, as_written=False)
+    ctx.nmf_fit(R, P0, Q0, n_epochs=epochs, as_written=False)
+    ms = ctx.last_kernel_ms() / epochs
+    nnz = len(r)
+    ab = nnz * (8 + 20 * k) + nu * 28 * k + ni * 24 * k
+    t0 = time.perf_counter()
+    O.nmf_fit(u, i, r, P0, Q0, epochs=1, as_written=False)
+    t_cpu = time.perf_counter() - t0
+    emit({"config": "NMF nFactors=15 ML-1M-shaped (no BASELINE config)", "kernel": "nmf_pass_kernel x2",
+          "updates_per_s": nnz / (ms / 1e3), "epoch_ms_kernel": ms,
+          "roofline": {"bound": "hbm", "achieved_GBs": ab / (ms / 1e3) / 1e9, "peak_GBs": HBM_PEAK,
+                       "frac": ab / (ms / 1e3) / 1e9 / HBM_PEAK, "algorithmic_bytes": ab},
+          "cpu_baseline": {"value": nnz / t_cpu, "unit": "updates/s", "cores": 1, "kind": "port",
+                           "sample": "1 epoch, svd.go:178-250 restatement"}}, out)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--only", default="3,4,nmf")
+    ap.add_argument("--out", default="")
+    a = ap.parse_args()
+    import rsgpu
+    ctx = rsgpu.Context(0)
+    which = a.only.split(",")
+    if "3" in which:
+        config3(ctx, a.out)
+    if "nmf" in which:
+        nmf(ctx, a.out)
+    if "4" in which:
+        config4(ctx, a.out)
+    ctx.close()
+
+
+if __name__ == "__main__":
+    main()
