@@ -1,0 +1,170 @@
+// core_test.cpp -- the reference's own Go tests for the hot path, restated against the C++ host
+// mirror (core.hpp) over the C-ABI:
+//   sim_test.go:9-60   TestCosine / TestMSD / TestPearson (epsilon 0.01)
+//   base_test.go:8-64  Evaluate(): 5-fold CrossValidate, mean RMSE/MAE <= expected + 0.008 for SVD,
+//                      NMF, KNN, KNNWithMean, KNNWithZScore, KNNBaseLine (+ the commented-out SVD++)
+//   eval_test.go       RMSE/MAE on fixed predictions
+// plus host-only checks of the Go semantics the mirror restates (Parameters panics, first-appearance
+// inner ids, KFold partition, the float loader, the ignored KNN type of Q9).
+//
+// usage: core_test [--cpu-only] <ml-100k u.data path>
+//   --cpu-only runs only the host tests (no device is opened).
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <functional>
+#include <numeric>
+#include <set>
+#include <string>
+#include <vector>
+
+#include "core.hpp"
+
+using namespace core;
+
+static int g_failed = 0, g_run = 0;
+
+#define CHECK(cond)                                                                   \
+    do {                                                                              \
+        if (!(cond)) throw std::runtime_error(std::string("check failed: ") + #cond); \
+    } while (0)
+
+static void run(const char* name, const std::function<void()>& fn) {
+    ++g_run;
+    try {
+        fn();
+        std::printf("PASS %s\n", name);
+    } catch (const std::exception& e) {
+        ++g_failed;
+        std::printf("FAIL %s: %s\n", name, e.what());
+    }
+    std::fflush(stdout);
+}
+
+static std::vector<IDRating> kat_a() { return {{1, 4}, {2, 5}, {3, 6}}; }
+static std::vector<IDRating> kat_b() { return {{0, 0}, {1, 1}, {2, 2}}; }
+
+// base_test.go:8-24
+static void evaluate(const Estimator& algo, const DataSet& data, double expectRMSE, double expectMAE,
+                     const Parameters& params = {}) {
+    const double eps = 0.008;
+    auto res = CrossValidate(algo, data, {RMSE, MAE}, 5, 0, params);
+    const double rmse = std::accumulate(res[0].Tests.begin(), res[0].Tests.end(), 0.0) / 5;
+    const double mae = std::accumulate(res[1].Tests.begin(), res[1].Tests.end(), 0.0) / 5;
+    std::printf("     RMSE %.4f (<= %.3f)  MAE %.4f (<= %.3f)\n", rmse, expectRMSE + eps, mae,
+                expectMAE + eps);
+    if (!(rmse <= expectRMSE + eps)) throw std::runtime_error("RMSE " + std::to_string(rmse));
+    if (!(mae <= expectMAE + eps)) throw std::runtime_error("MAE " + std::to_string(mae));
+}
+
+int main(int argc, char** argv) {
+    bool cpu_only = false;
+    const char* path = nullptr;
+    for (int a = 1; a < argc; ++a) {
+        if (!std::strcmp(argv[a], "--cpu-only")) cpu_only = true;
+        else path = argv[a];
+    }
+    if (!path) {
+        std::fprintf(stderr, "usage: core_test [--cpu-only] <u.data>\n");
+        return 2;
+    }
+    DataSet data = LoadDataFromFile(path, "\t");
+
+    // ---- host-only ---------------------------------------------------------------------------
+    run("TestLoadDataFromFile", [&] {
+        CHECK(data.Length() == 100000);
+        std::set<int64_t> u(data.Users.begin(), data.Users.end()), i(data.Items.begin(), data.Items.end());
+        CHECK(u.size() == 943 && i.size() == 1682);
+    });
+    run("TestParametersPanic", [] {
+        Parameters p{{"nFactors", 10}, {"lr", 0.01}, {"sim", Sim::Pearson}};
+        CHECK(p.GetInt("nFactors", 1) == 10 && p.GetFloat64("lr", 0) == 0.01);
+        CHECK(p.GetSim("sim", Sim::MSD) == Sim::Pearson && p.GetInt("missing", 7) == 7);
+        bool threw = false;
+        try {
+            p.GetInt("lr", 0);  // base.go:26-30: value.(int) on a float64 panics
+        } catch (const Panic&) {
+            threw = true;
+        }
+        CHECK(threw);
+    });
+    run("TestTrainSetFirstAppearance", [] {
+        DataSet d;
+        d.Users = {50, 7, 50, 9};
+        d.Items = {3, 3, 8, 1};
+        d.Ratings = {1, 2, 3, 4};
+        TrainSet t = NewTrainSet(d);
+        CHECK(t.UserCount == 3 && t.ItemCount == 3);
+        CHECK(t.ConvertUserID(50) == 0 && t.ConvertUserID(7) == 1 && t.ConvertUserID(9) == 2);
+        CHECK(t.ConvertItemID(3) == 0 && t.ConvertItemID(8) == 1 && t.ConvertItemID(1) == 2);
+        CHECK(t.ConvertUserID(1234) == newID && t.GlobalMean == 2.5);
+        CHECK(t.UserRatings()[0].size() == 2 && t.UserRatings()[0][1].ID == 1);
+        CHECK(t.ItemRatings()[0][1].ID == 1 && t.ItemRatings()[0][1].Rating == 2);
+    });
+    run("TestKFoldPartition", [&] {
+        std::vector<int64_t> perm(data.Length());
+        std::iota(perm.rbegin(), perm.rend(), 0);
+        std::vector<TrainSet> trains;
+        std::vector<DataSet> tests;
+        data.KFold(3, perm, trains, tests);
+        CHECK(trains.size() == 3 && tests[0].Length() == 33334 && tests[1].Length() == 33333);
+        int64_t total = 0;
+        for (int f = 0; f < 3; ++f) {
+            CHECK(trains[f].Length() + tests[f].Length() == data.Length());
+            total += tests[f].Length();
+        }
+        CHECK(total == data.Length());
+        CHECK(tests[0].Users[0] == data.Users[data.Length() - 1]);
+    });
+    run("TestKNNTypeIgnoresParams", [] {  // knn.go:131-154 (Q9)
+        auto k = NewKNN({{"type", std::string("zscore")}});
+        CHECK(k->KNNType == "basic" && NewKNNBaseLine()->KNNType == "baseline");
+    });
+    run("TestRMSE_MAE", [] {  // eval_test.go: predictions {-2, 0, 2} against 0
+        struct Fixed : Estimator {
+            double Predict(int64_t u, int64_t) override { return static_cast<double>(u); }
+            void Fit(const TrainSet&) override {}
+            std::unique_ptr<Estimator> Clone() const override { return std::make_unique<Fixed>(*this); }
+        } e;
+        DataSet t;
+        t.Users = {-2, 0, 2};
+        t.Items = {0, 0, 0};
+        t.Ratings = {0, 0, 0};
+        CHECK(std::fabs(RMSE(e, t) - 1.63299) < 1e-5 && std::fabs(MAE(e, t) - 1.33333) < 1e-5);
+    });
+    if (cpu_only) {
+        std::printf("%d/%d passed\n", g_run - g_failed, g_run);
+        return g_failed ? 1 : 0;
+    }
+
+    // ---- device (sim_test.go, base_test.go) ----------------------------------------------------
+    const double epsilon = 0.01;
+    run("TestCosine", [&] { CHECK(std::fabs(Cosine(kat_a(), kat_b()) - 0.978) <= epsilon); });
+    run("TestMSD", [&] { CHECK(std::fabs(MSD(kat_a(), kat_b()) - 0.1) <= epsilon); });
+    run("TestPearson", [&] { CHECK(std::fabs(Pearson(kat_a(), kat_b())) <= epsilon); });
+    run("TestSVD", [&] { evaluate(*NewSVD(), data, 0.934, 0.737); });
+    // base_test.go:38-40 is commented out upstream; its bound holds for the FAST kernel.
+    run("TestSVDPP", [&] { evaluate(*NewSVDpp(), data, 0.92, 0.722); });
+    // svd.go:243-249 as written diverges (Q5); the bound holds for the intended update.
+    run("TestNMF", [&] { evaluate(*NewNMF(), data, 0.963, 0.758, {{"asWritten", false}}); });
+    run("TestKNN", [&] { evaluate(*NewKNN(), data, 0.98, 0.774); });
+    run("TestKNNWithMean", [&] { evaluate(*NewKNNWithMean(), data, 0.951, 0.749); });
+    run("TestNewKNNZScore", [&] { evaluate(*NewKNNWithZScore(), data, 0.951, 0.746); });
+    run("TestKNNBaseLine", [&] { evaluate(*NewKNNBaseLine(), data, 0.931, 0.733); });
+    run("TestSVDOrderedMatchesPredict", [&] {
+        // ORDERED is the reference's own visit order; Predict must reproduce svd.go:32-51 on it.
+        TrainSet t = NewTrainSet(data.SubSet([&] {
+            std::vector<int64_t> idx(2000);
+            std::iota(idx.begin(), idx.end(), 0);
+            return idx;
+        }()));
+        auto s = NewSVD({{"mode", std::string("ordered")}, {"seed", 3}, {"nEpochs", 2}, {"nFactors", 8}});
+        s->Fit(t);
+        const double p = s->Predict(data.Users[0], data.Items[0]);
+        double want = s->GlobalBias + s->UserBias[0] + s->ItemBias[0];
+        for (int f = 0; f < 8; ++f) want += s->UserFactor[0][f] * s->ItemFactor[0][f];
+        CHECK(p == want && s->Predict(-5, data.Items[0]) == s->GlobalBias + s->ItemBias[0]);
+    });
+    std::printf("%d/%d passed\n", g_run - g_failed, g_run);
+    return g_failed ? 1 : 0;
+}

@@ -73,5 +73,39 @@ def build(verbose: bool = False, jobs: int = 8) -> str:
     return LIB
 
 
+HOST = os.path.join(ROOT, "host")
+HOST_LIB = os.path.join(HOST, "librscore.so")
+HOST_TEST = os.path.join(HOST, "tests", "core_test")
+CXX = os.environ.get("CXX", "g++")
+
+
+def build_host(verbose: bool = False) -> str:
+    """C++ mirror of the Go core API (host/core.cpp) -> host/librscore.so linked against
+    librsgpu.so, and its test binary host/tests/core_test.  rpath $ORIGIN-relative, so both run
+    from the snapshot on the GPU box."""
+    lib = build(verbose)
+    flags = ["-O2", "-std=c++17", "-fPIC", "-Wall", "-Wextra", f"-I{INCLUDE}", f"-I{HOST}"]
+    steps = [
+        ([os.path.join(HOST, "core.cpp")], HOST_LIB,
+         ["-shared", f"-L{PKG_DIR}", "-lrsgpu", "-Wl,-rpath,$ORIGIN/../rsgpu"]),
+        ([os.path.join(HOST, "tests", "core_test.cpp")], HOST_TEST,
+         [f"-L{HOST}", "-lrscore", f"-L{PKG_DIR}", "-lrsgpu",
+          "-Wl,-rpath,$ORIGIN/..", "-Wl,-rpath,$ORIGIN/../../rsgpu"]),
+    ]
+    deps = [os.path.join(HOST, "core.hpp"), os.path.join(INCLUDE, "rsgpu.h"), lib]
+    for srcs, out, extra in steps:
+        newest = max(os.path.getmtime(p) for p in srcs + deps)
+        if os.path.exists(out) and os.path.getmtime(out) >= newest:
+            continue
+        r = subprocess.run([CXX] + flags + srcs + ["-o", out] + extra, capture_output=True, text=True)
+        if r.returncode != 0:
+            raise RuntimeError(f"{CXX} failed for {srcs[0]}:\n{r.stderr}")
+        if verbose:
+            print(f"built {out}")
+        deps.append(out)
+    return HOST_LIB
+
+
 if __name__ == "__main__":
     print(build(verbose=True))
+    print(build_host(verbose=True))
