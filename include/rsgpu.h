@@ -10,11 +10,11 @@
  *   rs_svd_fit        <- core/svd.go:63-132    (*SVD).Fit            (per-epoch SGD, K1)
  *   rs_svdpp_fit      <- core/svd.go:316-427   (*SVDPP).Fit          (K2)
  *   rs_nmf_fit        <- core/svd.go:158-251   (*NMF).Fit            (K3)
- *   rs_knn_sims       <- core/knn.go:224-298   (*KNN).Fit pair loop  (K4 Cosine/MSD, K5 Pearson)
+ *   rs_knn_sims       <- core/knn.go:143-217   (*KNN).Fit pair loop  (K4 Cosine/MSD, K5 Pearson)
  *                        with core/sim.go:10-81 Cosine / MSD / Pearson as the pair function
  *   rs_sim_pair       <- core/sim.go:7-81      Sim func(a, b SortedIdRatings) float64
  *   rs_svd_predict    <- core/svd.go:32-51     (*SVD).Predict (batched; next-row §8f)
- *   rs_baseline_fit   <- core/base.go:433-461  (*BaseLine).Fit (used by KNN-baseline knn.go:260)
+ *   rs_baseline_fit   <- core/base.go:135-163  (*BaseLine).Fit (used by KNN-baseline knn.go:179)
  *
  * Conventions
  *   - Ratings arrive as the TrainSet's COO triples (core/data.go:109-127) in TRAIN-SET ORDER with
@@ -114,12 +114,12 @@ int rs_svdpp_fit(rs_ctx* ctx, const rs_ratings* r, const rs_sgd_params* p, doubl
 int rs_nmf_fit(rs_ctx* ctx, const rs_ratings* r, int32_t n_factors, int32_t n_epochs, double reg,
                int32_t as_written, double* P, double* Q);
 
-/* core/base.go:433-461 BaseLine.Fit (bias-only SGD, ORDERED semantics). */
+/* core/base.go:135-163 BaseLine.Fit (bias-only SGD, ORDERED semantics). */
 int rs_baseline_fit(rs_ctx* ctx, const rs_ratings* r, int32_t n_epochs, double lr, double reg,
                     double* bu, double* bi, double* gb);
 
-/* core/knn.go:224-298 pair loop: sims (n_left x n_left, row-major float64) = sim(left_a, left_b)
- * over the co-rated right ids, NaN where nothing is co-rated and on the diagonal (knn.go:238,283).
+/* core/knn.go:143-217 pair loop: sims (n_left x n_left, row-major float64) = sim(left_a, left_b)
+ * over the co-rated right ids, NaN where nothing is co-rated and on the diagonal (knn.go:157,283).
  * Rows are CSR (rowptr[n_left+1], ids in [0, n_right), ratings) in any order within a row. */
 int rs_knn_sims(rs_ctx* ctx, int32_t kind, int32_t n_left, int32_t n_right, const int64_t* rowptr,
                 const int32_t* ids, const double* ratings, double* sims);

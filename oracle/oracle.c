@@ -446,15 +446,15 @@ void or_knn_sims(int32_t kind, int32_t L, const int64_t* rowptr, const int32_t* 
     }
     free(tmp);
     const int64_t LL = (int64_t)L * L;
-    for (int64_t t = 0; t < LL; t++) sims[t] = NAN;         /* knn.go:238/242 newNanMatrix */
-    for (int32_t a = 0; a < L; a++) {                       /* knn.go:280 (nJobs = 1) */
-        for (int32_t b = 0; b < L; b++) {                   /* knn.go:282 */
-            if (a == b) continue;                           /* knn.go:283: diagonal stays NaN */
-            if (!isnan(sims[(int64_t)a * L + b])) continue; /* knn.go:284 */
+    for (int64_t t = 0; t < LL; t++) sims[t] = NAN;         /* knn.go:157/161 newNanMatrix */
+    for (int32_t a = 0; a < L; a++) {                       /* knn.go:199 (nJobs = 1) */
+        for (int32_t b = 0; b < L; b++) {                   /* knn.go:201 */
+            if (a == b) continue;                           /* knn.go:202: diagonal stays NaN */
+            if (!isnan(sims[(int64_t)a * L + b])) continue; /* knn.go:203 */
             const double v = or_sim(kind, rowptr[a + 1] - rowptr[a], sid + rowptr[a],
                                     sr + rowptr[a], rowptr[b + 1] - rowptr[b], sid + rowptr[b],
                                     sr + rowptr[b]);
-            if (!isnan(v)) {                                /* knn.go:286-289 */
+            if (!isnan(v)) {                                /* knn.go:205-208 */
                 sims[(int64_t)a * L + b] = v;
                 sims[(int64_t)b * L + a] = v;
             }
@@ -489,7 +489,7 @@ static int cmp_cand(const void* x, const void* y) {
     const cand* a = (const cand*)x;
     const cand* b = (const cand*)y;
     const double sa = g_sim_row[a->id], sb = g_sim_row[b->id];
-    if (sa > sb) return -1;                                 /* knn.go:124-126: desc by sim */
+    if (sa > sb) return -1;                                 /* knn.go:43-45: desc by sim */
     if (sa < sb) return 1;
     return (a->pos > b->pos) - (a->pos < b->pos);           /* documented tie rule */
 }
@@ -508,13 +508,13 @@ void or_knn_predict(int32_t type, int32_t L, const double* sims, const int64_t* 
     cand* c = (cand*)malloc((size_t)maxdeg * sizeof(cand));
     for (int64_t x = 0; x < n; x++) {
         const int32_t li = left[x], ri = right[x];
-        if (li < 0 || ri < 0) {                             /* knn.go:170-172 */
+        if (li < 0 || ri < 0) {                             /* knn.go:89-91 */
             out[x] = global_mean;
             continue;
         }
         const double* srow = sims + (int64_t)li * L;
         int64_t nc = 0;
-        for (int64_t t = right_rowptr[ri]; t < right_rowptr[ri + 1]; t++) { /* knn.go:176-180 */
+        for (int64_t t = right_rowptr[ri]; t < right_rowptr[ri + 1]; t++) { /* knn.go:95-99 */
             if (!isnan(srow[right_ids[t]])) {
                 c[nc].id = right_ids[t];
                 c[nc].r = right_r[t];
@@ -522,15 +522,15 @@ void or_knn_predict(int32_t type, int32_t L, const double* sims, const int64_t* 
                 nc++;
             }
         }
-        if (nc <= min_k) {                                  /* knn.go:183-185 */
+        if (nc <= min_k) {                                  /* knn.go:102-104 */
             out[x] = global_mean;
             continue;
         }
         g_sim_row = srow;
-        qsort(c, (size_t)nc, sizeof(cand), cmp_cand);       /* knn.go:188-189 */
-        const int64_t nn = nc < k ? nc : k;                 /* knn.go:192-195 */
+        qsort(c, (size_t)nc, sizeof(cand), cmp_cand);       /* knn.go:107-108 */
+        const int64_t nn = nc < k ? nc : k;                 /* knn.go:111-114 */
         double weightSum = 0.0, weightRating = 0.0;
-        for (int64_t t = 0; t < nn; t++) {                  /* knn.go:199-211 */
+        for (int64_t t = 0; t < nn; t++) {                  /* knn.go:118-130 */
             weightSum += srow[c[t].id];
             double rating = c[t].r;
             if (type == 1) rating -= means[c[t].id];
@@ -538,7 +538,7 @@ void or_knn_predict(int32_t type, int32_t L, const double* sims, const int64_t* 
             else if (type == 3) rating -= bias[c[t].id];
             weightRating += srow[c[t].id] * rating;
         }
-        double prediction = weightRating / weightSum;       /* knn.go:212-220 */
+        double prediction = weightRating / weightSum;       /* knn.go:131-139 */
         if (type == 1) prediction += means[li];
         else if (type == 3) prediction += bias[li];
         else if (type == 2) {
@@ -553,15 +553,15 @@ void or_knn_predict(int32_t type, int32_t L, const double* sims, const int64_t* 
 void or_baseline_fit(int64_t n, const int32_t* u, const int32_t* i, const double* r,
                      int32_t epochs, double lr, double reg, double* bu, double* bi, double* gb) {
     double GB = *gb;
-    for (int32_t epoch = 0; epoch < epochs; epoch++) {      /* base.go:443 */
+    for (int32_t epoch = 0; epoch < epochs; epoch++) {      /* base.go:145 */
         for (int64_t t = 0; t < n; t++) {
             const int32_t uu = u[t], ii = i[t];
             const double userBias = bu[uu], itemBias = bi[ii];
-            double pred = GB;                               /* base.go:420-431 */
+            double pred = GB;                               /* base.go:122-133 */
             pred += bu[uu];
             pred += bi[ii];
             const double diff = pred - r[t];
-            GB -= lr * diff;                                /* base.go:456-458 */
+            GB -= lr * diff;                                /* base.go:158-160 */
             bu[uu] -= lr * (diff + reg * userBias);
             bi[ii] -= lr * (diff + reg * itemBias);
         }

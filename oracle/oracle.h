@@ -69,7 +69,7 @@ void or_nmf_predict(int64_t n, const int32_t* u, const int32_t* i, int32_t k,
 double or_sim(int32_t kind, int64_t na, const int32_t* a_id, const double* a_r,
               int64_t nb, const int32_t* b_id, const double* b_r);
 
-/* knn.go:270-297 (KNN.Fit pair loop) with nJobs = 1: Sims L x L, NaN where no co-rating, NaN
+/* knn.go:189-216 (KNN.Fit pair loop) with nJobs = 1: Sims L x L, NaN where no co-rating, NaN
  * diagonal.  Rows are given as CSR (rowptr int64[L+1], ids, ratings) in data order and sorted by
  * ID here (data.go:236-243 sorts). */
 void or_knn_sims(int32_t kind, int32_t L, const int64_t* rowptr, const int32_t* ids,
@@ -79,8 +79,8 @@ void or_knn_sims(int32_t kind, int32_t L, const int64_t* rowptr, const int32_t* 
 void or_knn_sims_rows(int32_t kind, int32_t L, const int64_t* rowptr, const int32_t* sorted_ids,
                       const double* sorted_r, int32_t row_begin, int32_t row_end, double* out);
 
-/* knn.go:156-222 KNN.Predict with ties broken by (sim desc, position asc) -- the reference uses
- * Go's unstable sort.Sort (knn.go:189), so tie order is the one documented deviation.
+/* knn.go:75-141 KNN.Predict with ties broken by (sim desc, position asc) -- the reference uses
+ * Go's unstable sort.Sort (knn.go:108), so tie order is the one documented deviation.
  * type: 0 basic, 1 centered, 2 zscore, 3 baseline.  right_* is RightRatings CSR in data order. */
 void or_knn_predict(int32_t type, int32_t L, const double* sims, const int64_t* right_rowptr,
                     const int32_t* right_ids, const double* right_r, const double* means,
@@ -88,7 +88,7 @@ void or_knn_predict(int32_t type, int32_t L, const double* sims, const int64_t* 
                     int32_t k, int32_t min_k, int64_t n, const int32_t* left, const int32_t* right,
                     double* out);
 
-/* base.go:433-461 BaseLine.Fit (bias-only SGD, used by KNN baseline knn.go:260-268). */
+/* base.go:135-163 BaseLine.Fit (bias-only SGD, used by KNN baseline knn.go:179-187). */
 void or_baseline_fit(int64_t n, const int32_t* u, const int32_t* i, const double* r,
                      int32_t epochs, double lr, double reg, double* bu, double* bi, double* gb);
 

@@ -1,5 +1,5 @@
-// baseline.hip -- BaseLine.Fit (reference core/base.go:433-461), used by KNN-baseline
-// (core/knn.go:260-268).  Bias-only SGD is one serial scalar chain (every rating updates the global
+// baseline.hip -- BaseLine.Fit (reference core/base.go:135-163), used by KNN-baseline
+// (core/knn.go:179-187).  Bias-only SGD is one serial scalar chain (every rating updates the global
 // bias, Q2), so the exact reference order is kept: one wave stages 64 (u, i, r) triples at a time
 // into LDS and lane 0 walks them in train-set order with the biases resident in LDS (float64,
 // -ffp-contract=off), bitwise equal to the fp64 restatement.
@@ -36,7 +36,7 @@ __global__ __launch_bounds__(64) void baseline_fit_kernel(int64_t nnz, const int
         __syncthreads();
     }
     double gb = gb_io[0];
-    for (int32_t epoch = 0; epoch < epochs; ++epoch) {              // base.go:443
+    for (int32_t epoch = 0; epoch < epochs; ++epoch) {              // base.go:145
         for (int64_t base = 0; base < nnz; base += 64) {
             if (base + lane < nnz) {
                 su[lane] = users[base + lane];
@@ -46,16 +46,16 @@ __global__ __launch_bounds__(64) void baseline_fit_kernel(int64_t nnz, const int
             __syncthreads();
             if (lane == 0) {
                 const int32_t m = static_cast<int32_t>(nnz - base < 64 ? nnz - base : 64);
-                for (int32_t t = 0; t < m; ++t) {                   // base.go:444
+                for (int32_t t = 0; t < m; ++t) {                   // base.go:146
                     const int32_t u = su[t], i = si[t];
-                    const double userBias = bu[u], itemBias = bi[i];  // base.go:448-449
-                    double pred = gb;                               // Predict base.go:424-431
+                    const double userBias = bu[u], itemBias = bi[i];  // base.go:150-151
+                    double pred = gb;                               // Predict base.go:126-133
                     pred += bu[u];
                     pred += bi[i];
-                    const double diff = pred - sr[t];               // base.go:451
-                    gb -= lr * diff;                                // base.go:456
-                    bu[u] -= lr * (diff + reg * userBias);          // base.go:457
-                    bi[i] -= lr * (diff + reg * itemBias);          // base.go:458
+                    const double diff = pred - sr[t];               // base.go:153
+                    gb -= lr * diff;                                // base.go:158
+                    bu[u] -= lr * (diff + reg * userBias);          // base.go:159
+                    bi[i] -= lr * (diff + reg * itemBias);          // base.go:160
                 }
             }
             __syncthreads();

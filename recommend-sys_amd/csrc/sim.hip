@@ -1,4 +1,4 @@
-// sim.hip -- K4 / K5: all-pairs similarity of KNN.Fit (reference core/knn.go:224-298 with
+// sim.hip -- K4 / K5: all-pairs similarity of KNN.Fit (reference core/knn.go:143-217 with
 // core/sim.go:10-81 as the pair function), gfx950.
 //
 // K4 (Cosine, MSD; bit-exact): when every rating is r = x / s with integer x, s in {1, 2} and
@@ -10,9 +10,9 @@
 //     Cosine  l / (sqrt(m) * sqrt(n))            (sim.go:24)
 //     MSD     1 / (sum / count + 1), sum = m + n - 2 l  (sim.go:43)
 // on the exactly-representable sums, so every similarity (and the NaN pattern: 0/0 where nothing
-// is co-rated, knn.go:286) is bitwise equal to the reference's sorted-merge result.
-// Only tiles of the upper triangle are computed; each writes S[a][b] and S[b][a] (knn.go:287-288)
-// and the diagonal stays NaN (knn.go:283).
+// is co-rated, knn.go:205) is bitwise equal to the reference's sorted-merge result.
+// Only tiles of the upper triangle are computed; each writes S[a][b] and S[b][a] (knn.go:206-207)
+// and the diagonal stays NaN (knn.go:202).
 //
 // K5 (Pearson, and Cosine/MSD when ratings are not of that form): one workgroup per left row a,
 // row a scattered densely into LDS (or a global scratch row), one thread per partner b > a walking
@@ -240,7 +240,7 @@ __global__ __launch_bounds__(256) void sims_merge_kernel(
         for (int32_t b = a + 1 + threadIdx.x; b < L; b += blockDim.x) {
             const double v = pair_sim<KIND>(dense, has, ma, rowptr[b], rowptr[b + 1], ids, r,
                                             KIND == 2 ? mean[b] : 0.0);
-            S[static_cast<int64_t>(a) * L + b] = v;  // NaN stays NaN (knn.go:286)
+            S[static_cast<int64_t>(a) * L + b] = v;  // NaN stays NaN (knn.go:205)
             S[static_cast<int64_t>(b) * L + a] = v;
         }
         __syncthreads();

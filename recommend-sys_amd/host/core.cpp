@@ -329,7 +329,7 @@ void NMF::Fit(const TrainSet& trainSet) {
 // KNN (knn.go)
 
 static std::unique_ptr<KNN> new_knn(const Parameters& params, const char* type) {
-    auto k = std::make_unique<KNN>(type);  // knn.go:131-154: the type ignores Params (Q9)
+    auto k = std::make_unique<KNN>(type);  // knn.go:50-73: the type ignores Params (Q9)
     k->Params = params;
     return k;
 }
@@ -338,7 +338,7 @@ std::unique_ptr<KNN> NewKNNWithMean(const Parameters& p) { return new_knn(p, "ce
 std::unique_ptr<KNN> NewKNNWithZScore(const Parameters& p) { return new_knn(p, "zscore"); }
 std::unique_ptr<KNN> NewKNNBaseLine(const Parameters& p) { return new_knn(p, "baseline"); }
 
-void KNN::Fit(const TrainSet& trainSet) {  // knn.go:224-298
+void KNN::Fit(const TrainSet& trainSet) {  // knn.go:143-217
     const Sim sim = Params.GetSim("sim", Sim::MSD);
     const bool userBased = Params.GetBool("userBased", true);
     Data = trainSet;
@@ -347,7 +347,7 @@ void KNN::Fit(const TrainSet& trainSet) {  // knn.go:224-298
     RightRatings = userBased ? Data.ItemRatings() : Data.UserRatings();
     L = static_cast<int>(LeftRatings.size());
     const int R = static_cast<int>(RightRatings.size());
-    if (KNNType == "centered" || KNNType == "zscore") {  // knn.go:245-247, data.go:222-235
+    if (KNNType == "centered" || KNNType == "zscore") {  // knn.go:164-166, data.go:222-235
         Means.assign(L, 0.0);
         for (int i = 0; i < L; ++i) {
             double sum = 0.0, count = 0.0;
@@ -358,7 +358,7 @@ void KNN::Fit(const TrainSet& trainSet) {  // knn.go:224-298
             Means[i] = sum / count;
         }
     }
-    if (KNNType == "zscore") {  // knn.go:248-258
+    if (KNNType == "zscore") {  // knn.go:167-177
         StdDevs.assign(L, 0.0);
         for (int i = 0; i < L; ++i) {
             double sum = 0.0, count = 0.0;
@@ -369,7 +369,7 @@ void KNN::Fit(const TrainSet& trainSet) {  // knn.go:224-298
             StdDevs[i] = std::sqrt(sum / count) + 1e-5;
         }
     }
-    if (KNNType == "baseline") {  // knn.go:260-268 -> base.go:433-461 with the KNN's Params
+    if (KNNType == "baseline") {  // knn.go:179-187 -> base.go:135-163 with the KNN's Params
         std::vector<double> bu(Data.UserCount, 0.0), bi(Data.ItemCount, 0.0), s;
         double gb = 0.0;
         rs_ratings r = Data.ratings_view(s);
@@ -394,7 +394,7 @@ void KNN::Fit(const TrainSet& trainSet) {  // knn.go:224-298
         panic_rs(context(), "KNN.Fit");
 }
 
-double KNN::Predict(int64_t userID, int64_t itemID) {  // knn.go:156-222
+double KNN::Predict(int64_t userID, int64_t itemID) {  // knn.go:75-141
     const int u = Data.ConvertUserID(userID), i = Data.ConvertItemID(itemID);
     const bool userBased = Params.GetBool("userBased", true);
     const int k = Params.GetInt("k", 40), minK = Params.GetInt("mink", 1);
@@ -405,7 +405,7 @@ double KNN::Predict(int64_t userID, int64_t itemID) {  // knn.go:156-222
     for (const IDRating& ir : RightRatings[right])
         if (!std::isnan(srow[ir.ID])) cand.push_back(ir);
     if (static_cast<int>(cand.size()) <= minK) return GlobalMean;
-    // knn.go:188-189 sort.Sort (Go's unstable pdqsort) by similarity descending; ties here keep
+    // knn.go:107-108 sort.Sort (Go's unstable pdqsort) by similarity descending; ties here keep
     // RightRatings order (stable) -- the one documented deviation of the host Predict.
     std::stable_sort(cand.begin(), cand.end(),
                      [&](const IDRating& a, const IDRating& b) { return srow[a.ID] > srow[b.ID]; });

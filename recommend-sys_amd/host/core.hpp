@@ -152,8 +152,8 @@ class NMF : public Estimator {
 };
 std::unique_ptr<NMF> NewNMF(const Parameters& params = {});
 
-// knn.go:17-298.  Parameters: sim (MSD), userBased (true), k (40), mink (1); the KNN type is the
-// constructor's default whatever Params says (Q9, knn.go:131-154).
+// knn.go:17-217.  Parameters: sim (MSD), userBased (true), k (40), mink (1); the KNN type is the
+// constructor's default whatever Params says (Q9, knn.go:50-73).
 class KNN : public Estimator {
    public:
     explicit KNN(std::string type) : KNNType(std::move(type)) {}

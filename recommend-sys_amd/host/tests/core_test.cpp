@@ -116,7 +116,7 @@ int main(int argc, char** argv) {
         CHECK(total == data.Length());
         CHECK(tests[0].Users[0] == data.Users[data.Length() - 1]);
     });
-    run("TestKNNTypeIgnoresParams", [] {  // knn.go:131-154 (Q9)
+    run("TestKNNTypeIgnoresParams", [] {  // knn.go:50-73 (Q9)
         auto k = NewKNN({{"type", std::string("zscore")}});
         CHECK(k->KNNType == "basic" && NewKNNBaseLine()->KNNType == "baseline");
     });

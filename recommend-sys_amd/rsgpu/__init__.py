@@ -215,7 +215,7 @@ class Context:
         return P, Q
 
     def baseline_fit(self, r: Ratings, n_epochs=20, lr=0.005, reg=0.02):
-        """core/base.go:433-461 BaseLine.Fit (exact reference order, float64)."""
+        """core/base.go:135-163 BaseLine.Fit (exact reference order, float64)."""
         bu, bi, g = np.zeros(r.n_users), np.zeros(r.n_items), np.zeros(1)
         rc = r.c()
         self.check(lib().rs_baseline_fit(self.h, C.byref(rc), n_epochs, lr, reg, _ptr(bu),
@@ -223,7 +223,7 @@ class Context:
         return bu, bi, float(g[0])
 
     def knn_sims(self, kind, rowptr, ids, ratings, n_right):
-        """core/knn.go:224-298 pair loop -> dense L x L float64 Sims (NaN = no co-rating)."""
+        """core/knn.go:143-217 pair loop -> dense L x L float64 Sims (NaN = no co-rating)."""
         rowptr = np.ascontiguousarray(rowptr, dtype=np.int64)
         ids = np.ascontiguousarray(ids, dtype=np.int32)
         ratings = np.ascontiguousarray(ratings, dtype=np.float64)

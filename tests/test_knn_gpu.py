@@ -1,6 +1,6 @@
 """GPU parity tests of K4 (int8-MFMA Cosine/MSD) and K5 (merge-order Pearson) through the C-ABI.
 
-P3: Sims bitwise equal to the oracle's restatement of core/knn.go:224-298 + core/sim.go (NaN
+P3: Sims bitwise equal to the oracle's restatement of core/knn.go:143-217 + core/sim.go (NaN
 pattern included), and therefore identical top-K neighbour lists under (sim desc, index asc).
 """
 import json
@@ -125,7 +125,7 @@ def test_knn_bad_arguments(ctx):
 
 
 def test_baseline_fit_bitwise(ctx, ml100k):
-    """core/base.go:433-461 BaseLine.Fit (used by KNNBaseLine, knn.go:260-268): float64 serial
+    """core/base.go:135-163 BaseLine.Fit (used by KNNBaseLine, knn.go:179-187): float64 serial
     chain in the reference order -> bitwise equal to the restatement."""
     from helpers import folds
     f = folds(*ml100k)[0]

@@ -27,14 +27,14 @@ def test_sim_known_answers():
 
 
 def test_sim_no_overlap_is_nan():
-    """sim.go:24/43: 0/0 when nothing is co-rated -> NaN (knn.go:286 keeps such pairs NaN)."""
+    """sim.go:24/43: 0/0 when nothing is co-rated -> NaN (knn.go:205 keeps such pairs NaN)."""
     for kind in (O.COSINE, O.MSD, O.PEARSON):
         assert math.isnan(O.sim(kind, [1, 2], [3.0, 4.0], [5, 6], [1.0, 2.0]))
     assert math.isnan(O.sim(O.COSINE, [], [], [1], [1.0]))
 
 
 def test_sim_symmetric_bitwise():
-    """Q8: sim(a,b) == sim(b,a) bitwise, which is what makes knn.go:287-288's race benign."""
+    """Q8: sim(a,b) == sim(b,a) bitwise, which is what makes knn.go:206-207's race benign."""
     rng = np.random.default_rng(3)
     for _ in range(200):
         a = np.sort(rng.choice(60, 25, replace=False))
@@ -158,6 +158,6 @@ def _knn_cv(fs, type_, kind=O.MSD, user_based=True):
                                          (O.ZSCORE, (0.951, 0.746)), (O.BASELINE, (0.931, 0.733))])
 def test_knn_accuracy_regression(ml100k_folds, type_, bound):
     """core/base_test.go:50-64 (KNN, KNNWithMean, KNNWithZScore, KNNBaseLine; user-based MSD,
-    k=40, minK=1 defaults of knn.go:160-162, 226-227)."""
+    k=40, minK=1 defaults of knn.go:79-81, 226-227)."""
     r, m = _knn_cv(ml100k_folds[:2], type_)
     assert r <= bound[0] + EPS and m <= bound[1] + EPS, (r, m)
