@@ -147,9 +147,19 @@ int rs_svd_plan_epochs(rs_svd_plan* plan, int32_t n_epochs, float lr, float reg,
 /* write_back: RS_SGD_WB_ATOMIC (default) or RS_SGD_WB_STORE; ring_depth: item-row prefetch distance
  * in ratings (4, 8 = default, 16). */
 int rs_svd_plan_set_mode(rs_svd_plan* plan, int32_t write_back, int32_t ring_depth);
+/* FAST-mode work items: users with more than split_cap ratings (default 0 = never split) run as
+ * ceil(deg / split_cap) near-equal pieces on separate waves from the same p_u, and the row becomes the
+ * count-weighted average of the pieces' end states after the epoch (or_svd_fit_chunked restates it).
+ * Faster epochs, lower accuracy on large-degree users (measured trade-off). */
+int rs_svd_plan_set_split(rs_svd_plan* plan, int32_t split_cap);
+/* FAST-mode hot items: an item with more than item_cap ratings (default 0 = never) gets
+ * ceil(deg / item_cap) row copies; its ratings are dealt over them in user-CSR order and the copies
+ * are merged by count-weighted average after every epoch.  Spreads the float atomics of hot rows. */
+int rs_svd_plan_set_item_split(rs_svd_plan* plan, int32_t item_cap);
 /* ---- item-sharded multi-GPU (north_star: Q sharded by item range, users replicated) --------- *
  * Each rank builds a plan over its item shard.  Per epoch: rs_svd_plan_epoch_delta leaves P at the
- * epoch start and writes dP[u] = w_u (p_u(end) - p_u(start)) (bias column included) and
+ * epoch start and writes dP[u] = w_u (p_u(end) - p_u(start)) (bias column included; for a split
+ * user the count-weighted average over its pieces) and
  * gbsum = sum_w n_w (gb_w - gb); the caller all-reduces (sum) dP and gbsum over the ranks (RCCL)
  * and calls rs_svd_plan_apply_delta(inv_total_nnz = 1 / total ratings over all ranks).
  * w_u = (ratings of u in this shard) / (ratings of u over all shards): the count-weighted average of

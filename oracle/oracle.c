@@ -639,10 +639,11 @@ void or_svd_fit_chunked(int32_t n_users, const int64_t* rowptr, const int32_t* i
             if (!wsplit[x]) {
                 memcpy(P + (int64_t)uu * k, lp + x * k, (size_t)k * sizeof(double));
                 bu[uu] = lbu[x];
-            } else {
+            } else {  /* split user: count-weighted average of the pieces' end states */
+                const double wgt = (double)(we[x] - wb[x]) / (double)(rowptr[uu + 1] - rowptr[uu]);
                 for (int32_t f = 0; f < k; f++)
-                    P[(int64_t)uu * k + f] += lp[x * k + f] - lp0[x * k + f];
-                bu[uu] += lbu[x] - lbu0[x];
+                    P[(int64_t)uu * k + f] += wgt * (lp[x * k + f] - lp0[x * k + f]);
+                bu[uu] += wgt * (lbu[x] - lbu0[x]);
             }
             gsum += (double)(we[x] - wb[x]) * (lgb[x] - GB);
         }

@@ -98,8 +98,9 @@ void or_baseline_fit(int64_t n, const int32_t* u, const int32_t* i, const double
  * (user, CSR range) chunks; all chunks advance in lock-step rounds (round t processes the t-th
  * rating of every live chunk in chunk order), which is the schedule the GPU runs when every chunk
  * is resident; per-chunk local GlobalBias, folded at epoch end as gb += sum(n_w * dgb_w) / nnz.
- * P deltas of split users are summed in chunk order.  Used for RMSE-parity studies and for the
- * race-free factor parity test (inputs where no two chunks share an item). */
+ * A split user's P row and bias become the count-weighted average of its pieces' end states
+ * (P += sum_pieces len/deg * (p_end - p_start)), applied in piece order.  Used for RMSE-parity
+ * studies and for the race-free factor parity test (inputs where no two chunks share an item). */
 void or_svd_fit_chunked(int32_t n_users, const int64_t* rowptr, const int32_t* items,
                         const double* r, int32_t chunk, int32_t k, int32_t epochs, double lr,
                         double reg, double* P, double* Q, double* bu, double* bi, double* gb);

@@ -1,12 +1,22 @@
 // sgd.hip -- K1: SGD epoch of the Funk-SVD model (reference core/svd.go:63-132), gfx950.
 //
 // Two schedules (SURVEY §8a parity contract):
-//   FAST    user-CSR, one wave per user row (heaviest user first, LPT); p_u in VGPRs for the whole
-//           row; q_i rows gathered D ratings ahead into a register ring; q_i updates written back
+//   FAST    user-CSR, one wave per work item (heaviest first, LPT); p_u in VGPRs for the whole
+//           item; q_i rows gathered D ratings ahead into a register ring; q_i updates written back
 //           as float-atomic deltas (RS_SGD_WB_ATOMIC, default: no lost updates) or as write-through
 //           stores (RS_SGD_WB_STORE: Hogwild, loses concurrent updates of hot items).  GlobalBias
 //           (Q2) is a per-wave local SGD copy folded at epoch end as gb += sum_w n_w (gb_w - gb)/nnz
 //           (fixed-order, deterministic).  RMSE parity with the reference (P2).
+//           A work item is a whole user row, or -- for users with more than split_cap ratings -- one
+//           of ceil(deg / split_cap) near-equal pieces of it: the pieces run as separate waves from
+//           the same p_u and the row becomes the count-weighted average of their end states
+//           (P += sum len/deg (p_end - p_start), merged after the epoch).  This cuts the per-user
+//           serial chain (ML-1M's heaviest user: 2,314 ratings) but costs accuracy on ML-1M-shaped
+//           data (measured), so it is off unless the caller asks (rs_svd_plan_set_split).
+//           Likewise items with more than item_cap ratings are dealt (in user-CSR order) over
+//           ceil(deg / item_cap) row copies, merged by count-weighted average after the epoch and
+//           re-broadcast: the float atomics of a hot row are spread over several rows, which the
+//           memory-side atomic unit otherwise serialises.  Off by default for the same reason.
 //   ORDERED one 16-lane group walks the ratings in train-set order with the exact update order of
 //           svd.go:93-129 (aliasing Q1: q_i is updated with the NEW p_u) -- factor parity (P1).
 //
@@ -55,12 +65,18 @@ __device__ __forceinline__ float lane63(float x) {
 // FAST epoch kernel (K1).  Item ids and ratings are wave-uniform: read 16 at a time with scalar
 // loads one batch ahead, so row addresses are SGPR arithmetic.  The 16-rating batch loop is
 // unrolled so every ring index is a compile-time constant.
+//
+// Write-back of p: direct store when dP is NULL; otherwise the weighted delta
+// scale * (p_end - p_start) is float-atomically added to dP (scale = piece fraction, times the
+// user's shard weight uw[u] in multi-GPU delta mode) -- except whole rows when whole_direct is set
+// (single-GPU: only split users need the merge).
 template <int E, int D, int WB>
 __global__ __launch_bounds__(256) void svd_epoch_fast_kernel(
-    const int32_t* __restrict__ work, int32_t n_work, const int64_t* __restrict__ rowptr,
-    const int32_t* __restrict__ items, const float* __restrict__ ratings, float* __restrict__ P,
-    float* Q, int32_t q_bytes, const double* __restrict__ gb_in, double* __restrict__ gb_partial,
-    float lr, float reg, float* __restrict__ dP, const float* __restrict__ uw) {
+    const int32_t* __restrict__ wk_user, const int64_t* __restrict__ wk_rng,
+    const float* __restrict__ wk_frac, int32_t n_work, const int32_t* __restrict__ items,
+    const float* __restrict__ ratings, float* __restrict__ P, float* Q, int32_t q_bytes,
+    const double* __restrict__ gb_in, double* __restrict__ gb_partial, float lr, float reg,
+    float* __restrict__ dP, const float* __restrict__ uw, int32_t whole_direct) {
 #pragma clang fp contract(fast)
     constexpr int LD = 64 * E, B = 16;
     static_assert(B % D == 0 && D <= B, "ring depth must divide the 16-rating batch");
@@ -76,8 +92,9 @@ __global__ __launch_bounds__(256) void svd_epoch_fast_kernel(
     double contrib = 0.0;
 
     if (w < n_work) {
-        const int32_t u = work[w];
-        const int64_t b = rowptr[u], e = rowptr[u + 1];
+        const int32_t u = wk_user[w];
+        const int64_t b = wk_rng[2 * w], e = wk_rng[2 * w + 1];
+        const float frac = wk_frac[w];
         float p[E];
         float* prow = P + static_cast<int64_t>(u) * LD;
 #pragma unroll
@@ -155,11 +172,11 @@ __global__ __launch_bounds__(256) void svd_epoch_fast_kernel(
 #pragma unroll
             for (int j = 0; j < B; ++j) it_nxt[j] = items[base + 2 * B + j];
         }
-        if (dP) {  // item-sharded multi-GPU: weighted delta, P itself stays at the epoch start
-            const float wu = uw[u];
+        if (dP && !(whole_direct && frac == 1.f)) {  // weighted delta, P stays at the epoch start
+            const float sc = uw ? frac * uw[u] : frac;
             float* drow = dP + static_cast<int64_t>(u) * LD;
 #pragma unroll
-            for (int x = 0; x < E; ++x) drow[lane + 64 * x] = wu * (p[x] - prow[lane + 64 * x]);
+            for (int x = 0; x < E; ++x) atomicAdd(drow + lane + 64 * x, sc * (p[x] - prow[lane + 64 * x]));
         } else {
 #pragma unroll
             for (int x = 0; x < E; ++x) prow[lane + 64 * x] = p[x];
@@ -185,6 +202,36 @@ __global__ __launch_bounds__(256) void gb_fold_kernel(const double* __restrict__
         __syncthreads();
     }
     if (threadIdx.x == 0) gb[0] += s[0] * inv_nnz;
+}
+
+// Split users (single GPU): P[u] += dP[u], dP[u] = 0 for the listed rows (one wave per row).
+__global__ __launch_bounds__(64) void svd_merge_rows_kernel(float* __restrict__ P, float* __restrict__ dP,
+                                                           const int32_t* __restrict__ rows, int32_t ld) {
+    const int64_t r = static_cast<int64_t>(rows[blockIdx.x]) * ld;
+    for (int32_t c = threadIdx.x; c < ld; c += 64) {
+        P[r + c] += dP[r + c];
+        dP[r + c] = 0.f;
+    }
+}
+
+// Split items: meta = {item row, first extra row, copies R, offset into frac}.  mode 0: the item row
+// and its R - 1 copies become the count-weighted average of the copies (fixed order); mode 1: the
+// copies are set to the item row (after an upload).  One wave per split item.
+__global__ __launch_bounds__(64) void svd_item_merge_kernel(float* __restrict__ Q,
+                                                           const int4* __restrict__ meta,
+                                                           const float* __restrict__ frac, int32_t ld,
+                                                           int32_t mode) {
+    const int4 m = meta[blockIdx.x];
+    auto row = [&](int32_t c) { return static_cast<int64_t>(c == 0 ? m.x : m.y + c - 1) * ld; };
+    for (int32_t col = threadIdx.x; col < ld; col += 64) {
+        float v = 0.f;
+        if (mode == 0) {
+            for (int32_t c = 0; c < m.z; ++c) v = __builtin_fmaf(frac[m.w + c], Q[row(c) + col], v);
+        } else {
+            v = Q[row(0) + col];
+        }
+        for (int32_t c = 0; c < m.z; ++c) Q[row(c) + col] = v;
+    }
 }
 
 // Multi-GPU: the all-reduced weighted user deltas and global-bias sum are applied in place.
@@ -303,10 +350,22 @@ struct rs_svd_plan {
     rs_ctx* ctx = nullptr;
     int32_t n_users = 0, n_items = 0, k = 0, ld = 0, n_work = 0;
     int64_t nnz = 0;
-    rs::DevBuf<int64_t> rowptr;
-    rs::DevBuf<int32_t> items;
+    std::vector<int64_t> h_rowptr;  // host user-CSR row pointers (work items are rebuilt from it)
+    std::vector<int32_t> h_cols;    // host user-CSR item ids (item copies are rebuilt from it)
+    rs::DevBuf<int32_t> items;      // user-CSR item rows (copies of split items), padded by 64
     rs::DevBuf<float> ratings;
-    rs::DevBuf<int32_t> work;
+    rs::DevBuf<int32_t> wk_user;      // work items: user, [begin, end) into the CSR, len / deg
+    rs::DevBuf<int64_t> wk_rng;
+    rs::DevBuf<float> wk_frac;
+    int32_t split_cap = 0;            // users with more ratings are split into pieces (0: never)
+    rs::DevBuf<float> dPs;            // split-user deltas (single GPU), zero between epochs
+    rs::DevBuf<int32_t> split_rows;   // users split into pieces
+    int32_t n_split = 0;
+    int32_t item_cap = 0;             // items with more ratings get row copies (0: never)
+    int32_t n_qrows = 0;              // item rows incl. copies (Q holds n_qrows x ld)
+    rs::DevBuf<int4> isplit_meta;     // split items: {row, first copy row, copies, frac offset}
+    rs::DevBuf<float> isplit_frac;
+    int32_t n_isplit = 0;
     rs::DevBuf<float> P, Q;  // bias in column ld - 1
     rs::DevBuf<double> gb, partial;
     rs::DevBuf<float> uw;  // per-user share of this shard (multi-GPU delta mode)
@@ -334,9 +393,14 @@ constexpr int32_t kMaxFactors = 511;
 template <int E, int D, int WB>
 static void launch_fast_t(rs_svd_plan* pl, float lr, float reg, hipStream_t s, float* dP) {
     const int32_t q_bytes = static_cast<int32_t>(pl->Q.n * sizeof(float));
+    // multi-GPU delta mode (caller's dP, shard weights): every item adds its weighted delta;
+    // single GPU: whole rows store P directly, pieces of split users add into the plan's dPs
+    const bool multi = dP != nullptr;
+    float* d = multi ? dP : (pl->n_split > 0 ? pl->dPs.p : nullptr);
     hipLaunchKernelGGL((svd_epoch_fast_kernel<E, D, WB>), dim3(pl->n_blocks), dim3(256), 0, s,
-                       pl->work.p, pl->n_work, pl->rowptr.p, pl->items.p, pl->ratings.p, pl->P.p,
-                       pl->Q.p, q_bytes, pl->gb.p, pl->partial.p, lr, reg, dP, pl->uw.p);
+                       pl->wk_user.p, pl->wk_rng.p, pl->wk_frac.p, pl->n_work, pl->items.p,
+                       pl->ratings.p, pl->P.p, pl->Q.p, q_bytes, pl->gb.p, pl->partial.p, lr, reg, d,
+                       multi ? pl->uw.p : nullptr, multi ? 0 : 1);
 }
 
 template <int D, int WB>
@@ -384,6 +448,123 @@ static void launch_ordered(int64_t nnz, const int32_t* u, const int32_t* i, cons
 
 int32_t fast_ld(int32_t k) { return 64 * ((k + 1 + 63) / 64); }
 
+static void plan_sync_last(rs_svd_plan* pl) {
+    if (pl->last_stream) RS_HIP(hipStreamSynchronize(pl->last_stream));
+}
+
+// Item row copies from the host CSR: an item with deg > item_cap gets R = ceil(deg / item_cap) rows
+// (its own plus R - 1 appended after n_items); its ratings are dealt in user-CSR order, piece
+// c taking positions [c deg / R, (c + 1) deg / R).  Q is (re)allocated to n_qrows rows keeping the
+// item rows; copies are synced from them.
+static void sync_item_copies(rs_svd_plan* pl, hipStream_t s, int32_t mode) {
+    if (pl->n_isplit > 0)
+        hipLaunchKernelGGL(svd_item_merge_kernel, dim3(pl->n_isplit), dim3(64), 0, s, pl->Q.p,
+                           pl->isplit_meta.p, pl->isplit_frac.p, pl->ld, mode);
+}
+
+static void build_items(rs_svd_plan* pl) {
+    hipStream_t s = pl->ctx->stream;
+    const int32_t ni = pl->n_items;
+    const std::vector<int32_t>& cols = pl->h_cols;
+    std::vector<int64_t> deg(std::max(1, ni), 0);
+    for (int32_t c : cols) deg[c]++;
+    std::vector<int32_t> R(std::max(1, ni), 1), first(std::max(1, ni), 0);
+    std::vector<int4> meta;
+    std::vector<float> frac;
+    int32_t extra = 0;
+    for (int32_t x = 0; x < ni; ++x) {
+        if (pl->item_cap > 0 && deg[x] > pl->item_cap) {
+            R[x] = static_cast<int32_t>((deg[x] + pl->item_cap - 1) / pl->item_cap);
+            first[x] = ni + extra;
+            meta.push_back(make_int4(x, ni + extra, R[x], static_cast<int32_t>(frac.size())));
+            for (int32_t c = 0; c < R[x]; ++c) {
+                const int64_t lo = deg[x] * c / R[x], hi = deg[x] * (c + 1) / R[x];
+                frac.push_back(static_cast<float>(static_cast<double>(hi - lo) / deg[x]));
+            }
+            extra += R[x] - 1;
+        }
+    }
+    std::vector<int32_t> remap(cols.size() + 64, 0);
+    std::vector<int64_t> seen(std::max(1, ni), 0);
+    for (size_t t = 0; t < cols.size(); ++t) {
+        const int32_t x = cols[t];
+        const int32_t c = static_cast<int32_t>(seen[x]++ * R[x] / deg[x]);
+        remap[t] = c == 0 ? x : first[x] + c - 1;
+    }
+    const int32_t rows = ni + extra;
+    if (static_cast<int64_t>(std::max(1, rows)) * pl->ld * 4 >= (int64_t{1} << 31) - 64)
+        throw std::invalid_argument("item rows * n_factors too large for 32-bit buffer offsets");
+    plan_sync_last(pl);
+    pl->items.alloc(remap.size());
+    pl->items.upload(remap.data(), remap.size(), s);
+    pl->n_isplit = static_cast<int32_t>(meta.size());
+    pl->isplit_meta.alloc(std::max<size_t>(1, meta.size()));
+    pl->isplit_frac.alloc(std::max<size_t>(1, frac.size()));
+    pl->isplit_meta.upload(meta.data(), meta.size(), s);
+    pl->isplit_frac.upload(frac.data(), frac.size(), s);
+    const size_t need = static_cast<size_t>(std::max(1, rows)) * pl->ld;
+    if (pl->Q.n != need) {
+        DevBuf<float> q(need);
+        RS_HIP(hipMemsetAsync(q.p, 0, need * sizeof(float), s));
+        if (pl->Q.p)
+            RS_HIP(hipMemcpyAsync(q.p, pl->Q.p, static_cast<size_t>(std::max(1, ni)) * pl->ld * sizeof(float),
+                                  hipMemcpyDeviceToDevice, s));
+        pl->Q = std::move(q);
+    }
+    pl->n_qrows = rows;
+    sync_item_copies(pl, s, 1);
+    RS_HIP(hipStreamSynchronize(s));  // host vectors die with this scope
+}
+
+// Work items from the host CSR: whole user rows, users with more than split_cap ratings cut into
+// ceil(deg / split_cap) near-equal pieces (the split of or_svd_fit_chunked); LPT order (longest
+// first, ties by user then piece); empty users dropped.
+static void build_work(rs_svd_plan* pl) {
+    hipStream_t s = pl->ctx->stream;
+    const std::vector<int64_t>& rp = pl->h_rowptr;
+    struct Item { int32_t u; int64_t b, e; float frac; };
+    std::vector<Item> wk;
+    std::vector<int32_t> split;
+    for (int32_t u = 0; u < pl->n_users; ++u) {
+        const int64_t d = rp[u + 1] - rp[u];
+        if (d == 0) continue;
+        const int64_t pieces = pl->split_cap > 0 ? (d + pl->split_cap - 1) / pl->split_cap : 1;
+        if (pieces > 1) split.push_back(u);
+        for (int64_t x = 0; x < pieces; ++x) {
+            const int64_t b = rp[u] + d * x / pieces, e = rp[u] + d * (x + 1) / pieces;
+            wk.push_back({u, b, e, pieces > 1 ? static_cast<float>(static_cast<double>(e - b) / d) : 1.f});
+        }
+    }
+    std::stable_sort(wk.begin(), wk.end(), [](const Item& x, const Item& y) { return x.e - x.b > y.e - y.b; });
+    std::vector<int32_t> wu(wk.size());
+    std::vector<int64_t> wr(2 * wk.size());
+    std::vector<float> wf(wk.size());
+    for (size_t x = 0; x < wk.size(); ++x) {
+        wu[x] = wk[x].u;
+        wr[2 * x] = wk[x].b;
+        wr[2 * x + 1] = wk[x].e;
+        wf[x] = wk[x].frac;
+    }
+    plan_sync_last(pl);
+    pl->n_work = static_cast<int32_t>(wk.size());
+    pl->n_blocks = std::max<int32_t>(1, (pl->n_work + 3) / 4);  // one wave per item, 4 per block
+    pl->wk_user.alloc(std::max<size_t>(1, wu.size()));
+    pl->wk_rng.alloc(std::max<size_t>(2, wr.size()));
+    pl->wk_frac.alloc(std::max<size_t>(1, wf.size()));
+    pl->partial.alloc(pl->n_blocks);
+    pl->wk_user.upload(wu.data(), wu.size(), s);
+    pl->wk_rng.upload(wr.data(), wr.size(), s);
+    pl->wk_frac.upload(wf.data(), wf.size(), s);
+    pl->n_split = static_cast<int32_t>(split.size());
+    pl->split_rows.alloc(std::max<size_t>(1, split.size()));
+    pl->split_rows.upload(split.data(), split.size(), s);
+    if (pl->n_split > 0 && pl->dPs.n != static_cast<size_t>(std::max(1, pl->n_users)) * pl->ld) {
+        pl->dPs.alloc(static_cast<size_t>(std::max(1, pl->n_users)) * pl->ld);
+        RS_HIP(hipMemsetAsync(pl->dPs.p, 0, pl->dPs.n * sizeof(float), s));
+    }
+    RS_HIP(hipStreamSynchronize(s));  // host vectors die with this scope
+}
+
 static void plan_build(rs_ctx* ctx, const rs_ratings* r, int32_t k, rs_svd_plan* pl) {
     hipStream_t s = ctx->stream;
     pl->ctx = ctx;
@@ -392,45 +573,23 @@ static void plan_build(rs_ctx* ctx, const rs_ratings* r, int32_t k, rs_svd_plan*
     pl->k = k;
     pl->ld = fast_ld(k);
     pl->nnz = r->nnz;
-    if (static_cast<int64_t>(std::max(1, r->n_items)) * pl->ld * 4 >= (int64_t{1} << 31) - 64)
-        throw std::invalid_argument("n_items * n_factors too large for 32-bit buffer offsets");
     UserCSR csr;
     build_csr(r->nnz, r->n_users, r->users, r->items, r->ratings, csr);
-    // LPT dispatch order: heaviest user first (ties by user id), empty users dropped.
-    std::vector<int32_t> order;
-    order.reserve(r->n_users);
-    for (int32_t x = 0; x < r->n_users; ++x)
-        if (csr.rowptr[x + 1] > csr.rowptr[x]) order.push_back(x);
-    std::stable_sort(order.begin(), order.end(), [&](int32_t a, int32_t b) {
-        return csr.rowptr[a + 1] - csr.rowptr[a] > csr.rowptr[b + 1] - csr.rowptr[b];
-    });
-    pl->n_work = static_cast<int32_t>(order.size());
-    pl->n_blocks = std::max<int32_t>(1, (pl->n_work + 3) / 4);  // one wave per user, 4 per block
     // items / ratings padded by 64 entries: the kernel reads whole 16-entry batches (two ahead)
-    csr.cols.resize(csr.cols.size() + 64, 0);
     csr.vals.resize(csr.vals.size() + 64, 0.f);
-    pl->rowptr.alloc(csr.rowptr.size());
-    pl->items.alloc(csr.cols.size());
     pl->ratings.alloc(csr.vals.size());
-    pl->work.alloc(std::max<size_t>(1, order.size()));
-    pl->rowptr.upload(csr.rowptr.data(), csr.rowptr.size(), s);
-    pl->items.upload(csr.cols.data(), csr.cols.size(), s);
     pl->ratings.upload(csr.vals.data(), csr.vals.size(), s);
-    pl->work.upload(order.data(), order.size(), s);
+    pl->h_rowptr = std::move(csr.rowptr);
+    pl->h_cols = std::move(csr.cols);
     pl->P.alloc(static_cast<size_t>(std::max(1, r->n_users)) * pl->ld);
-    pl->Q.alloc(static_cast<size_t>(std::max(1, r->n_items)) * pl->ld);
-    pl->gb.alloc(1);
-    pl->partial.alloc(pl->n_blocks);
     RS_HIP(hipMemsetAsync(pl->P.p, 0, pl->P.n * sizeof(float), s));
-    RS_HIP(hipMemsetAsync(pl->Q.p, 0, pl->Q.n * sizeof(float), s));
+    build_items(pl);
+    build_work(pl);
+    pl->gb.alloc(1);
     RS_HIP(hipMemsetAsync(pl->gb.p, 0, sizeof(double), s));
     RS_HIP(hipEventCreate(&pl->ev0));
     RS_HIP(hipEventCreate(&pl->ev1));
     RS_HIP(hipStreamSynchronize(s));  // host CSR vectors die with this scope
-}
-
-static void plan_sync_last(rs_svd_plan* pl) {
-    if (pl->last_stream) RS_HIP(hipStreamSynchronize(pl->last_stream));
 }
 
 // f64 factor rows (stride k) + bias -> f32 rows of ld floats with the bias in column ld - 1
@@ -462,7 +621,11 @@ static void plan_upload(rs_svd_plan* pl, const double* P, const double* Q, const
         RS_HIP(hipStreamSynchronize(s));
     };
     put(pl->P, pl->n_users, P, bu);
-    put(pl->Q, pl->n_items, Q, bi);
+    put(pl->Q, pl->n_items, Q, bi);  // item rows; their copies follow
+    if (Q || bi) {
+        sync_item_copies(pl, s, 1);
+        RS_HIP(hipStreamSynchronize(s));
+    }
     if (gb) {
         pl->gb.upload(gb, 1, s);
         RS_HIP(hipStreamSynchronize(s));
@@ -507,12 +670,16 @@ static void plan_epochs(rs_svd_plan* pl, int32_t epochs, float lr, float reg, hi
         if (pl->timing) RS_HIP(hipEventRecord(pl->tev[2 * e], s));
         launch_fast(pl, lr, reg, s);
         if (pl->timing) RS_HIP(hipEventRecord(pl->tev[2 * e + 1], s));
+        if (pl->n_split > 0)
+            hipLaunchKernelGGL(svd_merge_rows_kernel, dim3(pl->n_split), dim3(64), 0, s, pl->P.p,
+                               pl->dPs.p, pl->split_rows.p, pl->ld);
+        sync_item_copies(pl, s, 0);
         hipLaunchKernelGGL(gb_fold_kernel, dim3(1), dim3(256), 0, s, pl->partial.p,
                            static_cast<int64_t>(pl->n_blocks), pl->gb.p, inv_nnz);
         RS_HIP(hipGetLastError());
     }
     RS_HIP(hipEventRecord(pl->ev1, s));
-    pl->last_launches = pl->timing ? epochs : 2 * epochs;
+    pl->last_launches = pl->timing ? epochs : (2 + (pl->n_split > 0) + (pl->n_isplit > 0)) * epochs;
     pl->last_stream = s;
     pl->last_ms = -1.0;  // resolved lazily by rs_svd_plan_last_kernel_ms
 }
@@ -599,6 +766,7 @@ extern "C" int rs_svd_plan_epoch_delta(rs_svd_plan* pl, float lr, float reg, voi
         }
         RS_HIP(hipEventRecord(pl->ev0, s));
         rs::launch_fast(pl, lr, reg, s, static_cast<float*>(dP));
+        rs::sync_item_copies(pl, s, 0);  // hot-item copies are shard-local: merge them here
         if (pl->timing) RS_HIP(hipEventRecord(pl->tev[1], s));
         hipLaunchKernelGGL(rs::gb_sum_kernel, dim3(1), dim3(256), 0, s, pl->partial.p,
                            static_cast<int64_t>(pl->n_blocks), static_cast<double*>(gbsum));
@@ -636,6 +804,28 @@ extern "C" int rs_svd_plan_set_mode(rs_svd_plan* pl, int32_t write_back, int32_t
     pl->write_back = write_back;
     pl->ring_depth = ring_depth;
     return RS_OK;
+}
+
+extern "C" int rs_svd_plan_set_split(rs_svd_plan* pl, int32_t split_cap) {
+    if (!pl) return rs::set_error(nullptr, RS_ERR_INVALID, "plan is NULL");
+    return rs_guard(pl->ctx, [&]() -> int {
+        if (split_cap < 0 || (split_cap > 0 && split_cap < 16))
+            return rs::set_error(pl->ctx, RS_ERR_INVALID, "split_cap must be 0 (never) or >= 16");
+        pl->split_cap = split_cap;
+        rs::build_work(pl);
+        return RS_OK;
+    });
+}
+
+extern "C" int rs_svd_plan_set_item_split(rs_svd_plan* pl, int32_t item_cap) {
+    if (!pl) return rs::set_error(nullptr, RS_ERR_INVALID, "plan is NULL");
+    return rs_guard(pl->ctx, [&]() -> int {
+        if (item_cap < 0 || (item_cap > 0 && item_cap < 16))
+            return rs::set_error(pl->ctx, RS_ERR_INVALID, "item_cap must be 0 (never) or >= 16");
+        pl->item_cap = item_cap;
+        rs::build_items(pl);
+        return RS_OK;
+    });
 }
 
 extern "C" int rs_svd_plan_upload(rs_svd_plan* pl, const double* P, const double* Q,

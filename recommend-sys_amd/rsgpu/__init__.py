@@ -28,8 +28,9 @@ HEADER_SYMBOLS = (
     "rs_svd_fit", "rs_svd_predict", "rs_svdpp_fit", "rs_nmf_fit", "rs_baseline_fit",
     "rs_knn_sims", "rs_sim_pair", "rs_svd_plan_create", "rs_svd_plan_destroy",
     "rs_svd_plan_upload", "rs_svd_plan_download", "rs_svd_plan_epochs",
-    "rs_svd_plan_device_ptrs", "rs_svd_plan_set_mode", "rs_svd_plan_set_timing",
-    "rs_svd_plan_set_user_weights", "rs_svd_plan_epoch_delta", "rs_svd_plan_apply_delta", "rs_svd_plan_last_kernel_ms",
+    "rs_svd_plan_device_ptrs", "rs_svd_plan_set_mode", "rs_svd_plan_set_split",
+    "rs_svd_plan_set_item_split", "rs_svd_plan_set_timing", "rs_svd_plan_set_user_weights",
+    "rs_svd_plan_epoch_delta", "rs_svd_plan_apply_delta", "rs_svd_plan_last_kernel_ms",
 )
 
 
@@ -89,6 +90,8 @@ def lib():
             "rs_svd_plan_device_ptrs": (C.c_int, [_vp, C.POINTER(_vp), C.POINTER(_vp),
                                                   C.POINTER(_vp), C.POINTER(_i32)]),
             "rs_svd_plan_set_mode": (C.c_int, [_vp, _i32, _i32]),
+            "rs_svd_plan_set_split": (C.c_int, [_vp, _i32]),
+            "rs_svd_plan_set_item_split": (C.c_int, [_vp, _i32]),
             "rs_svd_plan_set_user_weights": (C.c_int, [_vp, _vp]),
             "rs_svd_plan_epoch_delta": (C.c_int, [_vp, _flt, _flt, _vp, _vp, _vp]),
             "rs_svd_plan_apply_delta": (C.c_int, [_vp, _vp, _vp, _dbl, _vp]),
@@ -281,6 +284,12 @@ class SvdPlan:
 
     def set_mode(self, write_back=WB_ATOMIC, ring_depth=8):
         self.ctx.check(lib().rs_svd_plan_set_mode(self.h, write_back, ring_depth))
+
+    def set_split(self, split_cap):
+        self.ctx.check(lib().rs_svd_plan_set_split(self.h, split_cap))
+
+    def set_item_split(self, item_cap):
+        self.ctx.check(lib().rs_svd_plan_set_item_split(self.h, item_cap))
 
     def device_ptrs(self):
         ps = [C.c_void_p() for _ in range(3)]

@@ -24,6 +24,12 @@ def ml100k():
 @pytest.fixture(scope="session")
 def ctx():
     import rsgpu
+    try:  # bring up torch's HIP runtime first: tests hand torch device buffers to the C-ABI
+        import torch
+        if torch.cuda.is_available():
+            torch.cuda.init()
+    except ImportError:
+        pass
     c = rsgpu.Context(0)
     yield c
     c.close()
