@@ -2,7 +2,7 @@
 // core/sim.go:10-81 as the pair function), gfx950.
 //
 // K4 (Cosine, MSD; bit-exact): when every rating is r = x / s with integer x, s in {1, 2} and
-// |x| <= 11 (ML-100K/1M integer stars: s = 1; ML-20M half stars: s = 2), the co-rated sums of
+// 1 <= x <= 11 (ML-100K/1M integer stars: s = 1; ML-20M half stars: s = 2), the co-rated sums of
 // sim.go are exact integers times 1/s^2.  They are computed as int8 x int8 -> int32 MFMA
 // contractions over the dense (left x right) matrices X (x), X2 (x^2) and M (1 where rated):
 //     l = X X^T,   m = X2 M^T,   n = M X2^T,   count = M M^T  (MSD only)
@@ -38,46 +38,67 @@ constexpr int kTile = 128;   // block tile (a x b)
 constexpr int kKBlock = 64;  // bytes of the contraction dimension per iteration
 
 // ---------------------------------------------------------------------------------------------
-// dense operands: X[a][k] = x, X2 = x^2, M = 1 (rows padded to kTile, k padded to kKBlock)
+// dense operand X[a][k] = x in [1, 11], 0 = not rated (rows padded to kTile, k padded to kKBlock)
 
 __global__ void knn_scatter_kernel(int32_t L, const int64_t* __restrict__ rowptr,
                                    const int32_t* __restrict__ ids, const int8_t* __restrict__ x,
-                                   int64_t ldk, int8_t* __restrict__ X, int8_t* __restrict__ X2,
-                                   int8_t* __restrict__ M) {
+                                   int64_t ldk, int8_t* __restrict__ X) {
     const int32_t a = blockIdx.x;
     if (a >= L) return;
-    for (int64_t t = rowptr[a] + threadIdx.x; t < rowptr[a + 1]; t += blockDim.x) {
-        const int64_t o = static_cast<int64_t>(a) * ldk + ids[t];
-        const int8_t v = x[t];
-        X[o] = v;
-        X2[o] = static_cast<int8_t>(v * v);
-        M[o] = 1;
-    }
+    for (int64_t t = rowptr[a] + threadIdx.x; t < rowptr[a + 1]; t += blockDim.x)
+        X[static_cast<int64_t>(a) * ldk + ids[t]] = x[t];
 }
 
-__device__ __forceinline__ void tri_tile(int32_t t, int32_t& ta, int32_t& tb) {
-    // t enumerates (ta, tb), ta <= tb, column-major over tb: t = tb (tb + 1) / 2 + ta
-    int32_t b = static_cast<int32_t>((sqrt(8.0 * t + 1.0) - 1.0) * 0.5);
-    while (static_cast<int64_t>(b) * (b + 1) / 2 > t) --b;
-    while (static_cast<int64_t>(b + 1) * (b + 2) / 2 <= t) ++b;
-    tb = b;
-    ta = t - b * (b + 1) / 2;
+// KIND 0 = Cosine (3 contractions), 1 = MSD (4 contractions).
+//
+// One 128 x 128 tile (ta <= tb) of the upper triangle per workgroup, tiles taken from a host-built
+// list in 16 x 16 super-tile groups so the workgroups resident together share row blocks.  Four
+// waves, each a 64 x 64 sub-tile of 2 x 2 v_mfma_i32_32x32x32_i8 tiles.  Only X is read from HBM:
+// every rating is x = r s with x in [1, 11] and 0 marks "not rated", so the loader derives
+// X2 = x^2 (two v_pk_mul_lo_u16 per dword) and M = [x > 0] (SWAR add/and) itself -- a third of
+// the global traffic of loading all three.  Per 64-byte K step the workgroup stages the A rows (ta)
+// and B rows (tb) of X, X2 and M into a double-buffered LDS tile; the next step's X loads are in
+// flight during the MFMAs, and the steps are separated by a raw s_barrier after an lgkmcnt-only
+// wait, so the loads stay in flight across it.  LDS rows are
+// 64 bytes with the 16-byte chunk c of row r stored at chunk c ^ ((r >> 2) & 3): the staging
+// writes and the fragment reads are both bank-conflict free.
+constexpr int kRowPad = 64;                             // bytes per staged row
+constexpr int kStageMat = kTile * kRowPad;              // one matrix, one side
+constexpr int kStageBytes = 3 * 2 * kStageMat;          // X, X2, M for A and B
+constexpr int kXChunks = 2 * kTile * (kKBlock / 16);    // 16-byte X chunks per step (A and B)
+constexpr int kXPerThread = kXChunks / 256;
+
+typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
+
+__device__ __forceinline__ uint32_t sq_bytes(uint32_t w) {  // per byte x^2 (x <= 11)
+    const uint32_t e = w & 0x00FF00FFu, o = (w >> 8) & 0x00FF00FFu;
+    const u16x2 e2 = __builtin_bit_cast(u16x2, e) * __builtin_bit_cast(u16x2, e);
+    const u16x2 o2 = __builtin_bit_cast(u16x2, o) * __builtin_bit_cast(u16x2, o);
+    return __builtin_bit_cast(uint32_t, e2) | (__builtin_bit_cast(uint32_t, o2) << 8);
+}
+__device__ __forceinline__ uint32_t mask_bytes(uint32_t w) {  // per byte [x > 0] (x <= 127)
+    return ((w + 0x7F7F7F7Fu) & 0x80808080u) >> 7;
 }
 
-// KIND 0 = Cosine (3 contractions), 1 = MSD (4 contractions)
+__device__ __forceinline__ void lds_barrier() {
+    __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0) only: global loads stay in flight
+    __builtin_amdgcn_s_barrier();
+}
+
 template <int KIND>
-__global__ __launch_bounds__(256) void knn_sims_mfma_kernel(
-    const int8_t* __restrict__ X, const int8_t* __restrict__ X2, const int8_t* __restrict__ M,
-    int64_t ldk, int32_t L, double inv_s2, double* __restrict__ S) {
+__global__ __launch_bounds__(256) void knn_sims_mfma_kernel(const int8_t* __restrict__ X,
+                                                            int64_t ldk, int32_t L,
+                                                            const int2* __restrict__ tiles,
+                                                            double inv_s2, double* __restrict__ S) {
     constexpr int NC = KIND == 0 ? 3 : 4;
-    int32_t ta, tb;
-    tri_tile(static_cast<int32_t>(blockIdx.x), ta, tb);
-    const int lane = threadIdx.x & 63;
-    const int wave = threadIdx.x >> 6;
+    extern __shared__ __attribute__((aligned(16))) int8_t smem[];
+    const int2 tile = tiles[blockIdx.x];
+    const int32_t ta = tile.x, tb = tile.y;
+    const int tid = threadIdx.x;
+    const int lane = tid & 63;
+    const int wave = tid >> 6;
     const int wa = wave >> 1, wb = wave & 1;
-    if (ta == tb && wa > wb) return;  // strictly below the diagonal: covered by its mirror
-    const int32_t r0 = ta * kTile + 64 * wa;  // left rows (a)
-    const int32_t c0 = tb * kTile + 64 * wb;  // partner rows (b)
+    const bool live = !(ta == tb && wa > wb);  // strictly below the diagonal: its mirror covers it
     const int row = lane & 31, half = lane >> 5;
 
     i32x16 acc[NC][2][2];
@@ -88,44 +109,90 @@ __global__ __launch_bounds__(256) void knn_sims_mfma_kernel(
 #pragma unroll
             for (int j = 0; j < 2; ++j) acc[c][i][j] = i32x16{};
 
-    // Lane (row, half) reads bytes [32 half, 32 half + 32) of each 64-byte K block of its row: the
-    // same bijection k <-> (lane, element) for both operands, so sum_k A[a][k] B[b][k] is exact
-    // whatever the MFMA's internal k order.
-    const int8_t* pa[3][2];
-    const int8_t* pb[3][2];
+    // staging map: chunk j of thread tid = side j >> 1, row (tid >> 2) + 64 (j & 1), 16-byte
+    // column tid & 3 -- a wave-uniform base per (side, j) plus one 32-bit lane offset
+    const int8_t* baseA = X + static_cast<int64_t>(ta) * kTile * ldk;
+    const int8_t* baseB = X + static_cast<int64_t>(tb) * kTile * ldk;
+    const uint32_t loff = static_cast<uint32_t>((tid >> 2) * ldk + 16 * (tid & 3));
+    const int64_t half_rows = 64 * ldk;
+    const int r_lo = tid >> 2;
+    int32_t dst[kXPerThread];
 #pragma unroll
-    for (int i = 0; i < 2; ++i) {
-        const int64_t oa = static_cast<int64_t>(r0 + 32 * i + row) * ldk + 32 * half;
-        const int64_t ob = static_cast<int64_t>(c0 + 32 * i + row) * ldk + 32 * half;
-        pa[0][i] = X + oa;  pa[1][i] = X2 + oa;  pa[2][i] = M + oa;
-        pb[0][i] = X + ob;  pb[1][i] = X2 + ob;  pb[2][i] = M + ob;
+    for (int j = 0; j < kXPerThread; ++j) {
+        const int side = j >> 1, r = r_lo + 64 * (j & 1), c = tid & 3;
+        dst[j] = side * kStageMat + r * kRowPad + 16 * (c ^ ((r >> 2) & 3));
     }
-    for (int64_t k0 = 0; k0 < ldk; k0 += kKBlock) {
-        i32x4 fa[3][2][2], fb[3][2][2];  // [matrix][tile][k-half of the 32 bytes]
+    auto gload = [&](i32x4 (&st)[kXPerThread], int64_t k0) {
 #pragma unroll
-        for (int m = 0; m < 3; ++m)
+        for (int j = 0; j < kXPerThread; ++j) {
+            const int8_t* base = ((j >> 1) ? baseB : baseA) + (j & 1) * half_rows + k0;
+            st[j] = *reinterpret_cast<const i32x4*>(base + loff);
+        }
+    };
+    auto lstore = [&](const i32x4 (&st)[kXPerThread], int buf) {
+        int8_t* b = smem + buf * kStageBytes;
 #pragma unroll
-            for (int i = 0; i < 2; ++i) {
-                const i32x4* qa = reinterpret_cast<const i32x4*>(pa[m][i] + k0);
-                const i32x4* qb = reinterpret_cast<const i32x4*>(pb[m][i] + k0);
-                fa[m][i][0] = qa[0];
-                fa[m][i][1] = qa[1];
-                fb[m][i][0] = qb[0];
-                fb[m][i][1] = qb[1];
-            }
+        for (int j = 0; j < kXPerThread; ++j) {
+            *reinterpret_cast<i32x4*>(b + 0 * 2 * kStageMat + dst[j]) = st[j];
+            i32x4 v;
 #pragma unroll
-        for (int s = 0; s < 2; ++s)
+            for (int d = 0; d < 4; ++d) v[d] = static_cast<int>(sq_bytes(static_cast<uint32_t>(st[j][d])));
+            *reinterpret_cast<i32x4*>(b + 1 * 2 * kStageMat + dst[j]) = v;
+#pragma unroll
+            for (int d = 0; d < 4; ++d) v[d] = static_cast<int>(mask_bytes(static_cast<uint32_t>(st[j][d])));
+            *reinterpret_cast<i32x4*>(b + 2 * 2 * kStageMat + dst[j]) = v;
+        }
+    };
+    // fragment of (matrix m, side, 32-row tile i, k sub-step s): lane (row, half) reads the 16
+    // bytes [32 s + 16 half, +16) of its row -- the same k bijection for both operands, so
+    // sum_k A[a][k] B[b][k] is exact whatever the MFMA's internal k order.
+    auto frag = [&](const int8_t* b, int m, int side, int i, int s) {
+        const int r = (side ? 64 * wb : 64 * wa) + 32 * i + row;
+        const int c = (2 * s + half) ^ ((r >> 2) & 3);
+        return *reinterpret_cast<const i32x4*>(b + (m * 2 + side) * kStageMat + r * kRowPad + 16 * c);
+    };
+    auto compute = [&](int buf) {
+        const int8_t* b = smem + buf * kStageBytes;
+#pragma unroll
+        for (int s = 0; s < 2; ++s) {
+            i32x4 fa[3][2], fb[3][2];
+#pragma unroll
+            for (int m = 0; m < 3; ++m)
+#pragma unroll
+                for (int i = 0; i < 2; ++i) {
+                    fa[m][i] = frag(b, m, 0, i, s);
+                    fb[m][i] = frag(b, m, 1, i, s);
+                }
 #pragma unroll
             for (int i = 0; i < 2; ++i)
 #pragma unroll
                 for (int j = 0; j < 2; ++j) {
-                    acc[0][i][j] = __builtin_amdgcn_mfma_i32_32x32x32_i8(fa[0][i][s], fb[0][j][s], acc[0][i][j], 0, 0, 0);
-                    acc[1][i][j] = __builtin_amdgcn_mfma_i32_32x32x32_i8(fa[1][i][s], fb[2][j][s], acc[1][i][j], 0, 0, 0);
-                    acc[2][i][j] = __builtin_amdgcn_mfma_i32_32x32x32_i8(fa[2][i][s], fb[1][j][s], acc[2][i][j], 0, 0, 0);
+                    acc[0][i][j] = __builtin_amdgcn_mfma_i32_32x32x32_i8(fa[0][i], fb[0][j], acc[0][i][j], 0, 0, 0);
+                    acc[1][i][j] = __builtin_amdgcn_mfma_i32_32x32x32_i8(fa[1][i], fb[2][j], acc[1][i][j], 0, 0, 0);
+                    acc[2][i][j] = __builtin_amdgcn_mfma_i32_32x32x32_i8(fa[2][i], fb[1][j], acc[2][i][j], 0, 0, 0);
                     if constexpr (NC == 4)
-                        acc[3][i][j] = __builtin_amdgcn_mfma_i32_32x32x32_i8(fa[2][i][s], fb[2][j][s], acc[3][i][j], 0, 0, 0);
+                        acc[3][i][j] = __builtin_amdgcn_mfma_i32_32x32x32_i8(fa[2][i], fb[2][j], acc[3][i][j], 0, 0, 0);
                 }
+        }
+    };
+
+    // the next step's X loads are in flight during this step's MFMAs (a second set in flight
+    // spills: 153 VGPRs, 3x slower -- measured)
+    const int64_t nsteps = ldk / kKBlock;
+    i32x4 st[kXPerThread];
+    gload(st, 0);
+    lstore(st, 0);
+    lds_barrier();
+    for (int64_t step = 0; step < nsteps; ++step) {
+        const int buf = static_cast<int>(step & 1);
+        if (step + 1 < nsteps) gload(st, (step + 1) * kKBlock);
+        compute(buf);
+        if (step + 1 < nsteps) lstore(st, buf ^ 1);  // buf ^ 1 was last read in step - 1
+        lds_barrier();
     }
+    if (!live) return;
+    const int32_t r0 = ta * kTile + 64 * wa;  // left rows (a)
+    const int32_t c0 = tb * kTile + 64 * wb;  // partner rows (b)
     // epilogue: C/D layout of 32x32 MFMA: col = lane & 31, row = (q & 3) + 8 (q >> 2) + 4 (lane >> 5)
     const double nan = __builtin_nan("");
 #pragma unroll
@@ -135,13 +202,13 @@ __global__ __launch_bounds__(256) void knn_sims_mfma_kernel(
 #pragma unroll
             for (int q = 0; q < 16; ++q) {
                 const int32_t a = r0 + 32 * i + (q & 3) + 8 * (q >> 2) + 4 * half;
-                const int32_t b = c0 + 32 * j + row;
-                if (a >= L || b >= L) continue;
-                if (a == b) {
-                    S[static_cast<int64_t>(a) * L + b] = nan;
+                const int32_t bb = c0 + 32 * j + row;
+                if (a >= L || bb >= L) continue;
+                if (a == bb) {
+                    S[static_cast<int64_t>(a) * L + bb] = nan;
                     continue;
                 }
-                if (ta == tb && a > b) continue;
+                if (ta == tb && a > bb) continue;
                 const int64_t li = acc[0][i][j][q], mi = acc[1][i][j][q], ni = acc[2][i][j][q];
                 double v;
                 if constexpr (KIND == 0) {
@@ -154,9 +221,25 @@ __global__ __launch_bounds__(256) void knn_sims_mfma_kernel(
                     const double count = static_cast<double>(acc[3][i][j][q]);
                     v = 1.0 / (sum / count + 1.0);
                 }
-                S[static_cast<int64_t>(a) * L + b] = v;
-                S[static_cast<int64_t>(b) * L + a] = v;
+                S[static_cast<int64_t>(a) * L + bb] = v;
+                S[static_cast<int64_t>(bb) * L + a] = v;
             }
+}
+
+// Upper-triangle tiles (ta <= tb < T) in 16 x 16 super-tile groups, super-tiles column-major
+// (measured on the ML-20M shape: 10 % less time than plain column-major order; an XCD-striped
+// variant of the groups was slower).
+static std::vector<int2> tile_order(int32_t T) {
+    constexpr int32_t G = 16;
+    std::vector<int2> t;
+    t.reserve(static_cast<size_t>(T) * (T + 1) / 2);
+    const int32_t NS = (T + G - 1) / G;
+    for (int32_t sj = 0; sj < NS; ++sj)
+        for (int32_t si = 0; si <= sj; ++si)
+            for (int32_t b = sj * G; b < std::min(T, (sj + 1) * G); ++b)
+                for (int32_t a = si * G; a < std::min(T, (si + 1) * G); ++a)
+                    if (a <= b) t.push_back(make_int2(a, b));
+    return t;
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -285,7 +368,7 @@ static int int8_scale(const SortedRows& sr) {
         bool ok = true;
         for (double v : sr.r) {
             const double x = v * s;
-            if (!(x == std::floor(x)) || std::fabs(x) > 11.0) {
+            if (!(x == std::floor(x)) || x < 1.0 || x > 11.0) {  // 0 marks "not rated"
                 ok = false;
                 break;
             }
@@ -320,24 +403,29 @@ static void sims_device(rs_ctx* ctx, int32_t kind, int32_t L, int32_t R, const S
         for (int64_t t = 0; t < nnz; ++t) hx[t] = static_cast<int8_t>(sr.r[t] * scale);
         DevBuf<int8_t> dx(std::max<int64_t>(1, nnz));
         dx.upload(hx.data(), nnz, s);
-        DevBuf<int8_t> X(Lp * ldk), X2(Lp * ldk), M(Lp * ldk);
+        DevBuf<int8_t> X(Lp * ldk);
         RS_HIP(hipMemsetAsync(X.p, 0, X.n, s));
-        RS_HIP(hipMemsetAsync(X2.p, 0, X2.n, s));
-        RS_HIP(hipMemsetAsync(M.p, 0, M.n, s));
         hipLaunchKernelGGL(knn_scatter_kernel, dim3(L), dim3(256), 0, s, L, drow.p, dids.p, dx.p,
-                           ldk, X.p, X2.p, M.p);
+                           ldk, X.p);
         RS_HIP(hipGetLastError());
         RS_HIP(hipStreamSynchronize(s));
-        kernel_span_begin(ctx);
         const int32_t T = static_cast<int32_t>(Lp / kTile);
-        const int64_t n_tiles = static_cast<int64_t>(T) * (T + 1) / 2;
+        const std::vector<int2> order = tile_order(T);
+        DevBuf<int2> dtiles(order.size());
+        dtiles.upload(order.data(), order.size(), s);
         const double inv_s2 = 1.0 / static_cast<double>(scale * scale);
+        const size_t lds = 2 * kStageBytes;
+        RS_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(&knn_sims_mfma_kernel<0>),
+                                   hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(lds)));
+        RS_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(&knn_sims_mfma_kernel<1>),
+                                   hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(lds)));
+        kernel_span_begin(ctx);
         if (kind == RS_SIM_COSINE)
-            hipLaunchKernelGGL(knn_sims_mfma_kernel<0>, dim3(n_tiles), dim3(256), 0, s, X.p, X2.p,
-                               M.p, ldk, L, inv_s2, dS.p);
+            hipLaunchKernelGGL(knn_sims_mfma_kernel<0>, dim3(order.size()), dim3(256), lds, s, X.p,
+                               ldk, L, dtiles.p, inv_s2, dS.p);
         else
-            hipLaunchKernelGGL(knn_sims_mfma_kernel<1>, dim3(n_tiles), dim3(256), 0, s, X.p, X2.p,
-                               M.p, ldk, L, inv_s2, dS.p);
+            hipLaunchKernelGGL(knn_sims_mfma_kernel<1>, dim3(order.size()), dim3(256), lds, s, X.p,
+                               ldk, L, dtiles.p, inv_s2, dS.p);
         RS_HIP(hipGetLastError());
         kernel_span_end(ctx);
         return;
