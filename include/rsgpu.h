@@ -13,7 +13,9 @@
  *   rs_knn_sims       <- core/knn.go:143-217   (*KNN).Fit pair loop  (K4 Cosine/MSD, K5 Pearson)
  *                        with core/sim.go:10-81 Cosine / MSD / Pearson as the pair function
  *   rs_sim_pair       <- core/sim.go:7-81      Sim func(a, b SortedIdRatings) float64
- *   rs_svd_predict    <- core/svd.go:32-51     (*SVD).Predict (batched; next-row §8f)
+ *   rs_knn_plan_*     <- core/knn.go:143-217 + knn.go:75-141 (*KNN).Predict on the device (§8f row 2)
+ *   rs_svd_predict    <- core/svd.go:32-51     (*SVD).Predict (batched, host)
+ *   rs_svd_plan_predict / _evaluate <- svd.go:32-51, utils.go:162-180 on the device (§8f row 1)
  *   rs_baseline_fit   <- core/base.go:135-163  (*BaseLine).Fit (used by KNN-baseline knn.go:179)
  *
  * Conventions
@@ -128,6 +130,26 @@ int rs_knn_sims(rs_ctx* ctx, int32_t kind, int32_t n_left, int32_t n_right, cons
 int rs_sim_pair(rs_ctx* ctx, int32_t kind, int64_t na, const int32_t* a_ids, const double* a_r,
                 int64_t nb, const int32_t* b_ids, const double* b_r, double* out);
 
+/* ---- device-resident KNN: similarities stay in HBM, Predict runs on them ---- */
+typedef struct rs_knn_plan rs_knn_plan;
+/* core/knn.go:143-217 pair loop, as rs_knn_sims, keeping the n_left x n_left float64 Sims on the
+ * device (K4 / K5). */
+int rs_knn_plan_create(rs_ctx* ctx, int32_t kind, int32_t n_left, int32_t n_right,
+                       const int64_t* rowptr, const int32_t* ids, const double* ratings,
+                       rs_knn_plan** out);
+void rs_knn_plan_destroy(rs_knn_plan* plan);
+int rs_knn_plan_sims(rs_knn_plan* plan, double* sims /* host, n_left x n_left */);
+/* core/knn.go:75-141 KNN.Predict for n (left, right) inner-id pairs (-1 / out of range = unknown):
+ * candidates RightRatings[right] (right CSR over n_right rows, data order, ids are left ids) with a
+ * non-NaN Sims[left][id]; top-k by (sim desc, position asc) -- the documented tie rule for the
+ * reference's unstable sort.Sort (knn.go:107-108) --; type 0 basic, 1 centered (means), 2 zscore
+ * (means, stddevs), 3 baseline (bias), arrays over left ids.  Bitwise equal to the restatement. */
+int rs_knn_plan_predict(rs_knn_plan* plan, int32_t type, int32_t n_right, const int64_t* right_rowptr,
+                        const int32_t* right_ids, const double* right_r, const double* means,
+                        const double* stddevs, const double* bias, double global_mean, int32_t k,
+                        int32_t min_k, int64_t n, const int32_t* left, const int32_t* right,
+                        double* out);
+
 /* ---- device-resident SVD plan (bench / multi-GPU hosts; device pointers) -------------------- */
 /* A plan uploads the user-CSR once and keeps the model resident in HBM: P (n_users x ld) and
  * Q (n_items x ld) float32 with ld = 64 * ceil((n_factors + 1) / 64); columns [0, n_factors) hold
@@ -179,6 +201,13 @@ int rs_svd_plan_set_timing(rs_svd_plan* plan, int32_t on);
  * stream).  Timing on: sum over the SGD kernels only, n_launches = epochs.  Timing off: the whole
  * enqueued span (SGD + global-bias fold kernels), n_launches = 2 * epochs. */
 int rs_svd_plan_last_kernel_ms(rs_svd_plan* plan, double* ms, int32_t* n_launches);
+/* Batched Predict on the plan's device factors (core/svd.go:32-51 per pair, inner ids, -1 = unknown,
+ * data.go:129), evaluated in float64 on the fp32 factors; and RMSE / MAE over a test set
+ * (core/utils.go:162-180; summed in a fixed order on the device).  SURVEY §8f row 1. */
+int rs_svd_plan_predict(rs_svd_plan* plan, int64_t n, const int32_t* users, const int32_t* items,
+                        double* out);
+int rs_svd_plan_evaluate(rs_svd_plan* plan, int64_t n, const int32_t* users, const int32_t* items,
+                         const double* ratings, double* rmse, double* mae);
 
 #ifdef __cplusplus
 }

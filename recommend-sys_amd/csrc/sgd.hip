@@ -35,6 +35,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cmath>
 #include <cstdlib>
 #include <numeric>
 #include <stdexcept>
@@ -262,6 +263,84 @@ __global__ __launch_bounds__(256) void gb_sum_kernel(const double* __restrict__ 
         __syncthreads();
     }
     if (threadIdx.x == 0) out[0] = s[0];
+}
+
+// --------------------------------------------------------------------------------------------
+// Batched Predict / RMSE / MAE on the plan's device factors.
+// svd.go:32-51 per (user, item) pair, -1 = unknown id (data.go:129): gb + b_u [u known] + b_i
+// [i known] + p_u . q_i [both known], evaluated in float64 on the fp32 factors.  One 16-lane group
+// per pair (lane l sums columns l + 16 x in order, then a fixed DPP tree).  With ratings, the block's
+// squared and absolute errors go to fixed per-block partials (utils.go:162-180), folded in order.
+__global__ __launch_bounds__(256) void svd_predict_kernel(
+    const float* __restrict__ P, const float* __restrict__ Q, int32_t ld, int32_t k, int32_t n_users,
+    int32_t n_items, const double* __restrict__ gb, int64_t n, const int32_t* __restrict__ users,
+    const int32_t* __restrict__ items, const double* __restrict__ ratings, double* __restrict__ out,
+    double* __restrict__ partial) {
+    __shared__ double s_sq[16], s_abs[16];
+    const int gl = threadIdx.x & 15, grp = threadIdx.x >> 4;
+    const int64_t t = static_cast<int64_t>(blockIdx.x) * 16 + grp;
+    double pred = 0.0;
+    if (t < n) {
+        const int32_t u = users[t], i = items[t];
+        const bool ku = u >= 0 && u < n_users, ki = i >= 0 && i < n_items;
+        double d = 0.0;
+        if (ku && ki) {
+            const float* pu = P + static_cast<int64_t>(u) * ld;
+            const float* qi = Q + static_cast<int64_t>(i) * ld;
+            for (int32_t c = gl; c < k; c += 16) d += static_cast<double>(pu[c]) * static_cast<double>(qi[c]);
+        }
+        d += __shfl_xor(d, 1, 16);
+        d += __shfl_xor(d, 2, 16);
+        d += __shfl_xor(d, 4, 16);
+        d += __shfl_xor(d, 8, 16);
+        pred = gb[0];
+        if (ku) pred += static_cast<double>(P[static_cast<int64_t>(u) * ld + ld - 1]);
+        if (ki) pred += static_cast<double>(Q[static_cast<int64_t>(i) * ld + ld - 1]);
+        if (ku && ki) pred += d;
+        if (out && gl == 0) out[t] = pred;
+    }
+    if (partial) {
+        const double e = t < n ? pred - ratings[t] : 0.0;
+        if (gl == 0) {
+            s_sq[grp] = e * e;
+            s_abs[grp] = fabs(e);
+        }
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            double a = 0.0, b = 0.0;
+            for (int x = 0; x < 16; ++x) {
+                a += s_sq[x];
+                b += s_abs[x];
+            }
+            partial[2 * blockIdx.x] = a;
+            partial[2 * blockIdx.x + 1] = b;
+        }
+    }
+}
+
+// out = {sum of even partials, sum of odd partials} in fixed order (one block)
+__global__ __launch_bounds__(256) void pair_sum_kernel(const double* __restrict__ partial, int64_t n_blocks,
+                                                       double* __restrict__ out) {
+    __shared__ double s[2][256];
+    double a = 0.0, b = 0.0;
+    for (int64_t x = threadIdx.x; x < n_blocks; x += 256) {
+        a += partial[2 * x];
+        b += partial[2 * x + 1];
+    }
+    s[0][threadIdx.x] = a;
+    s[1][threadIdx.x] = b;
+    __syncthreads();
+    for (int w = 128; w > 0; w >>= 1) {
+        if (static_cast<int>(threadIdx.x) < w) {
+            s[0][threadIdx.x] += s[0][threadIdx.x + w];
+            s[1][threadIdx.x] += s[1][threadIdx.x + w];
+        }
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) {
+        out[0] = s[0][0];
+        out[1] = s[1][0];
+    }
 }
 
 // --------------------------------------------------------------------------------------------
@@ -958,6 +1037,64 @@ extern "C" int rs_svd_fit(rs_ctx* ctx, const rs_ratings* r, const rs_sgd_params*
         rs::unpack_rows_f64(hQ, r->n_items, k, ld, Q);
         rs::unpack_rows_f64(hbu, r->n_users, 1, 1, bu);
         rs::unpack_rows_f64(hbi, r->n_items, 1, 1, bi);
+        return RS_OK;
+    });
+}
+
+namespace rs {
+// Upload the pairs, run svd_predict_kernel on the plan's factors; out and/or (rmse, mae).
+static void plan_predict(rs_svd_plan* pl, int64_t n, const int32_t* users, const int32_t* items,
+                         const double* ratings, double* out, double* rmse, double* mae) {
+    plan_sync_last(pl);
+    hipStream_t s = pl->ctx->stream;
+    if (n == 0) {
+        if (rmse) *rmse = std::nan("");  // utils.go:169: sqrt(0 / 0)
+        if (mae) *mae = std::nan("");
+        return;
+    }
+    DevBuf<int32_t> du(n), di(n);
+    DevBuf<double> dr(ratings ? n : 0), dout(out ? n : 0);
+    du.upload(users, n, s);
+    di.upload(items, n, s);
+    if (ratings) dr.upload(ratings, n, s);
+    const int64_t blocks = (n + 15) / 16;
+    DevBuf<double> part(ratings ? 2 * blocks : 0), sums(ratings ? 2 : 0);
+    hipLaunchKernelGGL(svd_predict_kernel, dim3(blocks), dim3(256), 0, s, pl->P.p, pl->Q.p, pl->ld, pl->k,
+                       pl->n_users, pl->n_items, pl->gb.p, n, du.p, di.p, dr.p, dout.p, part.p);
+    RS_HIP(hipGetLastError());
+    if (ratings) {
+        hipLaunchKernelGGL(pair_sum_kernel, dim3(1), dim3(256), 0, s, part.p, blocks, sums.p);
+        RS_HIP(hipGetLastError());
+        double h[2];
+        sums.download(h, 2, s);
+        RS_HIP(hipStreamSynchronize(s));
+        if (rmse) *rmse = std::sqrt(h[0] / static_cast<double>(n));
+        if (mae) *mae = h[1] / static_cast<double>(n);
+    }
+    if (out) dout.download(out, n, s);
+    RS_HIP(hipStreamSynchronize(s));
+}
+}  // namespace rs
+
+extern "C" int rs_svd_plan_predict(rs_svd_plan* pl, int64_t n, const int32_t* users,
+                                   const int32_t* items, double* out) {
+    if (!pl) return rs::set_error(nullptr, RS_ERR_INVALID, "plan is NULL");
+    return rs_guard(pl->ctx, [&]() -> int {
+        if (n < 0 || (n > 0 && (!users || !items || !out)))
+            return rs::set_error(pl->ctx, RS_ERR_INVALID, "bad predict arguments");
+        rs::plan_predict(pl, n, users, items, nullptr, out, nullptr, nullptr);
+        return RS_OK;
+    });
+}
+
+extern "C" int rs_svd_plan_evaluate(rs_svd_plan* pl, int64_t n, const int32_t* users,
+                                    const int32_t* items, const double* ratings, double* rmse,
+                                    double* mae) {
+    if (!pl) return rs::set_error(nullptr, RS_ERR_INVALID, "plan is NULL");
+    return rs_guard(pl->ctx, [&]() -> int {
+        if (n < 0 || (n > 0 && (!users || !items || !ratings)) || (!rmse && !mae))
+            return rs::set_error(pl->ctx, RS_ERR_INVALID, "bad evaluate arguments");
+        rs::plan_predict(pl, n, users, items, ratings, nullptr, rmse, mae);
         return RS_OK;
     });
 }

@@ -450,6 +450,112 @@ static void sims_device(rs_ctx* ctx, int32_t kind, int32_t L, int32_t R, const S
     kernel_span_end(ctx);
 }
 
+// ---------------------------------------------------------------------------------------------
+// KNN.Predict on the device (core/knn.go:75-141).  One wave per (left, right)
+// query: candidates are RightRatings[right] (data order) with a non-NaN similarity (knn.go:93-99);
+// at most min_k of them -> GlobalMean (knn.go:102-104); otherwise the top min(k, count) by
+// (similarity desc, position asc) -- the documented tie rule for the reference's unstable
+// sort.Sort (knn.go:107-108) -- are taken one per round by a wave arg-max below the previous pick,
+// and lane 0 accumulates weightSum / weightRating in exactly that order with the type-specific
+// centring (knn.go:116-140), so every output is bitwise equal to the restatement.
+constexpr int kPredCache = 4096;  // candidate similarities cached in LDS per query
+
+__global__ __launch_bounds__(64) void knn_predict_kernel(
+    const double* __restrict__ S, int32_t L, int32_t n_right, const int64_t* __restrict__ rrp,
+    const int32_t* __restrict__ rids, const double* __restrict__ rr, const double* __restrict__ means,
+    const double* __restrict__ stddevs, const double* __restrict__ bias, double gmean, int32_t type,
+    int32_t k, int32_t min_k, int64_t n, const int32_t* __restrict__ left,
+    const int32_t* __restrict__ right, double* __restrict__ out) {
+    __shared__ double cache[kPredCache];
+    const int64_t qi = blockIdx.x;
+    if (qi >= n) return;
+    const int lane = threadIdx.x;
+    const int32_t li = left[qi], ri = right[qi];
+    if (li < 0 || li >= L || ri < 0 || ri >= n_right) {  // knn.go:89-91
+        if (lane == 0) out[qi] = gmean;
+        return;
+    }
+    const double* srow = S + static_cast<int64_t>(li) * L;
+    const int64_t b = rrp[ri];
+    const int32_t m = static_cast<int32_t>(rrp[ri + 1] - b);
+    auto sim_at = [&](int32_t t) { return t < kPredCache ? cache[t] : srow[rids[b + t]]; };
+    int32_t cnt = 0;
+    for (int32_t t = lane; t < m; t += 64) {
+        const double v = srow[rids[b + t]];
+        if (t < kPredCache) cache[t] = v;
+        cnt += !isnan(v);
+    }
+    for (int off = 32; off > 0; off >>= 1) cnt += __shfl_xor(cnt, off);
+    __syncthreads();
+    if (cnt <= min_k) {
+        if (lane == 0) out[qi] = gmean;
+        return;
+    }
+    const int32_t nn = min(k, cnt);
+    double ps = 0.0;
+    int32_t pp = -1;  // previous pick; -1: none yet
+    double weightSum = 0.0, weightRating = 0.0;
+    for (int32_t j = 0; j < nn; ++j) {
+        bool found = false;
+        double bs = 0.0;
+        int32_t bp = 0;
+        for (int32_t t = lane; t < m; t += 64) {
+            const double v = sim_at(t);
+            if (isnan(v)) continue;
+            const bool below = pp < 0 || v < ps || (v == ps && t > pp);
+            if (below && (!found || v > bs)) {  // strided t ascending: ties keep the first
+                found = true;
+                bs = v;
+                bp = t;
+            }
+        }
+        for (int off = 32; off > 0; off >>= 1) {
+            const int of = __shfl_xor(static_cast<int>(found), off);
+            const double os = __shfl_xor(bs, off);
+            const int32_t op = __shfl_xor(bp, off);
+            if (of && (!found || os > bs || (os == bs && op < bp))) {
+                found = true;
+                bs = os;
+                bp = op;
+            }
+        }
+        ps = bs;
+        pp = bp;
+        if (lane == 0) {  // knn.go:118-130 in pick order
+            const int32_t id = rids[b + bp];
+            weightSum += bs;
+            double rating = rr[b + bp];
+            if (type == 1) rating -= means[id];
+            else if (type == 2) rating = (rating - means[id]) / stddevs[id];
+            else if (type == 3) rating -= bias[id];
+            weightRating += bs * rating;
+        }
+    }
+    if (lane == 0) {
+        double prediction = weightRating / weightSum;  // knn.go:131-139
+        if (type == 1) prediction += means[li];
+        else if (type == 3) prediction += bias[li];
+        else if (type == 2) {
+            prediction *= stddevs[li];
+            prediction += means[li];
+        }
+        out[qi] = prediction;
+    }
+}
+
+// Validates a left CSR (rowptr monotone, ids in [0, n_right)) for rs_knn_sims / plan creation.
+static int check_knn_csr(rs_ctx* ctx, int32_t n_left, int32_t n_right, const int64_t* rowptr,
+                         const int32_t* ids, const double* ratings) {
+    if (n_left < 0 || n_right < 0 || !rowptr) return set_error(ctx, RS_ERR_INVALID, "bad knn arguments");
+    const int64_t nnz = rowptr[n_left] - rowptr[0];
+    if (nnz > 0 && (!ids || !ratings)) return set_error(ctx, RS_ERR_INVALID, "ids/ratings NULL");
+    for (int32_t a = 0; a < n_left; ++a)
+        if (rowptr[a + 1] < rowptr[a]) return set_error(ctx, RS_ERR_INVALID, "rowptr not monotone");
+    for (int64_t t = rowptr[0]; t < rowptr[n_left]; ++t)
+        if (ids[t] < 0 || ids[t] >= n_right) return set_error(ctx, RS_ERR_INVALID, "id out of range");
+    return RS_OK;
+}
+
 }  // namespace rs
 
 extern "C" int rs_knn_sims(rs_ctx* ctx, int32_t kind, int32_t n_left, int32_t n_right,
@@ -459,14 +565,9 @@ extern "C" int rs_knn_sims(rs_ctx* ctx, int32_t kind, int32_t n_left, int32_t n_
     return rs_guard(ctx, [&]() -> int {
         if (kind < RS_SIM_COSINE || kind > RS_SIM_PEARSON)
             return rs::set_error(ctx, RS_ERR_INVALID, "unknown similarity kind");
-        if (n_left < 0 || n_right < 0 || !rowptr || (n_left > 0 && !sims))
-            return rs::set_error(ctx, RS_ERR_INVALID, "bad knn arguments");
-        const int64_t nnz = rowptr[n_left] - rowptr[0];
-        if (nnz > 0 && (!ids || !ratings)) return rs::set_error(ctx, RS_ERR_INVALID, "ids/ratings NULL");
-        for (int32_t a = 0; a < n_left; ++a)
-            if (rowptr[a + 1] < rowptr[a]) return rs::set_error(ctx, RS_ERR_INVALID, "rowptr not monotone");
-        for (int64_t t = rowptr[0]; t < rowptr[n_left]; ++t)
-            if (ids[t] < 0 || ids[t] >= n_right) return rs::set_error(ctx, RS_ERR_INVALID, "id out of range");
+        if (n_left > 0 && !sims) return rs::set_error(ctx, RS_ERR_INVALID, "sims is NULL");
+        const int st = rs::check_knn_csr(ctx, n_left, n_right, rowptr, ids, ratings);
+        if (st != RS_OK) return st;
         rs::SortedRows sr;
         rs::sort_rows(n_left, rowptr, ids, ratings, sr);
         rs::DevBuf<double> dS;
@@ -506,6 +607,106 @@ extern "C" int rs_sim_pair(rs_ctx* ctx, int32_t kind, int64_t na, const int32_t*
         dS.download(S, 4, ctx->stream);
         RS_HIP(hipStreamSynchronize(ctx->stream));
         *out = S[1];
+        return RS_OK;
+    });
+}
+
+// ------------------------------------------------------------------------------------------------
+// Device-resident KNN (similarities stay in HBM; Predict runs on them)
+
+struct rs_knn_plan {
+    rs_ctx* ctx = nullptr;
+    int32_t L = 0;
+    rs::DevBuf<double> S;
+};
+
+extern "C" int rs_knn_plan_create(rs_ctx* ctx, int32_t kind, int32_t n_left, int32_t n_right,
+                                  const int64_t* rowptr, const int32_t* ids, const double* ratings,
+                                  rs_knn_plan** out) {
+    if (!ctx) return rs::set_error(ctx, RS_ERR_INVALID, "ctx is NULL");
+    return rs_guard(ctx, [&]() -> int {
+        if (!out) return rs::set_error(ctx, RS_ERR_INVALID, "out is NULL");
+        *out = nullptr;
+        if (kind < RS_SIM_COSINE || kind > RS_SIM_PEARSON)
+            return rs::set_error(ctx, RS_ERR_INVALID, "unknown similarity kind");
+        const int st = rs::check_knn_csr(ctx, n_left, n_right, rowptr, ids, ratings);
+        if (st != RS_OK) return st;
+        auto* pl = new rs_knn_plan();
+        try {
+            pl->ctx = ctx;
+            pl->L = n_left;
+            rs::SortedRows sr;
+            rs::sort_rows(n_left, rowptr, ids, ratings, sr);
+            const char* env = std::getenv("RSGPU_KNN_NO_MFMA");
+            rs::sims_device(ctx, kind, n_left, n_right, sr, !(env && env[0] == '1'), pl->S);
+            RS_HIP(hipStreamSynchronize(ctx->stream));
+        } catch (...) {
+            delete pl;
+            throw;
+        }
+        *out = pl;
+        return RS_OK;
+    });
+}
+
+extern "C" void rs_knn_plan_destroy(rs_knn_plan* pl) {
+    if (!pl) return;
+    (void)hipSetDevice(pl->ctx->device);
+    delete pl;
+}
+
+extern "C" int rs_knn_plan_sims(rs_knn_plan* pl, double* sims) {
+    if (!pl) return rs::set_error(nullptr, RS_ERR_INVALID, "plan is NULL");
+    return rs_guard(pl->ctx, [&]() -> int {
+        if (pl->L > 0 && !sims) return rs::set_error(pl->ctx, RS_ERR_INVALID, "sims is NULL");
+        pl->S.download(sims, static_cast<int64_t>(pl->L) * pl->L, pl->ctx->stream);
+        RS_HIP(hipStreamSynchronize(pl->ctx->stream));
+        return RS_OK;
+    });
+}
+
+extern "C" int rs_knn_plan_predict(rs_knn_plan* pl, int32_t type, int32_t n_right,
+                                   const int64_t* right_rowptr, const int32_t* right_ids,
+                                   const double* right_r, const double* means,
+                                   const double* stddevs, const double* bias, double global_mean,
+                                   int32_t k, int32_t min_k, int64_t n, const int32_t* left,
+                                   const int32_t* right, double* out) {
+    if (!pl) return rs::set_error(nullptr, RS_ERR_INVALID, "plan is NULL");
+    rs_ctx* ctx = pl->ctx;
+    return rs_guard(ctx, [&]() -> int {
+        if (type < 0 || type > 3) return rs::set_error(ctx, RS_ERR_INVALID, "unknown KNN type");
+        if (n < 0 || n > INT32_MAX || (n > 0 && (!left || !right || !out)) || k < 0)
+            return rs::set_error(ctx, RS_ERR_INVALID, "bad predict arguments");
+        if ((type == 1 || type == 2) && !means) return rs::set_error(ctx, RS_ERR_INVALID, "means NULL");
+        if (type == 2 && !stddevs) return rs::set_error(ctx, RS_ERR_INVALID, "stddevs NULL");
+        if (type == 3 && !bias) return rs::set_error(ctx, RS_ERR_INVALID, "bias NULL");
+        const int st = rs::check_knn_csr(ctx, n_right, pl->L, right_rowptr, right_ids, right_r);
+        if (st != RS_OK) return st;
+        if (n == 0) return RS_OK;
+        hipStream_t s = ctx->stream;
+        const int64_t base = right_rowptr[0], nnz = right_rowptr[n_right] - base;
+        std::vector<int64_t> rp(right_rowptr, right_rowptr + n_right + 1);
+        for (auto& x : rp) x -= base;
+        rs::DevBuf<int64_t> drp(rp.size());
+        rs::DevBuf<int32_t> dids(std::max<int64_t>(1, nnz)), dl(n), dr(n);
+        rs::DevBuf<double> drr(std::max<int64_t>(1, nnz)), dout(n);
+        rs::DevBuf<double> dm(means ? pl->L : 0), dsd(stddevs ? pl->L : 0), db(bias ? pl->L : 0);
+        drp.upload(rp.data(), rp.size(), s);
+        dids.upload(right_ids + base, nnz, s);
+        drr.upload(right_r + base, nnz, s);
+        dl.upload(left, n, s);
+        dr.upload(right, n, s);
+        if (means) dm.upload(means, pl->L, s);
+        if (stddevs) dsd.upload(stddevs, pl->L, s);
+        if (bias) db.upload(bias, pl->L, s);
+        rs::kernel_span_begin(ctx);
+        hipLaunchKernelGGL(rs::knn_predict_kernel, dim3(static_cast<uint32_t>(n)), dim3(64), 0, s,
+                           pl->S.p, pl->L, n_right, drp.p, dids.p, drr.p, dm.p, dsd.p, db.p,
+                           global_mean, type, k, min_k, n, dl.p, dr.p, dout.p);
+        RS_HIP(hipGetLastError());
+        rs::kernel_span_end(ctx);
+        dout.download(out, n, s);
+        RS_HIP(hipStreamSynchronize(s));
         return RS_OK;
     });
 }

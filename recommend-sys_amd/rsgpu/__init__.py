@@ -31,6 +31,8 @@ HEADER_SYMBOLS = (
     "rs_svd_plan_device_ptrs", "rs_svd_plan_set_mode", "rs_svd_plan_set_split",
     "rs_svd_plan_set_item_split", "rs_svd_plan_set_timing", "rs_svd_plan_set_user_weights",
     "rs_svd_plan_epoch_delta", "rs_svd_plan_apply_delta", "rs_svd_plan_last_kernel_ms",
+    "rs_svd_plan_predict", "rs_svd_plan_evaluate",
+    "rs_knn_plan_create", "rs_knn_plan_destroy", "rs_knn_plan_sims", "rs_knn_plan_predict",
 )
 
 
@@ -97,6 +99,13 @@ def lib():
             "rs_svd_plan_apply_delta": (C.c_int, [_vp, _vp, _vp, _dbl, _vp]),
             "rs_svd_plan_set_timing": (C.c_int, [_vp, _i32]),
             "rs_svd_plan_last_kernel_ms": (C.c_int, [_vp, C.POINTER(_dbl), C.POINTER(_i32)]),
+            "rs_svd_plan_predict": (C.c_int, [_vp, _i64, _vp, _vp, _vp]),
+            "rs_knn_plan_create": (C.c_int, [_vp, _i32, _i32, _i32, _vp, _vp, _vp, C.POINTER(_vp)]),
+            "rs_knn_plan_destroy": (None, [_vp]),
+            "rs_knn_plan_sims": (C.c_int, [_vp, _vp]),
+            "rs_knn_plan_predict": (C.c_int, [_vp, _i32, _i32, _vp, _vp, _vp, _vp, _vp, _vp, _dbl,
+                                              _i32, _i32, _i64, _vp, _vp, _vp]),
+            "rs_svd_plan_evaluate": (C.c_int, [_vp, _i64, _vp, _vp, _vp, C.POINTER(_dbl), C.POINTER(_dbl)]),
         }
         for name, (res, args) in sig.items():
             f = getattr(L, name)
@@ -250,6 +259,9 @@ class Context:
     def svd_plan(self, r: Ratings, n_factors: int) -> "SvdPlan":
         return SvdPlan(self, r, n_factors)
 
+    def knn_plan(self, kind, rowptr, ids, ratings, n_right) -> "KnnPlan":
+        return KnnPlan(self, kind, rowptr, ids, ratings, n_right)
+
 
 class SvdPlan:
     """Device-resident user-CSR + factors (rs_svd_plan_*)."""
@@ -329,6 +341,22 @@ class SvdPlan:
         self.ctx.check(lib().rs_svd_plan_last_kernel_ms(self.h, C.byref(ms), C.byref(n)))
         return ms.value, n.value
 
+    def predict(self, users, items):
+        """svd.go:32-51 on the device factors for inner-id pairs (-1 = unknown)."""
+        u, i = np.ascontiguousarray(users, np.int32), np.ascontiguousarray(items, np.int32)
+        out = np.empty(len(u))
+        self.ctx.check(lib().rs_svd_plan_predict(self.h, len(u), _ptr(u), _ptr(i), _ptr(out)))
+        return out
+
+    def evaluate(self, users, items, ratings):
+        """(RMSE, MAE) over a test set (utils.go:162-180) on the device."""
+        u, i = np.ascontiguousarray(users, np.int32), np.ascontiguousarray(items, np.int32)
+        r = np.ascontiguousarray(ratings, np.float64)
+        a, b = _dbl(0), _dbl(0)
+        self.ctx.check(lib().rs_svd_plan_evaluate(self.h, len(u), _ptr(u), _ptr(i), _ptr(r),
+                                                  C.byref(a), C.byref(b)))
+        return a.value, b.value
+
     def close(self):
         if self.h:
             lib().rs_svd_plan_destroy(self.h)
@@ -350,3 +378,49 @@ def svd_predict(users, items, P, Q, bu, bi, gb):
     _check(lib().rs_svd_predict(None, len(u), _ptr(u), _ptr(i), P.shape[0], Q.shape[0],
                                 P.shape[1], _ptr(P), _ptr(Q), _ptr(bu), _ptr(bi), gb, _ptr(out)))
     return out
+
+
+class KnnPlan:
+    """Device-resident KNN similarities with Predict on the device (rs_knn_plan_*)."""
+
+    TYPES = {"basic": 0, "centered": 1, "zscore": 2, "baseline": 3}
+
+    def __init__(self, ctx: Context, kind, rowptr, ids, ratings, n_right):
+        self.ctx = ctx
+        rowptr = np.ascontiguousarray(rowptr, dtype=np.int64)
+        ids = np.ascontiguousarray(ids, dtype=np.int32)
+        ratings = np.ascontiguousarray(ratings, dtype=np.float64)
+        self.L = len(rowptr) - 1
+        h = C.c_void_p()
+        self.h = None
+        ctx.check(lib().rs_knn_plan_create(ctx.h, kind, self.L, n_right, _ptr(rowptr), _ptr(ids),
+                                           _ptr(ratings), C.byref(h)))
+        self.h = h
+        ctx._plans.add(self)
+
+    def sims(self):
+        out = np.empty((self.L, self.L))
+        self.ctx.check(lib().rs_knn_plan_sims(self.h, _ptr(out)))
+        return out
+
+    def predict(self, knn_type, right_rowptr, right_ids, right_r, left, right, global_mean,
+                means=None, stddevs=None, bias=None, k=40, min_k=1):
+        """core/knn.go:75-141 for (left, right) inner-id pairs on the device."""
+        t = self.TYPES[knn_type] if isinstance(knn_type, str) else int(knn_type)
+        rp = np.ascontiguousarray(right_rowptr, dtype=np.int64)
+        ri = np.ascontiguousarray(right_ids, dtype=np.int32)
+        rr = np.ascontiguousarray(right_r, dtype=np.float64)
+        lq = np.ascontiguousarray(left, dtype=np.int32)
+        rq = np.ascontiguousarray(right, dtype=np.int32)
+        arrs = [None if a is None else np.ascontiguousarray(a, dtype=np.float64)
+                for a in (means, stddevs, bias)]
+        out = np.empty(len(lq))
+        self.ctx.check(lib().rs_knn_plan_predict(self.h, t, len(rp) - 1, _ptr(rp), _ptr(ri), _ptr(rr),
+                                                 *[_ptr(a) for a in arrs], float(global_mean), k, min_k,
+                                                 len(lq), _ptr(lq), _ptr(rq), _ptr(out)))
+        return out
+
+    def close(self):
+        if self.h:
+            lib().rs_knn_plan_destroy(self.h)
+            self.h = None

@@ -132,3 +132,34 @@ def test_baseline_fit_bitwise(ctx, ml100k):
     ref = O.baseline_fit(f.iu, f.ii, f.r, f.nu, f.ni)
     got = ctx.baseline_fit(rsgpu.Ratings(f.iu, f.ii, f.r, f.nu, f.ni))
     assert np.array_equal(ref[0], got[0]) and np.array_equal(ref[1], got[1]) and ref[2] == got[2]
+
+
+@pytest.mark.parametrize("kind", [rsgpu.SIM_COSINE, rsgpu.SIM_PEARSON])
+@pytest.mark.parametrize("user_based", [True, False])
+def test_knn_plan_predict_bitwise(ctx, ml100k, kind, user_based):
+    """KNN.Predict (knn.go:75-141) on the device-resident Sims equals the
+    restatement bit for bit for all four KNN types, on fold 0 of ML-100K (train -> test pairs,
+    unknown ids included), with the reference defaults k=40, mink=1 and a tight k=3 / mink=5."""
+    from helpers import folds
+    f = folds(*ml100k)[0]
+    u, i, r = f.iu, f.ii, f.r
+    left_key, right_key = (u, i) if user_based else (i, u)
+    nl, nr = (f.nu, f.ni) if user_based else (f.ni, f.nu)
+    lrp, lids, lr = O.csr_by(left_key, nl, right_key, r)
+    rrp, rids, rr = O.csr_by(right_key, nr, left_key, r)
+    plan = ctx.knn_plan(kind, lrp, lids, lr, nr)
+    S = plan.sims()
+    deg = np.diff(lrp).astype(float)
+    means = np.add.reduceat(lr, lrp[:-1]) / np.maximum(deg, 1)      # data.go:222-235
+    dev = (lr - np.repeat(means, np.diff(lrp))) ** 2
+    stds = np.sqrt(np.add.reduceat(dev, lrp[:-1]) / np.maximum(deg, 1)) + 1e-5  # knn.go:167-177
+    bu, bi, _ = O.baseline_fit(u, i, r, f.nu, f.ni)
+    bias = bu if user_based else bi
+    ql, qr = (f.tu, f.ti) if user_based else (f.ti, f.tu)
+    gm = float(np.mean(r))
+    for t, name in enumerate(["basic", "centered", "zscore", "baseline"]):
+        for k, mink in [(40, 1), (3, 5)]:
+            got = plan.predict(name, rrp, rids, rr, ql, qr, gm, means, stds, bias, k=k, min_k=mink)
+            ref = O.knn_predict(t, S, rrp, rids, rr, means, stds, bias, gm, k, mink, ql, qr)
+            assert bitwise_equal(got, ref), (name, k, mink)
+    plan.close()

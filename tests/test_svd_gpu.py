@@ -312,3 +312,26 @@ def test_item_sharded_delta_mode_two_shards(ctx):
         np.testing.assert_allclose(bi[mine], ref[s].bi[mine], atol=TOL)
         assert abs(gb - ref[s].gb) < TOL
         pl.close()
+
+
+def test_plan_predict_and_evaluate_on_device(ctx, ml100k):
+    """batched Predict (svd.go:32-51, unknown ids -> newID rules) and RMSE / MAE
+    (utils.go:162-180) on the device factors equal the host restatement on the same factors."""
+    f = folds(*ml100k)[0]
+    k = 100
+    rng = np.random.default_rng(7)
+    plan = ctx.svd_plan(rsgpu.Ratings(f.iu, f.ii, f.r, f.nu, f.ni), k)
+    plan.upload(rng.normal(0, 0.1, (f.nu, k)), rng.normal(0, 0.1, (f.ni, k)), np.zeros(f.nu),
+                np.zeros(f.ni), 3.5)
+    plan.epochs(3)
+    model = plan.download()
+    tu, ti = f.tu.copy(), f.ti.copy()
+    tu[:50], ti[50:100], tu[100:110], ti[100:110] = -1, -1, f.nu + 5, -1  # unknown users / items
+    host = rsgpu.svd_predict(tu, ti, *model)
+    dev = plan.predict(tu, ti)
+    np.testing.assert_allclose(dev, host, rtol=1e-12, atol=1e-12)
+    assert np.all(dev[100:110] == model[4])  # both unknown: GlobalBias only
+    e_rmse, e_mae = plan.evaluate(tu, ti, f.te_r)
+    assert abs(e_rmse - rmse(host, f.te_r)) <= 1e-12 and abs(e_mae - float(np.mean(np.abs(host - f.te_r)))) <= 1e-12
+    assert np.isnan(plan.evaluate([], [], [])[0])
+    plan.close()
