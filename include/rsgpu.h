@@ -51,8 +51,10 @@ extern "C" {
 #define RS_SGD_ORDERED 1 /* single group, exact train-set order and update order of svd.go:93-129 */
 
 /* FAST-mode write-back of the item rows (rs_svd_plan_set_mode) */
-#define RS_SGD_WB_ATOMIC 0 /* float-atomic deltas at the memory side: no lost updates (default) */
-#define RS_SGD_WB_STORE 1  /* write-through stores: Hogwild, concurrent updates of a row can be lost */
+#define RS_SGD_WB_ATOMIC 0        /* float-atomic deltas at the memory side, no lost updates (default);
+                                    heavy users' deltas go through LDS rings to writer waves */
+#define RS_SGD_WB_STORE 1         /* write-through stores: Hogwild, concurrent updates of a row can be lost */
+#define RS_SGD_WB_ATOMIC_DIRECT 2 /* the same atomic deltas issued by each compute wave itself */
 
 /* Similarity kinds: core/sim.go Cosine (10-25), MSD (28-44), Pearson (47-81) */
 #define RS_SIM_COSINE 0
@@ -78,7 +80,7 @@ typedef struct {
     double lr;         /* "lr"       */
     double reg;        /* "reg"      */
     int32_t mode;      /* RS_SGD_FAST or RS_SGD_ORDERED */
-    int32_t write_back; /* FAST only: RS_SGD_WB_ATOMIC (0, default) or RS_SGD_WB_STORE */
+    int32_t write_back; /* FAST only: RS_SGD_WB_* (RS_SGD_WB_ATOMIC = 0 is the default) */
 } rs_sgd_params;
 
 /* ---- context -------------------------------------------------------------------------------- */
@@ -166,9 +168,19 @@ int rs_svd_plan_download(rs_svd_plan* plan, double* P, double* Q, double* bu, do
                          double* gb);
 /* Enqueue n_epochs fast-mode epochs (one SGD kernel + one global-bias fold per epoch). */
 int rs_svd_plan_epochs(rs_svd_plan* plan, int32_t n_epochs, float lr, float reg, void* stream);
-/* write_back: RS_SGD_WB_ATOMIC (default) or RS_SGD_WB_STORE; ring_depth: item-row prefetch distance
+/* write_back: RS_SGD_WB_ATOMIC (default), _STORE or _ATOMIC_DIRECT; ring_depth: item-row prefetch distance
  * in ratings (4, 8 = default, 16). */
 int rs_svd_plan_set_mode(rs_svd_plan* plan, int32_t write_back, int32_t ring_depth);
+/* RS_SGD_WB_ATOMIC schedule.  Work items with at least heavy_min ratings (default 1024; 0 = none) run
+ * as one SGD wave plus three writer waves that issue its atomics; the other (light) items are
+ * strided over light_blocks blocks of four waves (default < 0: 1.5 per CU; 0: one wave per item).
+ * Same arithmetic and results class as RS_SGD_WB_ATOMIC_DIRECT; only the visit timing changes
+ * (DESIGN.md K1). */
+int rs_svd_plan_set_schedule(rs_svd_plan* plan, int32_t heavy_min, int32_t light_blocks);
+/* Diagnostic: out == NULL enables a per-work-item timeline for RS_SGD_WB_ATOMIC epochs; otherwise
+ * copies the last epoch's {start, chain end, write-back end} (100 MHz ticks, 3 int64 per work item, LPT
+ * order) to out and the work items' users to user (may be NULL). */
+int rs_svd_plan_trace(rs_svd_plan* plan, int64_t* out, int32_t* user);
 /* FAST-mode work items: users with more than split_cap ratings (default 0 = never split) run as
  * ceil(deg / split_cap) near-equal pieces on separate waves from the same p_u, and the row becomes the
  * count-weighted average of the pieces' end states after the epoch (or_svd_fit_chunked restates it).

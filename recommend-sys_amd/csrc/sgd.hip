@@ -48,6 +48,7 @@ namespace rs {
 
 constexpr int32_t kOutOfRange = 0x7FFFFFF0;  // buffer offset past num_records: load 0 / drop store
 constexpr int kSgdAux = 16;                  // sc1
+constexpr int kVolatileAux = static_cast<int>(0x80000000u);  // buffer intrinsic aux bit 31: volatile
 
 // Sum over the 64 lanes of a wave: DPP inside each 16-lane row, then the gfx950 permlane swaps
 // across rows.  Every lane ends with the bitwise-identical total.
@@ -63,9 +64,135 @@ __device__ __forceinline__ float lane63(float x) {
     return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(x), 63));
 }
 
-// FAST epoch kernel (K1).  Item ids and ratings are wave-uniform: read 16 at a time with scalar
-// loads one batch ahead, so row addresses are SGPR arithmetic.  The 16-rating batch loop is
-// unrolled so every ring index is a compile-time constant.
+// One FAST work item (a user row or a piece of one): the SGD chain over its ratings with p_u in
+// VGPRs.  Every q_i update is handed to emit(row byte offset, q_new, q_old); the kernels below
+// differ only in how that update reaches memory.  Returns n * (gb_end - gb_start) for the fold.
+template <int E, int D, class Emit>
+__device__ __forceinline__ double sgd_work_item(
+    int32_t w, const int32_t* __restrict__ wk_user, const int64_t* __restrict__ wk_rng,
+    const float* __restrict__ wk_frac, const int32_t* __restrict__ items,
+    const float* __restrict__ ratings, float* __restrict__ P, __amdgpu_buffer_rsrc_t rq, float gb0,
+    float lr, float reg, float* __restrict__ dP, const float* __restrict__ uw, int32_t whole_direct,
+    Emit&& emit) {
+#pragma clang fp contract(fast)
+    constexpr int LD = 64 * E, B = 32;  // ratings per chunk (one unrolled loop body)
+    static_assert(B % D == 0 && D <= B, "ring depth must divide the 32-rating chunk");
+    const int lane = threadIdx.x & 63;
+    const int32_t lane4 = lane * 4;
+    const bool bias_lane = lane == 63;
+    const float a = 1.f - lr * reg;
+    const int32_t u = wk_user[w];
+    const int64_t b = wk_rng[2 * w], e = wk_rng[2 * w + 1];
+    const float frac = wk_frac[w];
+    float p[E];
+    float* prow = P + static_cast<int64_t>(u) * LD;
+#pragma unroll
+    for (int x = 0; x < E; ++x) p[x] = prow[lane + 64 * x];
+    float ub = lane63(p[E - 1]);
+    float gb = gb0;
+
+    auto load_row = [&](float (&q)[E], int32_t valid, int32_t item) {
+        const int32_t row = valid ? item * (LD * 4) : kOutOfRange;  // SGPR arithmetic
+#pragma unroll
+        for (int x = 0; x < E; ++x)
+            q[x] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rq, row + lane4 + 256 * x, 0, kSgdAux));
+    };
+
+    // Item ids and ratings come in 32-entry chunks, one vector load per chunk (lane l holds entry
+    // l & 31), issued a chunk ahead and read out with v_readlane: no scalar-memory wait sits in the
+    // chain (a per-batch s_load round trip, several microseconds while the memory side is
+    // saturated with atomics, was measured to set the heavy users' pace).  The loop body is two
+    // whole chunks with fixed register sets A and B, so every ring slot and readlane index is a
+    // compile-time constant and no register holding an in-flight load is ever copied (a rotating
+    // copy made the compiler drain the ring at every chunk).
+    const int32_t deg = static_cast<int32_t>(e - b);
+    const int32_t l32 = lane & 31;
+    // through buffer loads marked volatile (aux bit 31): LLVM would otherwise sink the chunk loads
+    // to the end of the next chunk, next to their first use, and every chunk would wait for them
+    const int32_t nrec = (deg + 128) * 4;  // arrays padded by 128 entries
+    const __amdgpu_buffer_rsrc_t ri = __builtin_amdgcn_make_buffer_rsrc(const_cast<int32_t*>(items + b), 0, nrec, 0x00020000);
+    const __amdgpu_buffer_rsrc_t rr = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(ratings + b), 0, nrec, 0x00020000);
+    auto ld_item = [&](int32_t pos) {
+        return static_cast<int32_t>(__builtin_amdgcn_raw_buffer_load_b32(ri, (pos + l32) * 4, 0, kVolatileAux));
+    };
+    auto ld_rating = [&](int32_t pos) {
+        return __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rr, (pos + l32) * 4, 0, kVolatileAux));
+    };
+    int32_t viA = ld_item(0), viB = ld_item(B);
+    float vrA = ld_rating(0), vrB = ld_rating(B);
+    // the first two chunks land before the ring loads (an asm that reads them forces the wait
+    // here), so the loop header never inherits a just-issued load from the preheader
+    asm volatile("" ::"v"(viA), "v"(viB), "v"(vrA), "v"(vrB));
+    float ring[D][E];
+#pragma unroll
+    for (int s = 0; s < D; ++s) {  // in slot order (the loop's waits assume it)
+        load_row(ring[s], s < deg, __builtin_amdgcn_readlane(viA, s));
+        __builtin_amdgcn_sched_barrier(0);
+    }
+
+    // the ratings [base, base + B) of the chunk held in (vi, vr); vn holds the next chunk's items
+    auto chunk = [&](int64_t base, int32_t vi, float vr, int32_t vn) {
+        const int32_t rem = static_cast<int32_t>(e - base);  // wave-uniform, SALU compares
+#pragma unroll
+        for (int j = 0; j < B; ++j) {
+            constexpr int kD = D;
+            const int slot = j % kD;
+            if (j < rem) {
+                float(&q)[E] = ring[slot];
+                const float bq = lane63(q[E - 1]);
+                const float rt = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(vr), j));
+                float s = 0.f;
+#pragma unroll
+                for (int x = 0; x < E - 1; ++x) s += p[x] * q[x];
+                s += p[E - 1] * (bias_lane ? 0.f : q[E - 1]);
+                s = wave_sum(s);
+                // svd.go:102-128 in FMA form: a = 1 - lr*reg, c = lr*diff:
+                // p <- a p - c q ; q <- a q - c p_new ; b <- a b - c ; gb <- gb - c
+                const float diff = ((gb + ub) + bq) + s - rt;
+                const float c = lr * diff;
+                gb -= c;
+                ub = __builtin_fmaf(ub, a, -c);
+                const float bq_new = __builtin_fmaf(bq, a, -c);
+                float qn[E];
+#pragma unroll
+                for (int x = 0; x < E; ++x) {
+                    p[x] = __builtin_fmaf(-c, q[x], p[x] * a);
+                    qn[x] = __builtin_fmaf(-c, p[x], q[x] * a);
+                }
+                p[E - 1] = bias_lane ? ub : p[E - 1];
+                qn[E - 1] = bias_lane ? bq_new : qn[E - 1];
+                emit(__builtin_amdgcn_readlane(vi, j) * (LD * 4), qn, q);
+            }
+            // refill this slot with the rating D ahead
+            const int jn = j + D;
+            load_row(ring[slot], jn < rem, jn < B ? __builtin_amdgcn_readlane(vi, jn % B)
+                                                  : __builtin_amdgcn_readlane(vn, jn % B));
+        }
+    };
+    // chunk loads two ahead stay inside the padding: base + 4B - 1 < e + 127
+    for (int32_t o = 0; o < deg; o += 2 * B) {
+        chunk(b + o, viA, vrA, viB);
+        viA = ld_item(o + 2 * B);
+        vrA = ld_rating(o + 2 * B);
+        if (o + B >= deg) break;
+        chunk(b + o + B, viB, vrB, viA);
+        viB = ld_item(o + 3 * B);
+        vrB = ld_rating(o + 3 * B);
+    }
+    if (dP && !(whole_direct && frac == 1.f)) {  // weighted delta, P stays at the epoch start
+        const float sc = uw ? frac * uw[u] : frac;
+        float* drow = dP + static_cast<int64_t>(u) * LD;
+#pragma unroll
+        for (int x = 0; x < E; ++x) atomicAdd(drow + lane + 64 * x, sc * (p[x] - prow[lane + 64 * x]));
+    } else {
+#pragma unroll
+        for (int x = 0; x < E; ++x) prow[lane + 64 * x] = p[x];
+    }
+    return static_cast<double>(deg) * (static_cast<double>(gb) - static_cast<double>(gb0));
+}
+
+// FAST epoch kernel (K1), direct write-back: each wave issues its own q_i updates -- float-atomic
+// deltas (WB 1) or write-through stores (WB 0).  Four waves per block, one work item per wave.
 //
 // Write-back of p: direct store when dP is NULL; otherwise the weighted delta
 // scale * (p_end - p_start) is float-atomically added to dP (scale = piece fraction, times the
@@ -78,116 +205,189 @@ __global__ __launch_bounds__(256) void svd_epoch_fast_kernel(
     const float* __restrict__ ratings, float* __restrict__ P, float* Q, int32_t q_bytes,
     const double* __restrict__ gb_in, double* __restrict__ gb_partial, float lr, float reg,
     float* __restrict__ dP, const float* __restrict__ uw, int32_t whole_direct) {
-#pragma clang fp contract(fast)
-    constexpr int LD = 64 * E, B = 16;
-    static_assert(B % D == 0 && D <= B, "ring depth must divide the 16-rating batch");
     __shared__ double s_contrib[4];
     const int lane = threadIdx.x & 63;
     const int wib = threadIdx.x >> 6;
     const int w = __builtin_amdgcn_readfirstlane(static_cast<int>(blockIdx.x) * 4 + wib);
-    const float gb0 = static_cast<float>(gb_in[0]);
     const __amdgpu_buffer_rsrc_t rq = __builtin_amdgcn_make_buffer_rsrc(Q, 0, q_bytes, 0x00020000);
     const int32_t lane4 = lane * 4;
-    const bool bias_lane = lane == 63;
-    const float a = 1.f - lr * reg;
     double contrib = 0.0;
-
     if (w < n_work) {
-        const int32_t u = wk_user[w];
-        const int64_t b = wk_rng[2 * w], e = wk_rng[2 * w + 1];
-        const float frac = wk_frac[w];
-        float p[E];
-        float* prow = P + static_cast<int64_t>(u) * LD;
+        contrib = sgd_work_item<E, D>(
+            w, wk_user, wk_rng, wk_frac, items, ratings, P, rq, static_cast<float>(gb_in[0]), lr, reg,
+            dP, uw, whole_direct, [&](int32_t row, const float (&qn)[E], const float (&q)[E]) {
 #pragma unroll
-        for (int x = 0; x < E; ++x) p[x] = prow[lane + 64 * x];
-        float ub = lane63(p[E - 1]);
-        float gb = gb0;
-
-        auto load_row = [&](float (&q)[E], int32_t valid, int32_t item) {
-            const int32_t row = valid ? item * (LD * 4) : kOutOfRange;  // SGPR arithmetic
-#pragma unroll
-            for (int x = 0; x < E; ++x)
-                q[x] = __uint_as_float(
-                    __builtin_amdgcn_raw_buffer_load_b32(rq, row + lane4 + 256 * x, 0, kSgdAux));
-        };
-
-        int32_t it_cur[B], it_nxt[B];
-#pragma unroll
-        for (int j = 0; j < B; ++j) it_cur[j] = items[b + j];  // arrays padded by 64 entries
-#pragma unroll
-        for (int j = 0; j < B; ++j) it_nxt[j] = items[b + B + j];
-        const int32_t deg = static_cast<int32_t>(e - b);
-        float ring[D][E];
-#pragma unroll
-        for (int s = 0; s < D; ++s) load_row(ring[s], s < deg, it_cur[s]);
-
-        for (int64_t base = b; base < e; base += B) {
-            const int32_t rem = static_cast<int32_t>(e - base);  // wave-uniform, SALU compares
-            float rt[B];
-#pragma unroll
-            for (int j = 0; j < B; ++j) rt[j] = ratings[base + j];
-#pragma unroll
-            for (int j = 0; j < B; ++j) {
-                constexpr int kD = D;
-                const int slot = j % kD;
-                if (j < rem) {
-                    float* q = ring[slot];
-                    const float bq = lane63(q[E - 1]);
-                    float s = 0.f;
-#pragma unroll
-                    for (int x = 0; x < E - 1; ++x) s += p[x] * q[x];
-                    s += p[E - 1] * (bias_lane ? 0.f : q[E - 1]);
-                    s = wave_sum(s);
-                    // svd.go:102-128 in FMA form: a = 1 - lr*reg, c = lr*diff:
-                    // p <- a p - c q ; q <- a q - c p_new ; b <- a b - c ; gb <- gb - c
-                    const float diff = ((gb + ub) + bq) + s - rt[j];
-                    const float c = lr * diff;
-                    gb -= c;
-                    ub = __builtin_fmaf(ub, a, -c);
-                    const float bq_new = __builtin_fmaf(bq, a, -c);
-                    float qn[E];
-#pragma unroll
-                    for (int x = 0; x < E; ++x) {
-                        p[x] = __builtin_fmaf(-c, q[x], p[x] * a);
-                        qn[x] = __builtin_fmaf(-c, p[x], q[x] * a);
-                    }
-                    p[E - 1] = bias_lane ? ub : p[E - 1];
-                    qn[E - 1] = bias_lane ? bq_new : qn[E - 1];
-                    const int32_t row = it_cur[j] * (LD * 4);
-#pragma unroll
-                    for (int x = 0; x < E; ++x) {
-                        if constexpr (WB == 1)
-                            __builtin_amdgcn_raw_ptr_buffer_atomic_fadd_f32(qn[x] - q[x], rq,
-                                                                           row + lane4 + 256 * x, 0, 0);
-                        else
-                            __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(qn[x]), rq,
-                                                                  row + lane4 + 256 * x, 0, kSgdAux);
-                    }
+                for (int x = 0; x < E; ++x) {
+                    if constexpr (WB == 1)
+                        __builtin_amdgcn_raw_ptr_buffer_atomic_fadd_f32(qn[x] - q[x], rq, row + lane4 + 256 * x, 0, 0);
+                    else if constexpr (WB == 4)
+                        __builtin_amdgcn_sched_barrier(0);
+                    else
+                        __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(qn[x]), rq, row + lane4 + 256 * x, 0, kSgdAux);
                 }
-                // refill this slot with the rating D ahead
-                const int jn = j + D;
-                load_row(ring[slot], jn < rem, jn < B ? it_cur[jn % B] : it_nxt[jn % B]);
-            }
-#pragma unroll
-            for (int j = 0; j < B; ++j) it_cur[j] = it_nxt[j];
-#pragma unroll
-            for (int j = 0; j < B; ++j) it_nxt[j] = items[base + 2 * B + j];
-        }
-        if (dP && !(whole_direct && frac == 1.f)) {  // weighted delta, P stays at the epoch start
-            const float sc = uw ? frac * uw[u] : frac;
-            float* drow = dP + static_cast<int64_t>(u) * LD;
-#pragma unroll
-            for (int x = 0; x < E; ++x) atomicAdd(drow + lane + 64 * x, sc * (p[x] - prow[lane + 64 * x]));
-        } else {
-#pragma unroll
-            for (int x = 0; x < E; ++x) prow[lane + 64 * x] = p[x];
-        }
-        contrib = static_cast<double>(deg) * (static_cast<double>(gb) - static_cast<double>(gb0));
+            });
     }
     if (lane == 0) s_contrib[wib] = contrib;
     __syncthreads();
     if (threadIdx.x == 0)
         gb_partial[blockIdx.x] = ((s_contrib[0] + s_contrib[1]) + s_contrib[2]) + s_contrib[3];
+}
+
+// FAST epoch kernel (K1), hybrid write-back (RS_SGD_WB_ATOMIC, the default).
+//
+// Why (measured): with direct atomics a wave's next q_i load waits, through the
+// in-order vmcnt, for the atomics it issued D ratings earlier.  While the chip is saturating the
+// memory-side atomic unit those take many microseconds, so a user's chain advances at
+// (atomic latency / D) per rating.  Light users do not care (there are thousands of them and the
+// epoch is throughput-bound while they run), but the heaviest users' chains set the epoch's tail.
+//
+// So the first n_heavy work items (the heaviest, LPT order) get a block each: wave 0 runs the SGD
+// chain and writes each q_i delta into an LDS ring (E ds_write_b32 per lane, a row word and the
+// tail word -- never waited on), and waves 1..3 drain it, writer w taking entries w, w + 3, ...,
+// and issue the float atomics: the producer's vmcnt then holds only its loads, and three writers
+// keep up to 3 x 63 atomics in flight.  A consumer that sees the tail sees the entry: a wave's DS
+// instructions execute in issue order.  Every other block is four light work items with direct
+// atomics.  The arithmetic and the memory-side deltas are those of RS_SGD_WB_ATOMIC_DIRECT.
+template <int E>
+struct HeavyRing {
+    static constexpr int kRing = E <= 2 ? 32 : (E <= 4 ? 16 : 8);  // <= 16 KB of LDS per block
+    static constexpr int kBatch = E <= 2 ? 8 : (E <= 4 ? 4 : 2);   // entries per writer LDS wait
+    static_assert((kRing & (kRing - 1)) == 0, "ring size is a power of two");
+};
+
+__device__ __forceinline__ int32_t lds_load_relaxed(const int32_t* p) {
+    return __builtin_amdgcn_readfirstlane(__hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP));
+}
+__device__ __forceinline__ void lds_store_relaxed(int32_t* p, int32_t v) {
+    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+
+template <int E, int D, bool DROP = false>
+__global__ __launch_bounds__(256) void svd_epoch_hybrid_kernel(
+    const int32_t* __restrict__ wk_user, const int64_t* __restrict__ wk_rng,
+    const float* __restrict__ wk_frac, int32_t n_work, int32_t n_heavy,
+    const int32_t* __restrict__ items, const float* __restrict__ ratings, float* __restrict__ P,
+    float* Q, int32_t q_bytes, const double* __restrict__ gb_in, double* __restrict__ gb_partial,
+    float lr, float reg, float* __restrict__ dP, const float* __restrict__ uw, int32_t whole_direct,
+    int64_t* __restrict__ trace) {
+    constexpr int R = HeavyRing<E>::kRing, NB = HeavyRing<E>::kBatch, LD = 64 * E, NW = 3;
+    // the producer's vmcnt holds only its q_i loads: prefetch as deep as the 63-op counter allows
+    constexpr int DH = E == 1 ? 32 : (E == 2 ? 32 : (E <= 4 ? 16 : 8));
+    __shared__ float s_q[R][LD];
+    __shared__ int32_t s_row[R];
+    __shared__ int32_t s_tail, s_done, s_head[NW];
+    __shared__ double s_contrib[4];
+    const int lane = threadIdx.x & 63;
+    const int wib = __builtin_amdgcn_readfirstlane(static_cast<int>(threadIdx.x) >> 6);
+    const __amdgpu_buffer_rsrc_t rq = __builtin_amdgcn_make_buffer_rsrc(Q, 0, q_bytes, 0x00020000);
+    const int32_t lane4 = lane * 4;
+    const float gb0 = static_cast<float>(gb_in[0]);
+    const int blk = static_cast<int>(blockIdx.x);
+    double contrib = 0.0;
+    if (blk >= n_heavy) {  // light blocks: four waves, each striding over the light work items
+        const int stride = (static_cast<int>(gridDim.x) - n_heavy) * 4;
+        for (int w = n_heavy + (blk - n_heavy) * 4 + wib; w < n_work; w += stride) {
+            const int64_t t0 = trace ? static_cast<int64_t>(__builtin_amdgcn_s_memrealtime()) : 0;
+            contrib += sgd_work_item<E, D>(
+                w, wk_user, wk_rng, wk_frac, items, ratings, P, rq, gb0, lr, reg, dP, uw, whole_direct,
+                [&](int32_t row, const float (&qn)[E], const float (&q)[E]) {
+#pragma unroll
+                    for (int x = 0; x < E; ++x)
+                        if constexpr (!DROP)
+                            __builtin_amdgcn_raw_ptr_buffer_atomic_fadd_f32(qn[x] - q[x], rq, row + lane4 + 256 * x, 0, 0);
+                });
+            if (trace && lane == 0) {  // diagnostic timeline (100 MHz clock)
+                const int64_t t1 = static_cast<int64_t>(__builtin_amdgcn_s_memrealtime());
+                trace[3 * w] = t0;
+                trace[3 * w + 1] = t1;
+                trace[3 * w + 2] = t1;
+            }
+        }
+        if (lane == 0) s_contrib[wib] = contrib;
+        __syncthreads();
+        if (threadIdx.x == 0)
+            gb_partial[blk] = ((s_contrib[0] + s_contrib[1]) + s_contrib[2]) + s_contrib[3];
+        return;
+    }
+    // heavy block (block-uniform branch): work item blk, wave 0 produces, waves 1..3 write
+    if (threadIdx.x == 0) {
+        s_tail = 0;
+        s_done = 0;
+    }
+    if (threadIdx.x < NW) s_head[threadIdx.x] = static_cast<int32_t>(threadIdx.x);
+    __syncthreads();
+    const int64_t t0 = trace ? static_cast<int64_t>(__builtin_amdgcn_s_memrealtime()) : 0;
+    if (wib == 0) {
+        int32_t tail = 0, free_end = R;  // entries [tail, free_end) may be written
+        contrib = sgd_work_item<E, DH>(
+            blk, wk_user, wk_rng, wk_frac, items, ratings, P, rq, gb0, lr, reg, dP, uw, whole_direct,
+            [&](int32_t row, const float (&qn)[E], const float (&q)[E]) {
+                if (tail >= free_end) {  // ring full: every entry below min(head) has been drained
+                    for (;;) {
+                        const int32_t h = min(min(lds_load_relaxed(&s_head[0]), lds_load_relaxed(&s_head[1])),
+                                              lds_load_relaxed(&s_head[2]));
+                        free_end = h + R;
+                        if (tail < free_end) break;
+                        __builtin_amdgcn_s_sleep(1);
+                    }
+                }
+                const int slot = tail & (R - 1);
+#pragma unroll
+                for (int x = 0; x < E; ++x) s_q[slot][lane + 64 * x] = qn[x] - q[x];
+                if (lane == 0) s_row[slot] = row;
+                __atomic_signal_fence(__ATOMIC_SEQ_CST);  // entry before tail, in issue order
+                ++tail;
+                if (lane == 0) lds_store_relaxed(&s_tail, tail);
+            });
+        __atomic_signal_fence(__ATOMIC_SEQ_CST);
+        if (lane == 0) lds_store_relaxed(&s_done, 1);
+        if (trace && lane == 0) trace[3 * blk + 1] = static_cast<int64_t>(__builtin_amdgcn_s_memrealtime());
+    } else {
+        const int wr = wib - 1;
+        int32_t next = wr;  // next entry index of this writer: wr, wr + 3, ...
+        for (;;) {
+            const int32_t done = lds_load_relaxed(&s_done);  // done before tail: the final tail
+            __atomic_signal_fence(__ATOMIC_SEQ_CST);
+            const int32_t tail = lds_load_relaxed(&s_tail);
+            __atomic_signal_fence(__ATOMIC_SEQ_CST);
+            if (next < tail) {
+                while (next < tail) {  // up to NB of this writer's entries per LDS wait
+                    const int32_t n = min((tail - next + NW - 1) / NW, NB);
+                    const int32_t myrow = s_row[(next + NW * (lane & (NB - 1))) & (R - 1)];
+                    float v[NB][E];
+#pragma unroll
+                    for (int j = 0; j < NB; ++j)
+#pragma unroll
+                        for (int x = 0; x < E; ++x) v[j][x] = s_q[(next + NW * j) & (R - 1)][lane + 64 * x];
+#pragma unroll
+                    for (int j = 0; j < NB; ++j) {
+                        if (j < n) {
+                            const int32_t row = __builtin_amdgcn_readlane(myrow, j);
+#pragma unroll
+                            for (int x = 0; x < E; ++x)
+                                if constexpr (!DROP)
+                                    __builtin_amdgcn_raw_ptr_buffer_atomic_fadd_f32(v[j][x], rq, row + lane4 + 256 * x, 0, 0);
+                        }
+                    }
+                    next += NW * n;
+                }
+                __atomic_signal_fence(__ATOMIC_SEQ_CST);  // entries read before their slots are freed
+                if (lane == 0) lds_store_relaxed(&s_head[wr], next);
+            } else if (done) {
+                break;
+            } else {
+                __builtin_amdgcn_s_sleep(1);
+            }
+        }
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        gb_partial[blk] = contrib;
+        if (trace) {
+            trace[3 * blk] = t0;
+            trace[3 * blk + 2] = static_cast<int64_t>(__builtin_amdgcn_s_memrealtime());
+        }
+    }
 }
 
 // gb += (sum of block partials in fixed order) / nnz  -- one block, deterministic tree.
@@ -431,7 +631,7 @@ struct rs_svd_plan {
     int64_t nnz = 0;
     std::vector<int64_t> h_rowptr;  // host user-CSR row pointers (work items are rebuilt from it)
     std::vector<int32_t> h_cols;    // host user-CSR item ids (item copies are rebuilt from it)
-    rs::DevBuf<int32_t> items;      // user-CSR item rows (copies of split items), padded by 64
+    rs::DevBuf<int32_t> items;      // user-CSR item rows (copies of split items), padded by 128
     rs::DevBuf<float> ratings;
     rs::DevBuf<int32_t> wk_user;      // work items: user, [begin, end) into the CSR, len / deg
     rs::DevBuf<int64_t> wk_rng;
@@ -450,6 +650,10 @@ struct rs_svd_plan {
     rs::DevBuf<float> uw;  // per-user share of this shard (multi-GPU delta mode)
     int32_t n_blocks = 0;
     int32_t write_back = RS_SGD_WB_ATOMIC;
+    int32_t heavy_min = 1024;  // work items with at least this many ratings get a producer + 3 writers
+    int32_t n_heavy = 0;       // leading (LPT-ordered) work items that are heavy
+    int32_t light_blocks = 0;  // cap on the light blocks (each wave strides over light items; 0 = none)
+    rs::DevBuf<int64_t> trace;  // diagnostic: {start, chain end, drained} per work item (RS_SGD_WB_ATOMIC)
     int32_t ring_depth = 8;
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
     double last_ms = 0.0;
@@ -469,6 +673,28 @@ namespace rs {
 
 constexpr int32_t kMaxFactors = 511;
 
+// Light blocks of the hybrid launch: 1.5 per CU (6 light waves per CU).  Measured on the ML-1M shape
+// (DESIGN.md K1): one wave per user puts ~6,000 waves' atomics in flight and the memory-side queue
+// latency that every q_i load then pays sets the heavy users' pace; 256-512 light blocks each
+// striding over the LPT-ordered light users keep the atomic unit as busy with far shorter queues.
+int32_t default_light_blocks(const rs_ctx* ctx) {
+    int cus = 0;
+    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, ctx->device) != hipSuccess || cus <= 0)
+        cus = 256;
+    return (3 * cus) / 2;
+}
+
+// Blocks of the FAST launch: four work items per block (direct write-back), or one block per heavy
+// work item plus four light items per block (hybrid).  gb partials are one per block.
+int32_t fast_blocks(const rs_svd_plan* pl) {
+    if (pl->write_back == RS_SGD_WB_ATOMIC || pl->write_back == 101) {
+        int32_t light = (pl->n_work - pl->n_heavy + 3) / 4;
+        if (pl->light_blocks > 0) light = std::min(light, pl->light_blocks);
+        return std::max<int32_t>(1, pl->n_heavy + light);
+    }
+    return std::max<int32_t>(1, (pl->n_work + 3) / 4);
+}
+
 template <int E, int D, int WB>
 static void launch_fast_t(rs_svd_plan* pl, float lr, float reg, hipStream_t s, float* dP) {
     const int32_t q_bytes = static_cast<int32_t>(pl->Q.n * sizeof(float));
@@ -476,10 +702,19 @@ static void launch_fast_t(rs_svd_plan* pl, float lr, float reg, hipStream_t s, f
     // single GPU: whole rows store P directly, pieces of split users add into the plan's dPs
     const bool multi = dP != nullptr;
     float* d = multi ? dP : (pl->n_split > 0 ? pl->dPs.p : nullptr);
-    hipLaunchKernelGGL((svd_epoch_fast_kernel<E, D, WB>), dim3(pl->n_blocks), dim3(256), 0, s,
-                       pl->wk_user.p, pl->wk_rng.p, pl->wk_frac.p, pl->n_work, pl->items.p,
-                       pl->ratings.p, pl->P.p, pl->Q.p, q_bytes, pl->gb.p, pl->partial.p, lr, reg, d,
-                       multi ? pl->uw.p : nullptr, multi ? 0 : 1);
+    pl->n_blocks = fast_blocks(pl);
+    if constexpr (WB == 2 || WB == 5) {
+        hipLaunchKernelGGL((svd_epoch_hybrid_kernel<E, D, WB == 5>), dim3(pl->n_blocks), dim3(256), 0, s,
+                           pl->wk_user.p, pl->wk_rng.p, pl->wk_frac.p, pl->n_work, pl->n_heavy,
+                           pl->items.p, pl->ratings.p, pl->P.p, pl->Q.p, q_bytes, pl->gb.p,
+                           pl->partial.p, lr, reg, d, multi ? pl->uw.p : nullptr, multi ? 0 : 1,
+                           pl->trace.n ? pl->trace.p : nullptr);
+    } else {
+        hipLaunchKernelGGL((svd_epoch_fast_kernel<E, D, WB>), dim3(pl->n_blocks), dim3(256), 0, s,
+                           pl->wk_user.p, pl->wk_rng.p, pl->wk_frac.p, pl->n_work, pl->items.p,
+                           pl->ratings.p, pl->P.p, pl->Q.p, q_bytes, pl->gb.p, pl->partial.p, lr, reg,
+                           d, multi ? pl->uw.p : nullptr, multi ? 0 : 1);
+    }
 }
 
 template <int D, int WB>
@@ -506,8 +741,13 @@ static void launch_fast_d(rs_svd_plan* pl, float lr, float reg, hipStream_t s, f
 }
 
 static void launch_fast(rs_svd_plan* pl, float lr, float reg, hipStream_t s, float* dP = nullptr) {
-    if (pl->write_back == RS_SGD_WB_STORE) launch_fast_d<0>(pl, lr, reg, s, dP);  // WB 0: store
-    else launch_fast_d<1>(pl, lr, reg, s, dP);                                    // WB 1: atomic
+    switch (pl->write_back) {
+        case RS_SGD_WB_STORE: launch_fast_d<0>(pl, lr, reg, s, dP); break;          // write-through stores
+        case RS_SGD_WB_ATOMIC_DIRECT: launch_fast_d<1>(pl, lr, reg, s, dP); break;  // per-wave atomics
+        case 100: launch_fast_d<4>(pl, lr, reg, s, dP); break;                      // DIAG: no write-back
+        case 101: launch_fast_d<5>(pl, lr, reg, s, dP); break;                      // DIAG: writer drops
+        default: launch_fast_d<2>(pl, lr, reg, s, dP); break;                       // hybrid
+    }
     RS_HIP(hipGetLastError());
 }
 
@@ -563,7 +803,7 @@ static void build_items(rs_svd_plan* pl) {
             extra += R[x] - 1;
         }
     }
-    std::vector<int32_t> remap(cols.size() + 64, 0);
+    std::vector<int32_t> remap(cols.size() + 128, 0);
     std::vector<int64_t> seen(std::max(1, ni), 0);
     for (size_t t = 0; t < cols.size(); ++t) {
         const int32_t x = cols[t];
@@ -626,11 +866,14 @@ static void build_work(rs_svd_plan* pl) {
     }
     plan_sync_last(pl);
     pl->n_work = static_cast<int32_t>(wk.size());
-    pl->n_blocks = std::max<int32_t>(1, (pl->n_work + 3) / 4);  // one wave per item, 4 per block
+    pl->n_heavy = 0;
+    if (pl->heavy_min > 0)
+        while (pl->n_heavy < pl->n_work && wr[2 * pl->n_heavy + 1] - wr[2 * pl->n_heavy] >= pl->heavy_min) ++pl->n_heavy;
+    pl->n_blocks = fast_blocks(pl);
     pl->wk_user.alloc(std::max<size_t>(1, wu.size()));
     pl->wk_rng.alloc(std::max<size_t>(2, wr.size()));
     pl->wk_frac.alloc(std::max<size_t>(1, wf.size()));
-    pl->partial.alloc(pl->n_blocks);
+    pl->partial.alloc(std::max<int32_t>(1, pl->n_work));  // >= blocks of any write-back mode
     pl->wk_user.upload(wu.data(), wu.size(), s);
     pl->wk_rng.upload(wr.data(), wr.size(), s);
     pl->wk_frac.upload(wf.data(), wf.size(), s);
@@ -647,6 +890,7 @@ static void build_work(rs_svd_plan* pl) {
 static void plan_build(rs_ctx* ctx, const rs_ratings* r, int32_t k, rs_svd_plan* pl) {
     hipStream_t s = ctx->stream;
     pl->ctx = ctx;
+    pl->light_blocks = default_light_blocks(ctx);
     pl->n_users = r->n_users;
     pl->n_items = r->n_items;
     pl->k = k;
@@ -654,8 +898,9 @@ static void plan_build(rs_ctx* ctx, const rs_ratings* r, int32_t k, rs_svd_plan*
     pl->nnz = r->nnz;
     UserCSR csr;
     build_csr(r->nnz, r->n_users, r->users, r->items, r->ratings, csr);
-    // items / ratings padded by 64 entries: the kernel reads whole 16-entry batches (two ahead)
-    csr.vals.resize(csr.vals.size() + 64, 0.f);
+    // items / ratings padded by 128 entries: the kernels read 32-entry chunks up to two ahead
+    // (entries < e + 96 for a row ending at e)
+    csr.vals.resize(csr.vals.size() + 128, 0.f);
     pl->ratings.alloc(csr.vals.size());
     pl->ratings.upload(csr.vals.data(), csr.vals.size(), s);
     pl->h_rowptr = std::move(csr.rowptr);
@@ -876,13 +1121,45 @@ extern "C" int rs_svd_plan_apply_delta(rs_svd_plan* pl, const void* dP, const vo
 
 extern "C" int rs_svd_plan_set_mode(rs_svd_plan* pl, int32_t write_back, int32_t ring_depth) {
     if (!pl) return rs::set_error(nullptr, RS_ERR_INVALID, "plan is NULL");
-    if (write_back != RS_SGD_WB_ATOMIC && write_back != RS_SGD_WB_STORE)
+    if ((write_back < RS_SGD_WB_ATOMIC || write_back > RS_SGD_WB_ATOMIC_DIRECT) && write_back != 100 && write_back != 101)
         return rs::set_error(pl->ctx, RS_ERR_INVALID, "unknown write-back mode");
     if (ring_depth != 4 && ring_depth != 8 && ring_depth != 16)
         return rs::set_error(pl->ctx, RS_ERR_INVALID, "ring depth must be 4, 8 or 16");
+    rs::plan_sync_last(pl);  // n_blocks (the fold's partial count) follows the mode
     pl->write_back = write_back;
     pl->ring_depth = ring_depth;
+    pl->n_blocks = rs::fast_blocks(pl);
     return RS_OK;
+}
+
+// Diagnostic timeline of the last RS_SGD_WB_ATOMIC epoch: 3 int64 per work item (LPT order) --
+// start, end of its SGD chain, end of its write-back -- in 100 MHz ticks; out NULL enables it.
+extern "C" int rs_svd_plan_trace(rs_svd_plan* pl, int64_t* out, int32_t* user) {
+    if (!pl) return rs::set_error(nullptr, RS_ERR_INVALID, "plan is NULL");
+    return rs_guard(pl->ctx, [&]() -> int {
+        hipStream_t s = pl->ctx->stream;
+        rs::plan_sync_last(pl);
+        if (!out) {
+            pl->trace.alloc(std::max<size_t>(3, 3 * static_cast<size_t>(pl->n_work)));
+            return RS_OK;
+        }
+        if (!pl->trace.n) return rs::set_error(pl->ctx, RS_ERR_INVALID, "trace not enabled");
+        pl->trace.download(out, 3 * static_cast<size_t>(pl->n_work), s);
+        if (user) pl->wk_user.download(user, pl->n_work, s);
+        RS_HIP(hipStreamSynchronize(s));
+        return RS_OK;
+    });
+}
+
+extern "C" int rs_svd_plan_set_schedule(rs_svd_plan* pl, int32_t heavy_min, int32_t light_blocks) {
+    if (!pl) return rs::set_error(nullptr, RS_ERR_INVALID, "plan is NULL");
+    return rs_guard(pl->ctx, [&]() -> int {
+        if (heavy_min < 0) return rs::set_error(pl->ctx, RS_ERR_INVALID, "heavy_min must be >= 0");
+        pl->heavy_min = heavy_min;
+        pl->light_blocks = light_blocks < 0 ? rs::default_light_blocks(pl->ctx) : light_blocks;
+        rs::build_work(pl);
+        return RS_OK;
+    });
 }
 
 extern "C" int rs_svd_plan_set_split(rs_svd_plan* pl, int32_t split_cap) {
@@ -988,7 +1265,7 @@ extern "C" int rs_svd_fit(rs_ctx* ctx, const rs_ratings* r, const rs_sgd_params*
         if (p->mode == RS_SGD_FAST) {
             rs_svd_plan pl;
             rs::plan_build(ctx, r, p->n_factors, &pl);
-            pl.write_back = p->write_back == RS_SGD_WB_STORE ? RS_SGD_WB_STORE : RS_SGD_WB_ATOMIC;
+            pl.write_back = p->write_back >= RS_SGD_WB_ATOMIC && p->write_back <= RS_SGD_WB_ATOMIC_DIRECT ? p->write_back : RS_SGD_WB_ATOMIC;
             if (p->n_epochs > 0) *gb = rs::gb_warm_start(r, bu, bi);
             rs::plan_upload(&pl, P, Q, bu, bi, gb);
             rs::kernel_span_begin(ctx);

@@ -19,7 +19,7 @@ _lib = None
 RS_OK = 0
 RS_ERR_INVALID, RS_ERR_HIP, RS_ERR_NOMEM, RS_ERR_UNSUPPORTED, RS_ERR_NO_DEVICE = -1, -2, -3, -4, -5
 SGD_FAST, SGD_ORDERED = 0, 1
-WB_ATOMIC, WB_STORE = 0, 1
+WB_ATOMIC, WB_STORE, WB_ATOMIC_DIRECT = 0, 1, 2
 SIM_COSINE, SIM_MSD, SIM_PEARSON = 0, 1, 2
 
 HEADER_SYMBOLS = (
@@ -28,7 +28,7 @@ HEADER_SYMBOLS = (
     "rs_svd_fit", "rs_svd_predict", "rs_svdpp_fit", "rs_nmf_fit", "rs_baseline_fit",
     "rs_knn_sims", "rs_sim_pair", "rs_svd_plan_create", "rs_svd_plan_destroy",
     "rs_svd_plan_upload", "rs_svd_plan_download", "rs_svd_plan_epochs",
-    "rs_svd_plan_device_ptrs", "rs_svd_plan_set_mode", "rs_svd_plan_set_split",
+    "rs_svd_plan_device_ptrs", "rs_svd_plan_set_mode", "rs_svd_plan_set_split", "rs_svd_plan_set_schedule", "rs_svd_plan_trace",
     "rs_svd_plan_set_item_split", "rs_svd_plan_set_timing", "rs_svd_plan_set_user_weights",
     "rs_svd_plan_epoch_delta", "rs_svd_plan_apply_delta", "rs_svd_plan_last_kernel_ms",
     "rs_svd_plan_predict", "rs_svd_plan_evaluate",
@@ -93,6 +93,8 @@ def lib():
                                                   C.POINTER(_vp), C.POINTER(_i32)]),
             "rs_svd_plan_set_mode": (C.c_int, [_vp, _i32, _i32]),
             "rs_svd_plan_set_split": (C.c_int, [_vp, _i32]),
+            "rs_svd_plan_set_schedule": (C.c_int, [_vp, _i32, _i32]),
+            "rs_svd_plan_trace": (C.c_int, [_vp, _vp, _vp]),
             "rs_svd_plan_set_item_split": (C.c_int, [_vp, _i32]),
             "rs_svd_plan_set_user_weights": (C.c_int, [_vp, _vp]),
             "rs_svd_plan_epoch_delta": (C.c_int, [_vp, _flt, _flt, _vp, _vp, _vp]),
@@ -296,6 +298,23 @@ class SvdPlan:
 
     def set_mode(self, write_back=WB_ATOMIC, ring_depth=8):
         self.ctx.check(lib().rs_svd_plan_set_mode(self.h, write_back, ring_depth))
+
+    def set_schedule(self, heavy_min=1024, light_blocks=-1):
+        """WB_ATOMIC schedule: items with >= heavy_min ratings get a producer wave + 3 writer waves;
+        light items stride over light_blocks blocks (-1: 1.5 per CU, 0: one wave per item)."""
+        self.ctx.check(lib().rs_svd_plan_set_schedule(self.h, heavy_min, light_blocks))
+
+    def trace(self, n_work=None):
+        """Diagnostic timeline: trace() enables it; trace(n_work) returns (ticks[n_work, 3], users)
+        of the last epoch (n_work = the plan's work items: its non-empty users when not split)."""
+        if n_work is None:
+            self.ctx.check(lib().rs_svd_plan_trace(self.h, None, None))
+            return None
+        n = n_work
+        t = np.zeros((n, 3), np.int64)
+        u = np.zeros(n, np.int32)
+        self.ctx.check(lib().rs_svd_plan_trace(self.h, t.ctypes.data, u.ctypes.data))
+        return t, u
 
     def set_split(self, split_cap):
         self.ctx.check(lib().rs_svd_plan_set_split(self.h, split_cap))

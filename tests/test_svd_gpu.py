@@ -70,7 +70,7 @@ def _disjoint_input(n_users=300, per_user=12, k=64, seed=4, ragged=True):
     return users, items, r, n_users, len(users)
 
 
-@pytest.mark.parametrize("wb", [rsgpu.WB_ATOMIC, rsgpu.WB_STORE])
+@pytest.mark.parametrize("wb", [rsgpu.WB_ATOMIC, rsgpu.WB_STORE, rsgpu.WB_ATOMIC_DIRECT])
 @pytest.mark.parametrize("k", [8, 20, 63, 64, 100, 128, 256, 511])
 def test_fast_matches_own_schedule_race_free(ctx, k, wb):
     u, i, r, nu, ni = _disjoint_input(k=k)
@@ -83,6 +83,28 @@ def test_fast_matches_own_schedule_race_free(ctx, k, wb):
                           mode=rsgpu.SGD_FAST, write_back=wb)
         assert _maxdiff(ref[:4], got[:4]) <= TOL, (k, epochs)
         assert abs(ref[4] - got[4]) <= TOL
+
+
+@pytest.mark.parametrize("heavy,lb", [(16, -1), (512, 3), (0, 1), (0, 0), (1024, -1)])
+@pytest.mark.parametrize("k", [20, 100, 300])
+def test_fast_long_rows_race_free(ctx, k, heavy, lb):
+    """Rows of hundreds of ratings through the hybrid write-back: heavy rows' LDS rings fill and wrap
+    many times (heavy 16: every row; 512: the longest; 0: none), light rows strided over few blocks
+    (lb 1 or 3) or one wave each (lb 0) -- equal to the restatement."""
+    u, i, r, nu, ni = _disjoint_input(n_users=40, per_user=400, k=k, seed=12)
+    rng = np.random.default_rng(k + 1)
+    P0, Q0 = rng.normal(0, 0.1, (nu, k)), rng.normal(0, 0.1, (ni, k))
+    bu0, bi0 = rng.normal(0, 0.1, nu), rng.normal(0, 0.1, ni)
+    rowptr, items, rr = O.csr_by(u, nu, i, r)
+    plan = ctx.svd_plan(rsgpu.Ratings(u, i, r, nu, ni), k)
+    plan.set_schedule(heavy, lb)
+    plan.upload(P0, Q0, bu0, bi0, 3.1)
+    plan.epochs(2)
+    got = plan.download()
+    plan.close()
+    ref = O.svd_fit_chunked(rowptr, items, rr, P0, Q0, 1 << 30, bu=bu0, bi=bi0, gb=3.1, epochs=2,
+                            warm=False)
+    assert _maxdiff(ref[:4], got[:4]) <= TOL and abs(ref[4] - got[4]) <= TOL
 
 
 @pytest.mark.parametrize("cap", [16, 40, 0])
