@@ -11,6 +11,7 @@
  *   rs_svdpp_fit      <- core/svd.go:316-427   (*SVDPP).Fit          (K2)
  *   rs_nmf_fit        <- core/svd.go:158-251   (*NMF).Fit            (K3)
  *   rs_knn_sims       <- core/knn.go:143-217   (*KNN).Fit pair loop  (K4 Cosine/MSD, K5 Pearson)
+ *   rs_knn_sims_part  <- core/knn.go:195-215   the nJobs row split, one part per GPU
  *                        with core/sim.go:10-81 Cosine / MSD / Pearson as the pair function
  *   rs_sim_pair       <- core/sim.go:7-81      Sim func(a, b SortedIdRatings) float64
  *   rs_knn_plan_*     <- core/knn.go:143-217 + knn.go:75-141 (*KNN).Predict on the device (§8f row 2)
@@ -127,6 +128,18 @@ int rs_baseline_fit(rs_ctx* ctx, const rs_ratings* r, int32_t n_epochs, double l
  * Rows are CSR (rowptr[n_left+1], ids in [0, n_right), ratings) in any order within a row. */
 int rs_knn_sims(rs_ctx* ctx, int32_t kind, int32_t n_left, int32_t n_right, const int64_t* rowptr,
                 const int32_t* ids, const double* ratings, double* sims);
+
+/* Multi-GPU form of rs_knn_sims (the knn.go:195-215 nJobs row split, one part per GPU).
+ * The rows are cut into 128-row blocks; part p of n_parts owns the blocks t with t mod 2n in
+ * {p, 2n-1-p} (near-equal triangle work) and writes ONLY the entries S[a][b] and S[b][a] with a in
+ * its blocks and b >= a.  Parts write disjoint entries of the same n_left x n_left buffer, so
+ * n_parts calls -- one per device, concurrently, into one shared host buffer -- assemble exactly
+ * the rs_knn_sims result with no collective.  part 0 of 1 is rs_knn_sims. */
+int rs_knn_sims_part(rs_ctx* ctx, int32_t kind, int32_t n_left, int32_t n_right,
+                     const int64_t* rowptr, const int32_t* ids, const double* ratings, int32_t part,
+                     int32_t n_parts, double* sims);
+/* Host only: owned[t] = 1 for the 128-row blocks t of part (ceil(n_left / 128) entries). */
+int rs_knn_part_blocks(int32_t n_left, int32_t part, int32_t n_parts, int32_t* owned);
 
 /* core/sim.go one pair (ID-ascending inputs), computed on the device by the K5 merge kernel. */
 int rs_sim_pair(rs_ctx* ctx, int32_t kind, int64_t na, const int32_t* a_ids, const double* a_r,

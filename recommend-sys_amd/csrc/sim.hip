@@ -242,6 +242,16 @@ static std::vector<int2> tile_order(int32_t T) {
     return t;
 }
 
+// Multi-GPU sharding: the L rows are cut into 128-row blocks and part p of n owns the
+// blocks t with t mod 2n in {p, 2n - 1 - p} (zig-zag: block t carries T - t tiles of the upper
+// triangle, so every part gets near-equal work).  A part computes every pair (a, b), b >= a, whose
+// row a lies in its blocks and writes both S[a][b] and S[b][a]: parts write disjoint entries, no
+// collective is needed, and the union of all parts is the full matrix.
+static bool part_owns(int32_t t, int32_t part, int32_t n_parts) {
+    const int32_t m = t % (2 * n_parts);
+    return m == part || m == 2 * n_parts - 1 - part;
+}
+
 // ---------------------------------------------------------------------------------------------
 // K5: merge-order float64 kernel (any ratings; Pearson always)
 
@@ -309,10 +319,12 @@ template <int KIND>
 __global__ __launch_bounds__(256) void sims_merge_kernel(
     int32_t L, int32_t R, const int64_t* __restrict__ rowptr, const int32_t* __restrict__ ids,
     const double* __restrict__ r, const double* __restrict__ mean, double* __restrict__ scratch,
-    uint8_t* __restrict__ scratch_has, double* __restrict__ S) {
+    uint8_t* __restrict__ scratch_has, double* __restrict__ S, const int32_t* __restrict__ rows,
+    int32_t n_rows) {
     double* dense = scratch + static_cast<int64_t>(blockIdx.x) * R;
     uint8_t* has = scratch_has + static_cast<int64_t>(blockIdx.x) * R;
-    for (int32_t a = blockIdx.x; a < L; a += gridDim.x) {
+    for (int32_t x = blockIdx.x; x < n_rows; x += gridDim.x) {
+        const int32_t a = rows[x];
         for (int64_t t = rowptr[a] + threadIdx.x; t < rowptr[a + 1]; t += blockDim.x) {
             dense[ids[t]] = r[t];
             has[ids[t]] = 1;
@@ -386,7 +398,7 @@ static bool has_repeats(int32_t L, const SortedRows& sr) {
 }
 
 static void sims_device(rs_ctx* ctx, int32_t kind, int32_t L, int32_t R, const SortedRows& sr,
-                        bool allow_mfma, DevBuf<double>& dS) {
+                        bool allow_mfma, DevBuf<double>& dS, int32_t part = 0, int32_t n_parts = 1) {
     hipStream_t s = ctx->stream;
     const int64_t nnz = static_cast<int64_t>(sr.ids.size());
     dS.alloc(std::max<int64_t>(1, static_cast<int64_t>(L) * L));
@@ -410,7 +422,14 @@ static void sims_device(rs_ctx* ctx, int32_t kind, int32_t L, int32_t R, const S
         RS_HIP(hipGetLastError());
         RS_HIP(hipStreamSynchronize(s));
         const int32_t T = static_cast<int32_t>(Lp / kTile);
-        const std::vector<int2> order = tile_order(T);
+        std::vector<int2> order = tile_order(T);
+        if (n_parts > 1) {
+            std::vector<int2> mine;
+            for (const int2& t : order)
+                if (part_owns(t.x, part, n_parts)) mine.push_back(t);
+            order.swap(mine);
+            if (order.empty()) return;
+        }
         DevBuf<int2> dtiles(order.size());
         dtiles.upload(order.data(), order.size(), s);
         const double inv_s2 = 1.0 / static_cast<double>(scale * scale);
@@ -434,18 +453,25 @@ static void sims_device(rs_ctx* ctx, int32_t kind, int32_t L, int32_t R, const S
     dr.upload(sr.r.data(), nnz, s);
     hipLaunchKernelGGL(row_mean_kernel, dim3((L + 255) / 256), dim3(256), 0, s, L, drow.p, dr.p,
                        dmean.p);
-    const int32_t grid = std::min<int32_t>(L, 2048);
+    std::vector<int32_t> rows;
+    for (int32_t a = 0; a < L; ++a)
+        if (n_parts == 1 || part_owns(a / kTile, part, n_parts)) rows.push_back(a);
+    if (rows.empty()) return;
+    DevBuf<int32_t> drows(rows.size());
+    drows.upload(rows.data(), rows.size(), s);
+    const int32_t n_rows = static_cast<int32_t>(rows.size());
+    const int32_t grid = std::min<int32_t>(n_rows, 2048);
     DevBuf<double> scratch(static_cast<int64_t>(std::max(1, R)) * grid);
     DevBuf<uint8_t> scratch_has(static_cast<int64_t>(std::max(1, R)) * grid);
     RS_HIP(hipMemsetAsync(scratch_has.p, 0, scratch_has.n, s));
     RS_HIP(hipStreamSynchronize(s));
     kernel_span_begin(ctx);
     if (kind == RS_SIM_COSINE)
-        hipLaunchKernelGGL(sims_merge_kernel<0>, dim3(grid), dim3(256), 0, s, L, R, drow.p, dids.p, dr.p, dmean.p, scratch.p, scratch_has.p, dS.p);
+        hipLaunchKernelGGL(sims_merge_kernel<0>, dim3(grid), dim3(256), 0, s, L, R, drow.p, dids.p, dr.p, dmean.p, scratch.p, scratch_has.p, dS.p, drows.p, n_rows);
     else if (kind == RS_SIM_MSD)
-        hipLaunchKernelGGL(sims_merge_kernel<1>, dim3(grid), dim3(256), 0, s, L, R, drow.p, dids.p, dr.p, dmean.p, scratch.p, scratch_has.p, dS.p);
+        hipLaunchKernelGGL(sims_merge_kernel<1>, dim3(grid), dim3(256), 0, s, L, R, drow.p, dids.p, dr.p, dmean.p, scratch.p, scratch_has.p, dS.p, drows.p, n_rows);
     else
-        hipLaunchKernelGGL(sims_merge_kernel<2>, dim3(grid), dim3(256), 0, s, L, R, drow.p, dids.p, dr.p, dmean.p, scratch.p, scratch_has.p, dS.p);
+        hipLaunchKernelGGL(sims_merge_kernel<2>, dim3(grid), dim3(256), 0, s, L, R, drow.p, dids.p, dr.p, dmean.p, scratch.p, scratch_has.p, dS.p, drows.p, n_rows);
     RS_HIP(hipGetLastError());
     kernel_span_end(ctx);
 }
@@ -558,13 +584,15 @@ static int check_knn_csr(rs_ctx* ctx, int32_t n_left, int32_t n_right, const int
 
 }  // namespace rs
 
-extern "C" int rs_knn_sims(rs_ctx* ctx, int32_t kind, int32_t n_left, int32_t n_right,
-                           const int64_t* rowptr, const int32_t* ids, const double* ratings,
-                           double* sims) {
+extern "C" int rs_knn_sims_part(rs_ctx* ctx, int32_t kind, int32_t n_left, int32_t n_right,
+                                const int64_t* rowptr, const int32_t* ids, const double* ratings,
+                                int32_t part, int32_t n_parts, double* sims) {
     if (!ctx) return rs::set_error(ctx, RS_ERR_INVALID, "ctx is NULL");
     return rs_guard(ctx, [&]() -> int {
         if (kind < RS_SIM_COSINE || kind > RS_SIM_PEARSON)
             return rs::set_error(ctx, RS_ERR_INVALID, "unknown similarity kind");
+        if (n_parts < 1 || part < 0 || part >= n_parts)
+            return rs::set_error(ctx, RS_ERR_INVALID, "part must be in [0, n_parts)");
         if (n_left > 0 && !sims) return rs::set_error(ctx, RS_ERR_INVALID, "sims is NULL");
         const int st = rs::check_knn_csr(ctx, n_left, n_right, rowptr, ids, ratings);
         if (st != RS_OK) return st;
@@ -572,11 +600,38 @@ extern "C" int rs_knn_sims(rs_ctx* ctx, int32_t kind, int32_t n_left, int32_t n_
         rs::sort_rows(n_left, rowptr, ids, ratings, sr);
         rs::DevBuf<double> dS;
         const char* env = std::getenv("RSGPU_KNN_NO_MFMA");
-        rs::sims_device(ctx, kind, n_left, n_right, sr, !(env && env[0] == '1'), dS);
-        dS.download(sims, static_cast<int64_t>(n_left) * n_left, ctx->stream);
-        RS_HIP(hipStreamSynchronize(ctx->stream));
+        rs::sims_device(ctx, kind, n_left, n_right, sr, !(env && env[0] == '1'), dS, part, n_parts);
+        hipStream_t s = ctx->stream;
+        if (n_parts == 1) {
+            dS.download(sims, static_cast<int64_t>(n_left) * n_left, s);
+        } else {  // the part's rows from their diagonal block rightwards, and the mirrored columns
+            const size_t pitch = static_cast<size_t>(n_left) * sizeof(double);
+            for (int32_t t = 0; t * rs::kTile < n_left; ++t) {
+                if (!rs::part_owns(t, part, n_parts)) continue;
+                const int32_t a0 = t * rs::kTile, na = std::min(rs::kTile, n_left - a0);
+                const size_t off = static_cast<size_t>(a0) * n_left + a0;
+                RS_HIP(hipMemcpy2DAsync(sims + off, pitch, dS.p + off, pitch, (n_left - a0) * sizeof(double),
+                                        na, hipMemcpyDeviceToHost, s));
+                RS_HIP(hipMemcpy2DAsync(sims + off, pitch, dS.p + off, pitch, na * sizeof(double),
+                                        n_left - a0, hipMemcpyDeviceToHost, s));
+            }
+        }
+        RS_HIP(hipStreamSynchronize(s));
         return RS_OK;
     });
+}
+
+extern "C" int rs_knn_sims(rs_ctx* ctx, int32_t kind, int32_t n_left, int32_t n_right,
+                           const int64_t* rowptr, const int32_t* ids, const double* ratings,
+                           double* sims) {
+    return rs_knn_sims_part(ctx, kind, n_left, n_right, rowptr, ids, ratings, 0, 1, sims);
+}
+
+extern "C" int rs_knn_part_blocks(int32_t n_left, int32_t part, int32_t n_parts, int32_t* owned) {
+    if (n_left < 0 || n_parts < 1 || part < 0 || part >= n_parts || !owned) return RS_ERR_INVALID;
+    const int32_t T = (n_left + rs::kTile - 1) / rs::kTile;
+    for (int32_t t = 0; t < T; ++t) owned[t] = rs::part_owns(t, part, n_parts) ? 1 : 0;
+    return RS_OK;
 }
 
 extern "C" int rs_sim_pair(rs_ctx* ctx, int32_t kind, int64_t na, const int32_t* a_ids,

@@ -26,7 +26,7 @@ HEADER_SYMBOLS = (
     "rs_version", "rs_device_count", "rs_open", "rs_close", "rs_last_error", "rs_synchronize",
     "rs_last_kernel_ms",
     "rs_svd_fit", "rs_svd_predict", "rs_svdpp_fit", "rs_nmf_fit", "rs_baseline_fit",
-    "rs_knn_sims", "rs_sim_pair", "rs_svd_plan_create", "rs_svd_plan_destroy",
+    "rs_knn_sims", "rs_knn_sims_part", "rs_knn_part_blocks", "rs_sim_pair", "rs_svd_plan_create", "rs_svd_plan_destroy",
     "rs_svd_plan_upload", "rs_svd_plan_download", "rs_svd_plan_epochs",
     "rs_svd_plan_device_ptrs", "rs_svd_plan_set_mode", "rs_svd_plan_set_split", "rs_svd_plan_set_schedule", "rs_svd_plan_trace",
     "rs_svd_plan_set_item_split", "rs_svd_plan_set_timing", "rs_svd_plan_set_user_weights",
@@ -83,6 +83,8 @@ def lib():
             "rs_baseline_fit": (C.c_int, [_vp, C.POINTER(_Ratings), _i32, _dbl, _dbl, _vp, _vp,
                                           _vp]),
             "rs_knn_sims": (C.c_int, [_vp, _i32, _i32, _i32, _vp, _vp, _vp, _vp]),
+            "rs_knn_sims_part": (C.c_int, [_vp, _i32, _i32, _i32, _vp, _vp, _vp, _i32, _i32, _vp]),
+            "rs_knn_part_blocks": (C.c_int, [_i32, _i32, _i32, _vp]),
             "rs_sim_pair": (C.c_int, [_vp, _i32, _i64, _vp, _vp, _i64, _vp, _vp, _vp]),
             "rs_svd_plan_create": (C.c_int, [_vp, C.POINTER(_Ratings), _i32, C.POINTER(_vp)]),
             "rs_svd_plan_destroy": (None, [_vp]),
@@ -236,15 +238,20 @@ class Context:
                                          _ptr(bi), _ptr(g)))
         return bu, bi, float(g[0])
 
-    def knn_sims(self, kind, rowptr, ids, ratings, n_right):
-        """core/knn.go:143-217 pair loop -> dense L x L float64 Sims (NaN = no co-rating)."""
+    def knn_sims(self, kind, rowptr, ids, ratings, n_right, part=0, n_parts=1, out=None):
+        """core/knn.go:143-217 pair loop -> dense L x L float64 Sims (NaN = no co-rating).
+        With n_parts > 1 only this part's entries of `out` (L x L, e.g. a shared memmap) are written
+        (rs_knn_sims_part): the union over parts is the full matrix."""
         rowptr = np.ascontiguousarray(rowptr, dtype=np.int64)
         ids = np.ascontiguousarray(ids, dtype=np.int32)
         ratings = np.ascontiguousarray(ratings, dtype=np.float64)
         L = len(rowptr) - 1
-        out = np.empty((L, L))
-        self.check(lib().rs_knn_sims(self.h, kind, L, n_right, _ptr(rowptr), _ptr(ids),
-                                     _ptr(ratings), _ptr(out)))
+        if out is None:
+            out = np.empty((L, L))
+        if out.shape != (L, L) or out.dtype != np.float64 or not out.flags.c_contiguous:
+            raise ValueError("out must be a C-contiguous L x L float64 array")
+        self.check(lib().rs_knn_sims_part(self.h, kind, L, n_right, _ptr(rowptr), _ptr(ids),
+                                          _ptr(ratings), part, n_parts, _ptr(out)))
         return out
 
     def sim_pair(self, kind, a_ids, a_r, b_ids, b_r):

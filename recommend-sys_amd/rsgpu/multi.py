@@ -52,3 +52,38 @@ class ItemShardedStep:
             self.dist.all_reduce(self.dP)
             self.dist.all_reduce(self.gbsum)
             self.plan.apply_delta_t(self.dP, self.gbsum, self.inv_total, self.stream)
+
+
+# ------------------------------------------------------------------------------------------------
+# KNN similarities across GPUs: independent units, no collective.  Every rank holds the
+# whole (replicated) rating matrix and computes only its part of the Sims (rs_knn_sims_part: its
+# 128-row blocks, zig-zag balanced over the triangle); the parts write disjoint entries of ONE
+# host-visible L x L float64 file, so the ranks only synchronise (two barriers), they never
+# exchange data.
+
+def knn_part_blocks(n_left: int, part: int, n_parts: int) -> np.ndarray:
+    """0/1 ownership of the 128-row blocks by `part` (rs_knn_part_blocks; host only)."""
+    from . import lib
+    out = np.zeros((n_left + 127) // 128, np.int32)
+    rc = lib().rs_knn_part_blocks(n_left, part, n_parts, out.ctypes.data)
+    if rc != 0:
+        raise ValueError("bad knn part arguments")
+    return out
+
+
+def knn_sims_shared(compute_part, n_left: int, path: str, rank: int, world: int, dist):
+    """Assemble the Sims of all ranks in the .npy file `path` (e.g. under /dev/shm).
+    compute_part(part, n_parts, out) writes the part's entries into the L x L memmap `out`; on a
+    GPU rank it is ctx.knn_sims(kind, rowptr, ids, ratings, n_right, part, n_parts, out).  Returns a
+    read-only memmap of the full matrix on every rank."""
+    if rank == 0:
+        mm = np.lib.format.open_memmap(path, mode="w+", dtype=np.float64, shape=(n_left, n_left))
+        mm.flush()
+        del mm
+    dist.barrier()
+    out = np.lib.format.open_memmap(path, mode="r+")
+    compute_part(rank, world, out)
+    out.flush()
+    del out
+    dist.barrier()
+    return np.lib.format.open_memmap(path, mode="r")

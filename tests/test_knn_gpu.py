@@ -105,6 +105,30 @@ def test_knn_sims_random_bitwise(ctx, kind, L, Rn, values):
     assert np.array_equal(ref[m].view(np.uint64), got[m].view(np.uint64))
 
 
+@pytest.mark.parametrize("n_parts", [2, 3, 8])
+@pytest.mark.parametrize("kind,values", [(rsgpu.SIM_COSINE, np.arange(1, 11) / 2.0),
+                                         (rsgpu.SIM_MSD, np.arange(1, 6, dtype=float)),
+                                         (rsgpu.SIM_PEARSON, np.arange(1, 6, dtype=float))])
+def test_knn_sims_parts_assemble_bitwise(ctx, n_parts, kind, values):
+    """the parts of rs_knn_sims_part (one per GPU in production; run here one after the
+    other on one device into one buffer) write disjoint entries whose union is rs_knn_sims, bitwise."""
+    L, Rn = 700, 900  # 6 row blocks of 128 (last ragged): every part owns >= 0 blocks
+    rowptr, ids, rr = _random_lists(L, Rn, 0.04, values, seed=n_parts + kind)
+    full = ctx.knn_sims(kind, rowptr, ids, rr, Rn)
+    out = np.full((L, L), 12345.0)
+    written = np.zeros((L, L), np.int32)
+    for part in range(n_parts):
+        mark = np.full((L, L), 12345.0)
+        ctx.knn_sims(kind, rowptr, ids, rr, Rn, part=part, n_parts=n_parts, out=mark)
+        wrote = mark != 12345.0
+        written += wrote
+        out[wrote] = mark[wrote]
+    assert written.max() == 1 and written.min() == 1  # disjoint and complete
+    assert np.array_equal(np.isnan(full), np.isnan(out))
+    m = ~np.isnan(full)
+    assert np.array_equal(full[m].view(np.uint64), out[m].view(np.uint64))
+
+
 def test_knn_empty_rows(ctx):
     rowptr = np.array([0, 0, 2, 2, 3], np.int64)
     ids = np.array([1, 0, 1], np.int32)

@@ -129,3 +129,65 @@ def test_two_rank_gloo_matches_single_process_merge():
         # each rank's item shard equals the shard trained in the single-process run
         mine = multi.item_shard_of(ni, 2) == rank
         np.testing.assert_allclose(Q[mine], plans[rank].Q[mine], atol=1e-6)
+
+
+# ---- KNN sims across ranks: disjoint parts, one shared file, no collective ----------
+
+def test_knn_part_blocks_partition_and_balance():
+    """Every 128-row block has exactly one owner and the triangle work (T - t tiles for block t) is
+    spread within 10 % (ML-20M: T = 209) for 2..8 parts."""
+    for L, n in ((26744, 2), (26744, 4), (26744, 8), (700, 3), (1, 2), (0, 4)):
+        T = (L + 127) // 128
+        own = np.stack([multi.knn_part_blocks(L, p, n) for p in range(n)]) if T else np.zeros((n, 0))
+        assert (own.sum(0) == 1).all()
+        if L == 26744:
+            work = own @ (T - np.arange(T))
+            assert work.max() <= 1.1 * work.min()
+
+
+def _host_part(kind, rowptr, ids, rr):
+    """CPU stand-in for ctx.knn_sims(..., part, n_parts, out): the oracle's Sims, entries of the part
+    only (rows of its blocks from the diagonal rightwards, and their mirrors)."""
+    full = O.knn_sims(kind, rowptr, ids, rr)
+    L = len(rowptr) - 1
+
+    def compute(part, n_parts, out):
+        own = multi.knn_part_blocks(L, part, n_parts)
+        for t in np.nonzero(own)[0]:
+            a0, a1 = 128 * t, min(L, 128 * t + 128)
+            out[a0:a1, a0:] = full[a0:a1, a0:]
+            out[a0:, a0:a1] = full[a0:, a0:a1]
+    return compute, full
+
+
+def _knn_worker(rank, world, port, path, out):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    rowptr, ids, rr = _knn_lists()
+    compute, _ = _host_part(0, rowptr, ids, rr)
+    S = multi.knn_sims_shared(compute, len(rowptr) - 1, path, rank, world, dist)
+    out[rank] = np.array(S)
+    dist.destroy_process_group()
+
+
+def _knn_lists():
+    rng = np.random.default_rng(5)
+    L, Rn = 300, 400
+    rows, cols = np.nonzero(rng.random((L, Rn)) < 0.05)
+    return O.csr_by(rows, L, cols, rng.integers(1, 6, len(rows)).astype(float))
+
+
+def test_two_rank_gloo_knn_sims_shared_file(tmp_path):
+    port = _free_port()
+    path = str(tmp_path / "sims.npy")
+    with mp.Manager() as m:
+        out = m.dict()
+        mp.spawn(_knn_worker, args=(2, port, path, out), nprocs=2, join=True)
+        res = dict(out)
+    rowptr, ids, rr = _knn_lists()
+    full = O.knn_sims(0, rowptr, ids, rr)
+    for rank in (0, 1):
+        got = res[rank]
+        assert np.array_equal(np.isnan(full), np.isnan(got))
+        m = ~np.isnan(full)
+        assert np.array_equal(full[m], got[m])
