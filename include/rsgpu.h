@@ -84,6 +84,36 @@ typedef struct {
     int32_t write_back; /* FAST only: RS_SGD_WB_* (RS_SGD_WB_ATOMIC = 0 is the default) */
 } rs_sgd_params;
 
+/* ---- TrainSet construction on the host (no GPU involved) ------------------ *
+ * rs_trainset_ids   <- core/data.go:137-151 NewTrainSet inner-id maps: inner[t] = first-appearance
+ *                      index of outer[t] (call once for Users, once for Items); outer_of_inner
+ *                      (n_unique entries, may be NULL) is the inverse map.  Parallel over n_threads
+ *                      (<= 0: up to 16), result independent of it.
+ * rs_csr_build      <- core/data.go:185-216 UserRatings / ItemRatings: stable CSR of COO rows (data
+ *                      order inside a row); rowptr n_rows + 1, cols_out / vals_out nnz (vals_out may be
+ *                      NULL), caller-allocated.
+ * rs_global_mean    <- core/data.go:134 stat.Mean(Ratings): fixed-order chunked sum / n.           */
+int rs_trainset_ids(int64_t n, const int64_t* outer, int32_t n_threads, int32_t* inner,
+                    int64_t* outer_of_inner, int32_t* n_unique);
+int rs_csr_build(int64_t nnz, int32_t n_rows, const int32_t* rows, const int32_t* cols,
+                 const double* vals, int32_t n_threads, int64_t* rowptr, int32_t* cols_out,
+                 float* vals_out);
+int rs_global_mean(int64_t n, const double* ratings, int32_t n_threads, double* mean);
+
+/* ---- synthetic benchmark sets (not a reference function; BASELINE configs[4] generator) ------- *
+ * Inner-id user-CSR of n_users x n_items: lognormal user degrees (mean mean_deg, sigma, clamped to
+ * [min_deg, max_deg]), Zipf(zipf_s) item popularity over a seeded id permutation, no repeated
+ * (u, i), integer ratings 1..5 from a planted rank-4 model.  Only the ratings of items in
+ * [item_lo, item_hi) are kept (an item-range shard of the same full set).  Deterministic in seed,
+ * independent of n_threads.  rs_synth_csr exposes the arrays (owned by the handle). */
+typedef struct rs_synth rs_synth;
+int rs_synth_create(int32_t n_users, int32_t n_items, double mean_deg, double sigma, int32_t min_deg,
+                    int32_t max_deg, double zipf_s, uint64_t seed, int32_t item_lo, int32_t item_hi,
+                    int32_t n_threads, rs_synth** out);
+int rs_synth_csr(const rs_synth* s, int64_t* nnz, const int64_t** rowptr, const int32_t** cols,
+                 const float** vals);
+void rs_synth_destroy(rs_synth* s);
+
 /* ---- context -------------------------------------------------------------------------------- */
 int32_t rs_version(void);
 int rs_device_count(int32_t* n);
@@ -173,6 +203,16 @@ int rs_knn_plan_predict(rs_knn_plan* plan, int32_t type, int32_t n_right, const 
 typedef struct rs_svd_plan rs_svd_plan;
 
 int rs_svd_plan_create(rs_ctx* ctx, const rs_ratings* r, int32_t n_factors, rs_svd_plan** out);
+/* The same plan from a user-CSR already in hand (rs_csr_build's output, or a generator's): rowptr has
+ * n_users + 1 entries, cols / vals are in data order inside each row (data.go:185-199).  Skips the
+ * COO -> CSR pass; the caller's arrays are copied and not retained. */
+int rs_svd_plan_create_csr(rs_ctx* ctx, int32_t n_users, int32_t n_items, const int64_t* rowptr,
+                           const int32_t* cols, const float* vals, int32_t n_factors, rs_svd_plan** out);
+/* Device-side init, replacing svd.go:77-85 without a host round trip of the factors: biases 0,
+ * factor entries N(mean, std_dev) from a counter-based hash of (seed, row, column), rows of P then Q
+ * (the reference's draws come from the unseeded global math/rand, Q4: distribution kept, sequence
+ * not); GlobalBias set to the FAST warm start (the mean rating, biases being 0). */
+int rs_svd_plan_init_normal(rs_svd_plan* plan, double mean, double std_dev, uint64_t seed);
 void rs_svd_plan_destroy(rs_svd_plan* plan);
 /* host f64 -> device f32 (any of the pointers may be NULL = leave unchanged) */
 int rs_svd_plan_upload(rs_svd_plan* plan, const double* P, const double* Q, const double* bu,

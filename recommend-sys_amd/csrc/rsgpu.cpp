@@ -91,8 +91,10 @@ extern "C" int rs_open(int32_t device, rs_ctx** out) {
         if (!out) return rs::set_error(nullptr, RS_ERR_INVALID, "out is NULL");
         *out = nullptr;
         int c = 0;
-        if (hipGetDeviceCount(&c) != hipSuccess || c == 0)
-            return rs::set_error(nullptr, RS_ERR_NO_DEVICE, "no HIP device visible");
+        const hipError_t ce = hipGetDeviceCount(&c);
+        if (ce != hipSuccess || c == 0)
+            return rs::set_error(nullptr, RS_ERR_NO_DEVICE,
+                                 std::string("no HIP device visible (hipGetDeviceCount: ") + hipGetErrorString(ce) + ")");
         if (device < 0 || device >= c) return rs::set_error(nullptr, RS_ERR_INVALID, "device out of range");
         hipDeviceProp_t prop;
         RS_HIP(hipGetDeviceProperties(&prop, device));

@@ -655,6 +655,7 @@ struct rs_svd_plan {
     int32_t light_blocks = 0;  // cap on the light blocks (each wave strides over light items; 0 = none)
     rs::DevBuf<int64_t> trace;  // diagnostic: {start, chain end, drained} per work item (RS_SGD_WB_ATOMIC)
     int32_t ring_depth = 8;
+    double mean_rating = 0.0;  // of the plan's ratings (FAST GlobalBias warm start at init)
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
     double last_ms = 0.0;
     int32_t last_launches = 0;
@@ -887,25 +888,30 @@ static void build_work(rs_svd_plan* pl) {
     RS_HIP(hipStreamSynchronize(s));  // host vectors die with this scope
 }
 
-static void plan_build(rs_ctx* ctx, const rs_ratings* r, int32_t k, rs_svd_plan* pl) {
+// Plan from a user-CSR (data order inside each row); the COO entry point builds it first.
+static void plan_build_csr(rs_ctx* ctx, int32_t n_users, int32_t n_items, UserCSR&& csr, int32_t k,
+                           rs_svd_plan* pl) {
     hipStream_t s = ctx->stream;
     pl->ctx = ctx;
     pl->light_blocks = default_light_blocks(ctx);
-    pl->n_users = r->n_users;
-    pl->n_items = r->n_items;
+    pl->n_users = n_users;
+    pl->n_items = n_items;
     pl->k = k;
     pl->ld = fast_ld(k);
-    pl->nnz = r->nnz;
-    UserCSR csr;
-    build_csr(r->nnz, r->n_users, r->users, r->items, r->ratings, csr);
+    pl->nnz = static_cast<int64_t>(csr.cols.size());
     // items / ratings padded by 128 entries: the kernels read 32-entry chunks up to two ahead
     // (entries < e + 96 for a row ending at e)
+    {
+        double sum = 0.0;
+        for (float v : csr.vals) sum += v;
+        pl->mean_rating = pl->nnz > 0 ? sum / static_cast<double>(pl->nnz) : 0.0;
+    }
     csr.vals.resize(csr.vals.size() + 128, 0.f);
     pl->ratings.alloc(csr.vals.size());
     pl->ratings.upload(csr.vals.data(), csr.vals.size(), s);
     pl->h_rowptr = std::move(csr.rowptr);
     pl->h_cols = std::move(csr.cols);
-    pl->P.alloc(static_cast<size_t>(std::max(1, r->n_users)) * pl->ld);
+    pl->P.alloc(static_cast<size_t>(std::max(1, n_users)) * pl->ld);
     RS_HIP(hipMemsetAsync(pl->P.p, 0, pl->P.n * sizeof(float), s));
     build_items(pl);
     build_work(pl);
@@ -914,6 +920,56 @@ static void plan_build(rs_ctx* ctx, const rs_ratings* r, int32_t k, rs_svd_plan*
     RS_HIP(hipEventCreate(&pl->ev0));
     RS_HIP(hipEventCreate(&pl->ev1));
     RS_HIP(hipStreamSynchronize(s));  // host CSR vectors die with this scope
+}
+
+static void plan_build(rs_ctx* ctx, const rs_ratings* r, int32_t k, rs_svd_plan* pl) {
+    UserCSR csr;
+    build_csr(r->nnz, r->n_users, r->users, r->items, r->ratings, csr);
+    plan_build_csr(ctx, r->n_users, r->n_items, std::move(csr), k, pl);
+}
+
+// Factor init on the device (svd.go:77-85: biases 0, factor entries N(mean, std), users then items;
+// the Go draws come from the unseeded global math/rand, Q4, so only the distribution is kept): entry
+// (row, f) of the P-then-Q row sequence is mean + std * Box-Muller(hash(seed, row, f)).
+__device__ __forceinline__ uint64_t dev_splitmix(uint64_t x) {
+    x += 0x9e3779b97f4a7c15ULL;
+    x = (x ^ (x >> 30)) * 0xbf58476d1ce4e5b9ULL;
+    x = (x ^ (x >> 27)) * 0x94d049bb133111ebULL;
+    return x ^ (x >> 31);
+}
+
+__global__ __launch_bounds__(256) void init_normal_kernel(float* __restrict__ F, int64_t rows, int64_t row0,
+                                                          int32_t k, int32_t ld, double mean, double sd,
+                                                          uint64_t seed) {
+    const int64_t n = rows * ld;
+    for (int64_t x = static_cast<int64_t>(blockIdx.x) * 256 + threadIdx.x; x < n;
+         x += static_cast<int64_t>(gridDim.x) * 256) {
+        const int64_t r = x / ld;
+        const int32_t f = static_cast<int32_t>(x - r * ld);
+        float v = 0.f;
+        if (f < k) {
+            const uint64_t h = dev_splitmix(dev_splitmix(seed ^ static_cast<uint64_t>(row0 + r)) ^ static_cast<uint64_t>(f));
+            const double u1 = (static_cast<double>(h >> 11) + 0.5) * (1.0 / 9007199254740992.0);
+            const double u2 = (static_cast<double>(dev_splitmix(h) >> 11) + 0.5) * (1.0 / 9007199254740992.0);
+            v = static_cast<float>(mean + sd * (sqrt(-2.0 * log(u1)) * cos(6.283185307179586 * u2)));
+        }
+        F[x] = v;
+    }
+}
+
+static void plan_init_normal(rs_svd_plan* pl, double mean, double sd, uint64_t seed) {
+    plan_sync_last(pl);
+    hipStream_t s = pl->ctx->stream;
+    hipLaunchKernelGGL(init_normal_kernel, dim3(4096), dim3(256), 0, s, pl->P.p, static_cast<int64_t>(pl->n_users),
+                       int64_t{0}, pl->k, pl->ld, mean, sd, seed);
+    hipLaunchKernelGGL(init_normal_kernel, dim3(4096), dim3(256), 0, s, pl->Q.p, static_cast<int64_t>(pl->n_items),
+                       static_cast<int64_t>(pl->n_users), pl->k, pl->ld, mean, sd, seed);
+    RS_HIP(hipGetLastError());
+    sync_item_copies(pl, s, 1);
+    // FAST GlobalBias warm start (common.hpp gb_warm_start) with zero biases: the mean rating
+    const double gb = pl->mean_rating;
+    pl->gb.upload(&gb, 1, s);
+    RS_HIP(hipStreamSynchronize(s));
 }
 
 // f64 factor rows (stride k) + bias -> f32 rows of ld floats with the bias in column ld - 1
@@ -1043,6 +1099,48 @@ extern "C" int rs_svd_plan_create(rs_ctx* ctx, const rs_ratings* r, int32_t n_fa
             throw;
         }
         *out = pl;
+        return RS_OK;
+    });
+}
+
+extern "C" int rs_svd_plan_create_csr(rs_ctx* ctx, int32_t n_users, int32_t n_items, const int64_t* rowptr,
+                                      const int32_t* cols, const float* vals, int32_t n_factors,
+                                      rs_svd_plan** out) {
+    if (!ctx) return rs::set_error(ctx, RS_ERR_INVALID, "ctx is NULL");
+    return rs_guard(ctx, [&]() -> int {
+        if (!out) return rs::set_error(ctx, RS_ERR_INVALID, "out is NULL");
+        *out = nullptr;
+        if (n_users < 0 || n_items < 0 || !rowptr) return rs::set_error(ctx, RS_ERR_INVALID, "bad CSR sizes");
+        if (n_factors < 1 || n_factors > rs::kMaxFactors)
+            return rs::set_error(ctx, RS_ERR_UNSUPPORTED, "n_factors must be in [1, 511]");
+        if (rowptr[0] != 0) return rs::set_error(ctx, RS_ERR_INVALID, "rowptr[0] != 0");
+        for (int32_t u = 0; u < n_users; ++u)
+            if (rowptr[u + 1] < rowptr[u]) return rs::set_error(ctx, RS_ERR_INVALID, "rowptr not monotone at " + std::to_string(u));
+        const int64_t nnz = rowptr[n_users];
+        if (nnz > 0 && (!cols || !vals)) return rs::set_error(ctx, RS_ERR_INVALID, "cols / vals are NULL");
+        for (int64_t t = 0; t < nnz; ++t)
+            if (cols[t] < 0 || cols[t] >= n_items)
+                return rs::set_error(ctx, RS_ERR_INVALID, "item id out of range at " + std::to_string(t));
+        rs::UserCSR csr;
+        csr.rowptr.assign(rowptr, rowptr + n_users + 1);
+        csr.cols.assign(cols, cols + nnz);
+        csr.vals.assign(vals, vals + nnz);
+        auto* pl = new rs_svd_plan();
+        try {
+            rs::plan_build_csr(ctx, n_users, n_items, std::move(csr), n_factors, pl);
+        } catch (...) {
+            delete pl;
+            throw;
+        }
+        *out = pl;
+        return RS_OK;
+    });
+}
+
+extern "C" int rs_svd_plan_init_normal(rs_svd_plan* pl, double mean, double std_dev, uint64_t seed) {
+    if (!pl) return rs::set_error(nullptr, RS_ERR_INVALID, "plan is NULL");
+    return rs_guard(pl->ctx, [&]() -> int {
+        rs::plan_init_normal(pl, mean, std_dev, seed);
         return RS_OK;
     });
 }

@@ -33,6 +33,9 @@ HEADER_SYMBOLS = (
     "rs_svd_plan_epoch_delta", "rs_svd_plan_apply_delta", "rs_svd_plan_last_kernel_ms",
     "rs_svd_plan_predict", "rs_svd_plan_evaluate",
     "rs_knn_plan_create", "rs_knn_plan_destroy", "rs_knn_plan_sims", "rs_knn_plan_predict",
+    "rs_svd_plan_create_csr", "rs_svd_plan_init_normal",
+    "rs_trainset_ids", "rs_csr_build", "rs_global_mean",
+    "rs_synth_create", "rs_synth_csr", "rs_synth_destroy",
 )
 
 
@@ -110,6 +113,16 @@ def lib():
             "rs_knn_plan_predict": (C.c_int, [_vp, _i32, _i32, _vp, _vp, _vp, _vp, _vp, _vp, _dbl,
                                               _i32, _i32, _i64, _vp, _vp, _vp]),
             "rs_svd_plan_evaluate": (C.c_int, [_vp, _i64, _vp, _vp, _vp, C.POINTER(_dbl), C.POINTER(_dbl)]),
+            "rs_svd_plan_create_csr": (C.c_int, [_vp, _i32, _i32, _vp, _vp, _vp, _i32, C.POINTER(_vp)]),
+            "rs_svd_plan_init_normal": (C.c_int, [_vp, _dbl, _dbl, C.c_uint64]),
+            "rs_trainset_ids": (C.c_int, [_i64, _vp, _i32, _vp, _vp, C.POINTER(_i32)]),
+            "rs_csr_build": (C.c_int, [_i64, _i32, _vp, _vp, _vp, _i32, _vp, _vp, _vp]),
+            "rs_global_mean": (C.c_int, [_i64, _vp, _i32, C.POINTER(_dbl)]),
+            "rs_synth_create": (C.c_int, [_i32, _i32, _dbl, _dbl, _i32, _i32, _dbl, C.c_uint64, _i32,
+                                          _i32, _i32, C.POINTER(_vp)]),
+            "rs_synth_csr": (C.c_int, [_vp, C.POINTER(_i64), C.POINTER(_vp), C.POINTER(_vp),
+                                       C.POINTER(_vp)]),
+            "rs_synth_destroy": (None, [_vp]),
         }
         for name, (res, args) in sig.items():
             f = getattr(L, name)
@@ -133,6 +146,71 @@ def device_count() -> int:
     n = _i32(0)
     code = lib().rs_device_count(C.byref(n))
     return n.value if code == RS_OK else 0
+
+
+# ---- TrainSet construction (host C++, no GPU; core/data.go:131-216) ------------------------------
+
+def trainset_ids(outer, n_threads=0):
+    """data.go:137-151: inner ids by first appearance.  Returns (inner int32, outer_of_inner int64)."""
+    o = np.ascontiguousarray(outer, dtype=np.int64)
+    inner = np.empty(len(o), np.int32)
+    inv = np.empty(len(o), np.int64)
+    n = _i32(0)
+    _check(lib().rs_trainset_ids(len(o), _ptr(o), n_threads, _ptr(inner), _ptr(inv), C.byref(n)))
+    return inner, inv[:n.value].copy()
+
+
+def csr_build(rows, cols, vals, n_rows, n_threads=0):
+    """data.go:185-216: stable CSR (data order in a row).  Returns (rowptr int64, cols int32, vals f32)."""
+    r = np.ascontiguousarray(rows, dtype=np.int32)
+    c = np.ascontiguousarray(cols, dtype=np.int32)
+    v = np.ascontiguousarray(vals, dtype=np.float64)
+    rowptr = np.empty(n_rows + 1, np.int64)
+    co, vo = np.empty(len(r), np.int32), np.empty(len(r), np.float32)
+    _check(lib().rs_csr_build(len(r), n_rows, _ptr(r), _ptr(c), _ptr(v), n_threads, _ptr(rowptr),
+                              _ptr(co), _ptr(vo)))
+    return rowptr, co, vo
+
+
+def global_mean(ratings, n_threads=0):
+    """data.go:134 stat.Mean (fixed-order chunked sum)."""
+    r = np.ascontiguousarray(ratings, dtype=np.float64)
+    m = _dbl(0)
+    _check(lib().rs_global_mean(len(r), _ptr(r), n_threads, C.byref(m)))
+    return m.value
+
+
+class Synth:
+    """Synthetic inner-id user-CSR (rs_synth_*; BASELINE configs[4] generator).  The arrays are
+    numpy views of library memory, valid until close()."""
+
+    def __init__(self, n_users, n_items, mean_deg=100.0, sigma=1.0, min_deg=1, max_deg=None,
+                 zipf_s=0.9, seed=20250826, item_lo=0, item_hi=None, n_threads=0):
+        h = C.c_void_p()
+        max_deg = n_items // 2 if max_deg is None else max_deg
+        item_hi = n_items if item_hi is None else item_hi
+        _check(lib().rs_synth_create(n_users, n_items, mean_deg, sigma, min_deg, max_deg, zipf_s,
+                                     seed, item_lo, item_hi, n_threads, C.byref(h)))
+        self.h, self.n_users, self.n_items = h, n_users, n_items
+        nnz, rp, co, va = _i64(0), C.c_void_p(), C.c_void_p(), C.c_void_p()
+        _check(lib().rs_synth_csr(h, C.byref(nnz), C.byref(rp), C.byref(co), C.byref(va)))
+        self.nnz = nnz.value
+        mk = lambda p, t, n: np.ctypeslib.as_array(C.cast(p, C.POINTER(t)), shape=(n,)) if n else np.empty(0)
+        self.rowptr = mk(rp, C.c_int64, n_users + 1)
+        self.cols = mk(co, C.c_int32, self.nnz)
+        self.vals = mk(va, C.c_float, self.nnz)
+
+    def close(self):
+        if self.h:
+            self.rowptr = self.cols = self.vals = None
+            lib().rs_synth_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
 
 
 class Ratings:
@@ -268,6 +346,9 @@ class Context:
     def svd_plan(self, r: Ratings, n_factors: int) -> "SvdPlan":
         return SvdPlan(self, r, n_factors)
 
+    def svd_plan_csr(self, n_users, n_items, rowptr, cols, vals, n_factors: int) -> "SvdPlan":
+        return SvdPlan(self, None, n_factors, csr=(n_users, n_items, rowptr, cols, vals))
+
     def knn_plan(self, kind, rowptr, ids, ratings, n_right) -> "KnnPlan":
         return KnnPlan(self, kind, rowptr, ids, ratings, n_right)
 
@@ -275,16 +356,30 @@ class Context:
 class SvdPlan:
     """Device-resident user-CSR + factors (rs_svd_plan_*)."""
 
-    def __init__(self, ctx: Context, r: Ratings, n_factors: int):
+    def __init__(self, ctx: Context, r, n_factors: int, csr=None):
+        """r: Ratings (COO), or None with csr = (n_users, n_items, rowptr, cols, vals float32)."""
         self.ctx = ctx
-        self.n_users, self.n_items, self.k = r.n_users, r.n_items, n_factors
-        self.nnz = len(r.ratings)
         h = C.c_void_p()
-        rc = r.c()
         self.h = None
-        ctx.check(lib().rs_svd_plan_create(ctx.h, C.byref(rc), n_factors, C.byref(h)))
+        if csr is None:
+            self.n_users, self.n_items, self.k = r.n_users, r.n_items, n_factors
+            self.nnz = len(r.ratings)
+            rc = r.c()
+            ctx.check(lib().rs_svd_plan_create(ctx.h, C.byref(rc), n_factors, C.byref(h)))
+        else:
+            nu, ni, rowptr, cols, vals = csr
+            rowptr = np.ascontiguousarray(rowptr, np.int64)
+            cols = np.ascontiguousarray(cols, np.int32)
+            vals = np.ascontiguousarray(vals, np.float32)
+            self.n_users, self.n_items, self.k, self.nnz = nu, ni, n_factors, int(rowptr[nu])
+            ctx.check(lib().rs_svd_plan_create_csr(ctx.h, nu, ni, _ptr(rowptr), _ptr(cols), _ptr(vals),
+                                                   n_factors, C.byref(h)))
         self.h = h
         ctx._plans.add(self)
+
+    def init_normal(self, mean=0.0, std=0.1, seed=1):
+        """Device-side factor init (svd.go:77-85 distribution); GlobalBias = FAST warm start."""
+        self.ctx.check(lib().rs_svd_plan_init_normal(self.h, mean, std, seed))
 
     def upload(self, P=None, Q=None, bu=None, bi=None, gb=None):
         arrs = [None if a is None else np.ascontiguousarray(a, dtype=np.float64)
