@@ -18,6 +18,8 @@
  *   rs_svd_predict    <- core/svd.go:32-51     (*SVD).Predict (batched, host)
  *   rs_svd_plan_predict / _evaluate <- svd.go:32-51, utils.go:162-180 on the device (§8f row 1)
  *   rs_baseline_fit   <- core/base.go:135-163  (*BaseLine).Fit (used by KNN-baseline knn.go:179)
+ *   rs_knn_sims(kind RS_DEV_SLOPE_ONE) <- core/slope_one.go:47-93 (*SlopeOne).Fit dev matrix (§8f row 4)
+ *   rs_slope_one_predict <- core/slope_one.go:21-45 (*SlopeOne).Predict on the device-resident dev
  *
  * Conventions
  *   - Ratings arrive as the TrainSet's COO triples (core/data.go:109-127) in TRAIN-SET ORDER with
@@ -61,6 +63,11 @@ extern "C" {
 #define RS_SIM_COSINE 0
 #define RS_SIM_MSD 1
 #define RS_SIM_PEARSON 2
+/* Not a similarity: the SlopeOne deviation matrix dev (core/slope_one.go:64-92), computed by the same
+ * pairwise machinery (rs_knn_sims / _part / rs_knn_plan_create with left = items, right = users):
+ * dev[i][j] = mean over co-rating users of (r_ui - r_uj), dev[j][i] = -dev[i][j], 0 on the diagonal
+ * and where nothing is co-rated. */
+#define RS_DEV_SLOPE_ONE 3
 
 typedef struct rs_ctx rs_ctx;
 
@@ -104,12 +111,14 @@ int rs_global_mean(int64_t n, const double* ratings, int32_t n_threads, double* 
  * Inner-id user-CSR of n_users x n_items: lognormal user degrees (mean mean_deg, sigma, clamped to
  * [min_deg, max_deg]), Zipf(zipf_s) item popularity over a seeded id permutation, no repeated
  * (u, i), integer ratings 1..5 from a planted rank-4 model.  Only the ratings of items in
- * [item_lo, item_hi) are kept (an item-range shard of the same full set).  Deterministic in seed,
- * independent of n_threads.  rs_synth_csr exposes the arrays (owned by the handle). */
+ * [item_lo, item_hi) are kept (an item-range shard of the same full set), and only the rows of users
+ * [user_lo, user_hi) are generated (a user-range shard: row x is user user_lo + x; the CSR has
+ * user_hi - user_lo rows).  Deterministic in seed, independent of n_threads.  rs_synth_csr exposes
+ * the arrays (owned by the handle). */
 typedef struct rs_synth rs_synth;
 int rs_synth_create(int32_t n_users, int32_t n_items, double mean_deg, double sigma, int32_t min_deg,
                     int32_t max_deg, double zipf_s, uint64_t seed, int32_t item_lo, int32_t item_hi,
-                    int32_t n_threads, rs_synth** out);
+                    int32_t user_lo, int32_t user_hi, int32_t n_threads, rs_synth** out);
 int rs_synth_csr(const rs_synth* s, int64_t* nnz, const int64_t** rowptr, const int32_t** cols,
                  const float** vals);
 void rs_synth_destroy(rs_synth* s);
@@ -202,6 +211,13 @@ int rs_knn_plan_predict(rs_knn_plan* plan, int32_t type, int32_t n_right, const 
  * float64.  Epochs are enqueued on `stream` without host syncs. */
 typedef struct rs_svd_plan rs_svd_plan;
 
+/* SlopeOne.Predict (core/slope_one.go:21-45) on a plan created with kind RS_DEV_SLOPE_ONE: user CSR of
+ * the TrainSet in data order (UserRatings, data.go:185-199), inner ids (-1 = unknown -> global mean /
+ * user mean as the reference); bitwise equal to the sequential definition. */
+int rs_slope_one_predict(rs_knn_plan* plan, int32_t n_users, const int64_t* user_rowptr,
+                         const int32_t* user_items, const double* user_ratings, double global_mean,
+                         int64_t n, const int32_t* users, const int32_t* items, double* out);
+
 int rs_svd_plan_create(rs_ctx* ctx, const rs_ratings* r, int32_t n_factors, rs_svd_plan** out);
 /* The same plan from a user-CSR already in hand (rs_csr_build's output, or a generator's): rowptr has
  * n_users + 1 entries, cols / vals are in data order inside each row (data.go:185-199).  Skips the
@@ -257,6 +273,18 @@ int rs_svd_plan_epoch_delta(rs_svd_plan* plan, float lr, float reg, void* dP, vo
                             void* stream);
 int rs_svd_plan_apply_delta(rs_svd_plan* plan, const void* dP, const void* gbsum,
                             double inv_total_nnz, void* stream);
+/* ---- user-sharded multi-GPU (the dual partition, SURVEY §8e "measured alternative") ---------- *
+ * Each rank builds a plan over its user range (local user ids) with ALL items; Q and b_i are
+ * replicated, P and b_u are exclusive to the rank.  Per epoch: rs_svd_plan_epoch_qdelta runs the
+ * FAST epoch (P in place), writes dQ[i] = w_i (q_i(end) - q_i(start)) (bias column included) and
+ * gbsum as rs_svd_plan_epoch_delta, and leaves Q at the epoch start; the caller all-reduces dQ
+ * (n_items x ld fp32 -- for U >> I far less than the item-sharded n_users x ld) and gbsum, then
+ * rs_svd_plan_apply_qdelta.  w_i = (ratings of i on this rank) / (ratings of i on all ranks). */
+int rs_svd_plan_set_item_weights(rs_svd_plan* plan, const float* w /* host, n_items; NULL clears */);
+int rs_svd_plan_epoch_qdelta(rs_svd_plan* plan, float lr, float reg, void* dQ, void* gbsum,
+                             void* stream);
+int rs_svd_plan_apply_qdelta(rs_svd_plan* plan, const void* dQ, const void* gbsum,
+                             double inv_total_nnz, void* stream);
 /* Device pointers of the resident state (layout above); ld = row stride in floats. */
 int rs_svd_plan_device_ptrs(rs_svd_plan* plan, void** P, void** Q, void** gb_f64, int32_t* ld);
 /* Per-launch timing: when on, rs_svd_plan_epochs brackets every SGD kernel with HIP events on

@@ -694,3 +694,81 @@ double or_gb_warm_start(int32_t n_users, const int64_t* rowptr, const int32_t* i
         for (int64_t t = rowptr[x]; t < rowptr[x + 1]; t++) s += r[t] - bu[x] - bi[items[t]];
     return s / (double)nnz;
 }
+
+/* ------------------------------------------------------------------------------------------ */
+/* SlopeOne                                                                                    */
+
+void or_slope_one_fit(int32_t L, const int64_t* rowptr, const int32_t* ids, const double* ratings,
+                      double* dev) {
+    const int64_t nnz = rowptr[L];
+    int32_t* sid = (int32_t*)malloc((size_t)(nnz > 0 ? nnz : 1) * sizeof(int32_t));
+    double* sr = (double*)malloc((size_t)(nnz > 0 ? nnz : 1) * sizeof(double));
+    idr* tmp = (idr*)malloc((size_t)(nnz > 0 ? nnz : 1) * sizeof(idr));
+    /* slope_one.go:62 sorts(itemRatings) (data.go:236-243): each item's list by user ID */
+    for (int32_t x = 0; x < L; x++) {
+        const int64_t b = rowptr[x], e = rowptr[x + 1];
+        for (int64_t t = b; t < e; t++) {
+            tmp[t - b].id = ids[t];
+            tmp[t - b].r = ratings[t];
+        }
+        qsort(tmp, (size_t)(e - b), sizeof(idr), cmp_idr);
+        for (int64_t t = b; t < e; t++) {
+            sid[t] = tmp[t - b].id;
+            sr[t] = tmp[t - b].r;
+        }
+    }
+    free(tmp);
+    const int64_t LL = (int64_t)L * L;
+    for (int64_t t = 0; t < LL; t++) dev[t] = 0.0;           /* slope_one.go:59 newZeroMatrix */
+    for (int32_t i = 0; i < L; i++) {                        /* slope_one.go:75 (nJobs = 1) */
+        const int64_t bi = rowptr[i], ni = rowptr[i + 1] - bi;
+        for (int32_t j = 0; j < i; j++) {                    /* slope_one.go:76 */
+            const int64_t bj = rowptr[j], nj = rowptr[j + 1] - bj;
+            double count = 0.0, sum = 0.0;
+            int64_t ptr = 0;
+            for (int64_t k = 0; k < ni && ptr < nj; k++) {   /* slope_one.go:78-87 */
+                const int32_t uid = sid[bi + k];
+                while (ptr < nj && sid[bj + ptr] < uid) ptr++;
+                if (ptr < nj && sid[bj + ptr] == uid) {
+                    count++;
+                    sum += sr[bi + k] - sr[bj + ptr];
+                }
+            }
+            if (count > 0) {                                 /* slope_one.go:88-91 */
+                dev[(int64_t)i * L + j] = sum / count;
+                dev[(int64_t)j * L + i] = -dev[(int64_t)i * L + j];
+            }
+        }
+    }
+    free(sid);
+    free(sr);
+}
+
+void or_slope_one_predict(int32_t L, const double* dev, int32_t n_users, const int64_t* user_rowptr,
+                          const int32_t* user_items, const double* user_ratings, double global_mean,
+                          int64_t n, const int32_t* users, const int32_t* items, double* out) {
+    for (int64_t q = 0; q < n; q++) {
+        const int32_t u = users[q], i = items[q];
+        const int ku = u >= 0 && u < n_users, ki = i >= 0 && i < L;
+        double prediction = 0.0;
+        if (ku) {                                            /* slope_one.go:26-30 */
+            double sum = 0.0, count = 0.0;                   /* means(), data.go:222-235 */
+            for (int64_t t = user_rowptr[u]; t < user_rowptr[u + 1]; t++) {
+                sum += user_ratings[t];
+                count++;
+            }
+            prediction = sum / count;
+        } else {
+            prediction = global_mean;
+        }
+        if (ki && ku) {                                      /* slope_one.go:32-42 */
+            double sum = 0.0, count = 0.0;
+            for (int64_t t = user_rowptr[u]; t < user_rowptr[u + 1]; t++) {
+                sum += dev[(int64_t)i * L + user_items[t]];
+                count++;
+            }
+            if (count > 0) prediction += sum / count;
+        }
+        out[q] = prediction;
+    }
+}

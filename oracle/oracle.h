@@ -92,6 +92,17 @@ void or_knn_predict(int32_t type, int32_t L, const double* sims, const int64_t* 
 void or_baseline_fit(int64_t n, const int32_t* u, const int32_t* i, const double* r,
                      int32_t epochs, double lr, double reg, double* bu, double* bi, double* gb);
 
+/* slope_one.go:47-93 SlopeOne.Fit with nJobs = 1: dev (L x L, L = items) from the item CSR (rows =
+ * ItemRatings in data order, user ids; sorted by ID here, slope_one.go:62). */
+void or_slope_one_fit(int32_t L, const int64_t* rowptr, const int32_t* ids, const double* ratings,
+                      double* dev);
+
+/* slope_one.go:21-45 SlopeOne.Predict for inner ids (-1 = unknown); user CSR = UserRatings in data
+ * order; userMeans = means() (data.go:222-235). */
+void or_slope_one_predict(int32_t L, const double* dev, int32_t n_users, const int64_t* user_rowptr,
+                          const int32_t* user_items, const double* user_ratings, double global_mean,
+                          int64_t n, const int32_t* users, const int32_t* items, double* out);
+
 /* ---- restatements of THIS build's own GPU schedules (not of the reference) ---- */
 
 /* Fast-mode SGD schedule of recommend-sys_amd/csrc/sgd.hip, single-threaded: work items are

@@ -71,6 +71,9 @@ def lib():
                                        C.c_int32, _f64p]
         L.or_gb_warm_start.argtypes = [C.c_int32, _i64p, _i32p, _f64p, _f64p, _f64p]
         L.or_gb_warm_start.restype = C.c_double
+        L.or_slope_one_fit.argtypes = [C.c_int32, _i64p, _i32p, _f64p, _f64p]
+        L.or_slope_one_predict.argtypes = [C.c_int32, _f64p, C.c_int32, _i64p, _i32p, _f64p,
+                                           C.c_double, C.c_int64, _i32p, _i32p, _f64p]
         _lib = L
     return _lib
 
@@ -238,6 +241,23 @@ def knn_predict(type_, sims, right_rowptr, right_ids, right_r, means, stddevs, b
                          _f64(right_r), _f64(z if means is None else means),
                          _f64(z if stddevs is None else stddevs), _f64(z if bias is None else bias),
                          global_mean, k, min_k, len(left), _i32(left), _i32(right), out)
+    return out
+
+
+def slope_one_fit(rowptr, ids, ratings):
+    """slope_one.go:47-93: dev matrix from the item CSR (user ids, data order)."""
+    L = len(rowptr) - 1
+    out = np.empty((L, L))
+    lib().or_slope_one_fit(L, _i64(rowptr), _i32(ids), _f64(ratings), out)
+    return out
+
+
+def slope_one_predict(dev, user_rowptr, user_items, user_ratings, global_mean, users, items):
+    """slope_one.go:21-45 for inner-id pairs (-1 = unknown)."""
+    out = np.empty(len(users))
+    lib().or_slope_one_predict(dev.shape[0], _f64(dev), len(user_rowptr) - 1, _i64(user_rowptr),
+                               _i32(user_items), _f64(user_ratings), global_mean, len(users),
+                               _i32(users), _i32(items), out)
     return out
 
 

@@ -450,6 +450,17 @@ __global__ __launch_bounds__(256) void svd_apply_delta_kernel(float4* __restrict
     if (blockIdx.x == 0 && threadIdx.x == 0) gb[0] += gbsum[0] * inv_total;
 }
 
+// User-sharded mode: dQ = w_i (Q - Q0) for the n_items item rows, and Q is restored to Q0.
+__global__ __launch_bounds__(256) void svd_qdelta_kernel(float* __restrict__ Q, const float* __restrict__ Q0,
+                                                         const float* __restrict__ w, float* __restrict__ dQ,
+                                                         int64_t n, int32_t ld) {
+    for (int64_t t = blockIdx.x * 256 + threadIdx.x; t < n; t += static_cast<int64_t>(gridDim.x) * 256) {
+        const float q0 = Q0[t];
+        dQ[t] = w[t / ld] * (Q[t] - q0);
+        Q[t] = q0;
+    }
+}
+
 // sum of block partials in fixed order (multi-GPU: the ranks' sums are all-reduced, then applied)
 __global__ __launch_bounds__(256) void gb_sum_kernel(const double* __restrict__ partial, int64_t n,
                                                      double* __restrict__ out) {
@@ -648,6 +659,8 @@ struct rs_svd_plan {
     rs::DevBuf<float> P, Q;  // bias in column ld - 1
     rs::DevBuf<double> gb, partial;
     rs::DevBuf<float> uw;  // per-user share of this shard (multi-GPU delta mode)
+    rs::DevBuf<float> iw;  // per-item share of this shard (user-sharded multi-GPU mode)
+    rs::DevBuf<float> Q0;  // Q at the epoch start (user-sharded mode)
     int32_t n_blocks = 0;
     int32_t write_back = RS_SGD_WB_ATOMIC;
     int32_t heavy_min = 1024;  // work items with at least this many ratings get a producer + 3 writers
@@ -1197,6 +1210,79 @@ extern "C" int rs_svd_plan_epoch_delta(rs_svd_plan* pl, float lr, float reg, voi
         pl->last_launches = pl->timing ? 1 : 2;
         pl->last_stream = s;
         pl->last_ms = -1.0;
+        return RS_OK;
+    });
+}
+
+extern "C" int rs_svd_plan_set_item_weights(rs_svd_plan* pl, const float* w) {
+    if (!pl) return rs::set_error(nullptr, RS_ERR_INVALID, "plan is NULL");
+    return rs_guard(pl->ctx, [&]() -> int {
+        if (!w) {
+            pl->iw.release();
+            return RS_OK;
+        }
+        pl->iw.alloc(std::max(1, pl->n_items));
+        pl->iw.upload(w, pl->n_items, pl->ctx->stream);
+        RS_HIP(hipStreamSynchronize(pl->ctx->stream));
+        return RS_OK;
+    });
+}
+
+extern "C" int rs_svd_plan_epoch_qdelta(rs_svd_plan* pl, float lr, float reg, void* dQ, void* gbsum,
+                                        void* stream) {
+    if (!pl) return rs::set_error(nullptr, RS_ERR_INVALID, "plan is NULL");
+    return rs_guard(pl->ctx, [&]() -> int {
+        if (!dQ || !gbsum) return rs::set_error(pl->ctx, RS_ERR_INVALID, "delta buffers are NULL");
+        if (!pl->iw.p) return rs::set_error(pl->ctx, RS_ERR_INVALID, "item weights not set");
+        hipStream_t s = stream ? static_cast<hipStream_t>(stream) : pl->ctx->stream;
+        const int64_t n = static_cast<int64_t>(pl->n_items) * pl->ld;
+        if (pl->Q0.n != static_cast<size_t>(std::max<int64_t>(1, n))) pl->Q0.alloc(std::max<int64_t>(1, n));
+        if (n) RS_HIP(hipMemcpyAsync(pl->Q0.p, pl->Q.p, n * sizeof(float), hipMemcpyDeviceToDevice, s));
+        if (pl->timing) {
+            if (pl->tev.size() < 2) {
+                for (int x = 0; x < 2; ++x) {
+                    hipEvent_t e;
+                    RS_HIP(hipEventCreate(&e));
+                    pl->tev.push_back(e);
+                }
+            }
+            pl->tev_used = 2;
+            RS_HIP(hipEventRecord(pl->tev[0], s));
+        }
+        RS_HIP(hipEventRecord(pl->ev0, s));
+        rs::launch_fast(pl, lr, reg, s);  // whole user rows: P stored in place (users are exclusive)
+        if (pl->timing) RS_HIP(hipEventRecord(pl->tev[1], s));
+        if (pl->n_split > 0)
+            hipLaunchKernelGGL(rs::svd_merge_rows_kernel, dim3(pl->n_split), dim3(64), 0, s, pl->P.p,
+                               pl->dPs.p, pl->split_rows.p, pl->ld);
+        rs::sync_item_copies(pl, s, 0);  // copies merged into the item rows before the delta
+        if (n)
+            hipLaunchKernelGGL(rs::svd_qdelta_kernel, dim3(1024), dim3(256), 0, s, pl->Q.p, pl->Q0.p,
+                               pl->iw.p, static_cast<float*>(dQ), n, pl->ld);
+        hipLaunchKernelGGL(rs::gb_sum_kernel, dim3(1), dim3(256), 0, s, pl->partial.p,
+                           static_cast<int64_t>(pl->n_blocks), static_cast<double*>(gbsum));
+        RS_HIP(hipGetLastError());
+        RS_HIP(hipEventRecord(pl->ev1, s));
+        pl->last_launches = pl->timing ? 1 : 3;
+        pl->last_stream = s;
+        pl->last_ms = -1.0;
+        return RS_OK;
+    });
+}
+
+extern "C" int rs_svd_plan_apply_qdelta(rs_svd_plan* pl, const void* dQ, const void* gbsum,
+                                        double inv_total_nnz, void* stream) {
+    if (!pl) return rs::set_error(nullptr, RS_ERR_INVALID, "plan is NULL");
+    return rs_guard(pl->ctx, [&]() -> int {
+        if (!dQ || !gbsum) return rs::set_error(pl->ctx, RS_ERR_INVALID, "delta buffers are NULL");
+        hipStream_t s = stream ? static_cast<hipStream_t>(stream) : pl->ctx->stream;
+        const int64_t n4 = static_cast<int64_t>(pl->n_items) * pl->ld / 4;
+        hipLaunchKernelGGL(rs::svd_apply_delta_kernel, dim3(1024), dim3(256), 0, s,
+                           reinterpret_cast<float4*>(pl->Q.p), static_cast<const float4*>(dQ), n4,
+                           pl->gb.p, static_cast<const double*>(gbsum), inv_total_nnz);
+        RS_HIP(hipGetLastError());
+        rs::sync_item_copies(pl, s, 1);  // copies follow the merged item rows
+        pl->last_stream = s;
         return RS_OK;
     });
 }

@@ -49,7 +49,8 @@ __global__ void knn_scatter_kernel(int32_t L, const int64_t* __restrict__ rowptr
         X[static_cast<int64_t>(a) * ldk + ids[t]] = x[t];
 }
 
-// KIND 0 = Cosine (3 contractions), 1 = MSD (4 contractions).
+// KIND 0 = Cosine (3 contractions), 1 = MSD (4 contractions), 2 = SlopeOne deviations
+// (3 contractions: X M^T, M X^T, M M^T; slope_one.go:64-92, see the epilogue).
 //
 // One 128 x 128 tile (ta <= tb) of the upper triangle per workgroup, tiles taken from a host-built
 // list in 16 x 16 super-tile groups so the workgroups resident together share row blocks.  Four
@@ -90,7 +91,7 @@ __global__ __launch_bounds__(256) void knn_sims_mfma_kernel(const int8_t* __rest
                                                             int64_t ldk, int32_t L,
                                                             const int2* __restrict__ tiles,
                                                             double inv_s2, double* __restrict__ S) {
-    constexpr int NC = KIND == 0 ? 3 : 4;
+    constexpr int NC = KIND == 1 ? 4 : 3;
     extern __shared__ __attribute__((aligned(16))) int8_t smem[];
     const int2 tile = tiles[blockIdx.x];
     const int32_t ta = tile.x, tb = tile.y;
@@ -135,9 +136,11 @@ __global__ __launch_bounds__(256) void knn_sims_mfma_kernel(const int8_t* __rest
         for (int j = 0; j < kXPerThread; ++j) {
             *reinterpret_cast<i32x4*>(b + 0 * 2 * kStageMat + dst[j]) = st[j];
             i32x4 v;
+            if constexpr (KIND != 2) {  // SlopeOne never reads X2
 #pragma unroll
-            for (int d = 0; d < 4; ++d) v[d] = static_cast<int>(sq_bytes(static_cast<uint32_t>(st[j][d])));
-            *reinterpret_cast<i32x4*>(b + 1 * 2 * kStageMat + dst[j]) = v;
+                for (int d = 0; d < 4; ++d) v[d] = static_cast<int>(sq_bytes(static_cast<uint32_t>(st[j][d])));
+                *reinterpret_cast<i32x4*>(b + 1 * 2 * kStageMat + dst[j]) = v;
+            }
 #pragma unroll
             for (int d = 0; d < 4; ++d) v[d] = static_cast<int>(mask_bytes(static_cast<uint32_t>(st[j][d])));
             *reinterpret_cast<i32x4*>(b + 2 * 2 * kStageMat + dst[j]) = v;
@@ -167,6 +170,12 @@ __global__ __launch_bounds__(256) void knn_sims_mfma_kernel(const int8_t* __rest
             for (int i = 0; i < 2; ++i)
 #pragma unroll
                 for (int j = 0; j < 2; ++j) {
+                    if constexpr (KIND == 2) {  // s1 = X_a M_b, s2 = M_a X_b, count = M_a M_b
+                        acc[0][i][j] = __builtin_amdgcn_mfma_i32_32x32x32_i8(fa[0][i], fb[2][j], acc[0][i][j], 0, 0, 0);
+                        acc[1][i][j] = __builtin_amdgcn_mfma_i32_32x32x32_i8(fa[2][i], fb[0][j], acc[1][i][j], 0, 0, 0);
+                        acc[2][i][j] = __builtin_amdgcn_mfma_i32_32x32x32_i8(fa[2][i], fb[2][j], acc[2][i][j], 0, 0, 0);
+                        continue;
+                    }
                     acc[0][i][j] = __builtin_amdgcn_mfma_i32_32x32x32_i8(fa[0][i], fb[0][j], acc[0][i][j], 0, 0, 0);
                     acc[1][i][j] = __builtin_amdgcn_mfma_i32_32x32x32_i8(fa[1][i], fb[2][j], acc[1][i][j], 0, 0, 0);
                     acc[2][i][j] = __builtin_amdgcn_mfma_i32_32x32x32_i8(fa[2][i], fb[1][j], acc[2][i][j], 0, 0, 0);
@@ -205,13 +214,26 @@ __global__ __launch_bounds__(256) void knn_sims_mfma_kernel(const int8_t* __rest
                 const int32_t bb = c0 + 32 * j + row;
                 if (a >= L || bb >= L) continue;
                 if (a == bb) {
-                    S[static_cast<int64_t>(a) * L + bb] = nan;
+                    S[static_cast<int64_t>(a) * L + bb] = KIND == 2 ? 0.0 : nan;  // dev: zero matrix
                     continue;
                 }
                 if (ta == tb && a > bb) continue;
                 const int64_t li = acc[0][i][j][q], mi = acc[1][i][j][q], ni = acc[2][i][j][q];
                 double v;
-                if constexpr (KIND == 0) {
+                if constexpr (KIND == 2) {
+                    // slope_one.go:68-88 for the pair i = bb > j = a: sum of (r_bb - r_a) over the
+                    // co-rated users, exact in float64 whatever the order (half-integers) and equal
+                    // to (sum x_bb - sum x_a) / s; dev[i][j] = sum / count, dev[j][i] = -dev[i][j];
+                    // nothing co-rated: both stay 0 (newZeroMatrix).  inv_s2 carries 1 / s here.
+                    double d = 0.0, md = 0.0;
+                    if (ni > 0) {
+                        d = static_cast<double>(mi - li) * inv_s2 / static_cast<double>(ni);
+                        md = -d;
+                    }
+                    S[static_cast<int64_t>(bb) * L + a] = d;
+                    S[static_cast<int64_t>(a) * L + bb] = md;
+                    continue;
+                } else if constexpr (KIND == 0) {
                     const double l = static_cast<double>(li) * inv_s2;
                     const double m = static_cast<double>(mi) * inv_s2;
                     const double n = static_cast<double>(ni) * inv_s2;
@@ -268,7 +290,7 @@ __global__ void row_mean_kernel(int32_t L, const int64_t* __restrict__ rowptr,
     mean[a] = sum / count;
 }
 
-template <int KIND>  // 0 Cosine, 1 MSD, 2 Pearson
+template <int KIND>  // 0 Cosine, 1 MSD, 2 Pearson, 3 SlopeOne dev[b][a] (NaN: nothing co-rated)
 __device__ __forceinline__ double pair_sim(const double* __restrict__ dense_a, const uint8_t* __restrict__ has_a,
                                            double mean_a, int64_t bb, int64_t be,
                                            const int32_t* __restrict__ ids, const double* __restrict__ r,
@@ -296,6 +318,16 @@ __device__ __forceinline__ double pair_sim(const double* __restrict__ dense_a, c
             }
         }
         return 1.0 / (sum / count + 1.0);
+    } else if constexpr (KIND == 3) {  // slope_one.go:72-87 with i = b (walked), j = a (dense)
+        double count = 0.0, sum = 0.0;
+        for (int64_t t = bb; t < be; ++t) {
+            const int32_t id = ids[t];
+            if (has_a[id]) {
+                count++;
+                sum += r[t] - dense_a[id];
+            }
+        }
+        return count > 0 ? sum / count : __builtin_nan("");
     } else {
         double m = 0.0, n = 0.0, l = 0.0;
         for (int64_t t = bb; t < be; ++t) {
@@ -331,12 +363,18 @@ __global__ __launch_bounds__(256) void sims_merge_kernel(
         }
         __syncthreads();
         const double ma = KIND == 2 ? mean[a] : 0.0;
-        if (threadIdx.x == 0) S[static_cast<int64_t>(a) * L + a] = __builtin_nan("");
+        if (threadIdx.x == 0) S[static_cast<int64_t>(a) * L + a] = KIND == 3 ? 0.0 : __builtin_nan("");
         for (int32_t b = a + 1 + threadIdx.x; b < L; b += blockDim.x) {
             const double v = pair_sim<KIND>(dense, has, ma, rowptr[b], rowptr[b + 1], ids, r,
                                             KIND == 2 ? mean[b] : 0.0);
-            S[static_cast<int64_t>(a) * L + b] = v;  // NaN stays NaN (knn.go:205)
-            S[static_cast<int64_t>(b) * L + a] = v;
+            if constexpr (KIND == 3) {  // dev[b][a] = v, dev[a][b] = -v; not co-rated: both 0
+                const bool none = isnan(v);
+                S[static_cast<int64_t>(b) * L + a] = none ? 0.0 : v;
+                S[static_cast<int64_t>(a) * L + b] = none ? 0.0 : -v;
+            } else {
+                S[static_cast<int64_t>(a) * L + b] = v;  // NaN stays NaN (knn.go:205)
+                S[static_cast<int64_t>(b) * L + a] = v;
+            }
         }
         __syncthreads();
         for (int64_t t = rowptr[a] + threadIdx.x; t < rowptr[a + 1]; t += blockDim.x) has[ids[t]] = 0;
@@ -432,18 +470,24 @@ static void sims_device(rs_ctx* ctx, int32_t kind, int32_t L, int32_t R, const S
         }
         DevBuf<int2> dtiles(order.size());
         dtiles.upload(order.data(), order.size(), s);
-        const double inv_s2 = 1.0 / static_cast<double>(scale * scale);
+        // Cosine / MSD scale the sums by 1 / s^2; SlopeOne's differences by 1 / s
+        const double inv_s2 = kind == RS_DEV_SLOPE_ONE ? 1.0 / scale : 1.0 / static_cast<double>(scale * scale);
         const size_t lds = 2 * kStageBytes;
         RS_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(&knn_sims_mfma_kernel<0>),
                                    hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(lds)));
         RS_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(&knn_sims_mfma_kernel<1>),
                                    hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(lds)));
+        RS_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(&knn_sims_mfma_kernel<2>),
+                                   hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(lds)));
         kernel_span_begin(ctx);
         if (kind == RS_SIM_COSINE)
             hipLaunchKernelGGL(knn_sims_mfma_kernel<0>, dim3(order.size()), dim3(256), lds, s, X.p,
                                ldk, L, dtiles.p, inv_s2, dS.p);
-        else
+        else if (kind == RS_SIM_MSD)
             hipLaunchKernelGGL(knn_sims_mfma_kernel<1>, dim3(order.size()), dim3(256), lds, s, X.p,
+                               ldk, L, dtiles.p, inv_s2, dS.p);
+        else
+            hipLaunchKernelGGL(knn_sims_mfma_kernel<2>, dim3(order.size()), dim3(256), lds, s, X.p,
                                ldk, L, dtiles.p, inv_s2, dS.p);
         RS_HIP(hipGetLastError());
         kernel_span_end(ctx);
@@ -470,8 +514,10 @@ static void sims_device(rs_ctx* ctx, int32_t kind, int32_t L, int32_t R, const S
         hipLaunchKernelGGL(sims_merge_kernel<0>, dim3(grid), dim3(256), 0, s, L, R, drow.p, dids.p, dr.p, dmean.p, scratch.p, scratch_has.p, dS.p, drows.p, n_rows);
     else if (kind == RS_SIM_MSD)
         hipLaunchKernelGGL(sims_merge_kernel<1>, dim3(grid), dim3(256), 0, s, L, R, drow.p, dids.p, dr.p, dmean.p, scratch.p, scratch_has.p, dS.p, drows.p, n_rows);
-    else
+    else if (kind == RS_SIM_PEARSON)
         hipLaunchKernelGGL(sims_merge_kernel<2>, dim3(grid), dim3(256), 0, s, L, R, drow.p, dids.p, dr.p, dmean.p, scratch.p, scratch_has.p, dS.p, drows.p, n_rows);
+    else
+        hipLaunchKernelGGL(sims_merge_kernel<3>, dim3(grid), dim3(256), 0, s, L, R, drow.p, dids.p, dr.p, dmean.p, scratch.p, scratch_has.p, dS.p, drows.p, n_rows);
     RS_HIP(hipGetLastError());
     kernel_span_end(ctx);
 }
@@ -569,6 +615,31 @@ __global__ __launch_bounds__(64) void knn_predict_kernel(
     }
 }
 
+// SlopeOne.Predict (core/slope_one.go:21-45), one thread per query, bitwise: prediction = the user's
+// mean rating (means(), data.go:222-235, precomputed by row_mean_kernel in the same order) or the
+// global mean for an unknown user; for a known (user, item) the user's ratings are walked in data
+// order (TrainSet.UserRatings) adding dev[item][j], and sum / count is added.
+__global__ __launch_bounds__(256) void slope_one_predict_kernel(
+    const double* __restrict__ dev, int32_t L, int32_t n_users, const int64_t* __restrict__ urp,
+    const int32_t* __restrict__ uitems, const double* __restrict__ umean, double gmean, int64_t n,
+    const int32_t* __restrict__ users, const int32_t* __restrict__ items, double* __restrict__ out) {
+    const int64_t q = static_cast<int64_t>(blockIdx.x) * 256 + threadIdx.x;
+    if (q >= n) return;
+    const int32_t u = users[q], i = items[q];
+    const bool ku = u >= 0 && u < n_users, ki = i >= 0 && i < L;
+    double prediction = ku ? umean[u] : gmean;
+    if (ku && ki) {
+        const double* row = dev + static_cast<int64_t>(i) * L;
+        double sum = 0.0, count = 0.0;
+        for (int64_t t = urp[u]; t < urp[u + 1]; ++t) {
+            sum += row[uitems[t]];
+            count++;
+        }
+        if (count > 0) prediction += sum / count;
+    }
+    out[q] = prediction;
+}
+
 // Validates a left CSR (rowptr monotone, ids in [0, n_right)) for rs_knn_sims / plan creation.
 static int check_knn_csr(rs_ctx* ctx, int32_t n_left, int32_t n_right, const int64_t* rowptr,
                          const int32_t* ids, const double* ratings) {
@@ -589,7 +660,7 @@ extern "C" int rs_knn_sims_part(rs_ctx* ctx, int32_t kind, int32_t n_left, int32
                                 int32_t part, int32_t n_parts, double* sims) {
     if (!ctx) return rs::set_error(ctx, RS_ERR_INVALID, "ctx is NULL");
     return rs_guard(ctx, [&]() -> int {
-        if (kind < RS_SIM_COSINE || kind > RS_SIM_PEARSON)
+        if (kind < RS_SIM_COSINE || kind > RS_DEV_SLOPE_ONE)
             return rs::set_error(ctx, RS_ERR_INVALID, "unknown similarity kind");
         if (n_parts < 1 || part < 0 || part >= n_parts)
             return rs::set_error(ctx, RS_ERR_INVALID, "part must be in [0, n_parts)");
@@ -641,6 +712,8 @@ extern "C" int rs_sim_pair(rs_ctx* ctx, int32_t kind, int64_t na, const int32_t*
     return rs_guard(ctx, [&]() -> int {
         if (!out || na < 0 || nb < 0 || (na && (!a_ids || !a_r)) || (nb && (!b_ids || !b_r)))
             return rs::set_error(ctx, RS_ERR_INVALID, "bad sim_pair arguments");
+        if (kind < RS_SIM_COSINE || kind > RS_SIM_PEARSON)
+            return rs::set_error(ctx, RS_ERR_INVALID, "unknown similarity kind");
         // a two-row KNN problem on the merge kernel: S[0][1] = sim(a, b)
         int32_t R = 1;
         for (int64_t t = 0; t < na; ++t) R = std::max(R, a_ids[t] + 1);
@@ -672,6 +745,7 @@ extern "C" int rs_sim_pair(rs_ctx* ctx, int32_t kind, int64_t na, const int32_t*
 struct rs_knn_plan {
     rs_ctx* ctx = nullptr;
     int32_t L = 0;
+    int32_t kind = 0;
     rs::DevBuf<double> S;
 };
 
@@ -682,7 +756,7 @@ extern "C" int rs_knn_plan_create(rs_ctx* ctx, int32_t kind, int32_t n_left, int
     return rs_guard(ctx, [&]() -> int {
         if (!out) return rs::set_error(ctx, RS_ERR_INVALID, "out is NULL");
         *out = nullptr;
-        if (kind < RS_SIM_COSINE || kind > RS_SIM_PEARSON)
+        if (kind < RS_SIM_COSINE || kind > RS_DEV_SLOPE_ONE)
             return rs::set_error(ctx, RS_ERR_INVALID, "unknown similarity kind");
         const int st = rs::check_knn_csr(ctx, n_left, n_right, rowptr, ids, ratings);
         if (st != RS_OK) return st;
@@ -690,6 +764,7 @@ extern "C" int rs_knn_plan_create(rs_ctx* ctx, int32_t kind, int32_t n_left, int
         try {
             pl->ctx = ctx;
             pl->L = n_left;
+            pl->kind = kind;
             rs::SortedRows sr;
             rs::sort_rows(n_left, rowptr, ids, ratings, sr);
             const char* env = std::getenv("RSGPU_KNN_NO_MFMA");
@@ -758,6 +833,46 @@ extern "C" int rs_knn_plan_predict(rs_knn_plan* pl, int32_t type, int32_t n_righ
         hipLaunchKernelGGL(rs::knn_predict_kernel, dim3(static_cast<uint32_t>(n)), dim3(64), 0, s,
                            pl->S.p, pl->L, n_right, drp.p, dids.p, drr.p, dm.p, dsd.p, db.p,
                            global_mean, type, k, min_k, n, dl.p, dr.p, dout.p);
+        RS_HIP(hipGetLastError());
+        rs::kernel_span_end(ctx);
+        dout.download(out, n, s);
+        RS_HIP(hipStreamSynchronize(s));
+        return RS_OK;
+    });
+}
+
+extern "C" int rs_slope_one_predict(rs_knn_plan* pl, int32_t n_users, const int64_t* user_rowptr,
+                                    const int32_t* user_items, const double* user_ratings,
+                                    double global_mean, int64_t n, const int32_t* users,
+                                    const int32_t* items, double* out) {
+    if (!pl) return rs::set_error(nullptr, RS_ERR_INVALID, "plan is NULL");
+    rs_ctx* ctx = pl->ctx;
+    return rs_guard(ctx, [&]() -> int {
+        if (pl->kind != RS_DEV_SLOPE_ONE)
+            return rs::set_error(ctx, RS_ERR_INVALID, "plan does not hold a SlopeOne deviation matrix");
+        if (n < 0 || (n > 0 && (!users || !items || !out)))
+            return rs::set_error(ctx, RS_ERR_INVALID, "bad predict arguments");
+        const int st = rs::check_knn_csr(ctx, n_users, pl->L, user_rowptr, user_items, user_ratings);
+        if (st != RS_OK) return st;
+        if (n == 0) return RS_OK;
+        hipStream_t s = ctx->stream;
+        const int64_t base = user_rowptr[0], nnz = user_rowptr[n_users] - base;
+        std::vector<int64_t> rp(user_rowptr, user_rowptr + n_users + 1);
+        for (auto& x : rp) x -= base;
+        rs::DevBuf<int64_t> drp(rp.size());
+        rs::DevBuf<int32_t> dit(std::max<int64_t>(1, nnz)), du(n), di(n);
+        rs::DevBuf<double> dr(std::max<int64_t>(1, nnz)), dmean(std::max(1, n_users)), dout(n);
+        drp.upload(rp.data(), rp.size(), s);
+        dit.upload(user_items + base, nnz, s);
+        dr.upload(user_ratings + base, nnz, s);
+        du.upload(users, n, s);
+        di.upload(items, n, s);
+        rs::kernel_span_begin(ctx);
+        if (n_users > 0)
+            hipLaunchKernelGGL(rs::row_mean_kernel, dim3((n_users + 255) / 256), dim3(256), 0, s, n_users,
+                               drp.p, dr.p, dmean.p);
+        hipLaunchKernelGGL(rs::slope_one_predict_kernel, dim3(static_cast<uint32_t>((n + 255) / 256)), dim3(256),
+                           0, s, pl->S.p, pl->L, n_users, drp.p, dit.p, dmean.p, global_mean, n, du.p, di.p, dout.p);
         RS_HIP(hipGetLastError());
         rs::kernel_span_end(ctx);
         dout.download(out, n, s);

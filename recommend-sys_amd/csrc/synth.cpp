@@ -55,7 +55,9 @@ inline double normal(uint64_t h) {  // Box-Muller on two halves of one stream
 
 static void synth_build(const int32_t n_users, const int32_t n_items, double mean_deg, double sigma,
                         int32_t min_deg, int32_t max_deg, double zipf_s, uint64_t seed, int32_t item_lo,
-                        int32_t item_hi, int32_t n_threads, rs_synth* out) {
+                        int32_t item_hi, int32_t user_lo, int32_t user_hi, int32_t n_threads,
+                        rs_synth* out) {
+    const int32_t n_rows = user_hi - user_lo;  // rows of the output CSR: users [user_lo, user_hi)
     const int32_t T = clamp_threads(n_threads);
     // Zipf CDF over ranks and the rank -> item permutation (Fisher-Yates on the seed)
     std::vector<double> cdf(n_items);
@@ -82,13 +84,13 @@ static void synth_build(const int32_t n_users, const int32_t n_items, double mea
         for (int f = 0; f < kRank; ++f) t[1 + f] = static_cast<float>(0.6 * normal(hash3(seed, 3 + f, x)));
     }
     const double mu = std::log(mean_deg) - 0.5 * sigma * sigma;
-    // thread t generates users [n_users t / T, n_users (t + 1) / T) into its own buffers
+    // thread t generates rows [n_rows t / T, n_rows (t + 1) / T) into its own buffers
     std::vector<std::vector<int32_t>> tc(T);
     std::vector<std::vector<float>> tv(T);
-    out->rowptr.assign(static_cast<size_t>(n_users) + 1, 0);
+    out->rowptr.assign(static_cast<size_t>(n_rows) + 1, 0);
     parallel_run(T, [&](int32_t t) {
-        const int32_t u0 = static_cast<int32_t>(static_cast<int64_t>(n_users) * t / T);
-        const int32_t u1 = static_cast<int32_t>(static_cast<int64_t>(n_users) * (t + 1) / T);
+        const int32_t u0 = user_lo + static_cast<int32_t>(static_cast<int64_t>(n_rows) * t / T);
+        const int32_t u1 = user_lo + static_cast<int32_t>(static_cast<int64_t>(n_rows) * (t + 1) / T);
         std::vector<int32_t> stamp(n_items, -1);  // user that last drew the item (dedup)
         std::vector<int32_t>& cols = tc[t];
         std::vector<float>& vals = tv[t];
@@ -127,22 +129,22 @@ static void synth_build(const int32_t n_users, const int32_t n_items, double mea
                 vals.push_back(static_cast<float>(std::min(5.0, std::max(1.0, std::nearbyint(s)))));
                 ++kept;
             }
-            out->rowptr[static_cast<size_t>(u) + 1] = kept;
+            out->rowptr[static_cast<size_t>(u - user_lo) + 1] = kept;
         }
     });
-    for (int32_t u = 0; u < n_users; ++u) out->rowptr[u + 1] += out->rowptr[u];
-    out->nnz = out->rowptr[n_users];
+    for (int32_t x = 0; x < n_rows; ++x) out->rowptr[x + 1] += out->rowptr[x];
+    out->nnz = out->rowptr[n_rows];
     out->cols.resize(static_cast<size_t>(out->nnz));
     out->vals.resize(static_cast<size_t>(out->nnz));
     parallel_run(T, [&](int32_t t) {
-        const int32_t u0 = static_cast<int32_t>(static_cast<int64_t>(n_users) * t / T);
-        const int64_t o = out->rowptr[u0];
+        const int32_t x0 = static_cast<int32_t>(static_cast<int64_t>(n_rows) * t / T);
+        const int64_t o = out->rowptr[x0];
         std::memcpy(out->cols.data() + o, tc[t].data(), tc[t].size() * sizeof(int32_t));
         std::memcpy(out->vals.data() + o, tv[t].data(), tv[t].size() * sizeof(float));
         std::vector<int32_t>().swap(tc[t]);
         std::vector<float>().swap(tv[t]);
     });
-    out->n_users = n_users;
+    out->n_users = n_rows;
     out->n_items = n_items;
 }
 
@@ -150,17 +152,19 @@ static void synth_build(const int32_t n_users, const int32_t n_items, double mea
 
 extern "C" int rs_synth_create(int32_t n_users, int32_t n_items, double mean_deg, double sigma,
                                int32_t min_deg, int32_t max_deg, double zipf_s, uint64_t seed,
-                               int32_t item_lo, int32_t item_hi, int32_t n_threads, rs_synth** out) {
+                               int32_t item_lo, int32_t item_hi, int32_t user_lo, int32_t user_hi,
+                               int32_t n_threads, rs_synth** out) {
     return rs_guard(nullptr, [&]() -> int {
         if (!out) return rs::set_error(nullptr, RS_ERR_INVALID, "out is NULL");
         *out = nullptr;
         if (n_users < 1 || n_items < 1 || !(mean_deg >= 1.0) || !(sigma >= 0.0) || min_deg < 1 ||
-            max_deg < min_deg || !(zipf_s >= 0.0) || item_lo < 0 || item_hi > n_items || item_lo >= item_hi)
+            max_deg < min_deg || !(zipf_s >= 0.0) || item_lo < 0 || item_hi > n_items || item_lo >= item_hi ||
+            user_lo < 0 || user_hi > n_users || user_lo >= user_hi)
             return rs::set_error(nullptr, RS_ERR_INVALID, "rs_synth_create: bad arguments");
         auto* s = new rs_synth();
         try {
             rs::synth_build(n_users, n_items, mean_deg, sigma, min_deg, max_deg, zipf_s, seed, item_lo,
-                            item_hi, n_threads, s);
+                            item_hi, user_lo, user_hi, n_threads, s);
         } catch (...) {
             delete s;
             throw;

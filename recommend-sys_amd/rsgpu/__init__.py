@@ -21,6 +21,7 @@ RS_ERR_INVALID, RS_ERR_HIP, RS_ERR_NOMEM, RS_ERR_UNSUPPORTED, RS_ERR_NO_DEVICE =
 SGD_FAST, SGD_ORDERED = 0, 1
 WB_ATOMIC, WB_STORE, WB_ATOMIC_DIRECT = 0, 1, 2
 SIM_COSINE, SIM_MSD, SIM_PEARSON = 0, 1, 2
+DEV_SLOPE_ONE = 3  # rs_knn_sims kind: SlopeOne deviation matrix (slope_one.go:64-92)
 
 HEADER_SYMBOLS = (
     "rs_version", "rs_device_count", "rs_open", "rs_close", "rs_last_error", "rs_synchronize",
@@ -33,9 +34,10 @@ HEADER_SYMBOLS = (
     "rs_svd_plan_epoch_delta", "rs_svd_plan_apply_delta", "rs_svd_plan_last_kernel_ms",
     "rs_svd_plan_predict", "rs_svd_plan_evaluate",
     "rs_knn_plan_create", "rs_knn_plan_destroy", "rs_knn_plan_sims", "rs_knn_plan_predict",
-    "rs_svd_plan_create_csr", "rs_svd_plan_init_normal",
+    "rs_svd_plan_create_csr", "rs_svd_plan_init_normal", "rs_slope_one_predict",
     "rs_trainset_ids", "rs_csr_build", "rs_global_mean",
     "rs_synth_create", "rs_synth_csr", "rs_synth_destroy",
+    "rs_svd_plan_set_item_weights", "rs_svd_plan_epoch_qdelta", "rs_svd_plan_apply_qdelta",
 )
 
 
@@ -113,13 +115,17 @@ def lib():
             "rs_knn_plan_predict": (C.c_int, [_vp, _i32, _i32, _vp, _vp, _vp, _vp, _vp, _vp, _dbl,
                                               _i32, _i32, _i64, _vp, _vp, _vp]),
             "rs_svd_plan_evaluate": (C.c_int, [_vp, _i64, _vp, _vp, _vp, C.POINTER(_dbl), C.POINTER(_dbl)]),
+            "rs_slope_one_predict": (C.c_int, [_vp, _i32, _vp, _vp, _vp, _dbl, _i64, _vp, _vp, _vp]),
             "rs_svd_plan_create_csr": (C.c_int, [_vp, _i32, _i32, _vp, _vp, _vp, _i32, C.POINTER(_vp)]),
             "rs_svd_plan_init_normal": (C.c_int, [_vp, _dbl, _dbl, C.c_uint64]),
             "rs_trainset_ids": (C.c_int, [_i64, _vp, _i32, _vp, _vp, C.POINTER(_i32)]),
             "rs_csr_build": (C.c_int, [_i64, _i32, _vp, _vp, _vp, _i32, _vp, _vp, _vp]),
             "rs_global_mean": (C.c_int, [_i64, _vp, _i32, C.POINTER(_dbl)]),
             "rs_synth_create": (C.c_int, [_i32, _i32, _dbl, _dbl, _i32, _i32, _dbl, C.c_uint64, _i32,
-                                          _i32, _i32, C.POINTER(_vp)]),
+                                          _i32, _i32, _i32, _i32, C.POINTER(_vp)]),
+            "rs_svd_plan_set_item_weights": (C.c_int, [_vp, _vp]),
+            "rs_svd_plan_epoch_qdelta": (C.c_int, [_vp, _flt, _flt, _vp, _vp, _vp]),
+            "rs_svd_plan_apply_qdelta": (C.c_int, [_vp, _vp, _vp, _dbl, _vp]),
             "rs_synth_csr": (C.c_int, [_vp, C.POINTER(_i64), C.POINTER(_vp), C.POINTER(_vp),
                                        C.POINTER(_vp)]),
             "rs_synth_destroy": (None, [_vp]),
@@ -185,12 +191,16 @@ class Synth:
     numpy views of library memory, valid until close()."""
 
     def __init__(self, n_users, n_items, mean_deg=100.0, sigma=1.0, min_deg=1, max_deg=None,
-                 zipf_s=0.9, seed=20250826, item_lo=0, item_hi=None, n_threads=0):
+                 zipf_s=0.9, seed=20250826, item_lo=0, item_hi=None, user_lo=0, user_hi=None,
+                 n_threads=0):
+        """Rows are users [user_lo, user_hi) (row x = user user_lo + x); items [item_lo, item_hi)."""
         h = C.c_void_p()
         max_deg = n_items // 2 if max_deg is None else max_deg
         item_hi = n_items if item_hi is None else item_hi
+        user_hi = n_users if user_hi is None else user_hi
         _check(lib().rs_synth_create(n_users, n_items, mean_deg, sigma, min_deg, max_deg, zipf_s,
-                                     seed, item_lo, item_hi, n_threads, C.byref(h)))
+                                     seed, item_lo, item_hi, user_lo, user_hi, n_threads, C.byref(h)))
+        n_users = user_hi - user_lo
         self.h, self.n_users, self.n_items = h, n_users, n_items
         nnz, rp, co, va = _i64(0), C.c_void_p(), C.c_void_p(), C.c_void_p()
         _check(lib().rs_synth_csr(h, C.byref(nnz), C.byref(rp), C.byref(co), C.byref(va)))
@@ -443,6 +453,19 @@ class SvdPlan:
         self.ctx.check(lib().rs_svd_plan_apply_delta(self.h, dP_ptr, gbsum_ptr, inv_total_nnz,
                                                      stream))
 
+    def set_item_weights(self, w):
+        self._iw = None if w is None else np.ascontiguousarray(w, dtype=np.float32)
+        self.ctx.check(lib().rs_svd_plan_set_item_weights(self.h, _ptr(self._iw)))
+
+    def epoch_qdelta_t(self, dQ, gbsum, lr, reg, stream=None):
+        """User-sharded mode: dQ (torch, n_items x ld fp32), gbsum (torch, 1 float64)."""
+        self.ctx.check(lib().rs_svd_plan_epoch_qdelta(self.h, lr, reg, dQ.data_ptr(), gbsum.data_ptr(),
+                                                      stream))
+
+    def apply_qdelta_t(self, dQ, gbsum, inv_total_nnz, stream=None):
+        self.ctx.check(lib().rs_svd_plan_apply_qdelta(self.h, dQ.data_ptr(), gbsum.data_ptr(),
+                                                      inv_total_nnz, stream))
+
     # torch-tensor forms used by rsgpu.multi.ItemShardedStep
     def epoch_delta_t(self, dP, gbsum, lr, reg, stream=None):
         self.epoch_delta(dP.data_ptr(), gbsum.data_ptr(), lr, reg, stream)
@@ -539,6 +562,17 @@ class KnnPlan:
         self.ctx.check(lib().rs_knn_plan_predict(self.h, t, len(rp) - 1, _ptr(rp), _ptr(ri), _ptr(rr),
                                                  *[_ptr(a) for a in arrs], float(global_mean), k, min_k,
                                                  len(lq), _ptr(lq), _ptr(rq), _ptr(out)))
+        return out
+
+    def slope_one_predict(self, user_rowptr, user_items, user_ratings, global_mean, users, items):
+        """slope_one.go:21-45 on the device dev matrix (plan kind DEV_SLOPE_ONE); user CSR in data order."""
+        rp = np.ascontiguousarray(user_rowptr, np.int64)
+        it = np.ascontiguousarray(user_items, np.int32)
+        rr = np.ascontiguousarray(user_ratings, np.float64)
+        u, i = np.ascontiguousarray(users, np.int32), np.ascontiguousarray(items, np.int32)
+        out = np.empty(len(u))
+        self.ctx.check(lib().rs_slope_one_predict(self.h, len(rp) - 1, _ptr(rp), _ptr(it), _ptr(rr),
+                                                  global_mean, len(u), _ptr(u), _ptr(i), _ptr(out)))
         return out
 
     def close(self):

@@ -54,6 +54,41 @@ class ItemShardedStep:
             self.plan.apply_delta_t(self.dP, self.gbsum, self.inv_total, self.stream)
 
 
+class UserShardedStep:
+    """The dual partition (SURVEY §8e "measured alternative"): each rank owns a user range (its plan
+    has local user ids and every item), Q and b_i are replicated.  Per epoch every rank runs its
+    users' FAST epoch with P in place (rs_svd_plan_epoch_qdelta), the ranks all-reduce the
+    count-weighted item deltas (n_items x ld fp32, one collective -- for configs[4], 1M items vs 10M
+    users, a tenth of the item-sharded volume) and the global-bias sum, and every rank applies the
+    same sum (rs_svd_plan_apply_qdelta), so Q, b_i and GlobalBias stay bitwise identical."""
+
+    def __init__(self, plan, dist, item_weights, total_nnz, device=None, stream=None):
+        import torch
+        self.plan, self.dist, self.stream = plan, dist, stream
+        self.dQ = torch.zeros((plan.n_items, plan.ld), dtype=torch.float32, device=device)
+        self.gbsum = torch.zeros(1, dtype=torch.float64, device=device)
+        self.inv_total = 1.0 / total_nnz if total_nnz > 0 else 0.0
+        plan.set_item_weights(item_weights)
+
+    def run(self, n_epochs, lr=0.005, reg=0.02):
+        for _ in range(n_epochs):
+            self.plan.epoch_qdelta_t(self.dQ, self.gbsum, lr, reg, self.stream)
+            self.dist.all_reduce(self.dQ)
+            self.dist.all_reduce(self.gbsum)
+            self.plan.apply_qdelta_t(self.dQ, self.gbsum, self.inv_total, self.stream)
+
+
+def count_weights(local_counts, dist, device=None):
+    """w = local / (sum over ranks) of per-row rating counts (one all-reduce); and the total."""
+    import torch
+    cnt = np.asarray(local_counts, dtype=np.float64)
+    t = torch.tensor(cnt, dtype=torch.float64, device=device)
+    dist.all_reduce(t)
+    tot = t.cpu().numpy()
+    w = np.divide(cnt, tot, out=np.zeros_like(cnt), where=tot > 0)
+    return w.astype(np.float32), float(tot.sum())
+
+
 # ------------------------------------------------------------------------------------------------
 # KNN similarities across GPUs (SURVEY §8e): independent units, no collective.  Every rank holds the
 # whole (replicated) rating matrix and computes only its part of the Sims (rs_knn_sims_part: its

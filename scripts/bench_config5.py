@@ -73,6 +73,9 @@ def main():
     ap.add_argument("--epochs", type=int, default=3)
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--shard", default="0/1")
+    ap.add_argument("--partition", choices=("items", "users"), default="items",
+                    help="items: north_star item-range shards + user-delta all-reduce; users: the dual "
+                         "partition (user-range shards + item-delta all-reduce)")
     ap.add_argument("--item-cap", type=int, default=1 << 16)
     ap.add_argument("--threads", type=int, default=16)
     ap.add_argument("--cpu-budget", type=float, default=10.0)
@@ -88,8 +91,11 @@ def main():
         p, n = rank, world
     else:
         p, n = (int(x) for x in args.shard.split("/"))
-    U, I, k = args.users, args.items, args.k
-    lo, hi = I * p // n, I * (p + 1) // n
+    U_all, I, k = args.users, args.items, args.k
+    by_users = args.partition == "users"
+    lo, hi = (0, I) if by_users else (I * p // n, I * (p + 1) // n)
+    ulo, uhi = (U_all * p // n, U_all * (p + 1) // n) if by_users else (0, U_all)
+    U = uhi - ulo  # rows of this rank's plan
 
     import torch
     dist = None
@@ -103,10 +109,11 @@ def main():
     ctx = rsgpu.Context(dev)  # device first: fail before minutes of data generation
 
     t0 = time.perf_counter()
-    s = rsgpu.Synth(U, I, mean_deg=args.mean_deg, sigma=1.0, min_deg=1, max_deg=I // 2, zipf_s=0.9,
-                    seed=20250826, item_lo=lo, item_hi=hi, n_threads=args.threads)
+    s = rsgpu.Synth(U_all, I, mean_deg=args.mean_deg, sigma=1.0, min_deg=1, max_deg=I // 2, zipf_s=0.9,
+                    seed=20250826, item_lo=lo, item_hi=hi, user_lo=ulo, user_hi=uhi,
+                    n_threads=args.threads)
     t_gen = time.perf_counter() - t0
-    log(f"rank {rank}: generated items [{lo}, {hi}): {s.nnz} ratings in {t_gen:.1f} s")
+    log(f"rank {rank}: generated users [{ulo}, {uhi}) x items [{lo}, {hi}): {s.nnz} ratings in {t_gen:.1f} s")
     deg = np.diff(s.rowptr)
     # hold out every 1024th rating of the CSR (rows are in random draw order)
     hold = np.zeros(s.nnz, bool)
@@ -120,7 +127,8 @@ def main():
     cols, vals = s.cols[keep], s.vals[keep]
     del keep, hold
     nnz = len(cols)
-    max_item = int(np.bincount(cols, minlength=I).max()) if nnz else 0
+    item_cnt = np.bincount(cols, minlength=I)
+    max_item = int(item_cnt.max()) if nnz else 0
     log(f"rank {rank}: train {nnz}, held out {len(r_h)}, max user deg {int(deg.max())}, "
         f"max item deg {max_item}")
     cpu = None
@@ -141,19 +149,18 @@ def main():
     delta = n > 1
     if delta:
         import rsgpu.multi as multi
-        cnt = torch.tensor(tr_deg.astype(np.float64), device=f"cuda:{dev}")
-        if dist:
-            dist.all_reduce(cnt)
-        tot = cnt.cpu().numpy()
-        w = np.divide(tr_deg, tot, out=np.zeros(U), where=tot > 0).astype(np.float32)
-        total_nnz = float(tot.sum()) if dist else float(nnz) * n  # one process: shard of an n-way run
 
         class _Solo:  # one process stands in for the n-way collective (identity all-reduce)
             @staticmethod
-            def all_reduce(t):
+            def all_reduce(t, op=None):
                 return None
-        step = multi.ItemShardedStep(plan, dist or _Solo, w, total_nnz, device=f"cuda:{dev}",
-                                     stream=stream)
+        d = dist or _Solo
+        local = item_cnt if by_users else tr_deg
+        w, total_nnz = multi.count_weights(local, d, device=f"cuda:{dev}")
+        if not dist:
+            total_nnz = float(nnz) * n  # one process: one shard of an n-way run
+        Step = multi.UserShardedStep if by_users else multi.ItemShardedStep
+        step = Step(plan, d, w, total_nnz, device=f"cuda:{dev}", stream=stream)
         run = lambda e: step.run(e, args.lr, args.reg)
     else:
         run = lambda e: plan.epochs(e, args.lr, args.reg, stream)
@@ -189,7 +196,8 @@ def main():
         line = {
             "config": "SVD nFactors=256 synthetic 10M x 1M x ~1B, item-sharded (BASELINE configs[4])",
             "shard": f"{p}/{n}" if world == 1 else f"all/{world}",
-            "n_gpus": world, "n_users": U, "n_items": I, "items_this_rank": hi - lo,
+            "partition": args.partition,
+            "n_gpus": world, "n_users": U_all, "users_this_rank": U, "n_items": I, "items_this_rank": hi - lo,
             "nnz_this_rank": nnz, "nnz_total": total, "n_factors": k,
             "max_user_deg": int(deg.max()), "max_item_deg": max_item, "item_cap": args.item_cap,
             "mode": "delta (multi-GPU protocol)" if delta else "single plan",
@@ -199,7 +207,7 @@ def main():
             "roofline": {"bound": "hbm", "algorithmic_bytes_per_launch": ab,
                          "achieved_GBs": ab / (kms / max(1, nl) / 1e3) / 1e9, "peak_GBs": HBM_PEAK,
                          "frac": ab / (kms / max(1, nl) / 1e3) / 1e9 / HBM_PEAK},
-            "allreduce_bytes_per_epoch": U * plan.ld * 4 + 8 if delta else 0,
+            "allreduce_bytes_per_epoch": ((I if by_users else U) * plan.ld * 4 + 8) if delta else 0,
             "holdout": {"n": int(len(r_h)), "rmse_init": rmse0, "rmse": rmse, "mae": mae,
                         "epochs_trained": args.warmup + args.epochs + 1},
             "gen_s": t_gen, "plan_build_s": t_plan,

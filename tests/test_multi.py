@@ -1,6 +1,6 @@
-"""Item-sharded multi-GPU schedule (rsgpu.multi): world_size-2 gloo tests on CPU with a host model
-of the plan (the shard's epoch is the oracle's restatement of the fast kernel's schedule), checked
-against a single-process computation of the same merge rule."""
+"""Item-sharded and user-sharded multi-GPU schedules (rsgpu.multi): world_size-2 gloo tests on CPU
+with a host model of the plan (the shard's epoch is the oracle's restatement of the fast kernel's
+schedule), checked against a single-process computation of the same merge rule."""
 import os
 import socket
 
@@ -129,6 +129,109 @@ def test_two_rank_gloo_matches_single_process_merge():
         # each rank's item shard equals the shard trained in the single-process run
         mine = multi.item_shard_of(ni, 2) == rank
         np.testing.assert_allclose(Q[mine], plans[rank].Q[mine], atol=1e-6)
+
+
+# ---- user-sharded (dual) partition: users split by range, item deltas all-reduced ---------------
+
+class HostUserPlan:
+    """CPU stand-in for SvdPlan's Q-delta interface over a user range (local user ids)."""
+
+    def __init__(self, users, items, r, n_users, n_items, P0, Q0, gb0):
+        self.k = P0.shape[1]
+        self.n_items, self.ld = n_items, self.k + 1
+        self.rowptr, self.items, self.r = O.csr_by(users, n_users, items, r)
+        self.P, self.Q = P0.copy(), Q0.copy()
+        self.bu, self.bi, self.gb = np.zeros(n_users), np.zeros(n_items), gb0
+        self.w = None
+
+    def set_item_weights(self, w):
+        self.w = np.asarray(w, np.float64)
+
+    def epoch_qdelta_t(self, dQ, gbsum, lr, reg, stream=None):
+        P, Q, bu, bi, g = O.svd_fit_chunked(self.rowptr, self.items, self.r, self.P, self.Q, 1 << 30,
+                                            bu=self.bu, bi=self.bi, gb=self.gb, epochs=1, lr=lr,
+                                            reg=reg, warm=False)
+        self.P, self.bu = P, bu
+        d = np.zeros((self.n_items, self.ld))
+        d[:, :self.k] = self.w[:, None] * (Q - self.Q)
+        d[:, self.k] = self.w * (bi - self.bi)
+        dQ.copy_(torch.from_numpy(d.astype(np.float32)))
+        nnz = float(self.rowptr[-1])
+        gbsum.copy_(torch.tensor([(g - self.gb) * nnz]))
+
+    def apply_qdelta_t(self, dQ, gbsum, inv_total, stream=None):
+        d = dQ.numpy().astype(np.float64)
+        self.Q = self.Q + d[:, :self.k]
+        self.bi = self.bi + d[:, self.k]
+        self.gb = self.gb + float(gbsum.item()) * inv_total
+
+
+def user_ranges(nu, world):
+    return [(nu * p // world, nu * (p + 1) // world) for p in range(world)]
+
+
+def user_shard(u, i, r, lo, hi):
+    m = (u >= lo) & (u < hi)
+    return (u[m] - lo).astype(np.int32), i[m], r[m]
+
+
+def reference_user_merge(u, i, r, nu, ni, P0, Q0, world, epochs=EPOCHS):
+    plans = []
+    cnt = []
+    for lo, hi in user_ranges(nu, world):
+        su, si, sr = user_shard(u, i, r, lo, hi)
+        plans.append(HostUserPlan(su, si, sr, hi - lo, ni, P0[lo:hi], Q0, 3.0))
+        cnt.append(np.bincount(si, minlength=ni))
+    tot = np.sum(cnt, 0)
+    for s, p in enumerate(plans):
+        p.set_item_weights(np.divide(cnt[s], tot, out=np.zeros(ni), where=tot > 0))
+    for _ in range(epochs):
+        ds, gs = [], []
+        for p in plans:
+            dQ, g = torch.zeros((ni, p.ld)), torch.zeros(1, dtype=torch.float64)
+            p.epoch_qdelta_t(dQ, g, 0.005, 0.02)
+            ds.append(dQ)
+            gs.append(g)
+        dsum, gsum = sum(ds), sum(gs)
+        for p in plans:
+            p.apply_qdelta_t(dsum, gsum, 1.0 / len(r))
+    return plans
+
+
+def _user_worker(rank, world, port, out):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    u, i, r, nu, ni = make_data(seed=3)
+    rng = np.random.default_rng(2)
+    P0, Q0 = rng.normal(0, 0.1, (nu, K)), rng.normal(0, 0.1, (ni, K))
+    lo, hi = user_ranges(nu, world)[rank]
+    su, si, sr = user_shard(u, i, r, lo, hi)
+    plan = HostUserPlan(su, si, sr, hi - lo, ni, P0[lo:hi], Q0, 3.0)
+    w, total = multi.count_weights(np.bincount(si, minlength=ni), dist)
+    assert total == len(r)
+    multi.UserShardedStep(plan, dist, w, total).run(EPOCHS)
+    out[rank] = (plan.P, plan.Q, plan.bu, plan.bi, plan.gb)
+    dist.destroy_process_group()
+
+
+def test_two_rank_gloo_user_sharded_matches_single_process_merge():
+    port = _free_port()
+    with mp.Manager() as m:
+        out = m.dict()
+        mp.spawn(_user_worker, args=(2, port, out), nprocs=2, join=True)
+        res = dict(out)
+    u, i, r, nu, ni = make_data(seed=3)
+    rng = np.random.default_rng(2)
+    P0, Q0 = rng.normal(0, 0.1, (nu, K)), rng.normal(0, 0.1, (ni, K))
+    plans = reference_user_merge(u, i, r, nu, ni, P0, Q0, 2)
+    for rank in (0, 1):
+        P, Q, bu, bi, gb = res[rank]
+        np.testing.assert_allclose(Q, plans[rank].Q, atol=1e-6)       # replicated item state
+        np.testing.assert_allclose(bi, plans[rank].bi, atol=1e-6)
+        np.testing.assert_array_equal(res[0][1], res[1][1])
+        assert abs(gb - plans[rank].gb) < 1e-9 and res[0][4] == res[1][4]
+        np.testing.assert_allclose(P, plans[rank].P, atol=1e-6)       # the rank's own users
+        np.testing.assert_allclose(bu, plans[rank].bu, atol=1e-6)
 
 
 # ---- KNN sims across ranks (SURVEY §8e): disjoint parts, one shared file, no collective ----------

@@ -161,3 +161,38 @@ def test_knn_accuracy_regression(ml100k_folds, type_, bound):
     k=40, minK=1 defaults of knn.go:79-81, 226-227)."""
     r, m = _knn_cv(ml100k_folds[:2], type_)
     assert r <= bound[0] + EPS and m <= bound[1] + EPS, (r, m)
+
+
+def test_slope_one_hand_case():
+    """slope_one.go:64-92 on a worked 3-user x 3-item case: dev[i][j] = mean over co-raters of
+    r_i - r_j, dev[j][i] = -dev[i][j], 0 where nothing is co-rated and on the diagonal."""
+    # item rows (user ids, ratings), data order unsorted on purpose
+    rowptr = np.array([0, 3, 5, 6], np.int64)
+    ids = np.array([2, 0, 1, 0, 2, 1], np.int32)
+    r = np.array([4.0, 5.0, 3.0, 2.0, 1.0, 4.0])
+    dev = O.slope_one_fit(rowptr, ids, r)
+    # item0: u0 5, u1 3, u2 4; item1: u0 2, u2 1; item2: u1 4
+    assert dev[1, 0] == ((2 - 5) + (1 - 4)) / 2 and dev[0, 1] == -dev[1, 0]
+    assert dev[2, 0] == (4 - 3) / 1 and dev[0, 2] == -1.0
+    assert dev[2, 1] == 0.0 and dev[1, 2] == 0.0  # no co-rater
+    assert np.all(np.diag(dev) == 0)
+    # Predict (slope_one.go:21-45): user 0 rated items 0 and 1 (data order 0 then 1)
+    urp = np.array([0, 2, 4, 6], np.int64)
+    uit = np.array([0, 1, 0, 2, 0, 1], np.int32)
+    ur = np.array([5.0, 2.0, 3.0, 4.0, 4.0, 1.0])
+    p = O.slope_one_predict(dev, urp, uit, ur, 3.1, np.array([0, -1, 0, 1]), np.array([2, 2, -1, 1]))
+    assert p[0] == 3.5 + (dev[2, 0] + dev[2, 1]) / 2
+    assert p[1] == 3.1 and p[2] == 3.5
+    assert p[3] == 3.5 + (dev[1, 0] + dev[1, 2]) / 2
+
+
+def test_slope_one_accuracy_regression(ml100k_folds):
+    """core/base_test.go:46-48 TestSlopeOne: 5-fold ML-100K RMSE <= 0.946+0.008, MAE <= 0.743+0.008."""
+    def fp(f):
+        ip, iid, ir = O.csr_by(f.ii, f.ni, f.iu, f.r)
+        up, uit, ur = O.csr_by(f.iu, f.nu, f.ii, f.r)
+        dev = O.slope_one_fit(ip, iid, ir)
+        return O.slope_one_predict(dev, up, uit, ur, float(np.mean(f.r)), f.tu, f.ti)
+
+    r, m = _cv(ml100k_folds, fp)
+    assert r <= 0.946 + EPS and m <= 0.743 + EPS, (r, m)

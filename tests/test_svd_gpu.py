@@ -336,6 +336,49 @@ def test_item_sharded_delta_mode_two_shards(ctx):
         pl.close()
 
 
+def test_user_sharded_qdelta_two_shards(ctx):
+    """rs_svd_plan_epoch_qdelta / apply_qdelta with two user-range shards on one device and the
+    all-reduce done on the host: equal to the host model of the merge rule (test_multi's
+    reference_user_merge; race-free input, so every kernel epoch is deterministic)."""
+    import torch
+    from test_multi import reference_user_merge, user_ranges, user_shard
+    u, i, r, nu, ni = _disjoint_input(n_users=120, k=16)
+    u, i = u.astype(np.int32), i.astype(np.int32)
+    k, epochs = 16, 3
+    rng = np.random.default_rng(9)
+    P0, Q0 = rng.normal(0, 0.1, (nu, k)), rng.normal(0, 0.1, (ni, k))
+    plans, cnt = [], []
+    for lo, hi in user_ranges(nu, 2):
+        su, si, sr = user_shard(u, i, r, lo, hi)
+        pl = ctx.svd_plan(rsgpu.Ratings(su, si, sr, hi - lo, ni), k)
+        pl.upload(P0[lo:hi], Q0, np.zeros(hi - lo), np.zeros(ni), 3.0)
+        plans.append(pl)
+        cnt.append(np.bincount(si, minlength=ni))
+    tot = np.sum(cnt, 0)
+    for pl, c in zip(plans, cnt):
+        pl.set_item_weights(np.divide(c, tot, out=np.zeros(ni), where=tot > 0))
+    ld = plans[0].ld
+    dQs = [torch.zeros((ni, ld), dtype=torch.float32, device="cuda") for _ in plans]
+    gss = [torch.zeros(1, dtype=torch.float64, device="cuda") for _ in plans]
+    for _ in range(epochs):
+        for pl, dQ, g in zip(plans, dQs, gss):
+            pl.epoch_qdelta_t(dQ, g, 0.005, 0.02)
+        torch.cuda.synchronize()
+        dsum, gsum = dQs[0] + dQs[1], gss[0] + gss[1]
+        for pl in plans:
+            pl.apply_qdelta_t(dsum, gsum, 1.0 / len(r))
+        torch.cuda.synchronize()
+    ref = reference_user_merge(u, i, r, nu, ni, P0, Q0, 2, epochs=epochs)
+    for s, pl in enumerate(plans):
+        P, Q, bu, bi, gb = pl.download()
+        np.testing.assert_allclose(Q, ref[s].Q, atol=TOL)
+        np.testing.assert_allclose(bi, ref[s].bi, atol=TOL)
+        np.testing.assert_allclose(P, ref[s].P, atol=TOL)
+        np.testing.assert_allclose(bu, ref[s].bu, atol=TOL)
+        assert abs(gb - ref[s].gb) < TOL
+        pl.close()
+
+
 def test_plan_predict_and_evaluate_on_device(ctx, ml100k):
     """batched Predict (svd.go:32-51, unknown ids -> newID rules) and RMSE / MAE
     (utils.go:162-180) on the device factors equal the host restatement on the same factors."""
