@@ -164,7 +164,7 @@ def main():
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
                          "traffic": traffic,
-                         "kernel": "svd_epoch_hybrid_kernel<E=2,D=8>",
+                         "kernel": "svd_epoch_hybrid_kernel<E=2,D=8,merge> (hot replicas 256x8)",
                          "avg_kernel_us": avg_kernel_s * 1e6,
                          "algorithmic_bytes_per_launch": ab},
             "finite": finite,

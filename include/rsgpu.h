@@ -259,6 +259,13 @@ int rs_svd_plan_set_split(rs_svd_plan* plan, int32_t split_cap);
  * ceil(deg / item_cap) row copies; its ratings are dealt over them in user-CSR order and the copies
  * are merged by count-weighted average after every epoch.  Spreads the float atomics of hot rows. */
 int rs_svd_plan_set_item_split(rs_svd_plan* plan, int32_t item_cap);
+/* Hot replicas: the n_hot most-rated items (0 = none) get `copies` row copies (2..8) over which their
+ * ratings are dealt, and in RS_SGD_WB_ATOMIC (hybrid) epochs one extra block keeps the copies merged
+ * while the epoch runs (delta sum: every update reaches every copy, at most one merge round late; a
+ * final round after the epoch leaves them equal).  Spreads a hot item's memory-side float atomics
+ * over several rows.  Hot replicas win over item_cap splitting for the items they take.
+ * Default 256 x 8 (set n_hot = 0 to turn them off). */
+int rs_svd_plan_set_hot_replicas(rs_svd_plan* plan, int32_t n_hot, int32_t copies);
 /* ---- item-sharded multi-GPU (north_star: Q sharded by item range, users replicated) --------- *
  * Each rank builds a plan over its item shard.  Per epoch: rs_svd_plan_epoch_delta leaves P at the
  * epoch start and writes dP[u] = w_u (p_u(end) - p_u(start)) (bias column included; for a split

@@ -262,14 +262,28 @@ __device__ __forceinline__ void lds_store_relaxed(int32_t* p, int32_t v) {
     __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
 }
 
-template <int E, int D, bool DROP = false>
+//
+// MERGE (hot replicas, rs_svd_plan_set_hot_replicas): the n_live most-rated items have R row copies
+// (their ratings dealt over the copies), so the memory-side float atomics of one hot item are spread
+// over R rows at different addresses instead of queueing on one.  The copies are kept one row in
+// Hogwild terms by a merger -- the grid's last block -- that, until every other block has counted
+// itself done in *done, repeatedly takes each live item's copies c_r and its last merged value L
+// (qlast) and sets every copy to N = L + sum_r (c_r - L) by adding N - c_r(read) with float atomics
+// (adds that land between the read and the add are kept, and counted in the next round), then
+// L = N.  Every update is applied to every copy exactly once (delta sum, not an average); a copy
+// misses the other copies' updates for at most one merge round.  svd_live_merge_kernel repeats the
+// round once after the epoch so the item row and its copies leave the epoch equal.
+constexpr int kMaxLiveCopies = 8;
+
+template <int E, int D, bool DROP = false, bool MERGE = false>
 __global__ __launch_bounds__(256) void svd_epoch_hybrid_kernel(
     const int32_t* __restrict__ wk_user, const int64_t* __restrict__ wk_rng,
     const float* __restrict__ wk_frac, int32_t n_work, int32_t n_heavy,
     const int32_t* __restrict__ items, const float* __restrict__ ratings, float* __restrict__ P,
     float* Q, int32_t q_bytes, const double* __restrict__ gb_in, double* __restrict__ gb_partial,
     float lr, float reg, float* __restrict__ dP, const float* __restrict__ uw, int32_t whole_direct,
-    int64_t* __restrict__ trace) {
+    int64_t* __restrict__ trace, const int4* __restrict__ live_meta, int32_t n_live,
+    float* __restrict__ qlast, int32_t* __restrict__ done) {
     constexpr int R = HeavyRing<E>::kRing, NB = HeavyRing<E>::kBatch, LD = 64 * E, NW = 3;
     // the producer's vmcnt holds only its q_i loads: prefetch as deep as the 63-op counter allows
     constexpr int DH = E == 1 ? 32 : (E == 2 ? 32 : (E <= 4 ? 16 : 8));
@@ -283,9 +297,59 @@ __global__ __launch_bounds__(256) void svd_epoch_hybrid_kernel(
     const int32_t lane4 = lane * 4;
     const float gb0 = static_cast<float>(gb_in[0]);
     const int blk = static_cast<int>(blockIdx.x);
+    const int n_merge_blocks = MERGE ? (n_live + 3) / 4 : 0;
+    const int n_sgd_blocks = static_cast<int>(gridDim.x) - n_merge_blocks;
     double contrib = 0.0;
+    if (MERGE && blk >= n_sgd_blocks) {  // mergers: one wave per live item (block-uniform branch)
+        const int h = (blk - n_sgd_blocks) * 4 + wib;
+        if (threadIdx.x == 0) gb_partial[blk] = 0.0;
+        if (h >= n_live) return;
+        const int4 m = live_meta[h];
+        const int R = m.z;
+        float last[E];
+#pragma unroll
+        for (int x = 0; x < E; ++x) last[x] = qlast[static_cast<int64_t>(h) * LD + lane + 64 * x];
+        for (;;) {
+            const int32_t d = __builtin_amdgcn_readfirstlane(
+                __hip_atomic_load(done, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+            {
+                float c[kMaxLiveCopies][E];
+#pragma unroll
+                for (int r = 0; r < kMaxLiveCopies; ++r) {
+                    const int32_t row = (r < R ? (r == 0 ? m.x : m.y + r - 1) * (LD * 4) : kOutOfRange);
+#pragma unroll
+                    for (int x = 0; x < E; ++x)
+                        c[r][x] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rq, row + lane4 + 256 * x, 0, kSgdAux));
+                }
+                float nv[E];
+#pragma unroll
+                for (int x = 0; x < E; ++x) {
+                    float acc = last[x];
+#pragma unroll
+                    for (int r = 0; r < kMaxLiveCopies; ++r)
+                        if (r < R) acc += c[r][x] - last[x];
+                    nv[x] = acc;
+                }
+#pragma unroll
+                for (int r = 0; r < kMaxLiveCopies; ++r) {
+                    if (r < R) {
+                        const int32_t row = (r == 0 ? m.x : m.y + r - 1) * (LD * 4);
+#pragma unroll
+                        for (int x = 0; x < E; ++x)
+                            __builtin_amdgcn_raw_ptr_buffer_atomic_fadd_f32(nv[x] - c[r][x], rq, row + lane4 + 256 * x, 0, 0);
+                    }
+                }
+#pragma unroll
+                for (int x = 0; x < E; ++x) last[x] = nv[x];
+            }
+            if (d >= n_sgd_blocks) break;  // one last round after everyone finished
+        }
+#pragma unroll
+        for (int x = 0; x < E; ++x) qlast[static_cast<int64_t>(h) * LD + lane + 64 * x] = last[x];
+        return;
+    }
     if (blk >= n_heavy) {  // light blocks: four waves, each striding over the light work items
-        const int stride = (static_cast<int>(gridDim.x) - n_heavy) * 4;
+        const int stride = (n_sgd_blocks - n_heavy) * 4;
         for (int w = n_heavy + (blk - n_heavy) * 4 + wib; w < n_work; w += stride) {
             const int64_t t0 = trace ? static_cast<int64_t>(__builtin_amdgcn_s_memrealtime()) : 0;
             contrib += sgd_work_item<E, D>(
@@ -305,8 +369,10 @@ __global__ __launch_bounds__(256) void svd_epoch_hybrid_kernel(
         }
         if (lane == 0) s_contrib[wib] = contrib;
         __syncthreads();
-        if (threadIdx.x == 0)
+        if (threadIdx.x == 0) {
             gb_partial[blk] = ((s_contrib[0] + s_contrib[1]) + s_contrib[2]) + s_contrib[3];
+            if (MERGE) __hip_atomic_fetch_add(done, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
         return;
     }
     // heavy block (block-uniform branch): work item blk, wave 0 produces, waves 1..3 write
@@ -383,6 +449,7 @@ __global__ __launch_bounds__(256) void svd_epoch_hybrid_kernel(
     __syncthreads();
     if (threadIdx.x == 0) {
         gb_partial[blk] = contrib;
+        if (MERGE) __hip_atomic_fetch_add(done, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         if (trace) {
             trace[3 * blk] = t0;
             trace[3 * blk + 2] = static_cast<int64_t>(__builtin_amdgcn_s_memrealtime());
@@ -432,6 +499,26 @@ __global__ __launch_bounds__(64) void svd_item_merge_kernel(float* __restrict__ 
             v = Q[row(0) + col];
         }
         for (int32_t c = 0; c < m.z; ++c) Q[row(c) + col] = v;
+    }
+}
+
+// Live (hot-replica) items around an epoch, one wave per item: meta = {item row, first extra row,
+// copies R, unused}.  mode 0 (before): L = the item row (all copies are equal here).  mode 1 (after):
+// the merge round of the hybrid kernel's merger, N = L + sum_r (c_r - L), written to every copy.
+__global__ __launch_bounds__(64) void svd_live_merge_kernel(float* __restrict__ Q, const int4* __restrict__ meta,
+                                                           float* __restrict__ qlast, int32_t ld, int32_t mode) {
+    const int4 m = meta[blockIdx.x];
+    auto row = [&](int32_t c) { return static_cast<int64_t>(c == 0 ? m.x : m.y + c - 1) * ld; };
+    float* L = qlast + static_cast<int64_t>(blockIdx.x) * ld;
+    for (int32_t col = threadIdx.x; col < ld; col += 64) {
+        if (mode == 0) {
+            L[col] = Q[row(0) + col];
+        } else {
+            const float l = L[col];
+            float v = l;
+            for (int32_t c = 0; c < m.z; ++c) v += Q[row(c) + col] - l;
+            for (int32_t c = 0; c < m.z; ++c) Q[row(c) + col] = v;
+        }
     }
 }
 
@@ -659,6 +746,13 @@ struct rs_svd_plan {
     rs::DevBuf<float> P, Q;  // bias in column ld - 1
     rs::DevBuf<double> gb, partial;
     rs::DevBuf<float> uw;  // per-user share of this shard (multi-GPU delta mode)
+    // hot replicas: most-rated items and copies each (0: none).  Default 256 x 8, measured on the
+    // ML-1M shape (scripts/exp_replicas.py): epoch 760 -> 585 us, held-out RMSE unchanged
+    int32_t live_req = 256, live_copies = 8;
+    int32_t n_live = 0;
+    rs::DevBuf<int4> live_meta;  // {item row, first extra row, copies, -}
+    rs::DevBuf<float> qlast;     // last merged value of every live item (n_live x ld)
+    rs::DevBuf<int32_t> done;    // blocks finished (the merger's exit condition)
     rs::DevBuf<float> iw;  // per-item share of this shard (user-sharded multi-GPU mode)
     rs::DevBuf<float> Q0;  // Q at the epoch start (user-sharded mode)
     int32_t n_blocks = 0;
@@ -704,7 +798,7 @@ int32_t fast_blocks(const rs_svd_plan* pl) {
     if (pl->write_back == RS_SGD_WB_ATOMIC || pl->write_back == 101) {
         int32_t light = (pl->n_work - pl->n_heavy + 3) / 4;
         if (pl->light_blocks > 0) light = std::min(light, pl->light_blocks);
-        return std::max<int32_t>(1, pl->n_heavy + light);
+        return std::max<int32_t>(1, pl->n_heavy + light) + (pl->n_live + 3) / 4;  // + live mergers
     }
     return std::max<int32_t>(1, (pl->n_work + 3) / 4);
 }
@@ -718,11 +812,21 @@ static void launch_fast_t(rs_svd_plan* pl, float lr, float reg, hipStream_t s, f
     float* d = multi ? dP : (pl->n_split > 0 ? pl->dPs.p : nullptr);
     pl->n_blocks = fast_blocks(pl);
     if constexpr (WB == 2 || WB == 5) {
-        hipLaunchKernelGGL((svd_epoch_hybrid_kernel<E, D, WB == 5>), dim3(pl->n_blocks), dim3(256), 0, s,
-                           pl->wk_user.p, pl->wk_rng.p, pl->wk_frac.p, pl->n_work, pl->n_heavy,
-                           pl->items.p, pl->ratings.p, pl->P.p, pl->Q.p, q_bytes, pl->gb.p,
-                           pl->partial.p, lr, reg, d, multi ? pl->uw.p : nullptr, multi ? 0 : 1,
-                           pl->trace.n ? pl->trace.p : nullptr);
+        if (pl->n_live > 0) {
+            RS_HIP(hipMemsetAsync(pl->done.p, 0, sizeof(int32_t), s));
+            hipLaunchKernelGGL((svd_epoch_hybrid_kernel<E, D, WB == 5, true>), dim3(pl->n_blocks), dim3(256), 0, s,
+                               pl->wk_user.p, pl->wk_rng.p, pl->wk_frac.p, pl->n_work, pl->n_heavy,
+                               pl->items.p, pl->ratings.p, pl->P.p, pl->Q.p, q_bytes, pl->gb.p,
+                               pl->partial.p, lr, reg, d, multi ? pl->uw.p : nullptr, multi ? 0 : 1,
+                               pl->trace.n ? pl->trace.p : nullptr, pl->live_meta.p, pl->n_live, pl->qlast.p,
+                               pl->done.p);
+        } else {
+            hipLaunchKernelGGL((svd_epoch_hybrid_kernel<E, D, WB == 5, false>), dim3(pl->n_blocks), dim3(256), 0, s,
+                               pl->wk_user.p, pl->wk_rng.p, pl->wk_frac.p, pl->n_work, pl->n_heavy,
+                               pl->items.p, pl->ratings.p, pl->P.p, pl->Q.p, q_bytes, pl->gb.p,
+                               pl->partial.p, lr, reg, d, multi ? pl->uw.p : nullptr, multi ? 0 : 1,
+                               pl->trace.n ? pl->trace.p : nullptr, nullptr, 0, nullptr, nullptr);
+        }
     } else {
         hipLaunchKernelGGL((svd_epoch_fast_kernel<E, D, WB>), dim3(pl->n_blocks), dim3(256), 0, s,
                            pl->wk_user.p, pl->wk_rng.p, pl->wk_frac.p, pl->n_work, pl->items.p,
@@ -755,6 +859,9 @@ static void launch_fast_d(rs_svd_plan* pl, float lr, float reg, hipStream_t s, f
 }
 
 static void launch_fast(rs_svd_plan* pl, float lr, float reg, hipStream_t s, float* dP = nullptr) {
+    if (pl->n_live > 0)  // L = the live items' rows at the epoch start
+        hipLaunchKernelGGL(svd_live_merge_kernel, dim3(pl->n_live), dim3(64), 0, s, pl->Q.p, pl->live_meta.p,
+                           pl->qlast.p, pl->ld, 0);
     switch (pl->write_back) {
         case RS_SGD_WB_STORE: launch_fast_d<0>(pl, lr, reg, s, dP); break;          // write-through stores
         case RS_SGD_WB_ATOMIC_DIRECT: launch_fast_d<1>(pl, lr, reg, s, dP); break;  // per-wave atomics
@@ -763,6 +870,13 @@ static void launch_fast(rs_svd_plan* pl, float lr, float reg, hipStream_t s, flo
         default: launch_fast_d<2>(pl, lr, reg, s, dP); break;                       // hybrid
     }
     RS_HIP(hipGetLastError());
+}
+
+// After an epoch: the live items' final merge round (their copies leave the epoch equal).
+static void live_merge_after(rs_svd_plan* pl, hipStream_t s) {
+    if (pl->n_live > 0)
+        hipLaunchKernelGGL(svd_live_merge_kernel, dim3(pl->n_live), dim3(64), 0, s, pl->Q.p, pl->live_meta.p,
+                           pl->qlast.p, pl->ld, 1);
 }
 
 static void launch_ordered(int64_t nnz, const int32_t* u, const int32_t* i, const float* r,
@@ -793,6 +907,13 @@ static void sync_item_copies(rs_svd_plan* pl, hipStream_t s, int32_t mode) {
     if (pl->n_isplit > 0)
         hipLaunchKernelGGL(svd_item_merge_kernel, dim3(pl->n_isplit), dim3(64), 0, s, pl->Q.p,
                            pl->isplit_meta.p, pl->isplit_frac.p, pl->ld, mode);
+    if (pl->n_live > 0) {
+        if (mode == 0)
+            live_merge_after(pl, s);  // delta-sum round (live items are never averaged)
+        else
+            hipLaunchKernelGGL(svd_item_merge_kernel, dim3(pl->n_live), dim3(64), 0, s, pl->Q.p,
+                               pl->live_meta.p, pl->isplit_frac.p, pl->ld, 1);
+    }
 }
 
 static void build_items(rs_svd_plan* pl) {
@@ -802,11 +923,28 @@ static void build_items(rs_svd_plan* pl) {
     std::vector<int64_t> deg(std::max(1, ni), 0);
     for (int32_t c : cols) deg[c]++;
     std::vector<int32_t> R(std::max(1, ni), 1), first(std::max(1, ni), 0);
-    std::vector<int4> meta;
+    std::vector<int4> meta, live;
     std::vector<float> frac;
     int32_t extra = 0;
+    // hot replicas (live-merged copies): the live_req most-rated items with at least one rating per copy
+    std::vector<uint8_t> is_live(std::max(1, ni), 0);
+    if (pl->live_req > 0) {
+        std::vector<int32_t> order;
+        for (int32_t x = 0; x < ni; ++x)
+            if (deg[x] >= pl->live_copies) order.push_back(x);
+        const size_t nh = std::min(order.size(), static_cast<size_t>(pl->live_req));
+        std::partial_sort(order.begin(), order.begin() + nh, order.end(), [&](int32_t a, int32_t b) {
+            return deg[a] != deg[b] ? deg[a] > deg[b] : a < b;
+        });
+        for (size_t h = 0; h < nh; ++h) is_live[order[h]] = 1;
+    }
     for (int32_t x = 0; x < ni; ++x) {
-        if (pl->item_cap > 0 && deg[x] > pl->item_cap) {
+        if (is_live[x]) {
+            R[x] = pl->live_copies;
+            first[x] = ni + extra;
+            live.push_back(make_int4(x, ni + extra, R[x], 0));
+            extra += R[x] - 1;
+        } else if (pl->item_cap > 0 && deg[x] > pl->item_cap) {
             R[x] = static_cast<int32_t>((deg[x] + pl->item_cap - 1) / pl->item_cap);
             first[x] = ni + extra;
             meta.push_back(make_int4(x, ni + extra, R[x], static_cast<int32_t>(frac.size())));
@@ -830,6 +968,11 @@ static void build_items(rs_svd_plan* pl) {
     plan_sync_last(pl);
     pl->items.alloc(remap.size());
     pl->items.upload(remap.data(), remap.size(), s);
+    pl->n_live = static_cast<int32_t>(live.size());
+    pl->live_meta.alloc(std::max<size_t>(1, live.size()));
+    pl->live_meta.upload(live.data(), live.size(), s);
+    pl->qlast.alloc(static_cast<size_t>(std::max(1, pl->n_live)) * pl->ld);
+    if (!pl->done.p) pl->done.alloc(1);
     pl->n_isplit = static_cast<int32_t>(meta.size());
     pl->isplit_meta.alloc(std::max<size_t>(1, meta.size()));
     pl->isplit_frac.alloc(std::max<size_t>(1, frac.size()));
@@ -887,7 +1030,7 @@ static void build_work(rs_svd_plan* pl) {
     pl->wk_user.alloc(std::max<size_t>(1, wu.size()));
     pl->wk_rng.alloc(std::max<size_t>(2, wr.size()));
     pl->wk_frac.alloc(std::max<size_t>(1, wf.size()));
-    pl->partial.alloc(std::max<int32_t>(1, pl->n_work));  // >= blocks of any write-back mode
+    pl->partial.alloc(pl->n_work + 1 + (pl->n_live + 3) / 4);  // >= blocks of any mode (+ live mergers)
     pl->wk_user.upload(wu.data(), wu.size(), s);
     pl->wk_rng.upload(wr.data(), wr.size(), s);
     pl->wk_frac.upload(wf.data(), wf.size(), s);
@@ -1353,6 +1496,18 @@ extern "C" int rs_svd_plan_set_split(rs_svd_plan* pl, int32_t split_cap) {
             return rs::set_error(pl->ctx, RS_ERR_INVALID, "split_cap must be 0 (never) or >= 16");
         pl->split_cap = split_cap;
         rs::build_work(pl);
+        return RS_OK;
+    });
+}
+
+extern "C" int rs_svd_plan_set_hot_replicas(rs_svd_plan* pl, int32_t n_hot, int32_t copies) {
+    if (!pl) return rs::set_error(nullptr, RS_ERR_INVALID, "plan is NULL");
+    return rs_guard(pl->ctx, [&]() -> int {
+        if (n_hot < 0 || copies < 2 || copies > rs::kMaxLiveCopies)
+            return rs::set_error(pl->ctx, RS_ERR_INVALID, "n_hot must be >= 0 and copies in [2, 8]");
+        pl->live_req = n_hot;
+        pl->live_copies = copies;
+        rs::build_items(pl);
         return RS_OK;
     });
 }

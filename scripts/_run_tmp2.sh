@@ -2,7 +2,8 @@ set -u
 cd $GRAFT_REPO_ROOT
 mkdir -p gpurun_out
 export TMPDIR=/tmp
-timeout -k 10 600 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread > gpurun_out/pytest_gpu.log 2>&1 || { echo "tests failed"; grep -E "FAIL|Error|error" gpurun_out/pytest_gpu.log | head -30; tail -40 gpurun_out/pytest_gpu.log; exit 1; }
-tail -3 gpurun_out/pytest_gpu.log
-timeout -k 10 400 python -u scripts/bench_config5.py --epochs 3 --shard 0/8 --partition users --cpu-budget 0 > gpurun_out/c5_u8.json 2> gpurun_out/c5_u8.log || { echo "c5 users shard failed"; tail -20 gpurun_out/c5_u8.log; exit 3; }
-cat gpurun_out/c5_u8.json
+for T in 0 100 300 1000; do
+  echo "== merge ticks $T" >> gpurun_out/rep_sweep.log
+  RSGPU_MERGE_TICKS=$T CFGS="256x8,384x8,512x8,256x4" timeout -k 10 300 python -u scripts/exp_replicas.py >> gpurun_out/rep_sweep.log 2>&1 || exit 1
+done
+cat gpurun_out/rep_sweep.log

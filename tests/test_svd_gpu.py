@@ -400,3 +400,81 @@ def test_plan_predict_and_evaluate_on_device(ctx, ml100k):
     assert abs(e_rmse - rmse(host, f.te_r)) <= 1e-12 and abs(e_mae - float(np.mean(np.abs(host - f.te_r)))) <= 1e-12
     assert np.isnan(plan.evaluate([], [], [])[0])
     plan.close()
+
+
+def _hot_input(n_users=64, n_hot=6, copies=4, per_user=20, seed=31):
+    """Private items per user, plus n_hot items each rated by exactly `copies` distinct users: with
+    hot replicas every copy of a hot item holds exactly one rating (no two users share a row)."""
+    rng = np.random.default_rng(seed)
+    users, items = [], []
+    nxt = n_hot
+    for x in range(n_users):
+        d = int(rng.integers(1, per_user))
+        users += [x] * d
+        items += list(range(nxt, nxt + d))
+        nxt += d
+    for h in range(n_hot):
+        for x in rng.choice(n_users, copies, replace=False):
+            users.append(int(x))
+            items.append(h)
+    users, items = np.array(users), np.array(items)
+    perm = rng.permutation(len(users))
+    r = rng.integers(1, 6, len(users)).astype(float)
+    return users[perm], items[perm], r[perm], n_users, nxt
+
+
+@pytest.mark.parametrize("k", [20, 100])
+def test_hot_replicas_direct_mode_delta_sum(ctx, k):
+    """Hot replicas with per-wave atomics (no in-kernel merger): each copy of a hot item gets one
+    user's update from the epoch-start row, and the epoch-end round sums the copies' deltas.  Equal to
+    the restatement run on the copies as separate items, merged by delta sum on the host."""
+    copies, n_hot = 4, 6
+    u, i, r, nu, ni = _hot_input(n_hot=n_hot, copies=copies)
+    rng = np.random.default_rng(k)
+    P0, Q0 = rng.normal(0, 0.1, (nu, k)), rng.normal(0, 0.1, (ni, k))
+    plan = ctx.svd_plan(rsgpu.Ratings(u, i, r, nu, ni), k)
+    plan.set_mode(rsgpu.WB_ATOMIC_DIRECT, 8)
+    plan.set_hot_replicas(n_hot, copies)
+    plan.upload(P0, Q0, np.zeros(nu), np.zeros(ni), 3.0)
+    plan.epochs(1)
+    got = plan.download()
+    plan.close()
+    # host model: copy c of hot item h = the c-th of its ratings in user-CSR order
+    rowptr, items, rr = O.csr_by(u, nu, i, r)
+    users_csr = np.repeat(np.arange(nu), np.diff(rowptr))
+    items2 = items.copy()
+    extra = ni
+    for h in range(n_hot):
+        pos = np.nonzero(items == h)[0]          # in user-CSR order
+        for c, t in enumerate(pos):
+            if c > 0:
+                items2[t] = extra + (h * (copies - 1)) + c - 1
+    n2 = ni + n_hot * (copies - 1)
+    Q2 = np.concatenate([Q0, np.repeat(Q0[:n_hot], copies - 1, axis=0)])
+    ref = O.svd_fit_chunked(rowptr, items2, rr, P0, Q2, 1 << 30, gb=3.0, epochs=1, warm=False)
+    P, Q, bu, bi, gb = ref
+    for h in range(n_hot):
+        rows = [h] + [ni + h * (copies - 1) + c for c in range(copies - 1)]
+        Q[h] = Q0[h] + sum(Q[x] - Q0[h] for x in rows)
+        bi[h] = 0.0 + sum(bi[x] for x in rows)
+    assert _maxdiff((P, Q[:ni], bu, bi[:ni]), got[:4]) <= TOL and abs(gb - got[4]) <= TOL
+    assert users_csr is not None
+
+
+def test_hot_replicas_rmse_parity_ml100k(ctx, ml100k):
+    """Hot replicas with the live merger (hybrid default write-back): 5-fold ML-100K RMSE within 0.003
+    of the reference order (P2), as the plain FAST schedule."""
+    k = 100
+    ref_r, gpu_r = [], []
+    for f in folds(*ml100k):
+        rng = np.random.default_rng(7)
+        P0, Q0 = rng.normal(0, 0.1, (f.nu, k)), rng.normal(0, 0.1, (f.ni, k))
+        a = O.svd_fit(f.iu, f.ii, f.r, P0, Q0)
+        ref_r.append(rmse(O.svd_predict(f.tu, f.ti, *a), f.te_r))
+        plan = ctx.svd_plan(rsgpu.Ratings(f.iu, f.ii, f.r, f.nu, f.ni), k)
+        plan.set_hot_replicas(64, 4)
+        plan.upload(P0, Q0, np.zeros(f.nu), np.zeros(f.ni), float(np.mean(f.r)))
+        plan.epochs(20)
+        gpu_r.append(plan.evaluate(f.tu, f.ti, f.te_r)[0])
+        plan.close()
+    assert abs(np.mean(gpu_r) - np.mean(ref_r)) <= 0.003, (np.mean(gpu_r), np.mean(ref_r))
