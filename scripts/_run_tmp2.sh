@@ -2,8 +2,7 @@ set -u
 cd $GRAFT_REPO_ROOT
 mkdir -p gpurun_out
 export TMPDIR=/tmp
-for T in 0 100 300 1000; do
-  echo "== merge ticks $T" >> gpurun_out/rep_sweep.log
-  RSGPU_MERGE_TICKS=$T CFGS="256x8,384x8,512x8,256x4" timeout -k 10 300 python -u scripts/exp_replicas.py >> gpurun_out/rep_sweep.log 2>&1 || exit 1
-done
-cat gpurun_out/rep_sweep.log
+timeout -k 10 300 python -u -m pytest tests/test_nmf_gpu.py -m gpu -x -v --timeout 120 --timeout-method thread > gpurun_out/t_nmf.log 2>&1 || { echo "tests failed"; tail -40 gpurun_out/t_nmf.log; exit 1; }
+tail -3 gpurun_out/t_nmf.log
+timeout -k 10 300 python -u scripts/bench_configs.py --only nmf > gpurun_out/nmf.json 2> gpurun_out/nmf.err || { tail gpurun_out/nmf.err; exit 2; }
+cat gpurun_out/nmf.json
