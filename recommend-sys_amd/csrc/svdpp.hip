@@ -21,6 +21,7 @@
 
 #include <algorithm>
 #include <cmath>
+#include <cstdlib>
 #include <vector>
 
 #include "common.hpp"
@@ -57,7 +58,8 @@ __global__ __launch_bounds__(256) void svdpp_epoch_fast_kernel(
     __shared__ double s_contrib[4];
     const int lane = threadIdx.x & 63;
     const int wib = threadIdx.x >> 6;
-    const int w = __builtin_amdgcn_readfirstlane(static_cast<int>(blockIdx.x) * 4 + wib);
+    const int w0 = __builtin_amdgcn_readfirstlane(static_cast<int>(blockIdx.x) * 4 + wib);
+    const int stride = static_cast<int>(gridDim.x) * 4;  // waves stride over the LPT-ordered users
     const float gb0 = static_cast<float>(gb_in[0]);
     const __amdgpu_buffer_rsrc_t rq = __builtin_amdgcn_make_buffer_rsrc(Q, 0, row_bytes_q, 0x00020000);
     const __amdgpu_buffer_rsrc_t ry = __builtin_amdgcn_make_buffer_rsrc(Y, 0, row_bytes_y, 0x00020000);
@@ -66,7 +68,7 @@ __global__ __launch_bounds__(256) void svdpp_epoch_fast_kernel(
     const float a = 1.f - lr * reg;
     double contrib = 0.0;
 
-    if (w < n_work) {
+    for (int w = w0; w < n_work; w += stride) {
         const int32_t u = work[w];
         const int64_t b = rowptr[u], e = rowptr[u + 1];
         const int32_t deg = static_cast<int32_t>(e - b);
@@ -180,7 +182,7 @@ __global__ __launch_bounds__(256) void svdpp_epoch_fast_kernel(
         }
 #pragma unroll
         for (int x = 0; x < E; ++x) prow[lane + 64 * x] = p[x];
-        contrib = static_cast<double>(deg) * (static_cast<double>(gb) - static_cast<double>(gb0));
+        contrib += static_cast<double>(deg) * (static_cast<double>(gb) - static_cast<double>(gb0));
     }
     if (lane == 0) s_contrib[wib] = contrib;
     __syncthreads();
@@ -393,7 +395,15 @@ extern "C" int rs_svdpp_fit(rs_ctx* ctx, const rs_ratings* r, const rs_sgd_param
         if (static_cast<int64_t>(std::max(1, r->n_items)) * ld * 4 >= (int64_t{1} << 31) - 64)
             return rs::set_error(ctx, RS_ERR_UNSUPPORTED, "n_items * n_factors too large");
         const int32_t n_work = static_cast<int32_t>(order.size());
-        const int32_t n_blocks = std::max<int32_t>(1, (n_work + 3) / 4);
+        // blocks of four waves striding over the LPT-ordered users: at most 1.5 blocks per CU (the
+        // K1 measurement: fewer waves keep the memory-side atomic queues, which every q_i / y_j load
+        // waits behind, short); RSGPU_PP_BLOCKS overrides (experiments)
+        int cus = 256;
+        if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, ctx->device) != hipSuccess || cus <= 0)
+            cus = 256;
+        int32_t cap = (3 * cus) / 2;
+        if (const char* env = std::getenv("RSGPU_PP_BLOCKS")) cap = std::max(1, std::atoi(env));
+        const int32_t n_blocks = std::max<int32_t>(1, std::min<int32_t>((n_work + 3) / 4, cap));
         rs::DevBuf<int32_t> dwork(std::max<size_t>(1, order.size()));
         dwork.upload(order.data(), order.size(), s);
         std::vector<float> hP, hQ, hY;
