@@ -47,150 +47,320 @@ __device__ __forceinline__ float pp_lane63(float x) {
 // ---------------------------------------------------------------------------------------------
 // FAST (lazy y) epoch kernel
 
+// Pass 1 of one user over the y rows j = b + first, b + first + step, ... (batches of YB rows):
+// the sum of the y_j (svd.go:276-278) in that order.
+template <int E, int YB>
+__device__ __forceinline__ void pp_sum_y(__amdgpu_buffer_rsrc_t ry, const int32_t* __restrict__ items,
+                                         int64_t b, int64_t e, int32_t first, int32_t step, int32_t lane4,
+                                         float (&S0)[E]) {
+    constexpr int LD = 64 * E;
+#pragma unroll
+    for (int x = 0; x < E; ++x) S0[x] = 0.f;
+    for (int64_t base = b + first; base < e; base += step) {
+        const int32_t rem = static_cast<int32_t>(e - base);
+        float yv[YB][E];
+#pragma unroll
+        for (int j = 0; j < YB; ++j) {
+            const int32_t row = j < rem ? items[base + j] * (LD * 4) : kPPOut;
+#pragma unroll
+            for (int x = 0; x < E; ++x)
+                yv[j][x] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(ry, row + lane4 + 256 * x, 0, kPPAux));
+        }
+#pragma unroll
+        for (int j = 0; j < YB; ++j)
+#pragma unroll
+            for (int x = 0; x < E; ++x) S0[x] += yv[j][x];
+    }
+}
+
+// Pass 3 over the same row subset: y_j += (A - 1) y_j - C (the deferred svd.go:399-422), atomics.
+template <int E, int YB>
+__device__ __forceinline__ void pp_update_y(__amdgpu_buffer_rsrc_t ry, const int32_t* __restrict__ items,
+                                            int64_t b, int64_t e, int32_t first, int32_t step,
+                                            int32_t lane4, float am1, const float (&Cv)[E]) {
+    constexpr int LD = 64 * E;
+    for (int64_t base = b + first; base < e; base += step) {
+        const int32_t rem = static_cast<int32_t>(e - base);
+        float yv[YB][E];
+        int32_t rows[YB];
+#pragma unroll
+        for (int j = 0; j < YB; ++j) {
+            rows[j] = j < rem ? items[base + j] * (LD * 4) : kPPOut;
+#pragma unroll
+            for (int x = 0; x < E; ++x)
+                yv[j][x] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(ry, rows[j] + lane4 + 256 * x, 0, kPPAux));
+        }
+#pragma unroll
+        for (int j = 0; j < YB; ++j)
+#pragma unroll
+            for (int x = 0; x < E; ++x)
+                __builtin_amdgcn_raw_ptr_buffer_atomic_fadd_f32(__builtin_fmaf(am1, yv[j][x], -Cv[x]), ry,
+                                                               rows[j] + lane4 + 256 * x, 0, 0);
+    }
+}
+
+// Pass 2 of one user: the ratings in data order with the lazy y state (S0, A, Cv).  Every q_i update
+// is handed to emit(row byte offset, q_new, q_old).  Returns with p (bias in lane 63), ub, gb, A, Cv
+// advanced.
+template <int E, int D, class Emit>
+__device__ __forceinline__ void pp_chain(__amdgpu_buffer_rsrc_t rq, const int32_t* __restrict__ items,
+                                         const float* __restrict__ ratings, int64_t b, int64_t e,
+                                         int32_t lane, float lr, float a, const float (&S0)[E], float (&p)[E],
+                                         float& ub, float& gb, float& A, float (&Cv)[E], Emit&& emit) {
+#pragma clang fp contract(fast)
+    constexpr int LD = 64 * E, B = 16;
+    static_assert(B % D == 0, "ring depth must divide the 16-rating batch");
+    const int32_t lane4 = lane * 4;
+    const bool bias_lane = lane == 63;
+    const int32_t deg = static_cast<int32_t>(e - b);
+    const float nf = static_cast<float>(deg);
+    const float rsq = 1.f / sqrtf(nf);  // the chain multiplies by 1/sqrt|N(u)| (no divide per rating)
+    auto load_rowq = [&](float (&q)[E], int32_t valid, int32_t item) {
+        const int32_t row = valid ? item * (LD * 4) : kPPOut;
+#pragma unroll
+        for (int x = 0; x < E; ++x)
+            q[x] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rq, row + lane4 + 256 * x, 0, kPPAux));
+    };
+    int32_t it_cur[B], it_nxt[B];
+#pragma unroll
+    for (int j = 0; j < B; ++j) it_cur[j] = items[b + j];
+#pragma unroll
+    for (int j = 0; j < B; ++j) it_nxt[j] = items[b + B + j];
+    float ring[D][E];
+#pragma unroll
+    for (int s = 0; s < D; ++s) load_rowq(ring[s], s < deg, it_cur[s]);
+    for (int64_t base = b; base < e; base += B) {
+        const int32_t rem = static_cast<int32_t>(e - base);
+        float rt[B];
+#pragma unroll
+        for (int j = 0; j < B; ++j) rt[j] = ratings[base + j];
+#pragma unroll
+        for (int j = 0; j < B; ++j) {
+            constexpr int kD = D;
+            const int slot = j % kD;
+            if (j < rem) {
+                float (&q)[E] = ring[slot];
+                const float bq = pp_lane63(q[E - 1]);
+                float ev[E];
+                float s = 0.f;
+#pragma unroll
+                for (int x = 0; x < E; ++x) {
+                    ev[x] = (A * S0[x] - nf * Cv[x]) * rsq;           // svd.go:271-282
+                    const float qx = (x == E - 1 && bias_lane) ? 0.f : q[x];
+                    s += (p[x] + ev[x]) * qx;                         // svd.go:302-305
+                }
+                s = pp_wave_sum(s);
+                const float diff = ((gb + ub) + bq) + s - rt[j];      // svd.go:363-364
+                const float c = lr * diff;
+                gb -= c;                                              // svd.go:366-367
+                ub = __builtin_fmaf(ub, a, -c);                       // svd.go:370-371
+                const float bq_new = __builtin_fmaf(bq, a, -c);       // svd.go:374-375
+                const float cy = c * rsq;                             // svd.go:410-412
+                A *= a;                                               // svd.go:413-417 (lazy)
+                float qw[E];
+#pragma unroll
+                for (int x = 0; x < E; ++x) {
+                    const float pn = __builtin_fmaf(-c, q[x], p[x] * a);           // 378-384
+                    const float qn = __builtin_fmaf(-c, pn + ev[x], q[x] * a);     // 387-396
+                    const bool bx = x == E - 1 && bias_lane;
+                    p[x] = bx ? ub : pn;
+                    qw[x] = bx ? bq_new : qn;
+                    Cv[x] = bx ? 0.f : __builtin_fmaf(cy, qn, Cv[x] * a);
+                }
+                emit(it_cur[j] * (LD * 4), qw, q);
+            }
+            const int jn = j + D;
+            load_rowq(ring[slot], jn < rem, jn < B ? it_cur[jn % B] : it_nxt[jn % B]);
+        }
+#pragma unroll
+        for (int j = 0; j < B; ++j) it_cur[j] = it_nxt[j];
+#pragma unroll
+        for (int j = 0; j < B; ++j) it_nxt[j] = items[base + 2 * B + j];
+    }
+}
+
+// FAST epoch.  Blocks [0, n_heavy) take one heavy user each (the first, heaviest work items):
+// pass 1 and pass 3 split over the block's four waves (rows j = 4 t YB + w YB ...), pass 2 on wave
+// 0 with its q_i deltas written to an LDS ring that waves 1..3 drain into the float atomics (the
+// K1 hybrid scheme: the chain's vmcnt then holds only its own loads).  The other blocks' waves
+// stride over the light users, each wave running all three passes itself with direct atomics.
+template <int E>
+struct PPRing {
+    static constexpr int kRing = E <= 2 ? 32 : (E <= 4 ? 16 : 8);
+    static constexpr int kBatch = E <= 2 ? 8 : (E <= 4 ? 4 : 2);
+};
+
+__device__ __forceinline__ int32_t pp_lds_load(const int32_t* p) {
+    return __builtin_amdgcn_readfirstlane(__hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP));
+}
+__device__ __forceinline__ void pp_lds_store(int32_t* p, int32_t v) {
+    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+
 template <int E, int D>
 __global__ __launch_bounds__(256) void svdpp_epoch_fast_kernel(
-    const int32_t* __restrict__ work, int32_t n_work, const int64_t* __restrict__ rowptr,
+    const int32_t* __restrict__ work, int32_t n_work, int32_t n_heavy, const int64_t* __restrict__ rowptr,
     const int32_t* __restrict__ items, const float* __restrict__ ratings, float* __restrict__ P,
     float* Q, float* Y, int32_t row_bytes_q, int32_t row_bytes_y, const double* __restrict__ gb_in,
     double* __restrict__ gb_partial, float lr, float reg) {
 #pragma clang fp contract(fast)
-    constexpr int LD = 64 * E, B = 16;
+    constexpr int LD = 64 * E;
     constexpr int YB = 8;  // y rows per pass-1/3 batch (24 was measured to break the FAST RMSE on ML-100K)
+    constexpr int R = PPRing<E>::kRing, NB = PPRing<E>::kBatch, NW = 3;
+    constexpr int DH = E <= 3 ? 16 : 8;  // heavy producer: its vmcnt holds only q loads
     __shared__ double s_contrib[4];
+    __shared__ float s_red[4][LD];
+    __shared__ float s_q[R][LD];
+    __shared__ int32_t s_row[R];
+    __shared__ int32_t s_tail, s_done, s_head[NW];
+    __shared__ float s_A;
     const int lane = threadIdx.x & 63;
-    const int wib = threadIdx.x >> 6;
-    const int w0 = __builtin_amdgcn_readfirstlane(static_cast<int>(blockIdx.x) * 4 + wib);
-    const int stride = static_cast<int>(gridDim.x) * 4;  // waves stride over the LPT-ordered users
+    const int wib = __builtin_amdgcn_readfirstlane(static_cast<int>(threadIdx.x) >> 6);
     const float gb0 = static_cast<float>(gb_in[0]);
     const __amdgpu_buffer_rsrc_t rq = __builtin_amdgcn_make_buffer_rsrc(Q, 0, row_bytes_q, 0x00020000);
     const __amdgpu_buffer_rsrc_t ry = __builtin_amdgcn_make_buffer_rsrc(Y, 0, row_bytes_y, 0x00020000);
     const int32_t lane4 = lane * 4;
-    const bool bias_lane = lane == 63;
     const float a = 1.f - lr * reg;
+    const int blk = static_cast<int>(blockIdx.x);
     double contrib = 0.0;
 
-    for (int w = w0; w < n_work; w += stride) {
-        const int32_t u = work[w];
-        const int64_t b = rowptr[u], e = rowptr[u + 1];
-        const int32_t deg = static_cast<int32_t>(e - b);
-        const float nf = static_cast<float>(deg);
-        const float sq = sqrtf(nf);
-        const float rsq = 1.f / sq;  // the chain multiplies by 1/sqrt|N(u)| (no divide per rating)
-        float p[E];
+    if (blk >= n_heavy) {  // light blocks
+        const int stride = (static_cast<int>(gridDim.x) - n_heavy) * 4;
+        for (int w = n_heavy + (blk - n_heavy) * 4 + wib; w < n_work; w += stride) {
+            const int32_t u = work[w];
+            const int64_t b = rowptr[u], e = rowptr[u + 1];
+            float p[E];
+            float* prow = P + static_cast<int64_t>(u) * LD;
+#pragma unroll
+            for (int x = 0; x < E; ++x) p[x] = prow[lane + 64 * x];
+            float ub = pp_lane63(p[E - 1]);
+            float gb = gb0, A = 1.f;
+            float S0[E], Cv[E];
+            pp_sum_y<E, YB>(ry, items, b, e, 0, YB, lane4, S0);
+#pragma unroll
+            for (int x = 0; x < E; ++x) Cv[x] = 0.f;
+            pp_chain<E, 8>(rq, items, ratings, b, e, lane, lr, a, S0, p, ub, gb, A, Cv,
+                           [&](int32_t row, const float (&qw)[E], const float (&q)[E]) {
+#pragma unroll
+                               for (int x = 0; x < E; ++x)
+                                   __builtin_amdgcn_raw_ptr_buffer_atomic_fadd_f32(qw[x] - q[x], rq, row + lane4 + 256 * x, 0, 0);
+                           });
+            pp_update_y<E, YB>(ry, items, b, e, 0, YB, lane4, A - 1.f, Cv);
+#pragma unroll
+            for (int x = 0; x < E; ++x) prow[lane + 64 * x] = p[x];
+            contrib += static_cast<double>(e - b) * (static_cast<double>(gb) - static_cast<double>(gb0));
+        }
+        if (lane == 0) s_contrib[wib] = contrib;
+        __syncthreads();
+        if (threadIdx.x == 0)
+            gb_partial[blk] = ((s_contrib[0] + s_contrib[1]) + s_contrib[2]) + s_contrib[3];
+        return;
+    }
+
+    // heavy block (block-uniform branch): user work[blk]
+    const int32_t u = work[blk];
+    const int64_t b = rowptr[u], e = rowptr[u + 1];
+    if (threadIdx.x == 0) {
+        s_tail = 0;
+        s_done = 0;
+    }
+    if (threadIdx.x < NW) s_head[threadIdx.x] = static_cast<int32_t>(threadIdx.x);
+    // pass 1 split over the four waves, the partial sums added in wave order (identical everywhere)
+    {
+        float S0w[E];
+        pp_sum_y<E, YB>(ry, items, b, e, wib * YB, 4 * YB, lane4, S0w);
+#pragma unroll
+        for (int x = 0; x < E; ++x) s_red[wib][lane + 64 * x] = S0w[x];
+    }
+    __syncthreads();
+    float Cv[E];
+#pragma unroll
+    for (int x = 0; x < E; ++x) Cv[x] = 0.f;
+    if (wib == 0) {
+        float S0[E], p[E];
+#pragma unroll
+        for (int x = 0; x < E; ++x)
+            S0[x] = ((s_red[0][lane + 64 * x] + s_red[1][lane + 64 * x]) + s_red[2][lane + 64 * x]) +
+                    s_red[3][lane + 64 * x];
         float* prow = P + static_cast<int64_t>(u) * LD;
 #pragma unroll
         for (int x = 0; x < E; ++x) p[x] = prow[lane + 64 * x];
         float ub = pp_lane63(p[E - 1]);
-        float gb = gb0;
-        auto load_rowq = [&](__amdgpu_buffer_rsrc_t rs_, float (&q)[E], int32_t valid, int32_t item) {
-            const int32_t row = valid ? item * (LD * 4) : kPPOut;
+        float gb = gb0, A = 1.f;
+        int32_t tail = 0, free_end = R;
+        pp_chain<E, DH>(rq, items, ratings, b, e, lane, lr, a, S0, p, ub, gb, A, Cv,
+                        [&](int32_t row, const float (&qw)[E], const float (&q)[E]) {
+                            if (tail >= free_end) {  // ring full: wait for the writers
+                                for (;;) {
+                                    const int32_t h = min(min(pp_lds_load(&s_head[0]), pp_lds_load(&s_head[1])),
+                                                          pp_lds_load(&s_head[2]));
+                                    free_end = h + R;
+                                    if (tail < free_end) break;
+                                    __builtin_amdgcn_s_sleep(1);
+                                }
+                            }
+                            const int slot = tail & (R - 1);
 #pragma unroll
-            for (int x = 0; x < E; ++x)
-                q[x] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rs_, row + lane4 + 256 * x, 0, kPPAux));
-        };
-
-        // pass 1: S0 = sum_{j in N(u)} y_j   (svd.go:276-278)
-        float S0[E];
+                            for (int x = 0; x < E; ++x) s_q[slot][lane + 64 * x] = qw[x] - q[x];
+                            if (lane == 0) s_row[slot] = row;
+                            __atomic_signal_fence(__ATOMIC_SEQ_CST);  // entry before tail, in issue order
+                            ++tail;
+                            if (lane == 0) pp_lds_store(&s_tail, tail);
+                        });
 #pragma unroll
-        for (int x = 0; x < E; ++x) S0[x] = 0.f;
-        // YB rows in flight per batch (the batch is latency-bound: fewer, fuller batches)
-        for (int64_t base = b; base < e; base += YB) {
-            const int32_t rem = static_cast<int32_t>(e - base);
-            float yv[YB][E];
-#pragma unroll
-            for (int j = 0; j < YB; ++j) load_rowq(ry, yv[j], j < rem, items[base + j]);
-#pragma unroll
-            for (int j = 0; j < YB; ++j)
-#pragma unroll
-                for (int x = 0; x < E; ++x) S0[x] += yv[j][x];
+        for (int x = 0; x < E; ++x) {
+            prow[lane + 64 * x] = p[x];
+            s_red[0][lane + 64 * x] = Cv[x];  // pass 3 reads C and A from LDS
         }
-        float A = 1.f;
-        float Cv[E];
+        if (lane == 0) s_A = A;
+        contrib = static_cast<double>(e - b) * (static_cast<double>(gb) - static_cast<double>(gb0));
+        __atomic_signal_fence(__ATOMIC_SEQ_CST);
+        if (lane == 0) pp_lds_store(&s_done, 1);
+    } else {
+        const int wr = wib - 1;
+        int32_t next = wr;
+        for (;;) {
+            const int32_t done = pp_lds_load(&s_done);
+            __atomic_signal_fence(__ATOMIC_SEQ_CST);
+            const int32_t tail = pp_lds_load(&s_tail);
+            __atomic_signal_fence(__ATOMIC_SEQ_CST);
+            if (next < tail) {
+                while (next < tail) {
+                    const int32_t n = min((tail - next + NW - 1) / NW, NB);
+                    const int32_t myrow = s_row[(next + NW * (lane & (NB - 1))) & (R - 1)];
+                    float v[NB][E];
 #pragma unroll
-        for (int x = 0; x < E; ++x) Cv[x] = 0.f;
-
-        // pass 2: the ratings of u in data order
-        int32_t it_cur[B], it_nxt[B];
+                    for (int j = 0; j < NB; ++j)
 #pragma unroll
-        for (int j = 0; j < B; ++j) it_cur[j] = items[b + j];
+                        for (int x = 0; x < E; ++x) v[j][x] = s_q[(next + NW * j) & (R - 1)][lane + 64 * x];
 #pragma unroll
-        for (int j = 0; j < B; ++j) it_nxt[j] = items[b + B + j];
-        float ring[D][E];
+                    for (int j = 0; j < NB; ++j) {
+                        if (j < n) {
+                            const int32_t row = __builtin_amdgcn_readlane(myrow, j);
 #pragma unroll
-        for (int s = 0; s < D; ++s) load_rowq(rq, ring[s], s < deg, it_cur[s]);
-        for (int64_t base = b; base < e; base += B) {
-            const int32_t rem = static_cast<int32_t>(e - base);
-            float rt[B];
-#pragma unroll
-            for (int j = 0; j < B; ++j) rt[j] = ratings[base + j];
-#pragma unroll
-            for (int j = 0; j < B; ++j) {
-                constexpr int kD = D;
-                const int slot = j % kD;
-                if (j < rem) {
-                    float* q = ring[slot];
-                    const float bq = pp_lane63(q[E - 1]);
-                    float ev[E];
-                    float s = 0.f;
-#pragma unroll
-                    for (int x = 0; x < E; ++x) {
-                        ev[x] = (A * S0[x] - nf * Cv[x]) * rsq;           // svd.go:271-282
-                        const float qx = (x == E - 1 && bias_lane) ? 0.f : q[x];
-                        s += (p[x] + ev[x]) * qx;                         // svd.go:302-305
+                            for (int x = 0; x < E; ++x)
+                                __builtin_amdgcn_raw_ptr_buffer_atomic_fadd_f32(v[j][x], rq, row + lane4 + 256 * x, 0, 0);
+                        }
                     }
-                    s = pp_wave_sum(s);
-                    const float diff = ((gb + ub) + bq) + s - rt[j];      // svd.go:363-364
-                    const float c = lr * diff;
-                    gb -= c;                                              // svd.go:366-367
-                    ub = __builtin_fmaf(ub, a, -c);                       // svd.go:370-371
-                    const float bq_new = __builtin_fmaf(bq, a, -c);       // svd.go:374-375
-                    const float cy = c * rsq;                             // svd.go:410-412
-                    A *= a;                                               // svd.go:413-417 (lazy)
-#pragma unroll
-                    for (int x = 0; x < E; ++x) {
-                        const float pn = __builtin_fmaf(-c, q[x], p[x] * a);           // 378-384
-                        const float qn = __builtin_fmaf(-c, pn + ev[x], q[x] * a);     // 387-396
-                        const bool bx = x == E - 1 && bias_lane;
-                        p[x] = bx ? ub : pn;
-                        const float qw = bx ? bq_new : qn;
-                        Cv[x] = bx ? 0.f : __builtin_fmaf(cy, qn, Cv[x] * a);
-                        __builtin_amdgcn_raw_ptr_buffer_atomic_fadd_f32(
-                            qw - q[x], rq, it_cur[j] * (LD * 4) + lane4 + 256 * x, 0, 0);
-                    }
+                    next += NW * n;
                 }
-                const int jn = j + D;
-                load_rowq(rq, ring[slot], jn < rem, jn < B ? it_cur[jn % B] : it_nxt[jn % B]);
-            }
-#pragma unroll
-            for (int j = 0; j < B; ++j) it_cur[j] = it_nxt[j];
-#pragma unroll
-            for (int j = 0; j < B; ++j) it_nxt[j] = items[base + 2 * B + j];
-        }
-
-        // pass 3: y_j += (A - 1) y_j - C for every j in N(u) (the deferred svd.go:399-422)
-        const float am1 = A - 1.f;
-        for (int64_t base = b; base < e; base += YB) {
-            const int32_t rem = static_cast<int32_t>(e - base);
-            float yv[YB][E];
-#pragma unroll
-            for (int j = 0; j < YB; ++j) load_rowq(ry, yv[j], j < rem, items[base + j]);
-#pragma unroll
-            for (int j = 0; j < YB; ++j) {
-                const int32_t row = j < rem ? items[base + j] * (LD * 4) : kPPOut;
-#pragma unroll
-                for (int x = 0; x < E; ++x)
-                    __builtin_amdgcn_raw_ptr_buffer_atomic_fadd_f32(__builtin_fmaf(am1, yv[j][x], -Cv[x]), ry,
-                                                                   row + lane4 + 256 * x, 0, 0);
+                __atomic_signal_fence(__ATOMIC_SEQ_CST);
+                if (lane == 0) pp_lds_store(&s_head[wr], next);
+            } else if (done) {
+                break;
+            } else {
+                __builtin_amdgcn_s_sleep(1);
             }
         }
-#pragma unroll
-        for (int x = 0; x < E; ++x) prow[lane + 64 * x] = p[x];
-        contrib += static_cast<double>(deg) * (static_cast<double>(gb) - static_cast<double>(gb0));
     }
-    if (lane == 0) s_contrib[wib] = contrib;
-    __syncthreads();
-    if (threadIdx.x == 0)
-        gb_partial[blockIdx.x] = ((s_contrib[0] + s_contrib[1]) + s_contrib[2]) + s_contrib[3];
+    __syncthreads();  // A and C in LDS; every q delta issued
+    {
+        float C[E];
+#pragma unroll
+        for (int x = 0; x < E; ++x) C[x] = s_red[0][lane + 64 * x];
+        pp_update_y<E, YB>(ry, items, b, e, wib * YB, 4 * YB, lane4, s_A - 1.f, C);
+    }
+    if (threadIdx.x == 0) gb_partial[blk] = contrib;
 }
 
 __global__ __launch_bounds__(256) void pp_gb_fold_kernel(const double* __restrict__ partial,
@@ -299,13 +469,13 @@ static void unpack_bias_rows(const std::vector<float>& src, int64_t rows, int32_
 }
 
 template <int E>
-static void launch_pp_fast(int32_t n_blocks, const DevBuf<int32_t>& work, int32_t n_work,
+static void launch_pp_fast(int32_t n_blocks, const DevBuf<int32_t>& work, int32_t n_work, int32_t n_heavy,
                            const DevBuf<int64_t>& rowptr, const DevBuf<int32_t>& items,
                            const DevBuf<float>& ratings, DevBuf<float>& P, DevBuf<float>& Q,
                            DevBuf<float>& Y, DevBuf<double>& gb, DevBuf<double>& partial, float lr,
                            float reg, hipStream_t s) {
     hipLaunchKernelGGL((svdpp_epoch_fast_kernel<E, 8>), dim3(n_blocks), dim3(256), 0, s, work.p,
-                       n_work, rowptr.p, items.p, ratings.p, P.p, Q.p, Y.p,
+                       n_work, n_heavy, rowptr.p, items.p, ratings.p, P.p, Q.p, Y.p,
                        static_cast<int32_t>(Q.n * 4), static_cast<int32_t>(Y.n * 4), gb.p,
                        partial.p, lr, reg);
 }
@@ -406,7 +576,15 @@ extern "C" int rs_svdpp_fit(rs_ctx* ctx, const rs_ratings* r, const rs_sgd_param
             cus = 256;
         int32_t cap = (3 * cus) / 2;
         if (const char* env = std::getenv("RSGPU_PP_BLOCKS")) cap = std::max(1, std::atoi(env));
-        const int32_t n_blocks = std::max<int32_t>(1, std::min<int32_t>((n_work + 3) / 4, cap));
+        // users with >= 1024 ratings (LPT order: the first n_heavy work items) get a block each
+        int32_t n_heavy = 0;
+        int32_t heavy_min = 1024;
+        if (const char* env = std::getenv("RSGPU_PP_HEAVY")) heavy_min = std::atoi(env);
+        while (heavy_min > 0 && n_heavy < n_work &&
+               csr.rowptr[order[n_heavy] + 1] - csr.rowptr[order[n_heavy]] >= heavy_min)
+            ++n_heavy;
+        const int32_t n_blocks =
+            n_heavy + std::max<int32_t>(1, std::min<int32_t>((n_work - n_heavy + 3) / 4, cap));
         rs::DevBuf<int32_t> dwork(std::max<size_t>(1, order.size()));
         dwork.upload(order.data(), order.size(), s);
         std::vector<float> hP, hQ, hY;
@@ -424,14 +602,14 @@ extern "C" int rs_svdpp_fit(rs_ctx* ctx, const rs_ratings* r, const rs_sgd_param
         rs::kernel_span_begin(ctx);
         for (int32_t ep = 0; ep < p->n_epochs; ++ep) {
             switch (E) {
-                case 1: rs::launch_pp_fast<1>(n_blocks, dwork, n_work, drow, dcol, dval, dP, dQ, dY, dgb, dpart, lr, reg, s); break;
-                case 2: rs::launch_pp_fast<2>(n_blocks, dwork, n_work, drow, dcol, dval, dP, dQ, dY, dgb, dpart, lr, reg, s); break;
-                case 3: rs::launch_pp_fast<3>(n_blocks, dwork, n_work, drow, dcol, dval, dP, dQ, dY, dgb, dpart, lr, reg, s); break;
-                case 4: rs::launch_pp_fast<4>(n_blocks, dwork, n_work, drow, dcol, dval, dP, dQ, dY, dgb, dpart, lr, reg, s); break;
-                case 5: rs::launch_pp_fast<5>(n_blocks, dwork, n_work, drow, dcol, dval, dP, dQ, dY, dgb, dpart, lr, reg, s); break;
-                case 6: rs::launch_pp_fast<6>(n_blocks, dwork, n_work, drow, dcol, dval, dP, dQ, dY, dgb, dpart, lr, reg, s); break;
-                case 7: rs::launch_pp_fast<7>(n_blocks, dwork, n_work, drow, dcol, dval, dP, dQ, dY, dgb, dpart, lr, reg, s); break;
-                default: rs::launch_pp_fast<8>(n_blocks, dwork, n_work, drow, dcol, dval, dP, dQ, dY, dgb, dpart, lr, reg, s); break;
+                case 1: rs::launch_pp_fast<1>(n_blocks, dwork, n_work, n_heavy, drow, dcol, dval, dP, dQ, dY, dgb, dpart, lr, reg, s); break;
+                case 2: rs::launch_pp_fast<2>(n_blocks, dwork, n_work, n_heavy, drow, dcol, dval, dP, dQ, dY, dgb, dpart, lr, reg, s); break;
+                case 3: rs::launch_pp_fast<3>(n_blocks, dwork, n_work, n_heavy, drow, dcol, dval, dP, dQ, dY, dgb, dpart, lr, reg, s); break;
+                case 4: rs::launch_pp_fast<4>(n_blocks, dwork, n_work, n_heavy, drow, dcol, dval, dP, dQ, dY, dgb, dpart, lr, reg, s); break;
+                case 5: rs::launch_pp_fast<5>(n_blocks, dwork, n_work, n_heavy, drow, dcol, dval, dP, dQ, dY, dgb, dpart, lr, reg, s); break;
+                case 6: rs::launch_pp_fast<6>(n_blocks, dwork, n_work, n_heavy, drow, dcol, dval, dP, dQ, dY, dgb, dpart, lr, reg, s); break;
+                case 7: rs::launch_pp_fast<7>(n_blocks, dwork, n_work, n_heavy, drow, dcol, dval, dP, dQ, dY, dgb, dpart, lr, reg, s); break;
+                default: rs::launch_pp_fast<8>(n_blocks, dwork, n_work, n_heavy, drow, dcol, dval, dP, dQ, dY, dgb, dpart, lr, reg, s); break;
             }
             RS_HIP(hipGetLastError());
             hipLaunchKernelGGL(rs::pp_gb_fold_kernel, dim3(1), dim3(256), 0, s, dpart.p,

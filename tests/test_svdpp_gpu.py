@@ -59,6 +59,29 @@ def test_svdpp_fast_lazy_matches_literal_race_free(ctx, k):
         assert abs(ref[5] - got[5]) <= TOL
 
 
+@pytest.mark.parametrize("heavy,k", [(16, 20), (40, 128), (1, 300)])
+def test_svdpp_fast_heavy_blocks_race_free(ctx, monkeypatch, heavy, k):
+    """Heavy-user blocks (pass 1/3 split over four waves, pass 2 on a producer wave whose q deltas
+    go through the LDS ring to three writer waves): forced onto every user with >= `heavy` ratings
+    (RSGPU_PP_HEAVY), the epoch must still equal the restatement on race-free input -- long rows
+    wrap the ring many times."""
+    rng = np.random.default_rng(heavy)
+    deg = rng.integers(1, 300, 40)
+    users = np.repeat(np.arange(40), deg)
+    items = np.arange(len(users))
+    perm = rng.permutation(len(users))
+    u, i, nu, ni = users[perm], items[perm], 40, len(users)
+    r = rng.integers(1, 6, len(users)).astype(float)
+    P0, Q0, Y0 = (rng.normal(0, 0.1, (m, k)) for m in (nu, ni, ni))
+    rowptr, it, rr = O.csr_by(u, nu, i, r)
+    monkeypatch.setenv("RSGPU_PP_HEAVY", str(heavy))
+    for epochs in (1, 2):
+        ref = O.svdpp_fit_userwise(rowptr, it, rr, P0, Q0, Y0, epochs=epochs)
+        got = ctx.svdpp_fit(rsgpu.Ratings(u, i, r, nu, ni), P0, Q0, Y0, n_epochs=epochs)
+        assert _maxdiff(ref[:5], got[:5]) <= TOL, (heavy, k, epochs)
+        assert abs(ref[5] - got[5]) <= TOL
+
+
 def test_svdpp_fast_rmse_near_literal(ctx, fold0):
     """Fast (lazy, user-major, Hogwild) vs the literal reference order on ML-100K fold 1, defaults
     (k=20, 20 epochs, lr 0.007, reg 0.02)."""
