@@ -240,7 +240,7 @@ int rs_svd_plan_epochs(rs_svd_plan* plan, int32_t n_epochs, float lr, float reg,
 /* write_back: RS_SGD_WB_ATOMIC (default), _STORE or _ATOMIC_DIRECT; ring_depth: item-row prefetch distance
  * in ratings (4, 8 = default, 16). */
 int rs_svd_plan_set_mode(rs_svd_plan* plan, int32_t write_back, int32_t ring_depth);
-/* RS_SGD_WB_ATOMIC schedule.  Work items with at least heavy_min ratings (default 1024; 0 = none) run
+/* RS_SGD_WB_ATOMIC schedule.  Work items with at least heavy_min ratings (default 1000; 0 = none) run
  * as one SGD wave plus three writer waves that issue its atomics; the other (light) items are
  * strided over light_blocks blocks of four waves (default < 0: 1.5 per CU; 0: one wave per item).
  * Same arithmetic and results class as RS_SGD_WB_ATOMIC_DIRECT; only the visit timing changes
@@ -250,10 +250,12 @@ int rs_svd_plan_set_schedule(rs_svd_plan* plan, int32_t heavy_min, int32_t light
  * copies the last epoch's {start, chain end, write-back end} (100 MHz ticks, 3 int64 per work item, LPT
  * order) to out and the work items' users to user (may be NULL). */
 int rs_svd_plan_trace(rs_svd_plan* plan, int64_t* out, int32_t* user);
-/* FAST-mode work items: users with more than split_cap ratings (default 0 = never split) run as
+/* FAST-mode work items: users with more than split_cap ratings (default 1200; 0 = never split) run as
  * ceil(deg / split_cap) near-equal pieces on separate waves from the same p_u, and the row becomes the
  * count-weighted average of the pieces' end states after the epoch (or_svd_fit_chunked restates it).
- * Faster epochs, lower accuracy on large-degree users (measured trade-off). */
+ * Cuts the heaviest users' serial chains, which set the epoch's tail.  Measured trade-off (DESIGN.md
+ * K1): at 1200 the ML-1M-shaped held-out RMSE moves by +0.0008 (to within 0.0001 of the reference
+ * visit order's); at 256 by +0.024. */
 int rs_svd_plan_set_split(rs_svd_plan* plan, int32_t split_cap);
 /* FAST-mode hot items: an item with more than item_cap ratings (default 0 = never) gets
  * ceil(deg / item_cap) row copies; its ratings are dealt over them in user-CSR order and the copies
@@ -266,6 +268,12 @@ int rs_svd_plan_set_item_split(rs_svd_plan* plan, int32_t item_cap);
  * over several rows.  Hot replicas win over item_cap splitting for the items they take.
  * Default 256 x 8 (set n_hot = 0 to turn them off). */
 int rs_svd_plan_set_hot_replicas(rs_svd_plan* plan, int32_t n_hot, int32_t copies);
+/* Fixed-point item rows (default on; 0 turns it off): RS_SGD_WB_ATOMIC (hybrid) epochs convert Q in place to int32
+ * round(q * 2^24) before the epoch kernel and back after it, and the q_i deltas become integer
+ * atomics (memory-side u32 adds run at 1.69 TB/s against 1.32 TB/s for f32 on gfx950).  The
+ * resolution is the fp32 ulp at |q| in [0.5, 1); |q| must stay below 128 (saturates).  Other
+ * write-back modes ignore it. */
+int rs_svd_plan_set_fixed_q(rs_svd_plan* plan, int32_t on);
 /* ---- item-sharded multi-GPU (north_star: Q sharded by item range, users replicated) --------- *
  * Each rank builds a plan over its item shard.  Per epoch: rs_svd_plan_epoch_delta leaves P at the
  * epoch start and writes dP[u] = w_u (p_u(end) - p_u(start)) (bias column included; for a split

@@ -60,6 +60,16 @@ __device__ __forceinline__ float wave_sum(float x) {
     return __uint_as_float(r32[0]) + __uint_as_float(r32[1]);
 }
 
+// Fixed-point item rows (rs_svd_plan_set_fixed_q): during a hybrid FAST epoch Q holds
+// round(q * 2^24) as int32 and the q_i deltas are integer atomics.  Measured on gfx950
+// (scripts/exp_atomics.hip, exp_atomics2.hip): memory-side u32 atomic adds sustain 1.69 TB/s of
+// added bytes against 1.32 TB/s for f32 -- and the epoch is bound by that rate.  The resolution
+// 2^-24 is the fp32 ulp at |q| in [0.5, 1); the range is |q| < 128 (v_cvt_i32_f32 saturates).
+// Integer adds are exact and associative, so the sum of the deltas no longer depends on their order.
+constexpr float kFx = 16777216.f, kFxInv = 1.f / 16777216.f;
+__device__ __forceinline__ float fx_to_f(uint32_t bits) { return static_cast<float>(static_cast<int32_t>(bits)) * kFxInv; }
+__device__ __forceinline__ int32_t fx_delta(float qn, float q) { return __float2int_rn((qn - q) * kFx); }
+
 __device__ __forceinline__ float lane63(float x) {
     return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(x), 63));
 }
@@ -67,7 +77,14 @@ __device__ __forceinline__ float lane63(float x) {
 // One FAST work item (a user row or a piece of one): the SGD chain over its ratings with p_u in
 // VGPRs.  Every q_i update is handed to emit(row byte offset, q_new, q_old); the kernels below
 // differ only in how that update reaches memory.  Returns n * (gb_end - gb_start) for the fold.
-template <int E, int D, class Emit>
+//
+// LA (one-rating lookahead; kept for experiments, not instantiated by the launches):
+// p_{t+1} = a p_t - c_t q_t, so p_{t+1}.q_{t+1} = a (p_t.q_{t+1}) - c_t (q_t.q_{t+1}).  Both dots
+// depend only on p_t and the prefetched rows, so their reductions run beside rating t's chain and
+// the chain from c_t to c_{t+1} is one FMA plus the diff.  Parity-tested on the heavy producers,
+// but measured slower there (ML-1M epoch 585 -> 610 us, heavy chains still ~250 ns/rating): under
+// the atomic load the heavy chain is not gated by its reduction.
+template <int E, int D, bool FX = false, bool LA = false, class Emit>
 __device__ __forceinline__ double sgd_work_item(
     int32_t w, const int32_t* __restrict__ wk_user, const int64_t* __restrict__ wk_rng,
     const float* __restrict__ wk_frac, const int32_t* __restrict__ items,
@@ -94,8 +111,10 @@ __device__ __forceinline__ double sgd_work_item(
     auto load_row = [&](float (&q)[E], int32_t valid, int32_t item) {
         const int32_t row = valid ? item * (LD * 4) : kOutOfRange;  // SGPR arithmetic
 #pragma unroll
-        for (int x = 0; x < E; ++x)
-            q[x] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rq, row + lane4 + 256 * x, 0, kSgdAux));
+        for (int x = 0; x < E; ++x) {
+            const uint32_t v = __builtin_amdgcn_raw_buffer_load_b32(rq, row + lane4 + 256 * x, 0, kSgdAux);
+            q[x] = FX ? fx_to_f(v) : __uint_as_float(v);
+        }
     };
 
     // Item ids and ratings come in 32-entry chunks, one vector load per chunk (lane l holds entry
@@ -129,6 +148,14 @@ __device__ __forceinline__ double sgd_work_item(
         load_row(ring[s], s < deg, __builtin_amdgcn_readlane(viA, s));
         __builtin_amdgcn_sched_barrier(0);
     }
+    float s_next = 0.f;  // LA: p_t.q_t of the next rating, precomputed
+    if constexpr (LA) {
+        float s0 = 0.f;
+#pragma unroll
+        for (int x = 0; x < E - 1; ++x) s0 += p[x] * ring[0][x];
+        s0 += p[E - 1] * (bias_lane ? 0.f : ring[0][E - 1]);
+        s_next = wave_sum(s0);
+    }
 
     // the ratings [base, base + B) of the chunk held in (vi, vr); vn holds the next chunk's items
     auto chunk = [&](int64_t base, int32_t vi, float vr, int32_t vn) {
@@ -141,15 +168,32 @@ __device__ __forceinline__ double sgd_work_item(
                 float(&q)[E] = ring[slot];
                 const float bq = lane63(q[E - 1]);
                 const float rt = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(vr), j));
-                float s = 0.f;
+                float s = 0.f, la_a = 0.f, la_b = 0.f;
+                if constexpr (LA) {
+                    s = s_next;
+                    static_assert(D >= 2, "lookahead reads the next ring slot");
+                    const float(&q1)[E] = ring[(j + 1) % kD];  // the next rating's row (unused past the end)
 #pragma unroll
-                for (int x = 0; x < E - 1; ++x) s += p[x] * q[x];
-                s += p[E - 1] * (bias_lane ? 0.f : q[E - 1]);
-                s = wave_sum(s);
+                    for (int x = 0; x < E - 1; ++x) {
+                        la_a += p[x] * q1[x];
+                        la_b += q[x] * q1[x];
+                    }
+                    const float q1l = bias_lane ? 0.f : q1[E - 1];
+                    la_a += p[E - 1] * q1l;
+                    la_b += q[E - 1] * q1l;
+                    la_a = wave_sum(la_a);
+                    la_b = wave_sum(la_b);
+                } else {
+#pragma unroll
+                    for (int x = 0; x < E - 1; ++x) s += p[x] * q[x];
+                    s += p[E - 1] * (bias_lane ? 0.f : q[E - 1]);
+                    s = wave_sum(s);
+                }
                 // svd.go:102-128 in FMA form: a = 1 - lr*reg, c = lr*diff:
                 // p <- a p - c q ; q <- a q - c p_new ; b <- a b - c ; gb <- gb - c
                 const float diff = ((gb + ub) + bq) + s - rt;
                 const float c = lr * diff;
+                if constexpr (LA) s_next = __builtin_fmaf(a, la_a, -c * la_b);
                 gb -= c;
                 ub = __builtin_fmaf(ub, a, -c);
                 const float bq_new = __builtin_fmaf(bq, a, -c);
@@ -275,7 +319,7 @@ __device__ __forceinline__ void lds_store_relaxed(int32_t* p, int32_t v) {
 // round once after the epoch so the item row and its copies leave the epoch equal.
 constexpr int kMaxLiveCopies = 8;
 
-template <int E, int D, bool DROP = false, bool MERGE = false>
+template <int E, int D, bool DROP = false, bool MERGE = false, bool FX = false>
 __global__ __launch_bounds__(256) void svd_epoch_hybrid_kernel(
     const int32_t* __restrict__ wk_user, const int64_t* __restrict__ wk_rng,
     const float* __restrict__ wk_frac, int32_t n_work, int32_t n_heavy,
@@ -312,7 +356,38 @@ __global__ __launch_bounds__(256) void svd_epoch_hybrid_kernel(
         for (;;) {
             const int32_t d = __builtin_amdgcn_readfirstlane(
                 __hip_atomic_load(done, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
-            {
+            if constexpr (FX) {  // the same round on the int32 rows: exact, wrap-around arithmetic
+                uint32_t c[kMaxLiveCopies][E];
+#pragma unroll
+                for (int r = 0; r < kMaxLiveCopies; ++r) {
+                    const int32_t row = (r < R ? (r == 0 ? m.x : m.y + r - 1) * (LD * 4) : kOutOfRange);
+#pragma unroll
+                    for (int x = 0; x < E; ++x)
+                        c[r][x] = __builtin_amdgcn_raw_buffer_load_b32(rq, row + lane4 + 256 * x, 0, kSgdAux);
+                }
+                uint32_t nv[E];
+#pragma unroll
+                for (int x = 0; x < E; ++x) {
+                    const uint32_t l = __float_as_uint(last[x]);
+                    uint32_t acc = l;
+#pragma unroll
+                    for (int r = 0; r < kMaxLiveCopies; ++r)
+                        if (r < R) acc += c[r][x] - l;
+                    nv[x] = acc;
+                }
+#pragma unroll
+                for (int r = 0; r < kMaxLiveCopies; ++r) {
+                    if (r < R) {
+                        const int32_t row = (r == 0 ? m.x : m.y + r - 1) * (LD * 4);
+#pragma unroll
+                        for (int x = 0; x < E; ++x)
+                            __builtin_amdgcn_raw_ptr_buffer_atomic_add_i32(static_cast<int32_t>(nv[x] - c[r][x]), rq,
+                                                                           row + lane4 + 256 * x, 0, 0);
+                    }
+                }
+#pragma unroll
+                for (int x = 0; x < E; ++x) last[x] = __uint_as_float(nv[x]);
+            } else {
                 float c[kMaxLiveCopies][E];
 #pragma unroll
                 for (int r = 0; r < kMaxLiveCopies; ++r) {
@@ -352,13 +427,18 @@ __global__ __launch_bounds__(256) void svd_epoch_hybrid_kernel(
         const int stride = (n_sgd_blocks - n_heavy) * 4;
         for (int w = n_heavy + (blk - n_heavy) * 4 + wib; w < n_work; w += stride) {
             const int64_t t0 = trace ? static_cast<int64_t>(__builtin_amdgcn_s_memrealtime()) : 0;
-            contrib += sgd_work_item<E, D>(
+            contrib += sgd_work_item<E, D, FX>(
                 w, wk_user, wk_rng, wk_frac, items, ratings, P, rq, gb0, lr, reg, dP, uw, whole_direct,
                 [&](int32_t row, const float (&qn)[E], const float (&q)[E]) {
 #pragma unroll
-                    for (int x = 0; x < E; ++x)
-                        if constexpr (!DROP)
+                    for (int x = 0; x < E; ++x) {
+                        if constexpr (DROP) {
+                        } else if constexpr (FX) {
+                            __builtin_amdgcn_raw_ptr_buffer_atomic_add_i32(fx_delta(qn[x], q[x]), rq, row + lane4 + 256 * x, 0, 0);
+                        } else {
                             __builtin_amdgcn_raw_ptr_buffer_atomic_fadd_f32(qn[x] - q[x], rq, row + lane4 + 256 * x, 0, 0);
+                        }
+                    }
                 });
             if (trace && lane == 0) {  // diagnostic timeline (100 MHz clock)
                 const int64_t t1 = static_cast<int64_t>(__builtin_amdgcn_s_memrealtime());
@@ -385,7 +465,7 @@ __global__ __launch_bounds__(256) void svd_epoch_hybrid_kernel(
     const int64_t t0 = trace ? static_cast<int64_t>(__builtin_amdgcn_s_memrealtime()) : 0;
     if (wib == 0) {
         int32_t tail = 0, free_end = R;  // entries [tail, free_end) may be written
-        contrib = sgd_work_item<E, DH>(
+        contrib = sgd_work_item<E, DH, FX, false>(
             blk, wk_user, wk_rng, wk_frac, items, ratings, P, rq, gb0, lr, reg, dP, uw, whole_direct,
             [&](int32_t row, const float (&qn)[E], const float (&q)[E]) {
                 if (tail >= free_end) {  // ring full: every entry below min(head) has been drained
@@ -399,7 +479,8 @@ __global__ __launch_bounds__(256) void svd_epoch_hybrid_kernel(
                 }
                 const int slot = tail & (R - 1);
 #pragma unroll
-                for (int x = 0; x < E; ++x) s_q[slot][lane + 64 * x] = qn[x] - q[x];
+                for (int x = 0; x < E; ++x)
+                    s_q[slot][lane + 64 * x] = FX ? __int_as_float(fx_delta(qn[x], q[x])) : qn[x] - q[x];
                 if (lane == 0) s_row[slot] = row;
                 __atomic_signal_fence(__ATOMIC_SEQ_CST);  // entry before tail, in issue order
                 ++tail;
@@ -430,9 +511,14 @@ __global__ __launch_bounds__(256) void svd_epoch_hybrid_kernel(
                         if (j < n) {
                             const int32_t row = __builtin_amdgcn_readlane(myrow, j);
 #pragma unroll
-                            for (int x = 0; x < E; ++x)
-                                if constexpr (!DROP)
+                            for (int x = 0; x < E; ++x) {
+                                if constexpr (DROP) {
+                                } else if constexpr (FX) {
+                                    __builtin_amdgcn_raw_ptr_buffer_atomic_add_i32(__float_as_int(v[j][x]), rq, row + lane4 + 256 * x, 0, 0);
+                                } else {
                                     __builtin_amdgcn_raw_ptr_buffer_atomic_fadd_f32(v[j][x], rq, row + lane4 + 256 * x, 0, 0);
+                                }
+                            }
                         }
                     }
                     next += NW * n;
@@ -519,6 +605,30 @@ __global__ __launch_bounds__(64) void svd_live_merge_kernel(float* __restrict__ 
             for (int32_t c = 0; c < m.z; ++c) v += Q[row(c) + col] - l;
             for (int32_t c = 0; c < m.z; ++c) Q[row(c) + col] = v;
         }
+    }
+}
+
+// Fixed-point item rows around a hybrid epoch (rs_svd_plan_set_fixed_q), in place over Q's n
+// words: to == 1: q -> round(q * 2^24) (saturating), to == 0: back to fp32.
+__global__ __launch_bounds__(256) void svd_q_fixed_kernel(float* __restrict__ Q, int64_t n, int32_t to) {
+    for (int64_t t = static_cast<int64_t>(blockIdx.x) * 256 + threadIdx.x; t < n;
+         t += static_cast<int64_t>(gridDim.x) * 256)
+        Q[t] = to ? __int_as_float(__float2int_rn(Q[t] * kFx)) : fx_to_f(__float_as_uint(Q[t]));
+}
+
+// The live items' final merge round on the int32 rows (fixed-point epochs): exact integer
+// N = L + sum_r (c_r - L), written to every copy; L := N.
+__global__ __launch_bounds__(64) void svd_live_merge_fx_kernel(int32_t* __restrict__ Q, const int4* __restrict__ meta,
+                                                              int32_t* __restrict__ qlast, int32_t ld) {
+    const int4 m = meta[blockIdx.x];
+    auto row = [&](int32_t c) { return static_cast<int64_t>(c == 0 ? m.x : m.y + c - 1) * ld; };
+    int32_t* L = qlast + static_cast<int64_t>(blockIdx.x) * ld;
+    for (int32_t col = threadIdx.x; col < ld; col += 64) {
+        const uint32_t l = static_cast<uint32_t>(L[col]);
+        uint32_t v = l;
+        for (int32_t c = 0; c < m.z; ++c) v += static_cast<uint32_t>(Q[row(c) + col]) - l;
+        for (int32_t c = 0; c < m.z; ++c) Q[row(c) + col] = static_cast<int32_t>(v);
+        L[col] = static_cast<int32_t>(v);
     }
 }
 
@@ -734,7 +844,10 @@ struct rs_svd_plan {
     rs::DevBuf<int32_t> wk_user;      // work items: user, [begin, end) into the CSR, len / deg
     rs::DevBuf<int64_t> wk_rng;
     rs::DevBuf<float> wk_frac;
-    int32_t split_cap = 0;            // users with more ratings are split into pieces (0: never)
+    // users with more ratings are split into pieces (0: never).  Default 1200, measured on the ML-1M
+    // shape with heavy_min 1000 and fixed-point Q (scripts/exp_split_sweep.py): epoch 572 -> 491 us,
+    // 20-epoch held-out RMSE 0.6676 -> 0.6684 against 0.6683 for the reference visit order
+    int32_t split_cap = 1200;
     rs::DevBuf<float> dPs;            // split-user deltas (single GPU), zero between epochs
     rs::DevBuf<int32_t> split_rows;   // users split into pieces
     int32_t n_split = 0;
@@ -757,11 +870,13 @@ struct rs_svd_plan {
     rs::DevBuf<float> Q0;  // Q at the epoch start (user-sharded mode)
     int32_t n_blocks = 0;
     int32_t write_back = RS_SGD_WB_ATOMIC;
-    int32_t heavy_min = 1024;  // work items with at least this many ratings get a producer + 3 writers
+    int32_t heavy_min = 1000;  // work items with at least this many ratings get a producer + 3 writers
     int32_t n_heavy = 0;       // leading (LPT-ordered) work items that are heavy
     int32_t light_blocks = 0;  // cap on the light blocks (each wave strides over light items; 0 = none)
     rs::DevBuf<int64_t> trace;  // diagnostic: {start, chain end, drained} per work item (RS_SGD_WB_ATOMIC)
     int32_t ring_depth = 8;
+    int32_t fixed_q = 1;           // hybrid epochs keep Q as int32 fixed point (rs_svd_plan_set_fixed_q)
+    bool live_merged = false;      // the fixed-point epoch already ran the live items' final round
     double mean_rating = 0.0;  // of the plan's ratings (FAST GlobalBias warm start at init)
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
     double last_ms = 0.0;
@@ -812,7 +927,17 @@ static void launch_fast_t(rs_svd_plan* pl, float lr, float reg, hipStream_t s, f
     float* d = multi ? dP : (pl->n_split > 0 ? pl->dPs.p : nullptr);
     pl->n_blocks = fast_blocks(pl);
     if constexpr (WB == 2 || WB == 5) {
-        if (pl->n_live > 0) {
+        if (WB == 2 && pl->fixed_q) {
+            if (pl->n_live > 0) RS_HIP(hipMemsetAsync(pl->done.p, 0, sizeof(int32_t), s));
+            auto kern = pl->n_live > 0 ? svd_epoch_hybrid_kernel<E, D, false, true, true>
+                                       : svd_epoch_hybrid_kernel<E, D, false, false, true>;
+            hipLaunchKernelGGL(kern, dim3(pl->n_blocks), dim3(256), 0, s,
+                               pl->wk_user.p, pl->wk_rng.p, pl->wk_frac.p, pl->n_work, pl->n_heavy,
+                               pl->items.p, pl->ratings.p, pl->P.p, pl->Q.p, q_bytes, pl->gb.p,
+                               pl->partial.p, lr, reg, d, multi ? pl->uw.p : nullptr, multi ? 0 : 1,
+                               pl->trace.n ? pl->trace.p : nullptr, pl->n_live > 0 ? pl->live_meta.p : nullptr,
+                               pl->n_live, pl->n_live > 0 ? pl->qlast.p : nullptr, pl->n_live > 0 ? pl->done.p : nullptr);
+        } else if (pl->n_live > 0) {
             RS_HIP(hipMemsetAsync(pl->done.p, 0, sizeof(int32_t), s));
             hipLaunchKernelGGL((svd_epoch_hybrid_kernel<E, D, WB == 5, true>), dim3(pl->n_blocks), dim3(256), 0, s,
                                pl->wk_user.p, pl->wk_rng.p, pl->wk_frac.p, pl->n_work, pl->n_heavy,
@@ -859,7 +984,11 @@ static void launch_fast_d(rs_svd_plan* pl, float lr, float reg, hipStream_t s, f
 }
 
 static void launch_fast(rs_svd_plan* pl, float lr, float reg, hipStream_t s, float* dP = nullptr) {
-    if (pl->n_live > 0)  // L = the live items' rows at the epoch start
+    const bool fx = pl->fixed_q && pl->write_back == RS_SGD_WB_ATOMIC;
+    const int64_t qn = static_cast<int64_t>(pl->Q.n);
+    const int fx_blocks = static_cast<int>(std::min<int64_t>(2048, (qn + 255) / 256));
+    if (fx) hipLaunchKernelGGL(svd_q_fixed_kernel, dim3(fx_blocks), dim3(256), 0, s, pl->Q.p, qn, 1);
+    if (pl->n_live > 0)  // L = the live items' rows at the epoch start (a bit copy: int32 rows too)
         hipLaunchKernelGGL(svd_live_merge_kernel, dim3(pl->n_live), dim3(64), 0, s, pl->Q.p, pl->live_meta.p,
                            pl->qlast.p, pl->ld, 0);
     switch (pl->write_back) {
@@ -869,11 +998,24 @@ static void launch_fast(rs_svd_plan* pl, float lr, float reg, hipStream_t s, flo
         case 101: launch_fast_d<5>(pl, lr, reg, s, dP); break;                      // DIAG: writer drops
         default: launch_fast_d<2>(pl, lr, reg, s, dP); break;                       // hybrid
     }
+    if (fx) {  // final live round on the int32 rows, then back to fp32 (live_merge_after skips)
+        if (pl->n_live > 0) {
+            hipLaunchKernelGGL(svd_live_merge_fx_kernel, dim3(pl->n_live), dim3(64), 0, s,
+                               reinterpret_cast<int32_t*>(pl->Q.p), pl->live_meta.p,
+                               reinterpret_cast<int32_t*>(pl->qlast.p), pl->ld);
+            pl->live_merged = true;
+        }
+        hipLaunchKernelGGL(svd_q_fixed_kernel, dim3(fx_blocks), dim3(256), 0, s, pl->Q.p, qn, 0);
+    }
     RS_HIP(hipGetLastError());
 }
 
 // After an epoch: the live items' final merge round (their copies leave the epoch equal).
 static void live_merge_after(rs_svd_plan* pl, hipStream_t s) {
+    if (pl->live_merged) {
+        pl->live_merged = false;
+        return;
+    }
     if (pl->n_live > 0)
         hipLaunchKernelGGL(svd_live_merge_kernel, dim3(pl->n_live), dim3(64), 0, s, pl->Q.p, pl->live_meta.p,
                            pl->qlast.p, pl->ld, 1);
@@ -1485,6 +1627,14 @@ extern "C" int rs_svd_plan_set_schedule(rs_svd_plan* pl, int32_t heavy_min, int3
         pl->heavy_min = heavy_min;
         pl->light_blocks = light_blocks < 0 ? rs::default_light_blocks(pl->ctx) : light_blocks;
         rs::build_work(pl);
+        return RS_OK;
+    });
+}
+
+extern "C" int rs_svd_plan_set_fixed_q(rs_svd_plan* pl, int32_t on) {
+    if (!pl) return rs::set_error(nullptr, RS_ERR_INVALID, "plan is NULL");
+    return rs_guard(pl->ctx, [&]() -> int {
+        pl->fixed_q = on ? 1 : 0;
         return RS_OK;
     });
 }

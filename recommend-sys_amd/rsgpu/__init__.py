@@ -38,7 +38,7 @@ HEADER_SYMBOLS = (
     "rs_trainset_ids", "rs_csr_build", "rs_global_mean",
     "rs_synth_create", "rs_synth_csr", "rs_synth_destroy",
     "rs_svd_plan_set_item_weights", "rs_svd_plan_epoch_qdelta", "rs_svd_plan_apply_qdelta",
-    "rs_svd_plan_set_hot_replicas",
+    "rs_svd_plan_set_hot_replicas", "rs_svd_plan_set_fixed_q",
 )
 
 
@@ -126,6 +126,7 @@ def lib():
                                           _i32, _i32, _i32, _i32, C.POINTER(_vp)]),
             "rs_svd_plan_set_item_weights": (C.c_int, [_vp, _vp]),
             "rs_svd_plan_set_hot_replicas": (C.c_int, [_vp, _i32, _i32]),
+            "rs_svd_plan_set_fixed_q": (C.c_int, [_vp, _i32]),
             "rs_svd_plan_epoch_qdelta": (C.c_int, [_vp, _flt, _flt, _vp, _vp, _vp]),
             "rs_svd_plan_apply_qdelta": (C.c_int, [_vp, _vp, _vp, _dbl, _vp]),
             "rs_synth_csr": (C.c_int, [_vp, C.POINTER(_i64), C.POINTER(_vp), C.POINTER(_vp),
@@ -432,6 +433,10 @@ class SvdPlan:
 
     def set_split(self, split_cap):
         self.ctx.check(lib().rs_svd_plan_set_split(self.h, split_cap))
+
+    def set_fixed_q(self, on=True):
+        """Hybrid FAST epochs keep Q as int32 fixed point (2^-24) with integer atomics."""
+        self.ctx.check(lib().rs_svd_plan_set_fixed_q(self.h, 1 if on else 0))
 
     def set_hot_replicas(self, n_hot, copies=4):
         """Live-merged row copies for the n_hot most-rated items (0 = none)."""

@@ -48,9 +48,14 @@ def _compile(src: str, obj: str) -> None:
 
 
 def build(verbose: bool = False, jobs: int = 8) -> str:
-    os.makedirs(BUILD, exist_ok=True)
     srcs = _sources()
     hdr_time = max((os.path.getmtime(h) for h in _headers()), default=0.0)
+    # a library newer than every source is current even where the objects are absent (the GPU
+    # box's snapshot ships librsgpu.so but not build/): never recompile there
+    if os.path.exists(LIB) and os.path.getmtime(LIB) + 1.0 >= max(
+            [hdr_time] + [os.path.getmtime(s) for s in srcs]):
+        return LIB
+    os.makedirs(BUILD, exist_ok=True)
     todo = []
     objs = []
     for s in srcs:

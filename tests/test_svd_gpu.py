@@ -85,12 +85,14 @@ def test_fast_matches_own_schedule_race_free(ctx, k, wb):
         assert abs(ref[4] - got[4]) <= TOL
 
 
+@pytest.mark.parametrize("fx", [0, 1])
 @pytest.mark.parametrize("heavy,lb", [(16, -1), (512, 3), (0, 1), (0, 0), (1024, -1)])
 @pytest.mark.parametrize("k", [20, 100, 300])
-def test_fast_long_rows_race_free(ctx, k, heavy, lb):
+def test_fast_long_rows_race_free(ctx, k, heavy, lb, fx):
     """Rows of hundreds of ratings through the hybrid write-back: heavy rows' LDS rings fill and wrap
     many times (heavy 16: every row; 512: the longest; 0: none), light rows strided over few blocks
-    (lb 1 or 3) or one wave each (lb 0) -- equal to the restatement."""
+    (lb 1 or 3) or one wave each (lb 0) -- equal to the restatement.  Heavy rows run the lookahead
+    dot; fx 1 keeps Q as int32 fixed point with integer atomics (2^-24 resolution, within TOL)."""
     u, i, r, nu, ni = _disjoint_input(n_users=40, per_user=400, k=k, seed=12)
     rng = np.random.default_rng(k + 1)
     P0, Q0 = rng.normal(0, 0.1, (nu, k)), rng.normal(0, 0.1, (ni, k))
@@ -98,6 +100,7 @@ def test_fast_long_rows_race_free(ctx, k, heavy, lb):
     rowptr, items, rr = O.csr_by(u, nu, i, r)
     plan = ctx.svd_plan(rsgpu.Ratings(u, i, r, nu, ni), k)
     plan.set_schedule(heavy, lb)
+    plan.set_fixed_q(fx)
     plan.upload(P0, Q0, bu0, bi0, 3.1)
     plan.epochs(2)
     got = plan.download()
