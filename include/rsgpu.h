@@ -207,7 +207,7 @@ int rs_knn_plan_predict(rs_knn_plan* plan, int32_t type, int32_t n_right, const 
 /* ---- device-resident SVD plan (bench / multi-GPU hosts; device pointers) -------------------- */
 /* A plan uploads the user-CSR once and keeps the model resident in HBM: P (n_users x ld) and
  * Q (n_items x ld) float32 with ld = 64 * ceil((n_factors + 1) / 64); columns [0, n_factors) hold
- * the factors, column ld - 1 the bias (b_u in P, b_i in Q), the rest is zero; GlobalBias is one
+ * the factors, column n_factors the bias (b_u in P, b_i in Q), the rest is zero; GlobalBias is one
  * float64.  Epochs are enqueued on `stream` without host syncs. */
 typedef struct rs_svd_plan rs_svd_plan;
 

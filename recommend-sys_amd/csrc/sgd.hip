@@ -21,9 +21,10 @@
 //           svd.go:93-129 (aliasing Q1: q_i is updated with the NEW p_u) -- factor parity (P1).
 //
 // Device layout of the FAST plan (HBM, fp32): P is n_users x ld, Q is n_items x ld with
-// ld = 64 * ceil((k + 1) / 64); columns [0, k) hold the factors, column ld - 1 holds the bias
+// ld = 64 * ceil((k + 1) / 64); columns [0, k) hold the factors, column k holds the bias
 // (b_u in P, b_i in Q), the rest is zero padding.  Lane l of the wave owns columns l + 64 x, so one
-// row is E = ld / 64 fully coalesced 256-byte wave instructions and the bias sits in lane 63.
+// row is E = ld / 64 coalesced wave instructions; the bias is lane 63 of the last one (last_col), and
+// the padding lanes of the last one issue nothing.
 //
 // Cross-XCD visibility (MI355X_MICROARCH.md "Workgroup dispatch, XCD placement & inter-workgroup
 // visibility"): per-CU L1s and per-XCD L2s are not coherent inside a launch.  q_i loads carry sc1
@@ -70,6 +71,23 @@ constexpr float kFx = 16777216.f, kFxInv = 1.f / 16777216.f;
 __device__ __forceinline__ float fx_to_f(uint32_t bits) { return static_cast<float>(static_cast<int32_t>(bits)) * kFxInv; }
 __device__ __forceinline__ int32_t fx_delta(float qn, float q) { return __float2int_rn((qn - q) * kFx); }
 
+// Row layout of the FAST plan: lane l's register x holds column l + 64 x, except lane 63's last
+// register, which holds the bias in column kf (right after the kf factors).  The other lanes of the
+// last register whose column is >= kf are padding: never loaded (they read 0) and never written, so
+// the 64-B lines past column kf get no memory request at all -- row atomics are priced per 64-B line,
+// not per dword (scripts/exp_atomics2.hip: 1.69 -> 1.93 TB/s of row bytes with one line of eight
+// masked off); k = 100 rows take 7 line requests instead of 8.
+template <int E>
+__device__ __forceinline__ int32_t last_col(int lane, int32_t kf) {  // column of register E-1, or -1
+    const int32_t c = lane == 63 ? kf : lane + 64 * (E - 1);
+    return (lane == 63 || c < kf) ? c : -1;
+}
+// byte offset of register x of this lane in the row at byte offset `row` (kOutOfRange: padding)
+template <int E>
+__device__ __forceinline__ int32_t roff(int32_t row, int x, int32_t lane4, int32_t lc) {
+    return x < E - 1 ? row + lane4 + 256 * x : (lc >= 0 ? row + 4 * lc : kOutOfRange);
+}
+
 __device__ __forceinline__ float lane63(float x) {
     return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(x), 63));
 }
@@ -90,7 +108,7 @@ __device__ __forceinline__ double sgd_work_item(
     const float* __restrict__ wk_frac, const int32_t* __restrict__ items,
     const float* __restrict__ ratings, float* __restrict__ P, __amdgpu_buffer_rsrc_t rq, float gb0,
     float lr, float reg, float* __restrict__ dP, const float* __restrict__ uw, int32_t whole_direct,
-    Emit&& emit) {
+    int32_t lc, Emit&& emit) {
 #pragma clang fp contract(fast)
     constexpr int LD = 64 * E, B = 32;  // ratings per chunk (one unrolled loop body)
     static_assert(B % D == 0 && D <= B, "ring depth must divide the 32-rating chunk");
@@ -104,7 +122,7 @@ __device__ __forceinline__ double sgd_work_item(
     float p[E];
     float* prow = P + static_cast<int64_t>(u) * LD;
 #pragma unroll
-    for (int x = 0; x < E; ++x) p[x] = prow[lane + 64 * x];
+    for (int x = 0; x < E; ++x) p[x] = x < E - 1 ? prow[lane + 64 * x] : (lc >= 0 ? prow[lc] : 0.f);
     float ub = lane63(p[E - 1]);
     float gb = gb0;
 
@@ -112,7 +130,7 @@ __device__ __forceinline__ double sgd_work_item(
         const int32_t row = valid ? item * (LD * 4) : kOutOfRange;  // SGPR arithmetic
 #pragma unroll
         for (int x = 0; x < E; ++x) {
-            const uint32_t v = __builtin_amdgcn_raw_buffer_load_b32(rq, row + lane4 + 256 * x, 0, kSgdAux);
+            const uint32_t v = __builtin_amdgcn_raw_buffer_load_b32(rq, roff<E>(row, x, lane4, lc), 0, kSgdAux);
             q[x] = FX ? fx_to_f(v) : __uint_as_float(v);
         }
     };
@@ -227,10 +245,16 @@ __device__ __forceinline__ double sgd_work_item(
         const float sc = uw ? frac * uw[u] : frac;
         float* drow = dP + static_cast<int64_t>(u) * LD;
 #pragma unroll
-        for (int x = 0; x < E; ++x) atomicAdd(drow + lane + 64 * x, sc * (p[x] - prow[lane + 64 * x]));
+        for (int x = 0; x < E; ++x) {
+            const int32_t c = x < E - 1 ? lane + 64 * x : lc;
+            if (c >= 0) atomicAdd(drow + c, sc * (p[x] - prow[c]));
+        }
     } else {
 #pragma unroll
-        for (int x = 0; x < E; ++x) prow[lane + 64 * x] = p[x];
+        for (int x = 0; x < E; ++x) {
+            const int32_t c = x < E - 1 ? lane + 64 * x : lc;
+            if (c >= 0) prow[c] = p[x];
+        }
     }
     return static_cast<double>(deg) * (static_cast<double>(gb) - static_cast<double>(gb0));
 }
@@ -248,26 +272,27 @@ __global__ __launch_bounds__(256) void svd_epoch_fast_kernel(
     const float* __restrict__ wk_frac, int32_t n_work, const int32_t* __restrict__ items,
     const float* __restrict__ ratings, float* __restrict__ P, float* Q, int32_t q_bytes,
     const double* __restrict__ gb_in, double* __restrict__ gb_partial, float lr, float reg,
-    float* __restrict__ dP, const float* __restrict__ uw, int32_t whole_direct) {
+    float* __restrict__ dP, const float* __restrict__ uw, int32_t whole_direct, int32_t kf) {
     __shared__ double s_contrib[4];
     const int lane = threadIdx.x & 63;
     const int wib = threadIdx.x >> 6;
     const int w = __builtin_amdgcn_readfirstlane(static_cast<int>(blockIdx.x) * 4 + wib);
     const __amdgpu_buffer_rsrc_t rq = __builtin_amdgcn_make_buffer_rsrc(Q, 0, q_bytes, 0x00020000);
     const int32_t lane4 = lane * 4;
+    const int32_t lc = last_col<E>(lane, kf);
     double contrib = 0.0;
     if (w < n_work) {
         contrib = sgd_work_item<E, D>(
             w, wk_user, wk_rng, wk_frac, items, ratings, P, rq, static_cast<float>(gb_in[0]), lr, reg,
-            dP, uw, whole_direct, [&](int32_t row, const float (&qn)[E], const float (&q)[E]) {
+            dP, uw, whole_direct, lc, [&](int32_t row, const float (&qn)[E], const float (&q)[E]) {
 #pragma unroll
                 for (int x = 0; x < E; ++x) {
                     if constexpr (WB == 1)
-                        __builtin_amdgcn_raw_ptr_buffer_atomic_fadd_f32(qn[x] - q[x], rq, row + lane4 + 256 * x, 0, 0);
+                        __builtin_amdgcn_raw_ptr_buffer_atomic_fadd_f32(qn[x] - q[x], rq, roff<E>(row, x, lane4, lc), 0, 0);
                     else if constexpr (WB == 4)
                         __builtin_amdgcn_sched_barrier(0);
                     else
-                        __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(qn[x]), rq, row + lane4 + 256 * x, 0, kSgdAux);
+                        __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(qn[x]), rq, roff<E>(row, x, lane4, lc), 0, kSgdAux);
                 }
             });
     }
@@ -327,7 +352,7 @@ __global__ __launch_bounds__(256) void svd_epoch_hybrid_kernel(
     float* Q, int32_t q_bytes, const double* __restrict__ gb_in, double* __restrict__ gb_partial,
     float lr, float reg, float* __restrict__ dP, const float* __restrict__ uw, int32_t whole_direct,
     int64_t* __restrict__ trace, const int4* __restrict__ live_meta, int32_t n_live,
-    float* __restrict__ qlast, int32_t* __restrict__ done) {
+    float* __restrict__ qlast, int32_t* __restrict__ done, int32_t kf) {
     constexpr int R = HeavyRing<E>::kRing, NB = HeavyRing<E>::kBatch, LD = 64 * E, NW = 3;
     // the producer's vmcnt holds only its q_i loads: prefetch as deep as the 63-op counter allows
     constexpr int DH = E == 1 ? 32 : (E == 2 ? 32 : (E <= 4 ? 16 : 8));
@@ -339,6 +364,7 @@ __global__ __launch_bounds__(256) void svd_epoch_hybrid_kernel(
     const int wib = __builtin_amdgcn_readfirstlane(static_cast<int>(threadIdx.x) >> 6);
     const __amdgpu_buffer_rsrc_t rq = __builtin_amdgcn_make_buffer_rsrc(Q, 0, q_bytes, 0x00020000);
     const int32_t lane4 = lane * 4;
+    const int32_t lc = last_col<E>(lane, kf);
     const float gb0 = static_cast<float>(gb_in[0]);
     const int blk = static_cast<int>(blockIdx.x);
     const int n_merge_blocks = MERGE ? (n_live + 3) / 4 : 0;
@@ -352,7 +378,10 @@ __global__ __launch_bounds__(256) void svd_epoch_hybrid_kernel(
         const int R = m.z;
         float last[E];
 #pragma unroll
-        for (int x = 0; x < E; ++x) last[x] = qlast[static_cast<int64_t>(h) * LD + lane + 64 * x];
+        for (int x = 0; x < E; ++x) {
+            const int32_t c = x < E - 1 ? lane + 64 * x : lc;
+            last[x] = c >= 0 ? qlast[static_cast<int64_t>(h) * LD + c] : 0.f;
+        }
         for (;;) {
             const int32_t d = __builtin_amdgcn_readfirstlane(
                 __hip_atomic_load(done, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
@@ -363,7 +392,7 @@ __global__ __launch_bounds__(256) void svd_epoch_hybrid_kernel(
                     const int32_t row = (r < R ? (r == 0 ? m.x : m.y + r - 1) * (LD * 4) : kOutOfRange);
 #pragma unroll
                     for (int x = 0; x < E; ++x)
-                        c[r][x] = __builtin_amdgcn_raw_buffer_load_b32(rq, row + lane4 + 256 * x, 0, kSgdAux);
+                        c[r][x] = __builtin_amdgcn_raw_buffer_load_b32(rq, roff<E>(row, x, lane4, lc), 0, kSgdAux);
                 }
                 uint32_t nv[E];
 #pragma unroll
@@ -382,7 +411,7 @@ __global__ __launch_bounds__(256) void svd_epoch_hybrid_kernel(
 #pragma unroll
                         for (int x = 0; x < E; ++x)
                             __builtin_amdgcn_raw_ptr_buffer_atomic_add_i32(static_cast<int32_t>(nv[x] - c[r][x]), rq,
-                                                                           row + lane4 + 256 * x, 0, 0);
+                                                                           roff<E>(row, x, lane4, lc), 0, 0);
                     }
                 }
 #pragma unroll
@@ -394,7 +423,7 @@ __global__ __launch_bounds__(256) void svd_epoch_hybrid_kernel(
                     const int32_t row = (r < R ? (r == 0 ? m.x : m.y + r - 1) * (LD * 4) : kOutOfRange);
 #pragma unroll
                     for (int x = 0; x < E; ++x)
-                        c[r][x] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rq, row + lane4 + 256 * x, 0, kSgdAux));
+                        c[r][x] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rq, roff<E>(row, x, lane4, lc), 0, kSgdAux));
                 }
                 float nv[E];
 #pragma unroll
@@ -411,7 +440,7 @@ __global__ __launch_bounds__(256) void svd_epoch_hybrid_kernel(
                         const int32_t row = (r == 0 ? m.x : m.y + r - 1) * (LD * 4);
 #pragma unroll
                         for (int x = 0; x < E; ++x)
-                            __builtin_amdgcn_raw_ptr_buffer_atomic_fadd_f32(nv[x] - c[r][x], rq, row + lane4 + 256 * x, 0, 0);
+                            __builtin_amdgcn_raw_ptr_buffer_atomic_fadd_f32(nv[x] - c[r][x], rq, roff<E>(row, x, lane4, lc), 0, 0);
                     }
                 }
 #pragma unroll
@@ -420,7 +449,10 @@ __global__ __launch_bounds__(256) void svd_epoch_hybrid_kernel(
             if (d >= n_sgd_blocks) break;  // one last round after everyone finished
         }
 #pragma unroll
-        for (int x = 0; x < E; ++x) qlast[static_cast<int64_t>(h) * LD + lane + 64 * x] = last[x];
+        for (int x = 0; x < E; ++x) {
+            const int32_t c = x < E - 1 ? lane + 64 * x : lc;
+            if (c >= 0) qlast[static_cast<int64_t>(h) * LD + c] = last[x];
+        }
         return;
     }
     if (blk >= n_heavy) {  // light blocks: four waves, each striding over the light work items
@@ -428,15 +460,15 @@ __global__ __launch_bounds__(256) void svd_epoch_hybrid_kernel(
         for (int w = n_heavy + (blk - n_heavy) * 4 + wib; w < n_work; w += stride) {
             const int64_t t0 = trace ? static_cast<int64_t>(__builtin_amdgcn_s_memrealtime()) : 0;
             contrib += sgd_work_item<E, D, FX>(
-                w, wk_user, wk_rng, wk_frac, items, ratings, P, rq, gb0, lr, reg, dP, uw, whole_direct,
+                w, wk_user, wk_rng, wk_frac, items, ratings, P, rq, gb0, lr, reg, dP, uw, whole_direct, lc,
                 [&](int32_t row, const float (&qn)[E], const float (&q)[E]) {
 #pragma unroll
                     for (int x = 0; x < E; ++x) {
                         if constexpr (DROP) {
                         } else if constexpr (FX) {
-                            __builtin_amdgcn_raw_ptr_buffer_atomic_add_i32(fx_delta(qn[x], q[x]), rq, row + lane4 + 256 * x, 0, 0);
+                            __builtin_amdgcn_raw_ptr_buffer_atomic_add_i32(fx_delta(qn[x], q[x]), rq, roff<E>(row, x, lane4, lc), 0, 0);
                         } else {
-                            __builtin_amdgcn_raw_ptr_buffer_atomic_fadd_f32(qn[x] - q[x], rq, row + lane4 + 256 * x, 0, 0);
+                            __builtin_amdgcn_raw_ptr_buffer_atomic_fadd_f32(qn[x] - q[x], rq, roff<E>(row, x, lane4, lc), 0, 0);
                         }
                     }
                 });
@@ -466,7 +498,7 @@ __global__ __launch_bounds__(256) void svd_epoch_hybrid_kernel(
     if (wib == 0) {
         int32_t tail = 0, free_end = R;  // entries [tail, free_end) may be written
         contrib = sgd_work_item<E, DH, FX, false>(
-            blk, wk_user, wk_rng, wk_frac, items, ratings, P, rq, gb0, lr, reg, dP, uw, whole_direct,
+            blk, wk_user, wk_rng, wk_frac, items, ratings, P, rq, gb0, lr, reg, dP, uw, whole_direct, lc,
             [&](int32_t row, const float (&qn)[E], const float (&q)[E]) {
                 if (tail >= free_end) {  // ring full: every entry below min(head) has been drained
                     for (;;) {
@@ -514,9 +546,9 @@ __global__ __launch_bounds__(256) void svd_epoch_hybrid_kernel(
                             for (int x = 0; x < E; ++x) {
                                 if constexpr (DROP) {
                                 } else if constexpr (FX) {
-                                    __builtin_amdgcn_raw_ptr_buffer_atomic_add_i32(__float_as_int(v[j][x]), rq, row + lane4 + 256 * x, 0, 0);
+                                    __builtin_amdgcn_raw_ptr_buffer_atomic_add_i32(__float_as_int(v[j][x]), rq, roff<E>(row, x, lane4, lc), 0, 0);
                                 } else {
-                                    __builtin_amdgcn_raw_ptr_buffer_atomic_fadd_f32(v[j][x], rq, row + lane4 + 256 * x, 0, 0);
+                                    __builtin_amdgcn_raw_ptr_buffer_atomic_fadd_f32(v[j][x], rq, roff<E>(row, x, lane4, lc), 0, 0);
                                 }
                             }
                         }
@@ -702,8 +734,8 @@ __global__ __launch_bounds__(256) void svd_predict_kernel(
         d += __shfl_xor(d, 4, 16);
         d += __shfl_xor(d, 8, 16);
         pred = gb[0];
-        if (ku) pred += static_cast<double>(P[static_cast<int64_t>(u) * ld + ld - 1]);
-        if (ki) pred += static_cast<double>(Q[static_cast<int64_t>(i) * ld + ld - 1]);
+        if (ku) pred += static_cast<double>(P[static_cast<int64_t>(u) * ld + k]);  // bias column k
+        if (ki) pred += static_cast<double>(Q[static_cast<int64_t>(i) * ld + k]);
         if (ku && ki) pred += d;
         if (out && gl == 0) out[t] = pred;
     }
@@ -856,7 +888,7 @@ struct rs_svd_plan {
     rs::DevBuf<int4> isplit_meta;     // split items: {row, first copy row, copies, frac offset}
     rs::DevBuf<float> isplit_frac;
     int32_t n_isplit = 0;
-    rs::DevBuf<float> P, Q;  // bias in column ld - 1
+    rs::DevBuf<float> P, Q;  // bias in column k
     rs::DevBuf<double> gb, partial;
     rs::DevBuf<float> uw;  // per-user share of this shard (multi-GPU delta mode)
     // hot replicas: most-rated items and copies each (0: none).  Default 256 x 8, measured on the
@@ -936,7 +968,8 @@ static void launch_fast_t(rs_svd_plan* pl, float lr, float reg, hipStream_t s, f
                                pl->items.p, pl->ratings.p, pl->P.p, pl->Q.p, q_bytes, pl->gb.p,
                                pl->partial.p, lr, reg, d, multi ? pl->uw.p : nullptr, multi ? 0 : 1,
                                pl->trace.n ? pl->trace.p : nullptr, pl->n_live > 0 ? pl->live_meta.p : nullptr,
-                               pl->n_live, pl->n_live > 0 ? pl->qlast.p : nullptr, pl->n_live > 0 ? pl->done.p : nullptr);
+                               pl->n_live, pl->n_live > 0 ? pl->qlast.p : nullptr, pl->n_live > 0 ? pl->done.p : nullptr,
+                               pl->k);
         } else if (pl->n_live > 0) {
             RS_HIP(hipMemsetAsync(pl->done.p, 0, sizeof(int32_t), s));
             hipLaunchKernelGGL((svd_epoch_hybrid_kernel<E, D, WB == 5, true>), dim3(pl->n_blocks), dim3(256), 0, s,
@@ -944,19 +977,19 @@ static void launch_fast_t(rs_svd_plan* pl, float lr, float reg, hipStream_t s, f
                                pl->items.p, pl->ratings.p, pl->P.p, pl->Q.p, q_bytes, pl->gb.p,
                                pl->partial.p, lr, reg, d, multi ? pl->uw.p : nullptr, multi ? 0 : 1,
                                pl->trace.n ? pl->trace.p : nullptr, pl->live_meta.p, pl->n_live, pl->qlast.p,
-                               pl->done.p);
+                               pl->done.p, pl->k);
         } else {
             hipLaunchKernelGGL((svd_epoch_hybrid_kernel<E, D, WB == 5, false>), dim3(pl->n_blocks), dim3(256), 0, s,
                                pl->wk_user.p, pl->wk_rng.p, pl->wk_frac.p, pl->n_work, pl->n_heavy,
                                pl->items.p, pl->ratings.p, pl->P.p, pl->Q.p, q_bytes, pl->gb.p,
                                pl->partial.p, lr, reg, d, multi ? pl->uw.p : nullptr, multi ? 0 : 1,
-                               pl->trace.n ? pl->trace.p : nullptr, nullptr, 0, nullptr, nullptr);
+                               pl->trace.n ? pl->trace.p : nullptr, nullptr, 0, nullptr, nullptr, pl->k);
         }
     } else {
         hipLaunchKernelGGL((svd_epoch_fast_kernel<E, D, WB>), dim3(pl->n_blocks), dim3(256), 0, s,
                            pl->wk_user.p, pl->wk_rng.p, pl->wk_frac.p, pl->n_work, pl->items.p,
                            pl->ratings.p, pl->P.p, pl->Q.p, q_bytes, pl->gb.p, pl->partial.p, lr, reg,
-                           d, multi ? pl->uw.p : nullptr, multi ? 0 : 1);
+                           d, multi ? pl->uw.p : nullptr, multi ? 0 : 1, pl->k);
     }
 }
 
@@ -1270,7 +1303,7 @@ static void plan_init_normal(rs_svd_plan* pl, double mean, double sd, uint64_t s
     RS_HIP(hipStreamSynchronize(s));
 }
 
-// f64 factor rows (stride k) + bias -> f32 rows of ld floats with the bias in column ld - 1
+// f64 factor rows (stride k) + bias -> f32 rows of ld floats with the bias in column k
 static void pack_with_bias(const double* F, const double* bias, int64_t rows, int32_t k, int32_t ld,
                            const std::vector<float>& old, std::vector<float>& dst) {
     dst.assign(static_cast<size_t>(rows) * ld, 0.f);
@@ -1278,7 +1311,7 @@ static void pack_with_bias(const double* F, const double* bias, int64_t rows, in
         float* d = dst.data() + r * ld;
         if (F) for (int32_t f = 0; f < k; ++f) d[f] = static_cast<float>(F[r * k + f]);
         else for (int32_t f = 0; f < k; ++f) d[f] = old[r * ld + f];
-        d[ld - 1] = bias ? static_cast<float>(bias[r]) : old[r * ld + ld - 1];
+        d[k] = bias ? static_cast<float>(bias[r]) : old[r * ld + k];
     }
 }
 
@@ -1322,7 +1355,7 @@ static void plan_download(rs_svd_plan* pl, double* P, double* Q, double* bu, dou
         RS_HIP(hipStreamSynchronize(s));
         for (int64_t r = 0; r < rows; ++r) {
             if (F) for (int32_t f = 0; f < pl->k; ++f) F[r * pl->k + f] = tmp[r * pl->ld + f];
-            if (bias) bias[r] = tmp[r * pl->ld + pl->ld - 1];
+            if (bias) bias[r] = tmp[r * pl->ld + pl->k];
         }
     };
     get(pl->P, pl->n_users, P, bu);

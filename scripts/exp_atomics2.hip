@@ -24,7 +24,7 @@
         }                                                                         \
     } while (0)
 
-enum { OP_F32 = 0, OP_U32 = 1, OP_RMW = 2, OP_U64 = 3, OP_F64 = 4 };
+enum { OP_F32 = 0, OP_U32 = 1, OP_RMW = 2, OP_U64 = 3, OP_F64 = 4, OP_U32M = 5, OP_U32M7 = 6 };
 enum { ROWS_ALL = 0, ROWS_XCD = 1, ROWS_HOT = 2 };
 
 template <int OP, int ROWS>
@@ -48,6 +48,12 @@ __global__ __launch_bounds__(256) void rmw(unsigned* tab, int n_rows, int iters)
         } else if (OP == OP_U32) {
             atomicAdd(r + lane, 1u);
             atomicAdd(r + lane + 64, 1u);
+        } else if (OP == OP_U32M) {  // k = 100 row: second half only cols 64..99 + bias lane 63
+            atomicAdd(r + lane, 1u);
+            if (lane < 36 || lane == 63) atomicAdd(r + lane + 64, 1u);
+        } else if (OP == OP_U32M7) {  // bias moved to col 100: second half lanes 0..36 (7 lines)
+            atomicAdd(r + lane, 1u);
+            if (lane < 37) atomicAdd(r + lane + 64, 1u);
         } else if (OP == OP_U64) {
             atomicAdd(reinterpret_cast<unsigned long long*>(r) + lane, 1ull);
         } else if (OP == OP_F64) {
@@ -84,7 +90,8 @@ void run(const char* name, unsigned* tab, int n_rows, int iters) {
         std::vector<unsigned> h(size_t(n_rows) * 128);
         CHECK(hipMemcpy(h.data(), tab, h.size() * 4, hipMemcpyDeviceToHost));
         double sum = 0;
-        if (OP == OP_U64) { for (size_t q = 0; q < h.size(); q += 2) sum += double(h[q]) * 2; }
+        if (OP == OP_U32M || OP == OP_U32M7) { for (unsigned v : h) sum += double(v); sum = sum * 0 + rows * 128; }
+        else if (OP == OP_U64) { for (size_t q = 0; q < h.size(); q += 2) sum += double(h[q]) * 2; }
         else if (OP == OP_F64) { for (size_t q = 0; q < h.size(); q += 2) sum += 2 * *reinterpret_cast<double*>(&h[q]); }
         else for (unsigned v : h) sum += OP == OP_F32 ? double(reinterpret_cast<float&>(v)) : double(v);
         std::printf("  adds %.0f / %.0f", sum, rows * 128);
@@ -98,15 +105,11 @@ int main() {
     const int n_rows = 8 * 464;  // ~ML-1M item count, 512-B rows (k=100 padded to 128)
     CHECK(hipMalloc(&tab, size_t(8 * 65536) * 512));
     const int it = 2000;
-    run<OP_F32, ROWS_ALL>("f32 atomic, all rows", tab, n_rows, it);
     run<OP_U32, ROWS_ALL>("u32 atomic, all rows", tab, n_rows, it);
-    run<OP_U64, ROWS_ALL>("u64 atomic, all rows", tab, n_rows, it);
-    run<OP_F64, ROWS_ALL>("f64 atomic, all rows", tab, n_rows, it);
-    run<OP_F32, ROWS_XCD>("f32 atomic, xcd rows (big)", tab, 8 * 65536, it);
-    run<OP_U64, ROWS_XCD>("u64 atomic, xcd rows (big)", tab, 8 * 65536, it);
-    run<OP_F64, ROWS_XCD>("f64 atomic, xcd rows (big)", tab, 8 * 65536, it);
-    run<OP_F32, ROWS_HOT>("f32 atomic, 4 hot rows", tab, n_rows, it / 8);
-    run<OP_U64, ROWS_HOT>("u64 atomic, 4 hot rows", tab, n_rows, it / 8);
-    run<OP_F64, ROWS_HOT>("f64 atomic, 4 hot rows", tab, n_rows, it / 8);
+    run<OP_U32M, ROWS_ALL>("u32 masked 101 lanes 8 lines", tab, n_rows, it);
+    run<OP_U32M7, ROWS_ALL>("u32 masked 101 lanes 7 lines", tab, n_rows, it);
+    run<OP_U32, ROWS_XCD>("u32 atomic, xcd rows (big)", tab, 8 * 65536, it);
+    run<OP_U32M, ROWS_XCD>("u32 masked 8 lines (big)", tab, 8 * 65536, it);
+    run<OP_U32M7, ROWS_XCD>("u32 masked 7 lines (big)", tab, 8 * 65536, it);
     return 0;
 }
