@@ -164,12 +164,12 @@ def main():
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
                          "traffic": traffic,
-                         "kernel": "svd_epoch_hybrid_kernel<E=2,D=8,merge,fixed-point> + 2 in-place Q conversions "
-                                   "(hot replicas 256x8, users split at 1200)",
+                         "kernel": "svd_epoch_hybrid_kernel<E=2,D=8,merge,fixed-point> "
+                                   "(hot replicas 256x8, users split at 1200, 7-line rows)",
                          "avg_kernel_us": avg_kernel_s * 1e6,
-                         "timed_span": "HIP events around the epoch's kernels on the launch stream: the "
-                                       "hybrid SGD kernel plus its Q fixed-point conversions and live-replica "
-                                       "merge rounds (rocprofv3 lists them separately, profiles/)",
+                         "timed_span": "HIP events around each epoch's SGD kernel on the launch stream "
+                                       "(the per-epoch epilogue and the per-call Q fixed-point conversions "
+                                       "are outside it but inside `value`; rocprofv3 lists them, profiles/)",
                          "algorithmic_bytes_per_launch": ab},
             "finite": finite,
         }

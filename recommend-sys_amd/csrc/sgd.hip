@@ -664,6 +664,55 @@ __global__ __launch_bounds__(64) void svd_live_merge_fx_kernel(int32_t* __restri
     }
 }
 
+// After each epoch of a fixed-point run (plan_epochs keeps Q in int32 across its epochs), one launch
+// does what three did: blocks [0, n_live) the live items' final integer merge round (as
+// svd_live_merge_fx_kernel: N = L + sum_r (c_r - L) to every copy, L := N), blocks
+// [n_live, n_live + n_split) the split users' row merges (as svd_merge_rows_kernel), and the last
+// block the GlobalBias fold (as gb_fold_kernel, the same 256-thread tree) plus re-arming the
+// merger's done counter for the next epoch.  Columns are independent, so the arithmetic is theirs.
+__global__ __launch_bounds__(256) void svd_epoch_epilogue_kernel(
+    int32_t* __restrict__ Q, const int4* __restrict__ meta, int32_t* __restrict__ qlast, int32_t n_live,
+    float* __restrict__ P, float* __restrict__ dP, const int32_t* __restrict__ rows, int32_t n_split,
+    int32_t ld, const double* __restrict__ partial, int64_t n_partial, double* __restrict__ gb,
+    double inv_nnz, int32_t* __restrict__ done) {
+    const int b = static_cast<int>(blockIdx.x);
+    const int tid = static_cast<int>(threadIdx.x);
+    if (b < n_live) {
+        const int4 m = meta[b];
+        auto row = [&](int32_t c) { return static_cast<int64_t>(c == 0 ? m.x : m.y + c - 1) * ld; };
+        int32_t* L = qlast + static_cast<int64_t>(b) * ld;
+        for (int32_t col = tid; col < ld; col += 256) {
+            const uint32_t l = static_cast<uint32_t>(L[col]);
+            uint32_t v = l;
+            for (int32_t c = 0; c < m.z; ++c) v += static_cast<uint32_t>(Q[row(c) + col]) - l;
+            for (int32_t c = 0; c < m.z; ++c) Q[row(c) + col] = static_cast<int32_t>(v);
+            L[col] = static_cast<int32_t>(v);
+        }
+        return;
+    }
+    if (b < n_live + n_split) {
+        const int64_t r = static_cast<int64_t>(rows[b - n_live]) * ld;
+        for (int32_t c = tid; c < ld; c += 256) {
+            P[r + c] += dP[r + c];
+            dP[r + c] = 0.f;
+        }
+        return;
+    }
+    __shared__ double sh[256];
+    double t = 0.0;
+    for (int64_t x = tid; x < n_partial; x += 256) t += partial[x];
+    sh[tid] = t;
+    __syncthreads();
+    for (int w = 128; w > 0; w >>= 1) {
+        if (tid < w) sh[tid] += sh[tid + w];
+        __syncthreads();
+    }
+    if (tid == 0) {
+        gb[0] += sh[0] * inv_nnz;
+        if (done) *done = 0;
+    }
+}
+
 // Multi-GPU: the all-reduced weighted user deltas and global-bias sum are applied in place.
 __global__ __launch_bounds__(256) void svd_apply_delta_kernel(float4* __restrict__ P,
                                                               const float4* __restrict__ dP, int64_t n4,
@@ -909,6 +958,7 @@ struct rs_svd_plan {
     int32_t ring_depth = 8;
     int32_t fixed_q = 1;           // hybrid epochs keep Q as int32 fixed point (rs_svd_plan_set_fixed_q)
     bool live_merged = false;      // the fixed-point epoch already ran the live items' final round
+    bool hoisted = false;          // plan_epochs: Q stays int32 across epochs, the epilogue re-arms done
     double mean_rating = 0.0;  // of the plan's ratings (FAST GlobalBias warm start at init)
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
     double last_ms = 0.0;
@@ -960,7 +1010,7 @@ static void launch_fast_t(rs_svd_plan* pl, float lr, float reg, hipStream_t s, f
     pl->n_blocks = fast_blocks(pl);
     if constexpr (WB == 2 || WB == 5) {
         if (WB == 2 && pl->fixed_q) {
-            if (pl->n_live > 0) RS_HIP(hipMemsetAsync(pl->done.p, 0, sizeof(int32_t), s));
+            if (pl->n_live > 0 && !pl->hoisted) RS_HIP(hipMemsetAsync(pl->done.p, 0, sizeof(int32_t), s));
             auto kern = pl->n_live > 0 ? svd_epoch_hybrid_kernel<E, D, false, true, true>
                                        : svd_epoch_hybrid_kernel<E, D, false, false, true>;
             hipLaunchKernelGGL(kern, dim3(pl->n_blocks), dim3(256), 0, s,
@@ -1017,6 +1067,11 @@ static void launch_fast_d(rs_svd_plan* pl, float lr, float reg, hipStream_t s, f
 }
 
 static void launch_fast(rs_svd_plan* pl, float lr, float reg, hipStream_t s, float* dP = nullptr) {
+    if (pl->hoisted) {  // plan_epochs does the conversions and the epilogue around its epoch loop
+        launch_fast_d<2>(pl, lr, reg, s, dP);
+        RS_HIP(hipGetLastError());
+        return;
+    }
     const bool fx = pl->fixed_q && pl->write_back == RS_SGD_WB_ATOMIC;
     const int64_t qn = static_cast<int64_t>(pl->Q.n);
     const int fx_blocks = static_cast<int>(std::min<int64_t>(2048, (qn + 255) / 256));
@@ -1377,6 +1432,45 @@ static void plan_epochs(rs_svd_plan* pl, int32_t epochs, float lr, float reg, hi
         pl->tev_used = 2 * epochs;
     }
     RS_HIP(hipEventRecord(pl->ev0, s));
+    // Fixed-point runs without item splitting keep Q in int32 for all their epochs: one conversion
+    // each way per call, and per epoch the SGD kernel plus one epilogue launch (merge rounds, split
+    // rows, GlobalBias fold) instead of six small launches.
+    const bool hoist = pl->fixed_q && pl->write_back == RS_SGD_WB_ATOMIC && pl->n_isplit == 0 && epochs > 0;
+    const int64_t qn = static_cast<int64_t>(pl->Q.n);
+    const int fx_blocks = static_cast<int>(std::min<int64_t>(2048, (qn + 255) / 256));
+    if (hoist) {
+        hipLaunchKernelGGL(svd_q_fixed_kernel, dim3(fx_blocks), dim3(256), 0, s, pl->Q.p, qn, 1);
+        if (pl->n_live > 0) {
+            hipLaunchKernelGGL(svd_live_merge_kernel, dim3(pl->n_live), dim3(64), 0, s, pl->Q.p, pl->live_meta.p,
+                               pl->qlast.p, pl->ld, 0);
+            RS_HIP(hipMemsetAsync(pl->done.p, 0, sizeof(int32_t), s));
+        }
+        struct HoistScope {  // launch_fast sees the hoisted state only inside this loop, even on a throw
+            rs_svd_plan* p;
+            ~HoistScope() { p->hoisted = false; }
+        } scope{pl};
+        pl->hoisted = true;
+        for (int32_t e = 0; e < epochs; ++e) {
+            if (pl->timing) RS_HIP(hipEventRecord(pl->tev[2 * e], s));
+            launch_fast(pl, lr, reg, s);
+            if (pl->timing) RS_HIP(hipEventRecord(pl->tev[2 * e + 1], s));
+            hipLaunchKernelGGL(svd_epoch_epilogue_kernel, dim3(pl->n_live + pl->n_split + 1), dim3(256), 0, s,
+                               reinterpret_cast<int32_t*>(pl->Q.p), pl->live_meta.p,
+                               reinterpret_cast<int32_t*>(pl->qlast.p), pl->n_live, pl->P.p, pl->dPs.p,
+                               pl->split_rows.p, pl->n_split, pl->ld, pl->partial.p,
+                               static_cast<int64_t>(pl->n_blocks), pl->gb.p, inv_nnz,
+                               pl->n_live > 0 ? pl->done.p : nullptr);
+            RS_HIP(hipGetLastError());
+        }
+        pl->hoisted = false;
+        hipLaunchKernelGGL(svd_q_fixed_kernel, dim3(fx_blocks), dim3(256), 0, s, pl->Q.p, qn, 0);
+        RS_HIP(hipGetLastError());
+        RS_HIP(hipEventRecord(pl->ev1, s));
+        pl->last_launches = pl->timing ? epochs : 2 * epochs;  // SGD + epilogue (conversions in the span)
+        pl->last_stream = s;
+        pl->last_ms = -1.0;
+        return;
+    }
     for (int32_t e = 0; e < epochs; ++e) {
         if (pl->timing) RS_HIP(hipEventRecord(pl->tev[2 * e], s));
         launch_fast(pl, lr, reg, s);
