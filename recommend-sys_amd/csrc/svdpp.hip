@@ -15,13 +15,17 @@
 //          memory side as float atomics (cross-XCD coherent, no lost updates), like K1.
 //
 // FAST device layout: P, Q, Y are (rows x ld) float32, ld = 64 ceil((k + 1) / 64); the bias (b_u in
-// P, b_i in Q) sits in column ld - 1, Y's column ld - 1 stays 0.
+// P, b_i in Q) sits in column k, right after the factors (lane 63 of the last register), Y's column k
+// stays 0.  Padding lanes of the last register (columns > k) are never loaded or written, and Y rows
+// skip lane 63 as well, so whole 64-B lines past the row get no request: the memory-side atomic unit
+// prices a row update per line (K1, scripts/exp_atomics2.hip).  k = 128: Q rows 9 lines of 12, Y 8.
 // Algorithmic bytes per epoch: nnz*(16 + 8k) + U*(16 + 8k) + nnz*(4 + 12k).
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
 #include <cmath>
 #include <cstdlib>
+#include <cstring>
 #include <vector>
 
 #include "common.hpp"
@@ -40,6 +44,35 @@ __device__ __forceinline__ float pp_wave_sum(float x) {
     return __uint_as_float(r32[0]) + __uint_as_float(r32[1]);
 }
 
+// column of this lane's last register (E - 1), or -1: lane 63 holds the bias (column kf) in P and Q
+// rows; Y rows have no bias, so there lane 63 is padding too
+template <int E>
+__device__ __forceinline__ int32_t pp_last_col(int lane, int32_t kf, bool bias) {
+    if (lane == 63) return bias ? kf : -1;
+    const int32_t c = lane + 64 * (E - 1);
+    return c < kf ? c : -1;
+}
+template <int E>
+__device__ __forceinline__ int32_t pp_roff(int32_t row, int x, int32_t lane4, int32_t lc) {
+    return x < E - 1 ? row + lane4 + 256 * x : (lc >= 0 ? row + 4 * lc : kPPOut);
+}
+
+// Fixed-point Q and Y (FX, the default; RSGPU_PP_FX=0 keeps fp32): the FAST fit packs Q and Y as
+// int32 round(v * 2^24) on the host and unpacks them after the last epoch; loads convert to fp32 and
+// the q_i / y_j deltas become integer atomics (memory-side u32 adds at 1.69 TB/s against 1.32 for
+// f32, K1).  Resolution 2^-24 (the fp32 ulp at |v| in [0.5, 1)), |v| < 128.
+constexpr float kPPFx = 16777216.f, kPPFxInv = 1.f / 16777216.f;
+__device__ __forceinline__ float pp_ld(uint32_t bits, bool fx) {
+    return fx ? static_cast<float>(static_cast<int32_t>(bits)) * kPPFxInv : __uint_as_float(bits);
+}
+template <bool FX>
+__device__ __forceinline__ void pp_atomic_add(float d, __amdgpu_buffer_rsrc_t r, int32_t off) {
+    if constexpr (FX)
+        __builtin_amdgcn_raw_ptr_buffer_atomic_add_i32(__float2int_rn(d * kPPFx), r, off, 0, 0);
+    else
+        __builtin_amdgcn_raw_ptr_buffer_atomic_fadd_f32(d, r, off, 0, 0);
+}
+
 __device__ __forceinline__ float pp_lane63(float x) {
     return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(x), 63));
 }
@@ -49,10 +82,10 @@ __device__ __forceinline__ float pp_lane63(float x) {
 
 // Pass 1 of one user over the y rows j = b + first, b + first + step, ... (batches of YB rows):
 // the sum of the y_j (svd.go:276-278) in that order.
-template <int E, int YB>
+template <int E, int YB, bool FX>
 __device__ __forceinline__ void pp_sum_y(__amdgpu_buffer_rsrc_t ry, const int32_t* __restrict__ items,
                                          int64_t b, int64_t e, int32_t first, int32_t step, int32_t lane4,
-                                         float (&S0)[E]) {
+                                         int32_t lcy, float (&S0)[E]) {
     constexpr int LD = 64 * E;
 #pragma unroll
     for (int x = 0; x < E; ++x) S0[x] = 0.f;
@@ -64,7 +97,7 @@ __device__ __forceinline__ void pp_sum_y(__amdgpu_buffer_rsrc_t ry, const int32_
             const int32_t row = j < rem ? items[base + j] * (LD * 4) : kPPOut;
 #pragma unroll
             for (int x = 0; x < E; ++x)
-                yv[j][x] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(ry, row + lane4 + 256 * x, 0, kPPAux));
+                yv[j][x] = pp_ld(__builtin_amdgcn_raw_buffer_load_b32(ry, pp_roff<E>(row, x, lane4, lcy), 0, kPPAux), FX);
         }
 #pragma unroll
         for (int j = 0; j < YB; ++j)
@@ -74,10 +107,10 @@ __device__ __forceinline__ void pp_sum_y(__amdgpu_buffer_rsrc_t ry, const int32_
 }
 
 // Pass 3 over the same row subset: y_j += (A - 1) y_j - C (the deferred svd.go:399-422), atomics.
-template <int E, int YB>
+template <int E, int YB, bool FX>
 __device__ __forceinline__ void pp_update_y(__amdgpu_buffer_rsrc_t ry, const int32_t* __restrict__ items,
                                             int64_t b, int64_t e, int32_t first, int32_t step,
-                                            int32_t lane4, float am1, const float (&Cv)[E]) {
+                                            int32_t lane4, int32_t lcy, float am1, const float (&Cv)[E]) {
     constexpr int LD = 64 * E;
     for (int64_t base = b + first; base < e; base += step) {
         const int32_t rem = static_cast<int32_t>(e - base);
@@ -88,24 +121,23 @@ __device__ __forceinline__ void pp_update_y(__amdgpu_buffer_rsrc_t ry, const int
             rows[j] = j < rem ? items[base + j] * (LD * 4) : kPPOut;
 #pragma unroll
             for (int x = 0; x < E; ++x)
-                yv[j][x] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(ry, rows[j] + lane4 + 256 * x, 0, kPPAux));
+                yv[j][x] = pp_ld(__builtin_amdgcn_raw_buffer_load_b32(ry, pp_roff<E>(rows[j], x, lane4, lcy), 0, kPPAux), FX);
         }
 #pragma unroll
         for (int j = 0; j < YB; ++j)
 #pragma unroll
             for (int x = 0; x < E; ++x)
-                __builtin_amdgcn_raw_ptr_buffer_atomic_fadd_f32(__builtin_fmaf(am1, yv[j][x], -Cv[x]), ry,
-                                                               rows[j] + lane4 + 256 * x, 0, 0);
+                pp_atomic_add<FX>(__builtin_fmaf(am1, yv[j][x], -Cv[x]), ry, pp_roff<E>(rows[j], x, lane4, lcy));
     }
 }
 
 // Pass 2 of one user: the ratings in data order with the lazy y state (S0, A, Cv).  Every q_i update
 // is handed to emit(row byte offset, q_new, q_old).  Returns with p (bias in lane 63), ub, gb, A, Cv
 // advanced.
-template <int E, int D, class Emit>
+template <int E, int D, bool FX, class Emit>
 __device__ __forceinline__ void pp_chain(__amdgpu_buffer_rsrc_t rq, const int32_t* __restrict__ items,
                                          const float* __restrict__ ratings, int64_t b, int64_t e,
-                                         int32_t lane, float lr, float a, const float (&S0)[E], float (&p)[E],
+                                         int32_t lane, int32_t lcq, float lr, float a, const float (&S0)[E], float (&p)[E],
                                          float& ub, float& gb, float& A, float (&Cv)[E], Emit&& emit) {
 #pragma clang fp contract(fast)
     constexpr int LD = 64 * E, B = 16;
@@ -119,7 +151,7 @@ __device__ __forceinline__ void pp_chain(__amdgpu_buffer_rsrc_t rq, const int32_
         const int32_t row = valid ? item * (LD * 4) : kPPOut;
 #pragma unroll
         for (int x = 0; x < E; ++x)
-            q[x] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rq, row + lane4 + 256 * x, 0, kPPAux));
+            q[x] = pp_ld(__builtin_amdgcn_raw_buffer_load_b32(rq, pp_roff<E>(row, x, lane4, lcq), 0, kPPAux), FX);
     };
     int32_t it_cur[B], it_nxt[B];
 #pragma unroll
@@ -197,12 +229,12 @@ __device__ __forceinline__ void pp_lds_store(int32_t* p, int32_t v) {
     __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
 }
 
-template <int E, int D>
+template <int E, int D, bool FX>
 __global__ __launch_bounds__(256) void svdpp_epoch_fast_kernel(
     const int32_t* __restrict__ work, int32_t n_work, int32_t n_heavy, const int64_t* __restrict__ rowptr,
     const int32_t* __restrict__ items, const float* __restrict__ ratings, float* __restrict__ P,
     float* Q, float* Y, int32_t row_bytes_q, int32_t row_bytes_y, const double* __restrict__ gb_in,
-    double* __restrict__ gb_partial, float lr, float reg) {
+    double* __restrict__ gb_partial, float lr, float reg, int32_t kf) {
 #pragma clang fp contract(fast)
     constexpr int LD = 64 * E;
     constexpr int YB = 8;  // y rows per pass-1/3 batch (24 was measured to break the FAST RMSE on ML-100K)
@@ -220,6 +252,8 @@ __global__ __launch_bounds__(256) void svdpp_epoch_fast_kernel(
     const __amdgpu_buffer_rsrc_t rq = __builtin_amdgcn_make_buffer_rsrc(Q, 0, row_bytes_q, 0x00020000);
     const __amdgpu_buffer_rsrc_t ry = __builtin_amdgcn_make_buffer_rsrc(Y, 0, row_bytes_y, 0x00020000);
     const int32_t lane4 = lane * 4;
+    const int32_t lcq = pp_last_col<E>(lane, kf, true), lcy = pp_last_col<E>(lane, kf, false);
+    auto pcol = [&](int x) { return x < E - 1 ? lane + 64 * x : lcq; };  // P row column, or -1
     const float a = 1.f - lr * reg;
     const int blk = static_cast<int>(blockIdx.x);
     double contrib = 0.0;
@@ -232,22 +266,23 @@ __global__ __launch_bounds__(256) void svdpp_epoch_fast_kernel(
             float p[E];
             float* prow = P + static_cast<int64_t>(u) * LD;
 #pragma unroll
-            for (int x = 0; x < E; ++x) p[x] = prow[lane + 64 * x];
+            for (int x = 0; x < E; ++x) p[x] = pcol(x) >= 0 ? prow[pcol(x)] : 0.f;
             float ub = pp_lane63(p[E - 1]);
             float gb = gb0, A = 1.f;
             float S0[E], Cv[E];
-            pp_sum_y<E, YB>(ry, items, b, e, 0, YB, lane4, S0);
+            pp_sum_y<E, YB, FX>(ry, items, b, e, 0, YB, lane4, lcy, S0);
 #pragma unroll
             for (int x = 0; x < E; ++x) Cv[x] = 0.f;
-            pp_chain<E, 8>(rq, items, ratings, b, e, lane, lr, a, S0, p, ub, gb, A, Cv,
-                           [&](int32_t row, const float (&qw)[E], const float (&q)[E]) {
+            pp_chain<E, 8, FX>(rq, items, ratings, b, e, lane, lcq, lr, a, S0, p, ub, gb, A, Cv,
+                               [&](int32_t row, const float (&qw)[E], const float (&q)[E]) {
 #pragma unroll
-                               for (int x = 0; x < E; ++x)
-                                   __builtin_amdgcn_raw_ptr_buffer_atomic_fadd_f32(qw[x] - q[x], rq, row + lane4 + 256 * x, 0, 0);
-                           });
-            pp_update_y<E, YB>(ry, items, b, e, 0, YB, lane4, A - 1.f, Cv);
+                                   for (int x = 0; x < E; ++x)
+                                       pp_atomic_add<FX>(qw[x] - q[x], rq, pp_roff<E>(row, x, lane4, lcq));
+                               });
+            pp_update_y<E, YB, FX>(ry, items, b, e, 0, YB, lane4, lcy, A - 1.f, Cv);
 #pragma unroll
-            for (int x = 0; x < E; ++x) prow[lane + 64 * x] = p[x];
+            for (int x = 0; x < E; ++x)
+                if (pcol(x) >= 0) prow[pcol(x)] = p[x];
             contrib += static_cast<double>(e - b) * (static_cast<double>(gb) - static_cast<double>(gb0));
         }
         if (lane == 0) s_contrib[wib] = contrib;
@@ -268,7 +303,7 @@ __global__ __launch_bounds__(256) void svdpp_epoch_fast_kernel(
     // pass 1 split over the four waves, the partial sums added in wave order (identical everywhere)
     {
         float S0w[E];
-        pp_sum_y<E, YB>(ry, items, b, e, wib * YB, 4 * YB, lane4, S0w);
+        pp_sum_y<E, YB, FX>(ry, items, b, e, wib * YB, 4 * YB, lane4, lcy, S0w);
 #pragma unroll
         for (int x = 0; x < E; ++x) s_red[wib][lane + 64 * x] = S0w[x];
     }
@@ -284,11 +319,11 @@ __global__ __launch_bounds__(256) void svdpp_epoch_fast_kernel(
                     s_red[3][lane + 64 * x];
         float* prow = P + static_cast<int64_t>(u) * LD;
 #pragma unroll
-        for (int x = 0; x < E; ++x) p[x] = prow[lane + 64 * x];
+        for (int x = 0; x < E; ++x) p[x] = pcol(x) >= 0 ? prow[pcol(x)] : 0.f;
         float ub = pp_lane63(p[E - 1]);
         float gb = gb0, A = 1.f;
         int32_t tail = 0, free_end = R;
-        pp_chain<E, DH>(rq, items, ratings, b, e, lane, lr, a, S0, p, ub, gb, A, Cv,
+        pp_chain<E, DH, FX>(rq, items, ratings, b, e, lane, lcq, lr, a, S0, p, ub, gb, A, Cv,
                         [&](int32_t row, const float (&qw)[E], const float (&q)[E]) {
                             if (tail >= free_end) {  // ring full: wait for the writers
                                 for (;;) {
@@ -309,7 +344,7 @@ __global__ __launch_bounds__(256) void svdpp_epoch_fast_kernel(
                         });
 #pragma unroll
         for (int x = 0; x < E; ++x) {
-            prow[lane + 64 * x] = p[x];
+            if (pcol(x) >= 0) prow[pcol(x)] = p[x];
             s_red[0][lane + 64 * x] = Cv[x];  // pass 3 reads C and A from LDS
         }
         if (lane == 0) s_A = A;
@@ -339,7 +374,7 @@ __global__ __launch_bounds__(256) void svdpp_epoch_fast_kernel(
                             const int32_t row = __builtin_amdgcn_readlane(myrow, j);
 #pragma unroll
                             for (int x = 0; x < E; ++x)
-                                __builtin_amdgcn_raw_ptr_buffer_atomic_fadd_f32(v[j][x], rq, row + lane4 + 256 * x, 0, 0);
+                                pp_atomic_add<FX>(v[j][x], rq, pp_roff<E>(row, x, lane4, lcq));
                         }
                     }
                     next += NW * n;
@@ -358,7 +393,7 @@ __global__ __launch_bounds__(256) void svdpp_epoch_fast_kernel(
         float C[E];
 #pragma unroll
         for (int x = 0; x < E; ++x) C[x] = s_red[0][lane + 64 * x];
-        pp_update_y<E, YB>(ry, items, b, e, wib * YB, 4 * YB, lane4, s_A - 1.f, C);
+        pp_update_y<E, YB, FX>(ry, items, b, e, wib * YB, 4 * YB, lane4, lcy, s_A - 1.f, C);
     }
     if (threadIdx.x == 0) gb_partial[blk] = contrib;
 }
@@ -451,20 +486,37 @@ __global__ __launch_bounds__(NT) void svdpp_ordered_kernel(
     if (f == 0) gb_io[0] = gb;
 }
 
+// fixed point (FX): the fp32 value v stored as int32 round(v * 2^24), saturating like v_cvt_i32_f32
+static float pp_host_fx(float v) {
+    const double t = std::nearbyint(static_cast<double>(v) * 16777216.0);
+    const int32_t i = t >= 2147483647.0 ? INT32_MAX : (t <= -2147483648.0 ? INT32_MIN : static_cast<int32_t>(t));
+    float out;
+    std::memcpy(&out, &i, 4);
+    return out;
+}
+static float pp_host_unfx(float bits) {
+    int32_t i;
+    std::memcpy(&i, &bits, 4);
+    return static_cast<float>(i) * (1.f / 16777216.f);
+}
+
 static void pack_bias_rows(const double* F, const double* bias, int64_t rows, int32_t k, int32_t ld,
-                           std::vector<float>& dst) {
+                           std::vector<float>& dst, bool fx = false) {
     dst.assign(static_cast<size_t>(rows) * ld, 0.f);
     for (int64_t r = 0; r < rows; ++r) {
         for (int32_t f = 0; f < k; ++f) dst[r * ld + f] = static_cast<float>(F[r * k + f]);
-        if (bias) dst[r * ld + ld - 1] = static_cast<float>(bias[r]);
+        if (bias) dst[r * ld + k] = static_cast<float>(bias[r]);  // bias column k
     }
+    if (fx)
+        for (float& v : dst) v = pp_host_fx(v);
 }
 
 static void unpack_bias_rows(const std::vector<float>& src, int64_t rows, int32_t k, int32_t ld,
-                             double* F, double* bias) {
+                             double* F, double* bias, bool fx = false) {
+    auto v = [&](int64_t x) { return fx ? pp_host_unfx(src[x]) : src[x]; };
     for (int64_t r = 0; r < rows; ++r) {
-        for (int32_t f = 0; f < k; ++f) F[r * k + f] = src[r * ld + f];
-        if (bias) bias[r] = src[r * ld + ld - 1];
+        for (int32_t f = 0; f < k; ++f) F[r * k + f] = v(r * ld + f);
+        if (bias) bias[r] = v(r * ld + k);
     }
 }
 
@@ -473,11 +525,12 @@ static void launch_pp_fast(int32_t n_blocks, const DevBuf<int32_t>& work, int32_
                            const DevBuf<int64_t>& rowptr, const DevBuf<int32_t>& items,
                            const DevBuf<float>& ratings, DevBuf<float>& P, DevBuf<float>& Q,
                            DevBuf<float>& Y, DevBuf<double>& gb, DevBuf<double>& partial, float lr,
-                           float reg, hipStream_t s) {
-    hipLaunchKernelGGL((svdpp_epoch_fast_kernel<E, 8>), dim3(n_blocks), dim3(256), 0, s, work.p,
+                           float reg, int32_t kf, bool fx, hipStream_t s) {
+    auto kern = fx ? svdpp_epoch_fast_kernel<E, 8, true> : svdpp_epoch_fast_kernel<E, 8, false>;
+    hipLaunchKernelGGL(kern, dim3(n_blocks), dim3(256), 0, s, work.p,
                        n_work, n_heavy, rowptr.p, items.p, ratings.p, P.p, Q.p, Y.p,
                        static_cast<int32_t>(Q.n * 4), static_cast<int32_t>(Y.n * 4), gb.p,
-                       partial.p, lr, reg);
+                       partial.p, lr, reg, kf);
 }
 
 }  // namespace rs
@@ -588,9 +641,11 @@ extern "C" int rs_svdpp_fit(rs_ctx* ctx, const rs_ratings* r, const rs_sgd_param
         rs::DevBuf<int32_t> dwork(std::max<size_t>(1, order.size()));
         dwork.upload(order.data(), order.size(), s);
         std::vector<float> hP, hQ, hY;
+        bool fx = true;  // fixed-point Q and Y (see pp_ld); RSGPU_PP_FX=0: fp32 float atomics
+        if (const char* env = std::getenv("RSGPU_PP_FX")) fx = std::atoi(env) != 0;
         rs::pack_bias_rows(P, bu, r->n_users, k, ld, hP);
-        rs::pack_bias_rows(Q, bi, r->n_items, k, ld, hQ);
-        rs::pack_bias_rows(Y, nullptr, r->n_items, k, ld, hY);
+        rs::pack_bias_rows(Q, bi, r->n_items, k, ld, hQ, fx);
+        rs::pack_bias_rows(Y, nullptr, r->n_items, k, ld, hY, fx);
         rs::DevBuf<float> dP(std::max<size_t>(1, hP.size())), dQ(std::max<size_t>(1, hQ.size())),
             dY(std::max<size_t>(1, hY.size()));
         rs::DevBuf<double> dpart(n_blocks);
@@ -602,14 +657,14 @@ extern "C" int rs_svdpp_fit(rs_ctx* ctx, const rs_ratings* r, const rs_sgd_param
         rs::kernel_span_begin(ctx);
         for (int32_t ep = 0; ep < p->n_epochs; ++ep) {
             switch (E) {
-                case 1: rs::launch_pp_fast<1>(n_blocks, dwork, n_work, n_heavy, drow, dcol, dval, dP, dQ, dY, dgb, dpart, lr, reg, s); break;
-                case 2: rs::launch_pp_fast<2>(n_blocks, dwork, n_work, n_heavy, drow, dcol, dval, dP, dQ, dY, dgb, dpart, lr, reg, s); break;
-                case 3: rs::launch_pp_fast<3>(n_blocks, dwork, n_work, n_heavy, drow, dcol, dval, dP, dQ, dY, dgb, dpart, lr, reg, s); break;
-                case 4: rs::launch_pp_fast<4>(n_blocks, dwork, n_work, n_heavy, drow, dcol, dval, dP, dQ, dY, dgb, dpart, lr, reg, s); break;
-                case 5: rs::launch_pp_fast<5>(n_blocks, dwork, n_work, n_heavy, drow, dcol, dval, dP, dQ, dY, dgb, dpart, lr, reg, s); break;
-                case 6: rs::launch_pp_fast<6>(n_blocks, dwork, n_work, n_heavy, drow, dcol, dval, dP, dQ, dY, dgb, dpart, lr, reg, s); break;
-                case 7: rs::launch_pp_fast<7>(n_blocks, dwork, n_work, n_heavy, drow, dcol, dval, dP, dQ, dY, dgb, dpart, lr, reg, s); break;
-                default: rs::launch_pp_fast<8>(n_blocks, dwork, n_work, n_heavy, drow, dcol, dval, dP, dQ, dY, dgb, dpart, lr, reg, s); break;
+                case 1: rs::launch_pp_fast<1>(n_blocks, dwork, n_work, n_heavy, drow, dcol, dval, dP, dQ, dY, dgb, dpart, lr, reg, k, fx, s); break;
+                case 2: rs::launch_pp_fast<2>(n_blocks, dwork, n_work, n_heavy, drow, dcol, dval, dP, dQ, dY, dgb, dpart, lr, reg, k, fx, s); break;
+                case 3: rs::launch_pp_fast<3>(n_blocks, dwork, n_work, n_heavy, drow, dcol, dval, dP, dQ, dY, dgb, dpart, lr, reg, k, fx, s); break;
+                case 4: rs::launch_pp_fast<4>(n_blocks, dwork, n_work, n_heavy, drow, dcol, dval, dP, dQ, dY, dgb, dpart, lr, reg, k, fx, s); break;
+                case 5: rs::launch_pp_fast<5>(n_blocks, dwork, n_work, n_heavy, drow, dcol, dval, dP, dQ, dY, dgb, dpart, lr, reg, k, fx, s); break;
+                case 6: rs::launch_pp_fast<6>(n_blocks, dwork, n_work, n_heavy, drow, dcol, dval, dP, dQ, dY, dgb, dpart, lr, reg, k, fx, s); break;
+                case 7: rs::launch_pp_fast<7>(n_blocks, dwork, n_work, n_heavy, drow, dcol, dval, dP, dQ, dY, dgb, dpart, lr, reg, k, fx, s); break;
+                default: rs::launch_pp_fast<8>(n_blocks, dwork, n_work, n_heavy, drow, dcol, dval, dP, dQ, dY, dgb, dpart, lr, reg, k, fx, s); break;
             }
             RS_HIP(hipGetLastError());
             hipLaunchKernelGGL(rs::pp_gb_fold_kernel, dim3(1), dim3(256), 0, s, dpart.p,
@@ -623,8 +678,8 @@ extern "C" int rs_svdpp_fit(rs_ctx* ctx, const rs_ratings* r, const rs_sgd_param
         dgb.download(gb, 1, s);
         RS_HIP(hipStreamSynchronize(s));
         rs::unpack_bias_rows(hP, r->n_users, k, ld, P, bu);
-        rs::unpack_bias_rows(hQ, r->n_items, k, ld, Q, bi);
-        rs::unpack_bias_rows(hY, r->n_items, k, ld, Y, nullptr);
+        rs::unpack_bias_rows(hQ, r->n_items, k, ld, Q, bi, fx);
+        rs::unpack_bias_rows(hY, r->n_items, k, ld, Y, nullptr, fx);
         return RS_OK;
     });
 }
