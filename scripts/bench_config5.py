@@ -77,6 +77,9 @@ def main():
                     help="items: north_star item-range shards + user-delta all-reduce; users: the dual "
                          "partition (user-range shards + item-delta all-reduce)")
     ap.add_argument("--item-cap", type=int, default=1 << 16)
+    ap.add_argument("--split", type=int, default=-1, help="user split cap (-1: plan default)")
+    ap.add_argument("--fixed-q", type=int, default=-1, help="fixed-point Q (-1: plan default)")
+    ap.add_argument("--hot", type=int, default=-1, help="hot replicas n_hot (-1: plan default)")
     ap.add_argument("--threads", type=int, default=16)
     ap.add_argument("--cpu-budget", type=float, default=10.0)
     ap.add_argument("--lr", type=float, default=0.005)
@@ -141,6 +144,12 @@ def main():
     plan = ctx.svd_plan_csr(U, I, tr_rowptr, cols, vals, k)
     if args.item_cap > 0:
         plan.set_item_split(args.item_cap)
+    if args.split >= 0:
+        plan.set_split(args.split)
+    if args.fixed_q >= 0:
+        plan.set_fixed_q(args.fixed_q)
+    if args.hot >= 0:
+        plan.set_hot_replicas(args.hot, 8)
     plan.init_normal(0.0, 0.1, seed=1)
     t_plan = time.perf_counter() - t0
     log(f"rank {rank}: plan built in {t_plan:.1f} s")
