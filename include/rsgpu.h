@@ -238,7 +238,7 @@ int rs_svd_plan_download(rs_svd_plan* plan, double* P, double* Q, double* bu, do
 /* Enqueue n_epochs fast-mode epochs (one SGD kernel + one global-bias fold per epoch). */
 int rs_svd_plan_epochs(rs_svd_plan* plan, int32_t n_epochs, float lr, float reg, void* stream);
 /* write_back: RS_SGD_WB_ATOMIC (default), _STORE or _ATOMIC_DIRECT; ring_depth: item-row prefetch distance
- * in ratings (4, 8 = default, 16). */
+ * in ratings (4, 8, 16 = default). */
 int rs_svd_plan_set_mode(rs_svd_plan* plan, int32_t write_back, int32_t ring_depth);
 /* RS_SGD_WB_ATOMIC schedule.  Work items with at least heavy_min ratings (default 1000; 0 = none) run
  * as one SGD wave plus three writer waves that issue its atomics; the other (light) items are

@@ -411,7 +411,7 @@ class SvdPlan:
     def epochs(self, n, lr=0.005, reg=0.02, stream=None):
         self.ctx.check(lib().rs_svd_plan_epochs(self.h, n, lr, reg, stream))
 
-    def set_mode(self, write_back=WB_ATOMIC, ring_depth=8):
+    def set_mode(self, write_back=WB_ATOMIC, ring_depth=16):
         self.ctx.check(lib().rs_svd_plan_set_mode(self.h, write_back, ring_depth))
 
     def set_schedule(self, heavy_min=1024, light_blocks=-1):
