@@ -36,6 +36,8 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <chrono>
+#include <cstdio>
 #include <cmath>
 #include <cstdlib>
 #include <numeric>
@@ -1193,11 +1195,19 @@ static void build_items(rs_svd_plan* pl) {
         }
     }
     std::vector<int32_t> remap(cols.size() + 128, 0);
-    std::vector<int64_t> seen(std::max(1, ni), 0);
-    for (size_t t = 0; t < cols.size(); ++t) {
-        const int32_t x = cols[t];
-        const int32_t c = static_cast<int32_t>(seen[x]++ * R[x] / deg[x]);
-        remap[t] = c == 0 ? x : first[x] + c - 1;
+    if (extra == 0) {
+        std::copy(cols.begin(), cols.end(), remap.begin());  // no copies: the item ids as they are
+    } else {
+        std::vector<int64_t> seen(std::max(1, ni), 0);
+        for (size_t t = 0; t < cols.size(); ++t) {
+            const int32_t x = cols[t];
+            if (R[x] == 1) {  // the common case: no 64-bit division per rating
+                remap[t] = x;
+                continue;
+            }
+            const int32_t c = static_cast<int32_t>(seen[x]++ * R[x] / deg[x]);
+            remap[t] = c == 0 ? x : first[x] + c - 1;
+        }
     }
     const int32_t rows = ni + extra;
     if (static_cast<int64_t>(std::max(1, rows)) * pl->ld * 4 >= (int64_t{1} << 31) - 64)
@@ -1306,8 +1316,15 @@ static void plan_build_csr(rs_ctx* ctx, int32_t n_users, int32_t n_items, UserCS
     pl->h_cols = std::move(csr.cols);
     pl->P.alloc(static_cast<size_t>(std::max(1, n_users)) * pl->ld);
     RS_HIP(hipMemsetAsync(pl->P.p, 0, pl->P.n * sizeof(float), s));
+    static const bool trace = std::getenv("RSGPU_FIT_TRACE") != nullptr;
+    auto t0 = std::chrono::steady_clock::now();
     build_items(pl);
+    auto t1 = std::chrono::steady_clock::now();
     build_work(pl);
+    if (trace)
+        std::fprintf(stderr, "fit-trace   items %8.3f ms, work %8.3f ms\n",
+                     std::chrono::duration<double, std::milli>(t1 - t0).count(),
+                     std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t1).count());
     pl->gb.alloc(1);
     RS_HIP(hipMemsetAsync(pl->gb.p, 0, sizeof(double), s));
     RS_HIP(hipEventCreate(&pl->ev0));
@@ -1886,15 +1903,37 @@ extern "C" int rs_svd_fit(rs_ctx* ctx, const rs_ratings* r, const rs_sgd_params*
             return rs::set_error(ctx, RS_ERR_INVALID, "output pointer is NULL");
         const float lr = static_cast<float>(p->lr), reg = static_cast<float>(p->reg);
         if (p->mode == RS_SGD_FAST) {
+            // RSGPU_FIT_TRACE=1: host phase times of this one-shot Fit on stderr (end-to-end study)
+            static const bool trace = std::getenv("RSGPU_FIT_TRACE") != nullptr;
+            auto now = [] { return std::chrono::steady_clock::now(); };
+            auto t = now();
+            auto mark = [&](const char* what) {
+                if (!trace) return;
+                (void)hipStreamSynchronize(ctx->stream);
+                const auto t1 = now();
+                std::fprintf(stderr, "fit-trace %-10s %8.3f ms\n", what,
+                             std::chrono::duration<double, std::milli>(t1 - t).count());
+                t = t1;
+            };
             rs_svd_plan pl;
-            rs::plan_build(ctx, r, p->n_factors, &pl);
+            {
+                rs::UserCSR csr;
+                rs::build_csr(r->nnz, r->n_users, r->users, r->items, r->ratings, csr);
+                mark("csr");
+                rs::plan_build_csr(ctx, r->n_users, r->n_items, std::move(csr), p->n_factors, &pl);
+                mark("plan");
+            }
             pl.write_back = p->write_back >= RS_SGD_WB_ATOMIC && p->write_back <= RS_SGD_WB_ATOMIC_DIRECT ? p->write_back : RS_SGD_WB_ATOMIC;
             if (p->n_epochs > 0) *gb = rs::gb_warm_start(r, bu, bi);
+            mark("warm");
             rs::plan_upload(&pl, P, Q, bu, bi, gb);
+            mark("upload");
             rs::kernel_span_begin(ctx);
             rs::plan_epochs(&pl, p->n_epochs, lr, reg, ctx->stream);
             rs::kernel_span_end(ctx);
+            mark("epochs");
             rs::plan_download(&pl, P, Q, bu, bi, gb);
+            mark("download");
             return RS_OK;
         }
         // ORDERED: COO in train-set order, one group, all epochs in one launch.
