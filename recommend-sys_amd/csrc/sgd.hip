@@ -41,6 +41,7 @@
 #include <cmath>
 #include <cstdlib>
 #include <numeric>
+#include <thread>
 #include <stdexcept>
 #include <vector>
 
@@ -1198,16 +1199,52 @@ static void build_items(rs_svd_plan* pl) {
     if (extra == 0) {
         std::copy(cols.begin(), cols.end(), remap.begin());  // no copies: the item ids as they are
     } else {
-        std::vector<int64_t> seen(std::max(1, ni), 0);
-        for (size_t t = 0; t < cols.size(); ++t) {
-            const int32_t x = cols[t];
-            if (R[x] == 1) {  // the common case: no 64-bit division per rating
-                remap[t] = x;
-                continue;
+        // Two passes over column chunks on host threads: the per-item position counter of a hot item is a
+        // serial store-to-load chain, so one thread walks ~10 ns per hot rating. Pass 1 counts each
+        // chunk's ratings of split/live items, an exclusive prefix over chunks gives each chunk its
+        // starting positions, pass 2 deals pieces exactly as the serial walk would (same output).
+        const size_t n = cols.size();
+        const int nt = n >= (size_t{1} << 18) ? 8 : 1;
+        std::vector<std::vector<int64_t>> cnt(nt, std::vector<int64_t>(std::max(1, ni), 0));
+        auto range = [&](int c, size_t& b, size_t& e) { b = n * c / nt; e = n * (c + 1) / nt; };
+        auto count = [&](int c) {
+            size_t b, e;
+            range(c, b, e);
+            std::vector<int64_t>& k = cnt[c];
+            for (size_t t = b; t < e; ++t)
+                if (R[cols[t]] > 1) k[cols[t]]++;
+        };
+        auto deal = [&](int c) {
+            size_t b, e;
+            range(c, b, e);
+            std::vector<int64_t>& seen = cnt[c];
+            for (size_t t = b; t < e; ++t) {
+                const int32_t x = cols[t];
+                if (R[x] == 1) {  // the common case: no 64-bit division per rating
+                    remap[t] = x;
+                    continue;
+                }
+                const int32_t p = static_cast<int32_t>(seen[x]++ * R[x] / deg[x]);
+                remap[t] = p == 0 ? x : first[x] + p - 1;
             }
-            const int32_t c = static_cast<int32_t>(seen[x]++ * R[x] / deg[x]);
-            remap[t] = c == 0 ? x : first[x] + c - 1;
+        };
+        auto run = [&](auto&& fn) {
+            std::vector<std::thread> th;
+            for (int c = 1; c < nt; ++c) th.emplace_back(fn, c);
+            fn(0);
+            for (std::thread& t : th) t.join();
+        };
+        run(count);
+        for (int32_t x = 0; x < ni; ++x) {
+            if (R[x] == 1) continue;
+            int64_t acc = 0;
+            for (int c = 0; c < nt; ++c) {
+                const int64_t v = cnt[c][x];
+                cnt[c][x] = acc;
+                acc += v;
+            }
         }
+        run(deal);
     }
     const int32_t rows = ni + extra;
     if (static_cast<int64_t>(std::max(1, rows)) * pl->ld * 4 >= (int64_t{1} << 31) - 64)
