@@ -53,11 +53,14 @@ extern "C" {
 #define RS_SGD_FAST 0    /* user-CSR, one wave per user, atomic q_i deltas, deferred global bias */
 #define RS_SGD_ORDERED 1 /* single group, exact train-set order and update order of svd.go:93-129 */
 
-/* FAST-mode write-back of the item rows (rs_svd_plan_set_mode) */
-#define RS_SGD_WB_ATOMIC 0        /* float-atomic deltas at the memory side, no lost updates (default);
-                                    heavy users' deltas go through LDS rings to writer waves */
-#define RS_SGD_WB_STORE 1         /* write-through stores: Hogwild, concurrent updates of a row can be lost */
-#define RS_SGD_WB_ATOMIC_DIRECT 2 /* the same atomic deltas issued by each compute wave itself */
+/* FAST-mode schedule / write-back of the item rows (rs_sgd_params.write_back, rs_svd_plan_set_mode) */
+#define RS_SGD_WB_TILE 0          /* default: user tiles in LDS (integer LDS atomics), one memory-side
+                                    integer atomic per (item, tile) run (sgd_tile.hip) */
+#define RS_SGD_WB_STORE 1         /* per-user waves, write-through stores: Hogwild, concurrent updates of a
+                                    row can be lost */
+#define RS_SGD_WB_ATOMIC_DIRECT 2 /* per-user waves, each issuing its q_i deltas as memory-side atomics */
+#define RS_SGD_WB_ATOMIC 3        /* per-user waves, memory-side atomic deltas with hot replicas, user
+                                    splitting and heavy users' deltas through LDS rings to writer waves */
 
 /* Similarity kinds: core/sim.go Cosine (10-25), MSD (28-44), Pearson (47-81) */
 #define RS_SIM_COSINE 0
@@ -88,7 +91,7 @@ typedef struct {
     double lr;         /* "lr"       */
     double reg;        /* "reg"      */
     int32_t mode;      /* RS_SGD_FAST or RS_SGD_ORDERED */
-    int32_t write_back; /* FAST only: RS_SGD_WB_* (RS_SGD_WB_ATOMIC = 0 is the default) */
+    int32_t write_back; /* FAST only: RS_SGD_WB_* (RS_SGD_WB_TILE = 0 is the default) */
 } rs_sgd_params;
 
 /* ---- TrainSet construction on the host (no GPU involved) ------------------ *
@@ -235,11 +238,27 @@ int rs_svd_plan_upload(rs_svd_plan* plan, const double* P, const double* Q, cons
                        const double* bi, const double* gb);
 int rs_svd_plan_download(rs_svd_plan* plan, double* P, double* Q, double* bu, double* bi,
                          double* gb);
-/* Enqueue n_epochs fast-mode epochs (one SGD kernel + one global-bias fold per epoch). */
+/* Enqueue n_epochs fast-mode epochs (one SGD kernel + one epilogue -- global-bias fold, split users'
+ * merge -- per epoch; Q converted to int32 fixed point before the first and back after the last). */
 int rs_svd_plan_epochs(rs_svd_plan* plan, int32_t n_epochs, float lr, float reg, void* stream);
-/* write_back: RS_SGD_WB_ATOMIC (default), _STORE or _ATOMIC_DIRECT; ring_depth: item-row prefetch distance
- * in ratings (4, 8, 16 = default). */
+/* write_back: RS_SGD_WB_TILE (default), _STORE, _ATOMIC_DIRECT or _ATOMIC; ring_depth: item-row prefetch
+ * distance in ratings of the per-user schedules (4, 8, 16 = default). */
 int rs_svd_plan_set_mode(rs_svd_plan* plan, int32_t write_back, int32_t ring_depth);
+/* RS_SGD_WB_TILE parameters: workgroups of the launch (0 = one per CU), waves per workgroup (1, 2, 4,
+ * 8 or 16; default 16), ratings per tile (0 = nnz / workgroups, bounded by the 160 KiB LDS), run cap
+ * (an item's run in a tile longer than this is cut into pieces on different waves; 0 = never; ignored
+ * with one wave), ring (q_i rows each wave keeps in flight: 0 = auto, else 4, 6, 8 or 12, clamped for
+ * wide rows).  Rebuilds the schedule. */
+int rs_svd_plan_set_tiles(rs_svd_plan* plan, int32_t workgroups, int32_t waves, int32_t target,
+                          int32_t run_cap, int32_t ring);
+/* Visit order of the tile schedule: pos[n] = user-CSR position (rowptr order, data order inside a row)
+ * of the n-th rating (nnz entries) as the kernel's streams walk it -- tile by tile, a tile's waves in
+ * order, a wave's runs in order --, and work_off (n_works + 1 entries) the boundaries of the (tile,
+ * wave) streams, the kernel's GlobalBias work items; n_works = tiles x waves.  Any pointer may be
+ * NULL (call once with pos = work_off = NULL for n_works).  With one workgroup of one wave an epoch
+ * is exactly the sequential SGD of svd.go:93-129 in this order with the work-local GlobalBias fold
+ * (the oracle's or_svd_fit_works restates it). */
+int rs_svd_plan_tile_order(rs_svd_plan* plan, int64_t* pos, int64_t* work_off, int32_t* n_works);
 /* RS_SGD_WB_ATOMIC schedule.  Work items with at least heavy_min ratings (default 1000; 0 = none) run
  * as one SGD wave plus three writer waves that issue its atomics; the other (light) items are
  * strided over light_blocks blocks of four waves (default < 0: 1.5 per CU; 0: one wave per item).

@@ -127,6 +127,43 @@ void or_svd_fit(int64_t n, const int32_t* u, const int32_t* i, const double* r, 
     *gb = GB;
 }
 
+/* Restatement of the GPU FAST schedules' GlobalBias semantics over explicit work items: the ratings
+ * (in the given order) are cut into n_works consecutive segments [work_off[w], work_off[w+1]); each
+ * runs the per-rating updates of svd.go:93-129 with a work-local GlobalBias copy starting from the
+ * epoch's value, P/Q/bu/bi updated in place, works one after another; after the epoch
+ * GB += sum_w n_w (gb_w - GB) / n (the fixed-order fold of sgd.hip / sgd_tile.hip).  Equal to the GPU
+ * kernels when their works do not race (one wave, or works with disjoint users and items). */
+void or_svd_fit_works(int64_t n, const int32_t* u, const int32_t* i, const double* r, int64_t n_works,
+                      const int64_t* work_off, int32_t k, int32_t epochs, double lr, double reg, double* P,
+                      double* Q, double* bu, double* bi, double* gb) {
+    double GB = *gb;
+    for (int32_t epoch = 0; epoch < epochs; epoch++) {
+        double fold = 0.0;
+        for (int64_t w = 0; w < n_works; w++) {
+            double g = GB;
+            for (int64_t t = work_off[w]; t < work_off[w + 1]; t++) {
+                const int32_t uu = u[t], ii = i[t];
+                const double userBias = bu[uu], itemBias = bi[ii];
+                double* pu = P + (int64_t)uu * k;
+                double* qi = Q + (int64_t)ii * k;
+                double pred = g;
+                pred += bu[uu];
+                pred += bi[ii];
+                pred += dot(pu, qi, k);
+                const double diff = pred - r[t];
+                g -= lr * diff;
+                bu[uu] -= lr * (diff + reg * userBias);
+                bi[ii] -= lr * (diff + reg * itemBias);
+                for (int32_t f = 0; f < k; f++) pu[f] = pu[f] - (qi[f] * diff + pu[f] * reg) * lr;
+                for (int32_t f = 0; f < k; f++) qi[f] = qi[f] - (pu[f] * diff + qi[f] * reg) * lr;
+            }
+            fold += (double)(work_off[w + 1] - work_off[w]) * (g - GB);
+        }
+        if (n > 0) GB += fold / (double)n;
+    }
+    *gb = GB;
+}
+
 void or_svd_predict(int64_t n, const int32_t* u, const int32_t* i, int32_t k, const double* P,
                     const double* Q, const double* bu, const double* bi, double gb, double* out) {
     for (int64_t t = 0; t < n; t++) {

@@ -38,6 +38,11 @@ void or_svd_fit(int64_t n, const int32_t* u, const int32_t* i, const double* r,
                 int32_t k, int32_t epochs, double lr, double reg,
                 double* P, double* Q, double* bu, double* bi, double* gb);
 
+/* The FAST schedules' GlobalBias semantics over explicit work items (segments of the given order),
+ * works run one after another: the GPU tile / per-user kernels' own schedule on race-free input. */
+void or_svd_fit_works(int64_t n, const int32_t* u, const int32_t* i, const double* r, int64_t n_works,
+                      const int64_t* work_off, int32_t k, int32_t epochs, double lr, double reg, double* P,
+                      double* Q, double* bu, double* bi, double* gb);
 /* svd.go:32-51 SVD.Predict for inner ids (-1 = unknown, data.go:129 newID). */
 void or_svd_predict(int64_t n, const int32_t* u, const int32_t* i, int32_t k,
                     const double* P, const double* Q, const double* bu, const double* bi,

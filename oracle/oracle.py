@@ -64,6 +64,8 @@ def lib():
         L.or_svdpp_fit_userwise.argtypes = [C.c_int32, _i64p, _i32p, _f64p, C.c_int32, C.c_int32,
                                             C.c_double, C.c_double, _f64p, _f64p, _f64p, _f64p,
                                             _f64p, _dp]
+        L.or_svd_fit_works.argtypes = [C.c_int64, _i32p, _i32p, _f64p, C.c_int64, _i64p, C.c_int32,
+                                       C.c_int32, C.c_double, C.c_double, _f64p, _f64p, _f64p, _f64p, _dp]
         L.or_svd_fit_chunked.argtypes = [C.c_int32, _i64p, _i32p, _f64p, C.c_int32, C.c_int32,
                                          C.c_int32, C.c_double, C.c_double, _f64p, _f64p, _f64p,
                                          _f64p, _dp]
@@ -143,6 +145,19 @@ def svd_fit(u, i, r, P, Q, bu=None, bi=None, gb=0.0, epochs=20, lr=0.005, reg=0.
     g = C.c_double(gb)
     lib().or_svd_fit(len(r), _i32(u), _i32(i), _f64(r), k, epochs, lr, reg, P, Q, bu, bi,
                      C.byref(g))
+    return P, Q, bu, bi, g.value
+
+
+def svd_fit_works(u, i, r, work_off, P, Q, bu=None, bi=None, gb=0.0, epochs=1, lr=0.005, reg=0.02):
+    """The FAST schedules' own semantics: ratings (in this order) cut into works at work_off, each
+    with a work-local GlobalBias folded after the epoch (or_svd_fit_works)."""
+    P, Q = _f64(P).copy(), _f64(Q).copy()
+    bu = np.zeros(P.shape[0]) if bu is None else _f64(bu).copy()
+    bi = np.zeros(Q.shape[0]) if bi is None else _f64(bi).copy()
+    g = C.c_double(gb)
+    wo = _i64(work_off)
+    lib().or_svd_fit_works(len(r), _i32(u), _i32(i), _f64(r), len(wo) - 1, wo, P.shape[1], epochs, lr,
+                           reg, P, Q, bu, bi, C.byref(g))
     return P, Q, bu, bi, g.value
 
 

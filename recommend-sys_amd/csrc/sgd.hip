@@ -47,53 +47,13 @@
 
 #include "common.hpp"
 #include "wave.hpp"
+#include "sgd_plan.hpp"
 
 namespace rs {
 
-constexpr int32_t kOutOfRange = 0x7FFFFFF0;  // buffer offset past num_records: load 0 / drop store
-constexpr int kSgdAux = 16;                  // sc1
 constexpr int kVolatileAux = static_cast<int>(0x80000000u);  // buffer intrinsic aux bit 31: volatile
 
-// Sum over the 64 lanes of a wave: DPP inside each 16-lane row, then the gfx950 permlane swaps
-// across rows.  Every lane ends with the bitwise-identical total.
-__device__ __forceinline__ float wave_sum(float x) {
-    x = group_sum<16>(x);
-    auto r16 = __builtin_amdgcn_permlane16_swap(__float_as_uint(x), __float_as_uint(x), false, false);
-    x = __uint_as_float(r16[0]) + __uint_as_float(r16[1]);
-    auto r32 = __builtin_amdgcn_permlane32_swap(__float_as_uint(x), __float_as_uint(x), false, false);
-    return __uint_as_float(r32[0]) + __uint_as_float(r32[1]);
-}
-
-// Fixed-point item rows (rs_svd_plan_set_fixed_q): during a hybrid FAST epoch Q holds
-// round(q * 2^24) as int32 and the q_i deltas are integer atomics.  Measured on gfx950
-// (scripts/exp_atomics.hip, exp_atomics2.hip): memory-side u32 atomic adds sustain 1.69 TB/s of
-// added bytes against 1.32 TB/s for f32 -- and the epoch is bound by that rate.  The resolution
-// 2^-24 is the fp32 ulp at |q| in [0.5, 1); the range is |q| < 128 (v_cvt_i32_f32 saturates).
-// Integer adds are exact and associative, so the sum of the deltas no longer depends on their order.
-constexpr float kFx = 16777216.f, kFxInv = 1.f / 16777216.f;
-__device__ __forceinline__ float fx_to_f(uint32_t bits) { return static_cast<float>(static_cast<int32_t>(bits)) * kFxInv; }
-__device__ __forceinline__ int32_t fx_delta(float qn, float q) { return __float2int_rn((qn - q) * kFx); }
-
-// Row layout of the FAST plan: lane l's register x holds column l + 64 x, except lane 63's last
-// register, which holds the bias in column kf (right after the kf factors).  The other lanes of the
-// last register whose column is >= kf are padding: never loaded (they read 0) and never written, so
-// the 64-B lines past column kf get no memory request at all -- row atomics are priced per 64-B line,
-// not per dword (scripts/exp_atomics2.hip: 1.69 -> 1.93 TB/s of row bytes with one line of eight
-// masked off); k = 100 rows take 7 line requests instead of 8.
-template <int E>
-__device__ __forceinline__ int32_t last_col(int lane, int32_t kf) {  // column of register E-1, or -1
-    const int32_t c = lane == 63 ? kf : lane + 64 * (E - 1);
-    return (lane == 63 || c < kf) ? c : -1;
-}
-// byte offset of register x of this lane in the row at byte offset `row` (kOutOfRange: padding)
-template <int E>
-__device__ __forceinline__ int32_t roff(int32_t row, int x, int32_t lane4, int32_t lc) {
-    return x < E - 1 ? row + lane4 + 256 * x : (lc >= 0 ? row + 4 * lc : kOutOfRange);
-}
-
-__device__ __forceinline__ float lane63(float x) {
-    return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(x), 63));
-}
+// wave_sum, fx_to_f, fx_delta, last_col, roff, lane63: sgd_plan.hpp
 
 // One FAST work item (a user row or a piece of one): the SGD chain over its ratings with p_u in
 // VGPRs.  Every q_i update is handed to emit(row byte offset, q_new, q_old); the kernels below
@@ -915,69 +875,9 @@ __global__ __launch_bounds__(64) void svd_ordered_kernel(
 }  // namespace rs
 
 // ------------------------------------------------------------------------------------------------
-// Plan (device-resident CSR + factors)
+// Plan (device-resident CSR + factors): struct rs_svd_plan lives in sgd_plan.hpp (shared with
+// sgd_tile.hip, the tile schedule).
 
-struct rs_svd_plan {
-    rs_ctx* ctx = nullptr;
-    int32_t n_users = 0, n_items = 0, k = 0, ld = 0, n_work = 0;
-    int64_t nnz = 0;
-    std::vector<int64_t> h_rowptr;  // host user-CSR row pointers (work items are rebuilt from it)
-    std::vector<int32_t> h_cols;    // host user-CSR item ids (item copies are rebuilt from it)
-    rs::DevBuf<int32_t> items;      // user-CSR item rows (copies of split items), padded by 128
-    rs::DevBuf<float> ratings;
-    rs::DevBuf<int32_t> wk_user;      // work items: user, [begin, end) into the CSR, len / deg
-    rs::DevBuf<int64_t> wk_rng;
-    rs::DevBuf<float> wk_frac;
-    // users with more ratings are split into pieces (0: never).  Default 1200, measured on the ML-1M
-    // shape with heavy_min 1000 and fixed-point Q (scripts/exp_split_sweep.py): epoch 572 -> 491 us,
-    // 20-epoch held-out RMSE 0.6676 -> 0.6684 against 0.6683 for the reference visit order
-    int32_t split_cap = 1200;
-    rs::DevBuf<float> dPs;            // split-user deltas (single GPU), zero between epochs
-    rs::DevBuf<int32_t> split_rows;   // users split into pieces
-    int32_t n_split = 0;
-    int32_t item_cap = 0;             // items with more ratings get row copies (0: never)
-    int32_t n_qrows = 0;              // item rows incl. copies (Q holds n_qrows x ld)
-    rs::DevBuf<int4> isplit_meta;     // split items: {row, first copy row, copies, frac offset}
-    rs::DevBuf<float> isplit_frac;
-    int32_t n_isplit = 0;
-    rs::DevBuf<float> P, Q;  // bias in column k
-    rs::DevBuf<double> gb, partial;
-    rs::DevBuf<float> uw;  // per-user share of this shard (multi-GPU delta mode)
-    // hot replicas: most-rated items and copies each (0: none).  Default 256 x 8, measured on the
-    // ML-1M shape (scripts/exp_replicas.py): epoch 760 -> 585 us, held-out RMSE unchanged
-    int32_t live_req = 256, live_copies = 8;
-    int32_t n_live = 0;
-    rs::DevBuf<int4> live_meta;  // {item row, first extra row, copies, -}
-    rs::DevBuf<float> qlast;     // last merged value of every live item (n_live x ld)
-    rs::DevBuf<int32_t> done;    // blocks finished (the merger's exit condition)
-    rs::DevBuf<float> iw;  // per-item share of this shard (user-sharded multi-GPU mode)
-    rs::DevBuf<float> Q0;  // Q at the epoch start (user-sharded mode)
-    int32_t n_blocks = 0;
-    int32_t write_back = RS_SGD_WB_ATOMIC;
-    int32_t heavy_min = 1000;  // work items with at least this many ratings get a producer + 3 writers
-    int32_t n_heavy = 0;       // leading (LPT-ordered) work items that are heavy
-    int32_t light_blocks = 0;  // cap on the light blocks (each wave strides over light items; 0 = none)
-    rs::DevBuf<int64_t> trace;  // diagnostic: {start, chain end, drained} per work item (RS_SGD_WB_ATOMIC)
-    // q_i prefetch distance of the light waves: 16 since the end of round 1 (ML-1M shape with the
-    // default schedule: epoch 435 -> 428 us, held-out RMSE 0.6685 either way; exp_split_sweep.py)
-    int32_t ring_depth = 16;
-    int32_t fixed_q = 1;           // hybrid epochs keep Q as int32 fixed point (rs_svd_plan_set_fixed_q)
-    bool live_merged = false;      // the fixed-point epoch already ran the live items' final round
-    bool hoisted = false;          // plan_epochs: Q stays int32 across epochs, the epilogue re-arms done
-    double mean_rating = 0.0;  // of the plan's ratings (FAST GlobalBias warm start at init)
-    hipEvent_t ev0 = nullptr, ev1 = nullptr;
-    double last_ms = 0.0;
-    int32_t last_launches = 0;
-    bool timing = false;
-    hipStream_t last_stream = nullptr;  // stream of the last enqueued epochs (synced before copies)
-    std::vector<hipEvent_t> tev;        // timing mode: [2 * epoch] start, [2 * epoch + 1] end
-    int32_t tev_used = 0;
-    ~rs_svd_plan() {
-        if (ev0) (void)hipEventDestroy(ev0);
-        if (ev1) (void)hipEventDestroy(ev1);
-        for (hipEvent_t e : tev) (void)hipEventDestroy(e);
-    }
-};
 
 namespace rs {
 
@@ -1072,6 +972,19 @@ static void launch_fast_d(rs_svd_plan* pl, float lr, float reg, hipStream_t s, f
 }
 
 static void launch_fast(rs_svd_plan* pl, float lr, float reg, hipStream_t s, float* dP = nullptr) {
+    if (pl->write_back == RS_SGD_WB_TILE) {  // sgd_tile.hip; Q is int32 fixed point inside
+        if (pl->hoisted) {
+            tile_launch(pl, lr, reg, s, dP);
+            return;
+        }
+        const int64_t qn = static_cast<int64_t>(pl->Q.n);
+        const int fx_blocks = static_cast<int>(std::min<int64_t>(2048, (qn + 255) / 256));
+        hipLaunchKernelGGL(svd_q_fixed_kernel, dim3(fx_blocks), dim3(256), 0, s, pl->Q.p, qn, 1);
+        tile_launch(pl, lr, reg, s, dP);
+        hipLaunchKernelGGL(svd_q_fixed_kernel, dim3(fx_blocks), dim3(256), 0, s, pl->Q.p, qn, 0);
+        RS_HIP(hipGetLastError());
+        return;
+    }
     if (pl->hoisted) {  // plan_epochs does the conversions and the epilogue around its epoch loop
         launch_fast_d<2>(pl, lr, reg, s, dP);
         RS_HIP(hipGetLastError());
@@ -1114,6 +1027,15 @@ static void live_merge_after(rs_svd_plan* pl, hipStream_t s) {
                            pl->qlast.p, pl->ld, 1);
 }
 
+// Split users' pieces (count-weighted deltas in dPs) merged into P after an epoch.
+static void merge_split_rows(rs_svd_plan* pl, hipStream_t s) {
+    const bool tile = pl->write_back == RS_SGD_WB_TILE;
+    const int32_t n = tile ? pl->t_n_split : pl->n_split;
+    if (n > 0)
+        hipLaunchKernelGGL(svd_merge_rows_kernel, dim3(n), dim3(64), 0, s, pl->P.p, pl->dPs.p,
+                           tile ? pl->t_split_rows.p : pl->split_rows.p, pl->ld);
+}
+
 static void launch_ordered(int64_t nnz, const int32_t* u, const int32_t* i, const float* r,
                            float* P, float* Q, float* bu, float* bi, int32_t ld, double* gb,
                            int32_t epochs, float lr, float reg, hipStream_t s) {
@@ -1130,7 +1052,7 @@ static void launch_ordered(int64_t nnz, const int32_t* u, const int32_t* i, cons
 
 int32_t fast_ld(int32_t k) { return 64 * ((k + 1 + 63) / 64); }
 
-static void plan_sync_last(rs_svd_plan* pl) {
+void plan_sync_last(rs_svd_plan* pl) {
     if (pl->last_stream) RS_HIP(hipStreamSynchronize(pl->last_stream));
 }
 
@@ -1328,6 +1250,25 @@ static void build_work(rs_svd_plan* pl) {
     RS_HIP(hipStreamSynchronize(s));  // host vectors die with this scope
 }
 
+// The per-user schedules' structures (hybrid / direct / store write-back): the user-CSR item ids
+// with hot-item copies, the ratings and the work list.  Built when a plan first runs in one of those
+// modes (the tile schedule, the default, has its own arrays).
+static void ensure_hybrid(rs_svd_plan* pl) {
+    if (pl->hybrid_built) return;
+    hipStream_t s = pl->ctx->stream;
+    // items / ratings padded by 128 entries: the kernels read 32-entry chunks up to two ahead
+    // (entries < e + 96 for a row ending at e)
+    std::vector<float> v(pl->h_vals);
+    v.resize(v.size() + 128, 0.f);
+    plan_sync_last(pl);
+    pl->ratings.alloc(v.size());
+    pl->ratings.upload(v.data(), v.size(), s);
+    build_items(pl);
+    build_work(pl);
+    pl->hybrid_built = true;
+    RS_HIP(hipStreamSynchronize(s));
+}
+
 // Plan from a user-CSR (data order inside each row); the COO entry point builds it first.
 static void plan_build_csr(rs_ctx* ctx, int32_t n_users, int32_t n_items, UserCSR&& csr, int32_t k,
                            rs_svd_plan* pl) {
@@ -1339,29 +1280,26 @@ static void plan_build_csr(rs_ctx* ctx, int32_t n_users, int32_t n_items, UserCS
     pl->k = k;
     pl->ld = fast_ld(k);
     pl->nnz = static_cast<int64_t>(csr.cols.size());
-    // items / ratings padded by 128 entries: the kernels read 32-entry chunks up to two ahead
-    // (entries < e + 96 for a row ending at e)
     {
         double sum = 0.0;
         for (float v : csr.vals) sum += v;
         pl->mean_rating = pl->nnz > 0 ? sum / static_cast<double>(pl->nnz) : 0.0;
     }
-    csr.vals.resize(csr.vals.size() + 128, 0.f);
-    pl->ratings.alloc(csr.vals.size());
-    pl->ratings.upload(csr.vals.data(), csr.vals.size(), s);
     pl->h_rowptr = std::move(csr.rowptr);
     pl->h_cols = std::move(csr.cols);
+    pl->h_vals = std::move(csr.vals);
     pl->P.alloc(static_cast<size_t>(std::max(1, n_users)) * pl->ld);
     RS_HIP(hipMemsetAsync(pl->P.p, 0, pl->P.n * sizeof(float), s));
+    pl->Q.alloc(static_cast<size_t>(std::max(1, n_items)) * pl->ld);
+    RS_HIP(hipMemsetAsync(pl->Q.p, 0, pl->Q.n * sizeof(float), s));
+    pl->n_qrows = n_items;
     static const bool trace = std::getenv("RSGPU_FIT_TRACE") != nullptr;
     auto t0 = std::chrono::steady_clock::now();
-    build_items(pl);
-    auto t1 = std::chrono::steady_clock::now();
-    build_work(pl);
+    if (pl->write_back == RS_SGD_WB_TILE) tile_build(pl);
+    else ensure_hybrid(pl);
     if (trace)
-        std::fprintf(stderr, "fit-trace   items %8.3f ms, work %8.3f ms\n",
-                     std::chrono::duration<double, std::milli>(t1 - t0).count(),
-                     std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t1).count());
+        std::fprintf(stderr, "fit-trace   schedule %8.3f ms\n",
+                     std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count());
     pl->gb.alloc(1);
     RS_HIP(hipMemsetAsync(pl->gb.p, 0, sizeof(double), s));
     RS_HIP(hipEventCreate(&pl->ev0));
@@ -1496,12 +1434,13 @@ static void plan_epochs(rs_svd_plan* pl, int32_t epochs, float lr, float reg, hi
     // Fixed-point runs without item splitting keep Q in int32 for all their epochs: one conversion
     // each way per call, and per epoch the SGD kernel plus one epilogue launch (merge rounds, split
     // rows, GlobalBias fold) instead of six small launches.
-    const bool hoist = pl->fixed_q && pl->write_back == RS_SGD_WB_ATOMIC && pl->n_isplit == 0 && epochs > 0;
+    const bool tile = pl->write_back == RS_SGD_WB_TILE;
+    const bool hoist = (tile || (pl->fixed_q && pl->write_back == RS_SGD_WB_ATOMIC && pl->n_isplit == 0)) && epochs > 0;
     const int64_t qn = static_cast<int64_t>(pl->Q.n);
     const int fx_blocks = static_cast<int>(std::min<int64_t>(2048, (qn + 255) / 256));
     if (hoist) {
         hipLaunchKernelGGL(svd_q_fixed_kernel, dim3(fx_blocks), dim3(256), 0, s, pl->Q.p, qn, 1);
-        if (pl->n_live > 0) {
+        if (!tile && pl->n_live > 0) {
             hipLaunchKernelGGL(svd_live_merge_kernel, dim3(pl->n_live), dim3(64), 0, s, pl->Q.p, pl->live_meta.p,
                                pl->qlast.p, pl->ld, 0);
             RS_HIP(hipMemsetAsync(pl->done.p, 0, sizeof(int32_t), s));
@@ -1515,12 +1454,13 @@ static void plan_epochs(rs_svd_plan* pl, int32_t epochs, float lr, float reg, hi
             if (pl->timing) RS_HIP(hipEventRecord(pl->tev[2 * e], s));
             launch_fast(pl, lr, reg, s);
             if (pl->timing) RS_HIP(hipEventRecord(pl->tev[2 * e + 1], s));
-            hipLaunchKernelGGL(svd_epoch_epilogue_kernel, dim3(pl->n_live + pl->n_split + 1), dim3(256), 0, s,
+            const int32_t n_live = tile ? 0 : pl->n_live, n_split = tile ? pl->t_n_split : pl->n_split;
+            hipLaunchKernelGGL(svd_epoch_epilogue_kernel, dim3(n_live + n_split + 1), dim3(256), 0, s,
                                reinterpret_cast<int32_t*>(pl->Q.p), pl->live_meta.p,
-                               reinterpret_cast<int32_t*>(pl->qlast.p), pl->n_live, pl->P.p, pl->dPs.p,
-                               pl->split_rows.p, pl->n_split, pl->ld, pl->partial.p,
+                               reinterpret_cast<int32_t*>(pl->qlast.p), n_live, pl->P.p, pl->dPs.p,
+                               tile ? pl->t_split_rows.p : pl->split_rows.p, n_split, pl->ld, pl->partial.p,
                                static_cast<int64_t>(pl->n_blocks), pl->gb.p, inv_nnz,
-                               pl->n_live > 0 ? pl->done.p : nullptr);
+                               n_live > 0 ? pl->done.p : nullptr);
             RS_HIP(hipGetLastError());
         }
         pl->hoisted = false;
@@ -1536,9 +1476,7 @@ static void plan_epochs(rs_svd_plan* pl, int32_t epochs, float lr, float reg, hi
         if (pl->timing) RS_HIP(hipEventRecord(pl->tev[2 * e], s));
         launch_fast(pl, lr, reg, s);
         if (pl->timing) RS_HIP(hipEventRecord(pl->tev[2 * e + 1], s));
-        if (pl->n_split > 0)
-            hipLaunchKernelGGL(svd_merge_rows_kernel, dim3(pl->n_split), dim3(64), 0, s, pl->P.p,
-                               pl->dPs.p, pl->split_rows.p, pl->ld);
+        merge_split_rows(pl, s);
         sync_item_copies(pl, s, 0);
         hipLaunchKernelGGL(gb_fold_kernel, dim3(1), dim3(256), 0, s, pl->partial.p,
                            static_cast<int64_t>(pl->n_blocks), pl->gb.p, inv_nnz);
@@ -1674,7 +1612,7 @@ extern "C" int rs_svd_plan_epoch_delta(rs_svd_plan* pl, float lr, float reg, voi
         }
         RS_HIP(hipEventRecord(pl->ev0, s));
         rs::launch_fast(pl, lr, reg, s, static_cast<float*>(dP));
-        rs::sync_item_copies(pl, s, 0);  // hot-item copies are shard-local: merge them here
+        if (pl->write_back != RS_SGD_WB_TILE) rs::sync_item_copies(pl, s, 0);  // shard-local hot-item copies
         if (pl->timing) RS_HIP(hipEventRecord(pl->tev[1], s));
         hipLaunchKernelGGL(rs::gb_sum_kernel, dim3(1), dim3(256), 0, s, pl->partial.p,
                            static_cast<int64_t>(pl->n_blocks), static_cast<double*>(gbsum));
@@ -1725,10 +1663,8 @@ extern "C" int rs_svd_plan_epoch_qdelta(rs_svd_plan* pl, float lr, float reg, vo
         RS_HIP(hipEventRecord(pl->ev0, s));
         rs::launch_fast(pl, lr, reg, s);  // whole user rows: P stored in place (users are exclusive)
         if (pl->timing) RS_HIP(hipEventRecord(pl->tev[1], s));
-        if (pl->n_split > 0)
-            hipLaunchKernelGGL(rs::svd_merge_rows_kernel, dim3(pl->n_split), dim3(64), 0, s, pl->P.p,
-                               pl->dPs.p, pl->split_rows.p, pl->ld);
-        rs::sync_item_copies(pl, s, 0);  // copies merged into the item rows before the delta
+        rs::merge_split_rows(pl, s);
+        if (pl->write_back != RS_SGD_WB_TILE) rs::sync_item_copies(pl, s, 0);  // copies into the item rows
         if (n)
             hipLaunchKernelGGL(rs::svd_qdelta_kernel, dim3(1024), dim3(256), 0, s, pl->Q.p, pl->Q0.p,
                                pl->iw.p, static_cast<float*>(dQ), n, pl->ld);
@@ -1778,15 +1714,55 @@ extern "C" int rs_svd_plan_apply_delta(rs_svd_plan* pl, const void* dP, const vo
 
 extern "C" int rs_svd_plan_set_mode(rs_svd_plan* pl, int32_t write_back, int32_t ring_depth) {
     if (!pl) return rs::set_error(nullptr, RS_ERR_INVALID, "plan is NULL");
-    if ((write_back < RS_SGD_WB_ATOMIC || write_back > RS_SGD_WB_ATOMIC_DIRECT) && write_back != 100 && write_back != 101)
+    if ((write_back < RS_SGD_WB_TILE || write_back > RS_SGD_WB_ATOMIC) && write_back != 100 && write_back != 101)
         return rs::set_error(pl->ctx, RS_ERR_INVALID, "unknown write-back mode");
     if (ring_depth != 4 && ring_depth != 8 && ring_depth != 16)
         return rs::set_error(pl->ctx, RS_ERR_INVALID, "ring depth must be 4, 8 or 16");
-    rs::plan_sync_last(pl);  // n_blocks (the fold's partial count) follows the mode
-    pl->write_back = write_back;
-    pl->ring_depth = ring_depth;
-    pl->n_blocks = rs::fast_blocks(pl);
-    return RS_OK;
+    return rs_guard(pl->ctx, [&]() -> int {
+        rs::plan_sync_last(pl);  // n_blocks (the fold's partial count) follows the mode
+        const bool was_tile = pl->write_back == RS_SGD_WB_TILE;
+        pl->write_back = write_back;
+        pl->ring_depth = ring_depth;
+        if (write_back == RS_SGD_WB_TILE) {
+            if (!pl->tiles_built) rs::tile_build(pl);
+            pl->n_blocks = rs::tile_partials(pl);
+        } else {
+            rs::ensure_hybrid(pl);
+            if (was_tile) {  // the tile epochs trained the item rows only: refresh their copies
+                rs::sync_item_copies(pl, pl->ctx->stream, 1);
+                RS_HIP(hipStreamSynchronize(pl->ctx->stream));
+            }
+            pl->n_blocks = rs::fast_blocks(pl);
+        }
+        return RS_OK;
+    });
+}
+
+// Tile schedule parameters (RS_SGD_WB_TILE), include/rsgpu.h.
+extern "C" int rs_svd_plan_set_tiles(rs_svd_plan* pl, int32_t workgroups, int32_t waves, int32_t target,
+                                     int32_t run_cap, int32_t ring) {
+    if (!pl) return rs::set_error(nullptr, RS_ERR_INVALID, "plan is NULL");
+    if (workgroups < 0 || target < 0 || run_cap < 0 || ring < 0 ||
+        (waves != 1 && waves != 2 && waves != 4 && waves != 8 && waves != 16))
+        return rs::set_error(pl->ctx, RS_ERR_INVALID, "bad tile parameters");
+    return rs_guard(pl->ctx, [&]() -> int {
+        pl->tile_wg = workgroups;
+        pl->tile_waves = waves;
+        pl->tile_target = target;
+        pl->tile_run_cap = run_cap;
+        pl->tile_ring = ring;
+        rs::tile_build(pl);
+        if (pl->write_back == RS_SGD_WB_TILE) pl->n_blocks = rs::tile_partials(pl);
+        return RS_OK;
+    });
+}
+
+extern "C" int rs_svd_plan_tile_order(rs_svd_plan* pl, int64_t* pos, int64_t* work_off, int32_t* n_works) {
+    if (!pl) return rs::set_error(nullptr, RS_ERR_INVALID, "plan is NULL");
+    return rs_guard(pl->ctx, [&]() -> int {
+        rs::tile_order(pl, pos, work_off, n_works);
+        return RS_OK;
+    });
 }
 
 // Diagnostic timeline of the last RS_SGD_WB_ATOMIC epoch: 3 int64 per work item (LPT order) --
@@ -1814,7 +1790,7 @@ extern "C" int rs_svd_plan_set_schedule(rs_svd_plan* pl, int32_t heavy_min, int3
         if (heavy_min < 0) return rs::set_error(pl->ctx, RS_ERR_INVALID, "heavy_min must be >= 0");
         pl->heavy_min = heavy_min;
         pl->light_blocks = light_blocks < 0 ? rs::default_light_blocks(pl->ctx) : light_blocks;
-        rs::build_work(pl);
+        if (pl->hybrid_built) rs::build_work(pl);
         return RS_OK;
     });
 }
@@ -1833,7 +1809,7 @@ extern "C" int rs_svd_plan_set_split(rs_svd_plan* pl, int32_t split_cap) {
         if (split_cap < 0 || (split_cap > 0 && split_cap < 16))
             return rs::set_error(pl->ctx, RS_ERR_INVALID, "split_cap must be 0 (never) or >= 16");
         pl->split_cap = split_cap;
-        rs::build_work(pl);
+        if (pl->hybrid_built) rs::build_work(pl);
         return RS_OK;
     });
 }
@@ -1845,7 +1821,7 @@ extern "C" int rs_svd_plan_set_hot_replicas(rs_svd_plan* pl, int32_t n_hot, int3
             return rs::set_error(pl->ctx, RS_ERR_INVALID, "n_hot must be >= 0 and copies in [2, 8]");
         pl->live_req = n_hot;
         pl->live_copies = copies;
-        rs::build_items(pl);
+        if (pl->hybrid_built) rs::build_items(pl);
         return RS_OK;
     });
 }
@@ -1856,7 +1832,7 @@ extern "C" int rs_svd_plan_set_item_split(rs_svd_plan* pl, int32_t item_cap) {
         if (item_cap < 0 || (item_cap > 0 && item_cap < 16))
             return rs::set_error(pl->ctx, RS_ERR_INVALID, "item_cap must be 0 (never) or >= 16");
         pl->item_cap = item_cap;
-        rs::build_items(pl);
+        if (pl->hybrid_built) rs::build_items(pl);
         return RS_OK;
     });
 }
@@ -1953,6 +1929,7 @@ extern "C" int rs_svd_fit(rs_ctx* ctx, const rs_ratings* r, const rs_sgd_params*
                 t = t1;
             };
             rs_svd_plan pl;
+            pl.write_back = p->write_back >= RS_SGD_WB_TILE && p->write_back <= RS_SGD_WB_ATOMIC ? p->write_back : RS_SGD_WB_TILE;
             {
                 rs::UserCSR csr;
                 rs::build_csr(r->nnz, r->n_users, r->users, r->items, r->ratings, csr);
@@ -1960,7 +1937,6 @@ extern "C" int rs_svd_fit(rs_ctx* ctx, const rs_ratings* r, const rs_sgd_params*
                 rs::plan_build_csr(ctx, r->n_users, r->n_items, std::move(csr), p->n_factors, &pl);
                 mark("plan");
             }
-            pl.write_back = p->write_back >= RS_SGD_WB_ATOMIC && p->write_back <= RS_SGD_WB_ATOMIC_DIRECT ? p->write_back : RS_SGD_WB_ATOMIC;
             if (p->n_epochs > 0) *gb = rs::gb_warm_start(r, bu, bi);
             mark("warm");
             rs::plan_upload(&pl, P, Q, bu, bi, gb);

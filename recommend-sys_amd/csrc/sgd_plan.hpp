@@ -1,0 +1,149 @@
+// sgd_plan.hpp -- the device-resident SVD plan shared by sgd.hip (hybrid / direct / ordered
+// schedules, C-ABI) and sgd_tile.hip (tile schedule, the FAST default).
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+#include <vector>
+
+#include "common.hpp"
+#include "wave.hpp"
+
+struct rs_svd_plan {
+    rs_ctx* ctx = nullptr;
+    int32_t n_users = 0, n_items = 0, k = 0, ld = 0, n_work = 0;
+    int64_t nnz = 0;
+    std::vector<int64_t> h_rowptr;  // host user-CSR row pointers (work items are rebuilt from it)
+    std::vector<int32_t> h_cols;    // host user-CSR item ids (item copies are rebuilt from it)
+    rs::DevBuf<int32_t> items;      // user-CSR item rows (copies of split items), padded by 128
+    rs::DevBuf<float> ratings;
+    rs::DevBuf<int32_t> wk_user;      // work items: user, [begin, end) into the CSR, len / deg
+    rs::DevBuf<int64_t> wk_rng;
+    rs::DevBuf<float> wk_frac;
+    // users with more ratings are split into pieces (0: never).  Default 1200, measured on the ML-1M
+    // shape with heavy_min 1000 and fixed-point Q (scripts/experiments/exp_split_sweep.py): epoch 572 -> 491 us,
+    // 20-epoch held-out RMSE 0.6676 -> 0.6684 against 0.6683 for the reference visit order
+    int32_t split_cap = 1200;
+    rs::DevBuf<float> dPs;            // split-user deltas (single GPU), zero between epochs
+    rs::DevBuf<int32_t> split_rows;   // users split into pieces
+    int32_t n_split = 0;
+    int32_t item_cap = 0;             // items with more ratings get row copies (0: never)
+    int32_t n_qrows = 0;              // item rows incl. copies (Q holds n_qrows x ld)
+    rs::DevBuf<int4> isplit_meta;     // split items: {row, first copy row, copies, frac offset}
+    rs::DevBuf<float> isplit_frac;
+    int32_t n_isplit = 0;
+    rs::DevBuf<float> P, Q;  // bias in column k
+    rs::DevBuf<double> gb, partial;
+    rs::DevBuf<float> uw;  // per-user share of this shard (multi-GPU delta mode)
+    // hot replicas: most-rated items and copies each (0: none).  Default 256 x 8, measured on the
+    // ML-1M shape (scripts/experiments/exp_replicas.py): epoch 760 -> 585 us, held-out RMSE unchanged
+    int32_t live_req = 256, live_copies = 8;
+    int32_t n_live = 0;
+    rs::DevBuf<int4> live_meta;  // {item row, first extra row, copies, -}
+    rs::DevBuf<float> qlast;     // last merged value of every live item (n_live x ld)
+    rs::DevBuf<int32_t> done;    // blocks finished (the merger's exit condition)
+    rs::DevBuf<float> iw;  // per-item share of this shard (user-sharded multi-GPU mode)
+    rs::DevBuf<float> Q0;  // Q at the epoch start (user-sharded mode)
+    int32_t n_blocks = 0;
+    int32_t write_back = RS_SGD_WB_TILE;
+    int32_t heavy_min = 1000;  // work items with at least this many ratings get a producer + 3 writers
+    int32_t n_heavy = 0;       // leading (LPT-ordered) work items that are heavy
+    int32_t light_blocks = 0;  // cap on the light blocks (each wave strides over light items; 0 = none)
+    rs::DevBuf<int64_t> trace;  // diagnostic: {start, chain end, drained} per work item (RS_SGD_WB_ATOMIC)
+    // q_i prefetch distance of the light waves: 16 since the end of round 1 (ML-1M shape with the
+    // default schedule: epoch 435 -> 428 us, held-out RMSE 0.6685 either way; exp_split_sweep.py)
+    int32_t ring_depth = 16;
+    int32_t fixed_q = 1;           // hybrid epochs keep Q as int32 fixed point (rs_svd_plan_set_fixed_q)
+    bool live_merged = false;      // the fixed-point epoch already ran the live items' final round
+    bool hoisted = false;          // plan_epochs: Q stays int32 across epochs, the epilogue re-arms done
+    double mean_rating = 0.0;  // of the plan's ratings (FAST GlobalBias warm start at init)
+    hipEvent_t ev0 = nullptr, ev1 = nullptr;
+    double last_ms = 0.0;
+    int32_t last_launches = 0;
+    bool timing = false;
+    hipStream_t last_stream = nullptr;  // stream of the last enqueued epochs (synced before copies)
+    std::vector<hipEvent_t> tev;        // timing mode: [2 * epoch] start, [2 * epoch + 1] end
+    int32_t tev_used = 0;
+    // tile schedule (RS_SGD_WB_TILE, the default; sgd_tile.hip): users cut into tiles whose P rows
+    // stay in one workgroup's LDS for the epoch, the tile's ratings grouped into per-item runs
+    int32_t tile_wg = 0;      // workgroups of the launch (0 = one per CU)
+    int32_t tile_waves = 16;  // waves per workgroup (1, 2, 4, 8 or 16)
+    int32_t tile_target = 0;  // ratings per tile (0 = nnz / workgroups, bounded by the LDS)
+    int32_t tile_run_cap = 0; // runs longer than this are cut over waves (0 = never)
+    int32_t tile_ring = 0;    // q_i rows prefetched per wave (0 = auto: 12, fewer for wide rows)
+    int32_t n_tiles = 0, tile_grid = 0;
+    size_t tile_lds = 0;      // dynamic LDS bytes of the launch (the largest tile)
+    bool tiles_built = false, hybrid_built = false;
+    std::vector<float> h_vals;  // host user-CSR ratings (the hybrid structures are built lazily)
+    rs::DevBuf<int4> t_tiles;   // {first user (into t_users), users, first run, first record}
+    rs::DevBuf<int2> t_users;       // tile entries {user, frac bits} (frac < 1: a piece of a split user)
+    rs::DevBuf<int32_t> t_streams;  // per tile: waves + 1 run offsets
+    rs::DevBuf<int2> t_runs;    // {item, first record (tile-local)}, a sentinel after each tile
+    rs::DevBuf<int2> t_recs;    // {user (tile-local), rating bits}
+    rs::DevBuf<int32_t> t_split_rows;  // users cut into pieces over several tiles
+    int32_t t_n_split = 0;
+    ~rs_svd_plan() {
+        if (ev0) (void)hipEventDestroy(ev0);
+        if (ev1) (void)hipEventDestroy(ev1);
+        for (hipEvent_t e : tev) (void)hipEventDestroy(e);
+    }
+};
+
+namespace rs {
+constexpr int32_t kOutOfRange = 0x7FFFFFF0;  // buffer offset past num_records: load 0 / drop store
+constexpr int kSgdAux = 16;                  // sc1
+// Fixed-point rows (2^-24 resolution, |v| < 128): see sgd.hip
+constexpr float kFx = 16777216.f, kFxInv = 1.f / 16777216.f;
+
+// Sum over the 64 lanes of a wave: DPP inside each 16-lane row, then the gfx950 permlane swaps
+// across rows.  Every lane ends with the bitwise-identical total.
+__device__ __forceinline__ float wave_sum(float x) {
+    x = group_sum<16>(x);
+    auto r16 = __builtin_amdgcn_permlane16_swap(__float_as_uint(x), __float_as_uint(x), false, false);
+    x = __uint_as_float(r16[0]) + __uint_as_float(r16[1]);
+    auto r32 = __builtin_amdgcn_permlane32_swap(__float_as_uint(x), __float_as_uint(x), false, false);
+    return __uint_as_float(r32[0]) + __uint_as_float(r32[1]);
+}
+
+// Fixed-point item rows (rs_svd_plan_set_fixed_q): during a hybrid FAST epoch Q holds
+// round(q * 2^24) as int32 and the q_i deltas are integer atomics.  Measured on gfx950
+// (scripts/experiments/exp_atomics.hip, exp_atomics2.hip): memory-side u32 atomic adds sustain 1.69 TB/s of
+// added bytes against 1.32 TB/s for f32 -- and the epoch is bound by that rate.  The resolution
+// 2^-24 is the fp32 ulp at |q| in [0.5, 1); the range is |q| < 128 (v_cvt_i32_f32 saturates).
+// Integer adds are exact and associative, so the sum of the deltas no longer depends on their order.
+__device__ __forceinline__ float fx_to_f(uint32_t bits) { return static_cast<float>(static_cast<int32_t>(bits)) * kFxInv; }
+__device__ __forceinline__ int32_t fx_delta(float qn, float q) { return __float2int_rn((qn - q) * kFx); }
+
+// Row layout of the FAST plan: lane l's register x holds column l + 64 x, except lane 63's last
+// register, which holds the bias in column kf (right after the kf factors).  The other lanes of the
+// last register whose column is >= kf are padding: never loaded (they read 0) and never written, so
+// the 64-B lines past column kf get no memory request at all -- row atomics are priced per 64-B line,
+// not per dword (scripts/experiments/exp_atomics2.hip: 1.69 -> 1.93 TB/s of row bytes with one line of eight
+// masked off); k = 100 rows take 7 line requests instead of 8.
+template <int E>
+__device__ __forceinline__ int32_t last_col(int lane, int32_t kf) {  // column of register E-1, or -1
+    const int32_t c = lane == 63 ? kf : lane + 64 * (E - 1);
+    return (lane == 63 || c < kf) ? c : -1;
+}
+// byte offset of register x of this lane in the row at byte offset `row` (kOutOfRange: padding)
+template <int E>
+__device__ __forceinline__ int32_t roff(int32_t row, int x, int32_t lane4, int32_t lc) {
+    return x < E - 1 ? row + lane4 + 256 * x : (lc >= 0 ? row + 4 * lc : kOutOfRange);
+}
+
+__device__ __forceinline__ float lane63(float x) {
+    return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(x), 63));
+}
+
+// sgd.hip
+void plan_sync_last(rs_svd_plan* pl);  // waits for the stream of the last enqueued epochs
+
+// sgd_tile.hip
+void tile_build(rs_svd_plan* pl);  // (re)builds the tile schedule from the host CSR
+void tile_launch(rs_svd_plan* pl, float lr, float reg, hipStream_t s, float* dP);  // one epoch (Q int32)
+int32_t tile_partials(const rs_svd_plan* pl);  // GlobalBias partials the launch writes
+// visit order of the tile schedule (user-CSR positions, nnz entries) and its GlobalBias work items
+// (one per tile and wave: n_works + 1 offsets into pos); any pointer may be NULL
+void tile_order(rs_svd_plan* pl, int64_t* pos, int64_t* work_off, int32_t* n_works);
+}  // namespace rs

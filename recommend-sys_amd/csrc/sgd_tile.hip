@@ -1,0 +1,524 @@
+// sgd_tile.hip -- K1 tile schedule (RS_SGD_WB_TILE, the FAST default): the SGD epoch of the Funk-SVD
+// model (reference core/svd.go:92-130) with the user rows held in LDS and the item rows combined
+// per workgroup, gfx950.
+//
+// Why (measured): every schedule that writes each rating's q_i update to memory is
+// bound by the memory-side atomic unit (u32 adds 1.69 TB/s on gfx950, float adds 1.3 TB/s: one
+// 448-B row per rating at k = 100 is 0.45 GB per ML-1M epoch, >= 265 us).  Integer LDS atomics, on
+// the other hand, run at the LDS write rate (scripts/experiments/exp_lds_atomics.hip: ds_add_u32
+// 8.7 cycles per 512-B row per CU at 16 waves, the same as ds_write_b32; ds_add_f32 is 44x slower).
+// So the epoch is reorganised around them:
+//
+//   * Users are cut into TILES (consecutive users, about nnz / #CUs ratings each, bounded by the
+//     LDS).  One workgroup of NW waves owns a tile at a time: its P rows are staged into LDS as
+//     int32 fixed point round(p * 2^24) and every p_u update is a ds_add_u32 of the rounded delta --
+//     exact and order-free, so the NW waves share the rows without locks (Hogwild inside the CU, no
+//     update lost).  Tiles hold disjoint users, so P needs no cross-CU coherence at all.
+//   * The tile's ratings are grouped into RUNS, one per item (the item's ratings by the tile's
+//     users).  A wave takes a run, loads q_i once (an sc1 load of the int32 row), applies the run's
+//     ratings one after the other with q_i in VGPRs -- the sequential update order of svd.go:97-128
+//     inside the run, including the aliasing Q1 (q_i moves with the NEW p_u) -- and adds the
+//     run's total delta to memory with one integer atomic per row line.  The memory-side traffic
+//     per epoch drops from one row per rating to one row per (item, tile) pair: 1.0M -> 0.44M rows
+//     on the ML-1M shape with 256 tiles.
+//   * Runs are dealt to the waves of a tile in a per-tile pseudo-random order (longest-first
+//     balancing over waves), so a hot item's runs are spread over the epoch in time: the staleness
+//     of a hot q_i (updates other workgroups hold in registers while this one reads it) stays at
+//     ~ deg * run time / epoch, a few tens of ratings, like the per-rating schedules.
+//
+// GlobalBias (Q2) is a per-wave local SGD copy folded at epoch end (gb += sum n_w (gb_w - gb)/nnz,
+// fixed order), as in the other FAST schedules.  A user too heavy for one tile's LDS is cut into
+// pieces in different tiles, each from the same p_u, merged by count-weighted average after the
+// epoch (as rs_svd_plan_set_split).
+//
+// Visit order: tile by tile, a tile's runs in their dealt order, a run's ratings in user order.  With
+// one workgroup of one wave the kernel is the sequential SGD in that order (rs_svd_plan_tile_order
+// exports it; tests/test_tile_gpu.py restates it with the ORDERED oracle).
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstring>
+#include <numeric>
+#include <stdexcept>
+#include <thread>
+#include <vector>
+
+#include "common.hpp"
+#include "sgd_plan.hpp"
+#include "wave.hpp"
+
+namespace rs {
+
+constexpr size_t kTileLdsBudget = 160 * 1024 - 512;  // gfx950: 160 KiB of LDS per workgroup
+
+template <int E, int NW, int RQ>
+__global__ __launch_bounds__(NW * 64) void svd_epoch_tile_kernel(
+    const int4* __restrict__ tiles, int32_t n_tiles, const int2* __restrict__ tile_users,
+    const int32_t* __restrict__ streams, const int2* __restrict__ runs, const int2* __restrict__ recs,
+    float* __restrict__ P, int32_t* Q, int32_t q_bytes, const double* __restrict__ gb_in,
+    double* __restrict__ gb_partial, float lr, float reg, float* __restrict__ dP,
+    const float* __restrict__ uw, float* __restrict__ dPs, int32_t kf) {
+#pragma clang fp contract(fast)
+    constexpr int LD = 64 * E, NT = NW * 64;
+    static_assert(2 * E * RQ <= 60, "ring loads and atomics must fit the 63-op vmcnt");
+    extern __shared__ __align__(16) int32_t lds[];
+    const int tid = static_cast<int>(threadIdx.x), lane = tid & 63;
+    const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int32_t lane4 = lane * 4;
+    const int32_t lc = last_col<E>(lane, kf);
+    const bool bias_lane = lane == 63;
+    const __amdgpu_buffer_rsrc_t rq = __builtin_amdgcn_make_buffer_rsrc(Q, 0, q_bytes, 0x00020000);
+    const double gb0 = gb_in[0];
+    const float a = 1.f - lr * reg;
+    int32_t pcol[E];  // LDS column of register x of this lane (-1: padding, never touched)
+#pragma unroll
+    for (int x = 0; x < E; ++x) pcol[x] = x < E - 1 ? lane + 64 * x : lc;
+    double contrib = 0.0;
+
+    for (int32_t t = static_cast<int32_t>(blockIdx.x); t < n_tiles; t += static_cast<int32_t>(gridDim.x)) {
+        const int4 tm = tiles[t];  // {first user entry, entries, first run, first record}
+        const int32_t nu = tm.y;
+        const int32_t* sp = streams + static_cast<int64_t>(t) * (NW + 1);
+        const int32_t n_runs = sp[NW];
+        const int2* tr = runs + tm.z;  // n_runs + 1 entries: a sentinel holds the record count
+        const int32_t n_rec = tr[n_runs].y;
+        int32_t* Pl = lds;
+        int2* Rl = reinterpret_cast<int2*>(lds + nu * LD);
+        int2* Ul = Rl + n_rec;
+        // stage the tile: P rows as int32 fixed point, records, runs
+        for (int32_t x = tid; x < nu * LD; x += NT) {
+            const int32_t ul = x / LD, c = x - ul * LD;
+            const float v = P[static_cast<int64_t>(tile_users[tm.x + ul].x) * LD + c];
+            Pl[x] = __float2int_rn(v * kFx);
+        }
+        for (int32_t x = tid; x < n_rec; x += NT) Rl[x] = recs[tm.w + x];
+        for (int32_t x = tid; x <= n_runs; x += NT) Ul[x] = tr[x];
+        __syncthreads();
+
+        const int32_t r0 = sp[w], r1 = sp[w + 1];
+        auto item_of = [&](int32_t r) -> int32_t {
+            return r < r1 ? __builtin_amdgcn_readfirstlane(Ul[r].x) : -1;
+        };
+        auto load_q = [&](int32_t (&q)[E], int32_t item) {
+            const int32_t row = item >= 0 ? item * (LD * 4) : kOutOfRange;  // SGPR arithmetic
+#pragma unroll
+            for (int x = 0; x < E; ++x)
+                q[x] = static_cast<int32_t>(
+                    __builtin_amdgcn_raw_buffer_load_b32(rq, roff<E>(row, x, lane4, lc), 0, kSgdAux));
+        };
+        int32_t ring[RQ][E];
+#pragma unroll
+        for (int s = 0; s < RQ; ++s) {
+            load_q(ring[s], item_of(r0 + s));
+            // dropped atomics (out-of-range offsets): the loop is entered with the same pattern of
+            // loads and atomics in flight as its back edge carries, so the compiler's vmcnt waits
+            // keep the whole ring in flight instead of draining to the prologue's count
+#pragma unroll
+            for (int x = 0; x < E; ++x) {  // per-lane offsets and value: not folded into one lane
+                int32_t z;
+                asm volatile("v_mov_b32 %0, 0" : "=v"(z));
+                __builtin_amdgcn_raw_ptr_buffer_atomic_add_i32(z, rq, roff<E>(kOutOfRange, x, lane4, lc), 0, 0);
+            }
+        }
+        double gb = gb0;
+        int32_t nr = 0;
+        for (int32_t r = r0; r < r1; r += RQ) {
+#pragma unroll
+            for (int s = 0; s < RQ; ++s) {
+                const int32_t rr = r + s;
+                const bool live = rr < r1;  // wave-uniform
+                int32_t q0[E];
+                float q[E];
+#pragma unroll
+                for (int x = 0; x < E; ++x) {
+                    // a real copy: ring[s] is then dead and its refill lands in the same registers (a
+                    // coalesced copy would keep both live and the compiler would rotate the ring with
+                    // moves at the loop back edge, waiting for every load in flight there)
+                    asm volatile("v_mov_b32 %0, %1" : "=v"(q0[x]) : "v"(ring[s][x]));
+                    q[x] = fx_to_f(static_cast<uint32_t>(q0[x]));
+                }
+                int32_t item = -1, b = 0, e = 0;
+                if (live) {
+                    item = __builtin_amdgcn_readfirstlane(Ul[rr].x);
+                    b = __builtin_amdgcn_readfirstlane(Ul[rr].y);
+                    e = __builtin_amdgcn_readfirstlane(Ul[rr + 1].y);
+                }
+                load_q(ring[s], item_of(rr + RQ));  // refill: every slot issues E loads + E atomics
+                for (int32_t cb = b; cb < e; cb += 64) {
+                    const int32_t cn = min(64, e - cb);
+                    int2 rc = make_int2(0, 0);
+                    if (lane < cn) rc = Rl[cb + lane];
+                    for (int32_t j = 0; j < cn; ++j) {
+                        const int32_t ul = __builtin_amdgcn_readlane(rc.x, j);
+                        const float rt = __int_as_float(__builtin_amdgcn_readlane(rc.y, j));
+                        int32_t* prow = Pl + ul * LD;
+                        float p[E];
+#pragma unroll
+                        for (int x = 0; x < E; ++x)
+                            p[x] = pcol[x] >= 0 ? fx_to_f(static_cast<uint32_t>(prow[pcol[x]])) : 0.f;
+                        const float ub = lane63(p[E - 1]), bq = lane63(q[E - 1]);
+                        float sd = 0.f;
+#pragma unroll
+                        for (int x = 0; x < E - 1; ++x) sd += p[x] * q[x];
+                        sd += p[E - 1] * (bias_lane ? 0.f : q[E - 1]);
+                        sd = wave_sum(sd);
+                        // svd.go:102-128 in FMA form: a = 1 - lr*reg, c = lr*diff:
+                        // p <- a p - c q ; q <- a q - c p_new ; b <- a b - c ; gb <- gb - c
+                        const float diff = ((static_cast<float>(gb) + ub) + bq) + sd - rt;
+                        const float c = lr * diff;
+                        gb -= static_cast<double>(c);  // a double: the fold sees the exact walk
+                        const float ubn = __builtin_fmaf(ub, a, -c), bqn = __builtin_fmaf(bq, a, -c);
+#pragma unroll
+                        for (int x = 0; x < E; ++x) {
+                            float pn = __builtin_fmaf(-c, q[x], p[x] * a);
+                            float qn = __builtin_fmaf(-c, pn, q[x] * a);
+                            if (x == E - 1 && bias_lane) {
+                                pn = ubn;
+                                qn = bqn;
+                            }
+                            if (pcol[x] >= 0)
+                                __hip_atomic_fetch_add(prow + pcol[x], __float2int_rn((pn - p[x]) * kFx),
+                                                       __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                            q[x] = qn;
+                        }
+                    }
+                }
+                nr += e - b;
+                const int32_t row = live ? item * (LD * 4) : kOutOfRange;
+#pragma unroll
+                for (int x = 0; x < E; ++x)
+                    __builtin_amdgcn_raw_ptr_buffer_atomic_add_i32(__float2int_rn(q[x] * kFx) - q0[x], rq,
+                                                                   roff<E>(row, x, lane4, lc), 0, 0);
+            }
+        }
+        contrib += static_cast<double>(nr) * (gb - static_cast<double>(gb0));
+        __syncthreads();
+        // write the tile's P rows back: whole users stored (or their weighted delta to dP in
+        // multi-GPU delta mode), pieces of split users as count-weighted deltas
+        for (int32_t x = tid; x < nu * LD; x += NT) {
+            const int32_t ul = x / LD, c = x - ul * LD;
+            const int2 te = tile_users[tm.x + ul];  // {user, frac bits}
+            const float frac = __int_as_float(te.y);
+            const int64_t g = static_cast<int64_t>(te.x) * LD + c;
+            const float v = fx_to_f(static_cast<uint32_t>(Pl[x]));
+            if (dP) {
+                const float d = uw[te.x] * frac * (v - P[g]);
+                if (frac == 1.f) dP[g] = d;
+                else atomicAdd(dP + g, d);
+            } else if (frac == 1.f) {
+                P[g] = v;
+            } else {
+                atomicAdd(dPs + g, frac * (v - P[g]));
+            }
+        }
+        __syncthreads();  // the next tile's staging overwrites the LDS
+    }
+    if (lane == 0) gb_partial[static_cast<int64_t>(blockIdx.x) * NW + w] = contrib;
+}
+
+namespace {
+
+uint32_t mix32(uint64_t x) {
+    x += 0x9e3779b97f4a7c15ULL;
+    x = (x ^ (x >> 30)) * 0xbf58476d1ce4e5b9ULL;
+    x = (x ^ (x >> 27)) * 0x94d049bb133111ebULL;
+    return static_cast<uint32_t>((x ^ (x >> 31)) >> 16);
+}
+
+struct TileHost {
+    std::vector<int4> tiles;
+    std::vector<int2> users;      // {user, frac bits}
+    std::vector<int32_t> streams; // per tile NW + 1
+    std::vector<int2> runs, recs;
+    std::vector<int64_t> pos;     // CSR position of every record (want_pos only)
+    std::vector<int32_t> split;   // users cut into pieces
+    size_t lds = 0;
+};
+
+int32_t device_cus(const rs_ctx* ctx) {
+    int cus = 0;
+    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, ctx->device) != hipSuccess || cus <= 0)
+        cus = 256;
+    return cus;
+}
+
+size_t tile_bytes(int64_t users, int64_t recs, int64_t runs, int32_t ld) {
+    return static_cast<size_t>(users) * ld * 4 + static_cast<size_t>(recs) * 8 + static_cast<size_t>(runs + 1) * 8;
+}
+
+// Tiles from the host user-CSR.  Entries (user pieces) are consecutive users; a tile closes when the
+// next entry would pass the rating target or the LDS bound (runs <= records).  A user whose ratings
+// do not fit one tile's LDS is cut into near-equal pieces (count-weighted merge after the epoch).
+void build_tile_host(const rs_svd_plan* pl, int32_t nw, int64_t target, int32_t run_cap, bool want_pos,
+                     TileHost& th) {
+    const std::vector<int64_t>& rp = pl->h_rowptr;
+    const int32_t ld = pl->ld;
+    // one entry alone must fit: ld*4 + d*16 + 8 <= budget
+    const int64_t rec_cap = static_cast<int64_t>((kTileLdsBudget - 16 - static_cast<size_t>(ld) * 4) / 16);
+    if (rec_cap < 64) throw std::invalid_argument("n_factors too large for the tile schedule's LDS");
+    struct Ent { int32_t u; int64_t b, e; float frac; };
+    std::vector<Ent> ents;
+    for (int32_t u = 0; u < pl->n_users; ++u) {
+        const int64_t d = rp[u + 1] - rp[u];
+        if (d == 0) continue;
+        const int64_t cap = std::min<int64_t>(rec_cap, std::max<int64_t>(target, 1));
+        const int64_t pieces = d > rec_cap ? (d + cap - 1) / cap : 1;
+        if (pieces > 1) th.split.push_back(u);
+        for (int64_t x = 0; x < pieces; ++x) {
+            const int64_t b = rp[u] + d * x / pieces, e = rp[u] + d * (x + 1) / pieces;
+            ents.push_back({u, b, e, pieces > 1 ? static_cast<float>(static_cast<double>(e - b) / d) : 1.f});
+        }
+    }
+    // tile boundaries over the entries
+    std::vector<size_t> tb{0};
+    {
+        int64_t nu = 0, nrec = 0;
+        for (size_t x = 0; x < ents.size(); ++x) {
+            const int64_t d = ents[x].e - ents[x].b;
+            if (nu > 0 && (nrec + d > target || tile_bytes(nu + 1, nrec + d, nrec + d, ld) > kTileLdsBudget)) {
+                tb.push_back(x);
+                nu = 0;
+                nrec = 0;
+            }
+            ++nu;
+            nrec += d;
+        }
+        if (tb.back() != ents.size()) tb.push_back(ents.size());
+    }
+    const size_t nt = tb.size() - 1;
+    // per tile: runs grouped by item in a per-tile pseudo-random item order, dealt to nw streams
+    struct Local {
+        std::vector<int32_t> st;   // nw + 1 run offsets
+        std::vector<int2> runs;    // + sentinel
+        std::vector<int2> recs;
+        std::vector<int64_t> pos;
+    };
+    std::vector<Local> loc(nt);
+    const std::vector<int32_t>& cols = pl->h_cols;
+    const std::vector<float>& vals = pl->h_vals;
+    auto build_one = [&](size_t t) {
+        Local& L = loc[t];
+        struct R { uint32_t key; int32_t item; int32_t ul; int64_t p; };
+        std::vector<R> v;
+        for (size_t x = tb[t]; x < tb[t + 1]; ++x)
+            for (int64_t p = ents[x].b; p < ents[x].e; ++p)
+                v.push_back({mix32((static_cast<uint64_t>(cols[p]) << 20) ^ (t * 0x9E3779B1ULL)), cols[p],
+                             static_cast<int32_t>(x - tb[t]), p});
+        std::sort(v.begin(), v.end(), [](const R& x, const R& y) {
+            return x.key != y.key ? x.key < y.key : (x.item != y.item ? x.item < y.item : x.ul < y.ul);
+        });
+        // runs: maximal equal-item groups; with run_cap (and more than one wave) cut into pieces that
+        // go to different waves (two pieces in one wave's ring reach would read q_i before the
+        // earlier piece's atomic landed)
+        struct Run { size_t b, e; int32_t piece; };
+        std::vector<Run> rs_;
+        const size_t cap = (run_cap > 0 && nw > 1) ? static_cast<size_t>(run_cap) : 0;
+        for (size_t x = 0; x < v.size();) {
+            size_t y = x;
+            while (y < v.size() && v[y].item == v[x].item) ++y;
+            const size_t pieces = cap ? std::min<size_t>((y - x + cap - 1) / cap, static_cast<size_t>(nw)) : 1;
+            for (size_t c = 0; c < pieces; ++c)
+                rs_.push_back({x + (y - x) * c / pieces, x + (y - x) * (c + 1) / pieces, static_cast<int32_t>(c)});
+            x = y;
+        }
+        // deal (in key order) to the least-loaded stream; cost ~ ratings + a run start.  The pieces
+        // of one item take distinct streams.
+        std::vector<int64_t> load(nw, 0);
+        std::vector<std::vector<size_t>> sr(nw);
+        std::vector<uint8_t> used(nw, 0);
+        for (size_t r = 0; r < rs_.size(); ++r) {
+            if (rs_[r].piece == 0) std::fill(used.begin(), used.end(), 0);
+            int best = -1;
+            for (int s = 0; s < nw; ++s)
+                if (!used[s] && (best < 0 || load[s] < load[best])) best = s;
+            used[best] = 1;
+            load[best] += static_cast<int64_t>(rs_[r].e - rs_[r].b) + 2;
+            sr[best].push_back(r);
+        }
+        L.st.assign(nw + 1, 0);
+        for (int s = 0; s < nw; ++s) {
+            L.st[s] = static_cast<int32_t>(L.runs.size());
+            for (size_t r : sr[s]) {
+                L.runs.push_back(make_int2(v[rs_[r].b].item, static_cast<int32_t>(L.recs.size())));
+                for (size_t x = rs_[r].b; x < rs_[r].e; ++x) {
+                    int32_t bits;
+                    std::memcpy(&bits, &vals[v[x].p], 4);
+                    L.recs.push_back(make_int2(v[x].ul, bits));
+                    if (want_pos) L.pos.push_back(v[x].p);
+                }
+            }
+        }
+        L.st[nw] = static_cast<int32_t>(L.runs.size());
+        L.runs.push_back(make_int2(-1, static_cast<int32_t>(L.recs.size())));  // sentinel
+    };
+    {
+        const int nth = static_cast<int>(std::min<size_t>(16, std::max<size_t>(1, nt / 64)));
+        std::vector<std::thread> th;
+        for (int c = 0; c < nth; ++c)
+            th.emplace_back([&, c] {
+                for (size_t t = c; t < nt; t += nth) build_one(t);
+            });
+        for (std::thread& x : th) x.join();
+    }
+    th.tiles.resize(nt);
+    th.streams.reserve(nt * (nw + 1));
+    int64_t run_off = 0, rec_off = 0;
+    for (size_t t = 0; t < nt; ++t) {
+        const Local& L = loc[t];
+        if (run_off + static_cast<int64_t>(L.runs.size()) >= (int64_t{1} << 31) ||
+            rec_off + static_cast<int64_t>(L.recs.size()) >= (int64_t{1} << 31))
+            throw std::invalid_argument("tile schedule: more than 2^31 runs or ratings");
+        th.tiles[t] = make_int4(static_cast<int32_t>(tb[t]), static_cast<int32_t>(tb[t + 1] - tb[t]),
+                                static_cast<int32_t>(run_off), static_cast<int32_t>(rec_off));
+        th.streams.insert(th.streams.end(), L.st.begin(), L.st.end());
+        th.runs.insert(th.runs.end(), L.runs.begin(), L.runs.end());
+        th.recs.insert(th.recs.end(), L.recs.begin(), L.recs.end());
+        if (want_pos) th.pos.insert(th.pos.end(), L.pos.begin(), L.pos.end());
+        th.lds = std::max(th.lds, tile_bytes(static_cast<int64_t>(tb[t + 1] - tb[t]), static_cast<int64_t>(L.recs.size()),
+                                             static_cast<int64_t>(L.runs.size()) - 1, ld));
+        run_off += static_cast<int64_t>(L.runs.size());
+        rec_off += static_cast<int64_t>(L.recs.size());
+        loc[t] = Local();
+    }
+    th.users.resize(ents.size());
+    for (size_t x = 0; x < ents.size(); ++x) {
+        int32_t bits;
+        std::memcpy(&bits, &ents[x].frac, 4);
+        th.users[x] = make_int2(ents[x].u, bits);
+    }
+    if (th.lds > kTileLdsBudget) throw std::logic_error("tile schedule exceeds the LDS");
+}
+
+int64_t tile_target_of(const rs_svd_plan* pl, int32_t grid) {
+    if (pl->tile_target > 0) return pl->tile_target;
+    return std::max<int64_t>(64, (pl->nnz + grid - 1) / std::max(1, grid));
+}
+
+}  // namespace
+
+int32_t tile_partials(const rs_svd_plan* pl) { return std::max(1, pl->tile_grid) * pl->tile_waves; }
+
+void tile_build(rs_svd_plan* pl) {
+    hipStream_t s = pl->ctx->stream;
+    const int32_t cus = device_cus(pl->ctx);
+    const int32_t grid0 = pl->tile_wg > 0 ? pl->tile_wg : cus;
+    TileHost th;
+    build_tile_host(pl, pl->tile_waves, tile_target_of(pl, grid0), pl->tile_run_cap, false, th);
+    plan_sync_last(pl);
+    pl->n_tiles = static_cast<int32_t>(th.tiles.size());
+    pl->tile_grid = std::max(1, std::min(grid0, pl->n_tiles));
+    pl->tile_lds = std::max<size_t>(th.lds, 16);
+    pl->t_tiles.alloc(std::max<size_t>(1, th.tiles.size()));
+    pl->t_users.alloc(std::max<size_t>(1, th.users.size()));
+    pl->t_streams.alloc(std::max<size_t>(1, th.streams.size()));
+    pl->t_runs.alloc(std::max<size_t>(1, th.runs.size()));
+    pl->t_recs.alloc(std::max<size_t>(1, th.recs.size()));
+    pl->t_tiles.upload(th.tiles.data(), th.tiles.size(), s);
+    pl->t_users.upload(th.users.data(), th.users.size(), s);
+    pl->t_streams.upload(th.streams.data(), th.streams.size(), s);
+    pl->t_runs.upload(th.runs.data(), th.runs.size(), s);
+    pl->t_recs.upload(th.recs.data(), th.recs.size(), s);
+    pl->t_n_split = static_cast<int32_t>(th.split.size());
+    pl->t_split_rows.alloc(std::max<size_t>(1, th.split.size()));
+    pl->t_split_rows.upload(th.split.data(), th.split.size(), s);
+    if (pl->t_n_split > 0 && pl->dPs.n != static_cast<size_t>(std::max(1, pl->n_users)) * pl->ld) {
+        pl->dPs.alloc(static_cast<size_t>(std::max(1, pl->n_users)) * pl->ld);
+        RS_HIP(hipMemsetAsync(pl->dPs.p, 0, pl->dPs.n * sizeof(float), s));
+    }
+    const size_t parts = static_cast<size_t>(tile_partials(pl));
+    if (pl->partial.n < parts) pl->partial.alloc(parts);
+    pl->tiles_built = true;
+    RS_HIP(hipStreamSynchronize(s));  // host vectors die with this scope
+}
+
+void tile_order(rs_svd_plan* pl, int64_t* pos, int64_t* work_off, int32_t* n_works) {
+    const int32_t cus = device_cus(pl->ctx);
+    const int32_t grid0 = pl->tile_wg > 0 ? pl->tile_wg : cus;
+    TileHost th;
+    build_tile_host(pl, pl->tile_waves, tile_target_of(pl, grid0), pl->tile_run_cap, true, th);
+    const size_t nw = th.tiles.size() * pl->tile_waves;
+    if (n_works) *n_works = static_cast<int32_t>(nw);
+    if (pos) std::copy(th.pos.begin(), th.pos.end(), pos);
+    if (work_off) {  // stream s of tile t covers records [runs[first + st[s]].y, runs[first + st[s+1]].y)
+        for (size_t t = 0; t < th.tiles.size(); ++t) {
+            const int32_t* st = th.streams.data() + t * (pl->tile_waves + 1);
+            for (int32_t s = 0; s <= pl->tile_waves; ++s) {
+                if (s == pl->tile_waves && t + 1 < th.tiles.size()) break;
+                work_off[t * pl->tile_waves + s] = th.tiles[t].w + th.runs[th.tiles[t].z + st[s]].y;
+            }
+        }
+    }
+}
+
+template <int E, int NW, int RQ>
+static void tile_launch_t(rs_svd_plan* pl, float lr, float reg, hipStream_t s, float* dP) {
+    auto kern = svd_epoch_tile_kernel<E, NW, RQ>;
+    static bool attr = false;  // per instantiation
+    if (!attr) {
+        RS_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(kern),
+                                   hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(kTileLdsBudget)));
+        attr = true;
+    }
+    const int32_t q_bytes = static_cast<int32_t>(pl->Q.n * sizeof(float));
+    hipLaunchKernelGGL(kern, dim3(pl->tile_grid), dim3(NW * 64), pl->tile_lds, s, pl->t_tiles.p, pl->n_tiles,
+                       pl->t_users.p, pl->t_streams.p, pl->t_runs.p, pl->t_recs.p, pl->P.p,
+                       reinterpret_cast<int32_t*>(pl->Q.p), q_bytes, pl->gb.p, pl->partial.p, lr, reg, dP,
+                       dP ? pl->uw.p : nullptr, pl->dPs.p, pl->k);
+}
+
+// q_i rows in flight per wave (runs ahead): the ring's loads and the runs' atomics share the wave's
+// in-order vmcnt, so a slot's load also waits for every atomic issued before it; the deeper the ring,
+// the longer an atomic has to complete before a load behind it is needed
+template <int E, int NW>
+static void tile_launch_r(rs_svd_plan* pl, float lr, float reg, hipStream_t s, float* dP) {
+    constexpr int kMax = 60 / (2 * E);  // 15 at E = 2 (k <= 127), 6 at E = 5 (k <= 319), 3 at E = 8
+    const int want = pl->tile_ring > 0 ? pl->tile_ring : 12;
+    if constexpr (kMax >= 12) {
+        if (want >= 12) return tile_launch_t<E, NW, 12>(pl, lr, reg, s, dP);
+    }
+    if constexpr (kMax >= 8) {
+        if (want >= 8) return tile_launch_t<E, NW, 8>(pl, lr, reg, s, dP);
+    }
+    if constexpr (kMax >= 6) {
+        if (want >= 6) return tile_launch_t<E, NW, 6>(pl, lr, reg, s, dP);
+    }
+    if constexpr (kMax >= 4) {
+        return tile_launch_t<E, NW, 4>(pl, lr, reg, s, dP);
+    } else {
+        return tile_launch_t<E, NW, kMax>(pl, lr, reg, s, dP);
+    }
+}
+
+template <int E>
+static void tile_launch_w(rs_svd_plan* pl, float lr, float reg, hipStream_t s, float* dP) {
+    switch (pl->tile_waves) {
+        case 1: tile_launch_r<E, 1>(pl, lr, reg, s, dP); break;
+        case 2: tile_launch_r<E, 2>(pl, lr, reg, s, dP); break;
+        case 4: tile_launch_r<E, 4>(pl, lr, reg, s, dP); break;
+        case 8: tile_launch_r<E, 8>(pl, lr, reg, s, dP); break;
+        default: tile_launch_r<E, 16>(pl, lr, reg, s, dP); break;
+    }
+}
+
+void tile_launch(rs_svd_plan* pl, float lr, float reg, hipStream_t s, float* dP) {
+    if (!pl->tiles_built) tile_build(pl);
+    pl->n_blocks = tile_partials(pl);
+    if (pl->n_tiles == 0) {  // no ratings: the fold still reads its partials
+        RS_HIP(hipMemsetAsync(pl->partial.p, 0, pl->partial.n * sizeof(double), s));
+        return;
+    }
+    switch (pl->ld / 64) {
+        case 1: tile_launch_w<1>(pl, lr, reg, s, dP); break;
+        case 2: tile_launch_w<2>(pl, lr, reg, s, dP); break;
+        case 3: tile_launch_w<3>(pl, lr, reg, s, dP); break;
+        case 4: tile_launch_w<4>(pl, lr, reg, s, dP); break;
+        case 5: tile_launch_w<5>(pl, lr, reg, s, dP); break;
+        case 6: tile_launch_w<6>(pl, lr, reg, s, dP); break;
+        case 7: tile_launch_w<7>(pl, lr, reg, s, dP); break;
+        default: tile_launch_w<8>(pl, lr, reg, s, dP); break;
+    }
+    RS_HIP(hipGetLastError());
+}
+
+}  // namespace rs

@@ -18,7 +18,7 @@
 // P, b_i in Q) sits in column k, right after the factors (lane 63 of the last register), Y's column k
 // stays 0.  Padding lanes of the last register (columns > k) are never loaded or written, and Y rows
 // skip lane 63 as well, so whole 64-B lines past the row get no request: the memory-side atomic unit
-// prices a row update per line (K1, scripts/exp_atomics2.hip).  k = 128: Q rows 9 lines of 12, Y 8.
+// prices a row update per line (K1, scripts/experiments/exp_atomics2.hip).  k = 128: Q rows 9 lines of 12, Y 8.
 // Algorithmic bytes per epoch: nnz*(16 + 8k) + U*(16 + 8k) + nnz*(4 + 12k).
 #include <hip/hip_runtime.h>
 

@@ -227,7 +227,7 @@ void SVD::Fit(const TrainSet& trainSet) {
     GlobalBias = 0.0;
     std::vector<double> P = flatten(UserFactor, k), Q = flatten(ItemFactor, k), scratch;
     rs_ratings r = Data.ratings_view(scratch);
-    rs_sgd_params p{k, epochs, lr, reg, sgd_mode(Params), RS_SGD_WB_ATOMIC};
+    rs_sgd_params p{k, epochs, lr, reg, sgd_mode(Params), RS_SGD_WB_TILE};
     if (rs_svd_fit(context(), &r, &p, P.data(), Q.data(), UserBias.data(), ItemBias.data(), &GlobalBias) != RS_OK)
         panic_rs(context(), "SVD.Fit");
     UserFactor = unflatten(P, Data.UserCount, k);
@@ -282,7 +282,7 @@ void SVDPP::Fit(const TrainSet& trainSet) {
     GlobalBias = 0.0;
     std::vector<double> P = flatten(UserFactor, k), Q = flatten(ItemFactor, k), Y = flatten(ImplFactor, k), s;
     rs_ratings r = Data.ratings_view(s);
-    rs_sgd_params p{k, epochs, lr, reg, sgd_mode(Params), RS_SGD_WB_ATOMIC};
+    rs_sgd_params p{k, epochs, lr, reg, sgd_mode(Params), RS_SGD_WB_TILE};
     if (rs_svdpp_fit(context(), &r, &p, P.data(), Q.data(), Y.data(), UserBias.data(), ItemBias.data(),
                      &GlobalBias) != RS_OK)
         panic_rs(context(), "SVDPP.Fit");

@@ -19,7 +19,7 @@ _lib = None
 RS_OK = 0
 RS_ERR_INVALID, RS_ERR_HIP, RS_ERR_NOMEM, RS_ERR_UNSUPPORTED, RS_ERR_NO_DEVICE = -1, -2, -3, -4, -5
 SGD_FAST, SGD_ORDERED = 0, 1
-WB_ATOMIC, WB_STORE, WB_ATOMIC_DIRECT = 0, 1, 2
+WB_TILE, WB_STORE, WB_ATOMIC_DIRECT, WB_ATOMIC = 0, 1, 2, 3  # WB_TILE: the default schedule
 SIM_COSINE, SIM_MSD, SIM_PEARSON = 0, 1, 2
 DEV_SLOPE_ONE = 3  # rs_knn_sims kind: SlopeOne deviation matrix (slope_one.go:64-92)
 
@@ -38,7 +38,8 @@ HEADER_SYMBOLS = (
     "rs_trainset_ids", "rs_csr_build", "rs_global_mean",
     "rs_synth_create", "rs_synth_csr", "rs_synth_destroy",
     "rs_svd_plan_set_item_weights", "rs_svd_plan_epoch_qdelta", "rs_svd_plan_apply_qdelta",
-    "rs_svd_plan_set_hot_replicas", "rs_svd_plan_set_fixed_q",
+    "rs_svd_plan_set_hot_replicas", "rs_svd_plan_set_fixed_q", "rs_svd_plan_set_tiles",
+    "rs_svd_plan_tile_order",
 )
 
 
@@ -127,6 +128,8 @@ def lib():
             "rs_svd_plan_set_item_weights": (C.c_int, [_vp, _vp]),
             "rs_svd_plan_set_hot_replicas": (C.c_int, [_vp, _i32, _i32]),
             "rs_svd_plan_set_fixed_q": (C.c_int, [_vp, _i32]),
+            "rs_svd_plan_set_tiles": (C.c_int, [_vp, _i32, _i32, _i32, _i32, _i32]),
+            "rs_svd_plan_tile_order": (C.c_int, [_vp, _vp, _vp, C.POINTER(_i32)]),
             "rs_svd_plan_epoch_qdelta": (C.c_int, [_vp, _flt, _flt, _vp, _vp, _vp]),
             "rs_svd_plan_apply_qdelta": (C.c_int, [_vp, _vp, _vp, _dbl, _vp]),
             "rs_synth_csr": (C.c_int, [_vp, C.POINTER(_i64), C.POINTER(_vp), C.POINTER(_vp),
@@ -284,7 +287,7 @@ class Context:
     # ---- estimators --------------------------------------------------------------------------
 
     def svd_fit(self, r: Ratings, P, Q, bu=None, bi=None, gb=0.0, n_epochs=20, lr=0.005,
-                reg=0.02, mode=SGD_FAST, write_back=WB_ATOMIC):
+                reg=0.02, mode=SGD_FAST, write_back=WB_TILE):
         P = np.array(P, dtype=np.float64, order="C")
         Q = np.array(Q, dtype=np.float64, order="C")
         bu = np.zeros(r.n_users) if bu is None else np.array(bu, dtype=np.float64)
@@ -411,8 +414,22 @@ class SvdPlan:
     def epochs(self, n, lr=0.005, reg=0.02, stream=None):
         self.ctx.check(lib().rs_svd_plan_epochs(self.h, n, lr, reg, stream))
 
-    def set_mode(self, write_back=WB_ATOMIC, ring_depth=16):
+    def set_mode(self, write_back=WB_TILE, ring_depth=16):
         self.ctx.check(lib().rs_svd_plan_set_mode(self.h, write_back, ring_depth))
+
+    def set_tiles(self, workgroups=0, waves=16, target=0, run_cap=0, ring=0):
+        """WB_TILE schedule parameters (rs_svd_plan_set_tiles); rebuilds the tiles."""
+        self.ctx.check(lib().rs_svd_plan_set_tiles(self.h, workgroups, waves, target, run_cap, ring))
+
+    def tile_order(self):
+        """(pos, work_off): user-CSR positions in the tile schedule's visit order and the boundaries
+        of its (tile, wave) GlobalBias work items (rs_svd_plan_tile_order)."""
+        nw = _i32(0)
+        self.ctx.check(lib().rs_svd_plan_tile_order(self.h, None, None, C.byref(nw)))
+        pos = np.empty(self.nnz, np.int64)
+        off = np.empty(nw.value + 1, np.int64)
+        self.ctx.check(lib().rs_svd_plan_tile_order(self.h, pos.ctypes.data, off.ctypes.data, C.byref(nw)))
+        return pos, off
 
     def set_schedule(self, heavy_min=1024, light_blocks=-1):
         """WB_ATOMIC schedule: items with >= heavy_min ratings get a producer wave + 3 writer waves;

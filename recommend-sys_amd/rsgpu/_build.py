@@ -38,6 +38,24 @@ def _headers():
     return glob.glob(os.path.join(CSRC, "*.hpp")) + glob.glob(os.path.join(INCLUDE, "*.h"))
 
 
+def _deps(path, seen=None):
+    """The source and every local header it includes (transitively)."""
+    seen = set() if seen is None else seen
+    if path in seen or not os.path.exists(path):
+        return seen
+    seen.add(path)
+    for line in open(path, errors="ignore"):
+        line = line.strip()
+        if line.startswith("#include \""):
+            name = line.split('"')[1]
+            for d in (os.path.dirname(path), CSRC, INCLUDE):
+                cand = os.path.join(d, name)
+                if os.path.exists(cand):
+                    _deps(cand, seen)
+                    break
+    return seen
+
+
 def _compile(src: str, obj: str) -> None:
     cmd = [HIPCC] + CFLAGS + ["-c", src, "-o", obj]
     if src.endswith(".cpp"):
@@ -61,7 +79,7 @@ def build(verbose: bool = False, jobs: int = 8) -> str:
     for s in srcs:
         o = os.path.join(BUILD, os.path.basename(s) + ".o")
         objs.append(o)
-        if not os.path.exists(o) or os.path.getmtime(o) < max(os.path.getmtime(s), hdr_time):
+        if not os.path.exists(o) or os.path.getmtime(o) < max(os.path.getmtime(d) for d in _deps(s)):
             todo.append((s, o))
     if todo:
         with cf.ThreadPoolExecutor(max_workers=min(jobs, len(todo))) as ex:

@@ -34,6 +34,7 @@ def test_csr_plan_equals_coo_plan_race_free(ctx, k):
     outs = []
     for plan in (ctx.svd_plan(rsgpu.Ratings(u, i, r, nu, ni), k),
                  ctx.svd_plan_csr(nu, ni, rowptr, cols, vals, k)):
+        plan.set_mode(rsgpu.WB_ATOMIC)  # the restatement's work items are user rows
         plan.upload(P0, Q0, np.zeros(nu), np.zeros(ni), 3.0)
         plan.epochs(3)
         outs.append(plan.download())

@@ -99,6 +99,7 @@ def test_fast_long_rows_race_free(ctx, k, heavy, lb, fx):
     bu0, bi0 = rng.normal(0, 0.1, nu), rng.normal(0, 0.1, ni)
     rowptr, items, rr = O.csr_by(u, nu, i, r)
     plan = ctx.svd_plan(rsgpu.Ratings(u, i, r, nu, ni), k)
+    plan.set_mode(rsgpu.WB_ATOMIC)
     plan.set_schedule(heavy, lb)
     plan.set_fixed_q(fx)
     plan.upload(P0, Q0, bu0, bi0, 3.1)
@@ -122,6 +123,7 @@ def test_fast_split_users_match_own_schedule(ctx, cap):
     rowptr, items, rr = O.csr_by(u, nu, i, r)
     assert np.diff(rowptr).max() > 2 * max(cap, 16)  # pieces really happen
     plan = ctx.svd_plan(rsgpu.Ratings(u, i, r, nu, ni), k)
+    plan.set_mode(rsgpu.WB_ATOMIC)
     plan.set_split(cap)
     plan.upload(P0, Q0, bu0, bi0, 3.1)
     plan.epochs(3)
@@ -143,6 +145,7 @@ def test_split_delta_mode_equals_direct(ctx):
     plans = []
     for _ in range(2):
         pl = ctx.svd_plan(rsgpu.Ratings(u, i, r, nu, ni), k)
+        pl.set_mode(rsgpu.WB_ATOMIC)
         pl.set_split(32)
         pl.upload(P0, Q0, np.zeros(nu), np.zeros(ni), 3.5)
         plans.append(pl)
@@ -169,6 +172,7 @@ def test_item_split_roundtrip_and_finite(ctx):
     P0, Q0 = rng.normal(0, 0.1, (nu, k)), rng.normal(0, 0.1, (ni, k))
     bi0 = rng.normal(0, 0.1, ni)
     plan = ctx.svd_plan(rsgpu.Ratings(u, i, r, nu, ni), k)
+    plan.set_mode(rsgpu.WB_ATOMIC)
     plan.set_item_split(32)
     plan.upload(P0, Q0, np.zeros(nu), bi0, 3.5)
     P, Q, bu, bi, gb = plan.download()
@@ -197,6 +201,7 @@ def test_item_split_rmse_ml100k(ctx, ml100k, item_cap):
         rowptr, items, rr = O.csr_by(f.iu, f.nu, f.ii, f.r)
         gb0 = O.gb_warm_start(rowptr, items, rr, np.zeros(f.nu), np.zeros(f.ni))
         plan = ctx.svd_plan(rsgpu.Ratings(f.iu, f.ii, f.r, f.nu, f.ni), k)
+        plan.set_mode(rsgpu.WB_ATOMIC)
         plan.set_item_split(item_cap)
         plan.upload(P0, Q0, np.zeros(f.nu), np.zeros(f.ni), gb0)
         plan.epochs(20)
@@ -206,7 +211,8 @@ def test_item_split_rmse_ml100k(ctx, ml100k, item_cap):
 
 
 def test_fast_rmse_parity_ml100k(ctx, ml100k):
-    """P2 on the reference's own dataset and test (core/base_test.go:34-36, k=100, 20 epochs)."""
+    """P2 on the reference's own dataset and test (core/base_test.go:34-36, k=100, 20 epochs), with
+    the library's default FAST schedule (the tile schedule)."""
     k = 100
     ref_r, gpu_r = [], []
     for f in folds(*ml100k):
@@ -313,6 +319,7 @@ def test_item_sharded_delta_mode_two_shards(ctx):
     for s in (0, 1):
         su, si, sr = multi.take_shard(u, i, r, sh, s)
         pl = ctx.svd_plan(rsgpu.Ratings(su, si, sr, nu, ni), k)
+        pl.set_mode(rsgpu.WB_ATOMIC)  # the host model's work items are user rows
         pl.upload(P0, Q0, np.zeros(nu), np.zeros(ni), 3.0)
         pl.set_user_weights(np.divide(cnt[s], cnt.sum(0), out=np.zeros(nu), where=cnt.sum(0) > 0))
         plans.append(pl)
@@ -354,6 +361,7 @@ def test_user_sharded_qdelta_two_shards(ctx):
     for lo, hi in user_ranges(nu, 2):
         su, si, sr = user_shard(u, i, r, lo, hi)
         pl = ctx.svd_plan(rsgpu.Ratings(su, si, sr, hi - lo, ni), k)
+        pl.set_mode(rsgpu.WB_ATOMIC)  # the host model's work items are user rows
         pl.upload(P0[lo:hi], Q0, np.zeros(hi - lo), np.zeros(ni), 3.0)
         plans.append(pl)
         cnt.append(np.bincount(si, minlength=ni))
@@ -395,7 +403,10 @@ def test_plan_predict_and_evaluate_on_device(ctx, ml100k):
     model = plan.download()
     tu, ti = f.tu.copy(), f.ti.copy()
     tu[:50], ti[50:100], tu[100:110], ti[100:110] = -1, -1, f.nu + 5, -1  # unknown users / items
-    host = rsgpu.svd_predict(tu, ti, *model)
+    # checker: the oracle's restatement of svd.go:32-51 (inner ids outside the TrainSet are newID, -1)
+    ou = np.where((tu >= 0) & (tu < f.nu), tu, -1).astype(np.int32)
+    oi = np.where((ti >= 0) & (ti < f.ni), ti, -1).astype(np.int32)
+    host = O.svd_predict(ou, oi, *model)
     dev = plan.predict(tu, ti)
     np.testing.assert_allclose(dev, host, rtol=1e-12, atol=1e-12)
     assert np.all(dev[100:110] == model[4])  # both unknown: GlobalBias only
@@ -475,6 +486,7 @@ def test_hot_replicas_rmse_parity_ml100k(ctx, ml100k):
         a = O.svd_fit(f.iu, f.ii, f.r, P0, Q0)
         ref_r.append(rmse(O.svd_predict(f.tu, f.ti, *a), f.te_r))
         plan = ctx.svd_plan(rsgpu.Ratings(f.iu, f.ii, f.r, f.nu, f.ni), k)
+        plan.set_mode(rsgpu.WB_ATOMIC)
         plan.set_hot_replicas(64, 4)
         plan.upload(P0, Q0, np.zeros(f.nu), np.zeros(f.ni), float(np.mean(f.r)))
         plan.epochs(20)
