@@ -153,7 +153,9 @@ def main():
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,
-            "dtype": "f32",
+            "dtype": "f32/fx24",  # fp32 arithmetic; P (LDS) and Q (HBM) stored as int32 round(v * 2^24)
+            "storage": "P rows int32 fixed point 2^-24 in LDS during the epoch; Q int32 fixed point 2^-24 "
+                       "in HBM during a call (fp32 outside); the deltas are integer LDS / memory-side atomics",
             "data": "synthetic ML-1M-shaped ratings (rsgpu/synth.py: 6040 users x 3706 items, "
                     "1,000,209 ratings per rank, seed 20250824+rank); random-init factors N(0,0.1)",
             "config": {"workload": "SVD nFactors=100 fast-mode SGD, 1 epoch over ML-1M-shaped set "
@@ -164,8 +166,8 @@ def main():
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
                          "traffic": traffic,
-                         "kernel": "svd_epoch_hybrid_kernel<E=2,D=8,merge,fixed-point> "
-                                   "(hot replicas 256x8, users split at 1200, 7-line rows)",
+                         "kernel": "svd_epoch_tile_kernel<E=2,NW=16,RQ=4> (tile schedule: user tiles in LDS, "
+                                   "integer LDS atomics, one memory-side atomic per (item, tile) run)",
                          "avg_kernel_us": avg_kernel_s * 1e6,
                          "timed_span": "HIP events around each epoch's SGD kernel on the launch stream "
                                        "(the per-epoch epilogue and the per-call Q fixed-point conversions "

@@ -246,9 +246,10 @@ int rs_svd_plan_epochs(rs_svd_plan* plan, int32_t n_epochs, float lr, float reg,
 int rs_svd_plan_set_mode(rs_svd_plan* plan, int32_t write_back, int32_t ring_depth);
 /* RS_SGD_WB_TILE parameters: workgroups of the launch (0 = one per CU), waves per workgroup (1, 2, 4,
  * 8 or 16; default 16), ratings per tile (0 = nnz / workgroups, bounded by the 160 KiB LDS), run cap
- * (an item's run in a tile longer than this is cut into pieces on different waves; 0 = never; ignored
- * with one wave), ring (q_i rows each wave keeps in flight: 0 = auto, else 4, 6, 8 or 12, clamped for
- * wide rows).  Rebuilds the schedule. */
+ * (an item's run in a tile longer than this is cut into pieces on different waves; 0 = auto: hot items
+ * cut so that ~100 of an item's updates are in flight; a huge value = never; ignored with
+ * one wave), ring (q_i rows each wave keeps in flight: 0 = auto, else 4, 6, 8 or 12, clamped for wide
+ * rows).  Rebuilds the schedule. */
 int rs_svd_plan_set_tiles(rs_svd_plan* plan, int32_t workgroups, int32_t waves, int32_t target,
                           int32_t run_cap, int32_t ring);
 /* Visit order of the tile schedule: pos[n] = user-CSR position (rowptr order, data order inside a row)
@@ -259,6 +260,9 @@ int rs_svd_plan_set_tiles(rs_svd_plan* plan, int32_t workgroups, int32_t waves, 
  * is exactly the sequential SGD of svd.go:93-129 in this order with the work-local GlobalBias fold
  * (the oracle's or_svd_fit_works restates it). */
 int rs_svd_plan_tile_order(rs_svd_plan* plan, int64_t* pos, int64_t* work_off, int32_t* n_works);
+/* Diagnostic (experiments): per-wave phase clocks of the last timed tile epoch (RSGPU_TILE_DIAG=16):
+ * {staging, q-ring waits, rating loops, write-back} shader cycles per wave, up to n int64 values. */
+int rs_svd_plan_tile_clocks(rs_svd_plan* plan, int64_t* out, int64_t n);
 /* RS_SGD_WB_ATOMIC schedule.  Work items with at least heavy_min ratings (default 1000; 0 = none) run
  * as one SGD wave plus three writer waves that issue its atomics; the other (light) items are
  * strided over light_blocks blocks of four waves (default < 0: 1.5 per CU; 0: one wave per item).

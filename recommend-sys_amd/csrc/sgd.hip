@@ -881,7 +881,7 @@ __global__ __launch_bounds__(64) void svd_ordered_kernel(
 
 namespace rs {
 
-constexpr int32_t kMaxFactors = 511;
+constexpr int32_t kMaxFactors = 510;  // the tile kernel's registers hold k + 2 columns (<= 512)
 
 // Light blocks of the hybrid launch: 1.5 per CU (6 light waves per CU).  Measured on the ML-1M shape
 // (DESIGN.md K1): one wave per user puts ~6,000 waves' atomics in flight and the memory-side queue
@@ -1493,7 +1493,7 @@ static int check_sgd(rs_ctx* ctx, const rs_ratings* r, const rs_sgd_params* p) {
     if (st != RS_OK) return st;
     if (!p) return set_error(ctx, RS_ERR_INVALID, "params is NULL");
     if (p->n_factors < 1 || p->n_factors > kMaxFactors)
-        return set_error(ctx, RS_ERR_UNSUPPORTED, "n_factors must be in [1, 511]");
+        return set_error(ctx, RS_ERR_UNSUPPORTED, "n_factors must be in [1, 510]");
     if (p->n_epochs < 0) return set_error(ctx, RS_ERR_INVALID, "n_epochs < 0");
     if (p->mode != RS_SGD_FAST && p->mode != RS_SGD_ORDERED)
         return set_error(ctx, RS_ERR_INVALID, "unknown SGD mode");
@@ -1514,7 +1514,7 @@ extern "C" int rs_svd_plan_create(rs_ctx* ctx, const rs_ratings* r, int32_t n_fa
         int st = rs::check_ratings(ctx, r);
         if (st != RS_OK) return st;
         if (n_factors < 1 || n_factors > rs::kMaxFactors)
-            return rs::set_error(ctx, RS_ERR_UNSUPPORTED, "n_factors must be in [1, 511]");
+            return rs::set_error(ctx, RS_ERR_UNSUPPORTED, "n_factors must be in [1, 510]");
         auto* pl = new rs_svd_plan();
         try {
             rs::plan_build(ctx, r, n_factors, pl);
@@ -1536,7 +1536,7 @@ extern "C" int rs_svd_plan_create_csr(rs_ctx* ctx, int32_t n_users, int32_t n_it
         *out = nullptr;
         if (n_users < 0 || n_items < 0 || !rowptr) return rs::set_error(ctx, RS_ERR_INVALID, "bad CSR sizes");
         if (n_factors < 1 || n_factors > rs::kMaxFactors)
-            return rs::set_error(ctx, RS_ERR_UNSUPPORTED, "n_factors must be in [1, 511]");
+            return rs::set_error(ctx, RS_ERR_UNSUPPORTED, "n_factors must be in [1, 510]");
         if (rowptr[0] != 0) return rs::set_error(ctx, RS_ERR_INVALID, "rowptr[0] != 0");
         for (int32_t u = 0; u < n_users; ++u)
             if (rowptr[u + 1] < rowptr[u]) return rs::set_error(ctx, RS_ERR_INVALID, "rowptr not monotone at " + std::to_string(u));
@@ -1753,6 +1753,17 @@ extern "C" int rs_svd_plan_set_tiles(rs_svd_plan* pl, int32_t workgroups, int32_
         pl->tile_ring = ring;
         rs::tile_build(pl);
         if (pl->write_back == RS_SGD_WB_TILE) pl->n_blocks = rs::tile_partials(pl);
+        return RS_OK;
+    });
+}
+
+extern "C" int rs_svd_plan_tile_clocks(rs_svd_plan* pl, int64_t* out, int64_t n) {
+    if (!pl || !out || n < 0) return rs::set_error(pl ? pl->ctx : nullptr, RS_ERR_INVALID, "bad arguments");
+    return rs_guard(pl->ctx, [&]() -> int {
+        rs::plan_sync_last(pl);
+        const size_t m = std::min(static_cast<size_t>(n), pl->trace.n);
+        pl->trace.download(out, m, pl->ctx->stream);
+        RS_HIP(hipStreamSynchronize(pl->ctx->stream));
         return RS_OK;
     });
 }

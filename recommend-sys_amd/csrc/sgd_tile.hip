@@ -38,8 +38,11 @@
 
 #include <algorithm>
 #include <cmath>
+#include <cstdlib>
 #include <cstring>
 #include <numeric>
+#include <queue>
+#include <utility>
 #include <stdexcept>
 #include <thread>
 #include <vector>
@@ -52,31 +55,58 @@ namespace rs {
 
 constexpr size_t kTileLdsBudget = 160 * 1024 - 512;  // gfx950: 160 KiB of LDS per workgroup
 
-template <int E, int NW, int RQ>
+// Wave sum ending in lane 63 (GFX9 DPP row broadcasts): the in-row tree gives every lane its row's
+// sum, row_bcast:15 adds row 0 / 2's sum into rows 1 / 3, row_bcast:31 adds rows 0-1 into rows 2-3.
+// Six VALU ops and a v_readlane, against ten for the all-lanes form (the value is needed as a scalar).
+__device__ __forceinline__ float wave_sum_l63(float x) {
+    x = group_sum<16>(x);
+    x += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(x), 0x142, 0xA, 0xF, false));  // row_bcast:15
+    x += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(x), 0x143, 0xC, 0xF, false));  // row_bcast:31
+    return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(x), 63));
+}
+
+// Register layout of the tile kernel: lane l's register x holds logical column c = l + 64 x.  Columns
+// [0, k) are the factors; the biases fold into the dot product with a constant partner column:
+//   P row: [p_0 .. p_{k-1}, b_u, 1]     Q row: [q_0 .. q_{k-1}, 1, b_i]
+// so p.q over all columns = p.q + b_u + b_i, and the one update formula p <- a p - c q,
+// q <- a q - c p_new gives b_u <- a b_u - c and b_i <- a b_i - c (svd.go:108-112); only the two
+// constant columns are held at 1 by a select.  In memory the bias sits in column k of both rows
+// (the 64-B line budget of the global atomics, sgd.hip) and nothing is stored past it.
+template <int E, int NW, int RQ, int DIAG = 0>
 __global__ __launch_bounds__(NW * 64) void svd_epoch_tile_kernel(
     const int4* __restrict__ tiles, int32_t n_tiles, const int2* __restrict__ tile_users,
     const int32_t* __restrict__ streams, const int2* __restrict__ runs, const int2* __restrict__ recs,
     float* __restrict__ P, int32_t* Q, int32_t q_bytes, const double* __restrict__ gb_in,
     double* __restrict__ gb_partial, float lr, float reg, float* __restrict__ dP,
-    const float* __restrict__ uw, float* __restrict__ dPs, int32_t kf) {
+    const float* __restrict__ uw, float* __restrict__ dPs, int32_t kf, int32_t ldm, int64_t* __restrict__ dbg) {
 #pragma clang fp contract(fast)
-    constexpr int LD = 64 * E, NT = NW * 64;
+    constexpr int LD = 64 * E, NT = NW * 64;  // LD: LDS row (k + 2 columns fit); ldm: the rows in HBM
+    constexpr bool TIMED = (DIAG & 16) != 0;  // per-wave phase clocks into dbg (experiments)
+    int64_t tm_stage = 0, tm_ring = 0, tm_loop = 0, tm_tail = 0, tm_c = 0;
+    auto clk = [] { return static_cast<int64_t>(__builtin_amdgcn_s_memtime()); };
     static_assert(2 * E * RQ <= 60, "ring loads and atomics must fit the 63-op vmcnt");
+    typedef float f2 __attribute__((ext_vector_type(2)));
     extern __shared__ __align__(16) int32_t lds[];
     const int tid = static_cast<int>(threadIdx.x), lane = tid & 63;
     const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
-    const int32_t lane4 = lane * 4;
-    const int32_t lc = last_col<E>(lane, kf);
-    const bool bias_lane = lane == 63;
     const __amdgpu_buffer_rsrc_t rq = __builtin_amdgcn_make_buffer_rsrc(Q, 0, q_bytes, 0x00020000);
     const double gb0 = gb_in[0];
-    const float a = 1.f - lr * reg;
-    int32_t pcol[E];  // LDS column of register x of this lane (-1: padding, never touched)
+    const float a = 1.f - lr * reg, am1 = -lr * reg;
+    // per register: global byte offset of this lane's Q element in a row (-1: none), constant lanes
+    int32_t qoff[E];
+    bool qone[E], pone[E];
 #pragma unroll
-    for (int x = 0; x < E; ++x) pcol[x] = x < E - 1 ? lane + 64 * x : lc;
+    for (int x = 0; x < E; ++x) {
+        const int32_t c = lane + 64 * x;
+        qoff[x] = c < kf ? 4 * c : (c == kf + 1 ? 4 * kf : -1);
+        qone[x] = c == kf;      // Q's constant 1 (partner of b_u)
+        pone[x] = c == kf + 1;  // P's constant 1 (partner of b_i)
+    }
+    auto qaddr = [&](int32_t row, int x) { return (row >= 0 && qoff[x] >= 0) ? row + qoff[x] : kOutOfRange; };
     double contrib = 0.0;
 
     for (int32_t t = static_cast<int32_t>(blockIdx.x); t < n_tiles; t += static_cast<int32_t>(gridDim.x)) {
+        if constexpr (TIMED) tm_c = clk();
         const int4 tm = tiles[t];  // {first user entry, entries, first run, first record}
         const int32_t nu = tm.y;
         const int32_t* sp = streams + static_cast<int64_t>(t) * (NW + 1);
@@ -84,28 +114,46 @@ __global__ __launch_bounds__(NW * 64) void svd_epoch_tile_kernel(
         const int2* tr = runs + tm.z;  // n_runs + 1 entries: a sentinel holds the record count
         const int32_t n_rec = tr[n_runs].y;
         int32_t* Pl = lds;
-        int2* Rl = reinterpret_cast<int2*>(lds + nu * LD);
+        int2* Rl = reinterpret_cast<int2*>(Pl + nu * LD);
         int2* Ul = Rl + n_rec;
-        // stage the tile: P rows as int32 fixed point, records, runs
+        // stage the tile: P rows as int32 fixed point in the register layout above, records, runs
         for (int32_t x = tid; x < nu * LD; x += NT) {
             const int32_t ul = x / LD, c = x - ul * LD;
-            const float v = P[static_cast<int64_t>(tile_users[tm.x + ul].x) * LD + c];
-            Pl[x] = __float2int_rn(v * kFx);
+            int32_t v = 0;
+            if (c <= kf) v = __float2int_rn(P[static_cast<int64_t>(tile_users[tm.x + ul].x) * ldm + c] * kFx);
+            else if (c == kf + 1) v = 1 << 24;
+            Pl[x] = v;
         }
         for (int32_t x = tid; x < n_rec; x += NT) Rl[x] = recs[tm.w + x];
         for (int32_t x = tid; x <= n_runs; x += NT) Ul[x] = tr[x];
         __syncthreads();
+        if constexpr (TIMED) {
+            const int64_t c = clk();
+            tm_stage += c - tm_c;
+            tm_c = c;
+        }
 
         const int32_t r0 = sp[w], r1 = sp[w + 1];
-        auto item_of = [&](int32_t r) -> int32_t {
-            return r < r1 ? __builtin_amdgcn_readfirstlane(Ul[r].x) : -1;
+        // Run headers and records are read from LDS in 64-entry windows (one lane-parallel read per 64
+        // runs / ratings, then v_readlane with an SGPR index): no LDS round trip per run or rating.
+        int32_t hb = r0;  // run window base: lane l of (hw0, hw1) holds run hb + l, hb + 64 + l
+        int2 hw0 = Ul[min(hb + lane, n_runs)], hw1 = Ul[min(hb + 64 + lane, n_runs)];
+        auto run_hdr = [&](int32_t r, bool want_begin) -> int32_t {  // item or first record of run r
+            const int32_t o = r - hb;
+            const int32_t v = o < 64 ? (want_begin ? hw0.y : hw0.x) : (want_begin ? hw1.y : hw1.x);
+            return __builtin_amdgcn_readlane(v, o & 63);
         };
+        auto item_of = [&](int32_t r) -> int32_t { return r < r1 ? run_hdr(r, false) : -1; };
+        const int32_t s_end = __builtin_amdgcn_readfirstlane(Ul[r1].y);  // records [first of r0, first of r1)
+        const int32_t s_begin = run_hdr(r0, true);
+        int32_t rb = s_begin;  // record window base (tile-local)
+        int2 rw0 = Rl[min(rb + lane, n_rec - 1)], rw1 = Rl[min(rb + 64 + lane, n_rec - 1)];
         auto load_q = [&](int32_t (&q)[E], int32_t item) {
-            const int32_t row = item >= 0 ? item * (LD * 4) : kOutOfRange;  // SGPR arithmetic
+            const int32_t row = item >= 0 ? item * (ldm * 4) : -1;  // SGPR arithmetic
 #pragma unroll
             for (int x = 0; x < E; ++x)
-                q[x] = static_cast<int32_t>(
-                    __builtin_amdgcn_raw_buffer_load_b32(rq, roff<E>(row, x, lane4, lc), 0, kSgdAux));
+                q[x] = (DIAG & 2) ? 0
+                                  : static_cast<int32_t>(__builtin_amdgcn_raw_buffer_load_b32(rq, qaddr(row, x), 0, kSgdAux));
         };
         int32_t ring[RQ][E];
 #pragma unroll
@@ -118,16 +166,24 @@ __global__ __launch_bounds__(NW * 64) void svd_epoch_tile_kernel(
             for (int x = 0; x < E; ++x) {  // per-lane offsets and value: not folded into one lane
                 int32_t z;
                 asm volatile("v_mov_b32 %0, 0" : "=v"(z));
-                __builtin_amdgcn_raw_ptr_buffer_atomic_add_i32(z, rq, roff<E>(kOutOfRange, x, lane4, lc), 0, 0);
+                __builtin_amdgcn_raw_ptr_buffer_atomic_add_i32(z, rq, kOutOfRange + lane * 4 + 256 * x, 0, 0);
             }
         }
         double gb = gb0;
-        int32_t nr = 0;
+        const float klr = lr * kFxInv;  // c = lr * (s * 2^-24 + gb - r): p.q arrives in 2^24 units
+        int32_t j = rb;                 // next record
         for (int32_t r = r0; r < r1; r += RQ) {
 #pragma unroll
             for (int s = 0; s < RQ; ++s) {
                 const int32_t rr = r + s;
                 const bool live = rr < r1;  // wave-uniform
+                if (live && rr - hb >= 64) {  // slide the run window (every 64 runs)
+                    hb += 64;
+                    hw0 = hw1;
+                    hw1 = Ul[min(hb + 64 + lane, n_runs)];
+                }
+                int64_t c0 = 0;
+                if constexpr (TIMED) c0 = clk();
                 int32_t q0[E];
                 float q[E];
 #pragma unroll
@@ -136,71 +192,104 @@ __global__ __launch_bounds__(NW * 64) void svd_epoch_tile_kernel(
                     // coalesced copy would keep both live and the compiler would rotate the ring with
                     // moves at the loop back edge, waiting for every load in flight there)
                     asm volatile("v_mov_b32 %0, %1" : "=v"(q0[x]) : "v"(ring[s][x]));
-                    q[x] = fx_to_f(static_cast<uint32_t>(q0[x]));
+                    q[x] = qone[x] ? 1.f : fx_to_f(static_cast<uint32_t>(q0[x]));
                 }
-                int32_t item = -1, b = 0, e = 0;
-                if (live) {
-                    item = __builtin_amdgcn_readfirstlane(Ul[rr].x);
-                    b = __builtin_amdgcn_readfirstlane(Ul[rr].y);
-                    e = __builtin_amdgcn_readfirstlane(Ul[rr + 1].y);
+                if constexpr (TIMED) {
+                    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // (timed variant only) honest split
+                    const int64_t c1 = clk();
+                    tm_ring += c1 - c0;
+                    c0 = c1;
                 }
+                const int32_t item = live ? run_hdr(rr, false) : -1;
+                const int32_t e = live ? run_hdr(rr + 1, true) : j;
                 load_q(ring[s], item_of(rr + RQ));  // refill: every slot issues E loads + E atomics
-                for (int32_t cb = b; cb < e; cb += 64) {
-                    const int32_t cn = min(64, e - cb);
-                    int2 rc = make_int2(0, 0);
-                    if (lane < cn) rc = Rl[cb + lane];
-                    for (int32_t j = 0; j < cn; ++j) {
-                        const int32_t ul = __builtin_amdgcn_readlane(rc.x, j);
-                        const float rt = __int_as_float(__builtin_amdgcn_readlane(rc.y, j));
-                        int32_t* prow = Pl + ul * LD;
-                        float p[E];
+                const float gbf = static_cast<float>(gb);
+                float cs = 0.f;  // sum of this run's c: GlobalBias moves by -cs (folded in double)
+                for (; j < e; ++j) {
+                    if (j - rb >= 64) {  // slide the record window (every 64 ratings)
+                        rb += 64;
+                        rw0 = rw1;
+                        rw1 = Rl[min(rb + 64 + lane, n_rec - 1)];
+                    }
+                    const int32_t o = j - rb;
+                    const int32_t ul = __builtin_amdgcn_readlane(rw0.x, o);
+                    const float rt = __int_as_float(__builtin_amdgcn_readlane(rw0.y, o));
+                    int32_t* prow = Pl + ul * LD + lane;
+                    float pu[E];  // p in 2^-24 units
 #pragma unroll
-                        for (int x = 0; x < E; ++x)
-                            p[x] = pcol[x] >= 0 ? fx_to_f(static_cast<uint32_t>(prow[pcol[x]])) : 0.f;
-                        const float ub = lane63(p[E - 1]), bq = lane63(q[E - 1]);
-                        float sd = 0.f;
+                    for (int x = 0; x < E; ++x)
+                        pu[x] = (DIAG & 8) ? 1e5f * ul : static_cast<float>(prow[64 * x]);
+                    // dot over all columns (biases included), two columns per packed op
+                    float sd;
+                    {
+                        f2 acc = {0.f, 0.f};
 #pragma unroll
-                        for (int x = 0; x < E - 1; ++x) sd += p[x] * q[x];
-                        sd += p[E - 1] * (bias_lane ? 0.f : q[E - 1]);
-                        sd = wave_sum(sd);
-                        // svd.go:102-128 in FMA form: a = 1 - lr*reg, c = lr*diff:
-                        // p <- a p - c q ; q <- a q - c p_new ; b <- a b - c ; gb <- gb - c
-                        const float diff = ((static_cast<float>(gb) + ub) + bq) + sd - rt;
-                        const float c = lr * diff;
-                        gb -= static_cast<double>(c);  // a double: the fold sees the exact walk
-                        const float ubn = __builtin_fmaf(ub, a, -c), bqn = __builtin_fmaf(bq, a, -c);
+                        for (int x = 0; x + 1 < E; x += 2) {
+                            const f2 pv = {pu[x], pu[x + 1]}, qv = {q[x], q[x + 1]};
+                            acc = __builtin_elementwise_fma(pv, qv, acc);
+                        }
+                        sd = acc.x + acc.y;
+                        if constexpr (E & 1) sd = __builtin_fmaf(pu[E - 1], q[E - 1], sd);
+                    }
+                    sd = wave_sum_l63(sd);
+                    // svd.go:102-128: diff = (gb + b_u + b_i + p.q) - r, c = lr diff;
+                    // p <- a p - c q ; q <- a q - c p_new (Q1) ; gb <- gb - c
+                    const float c = __builtin_fmaf(sd, klr, lr * ((gbf - cs) - rt));
+                    cs += c;
+                    const float cfx = c * kFx, cq = c * kFxInv;
+                    float pn[E];
 #pragma unroll
-                        for (int x = 0; x < E; ++x) {
-                            float pn = __builtin_fmaf(-c, q[x], p[x] * a);
-                            float qn = __builtin_fmaf(-c, pn, q[x] * a);
-                            if (x == E - 1 && bias_lane) {
-                                pn = ubn;
-                                qn = bqn;
-                            }
-                            if (pcol[x] >= 0)
-                                __hip_atomic_fetch_add(prow + pcol[x], __float2int_rn((pn - p[x]) * kFx),
-                                                       __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-                            q[x] = qn;
+                    for (int x = 0; x + 1 < E + 1; x += 2) {
+                        if (x + 1 < E) {  // d = (a - 1) p - c q in 2^-24 units; p_new = p + d
+                            const f2 pv = {pu[x], pu[x + 1]}, qv = {q[x], q[x + 1]};
+                            f2 d = __builtin_elementwise_fma(qv, f2{-cfx, -cfx}, pv * f2{am1, am1});
+                            if (pone[x]) d.x = 0.f;  // P's constant column stays 1 (b_i's partner)
+                            if (pone[x + 1]) d.y = 0.f;
+                            const f2 np = pv + d;
+                            const f2 nq = __builtin_elementwise_fma(np, f2{-cq, -cq}, qv * f2{a, a});
+                            pn[x] = d.x;
+                            pn[x + 1] = d.y;
+                            q[x] = nq.x;
+                            q[x + 1] = nq.y;
+                        } else {
+                            const float d = pone[x] ? 0.f : __builtin_fmaf(q[x], -cfx, pu[x] * am1);
+                            pn[x] = d;
+                            q[x] = __builtin_fmaf(pu[x] + d, -cq, q[x] * a);
                         }
                     }
-                }
-                nr += e - b;
-                const int32_t row = live ? item * (LD * 4) : kOutOfRange;
 #pragma unroll
-                for (int x = 0; x < E; ++x)
-                    __builtin_amdgcn_raw_ptr_buffer_atomic_add_i32(__float2int_rn(q[x] * kFx) - q0[x], rq,
-                                                                   roff<E>(row, x, lane4, lc), 0, 0);
+                    for (int x = 0; x < E; ++x) {
+                        if (qone[x]) q[x] = 1.f;
+                        const int32_t di = __float2int_rn(pn[x]);
+                        if (!(DIAG & 4))
+                            __hip_atomic_fetch_add(prow + 64 * x, di, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                    }
+                }
+                gb -= static_cast<double>(cs);
+                if constexpr (TIMED) tm_loop += clk() - c0;
+                const int32_t row = live ? item * (ldm * 4) : -1;
+#pragma unroll
+                for (int x = 0; x < E; ++x) {
+                    const int32_t dq = __float2int_rn(q[x] * kFx) - q0[x];
+                    if constexpr (DIAG & 1)  // diagnostic: the atomic goes nowhere (same issue count)
+                        __builtin_amdgcn_raw_ptr_buffer_atomic_add_i32(dq, rq, kOutOfRange + lane * 4 + 256 * x, 0, 0);
+                    else
+                        __builtin_amdgcn_raw_ptr_buffer_atomic_add_i32(dq, rq, qaddr(row, x), 0, 0);
+                }
             }
         }
-        contrib += static_cast<double>(nr) * (gb - static_cast<double>(gb0));
+        const int32_t nr = s_end - s_begin;
+        if constexpr (TIMED) tm_c = clk();
+        contrib += static_cast<double>(nr) * (gb - gb0);
         __syncthreads();
         // write the tile's P rows back: whole users stored (or their weighted delta to dP in
         // multi-GPU delta mode), pieces of split users as count-weighted deltas
         for (int32_t x = tid; x < nu * LD; x += NT) {
             const int32_t ul = x / LD, c = x - ul * LD;
+            if (c > kf) continue;  // the constant column and padding are not stored
             const int2 te = tile_users[tm.x + ul];  // {user, frac bits}
             const float frac = __int_as_float(te.y);
-            const int64_t g = static_cast<int64_t>(te.x) * LD + c;
+            const int64_t g = static_cast<int64_t>(te.x) * ldm + c;
             const float v = fx_to_f(static_cast<uint32_t>(Pl[x]));
             if (dP) {
                 const float d = uw[te.x] * frac * (v - P[g]);
@@ -213,8 +302,18 @@ __global__ __launch_bounds__(NW * 64) void svd_epoch_tile_kernel(
             }
         }
         __syncthreads();  // the next tile's staging overwrites the LDS
+        if constexpr (TIMED) tm_tail += clk() - tm_c;
     }
     if (lane == 0) gb_partial[static_cast<int64_t>(blockIdx.x) * NW + w] = contrib;
+    if constexpr (TIMED) {
+        if (lane == 0) {
+            int64_t* d = dbg + (static_cast<int64_t>(blockIdx.x) * NW + w) * 4;
+            d[0] = tm_stage;
+            d[1] = tm_ring;
+            d[2] = tm_loop;
+            d[3] = tm_tail;
+        }
+    }
 }
 
 namespace {
@@ -243,7 +342,7 @@ int32_t device_cus(const rs_ctx* ctx) {
     return cus;
 }
 
-size_t tile_bytes(int64_t users, int64_t recs, int64_t runs, int32_t ld) {
+size_t tile_bytes(int64_t users, int64_t recs, int64_t runs, int32_t ld) {  // ld: the LDS row
     return static_cast<size_t>(users) * ld * 4 + static_cast<size_t>(recs) * 8 + static_cast<size_t>(runs + 1) * 8;
 }
 
@@ -253,7 +352,7 @@ size_t tile_bytes(int64_t users, int64_t recs, int64_t runs, int32_t ld) {
 void build_tile_host(const rs_svd_plan* pl, int32_t nw, int64_t target, int32_t run_cap, bool want_pos,
                      TileHost& th) {
     const std::vector<int64_t>& rp = pl->h_rowptr;
-    const int32_t ld = pl->ld;
+    const int32_t ld = 64 * ((pl->k + 2 + 63) / 64);  // LDS row: k factors + the two bias columns
     // one entry alone must fit: ld*4 + d*16 + 8 <= budget
     const int64_t rec_cap = static_cast<int64_t>((kTileLdsBudget - 16 - static_cast<size_t>(ld) * 4) / 16);
     if (rec_cap < 64) throw std::invalid_argument("n_factors too large for the tile schedule's LDS");
@@ -270,21 +369,66 @@ void build_tile_host(const rs_svd_plan* pl, int32_t nw, int64_t target, int32_t 
             ents.push_back({u, b, e, pieces > 1 ? static_cast<float>(static_cast<double>(e - b) / d) : 1.f});
         }
     }
-    // tile boundaries over the entries
+    // Tiles by LPT over the entries (heaviest first, each to the least-loaded tile its LDS still takes):
+    // near-equal ratings per tile -- the epoch is its slowest workgroup, and a workgroup's time tracks
+    // its tile's ratings (measured: correlation 0.90 on the ML-1M shape).  The tile count is the
+    // larger of nnz / target and what the LDS needs; entries of a tile keep user order.
     std::vector<size_t> tb{0};
     {
-        int64_t nu = 0, nrec = 0;
-        for (size_t x = 0; x < ents.size(); ++x) {
-            const int64_t d = ents[x].e - ents[x].b;
-            if (nu > 0 && (nrec + d > target || tile_bytes(nu + 1, nrec + d, nrec + d, ld) > kTileLdsBudget)) {
-                tb.push_back(x);
-                nu = 0;
-                nrec = 0;
-            }
-            ++nu;
-            nrec += d;
+        int64_t total = 0;
+        double bytes = 0;
+        for (const Ent& x : ents) {
+            total += x.e - x.b;
+            bytes += static_cast<double>(ld) * 4 + 16.0 * static_cast<double>(x.e - x.b);
         }
-        if (tb.back() != ents.size()) tb.push_back(ents.size());
+        const int64_t n0 = std::max<int64_t>(
+            {1, (total + target - 1) / std::max<int64_t>(target, 1),
+             static_cast<int64_t>(std::ceil(bytes / (0.85 * static_cast<double>(kTileLdsBudget))))});
+        std::vector<size_t> order(ents.size());
+        std::iota(order.begin(), order.end(), size_t{0});
+        std::stable_sort(order.begin(), order.end(), [&](size_t a, size_t b) {
+            return ents[a].e - ents[a].b > ents[b].e - ents[b].b;
+        });
+        struct Bin { int64_t recs = 0, users = 0; std::vector<size_t> ents; };
+        std::vector<Bin> bins(static_cast<size_t>(n0));
+        using HE = std::pair<int64_t, size_t>;  // (ratings, bin), least first
+        std::priority_queue<HE, std::vector<HE>, std::greater<HE>> heap;
+        for (size_t b = 0; b < bins.size(); ++b) heap.push({0, b});
+        std::vector<HE> aside;
+        for (size_t x : order) {
+            const int64_t d = ents[x].e - ents[x].b;
+            size_t pick = SIZE_MAX;
+            while (!heap.empty() && aside.size() < 8) {
+                const HE h = heap.top();
+                heap.pop();
+                const Bin& bn = bins[h.second];
+                if (tile_bytes(bn.users + 1, bn.recs + d, bn.recs + d, ld) <= kTileLdsBudget) {
+                    pick = h.second;
+                    break;
+                }
+                aside.push_back(h);
+            }
+            for (const HE& h : aside) heap.push(h);
+            aside.clear();
+            if (pick == SIZE_MAX) {  // no tile with room: a new one
+                pick = bins.size();
+                bins.emplace_back();
+            }
+            Bin& bn = bins[pick];
+            bn.recs += d;
+            bn.users += 1;
+            bn.ents.push_back(x);
+            heap.push({bn.recs, pick});
+        }
+        std::vector<Ent> sorted;
+        sorted.reserve(ents.size());
+        for (Bin& bn : bins) {
+            if (bn.ents.empty()) continue;
+            std::sort(bn.ents.begin(), bn.ents.end());
+            for (size_t x : bn.ents) sorted.push_back(ents[x]);
+            tb.push_back(sorted.size());
+        }
+        ents.swap(sorted);
     }
     const size_t nt = tb.size() - 1;
     // per tile: runs grouped by item in a per-tile pseudo-random item order, dealt to nw streams
@@ -390,9 +534,30 @@ void build_tile_host(const rs_svd_plan* pl, int32_t nw, int64_t target, int32_t 
     if (th.lds > kTileLdsBudget) throw std::logic_error("tile schedule exceeds the LDS");
 }
 
+// Run cap when the caller leaves it to the library (0): hot items' runs are cut so that the updates
+// of one item held in registers by concurrent runs stay near kStaleTarget.  Model (measured on the
+// ML-1M shape): an item of degree d cut into runs of c ratings is held by
+// d * grid * waves / nnz runs at a time, each c/2 updates ahead of memory on average, so about
+// S = d * grid * waves * c / (2 nnz); uncut runs (c = d / grid) give S = waves * d^2 / (2 nnz) -- 290 for
+// ML-1M's hottest item at 16 waves, where 20-epoch training diverged; 8-rating pieces give ~100.
+constexpr double kStaleTarget = 100.0;
+int32_t auto_run_cap(const rs_svd_plan* pl, int32_t grid, int32_t waves) {
+    if (waves <= 1 || pl->nnz == 0) return 0;
+    std::vector<int64_t> deg(std::max(1, pl->n_items), 0);
+    for (int32_t c : pl->h_cols) deg[c]++;
+    const int64_t dmax = *std::max_element(deg.begin(), deg.end());
+    const double c = 2.0 * kStaleTarget * static_cast<double>(pl->nnz) /
+                     (static_cast<double>(dmax) * grid * waves);
+    return c >= 1e6 ? 0 : std::max(2, static_cast<int32_t>(c));
+}
+
+// Ratings per tile: nnz / workgroups, but at least the heaviest user's ratings (cutting users into
+// pieces costs accuracy -- their rows are averaged after the epoch -- so small sets get fewer tiles).
 int64_t tile_target_of(const rs_svd_plan* pl, int32_t grid) {
     if (pl->tile_target > 0) return pl->tile_target;
-    return std::max<int64_t>(64, (pl->nnz + grid - 1) / std::max(1, grid));
+    int64_t dmax = 0;
+    for (int32_t u = 0; u < pl->n_users; ++u) dmax = std::max(dmax, pl->h_rowptr[u + 1] - pl->h_rowptr[u]);
+    return std::max<int64_t>({64, dmax, (pl->nnz + grid - 1) / std::max(1, grid)});
 }
 
 }  // namespace
@@ -404,7 +569,8 @@ void tile_build(rs_svd_plan* pl) {
     const int32_t cus = device_cus(pl->ctx);
     const int32_t grid0 = pl->tile_wg > 0 ? pl->tile_wg : cus;
     TileHost th;
-    build_tile_host(pl, pl->tile_waves, tile_target_of(pl, grid0), pl->tile_run_cap, false, th);
+    const int32_t cap = pl->tile_run_cap > 0 ? pl->tile_run_cap : auto_run_cap(pl, grid0, pl->tile_waves);
+    build_tile_host(pl, pl->tile_waves, tile_target_of(pl, grid0), cap, false, th);
     plan_sync_last(pl);
     pl->n_tiles = static_cast<int32_t>(th.tiles.size());
     pl->tile_grid = std::max(1, std::min(grid0, pl->n_tiles));
@@ -436,7 +602,8 @@ void tile_order(rs_svd_plan* pl, int64_t* pos, int64_t* work_off, int32_t* n_wor
     const int32_t cus = device_cus(pl->ctx);
     const int32_t grid0 = pl->tile_wg > 0 ? pl->tile_wg : cus;
     TileHost th;
-    build_tile_host(pl, pl->tile_waves, tile_target_of(pl, grid0), pl->tile_run_cap, true, th);
+    const int32_t cap = pl->tile_run_cap > 0 ? pl->tile_run_cap : auto_run_cap(pl, grid0, pl->tile_waves);
+    build_tile_host(pl, pl->tile_waves, tile_target_of(pl, grid0), cap, true, th);
     const size_t nw = th.tiles.size() * pl->tile_waves;
     if (n_works) *n_works = static_cast<int32_t>(nw);
     if (pos) std::copy(th.pos.begin(), th.pos.end(), pos);
@@ -451,9 +618,9 @@ void tile_order(rs_svd_plan* pl, int64_t* pos, int64_t* work_off, int32_t* n_wor
     }
 }
 
-template <int E, int NW, int RQ>
+template <int E, int NW, int RQ, int DIAG = 0>
 static void tile_launch_t(rs_svd_plan* pl, float lr, float reg, hipStream_t s, float* dP) {
-    auto kern = svd_epoch_tile_kernel<E, NW, RQ>;
+    auto kern = svd_epoch_tile_kernel<E, NW, RQ, DIAG>;
     static bool attr = false;  // per instantiation
     if (!attr) {
         RS_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(kern),
@@ -464,7 +631,7 @@ static void tile_launch_t(rs_svd_plan* pl, float lr, float reg, hipStream_t s, f
     hipLaunchKernelGGL(kern, dim3(pl->tile_grid), dim3(NW * 64), pl->tile_lds, s, pl->t_tiles.p, pl->n_tiles,
                        pl->t_users.p, pl->t_streams.p, pl->t_runs.p, pl->t_recs.p, pl->P.p,
                        reinterpret_cast<int32_t*>(pl->Q.p), q_bytes, pl->gb.p, pl->partial.p, lr, reg, dP,
-                       dP ? pl->uw.p : nullptr, pl->dPs.p, pl->k);
+                       dP ? pl->uw.p : nullptr, pl->dPs.p, pl->k, pl->ld, pl->trace.p);
 }
 
 // q_i rows in flight per wave (runs ahead): the ring's loads and the runs' atomics share the wave's
@@ -473,7 +640,25 @@ static void tile_launch_t(rs_svd_plan* pl, float lr, float reg, hipStream_t s, f
 template <int E, int NW>
 static void tile_launch_r(rs_svd_plan* pl, float lr, float reg, hipStream_t s, float* dP) {
     constexpr int kMax = 60 / (2 * E);  // 15 at E = 2 (k <= 127), 6 at E = 5 (k <= 319), 3 at E = 8
-    const int want = pl->tile_ring > 0 ? pl->tile_ring : 12;
+    const int want = pl->tile_ring > 0 ? pl->tile_ring : 4;
+    if constexpr (E == 2 && NW == 16) {  // diagnostics (RSGPU_TILE_DIAG, experiments only): bits drop
+        static const int diag = std::getenv("RSGPU_TILE_DIAG") ? std::atoi(std::getenv("RSGPU_TILE_DIAG")) : 0;
+        switch (diag) {  // 1 q atomics, 2 q loads, 4 p LDS atomics, 8 p LDS reads
+            case 1: return tile_launch_t<E, NW, 4, 1>(pl, lr, reg, s, dP);
+            case 2: return tile_launch_t<E, NW, 4, 2>(pl, lr, reg, s, dP);
+            case 3: return tile_launch_t<E, NW, 4, 3>(pl, lr, reg, s, dP);
+            case 4: return tile_launch_t<E, NW, 4, 4>(pl, lr, reg, s, dP);
+            case 12: return tile_launch_t<E, NW, 4, 12>(pl, lr, reg, s, dP);
+            case 15: return tile_launch_t<E, NW, 4, 15>(pl, lr, reg, s, dP);
+            case 16:
+                if (pl->trace.n < static_cast<size_t>(pl->tile_grid) * NW * 4) {
+                    pl->trace.alloc(static_cast<size_t>(pl->tile_grid) * NW * 4);
+                    RS_HIP(hipMemsetAsync(pl->trace.p, 0, pl->trace.n * 8, s));
+                }
+                return tile_launch_t<E, NW, 4, 16>(pl, lr, reg, s, dP);
+            default: break;
+        }
+    }
     if constexpr (kMax >= 12) {
         if (want >= 12) return tile_launch_t<E, NW, 12>(pl, lr, reg, s, dP);
     }
@@ -483,6 +668,8 @@ static void tile_launch_r(rs_svd_plan* pl, float lr, float reg, hipStream_t s, f
     if constexpr (kMax >= 6) {
         if (want >= 6) return tile_launch_t<E, NW, 6>(pl, lr, reg, s, dP);
     }
+    if (want <= 2) return tile_launch_t<E, NW, 2>(pl, lr, reg, s, dP);
+    if (want == 3) return tile_launch_t<E, NW, 3>(pl, lr, reg, s, dP);
     if constexpr (kMax >= 4) {
         return tile_launch_t<E, NW, 4>(pl, lr, reg, s, dP);
     } else {
@@ -504,11 +691,16 @@ static void tile_launch_w(rs_svd_plan* pl, float lr, float reg, hipStream_t s, f
 void tile_launch(rs_svd_plan* pl, float lr, float reg, hipStream_t s, float* dP) {
     if (!pl->tiles_built) tile_build(pl);
     pl->n_blocks = tile_partials(pl);
+    if (pl->partial.n < static_cast<size_t>(pl->n_blocks)) {  // another schedule resized it
+        plan_sync_last(pl);
+        RS_HIP(hipStreamSynchronize(s));
+        pl->partial.alloc(static_cast<size_t>(pl->n_blocks));
+    }
     if (pl->n_tiles == 0) {  // no ratings: the fold still reads its partials
         RS_HIP(hipMemsetAsync(pl->partial.p, 0, pl->partial.n * sizeof(double), s));
         return;
     }
-    switch (pl->ld / 64) {
+    switch ((pl->k + 2 + 63) / 64) {  // registers per row: k factors + the two bias columns
         case 1: tile_launch_w<1>(pl, lr, reg, s, dP); break;
         case 2: tile_launch_w<2>(pl, lr, reg, s, dP); break;
         case 3: tile_launch_w<3>(pl, lr, reg, s, dP); break;

@@ -39,7 +39,7 @@ HEADER_SYMBOLS = (
     "rs_synth_create", "rs_synth_csr", "rs_synth_destroy",
     "rs_svd_plan_set_item_weights", "rs_svd_plan_epoch_qdelta", "rs_svd_plan_apply_qdelta",
     "rs_svd_plan_set_hot_replicas", "rs_svd_plan_set_fixed_q", "rs_svd_plan_set_tiles",
-    "rs_svd_plan_tile_order",
+    "rs_svd_plan_tile_order", "rs_svd_plan_tile_clocks",
 )
 
 
@@ -61,6 +61,12 @@ class _SgdParams(C.Structure):
 
 _vp = C.c_void_p
 _i32, _i64, _dbl, _flt = C.c_int32, C.c_int64, C.c_double, C.c_float
+
+
+def _torch_stream(t):
+    """torch's current HIP stream on tensor t's device (a hipStream_t as int)."""
+    import torch
+    return torch.cuda.current_stream(t.device).cuda_stream
 
 
 def lib():
@@ -130,6 +136,7 @@ def lib():
             "rs_svd_plan_set_fixed_q": (C.c_int, [_vp, _i32]),
             "rs_svd_plan_set_tiles": (C.c_int, [_vp, _i32, _i32, _i32, _i32, _i32]),
             "rs_svd_plan_tile_order": (C.c_int, [_vp, _vp, _vp, C.POINTER(_i32)]),
+            "rs_svd_plan_tile_clocks": (C.c_int, [_vp, _vp, _i64]),
             "rs_svd_plan_epoch_qdelta": (C.c_int, [_vp, _flt, _flt, _vp, _vp, _vp]),
             "rs_svd_plan_apply_qdelta": (C.c_int, [_vp, _vp, _vp, _dbl, _vp]),
             "rs_synth_csr": (C.c_int, [_vp, C.POINTER(_i64), C.POINTER(_vp), C.POINTER(_vp),
@@ -486,19 +493,25 @@ class SvdPlan:
         self.ctx.check(lib().rs_svd_plan_set_item_weights(self.h, _ptr(self._iw)))
 
     def epoch_qdelta_t(self, dQ, gbsum, lr, reg, stream=None):
-        """User-sharded mode: dQ (torch, n_items x ld fp32), gbsum (torch, 1 float64)."""
+        """User-sharded mode: dQ (torch, n_items x ld fp32), gbsum (torch, 1 float64).  stream None:
+        torch's current stream on dQ's device, so the kernels are ordered with the collectives
+        torch enqueues there (the library's own ctx stream is not)."""
+        stream = _torch_stream(dQ) if stream is None else stream
         self.ctx.check(lib().rs_svd_plan_epoch_qdelta(self.h, lr, reg, dQ.data_ptr(), gbsum.data_ptr(),
                                                       stream))
 
     def apply_qdelta_t(self, dQ, gbsum, inv_total_nnz, stream=None):
+        stream = _torch_stream(dQ) if stream is None else stream
         self.ctx.check(lib().rs_svd_plan_apply_qdelta(self.h, dQ.data_ptr(), gbsum.data_ptr(),
                                                       inv_total_nnz, stream))
 
     # torch-tensor forms used by rsgpu.multi.ItemShardedStep
     def epoch_delta_t(self, dP, gbsum, lr, reg, stream=None):
+        stream = _torch_stream(dP) if stream is None else stream  # ordered with torch's collectives
         self.epoch_delta(dP.data_ptr(), gbsum.data_ptr(), lr, reg, stream)
 
     def apply_delta_t(self, dP, gbsum, inv_total_nnz, stream=None):
+        stream = _torch_stream(dP) if stream is None else stream
         self.apply_delta(dP.data_ptr(), gbsum.data_ptr(), inv_total_nnz, stream)
 
     @property

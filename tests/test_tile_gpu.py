@@ -72,7 +72,7 @@ def _private_items(n_users=300, per_user=25, seed=4):
     return users[perm], items[perm], r[perm], n_users, len(users)
 
 
-@pytest.mark.parametrize("k", [8, 64, 100, 300, 511])
+@pytest.mark.parametrize("k", [8, 63, 64, 100, 127, 300, 510])
 @pytest.mark.parametrize("wg", [3, 0])
 def test_workgroups_race_free(ctx, k, wg):
     """Several workgroups (3, or one per CU), one wave each, many tiles per workgroup, private items
