@@ -166,7 +166,7 @@ def main():
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
                          "traffic": traffic,
-                         "kernel": "svd_epoch_tile_kernel<E=2,NW=16,RQ=4> (tile schedule: user tiles in LDS, "
+                         "kernel": "svd_epoch_tile_kernel<E=2,NW=16,RQ=2> (tile schedule: user tiles in LDS, "
                                    "integer LDS atomics, one memory-side atomic per (item, tile) run)",
                          "avg_kernel_us": avg_kernel_s * 1e6,
                          "timed_span": "HIP events around each epoch's SGD kernel on the launch stream "

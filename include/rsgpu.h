@@ -248,8 +248,8 @@ int rs_svd_plan_set_mode(rs_svd_plan* plan, int32_t write_back, int32_t ring_dep
  * 8 or 16; default 16), ratings per tile (0 = nnz / workgroups, bounded by the 160 KiB LDS), run cap
  * (an item's run in a tile longer than this is cut into pieces on different waves; 0 = auto: hot items
  * cut so that ~100 of an item's updates are in flight; a huge value = never; ignored with
- * one wave), ring (q_i rows each wave keeps in flight: 0 = auto, else 4, 6, 8 or 12, clamped for wide
- * rows).  Rebuilds the schedule. */
+ * one wave), ring (q_i rows each wave loads ahead, in runs: 0 = auto = 2, else 2, 3, 4, 6, 8 or 12, clamped
+ * for wide rows; deeper rings read hot rows earlier, i.e. staler).  Rebuilds the schedule. */
 int rs_svd_plan_set_tiles(rs_svd_plan* plan, int32_t workgroups, int32_t waves, int32_t target,
                           int32_t run_cap, int32_t ring);
 /* Visit order of the tile schedule: pos[n] = user-CSR position (rowptr order, data order inside a row)

@@ -722,6 +722,72 @@ void or_svdpp_fit_userwise(int32_t n_users, const int64_t* rowptr, const int32_t
     free(uu);
 }
 
+/* The same schedule as or_svdpp_fit_userwise in O(nnz k) per epoch: inside a user's row every y-step
+ * of svd.go:408-418 is one affine map for all j in N(u), y_j <- a y_j - b_t q_i (a = 1 - lr reg,
+ * b_t = lr diff_t / sqrt|N(u)|), so y_j = A y_j0 - C with A = a^t and C = a C + b_t q_i, the implicit
+ * sum of svd.go:271-282 is (A S0 - n C) / sqrt n with S0 = sum y_j0, and the rows are written once at
+ * the user's end (equal to the literal form up to rounding for rows without repeated
+ * items).  Used as the checker at BASELINE configs[2] scale, where the literal form is O(sum |N|^2 k). */
+void or_svdpp_fit_lazy(int32_t n_users, const int64_t* rowptr, const int32_t* items, const double* r,
+                       int32_t k, int32_t epochs, double lr, double reg, double* P, double* Q, double* Y,
+                       double* bu, double* bi, double* gb) {
+    const int64_t nnz = rowptr[n_users];
+    double* S0 = (double*)malloc((size_t)k * sizeof(double));
+    double* Cv = (double*)malloc((size_t)k * sizeof(double));
+    double* e = (double*)malloc((size_t)k * sizeof(double));
+    const double al = 1.0 - lr * reg;
+    double GB = *gb;
+    for (int32_t epoch = 0; epoch < epochs; epoch++) {
+        double gsum = 0.0;
+        for (int32_t x = 0; x < n_users; x++) {
+            const int64_t b = rowptr[x], en = rowptr[x + 1];
+            if (en == b) continue;
+            const double n = (double)(en - b), sq = sqrt(n);
+            for (int32_t f = 0; f < k; f++) {
+                S0[f] = 0.0;
+                Cv[f] = 0.0;
+            }
+            for (int64_t t = b; t < en; t++)
+                for (int32_t f = 0; f < k; f++) S0[f] += Y[(int64_t)items[t] * k + f];
+            double A = 1.0, g = GB;
+            double* pu = P + (int64_t)x * k;
+            for (int64_t t = b; t < en; t++) {
+                const int32_t ii = items[t];
+                double* qi = Q + (int64_t)ii * k;
+                const double userBias = bu[x], itemBias = bi[ii];
+                double pred = g;
+                pred += bu[x];
+                pred += bi[ii];
+                double s = 0.0;
+                for (int32_t f = 0; f < k; f++) {
+                    e[f] = (A * S0[f] - n * Cv[f]) / sq;
+                    s += (pu[f] + e[f]) * qi[f];
+                }
+                pred += s;
+                const double diff = pred - r[t];
+                g -= lr * diff;
+                bu[x] -= lr * (diff + reg * userBias);
+                bi[ii] -= lr * (diff + reg * itemBias);
+                for (int32_t f = 0; f < k; f++) pu[f] = pu[f] - (qi[f] * diff + pu[f] * reg) * lr;
+                for (int32_t f = 0; f < k; f++) qi[f] = qi[f] - ((pu[f] + e[f]) * diff + qi[f] * reg) * lr;
+                const double bt = lr * diff / sq;
+                for (int32_t f = 0; f < k; f++) Cv[f] = al * Cv[f] + bt * qi[f];
+                A *= al;
+            }
+            for (int64_t t = b; t < en; t++) {
+                double* y = Y + (int64_t)items[t] * k;
+                for (int32_t f = 0; f < k; f++) y[f] = A * y[f] - Cv[f];
+            }
+            gsum += n * (g - GB);
+        }
+        if (nnz > 0) GB += gsum / (double)nnz;
+    }
+    *gb = GB;
+    free(S0);
+    free(Cv);
+    free(e);
+}
+
 double or_gb_warm_start(int32_t n_users, const int64_t* rowptr, const int32_t* items,
                         const double* r, const double* bu, const double* bi) {
     const int64_t nnz = rowptr[n_users];

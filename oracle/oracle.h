@@ -125,6 +125,10 @@ void or_svd_fit_chunked(int32_t n_users, const int64_t* rowptr, const int32_t* i
 double or_gb_warm_start(int32_t n_users, const int64_t* rowptr, const int32_t* items,
                         const double* r, const double* bu, const double* bi);
 
+/* or_svdpp_fit_userwise in its O(nnz k) lazy affine form (rows without repeated items). */
+void or_svdpp_fit_lazy(int32_t n_users, const int64_t* rowptr, const int32_t* items, const double* r,
+                       int32_t k, int32_t epochs, double lr, double reg, double* P, double* Q, double* Y,
+                       double* bu, double* bi, double* gb);
 /* Restatement of the GPU FAST SVD++ schedule (svdpp.hip): user rows processed one after another,
  * each with the literal per-rating reference updates (svd.go:352-424) restricted to that user's row,
  * a user-local GlobalBias copy folded at epoch end as in or_svd_fit_chunked.  Equal to the GPU's

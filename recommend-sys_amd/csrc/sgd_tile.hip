@@ -65,6 +65,13 @@ __device__ __forceinline__ float wave_sum_l63(float x) {
     return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(x), 63));
 }
 
+// floor(x + 0.5) as int32 in one VALU op (v_cvt_rpi_i32_f32; __float2int_rn is rndne + cvt)
+__device__ __forceinline__ int32_t cvt_rpi(float x) {
+    int32_t r;
+    asm("v_cvt_rpi_i32_f32 %0, %1" : "=v"(r) : "v"(x));
+    return r;
+}
+
 // Register layout of the tile kernel: lane l's register x holds logical column c = l + 64 x.  Columns
 // [0, k) are the factors; the biases fold into the dot product with a constant partner column:
 //   P row: [p_0 .. p_{k-1}, b_u, 1]     Q row: [q_0 .. q_{k-1}, 1, b_i]
@@ -170,7 +177,7 @@ __global__ __launch_bounds__(NW * 64) void svd_epoch_tile_kernel(
             }
         }
         double gb = gb0;
-        const float klr = lr * kFxInv;  // c = lr * (s * 2^-24 + gb - r): p.q arrives in 2^24 units
+        const float klr = lr * kFxInv * kFxInv;  // c = lr (s 2^-48 + gb - r): p and q in 2^-24 units
         int32_t j = rb;                 // next record
         for (int32_t r = r0; r < r1; r += RQ) {
 #pragma unroll
@@ -192,7 +199,7 @@ __global__ __launch_bounds__(NW * 64) void svd_epoch_tile_kernel(
                     // coalesced copy would keep both live and the compiler would rotate the ring with
                     // moves at the loop back edge, waiting for every load in flight there)
                     asm volatile("v_mov_b32 %0, %1" : "=v"(q0[x]) : "v"(ring[s][x]));
-                    q[x] = qone[x] ? 1.f : fx_to_f(static_cast<uint32_t>(q0[x]));
+                    q[x] = qone[x] ? kFx : static_cast<float>(q0[x]);  // q in 2^-24 units too
                 }
                 if constexpr (TIMED) {
                     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // (timed variant only) honest split
@@ -236,31 +243,31 @@ __global__ __launch_bounds__(NW * 64) void svd_epoch_tile_kernel(
                     // p <- a p - c q ; q <- a q - c p_new (Q1) ; gb <- gb - c
                     const float c = __builtin_fmaf(sd, klr, lr * ((gbf - cs) - rt));
                     cs += c;
-                    const float cfx = c * kFx, cq = c * kFxInv;
+
                     float pn[E];
 #pragma unroll
                     for (int x = 0; x + 1 < E + 1; x += 2) {
                         if (x + 1 < E) {  // d = (a - 1) p - c q in 2^-24 units; p_new = p + d
                             const f2 pv = {pu[x], pu[x + 1]}, qv = {q[x], q[x + 1]};
-                            f2 d = __builtin_elementwise_fma(qv, f2{-cfx, -cfx}, pv * f2{am1, am1});
+                            f2 d = __builtin_elementwise_fma(qv, f2{-c, -c}, pv * f2{am1, am1});
                             if (pone[x]) d.x = 0.f;  // P's constant column stays 1 (b_i's partner)
                             if (pone[x + 1]) d.y = 0.f;
                             const f2 np = pv + d;
-                            const f2 nq = __builtin_elementwise_fma(np, f2{-cq, -cq}, qv * f2{a, a});
+                            const f2 nq = __builtin_elementwise_fma(np, f2{-c, -c}, qv * f2{a, a});
                             pn[x] = d.x;
                             pn[x + 1] = d.y;
                             q[x] = nq.x;
                             q[x + 1] = nq.y;
                         } else {
-                            const float d = pone[x] ? 0.f : __builtin_fmaf(q[x], -cfx, pu[x] * am1);
+                            const float d = pone[x] ? 0.f : __builtin_fmaf(q[x], -c, pu[x] * am1);
                             pn[x] = d;
-                            q[x] = __builtin_fmaf(pu[x] + d, -cq, q[x] * a);
+                            q[x] = __builtin_fmaf(pu[x] + d, -c, q[x] * a);
                         }
                     }
 #pragma unroll
                     for (int x = 0; x < E; ++x) {
-                        if (qone[x]) q[x] = 1.f;
-                        const int32_t di = __float2int_rn(pn[x]);
+                        if (qone[x]) q[x] = kFx;
+                        const int32_t di = cvt_rpi(pn[x]);
                         if (!(DIAG & 4))
                             __hip_atomic_fetch_add(prow + 64 * x, di, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
                     }
@@ -270,7 +277,7 @@ __global__ __launch_bounds__(NW * 64) void svd_epoch_tile_kernel(
                 const int32_t row = live ? item * (ldm * 4) : -1;
 #pragma unroll
                 for (int x = 0; x < E; ++x) {
-                    const int32_t dq = __float2int_rn(q[x] * kFx) - q0[x];
+                    const int32_t dq = cvt_rpi(q[x]) - q0[x];
                     if constexpr (DIAG & 1)  // diagnostic: the atomic goes nowhere (same issue count)
                         __builtin_amdgcn_raw_ptr_buffer_atomic_add_i32(dq, rq, kOutOfRange + lane * 4 + 256 * x, 0, 0);
                     else
@@ -419,6 +426,64 @@ void build_tile_host(const rs_svd_plan* pl, int32_t nw, int64_t target, int32_t 
             bn.users += 1;
             bn.ents.push_back(x);
             heap.push({bn.recs, pick});
+        }
+        // Refinement by cost: a workgroup's time is ~ ratings + kRunCost * runs (one run per distinct item
+        // of the tile; measured on the ML-1M shape: ~120 cycles per run against ~34 per rating, so
+        // tiles of many light users -- more shared items -- are cheaper than tiles of one heavy user).
+        // Move users from the costliest tile to the cheapest while that lowers the maximum.
+        const size_t nb = bins.size();
+        if (nb > 1 && nb <= 8192 && static_cast<double>(nb) * std::max(1, pl->n_items) <= 6.4e7) {
+            constexpr int64_t kRunCost = 3;
+            std::vector<int32_t> cnt(nb * static_cast<size_t>(std::max(1, pl->n_items)), 0);
+            std::vector<int64_t> runs(nb, 0), cost(nb, 0);
+            auto row = [&](size_t b) { return cnt.data() + b * static_cast<size_t>(pl->n_items); };
+            const std::vector<int32_t>& cols0 = pl->h_cols;
+            for (size_t b = 0; b < nb; ++b) {
+                int32_t* c = row(b);
+                for (size_t x : bins[b].ents)
+                    for (int64_t q = ents[x].b; q < ents[x].e; ++q) runs[b] += c[cols0[q]]++ == 0;
+                cost[b] = bins[b].recs + kRunCost * runs[b];
+            }
+            for (size_t it = 0; it < 4 * nb; ++it) {
+                const size_t hi = static_cast<size_t>(std::max_element(cost.begin(), cost.end()) - cost.begin());
+                const size_t lo = static_cast<size_t>(std::min_element(cost.begin(), cost.end()) - cost.begin());
+                if (hi == lo || bins[hi].ents.size() < 2) break;
+                int64_t best = cost[hi];
+                size_t best_k = SIZE_MAX;
+                int64_t bh = 0, bl = 0;
+                for (size_t kk = 0; kk < bins[hi].ents.size(); ++kk) {
+                    const Ent& en = ents[bins[hi].ents[kk]];
+                    const int64_t d = en.e - en.b;
+                    if (tile_bytes(bins[lo].users + 1, bins[lo].recs + d, bins[lo].recs + d, ld) > kTileLdsBudget) continue;
+                    int64_t lost = 0, gained = 0;
+                    for (int64_t q = en.b; q < en.e; ++q) {
+                        lost += row(hi)[cols0[q]] == 1;
+                        gained += row(lo)[cols0[q]] == 0;
+                    }
+                    const int64_t ch = cost[hi] - d - kRunCost * lost, cl = cost[lo] + d + kRunCost * gained;
+                    if (std::max(ch, cl) < best) {
+                        best = std::max(ch, cl);
+                        best_k = kk;
+                        bh = ch;
+                        bl = cl;
+                    }
+                }
+                if (best_k == SIZE_MAX) break;
+                const size_t x = bins[hi].ents[best_k];
+                for (int64_t q = ents[x].b; q < ents[x].e; ++q) {
+                    row(hi)[cols0[q]]--;
+                    row(lo)[cols0[q]]++;
+                }
+                const int64_t d = ents[x].e - ents[x].b;
+                bins[hi].ents.erase(bins[hi].ents.begin() + static_cast<std::ptrdiff_t>(best_k));
+                bins[hi].recs -= d;
+                bins[hi].users -= 1;
+                bins[lo].ents.push_back(x);
+                bins[lo].recs += d;
+                bins[lo].users += 1;
+                cost[hi] = bh;
+                cost[lo] = bl;
+            }
         }
         std::vector<Ent> sorted;
         sorted.reserve(ents.size());
@@ -640,7 +705,7 @@ static void tile_launch_t(rs_svd_plan* pl, float lr, float reg, hipStream_t s, f
 template <int E, int NW>
 static void tile_launch_r(rs_svd_plan* pl, float lr, float reg, hipStream_t s, float* dP) {
     constexpr int kMax = 60 / (2 * E);  // 15 at E = 2 (k <= 127), 6 at E = 5 (k <= 319), 3 at E = 8
-    const int want = pl->tile_ring > 0 ? pl->tile_ring : 4;
+    const int want = pl->tile_ring > 0 ? pl->tile_ring : 2;
     if constexpr (E == 2 && NW == 16) {  // diagnostics (RSGPU_TILE_DIAG, experiments only): bits drop
         static const int diag = std::getenv("RSGPU_TILE_DIAG") ? std::atoi(std::getenv("RSGPU_TILE_DIAG")) : 0;
         switch (diag) {  // 1 q atomics, 2 q loads, 4 p LDS atomics, 8 p LDS reads

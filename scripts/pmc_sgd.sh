@@ -12,4 +12,4 @@ for C in FETCH_SIZE WRITE_SIZE; do
   timeout -k 10 300 rocprofv3 --pmc $C --kernel-trace --output-format csv -d "$OUT/$C" -o run -- \
       python3 "$ROOT/bench.py" --steps 5 --warmup 1 --no-cpu-baseline > "$OUT/$C.log" 2>&1 || exit 20
 done
-python3 "$ROOT/scripts/parse_pmc.py" "$OUT" svd_epoch_hybrid_kernel > "$ROOT/gpurun_out/sgd_traffic.json"
+python3 "$ROOT/scripts/parse_pmc.py" "$OUT" svd_epoch_tile_kernel > "$ROOT/gpurun_out/sgd_traffic.json"

@@ -79,6 +79,27 @@ def test_chunked_single_user_equals_ordered():
     assert abs(a[4] - b[4]) < 1e-12
 
 
+def test_svdpp_lazy_equals_userwise_literal():
+    """or_svdpp_fit_lazy (O(nnz k)) is the user-major schedule of or_svdpp_fit_userwise (literal
+    svd.go:352-424 per rating, O(sum |N|^2 k)) up to rounding: rows without repeated items."""
+    rng = np.random.default_rng(5)
+    nu, ni, k = 40, 60, 12
+    us, it = [], []
+    for x in range(nu):
+        d = int(rng.integers(1, 30))
+        us.append(np.full(d, x))
+        it.append(rng.choice(ni, d, replace=False))
+    u, i = np.concatenate(us), np.concatenate(it)
+    r = rng.integers(1, 6, len(u)).astype(float)
+    rowptr, items, rr = O.csr_by(u, nu, i, r)
+    P0, Q0, Y0 = rng.normal(0, 0.1, (nu, k)), rng.normal(0, 0.1, (ni, k)), rng.normal(0, 0.1, (ni, k))
+    a = O.svdpp_fit_userwise(rowptr, items, rr, P0, Q0, Y0, epochs=3)
+    b = O.svdpp_fit_lazy(rowptr, items, rr, P0, Q0, Y0, epochs=3)
+    for x, y in zip(a[:5], b[:5]):
+        np.testing.assert_allclose(x, y, rtol=0, atol=1e-10)
+    assert abs(a[5] - b[5]) < 1e-12
+
+
 @pytest.fixture(scope="module")
 def ml100k_folds(ml100k):
     return folds(*ml100k)
