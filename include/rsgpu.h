@@ -48,6 +48,8 @@ extern "C" {
 #define RS_ERR_NOMEM (-3)       /* host or device allocation failed                               */
 #define RS_ERR_UNSUPPORTED (-4) /* valid request this build does not implement                    */
 #define RS_ERR_NO_DEVICE (-5)   /* no gfx950 device visible                                       */
+#define RS_ERR_NUMERIC (-6)     /* the model left its number format (non-finite or |q| >= 128);
+                                   the values are still returned                                   */
 
 /* SGD visit schedule (SURVEY §8a parity contract P1/P2) */
 #define RS_SGD_FAST 0    /* user-CSR, one wave per user, atomic q_i deltas, deferred global bias */
@@ -280,9 +282,12 @@ int rs_svd_plan_trace(rs_svd_plan* plan, int64_t* out, int32_t* user);
  * K1): at 1200 the ML-1M-shaped held-out RMSE moves by +0.0008 (to within 0.0001 of the reference
  * visit order's); at 256 by +0.024. */
 int rs_svd_plan_set_split(rs_svd_plan* plan, int32_t split_cap);
-/* FAST-mode hot items: an item with more than item_cap ratings (default 0 = never) gets
+/* RS_SGD_WB_ATOMIC (hybrid) hot items: an item with more than item_cap ratings gets
  * ceil(deg / item_cap) row copies; its ratings are dealt over them in user-CSR order and the copies
- * are merged by count-weighted average after every epoch.  Spreads the float atomics of hot rows. */
+ * are merged by count-weighted average after every epoch.  Spreads the atomics of hot rows.
+ * item_cap = 0 (default) is automatic: only items too hot for hot replicas (more than 65536 x copies
+ * ratings, whose live copies diverge) are cut, into 65536-rating pieces.
+ * The tile schedule (RS_SGD_WB_TILE) bounds hot-item staleness by its own run cap instead. */
 int rs_svd_plan_set_item_split(rs_svd_plan* plan, int32_t item_cap);
 /* Hot replicas: the n_hot most-rated items (0 = none) get `copies` row copies (2..8) over which their
  * ratings are dealt, and in RS_SGD_WB_ATOMIC (hybrid) epochs one extra block keeps the copies merged
@@ -294,8 +299,10 @@ int rs_svd_plan_set_hot_replicas(rs_svd_plan* plan, int32_t n_hot, int32_t copie
 /* Fixed-point item rows (default on; 0 turns it off): RS_SGD_WB_ATOMIC (hybrid) epochs convert Q in place to int32
  * round(q * 2^24) before the epoch kernel and back after it, and the q_i deltas become integer
  * atomics (memory-side u32 adds run at 1.69 TB/s against 1.32 TB/s for f32 on gfx950).  The
- * resolution is the fp32 ulp at |q| in [0.5, 1); |q| must stay below 128 (saturates).  Other
- * write-back modes ignore it. */
+ * resolution is the fp32 ulp at |q| in [0.5, 1); |q| must stay below 128: the conversion to int32
+ * saturates, but integer atomics wrap, so the conversion back flags a row that reached the range
+ * limit or a non-finite value and the next call returns RS_ERR_NUMERIC.  The tile schedule
+ * (RS_SGD_WB_TILE) always keeps Q in this format during a call, with the same check. */
 int rs_svd_plan_set_fixed_q(rs_svd_plan* plan, int32_t on);
 /* ---- item-sharded multi-GPU (north_star: Q sharded by item range, users replicated) --------- *
  * Each rank builds a plan over its item shard.  Per epoch: rs_svd_plan_epoch_delta leaves P at the

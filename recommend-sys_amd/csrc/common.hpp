@@ -41,6 +41,11 @@ struct HipError {
     std::string what;
 };
 
+// a result the device flagged as out of its number format (RS_ERR_NUMERIC)
+struct NumericError {
+    std::string what;
+};
+
 #define RS_HIP(call)                                                                          \
     do {                                                                                      \
         hipError_t _e = (call);                                                               \
@@ -119,6 +124,8 @@ int rs_guard(rs_ctx* ctx, F&& body) {
         return body();
     } catch (const rs::HipError& e) {
         return rs::set_error(ctx, e.code == hipErrorOutOfMemory ? RS_ERR_NOMEM : RS_ERR_HIP, e.what);
+    } catch (const rs::NumericError& e) {
+        return rs::set_error(ctx, RS_ERR_NUMERIC, e.what);
     } catch (const std::bad_alloc&) {
         return rs::set_error(ctx, RS_ERR_NOMEM, "host allocation failed");
     } catch (const std::exception& e) {

@@ -603,12 +603,26 @@ __global__ __launch_bounds__(64) void svd_live_merge_kernel(float* __restrict__ 
     }
 }
 
-// Fixed-point item rows around a hybrid epoch (rs_svd_plan_set_fixed_q), in place over Q's n
-// words: to == 1: q -> round(q * 2^24) (saturating), to == 0: back to fp32.
-__global__ __launch_bounds__(256) void svd_q_fixed_kernel(float* __restrict__ Q, int64_t n, int32_t to) {
+// Fixed-point item rows around a call (tile schedule; hybrid with rs_svd_plan_set_fixed_q), in place
+// over Q's n words: to == 1: q -> round(q * 2^24) (saturating), to == 0: back to fp32.  A value that
+// is non-finite or |q| >= 128 going in, or within 2^-1 of the int32 range coming back (integer
+// atomics wrap), raises *flag (plan_download reports RS_ERR_NUMERIC).
+__global__ __launch_bounds__(256) void svd_q_fixed_kernel(float* __restrict__ Q, int64_t n, int32_t to,
+                                                          int32_t* __restrict__ flag) {
+    bool bad = false;
     for (int64_t t = static_cast<int64_t>(blockIdx.x) * 256 + threadIdx.x; t < n;
-         t += static_cast<int64_t>(gridDim.x) * 256)
-        Q[t] = to ? __int_as_float(__float2int_rn(Q[t] * kFx)) : fx_to_f(__float_as_uint(Q[t]));
+         t += static_cast<int64_t>(gridDim.x) * 256) {
+        if (to) {
+            const float v = Q[t];
+            bad |= !(fabsf(v) < 128.0f);
+            Q[t] = __int_as_float(__float2int_rn(v * kFx));
+        } else {
+            const int32_t v = __float_as_int(Q[t]);
+            bad |= v >= (127 << 24) + (1 << 23) || v <= -((127 << 24) + (1 << 23));
+            Q[t] = fx_to_f(static_cast<uint32_t>(v));
+        }
+    }
+    if (bad) flag[0] = 1;
 }
 
 // The live items' final merge round on the int32 rows (fixed-point epochs): exact integer
@@ -979,9 +993,9 @@ static void launch_fast(rs_svd_plan* pl, float lr, float reg, hipStream_t s, flo
         }
         const int64_t qn = static_cast<int64_t>(pl->Q.n);
         const int fx_blocks = static_cast<int>(std::min<int64_t>(2048, (qn + 255) / 256));
-        hipLaunchKernelGGL(svd_q_fixed_kernel, dim3(fx_blocks), dim3(256), 0, s, pl->Q.p, qn, 1);
+        hipLaunchKernelGGL(svd_q_fixed_kernel, dim3(fx_blocks), dim3(256), 0, s, pl->Q.p, qn, 1, numflag(pl));
         tile_launch(pl, lr, reg, s, dP);
-        hipLaunchKernelGGL(svd_q_fixed_kernel, dim3(fx_blocks), dim3(256), 0, s, pl->Q.p, qn, 0);
+        hipLaunchKernelGGL(svd_q_fixed_kernel, dim3(fx_blocks), dim3(256), 0, s, pl->Q.p, qn, 0, numflag(pl));
         RS_HIP(hipGetLastError());
         return;
     }
@@ -993,7 +1007,7 @@ static void launch_fast(rs_svd_plan* pl, float lr, float reg, hipStream_t s, flo
     const bool fx = pl->fixed_q && pl->write_back == RS_SGD_WB_ATOMIC;
     const int64_t qn = static_cast<int64_t>(pl->Q.n);
     const int fx_blocks = static_cast<int>(std::min<int64_t>(2048, (qn + 255) / 256));
-    if (fx) hipLaunchKernelGGL(svd_q_fixed_kernel, dim3(fx_blocks), dim3(256), 0, s, pl->Q.p, qn, 1);
+    if (fx) hipLaunchKernelGGL(svd_q_fixed_kernel, dim3(fx_blocks), dim3(256), 0, s, pl->Q.p, qn, 1, numflag(pl));
     if (pl->n_live > 0)  // L = the live items' rows at the epoch start (a bit copy: int32 rows too)
         hipLaunchKernelGGL(svd_live_merge_kernel, dim3(pl->n_live), dim3(64), 0, s, pl->Q.p, pl->live_meta.p,
                            pl->qlast.p, pl->ld, 0);
@@ -1011,7 +1025,7 @@ static void launch_fast(rs_svd_plan* pl, float lr, float reg, hipStream_t s, flo
                                reinterpret_cast<int32_t*>(pl->qlast.p), pl->ld);
             pl->live_merged = true;
         }
-        hipLaunchKernelGGL(svd_q_fixed_kernel, dim3(fx_blocks), dim3(256), 0, s, pl->Q.p, qn, 0);
+        hipLaunchKernelGGL(svd_q_fixed_kernel, dim3(fx_blocks), dim3(256), 0, s, pl->Q.p, qn, 0, numflag(pl));
     }
     RS_HIP(hipGetLastError());
 }
@@ -1052,14 +1066,26 @@ static void launch_ordered(int64_t nnz, const int32_t* u, const int32_t* i, cons
 
 int32_t fast_ld(int32_t k) { return 64 * ((k + 1 + 63) / 64); }
 
+int32_t* numflag(rs_svd_plan* pl) {
+    if (!pl->numflag.p) {
+        pl->numflag.alloc(1);
+        RS_HIP(hipMemsetAsync(pl->numflag.p, 0, sizeof(int32_t), pl->ctx->stream));
+        RS_HIP(hipStreamSynchronize(pl->ctx->stream));
+    }
+    return pl->numflag.p;
+}
+
 void plan_sync_last(rs_svd_plan* pl) {
     if (pl->last_stream) RS_HIP(hipStreamSynchronize(pl->last_stream));
 }
 
-// Item row copies from the host CSR: an item with deg > item_cap gets R = ceil(deg / item_cap) rows
-// (its own plus R - 1 appended after n_items); its ratings are dealt in user-CSR order, piece
-// c taking positions [c deg / R, (c + 1) deg / R).  Q is (re)allocated to n_qrows rows keeping the
-// item rows; copies are synced from them.
+// Item row copies from the host CSR: an item with deg > cap gets R = ceil(deg / cap) rows (its own
+// plus R - 1 appended after n_items); its ratings are dealt in user-CSR order, the s-th rating of the
+// item going to piece floor(s R / deg), so piece c takes positions [ceil(c deg / R), ceil((c + 1) deg
+// / R)) and its merge weight is that count / deg.  cap = item_cap when set; with item_cap = 0 (the
+// default) only the items too hot for hot replicas (deg > kAutoItemCap x live_copies) are cut, into
+// kAutoItemCap-rating pieces.  Q is (re)allocated to n_qrows rows keeping the item rows; copies are
+// synced from them.
 static void sync_item_copies(rs_svd_plan* pl, hipStream_t s, int32_t mode) {
     if (pl->n_isplit > 0)
         hipLaunchKernelGGL(svd_item_merge_kernel, dim3(pl->n_isplit), dim3(64), 0, s, pl->Q.p,
@@ -1073,6 +1099,10 @@ static void sync_item_copies(rs_svd_plan* pl, hipStream_t s, int32_t mode) {
     }
 }
 
+// measured at configs[4] (Zipf head of 3.4M ratings in a 1/8 shard): 8 live copies of such an item
+// diverge to NaN within 5 epochs where 52 averaged copies of 65536 ratings train
+constexpr int64_t kAutoItemCap = 65536;
+
 static void build_items(rs_svd_plan* pl) {
     hipStream_t s = pl->ctx->stream;
     const int32_t ni = pl->n_items;
@@ -1085,15 +1115,13 @@ static void build_items(rs_svd_plan* pl) {
     int32_t extra = 0;
     // hot replicas (live-merged copies): the live_req most-rated items with at least one rating per copy
     std::vector<uint8_t> is_live(std::max(1, ni), 0);
+    const int64_t cap = pl->item_cap > 0 ? pl->item_cap : kAutoItemCap;
+    const int64_t split_above = pl->item_cap > 0 ? cap : cap * pl->live_copies;
     if (pl->live_req > 0) {
         std::vector<int32_t> order;
-        // an item that item_cap would cut into more than live_copies pieces stays with item_cap: measured
-        // at configs[4] (Zipf head of 3.4M ratings in a 1/8 shard), 8 live copies of such an item
-        // diverge to NaN within 5 epochs where 52 averaged copies train
+        // an item that the cap would cut into more than live_copies pieces is split instead
         for (int32_t x = 0; x < ni; ++x)
-            if (deg[x] >= pl->live_copies &&
-                !(pl->item_cap > 0 && deg[x] > static_cast<int64_t>(pl->item_cap) * pl->live_copies))
-                order.push_back(x);
+            if (deg[x] >= pl->live_copies && deg[x] <= cap * pl->live_copies) order.push_back(x);
         const size_t nh = std::min(order.size(), static_cast<size_t>(pl->live_req));
         std::partial_sort(order.begin(), order.begin() + nh, order.end(), [&](int32_t a, int32_t b) {
             return deg[a] != deg[b] ? deg[a] > deg[b] : a < b;
@@ -1106,12 +1134,12 @@ static void build_items(rs_svd_plan* pl) {
             first[x] = ni + extra;
             live.push_back(make_int4(x, ni + extra, R[x], 0));
             extra += R[x] - 1;
-        } else if (pl->item_cap > 0 && deg[x] > pl->item_cap) {
-            R[x] = static_cast<int32_t>((deg[x] + pl->item_cap - 1) / pl->item_cap);
+        } else if (deg[x] > split_above) {
+            R[x] = static_cast<int32_t>((deg[x] + cap - 1) / cap);
             first[x] = ni + extra;
             meta.push_back(make_int4(x, ni + extra, R[x], static_cast<int32_t>(frac.size())));
-            for (int32_t c = 0; c < R[x]; ++c) {
-                const int64_t lo = deg[x] * c / R[x], hi = deg[x] * (c + 1) / R[x];
+            for (int32_t c = 0; c < R[x]; ++c) {  // the deal's own bounds (see deal below)
+                const int64_t lo = (deg[x] * c + R[x] - 1) / R[x], hi = (deg[x] * (c + 1) + R[x] - 1) / R[x];
                 frac.push_back(static_cast<float>(static_cast<double>(hi - lo) / deg[x]));
             }
             extra += R[x] - 1;
@@ -1418,6 +1446,17 @@ static void plan_download(rs_svd_plan* pl, double* P, double* Q, double* bu, dou
         pl->gb.download(gb, 1, s);
         RS_HIP(hipStreamSynchronize(s));
     }
+    if (pl->numflag.p) {  // raised by a Q conversion: report once, values already returned
+        int32_t f = 0;
+        pl->numflag.download(&f, 1, s);
+        RS_HIP(hipStreamSynchronize(s));
+        if (f) {
+            RS_HIP(hipMemsetAsync(pl->numflag.p, 0, sizeof(int32_t), s));
+            RS_HIP(hipStreamSynchronize(s));
+            throw NumericError{"item factors left the fixed-point range (non-finite or |q| >= 128) during "
+                               "an epoch; the returned model is not trustworthy"};
+        }
+    }
 }
 
 static void plan_epochs(rs_svd_plan* pl, int32_t epochs, float lr, float reg, hipStream_t s) {
@@ -1439,7 +1478,7 @@ static void plan_epochs(rs_svd_plan* pl, int32_t epochs, float lr, float reg, hi
     const int64_t qn = static_cast<int64_t>(pl->Q.n);
     const int fx_blocks = static_cast<int>(std::min<int64_t>(2048, (qn + 255) / 256));
     if (hoist) {
-        hipLaunchKernelGGL(svd_q_fixed_kernel, dim3(fx_blocks), dim3(256), 0, s, pl->Q.p, qn, 1);
+        hipLaunchKernelGGL(svd_q_fixed_kernel, dim3(fx_blocks), dim3(256), 0, s, pl->Q.p, qn, 1, numflag(pl));
         if (!tile && pl->n_live > 0) {
             hipLaunchKernelGGL(svd_live_merge_kernel, dim3(pl->n_live), dim3(64), 0, s, pl->Q.p, pl->live_meta.p,
                                pl->qlast.p, pl->ld, 0);
@@ -1464,7 +1503,7 @@ static void plan_epochs(rs_svd_plan* pl, int32_t epochs, float lr, float reg, hi
             RS_HIP(hipGetLastError());
         }
         pl->hoisted = false;
-        hipLaunchKernelGGL(svd_q_fixed_kernel, dim3(fx_blocks), dim3(256), 0, s, pl->Q.p, qn, 0);
+        hipLaunchKernelGGL(svd_q_fixed_kernel, dim3(fx_blocks), dim3(256), 0, s, pl->Q.p, qn, 0, numflag(pl));
         RS_HIP(hipGetLastError());
         RS_HIP(hipEventRecord(pl->ev1, s));
         pl->last_launches = pl->timing ? epochs : 2 * epochs;  // SGD + epilogue (conversions in the span)
@@ -1889,8 +1928,11 @@ extern "C" int rs_svd_plan_device_ptrs(rs_svd_plan* pl, void** P, void** Q, void
 
 extern "C" int rs_svd_plan_set_timing(rs_svd_plan* pl, int32_t on) {
     if (!pl) return rs::set_error(nullptr, RS_ERR_INVALID, "plan is NULL");
-    pl->timing = on != 0;
-    return RS_OK;
+    return rs_guard(pl->ctx, [&]() -> int {
+        rs::plan_sync_last(pl);  // epochs in flight keep the timing mode they were enqueued with
+        pl->timing = on != 0;
+        return RS_OK;
+    });
 }
 
 extern "C" int rs_svd_plan_last_kernel_ms(rs_svd_plan* pl, double* ms, int32_t* n_launches) {

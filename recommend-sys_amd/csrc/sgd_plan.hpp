@@ -42,7 +42,8 @@ struct rs_svd_plan {
     int32_t n_live = 0;
     rs::DevBuf<int4> live_meta;  // {item row, first extra row, copies, -}
     rs::DevBuf<float> qlast;     // last merged value of every live item (n_live x ld)
-    rs::DevBuf<int32_t> done;    // blocks finished (the merger's exit condition)
+    rs::DevBuf<int32_t> done;
+    rs::DevBuf<int32_t> numflag;  // raised by svd_q_fixed_kernel (RS_ERR_NUMERIC at download)    // blocks finished (the merger's exit condition)
     rs::DevBuf<float> iw;  // per-item share of this shard (user-sharded multi-GPU mode)
     rs::DevBuf<float> Q0;  // Q at the epoch start (user-sharded mode)
     int32_t n_blocks = 0;
@@ -138,6 +139,7 @@ __device__ __forceinline__ float lane63(float x) {
 
 // sgd.hip
 void plan_sync_last(rs_svd_plan* pl);  // waits for the stream of the last enqueued epochs
+int32_t* numflag(rs_svd_plan* pl);  // the RS_ERR_NUMERIC device flag (allocated on first use)
 
 // sgd_tile.hip
 void tile_build(rs_svd_plan* pl);  // (re)builds the tile schedule from the host CSR

@@ -17,7 +17,7 @@ LIB_PATH = _build.LIB
 _lib = None
 
 RS_OK = 0
-RS_ERR_INVALID, RS_ERR_HIP, RS_ERR_NOMEM, RS_ERR_UNSUPPORTED, RS_ERR_NO_DEVICE = -1, -2, -3, -4, -5
+RS_ERR_INVALID, RS_ERR_HIP, RS_ERR_NOMEM, RS_ERR_UNSUPPORTED, RS_ERR_NO_DEVICE, RS_ERR_NUMERIC = -1, -2, -3, -4, -5, -6
 SGD_FAST, SGD_ORDERED = 0, 1
 WB_TILE, WB_STORE, WB_ATOMIC_DIRECT, WB_ATOMIC = 0, 1, 2, 3  # WB_TILE: the default schedule
 SIM_COSINE, SIM_MSD, SIM_PEARSON = 0, 1, 2

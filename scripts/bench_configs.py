@@ -1,9 +1,14 @@
 #!/usr/bin/env python3
 """Measures the BASELINE.json configurations that bench.py does not cover (bench.py = configs[1]):
 
-  config 3  SVD++ nFactors=128 on an ML-1M-shaped set (FAST lazy-y kernel K2)
-  config 4  KNN item-based Cosine on an ML-20M-shaped set (int8-MFMA K4)
-  extra     NMF nFactors=15 on the ML-1M-shaped set (K3; no BASELINE config)
+  0    configs[0]: SVD nFactors=20, 5-fold ML-100K (the reference's own u.data), CPU: the C fp64
+       restatement of core/svd.go:63-132 on one core (the Go Fit() plumbing of benchmark.go:12-52),
+       with the GPU fit of the same folds beside it
+  2    configs[2]: SVD++ nFactors=128 on an ML-1M-shaped set (FAST lazy-y kernel K2)
+  3    configs[3]: KNN item-based Cosine on an ML-20M-shaped set (int8-MFMA K4)
+  4    configs[4]: SVD nFactors=256 on the 1/8 item shard of the 10M x 1M x 1e9 synthetic set (one
+       GPU's share of the item-sharded fit), library defaults (tile schedule K1)
+  nmf  NMF nFactors=15 on the ML-1M-shaped set (K3; no BASELINE config)
 
 Each line: kernel-only device time (HIP events on the launch stream, rs_last_kernel_ms), the
 roofline fraction against the bound SURVEY §8d names, and a CPU baseline timed on this host on a
@@ -35,7 +40,54 @@ def emit(d, out):
             f.write(line + "\n")
 
 
-def config3(ctx, out, epochs=5):
+def host_info():
+    model = "unknown"
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                model = line.split(":", 1)[1].strip()
+                break
+    except OSError:
+        pass
+    return {"nproc": os.cpu_count(), "cpu_model": model}
+
+
+def config0(ctx, out, k=20, epochs=20):
+    import oracle as O
+    import rsgpu
+    sys.path.insert(0, os.path.join(REPO, "tests"))
+    from helpers import folds, rmse
+    d = np.load(os.path.join(REPO, "tests", "golden", "ml100k.npz"))
+    U, I, R = d["users"].astype(np.int64), d["items"].astype(np.int64), d["ratings"].astype(np.float64)
+    fl = folds(U, I, R)
+    cpu_s, gpu_s, cpu_rmse, gpu_rmse, n_upd = 0.0, 0.0, [], [], 0
+    for f in fl:
+        rng = np.random.default_rng(7)
+        P0, Q0 = rng.normal(0, 0.1, (f.nu, k)), rng.normal(0, 0.1, (f.ni, k))
+        t0 = time.perf_counter()
+        m = O.svd_fit(f.iu, f.ii, f.r, P0, Q0, epochs=epochs)
+        cpu_s += time.perf_counter() - t0
+        cpu_rmse.append(rmse(O.svd_predict(f.tu, f.ti, *m), f.te_r))
+        rr = rsgpu.Ratings(f.iu, f.ii, f.r, f.nu, f.ni)
+        ctx.svd_fit(rr, P0, Q0, n_epochs=1)  # warm-up (code objects, allocator)
+        t0 = time.perf_counter()
+        g = ctx.svd_fit(rr, P0, Q0, n_epochs=epochs)
+        gpu_s += time.perf_counter() - t0
+        gpu_rmse.append(rmse(O.svd_predict(f.tu, f.ti, *g), f.te_r))
+        n_upd += len(f.r) * epochs
+    emit({"config": "SVD nFactors=20, 5-fold CV on ML-100K (BASELINE configs[0], reference's own u.data)",
+          "cpu": {"fit_s_5_folds": cpu_s, "updates_per_s": n_upd / cpu_s, "cores": 1, "kind": "port",
+                  "what": "oracle C fp64 restatement of core/svd.go:63-132 (reference visit order), "
+                          "one thread, 20 epochs per fold", **host_info()},
+          "rmse_cpu_mean": float(np.mean(cpu_rmse)),
+          "gpu": {"fit_s_5_folds": gpu_s, "updates_per_s": n_upd / gpu_s,
+                  "what": "rs_svd_fit (one-shot Fit through the C-ABI, FAST tile schedule), wall "
+                          "time per call incl. host packing and H2D/D2H"},
+          "rmse_gpu_mean": float(np.mean(gpu_rmse)),
+          "reference_bound": "core/base_test.go:35 checks RMSE <= 0.942 on this CV"}, out)
+
+
+def config2(ctx, out, epochs=5):
     import oracle as O
     import rsgpu
     from rsgpu import synth
@@ -69,7 +121,7 @@ def config3(ctx, out, epochs=5):
                                      f"full-set |N(u)| (x{deg_full / deg_pref:.1f})"}}, out)
 
 
-def config4(ctx, out):
+def config3(ctx, out):
     import oracle as O
     import rsgpu
     from rsgpu import synth
@@ -106,13 +158,45 @@ def config4(ctx, out):
           "pairs_per_s": L * (L - 1) / 2 / (ms / 1e3),
           "roofline": {"bound": "mfma", "achieved_TOPs_executed": executed / (ms / 1e3) / 1e12,
                        "achieved_TOPs_algorithmic": algorithmic / (ms / 1e3) / 1e12,
-                       "peak_TOPs": I8_PEAK, "frac": executed / (ms / 1e3) / 1e12 / I8_PEAK,
+                       "peak_TOPs": I8_PEAK, "frac": algorithmic / (ms / 1e3) / 1e12 / I8_PEAK,
+                       "frac_executed": executed / (ms / 1e3) / 1e12 / I8_PEAK,
                        "executed_int8_ops": executed, "algorithmic_int8_ops": algorithmic},
           "parity_rows_0_63_bitwise": bool(same),
           "cpu_baseline": {"value": L * (L - 1) / 2 / t_full, "unit": "pairs/s", "cores": 1,
                            "kind": "port", "sample": f"rows 0-{rows - 1} x {L} partners, merge "
                            f"restatement {t_blk:.1f} s, extrapolated x{L / rows / 2:.0f} to the "
                            f"unique pairs ({t_full:.0f} s)"}}, out)
+
+
+def config4(ctx, out, epochs=5):
+    import rsgpu
+    n_users, n_items, k = 10_000_000, 1_000_000, 256
+    t0 = time.perf_counter()
+    s = rsgpu.Synth(n_users, n_items, mean_deg=100.0, seed=20250826, item_lo=0, item_hi=n_items // 8,
+                    n_threads=16)
+    t_gen = time.perf_counter() - t0
+    t0 = time.perf_counter()
+    plan = ctx.svd_plan_csr(n_users, n_items, s.rowptr, s.cols, s.vals, k)
+    t_build = time.perf_counter() - t0
+    plan.init_normal(0.0, 0.1, seed=1)
+    plan.epochs(1)
+    plan.set_timing(True)
+    plan.epochs(epochs)
+    ms, nl = plan.last_kernel_ms()
+    plan.set_timing(False)
+    P, Q, bu, bi, gb = plan.download()
+    finite = bool(np.isfinite(Q).all() and np.isfinite(P).all() and np.isfinite(gb))
+    nnz = s.nnz
+    ab = nnz * (16 + 8 * k) + n_users * (16 + 8 * k)
+    t_ep = ms / nl / 1e3
+    plan.close()
+    s.close()
+    emit({"config": "SVD nFactors=256, 1/8 item shard of the 10M x 1M x 1e9 synthetic set (BASELINE configs[4], one GPU's share)",
+          "kernel": "svd_epoch_tile_kernel<E=5,NW=16,RQ=2> (library defaults)",
+          "nnz": int(nnz), "epoch_ms_kernel": t_ep * 1e3, "updates_per_s": nnz / t_ep,
+          "plan_build_s": t_build, "synth_s": t_gen, "finite": finite,
+          "roofline": {"bound": "hbm", "achieved_GBs": ab / t_ep / 1e9, "peak_GBs": HBM_PEAK,
+                       "frac": ab / t_ep / 1e9 / HBM_PEAK, "algorithmic_bytes": ab}}, out)
 
 
 def nmf(ctx, out, epochs=50):
@@ -142,18 +226,16 @@ def nmf(ctx, out, epochs=50):
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--only", default="3,4,nmf")
+    ap.add_argument("--only", default="0,2,3,4,nmf")
     ap.add_argument("--out", default="")
     a = ap.parse_args()
     import rsgpu
     ctx = rsgpu.Context(0)
     which = a.only.split(",")
-    if "3" in which:
-        config3(ctx, a.out)
-    if "nmf" in which:
-        nmf(ctx, a.out)
-    if "4" in which:
-        config4(ctx, a.out)
+    for name, fn in (("0", config0), ("2", config2), ("nmf", nmf), ("3", config3), ("4", config4)):
+        if name in which:
+            print(f"running {name}", file=sys.stderr, flush=True)
+            fn(ctx, a.out)
     ctx.close()
 
 

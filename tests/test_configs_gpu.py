@@ -94,25 +94,30 @@ def test_config3_knn_cosine_ml20m_rows_bitwise(ctx):
 
 
 @pytest.mark.timeout(900)
-def test_config4_item_shard_k256_defaults(ctx):
+@pytest.mark.parametrize("mode", ["tile", "hybrid"])
+def test_config4_item_shard_k256_defaults(ctx, mode):
+    """Library defaults of the tile schedule (the FAST default) and of the hybrid schedule
+    (RS_SGD_WB_ATOMIC, whose automatic item cap splits the Zipf head instead of replicating it live)."""
     n_users, n_items, k = 10_000_000, 1_000_000, 256
     s = rsgpu.Synth(n_users, n_items, mean_deg=100.0, seed=20250826, item_lo=0,
                     item_hi=n_items // 8, n_threads=16)
     deg = np.diff(s.rowptr)
     hot = int(np.bincount(s.cols, minlength=n_items).max())
-    print(f"config4: shard of {s.nnz} ratings generated, hottest item {hot}", flush=True)
+    print(f"config4 {mode}: shard of {s.nnz} ratings generated, hottest item {hot}", flush=True)
     assert hot >= 1_000_000  # the Zipf head that diverged under round 1's defaults
     users = np.repeat(np.arange(n_users, dtype=np.int32), deg)
     hold = np.random.default_rng(0).random(s.nnz) < 0.001
     keep = ~hold
     tr_rowptr = np.concatenate([[0], np.cumsum(np.bincount(users[keep], minlength=n_users))]).astype(np.int64)
     plan = ctx.svd_plan_csr(n_users, n_items, tr_rowptr, s.cols[keep], s.vals[keep], k)
+    if mode == "hybrid":
+        plan.set_mode(rsgpu.WB_ATOMIC)
     plan.init_normal(0.0, 0.1, seed=1)
     e0 = plan.evaluate(users[hold], s.cols[hold], s.vals[hold])[0]
-    print(f"config4: plan built, held-out RMSE at init {e0:.4f}", flush=True)
+    print(f"config4 {mode}: plan built, held-out RMSE at init {e0:.4f}", flush=True)
     for ep in range(5):
         plan.epochs(1)
-        print(f"config4: epoch {ep + 1}: held-out RMSE {plan.evaluate(users[hold], s.cols[hold], s.vals[hold])[0]:.4f}",
+        print(f"config4 {mode}: epoch {ep + 1}: held-out RMSE {plan.evaluate(users[hold], s.cols[hold], s.vals[hold])[0]:.4f}",
               flush=True)
     e5, mae = plan.evaluate(users[hold], s.cols[hold], s.vals[hold])
     plan.close()

@@ -189,3 +189,24 @@ def test_mode_switch_keeps_model(ctx):
         assert not np.array_equal(before[1], plan.download()[1])
     plan.close()
     assert errs[-1] < errs[0] - 0.1 and all(b < a for a, b in zip(errs, errs[1:])), errs
+
+
+@pytest.mark.parametrize("mode", ["tile", "hybrid"])
+def test_out_of_range_q_is_reported(ctx, mode):
+    """Q is int32 fixed point (2^-24) during a call and integer atomics wrap: an item factor at or
+    beyond 128 (or non-finite) is flagged and download reports RS_ERR_NUMERIC once (values returned)."""
+    u, i, r, nu, ni = synth.small_like(200, 100, 4000, seed=3)
+    k = 16
+    rng = np.random.default_rng(0)
+    Q0 = rng.normal(0, 0.1, (ni, k))
+    Q0[7, 3] = 300.0
+    plan = ctx.svd_plan(rsgpu.Ratings(u, i, r, nu, ni), k)
+    if mode == "hybrid":
+        plan.set_mode(rsgpu.WB_ATOMIC)
+    plan.upload(rng.normal(0, 0.1, (nu, k)), Q0, np.zeros(nu), np.zeros(ni), 3.0)
+    plan.epochs(1)
+    with pytest.raises(rsgpu.RsError) as e:
+        plan.download()
+    assert e.value.code == rsgpu.RS_ERR_NUMERIC
+    plan.download()  # reported once
+    plan.close()
