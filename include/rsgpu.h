@@ -318,6 +318,41 @@ int rs_svd_plan_epoch_delta(rs_svd_plan* plan, float lr, float reg, void* dP, vo
                             void* stream);
 int rs_svd_plan_apply_delta(rs_svd_plan* plan, const void* dP, const void* gbsum,
                             double inv_total_nnz, void* stream);
+/* ---- item-sharded multi-GPU behind the library (RCCL over xGMI; multi.hip) ------------------- *
+ * The protocol above with the collective inside the library, pipelined per user block: the users are
+ * cut into n_blocks ranges of near-equal ratings, each with its own tiles; while block b + 1's SGD
+ * kernel runs, block b's dP rows are all-reduced (RCCL, in place) and applied to P on a second
+ * stream, so only the last block's exchange is exposed per epoch.  The user
+ * weights and the total are computed by the library.  Tile schedule only (RS_SGD_WB_TILE).
+ *
+ * One process per GPU (the Go host's one-process-per-GPU mode, bench.py --gpus N): rank 0 calls
+ * rs_comm_unique_id and sends the RS_COMM_ID_BYTES bytes to every rank (any channel); every rank
+ * builds a plan over its item shard (same users, same n_factors), uploads the same P / b_u / GlobalBias
+ * and calls rs_svd_plan_join (collective: all ranks together), then rs_svd_plan_epochs_sharded on every
+ * rank with the same arguments.  n_blocks 0 = automatic (1 for one rank, else about 256 MiB of deltas
+ * per block, 2..32).  rs_svd_plan_leave frees the communicator (rs_svd_plan_destroy does too). */
+#define RS_COMM_ID_BYTES 128
+int rs_comm_unique_id(void* id /* RS_COMM_ID_BYTES */);
+int rs_svd_plan_join(rs_svd_plan* plan, const void* id, int32_t rank, int32_t n_ranks, int32_t n_blocks);
+int rs_svd_plan_epochs_sharded(rs_svd_plan* plan, int32_t n_epochs, float lr, float reg, void* stream);
+int rs_svd_plan_leave(rs_svd_plan* plan);
+/* User blocks of the tile schedule (default 1): the visit order becomes block by block.  Set by
+ * rs_svd_plan_join; settable on its own so that a single plan reproduces a joined plan's order. */
+int rs_svd_plan_set_user_blocks(rs_svd_plan* plan, int32_t n_blocks);
+/* One process driving n shards (one host thread per shard): RCCL when every plan has its own device,
+ * otherwise (shards sharing a device: tests) an in-process exchange that sums the shards' deltas in
+ * shard order after a host barrier (same arithmetic, no overlap).  The plans stay owned by the caller;
+ * rs_svd_group_destroy detaches them. */
+typedef struct rs_svd_group rs_svd_group;
+int rs_svd_group_create(rs_svd_plan* const* plans, int32_t n, int32_t n_blocks, rs_svd_group** out);
+int rs_svd_group_epochs(rs_svd_group* group, int32_t n_epochs, float lr, float reg);
+void rs_svd_group_destroy(rs_svd_group* group);
+/* Item shards of near-equal ratings over contiguous inner item ids: bounds (n_shards + 1 entries). */
+int rs_item_shards(int64_t nnz, const int32_t* items, int32_t n_items, int32_t n_shards, int32_t* bounds);
+/* core/svd.go:63-132 (FAST tile schedule) on n_devices GPUs of this process, items sharded by
+ * rs_item_shards, as rs_svd_fit otherwise (GlobalBias warm start, host buffers in / out). */
+int rs_svd_fit_multi(const int32_t* devices, int32_t n_devices, const rs_ratings* r, const rs_sgd_params* p,
+                     int32_t n_blocks, double* P, double* Q, double* bu, double* bi, double* gb);
 /* ---- user-sharded multi-GPU (the dual partition, SURVEY §8e "measured alternative") ---------- *
  * Each rank builds a plan over its user range (local user ids) with ALL items; Q and b_i are
  * replicated, P and b_u are exclusive to the rank.  Per epoch: rs_svd_plan_epoch_qdelta runs the

@@ -1066,6 +1066,19 @@ static void launch_ordered(int64_t nnz, const int32_t* u, const int32_t* i, cons
 
 int32_t fast_ld(int32_t k) { return 64 * ((k + 1 + 63) / 64); }
 
+void q_convert(rs_svd_plan* pl, hipStream_t s, int32_t to_fixed) {
+    const int64_t qn = static_cast<int64_t>(pl->Q.n);
+    if (qn == 0) return;
+    const int fx_blocks = static_cast<int>(std::min<int64_t>(2048, (qn + 255) / 256));
+    hipLaunchKernelGGL(svd_q_fixed_kernel, dim3(fx_blocks), dim3(256), 0, s, pl->Q.p, qn, to_fixed, numflag(pl));
+    RS_HIP(hipGetLastError());
+}
+
+void gb_sum(const double* partial, int64_t n, double* out, hipStream_t s) {
+    hipLaunchKernelGGL(gb_sum_kernel, dim3(1), dim3(256), 0, s, partial, n, out);
+    RS_HIP(hipGetLastError());
+}
+
 int32_t* numflag(rs_svd_plan* pl) {
     if (!pl->numflag.p) {
         pl->numflag.alloc(1);

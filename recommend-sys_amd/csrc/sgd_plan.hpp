@@ -5,10 +5,15 @@
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
+#include <memory>
 #include <vector>
 
 #include "common.hpp"
 #include "wave.hpp"
+
+namespace rs {
+struct ShardComm;  // multi.hip
+}
 
 struct rs_svd_plan {
     rs_ctx* ctx = nullptr;
@@ -42,8 +47,8 @@ struct rs_svd_plan {
     int32_t n_live = 0;
     rs::DevBuf<int4> live_meta;  // {item row, first extra row, copies, -}
     rs::DevBuf<float> qlast;     // last merged value of every live item (n_live x ld)
-    rs::DevBuf<int32_t> done;
-    rs::DevBuf<int32_t> numflag;  // raised by svd_q_fixed_kernel (RS_ERR_NUMERIC at download)    // blocks finished (the merger's exit condition)
+    rs::DevBuf<int32_t> done;     // blocks finished (the merger's exit condition)
+    rs::DevBuf<int32_t> numflag;  // raised by svd_q_fixed_kernel (RS_ERR_NUMERIC at download)
     rs::DevBuf<float> iw;  // per-item share of this shard (user-sharded multi-GPU mode)
     rs::DevBuf<float> Q0;  // Q at the epoch start (user-sharded mode)
     int32_t n_blocks = 0;
@@ -84,6 +89,12 @@ struct rs_svd_plan {
     rs::DevBuf<int2> t_recs;    // {user (tile-local), rating bits}
     rs::DevBuf<int32_t> t_split_rows;  // users cut into pieces over several tiles
     int32_t t_n_split = 0;
+    // user blocks: consecutive user ranges of near-equal ratings, each with its own tiles (tiles
+    // [t_block_tile[b], t_block_tile[b+1]) hold users [t_block_user[b], t_block_user[b+1])); the
+    // item-sharded multi-GPU epoch all-reduces a block's user deltas while the next block computes
+    int32_t tile_ublocks = 1;
+    std::vector<int32_t> t_block_tile, t_block_user;
+    std::shared_ptr<rs::ShardComm> shard;  // item-sharded multi-GPU state (multi.hip), or empty
     ~rs_svd_plan() {
         if (ev0) (void)hipEventDestroy(ev0);
         if (ev1) (void)hipEventDestroy(ev1);
@@ -140,10 +151,16 @@ __device__ __forceinline__ float lane63(float x) {
 // sgd.hip
 void plan_sync_last(rs_svd_plan* pl);  // waits for the stream of the last enqueued epochs
 int32_t* numflag(rs_svd_plan* pl);  // the RS_ERR_NUMERIC device flag (allocated on first use)
+void q_convert(rs_svd_plan* pl, hipStream_t s, int32_t to_fixed);  // Q <-> int32 fixed point in place
+void gb_sum(const double* partial, int64_t n, double* out, hipStream_t s);  // fixed-order sum
 
 // sgd_tile.hip
 void tile_build(rs_svd_plan* pl);  // (re)builds the tile schedule from the host CSR
 void tile_launch(rs_svd_plan* pl, float lr, float reg, hipStream_t s, float* dP);  // one epoch (Q int32)
+// tiles [t0, t1) only (one user block), delta mode into dP (row stride ldd); returns the number of
+// GlobalBias partials written to pl->partial
+int32_t tile_launch_range(rs_svd_plan* pl, float lr, float reg, hipStream_t s, float* dP, int32_t ldd,
+                          int32_t t0, int32_t t1);
 int32_t tile_partials(const rs_svd_plan* pl);  // GlobalBias partials the launch writes
 // visit order of the tile schedule (user-CSR positions, nnz entries) and its GlobalBias work items
 // (one per tile and wave: n_works + 1 offsets into pos); any pointer may be NULL

@@ -85,7 +85,8 @@ __global__ __launch_bounds__(NW * 64) void svd_epoch_tile_kernel(
     const int32_t* __restrict__ streams, const int2* __restrict__ runs, const int2* __restrict__ recs,
     float* __restrict__ P, int32_t* Q, int32_t q_bytes, const double* __restrict__ gb_in,
     double* __restrict__ gb_partial, float lr, float reg, float* __restrict__ dP,
-    const float* __restrict__ uw, float* __restrict__ dPs, int32_t kf, int32_t ldm, int64_t* __restrict__ dbg) {
+    const float* __restrict__ uw, float* __restrict__ dPs, int32_t kf, int32_t ldm, int32_t ldd,
+    int64_t* __restrict__ dbg) {
 #pragma clang fp contract(fast)
     constexpr int LD = 64 * E, NT = NW * 64;  // LD: LDS row (k + 2 columns fit); ldm: the rows in HBM
     constexpr bool TIMED = (DIAG & 16) != 0;  // per-wave phase clocks into dbg (experiments)
@@ -298,10 +299,11 @@ __global__ __launch_bounds__(NW * 64) void svd_epoch_tile_kernel(
             const float frac = __int_as_float(te.y);
             const int64_t g = static_cast<int64_t>(te.x) * ldm + c;
             const float v = fx_to_f(static_cast<uint32_t>(Pl[x]));
-            if (dP) {
+            if (dP) {  // multi-GPU delta mode: dP rows of stride ldd
                 const float d = uw[te.x] * frac * (v - P[g]);
-                if (frac == 1.f) dP[g] = d;
-                else atomicAdd(dP + g, d);
+                const int64_t gd = static_cast<int64_t>(te.x) * ldd + c;
+                if (frac == 1.f) dP[gd] = d;
+                else atomicAdd(dP + gd, d);
             } else if (frac == 1.f) {
                 P[g] = v;
             } else {
@@ -356,8 +358,8 @@ size_t tile_bytes(int64_t users, int64_t recs, int64_t runs, int32_t ld) {  // l
 // Tiles from the host user-CSR.  Entries (user pieces) are consecutive users; a tile closes when the
 // next entry would pass the rating target or the LDS bound (runs <= records).  A user whose ratings
 // do not fit one tile's LDS is cut into near-equal pieces (count-weighted merge after the epoch).
-void build_tile_host(const rs_svd_plan* pl, int32_t nw, int64_t target, int32_t run_cap, bool want_pos,
-                     TileHost& th) {
+void build_tile_host(const rs_svd_plan* pl, int32_t u_begin, int32_t u_end, int32_t nw, int64_t target,
+                     int32_t run_cap, bool want_pos, TileHost& th) {
     const std::vector<int64_t>& rp = pl->h_rowptr;
     const int32_t ld = 64 * ((pl->k + 2 + 63) / 64);  // LDS row: k factors + the two bias columns
     // one entry alone must fit: ld*4 + d*16 + 8 <= budget
@@ -365,7 +367,7 @@ void build_tile_host(const rs_svd_plan* pl, int32_t nw, int64_t target, int32_t 
     if (rec_cap < 64) throw std::invalid_argument("n_factors too large for the tile schedule's LDS");
     struct Ent { int32_t u; int64_t b, e; float frac; };
     std::vector<Ent> ents;
-    for (int32_t u = 0; u < pl->n_users; ++u) {
+    for (int32_t u = u_begin; u < u_end; ++u) {
         const int64_t d = rp[u + 1] - rp[u];
         if (d == 0) continue;
         const int64_t cap = std::min<int64_t>(rec_cap, std::max<int64_t>(target, 1));
@@ -618,11 +620,53 @@ int32_t auto_run_cap(const rs_svd_plan* pl, int32_t grid, int32_t waves) {
 
 // Ratings per tile: nnz / workgroups, but at least the heaviest user's ratings (cutting users into
 // pieces costs accuracy -- their rows are averaged after the epoch -- so small sets get fewer tiles).
-int64_t tile_target_of(const rs_svd_plan* pl, int32_t grid) {
+int64_t tile_target_of(const rs_svd_plan* pl, int32_t grid, int32_t u_begin, int32_t u_end) {
     if (pl->tile_target > 0) return pl->tile_target;
     int64_t dmax = 0;
-    for (int32_t u = 0; u < pl->n_users; ++u) dmax = std::max(dmax, pl->h_rowptr[u + 1] - pl->h_rowptr[u]);
-    return std::max<int64_t>({64, dmax, (pl->nnz + grid - 1) / std::max(1, grid)});
+    for (int32_t u = u_begin; u < u_end; ++u) dmax = std::max(dmax, pl->h_rowptr[u + 1] - pl->h_rowptr[u]);
+    const int64_t n = pl->h_rowptr[u_end] - pl->h_rowptr[u_begin];
+    return std::max<int64_t>({64, dmax, (n + grid - 1) / std::max(1, grid)});
+}
+
+// User blocks: tile_ublocks consecutive user ranges of near-equal ratings, tiled one after the other
+// (block b's tiles are [block_tile[b], block_tile[b+1])).  One block: the plain tile schedule.
+void build_tile_blocks(const rs_svd_plan* pl, int32_t grid0, bool want_pos, TileHost& th,
+                       std::vector<int32_t>& block_tile, std::vector<int32_t>& block_user) {
+    const int32_t nb = std::max(1, std::min(pl->tile_ublocks, std::max(1, pl->n_users)));
+    const std::vector<int64_t>& rp = pl->h_rowptr;
+    block_user.assign(1, 0);
+    for (int32_t b = 1; b < nb; ++b) {  // first user whose ratings start at or past b/nb of nnz
+        const int64_t want = pl->nnz * b / nb;
+        const int32_t u = static_cast<int32_t>(std::lower_bound(rp.begin(), rp.begin() + pl->n_users + 1, want) - rp.begin());
+        block_user.push_back(std::max(block_user.back(), std::min(u, pl->n_users)));
+    }
+    block_user.push_back(pl->n_users);
+    const int32_t cap = pl->tile_run_cap > 0 ? pl->tile_run_cap : auto_run_cap(pl, grid0, pl->tile_waves);
+    block_tile.assign(1, 0);
+    for (int32_t b = 0; b < nb; ++b) {
+        const int32_t u0 = block_user[b], u1 = block_user[b + 1];
+        TileHost part;
+        build_tile_host(pl, u0, u1, pl->tile_waves, tile_target_of(pl, grid0, u0, u1), cap, want_pos, part);
+        if (b == 0) {
+            th = std::move(part);
+        } else {
+            const int32_t e0 = static_cast<int32_t>(th.users.size());
+            const int64_t r0 = static_cast<int64_t>(th.runs.size()), c0 = static_cast<int64_t>(th.recs.size());
+            if (r0 + static_cast<int64_t>(part.runs.size()) >= (int64_t{1} << 31) ||
+                c0 + static_cast<int64_t>(part.recs.size()) >= (int64_t{1} << 31))
+                throw std::invalid_argument("tile schedule: more than 2^31 runs or ratings");
+            for (int4 t : part.tiles)
+                th.tiles.push_back(make_int4(t.x + e0, t.y, t.z + static_cast<int32_t>(r0), t.w + static_cast<int32_t>(c0)));
+            th.users.insert(th.users.end(), part.users.begin(), part.users.end());
+            th.streams.insert(th.streams.end(), part.streams.begin(), part.streams.end());
+            th.runs.insert(th.runs.end(), part.runs.begin(), part.runs.end());
+            th.recs.insert(th.recs.end(), part.recs.begin(), part.recs.end());
+            th.pos.insert(th.pos.end(), part.pos.begin(), part.pos.end());
+            th.split.insert(th.split.end(), part.split.begin(), part.split.end());
+            th.lds = std::max(th.lds, part.lds);
+        }
+        block_tile.push_back(static_cast<int32_t>(th.tiles.size()));
+    }
 }
 
 }  // namespace
@@ -634,8 +678,7 @@ void tile_build(rs_svd_plan* pl) {
     const int32_t cus = device_cus(pl->ctx);
     const int32_t grid0 = pl->tile_wg > 0 ? pl->tile_wg : cus;
     TileHost th;
-    const int32_t cap = pl->tile_run_cap > 0 ? pl->tile_run_cap : auto_run_cap(pl, grid0, pl->tile_waves);
-    build_tile_host(pl, pl->tile_waves, tile_target_of(pl, grid0), cap, false, th);
+    build_tile_blocks(pl, grid0, false, th, pl->t_block_tile, pl->t_block_user);
     plan_sync_last(pl);
     pl->n_tiles = static_cast<int32_t>(th.tiles.size());
     pl->tile_grid = std::max(1, std::min(grid0, pl->n_tiles));
@@ -667,8 +710,8 @@ void tile_order(rs_svd_plan* pl, int64_t* pos, int64_t* work_off, int32_t* n_wor
     const int32_t cus = device_cus(pl->ctx);
     const int32_t grid0 = pl->tile_wg > 0 ? pl->tile_wg : cus;
     TileHost th;
-    const int32_t cap = pl->tile_run_cap > 0 ? pl->tile_run_cap : auto_run_cap(pl, grid0, pl->tile_waves);
-    build_tile_host(pl, pl->tile_waves, tile_target_of(pl, grid0), cap, true, th);
+    std::vector<int32_t> bt, bu;
+    build_tile_blocks(pl, grid0, true, th, bt, bu);
     const size_t nw = th.tiles.size() * pl->tile_waves;
     if (n_works) *n_works = static_cast<int32_t>(nw);
     if (pos) std::copy(th.pos.begin(), th.pos.end(), pos);
@@ -683,8 +726,12 @@ void tile_order(rs_svd_plan* pl, int64_t* pos, int64_t* work_off, int32_t* n_wor
     }
 }
 
+struct TileRange {  // tiles [t0, t1) into dP rows of stride ldd (delta mode), grid workgroups
+    int32_t t0, t1, ldd, grid;
+};
+
 template <int E, int NW, int RQ, int DIAG = 0>
-static void tile_launch_t(rs_svd_plan* pl, float lr, float reg, hipStream_t s, float* dP) {
+static void tile_launch_t(rs_svd_plan* pl, float lr, float reg, hipStream_t s, float* dP, const TileRange& tr) {
     auto kern = svd_epoch_tile_kernel<E, NW, RQ, DIAG>;
     static bool attr = false;  // per instantiation
     if (!attr) {
@@ -693,89 +740,111 @@ static void tile_launch_t(rs_svd_plan* pl, float lr, float reg, hipStream_t s, f
         attr = true;
     }
     const int32_t q_bytes = static_cast<int32_t>(pl->Q.n * sizeof(float));
-    hipLaunchKernelGGL(kern, dim3(pl->tile_grid), dim3(NW * 64), pl->tile_lds, s, pl->t_tiles.p, pl->n_tiles,
-                       pl->t_users.p, pl->t_streams.p, pl->t_runs.p, pl->t_recs.p, pl->P.p,
-                       reinterpret_cast<int32_t*>(pl->Q.p), q_bytes, pl->gb.p, pl->partial.p, lr, reg, dP,
-                       dP ? pl->uw.p : nullptr, pl->dPs.p, pl->k, pl->ld, pl->trace.p);
+    hipLaunchKernelGGL(kern, dim3(tr.grid), dim3(NW * 64), pl->tile_lds, s, pl->t_tiles.p + tr.t0, tr.t1 - tr.t0,
+                       pl->t_users.p, pl->t_streams.p + static_cast<int64_t>(tr.t0) * (NW + 1), pl->t_runs.p,
+                       pl->t_recs.p, pl->P.p, reinterpret_cast<int32_t*>(pl->Q.p), q_bytes, pl->gb.p, pl->partial.p,
+                       lr, reg, dP, dP ? pl->uw.p : nullptr, pl->dPs.p, pl->k, pl->ld, tr.ldd, pl->trace.p);
 }
 
 // q_i rows in flight per wave (runs ahead): the ring's loads and the runs' atomics share the wave's
 // in-order vmcnt, so a slot's load also waits for every atomic issued before it; the deeper the ring,
 // the longer an atomic has to complete before a load behind it is needed
 template <int E, int NW>
-static void tile_launch_r(rs_svd_plan* pl, float lr, float reg, hipStream_t s, float* dP) {
+static void tile_launch_r(rs_svd_plan* pl, float lr, float reg, hipStream_t s, float* dP, const TileRange& tr) {
     constexpr int kMax = 60 / (2 * E);  // 15 at E = 2 (k <= 127), 6 at E = 5 (k <= 319), 3 at E = 8
     const int want = pl->tile_ring > 0 ? pl->tile_ring : 2;
     if constexpr (E == 2 && NW == 16) {  // diagnostics (RSGPU_TILE_DIAG, experiments only): bits drop
         static const int diag = std::getenv("RSGPU_TILE_DIAG") ? std::atoi(std::getenv("RSGPU_TILE_DIAG")) : 0;
         switch (diag) {  // 1 q atomics, 2 q loads, 4 p LDS atomics, 8 p LDS reads
-            case 1: return tile_launch_t<E, NW, 4, 1>(pl, lr, reg, s, dP);
-            case 2: return tile_launch_t<E, NW, 4, 2>(pl, lr, reg, s, dP);
-            case 3: return tile_launch_t<E, NW, 4, 3>(pl, lr, reg, s, dP);
-            case 4: return tile_launch_t<E, NW, 4, 4>(pl, lr, reg, s, dP);
-            case 12: return tile_launch_t<E, NW, 4, 12>(pl, lr, reg, s, dP);
-            case 15: return tile_launch_t<E, NW, 4, 15>(pl, lr, reg, s, dP);
+            case 1: return tile_launch_t<E, NW, 4, 1>(pl, lr, reg, s, dP, tr);
+            case 2: return tile_launch_t<E, NW, 4, 2>(pl, lr, reg, s, dP, tr);
+            case 3: return tile_launch_t<E, NW, 4, 3>(pl, lr, reg, s, dP, tr);
+            case 4: return tile_launch_t<E, NW, 4, 4>(pl, lr, reg, s, dP, tr);
+            case 12: return tile_launch_t<E, NW, 4, 12>(pl, lr, reg, s, dP, tr);
+            case 15: return tile_launch_t<E, NW, 4, 15>(pl, lr, reg, s, dP, tr);
             case 16:
                 if (pl->trace.n < static_cast<size_t>(pl->tile_grid) * NW * 4) {
                     pl->trace.alloc(static_cast<size_t>(pl->tile_grid) * NW * 4);
                     RS_HIP(hipMemsetAsync(pl->trace.p, 0, pl->trace.n * 8, s));
                 }
-                return tile_launch_t<E, NW, 4, 16>(pl, lr, reg, s, dP);
+                return tile_launch_t<E, NW, 4, 16>(pl, lr, reg, s, dP, tr);
             default: break;
         }
     }
     if constexpr (kMax >= 12) {
-        if (want >= 12) return tile_launch_t<E, NW, 12>(pl, lr, reg, s, dP);
+        if (want >= 12) return tile_launch_t<E, NW, 12>(pl, lr, reg, s, dP, tr);
     }
     if constexpr (kMax >= 8) {
-        if (want >= 8) return tile_launch_t<E, NW, 8>(pl, lr, reg, s, dP);
+        if (want >= 8) return tile_launch_t<E, NW, 8>(pl, lr, reg, s, dP, tr);
     }
     if constexpr (kMax >= 6) {
-        if (want >= 6) return tile_launch_t<E, NW, 6>(pl, lr, reg, s, dP);
+        if (want >= 6) return tile_launch_t<E, NW, 6>(pl, lr, reg, s, dP, tr);
     }
-    if (want <= 2) return tile_launch_t<E, NW, 2>(pl, lr, reg, s, dP);
-    if (want == 3) return tile_launch_t<E, NW, 3>(pl, lr, reg, s, dP);
+    if (want <= 2) return tile_launch_t<E, NW, 2>(pl, lr, reg, s, dP, tr);
+    if (want == 3) return tile_launch_t<E, NW, 3>(pl, lr, reg, s, dP, tr);
     if constexpr (kMax >= 4) {
-        return tile_launch_t<E, NW, 4>(pl, lr, reg, s, dP);
+        return tile_launch_t<E, NW, 4>(pl, lr, reg, s, dP, tr);
     } else {
-        return tile_launch_t<E, NW, kMax>(pl, lr, reg, s, dP);
+        return tile_launch_t<E, NW, kMax>(pl, lr, reg, s, dP, tr);
     }
 }
 
 template <int E>
-static void tile_launch_w(rs_svd_plan* pl, float lr, float reg, hipStream_t s, float* dP) {
+static void tile_launch_w(rs_svd_plan* pl, float lr, float reg, hipStream_t s, float* dP, const TileRange& tr) {
     switch (pl->tile_waves) {
-        case 1: tile_launch_r<E, 1>(pl, lr, reg, s, dP); break;
-        case 2: tile_launch_r<E, 2>(pl, lr, reg, s, dP); break;
-        case 4: tile_launch_r<E, 4>(pl, lr, reg, s, dP); break;
-        case 8: tile_launch_r<E, 8>(pl, lr, reg, s, dP); break;
-        default: tile_launch_r<E, 16>(pl, lr, reg, s, dP); break;
+        case 1: tile_launch_r<E, 1>(pl, lr, reg, s, dP, tr); break;
+        case 2: tile_launch_r<E, 2>(pl, lr, reg, s, dP, tr); break;
+        case 4: tile_launch_r<E, 4>(pl, lr, reg, s, dP, tr); break;
+        case 8: tile_launch_r<E, 8>(pl, lr, reg, s, dP, tr); break;
+        default: tile_launch_r<E, 16>(pl, lr, reg, s, dP, tr); break;
+    }
+}
+
+static void tile_dispatch(rs_svd_plan* pl, float lr, float reg, hipStream_t s, float* dP, const TileRange& tr) {
+    switch ((pl->k + 2 + 63) / 64) {  // registers per row: k factors + the two bias columns
+        case 1: tile_launch_w<1>(pl, lr, reg, s, dP, tr); break;
+        case 2: tile_launch_w<2>(pl, lr, reg, s, dP, tr); break;
+        case 3: tile_launch_w<3>(pl, lr, reg, s, dP, tr); break;
+        case 4: tile_launch_w<4>(pl, lr, reg, s, dP, tr); break;
+        case 5: tile_launch_w<5>(pl, lr, reg, s, dP, tr); break;
+        case 6: tile_launch_w<6>(pl, lr, reg, s, dP, tr); break;
+        case 7: tile_launch_w<7>(pl, lr, reg, s, dP, tr); break;
+        default: tile_launch_w<8>(pl, lr, reg, s, dP, tr); break;
+    }
+    RS_HIP(hipGetLastError());
+}
+
+static void tile_partials_fit(rs_svd_plan* pl, hipStream_t s) {
+    if (pl->partial.n < static_cast<size_t>(tile_partials(pl))) {  // another schedule resized it
+        plan_sync_last(pl);
+        RS_HIP(hipStreamSynchronize(s));
+        pl->partial.alloc(static_cast<size_t>(tile_partials(pl)));
     }
 }
 
 void tile_launch(rs_svd_plan* pl, float lr, float reg, hipStream_t s, float* dP) {
     if (!pl->tiles_built) tile_build(pl);
     pl->n_blocks = tile_partials(pl);
-    if (pl->partial.n < static_cast<size_t>(pl->n_blocks)) {  // another schedule resized it
-        plan_sync_last(pl);
-        RS_HIP(hipStreamSynchronize(s));
-        pl->partial.alloc(static_cast<size_t>(pl->n_blocks));
-    }
+    tile_partials_fit(pl, s);
     if (pl->n_tiles == 0) {  // no ratings: the fold still reads its partials
         RS_HIP(hipMemsetAsync(pl->partial.p, 0, pl->partial.n * sizeof(double), s));
         return;
     }
-    switch ((pl->k + 2 + 63) / 64) {  // registers per row: k factors + the two bias columns
-        case 1: tile_launch_w<1>(pl, lr, reg, s, dP); break;
-        case 2: tile_launch_w<2>(pl, lr, reg, s, dP); break;
-        case 3: tile_launch_w<3>(pl, lr, reg, s, dP); break;
-        case 4: tile_launch_w<4>(pl, lr, reg, s, dP); break;
-        case 5: tile_launch_w<5>(pl, lr, reg, s, dP); break;
-        case 6: tile_launch_w<6>(pl, lr, reg, s, dP); break;
-        case 7: tile_launch_w<7>(pl, lr, reg, s, dP); break;
-        default: tile_launch_w<8>(pl, lr, reg, s, dP); break;
+    tile_dispatch(pl, lr, reg, s, dP, TileRange{0, pl->n_tiles, pl->ld, pl->tile_grid});
+}
+
+int32_t tile_launch_range(rs_svd_plan* pl, float lr, float reg, hipStream_t s, float* dP, int32_t ldd,
+                          int32_t t0, int32_t t1) {
+    if (!pl->tiles_built) tile_build(pl);
+    tile_partials_fit(pl, s);
+    const int32_t grid = std::max(1, std::min(pl->tile_grid, t1 - t0));
+    const int32_t parts = grid * pl->tile_waves;
+    if (t1 <= t0) {
+        RS_HIP(hipMemsetAsync(pl->partial.p, 0, static_cast<size_t>(parts) * sizeof(double), s));
+        return parts;
     }
-    RS_HIP(hipGetLastError());
+    tile_dispatch(pl, lr, reg, s, dP, TileRange{t0, t1, ldd, grid});
+    return parts;
 }
 
 }  // namespace rs

@@ -40,7 +40,11 @@ HEADER_SYMBOLS = (
     "rs_svd_plan_set_item_weights", "rs_svd_plan_epoch_qdelta", "rs_svd_plan_apply_qdelta",
     "rs_svd_plan_set_hot_replicas", "rs_svd_plan_set_fixed_q", "rs_svd_plan_set_tiles",
     "rs_svd_plan_tile_order", "rs_svd_plan_tile_clocks",
+    "rs_comm_unique_id", "rs_svd_plan_join", "rs_svd_plan_epochs_sharded", "rs_svd_plan_leave",
+    "rs_svd_plan_set_user_blocks", "rs_svd_group_create", "rs_svd_group_epochs", "rs_svd_group_destroy",
+    "rs_item_shards", "rs_svd_fit_multi",
 )
+COMM_ID_BYTES = 128
 
 
 class RsError(RuntimeError):
@@ -142,6 +146,17 @@ def lib():
             "rs_synth_csr": (C.c_int, [_vp, C.POINTER(_i64), C.POINTER(_vp), C.POINTER(_vp),
                                        C.POINTER(_vp)]),
             "rs_synth_destroy": (None, [_vp]),
+            "rs_comm_unique_id": (C.c_int, [_vp]),
+            "rs_svd_plan_join": (C.c_int, [_vp, _vp, _i32, _i32, _i32]),
+            "rs_svd_plan_epochs_sharded": (C.c_int, [_vp, _i32, _flt, _flt, _vp]),
+            "rs_svd_plan_leave": (C.c_int, [_vp]),
+            "rs_svd_plan_set_user_blocks": (C.c_int, [_vp, _i32]),
+            "rs_svd_group_create": (C.c_int, [_vp, _i32, _i32, C.POINTER(_vp)]),
+            "rs_svd_group_epochs": (C.c_int, [_vp, _i32, _flt, _flt]),
+            "rs_svd_group_destroy": (None, [_vp]),
+            "rs_item_shards": (C.c_int, [_i64, _vp, _i32, _i32, _vp]),
+            "rs_svd_fit_multi": (C.c_int, [_vp, _i32, C.POINTER(_Ratings), C.POINTER(_SgdParams), _i32,
+                                           _vp, _vp, _vp, _vp, _vp]),
         }
         for name, (res, args) in sig.items():
             f = getattr(L, name)
@@ -424,6 +439,23 @@ class SvdPlan:
     def set_mode(self, write_back=WB_TILE, ring_depth=16):
         self.ctx.check(lib().rs_svd_plan_set_mode(self.h, write_back, ring_depth))
 
+    def set_user_blocks(self, n_blocks):
+        """Tile schedule in n_blocks consecutive user blocks (rs_svd_plan_set_user_blocks)."""
+        self.ctx.check(lib().rs_svd_plan_set_user_blocks(self.h, n_blocks))
+
+    def join(self, comm_id: bytes, rank: int, n_ranks: int, n_blocks: int = 0):
+        """Item-sharded multi-GPU (rs_svd_plan_join; collective over the ranks): comm_id from
+        comm_unique_id() on rank 0, sent to every rank."""
+        assert len(comm_id) == COMM_ID_BYTES
+        buf = C.create_string_buffer(bytes(comm_id), COMM_ID_BYTES)
+        self.ctx.check(lib().rs_svd_plan_join(self.h, buf, rank, n_ranks, n_blocks))
+
+    def epochs_sharded(self, n, lr=0.005, reg=0.02, stream=None):
+        self.ctx.check(lib().rs_svd_plan_epochs_sharded(self.h, n, lr, reg, stream))
+
+    def leave(self):
+        self.ctx.check(lib().rs_svd_plan_leave(self.h))
+
     def set_tiles(self, workgroups=0, waves=16, target=0, run_cap=0, ring=0):
         """WB_TILE schedule parameters (rs_svd_plan_set_tiles); rebuilds the tiles."""
         self.ctx.check(lib().rs_svd_plan_set_tiles(self.h, workgroups, waves, target, run_cap, ring))
@@ -552,6 +584,63 @@ class SvdPlan:
             self.close()
         except Exception:
             pass
+
+
+def comm_unique_id() -> bytes:
+    """RS_COMM_ID_BYTES bytes naming a new RCCL communicator (rank 0 sends them to every rank)."""
+    buf = C.create_string_buffer(COMM_ID_BYTES)
+    _check(lib().rs_comm_unique_id(buf))
+    return buf.raw
+
+
+def item_shards(items, n_items, n_shards):
+    """Item ranges of near-equal ratings (rs_item_shards): bounds, n_shards + 1 entries."""
+    items = np.ascontiguousarray(items, np.int32)
+    b = np.empty(n_shards + 1, np.int32)
+    _check(lib().rs_item_shards(len(items), _ptr(items), n_items, n_shards, _ptr(b)))
+    return b
+
+
+class SvdGroup:
+    """Several shard plans driven by one process (rs_svd_group_*): RCCL when each plan has its own
+    device, else the in-process exchange."""
+
+    def __init__(self, plans, n_blocks=0):
+        self.plans = list(plans)
+        arr = (C.c_void_p * len(self.plans))(*[p.h for p in self.plans])
+        h = C.c_void_p()
+        _check(lib().rs_svd_group_create(arr, len(self.plans), n_blocks, C.byref(h)))
+        self.h = h
+
+    def epochs(self, n, lr=0.005, reg=0.02):
+        _check(lib().rs_svd_group_epochs(self.h, n, lr, reg))
+
+    def close(self):
+        if self.h is not None:
+            lib().rs_svd_group_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+def svd_fit_multi(devices, r: "Ratings", P, Q, bu=None, bi=None, gb=0.0, n_epochs=20, lr=0.005,
+                  reg=0.02, n_blocks=0):
+    """rs_svd_fit_multi: core/svd.go:63-132 over item shards on `devices` (one host thread each)."""
+    P = np.array(P, dtype=np.float64, order="C")
+    Q = np.array(Q, dtype=np.float64, order="C")
+    bu = np.zeros(r.n_users) if bu is None else np.array(bu, dtype=np.float64)
+    bi = np.zeros(r.n_items) if bi is None else np.array(bi, dtype=np.float64)
+    g = np.array([gb], dtype=np.float64)
+    dev = np.ascontiguousarray(devices, np.int32)
+    prm = _SgdParams(P.shape[1], n_epochs, lr, reg, SGD_FAST, WB_TILE)
+    rc = r.c()
+    _check(lib().rs_svd_fit_multi(_ptr(dev), len(dev), C.byref(rc), C.byref(prm), n_blocks, _ptr(P), _ptr(Q),
+                                  _ptr(bu), _ptr(bi), _ptr(g)))
+    return P, Q, bu, bi, float(g[0])
 
 
 def svd_predict(users, items, P, Q, bu, bi, gb):

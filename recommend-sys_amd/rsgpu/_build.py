@@ -89,7 +89,8 @@ def build(verbose: bool = False, jobs: int = 8) -> str:
                 print(f"compiled {len(todo)} sources")
     newest = max(os.path.getmtime(o) for o in objs)
     if todo or not os.path.exists(LIB) or os.path.getmtime(LIB) < newest:
-        cmd = [HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", LIB] + objs
+        cmd = [HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", LIB] + objs + [
+            "-L/opt/rocm/lib", "-lrccl", "-Wl,-rpath,/opt/rocm/lib"]
         r = subprocess.run(cmd, capture_output=True, text=True)
         if r.returncode != 0:
             raise RuntimeError(f"link failed:\n{r.stderr}")

@@ -294,3 +294,18 @@ def test_two_rank_gloo_knn_sims_shared_file(tmp_path):
         assert np.array_equal(np.isnan(full), np.isnan(got))
         m = ~np.isnan(full)
         assert np.array_equal(full[m], got[m])
+
+
+def test_rs_item_shards_balanced_ranges():
+    """rs_item_shards (host, no GPU): contiguous item ranges covering every item, split points at the
+    first item whose cumulative count reaches r/n of the ratings."""
+    import rsgpu
+    rng = np.random.default_rng(4)
+    ni = 500
+    items = rng.zipf(1.3, 40000) % ni
+    for n in (1, 2, 3, 8):
+        b = rsgpu.item_shards(items, ni, n)
+        assert b[0] == 0 and b[-1] == ni and np.all(np.diff(b) >= 0)
+        cum = np.concatenate([[0], np.cumsum(np.bincount(items, minlength=ni))])
+        for r in range(1, n):
+            assert b[r] == np.searchsorted(cum, len(items) * r // n, side="left")

@@ -1,0 +1,137 @@
+"""GPU tests of the item-sharded multi-GPU path behind the C-ABI (csrc/multi.hip; north_star's item
+sharding with an all-reduce of user-factor deltas once per epoch, core/svd.go:92-130 per shard).
+
+The one-GPU box runs N shards of one device through the in-process exchange (rs_svd_group with plans
+sharing a device) and the RCCL code with a single rank (rs_svd_group of one device, rs_svd_plan_join
+with n_ranks = 1): the block pipeline, the user weights, the GlobalBias fold and the apply are the
+same code as with 8 GPUs; only the RCCL ring itself is unexercised ("unmeasured on hardware").
+
+Checker: the delta protocol run by hand on plans of the same schedule (one workgroup of one wave:
+deterministic) -- rs_svd_plan_epoch_delta per shard, the shard deltas summed in shard order, and
+rs_svd_plan_apply_delta on every shard -- which test_tile_gpu.py::test_delta_mode_equals_direct pins
+to the plain epoch, itself pinned to the oracle (or_svd_fit_works).
+"""
+import numpy as np
+import pytest
+
+import oracle as O
+import rsgpu
+from helpers import folds, rmse
+
+pytestmark = pytest.mark.gpu
+TOL = 1e-5
+
+
+def _maxdiff(a, b):
+    return max(float(np.max(np.abs(np.asarray(x) - np.asarray(y)))) for x, y in zip(a, b))
+
+
+def _shards(u, i, r, nu, ni, n):
+    b = rsgpu.item_shards(i, ni, n)
+    out = []
+    for s in range(n):
+        m = (i >= b[s]) & (i < b[s + 1])
+        out.append((u[m], i[m] - b[s], r[m], nu, int(b[s + 1] - b[s]), int(b[s])))
+    return out
+
+
+def _plans(ctx, shards, k, P0, Q0, blocks, waves=1, wg=1):
+    plans = []
+    for su, si, sr, nu, ni_s, lo in shards:
+        pl = ctx.svd_plan(rsgpu.Ratings(su, si, sr, nu, ni_s), k)
+        pl.set_tiles(workgroups=wg, waves=waves)
+        pl.set_user_blocks(blocks)
+        pl.upload(P0, Q0[lo:lo + ni_s], np.zeros(nu), np.zeros(ni_s), 3.5)
+        plans.append(pl)
+    return plans
+
+
+def _manual(plans, shards, nu, epochs):
+    """The delta protocol by hand (torch buffers, sum in shard order)."""
+    import torch
+    tot = np.zeros(nu)
+    for su, *_ in shards:
+        tot += np.bincount(su, minlength=nu)
+    total = sum(len(sr) for _, _, sr, *_ in shards)
+    for pl, (su, *_) in zip(plans, shards):
+        c = np.bincount(su, minlength=nu)
+        pl.set_user_weights(np.divide(c, tot, out=np.zeros(nu), where=tot > 0).astype(np.float32))
+    ld = plans[0].ld
+    dPs = [torch.zeros((nu, ld), dtype=torch.float32, device="cuda") for _ in plans]
+    gs = [torch.zeros(1, dtype=torch.float64, device="cuda") for _ in plans]
+    for _ in range(epochs):
+        for pl, dP, g in zip(plans, dPs, gs):
+            pl.epoch_delta_t(dP, g, 0.005, 0.02)
+        torch.cuda.synchronize()
+        sdP, sg = dPs[0].clone(), gs[0].clone()
+        for dP, g in zip(dPs[1:], gs[1:]):
+            sdP += dP
+            sg += g
+        for pl in plans:
+            pl.apply_delta_t(sdP, sg, 1.0 / total)
+        torch.cuda.synchronize()
+
+
+@pytest.mark.parametrize("n_shards,blocks", [(2, 1), (2, 3), (3, 4)])
+def test_group_on_one_device_equals_manual_protocol(ctx, ml100k, n_shards, blocks):
+    f = folds(*ml100k)[2]
+    u, i, r, nu, ni = f.iu, f.ii, f.r, f.nu, f.ni
+    k = 24
+    rng = np.random.default_rng(n_shards + blocks)
+    P0, Q0 = rng.normal(0, 0.1, (nu, k)), rng.normal(0, 0.1, (ni, k))
+    sh = _shards(u, i, r, nu, ni, n_shards)
+    ref = _plans(ctx, sh, k, P0, Q0, blocks)
+    _manual(ref, sh, nu, epochs=2)
+    got = _plans(ctx, sh, k, P0, Q0, blocks)
+    g = rsgpu.SvdGroup(got, n_blocks=blocks)
+    g.epochs(2)
+    g.close()
+    a = [pl.download() for pl in ref]
+    b = [pl.download() for pl in got]
+    for pl in ref + got:
+        pl.close()
+    for x, y in zip(a, b):
+        assert _maxdiff(x[:4], y[:4]) <= TOL and abs(x[4] - y[4]) <= 1e-9
+    for y in b[1:]:  # the replicated state is bitwise identical across shards
+        assert np.array_equal(b[0][0], y[0]) and np.array_equal(b[0][2], y[2]) and b[0][4] == y[4]
+
+
+@pytest.mark.parametrize("api", ["group", "join"])
+def test_rccl_single_rank_equals_manual_protocol(ctx, ml100k, api):
+    """The RCCL exchange (communicator, block all-reduces on the comm stream, events) with one rank."""
+    f = folds(*ml100k)[3]
+    u, i, r, nu, ni = f.iu, f.ii, f.r, f.nu, f.ni
+    k = 40
+    rng = np.random.default_rng(11)
+    P0, Q0 = rng.normal(0, 0.1, (nu, k)), rng.normal(0, 0.1, (ni, k))
+    sh = _shards(u, i, r, nu, ni, 1)
+    ref = _plans(ctx, sh, k, P0, Q0, 3)
+    _manual(ref, sh, nu, epochs=3)
+    got = _plans(ctx, sh, k, P0, Q0, 3)
+    if api == "group":
+        g = rsgpu.SvdGroup(got, n_blocks=3)
+        g.epochs(3)
+        g.close()
+    else:
+        got[0].join(rsgpu.comm_unique_id(), 0, 1, 3)
+        got[0].epochs_sharded(3)
+        got[0].leave()
+    a, b = ref[0].download(), got[0].download()
+    for pl in ref + got:
+        pl.close()
+    assert _maxdiff(a[:4], b[:4]) <= TOL and abs(a[4] - b[4]) <= 1e-9
+
+
+def test_fit_multi_rmse_parity_ml100k(ctx, ml100k):
+    """rs_svd_fit_multi with two item shards on device 0 (default tile schedule, 16 waves): P2 --
+    5-fold ML-100K held-out RMSE within 0.003 of the reference visit order (core/base_test.go:34-36)."""
+    k = 100
+    ref_r, gpu_r = [], []
+    for f in folds(*ml100k):
+        rng = np.random.default_rng(7)
+        P0, Q0 = rng.normal(0, 0.1, (f.nu, k)), rng.normal(0, 0.1, (f.ni, k))
+        ref_r.append(rmse(O.svd_predict(f.tu, f.ti, *O.svd_fit(f.iu, f.ii, f.r, P0, Q0)), f.te_r))
+        got = rsgpu.svd_fit_multi([0, 0], rsgpu.Ratings(f.iu, f.ii, f.r, f.nu, f.ni), P0, Q0, n_blocks=2)
+        assert all(np.all(np.isfinite(x)) for x in got[:4])
+        gpu_r.append(rmse(O.svd_predict(f.tu, f.ti, *got), f.te_r))
+    assert abs(np.mean(gpu_r) - np.mean(ref_r)) <= 0.003, (np.mean(gpu_r), np.mean(ref_r))
