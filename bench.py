@@ -3,9 +3,18 @@
 
 One step = one fast-mode SGD epoch (core/svd.go:92-130) over all 1,000,209 ratings, inputs resident
 in HBM (user-CSR + factors uploaded before the timed region).  N>1 GPUs: one process per GPU
-(torch.distributed, backend nccl = RCCL over xGMI); each rank owns its own item-range shard of
-ML-1M size (weak scaling, users replicated) and the user-factor / user-bias / global-bias deltas are
-all-reduced once per epoch (north_star item sharding).
+(torch.distributed for the launch, barriers and the max-over-ranks clock); each rank owns its own
+item-range shard of ML-1M size (weak scaling, the 6040 users replicated) and the library's own RCCL
+communicator (rs_svd_plan_join) all-reduces the user-factor / user-bias / global-bias deltas once
+per epoch, pipelined per user block (north_star item sharding, csrc/multi.hip).
+
+Extra fields of the same line:
+  strong_scaling  BASELINE configs[4]'s shape at 1/8 scale (1.25M users x 125k items x ~125M ratings,
+                  k = 256: the same ratings-per-user and so the same exchange-to-compute ratio as the
+                  10M x 1M x 1e9 set) split over the N ranks by item range -- the north_star scaling
+                  question; the driver's N = 1, 2, 4, 8 lines give its curve.
+  ordered         N = 1: throughput of the ORDERED mode (the reference visit order, the mode that
+                  meets north_star's 1e-5 factor contract) on the same ML-1M-shaped set.
 
 Prints ONE JSON line on rank 0 (contract in the task statement).
 """
@@ -52,6 +61,72 @@ def cpu_baseline(u, i, r, n_users, n_items, budget_s=10.0):
                       f"of core/svd.go:92-130 (oracle/), single thread, {t_total:.1f} s"}
 
 
+def strong_scaling(ctx, rank, world, dist, dev, stream, epochs=3, warmup=1):
+    """configs[4] shape at 1/8 scale, items split over the ranks (rs_svd_plan_join when world > 1)."""
+    import torch
+    import rsgpu
+    n_users, n_items, k = 1_250_000, 125_000, 256
+    lo, hi = n_items * rank // world, n_items * (rank + 1) // world
+    t0 = time.perf_counter()
+    s = rsgpu.Synth(n_users, n_items, mean_deg=100.0, seed=20250827, item_lo=lo, item_hi=hi, n_threads=16)
+    plan = ctx.svd_plan_csr(n_users, hi - lo, s.rowptr, s.cols - lo, s.vals, k)
+    nnz, vsum = s.nnz, float(np.sum(s.vals, dtype=np.float64))
+    s.close()
+    plan.init_normal(0.0, 0.1, seed=3)  # P rows keyed by row id: identical on every rank
+    tot = torch.tensor([float(nnz), vsum], dtype=torch.float64, device=f"cuda:{dev}")
+    if dist:
+        dist.all_reduce(tot)
+        uid = [rsgpu.comm_unique_id() if rank == 0 else None]
+        dist.broadcast_object_list(uid, src=0)
+        plan.upload(gb=float(tot[1] / tot[0]))  # the same GlobalBias on every rank
+        plan.join(uid[0], rank, world)
+        run = lambda n: plan.epochs_sharded(n, LR, REG, stream)
+    else:
+        plan.upload(gb=float(tot[1] / tot[0]))
+        run = lambda n: plan.epochs(n, LR, REG, stream)
+    setup_s = time.perf_counter() - t0
+    run(warmup)
+    torch.cuda.synchronize()
+    if dist:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    run(epochs)
+    torch.cuda.synchronize()
+    if dist:
+        dist.barrier()
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    if dist:
+        t = torch.tensor([dt], dtype=torch.float64, device=f"cuda:{dev}")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        dt = float(t.item())
+    P, Q, bu, bi, gb = plan.download()
+    finite = bool(np.isfinite(P).all() and np.isfinite(Q).all() and np.isfinite(gb))
+    plan.close()
+    total = int(tot[0].item())
+    return {"workload": "SVD nFactors=256, configs[4] shape at 1/8 scale: 1.25M users x 125k items, "
+                        f"{total} ratings (mean 100 per user, Zipf items), split by item range over "
+                        f"{world} GPU(s)", "scaling": "strong", "n_gpus": world, "epochs": epochs,
+            "value": total * epochs / dt, "unit": "updates/s", "ms_per_epoch": dt / epochs * 1e3,
+            "setup_s_rank0": setup_s, "finite": finite,
+            "exchange": "rs_svd_plan_join + rs_svd_plan_epochs_sharded (RCCL all-reduce of user deltas, "
+                        "pipelined per user block)" if world > 1 else "none (one GPU)"}
+
+
+def ordered_throughput(ctx, u, i, r, n_users, n_items):
+    """ORDERED mode (core/svd.go:93-129 in the reference's visit order), one epoch, kernel time."""
+    import rsgpu
+    rng = np.random.default_rng(1)
+    P0, Q0 = rng.normal(0, 0.1, (n_users, K)), rng.normal(0, 0.1, (n_items, K))
+    R = rsgpu.Ratings(u, i, r, n_users, n_items)
+    ctx.svd_fit(R, P0[:, :K], Q0, n_epochs=1, mode=rsgpu.SGD_ORDERED)
+    ms = ctx.last_kernel_ms()
+    return {"value": len(r) / (ms / 1e3), "unit": "updates/s", "epoch_ms_kernel": ms,
+            "note": "one 16-lane group walks the ratings in the reference order (factors within 1e-5 of "
+                    "the oracle); kernel-only time of one epoch"}
+
+
 def load_traffic():
     """HBM bytes per SGD launch measured by rocprofv3 --pmc (separate pass, committed summary)."""
     p = os.path.join(REPO, "profiles", "sgd_traffic.json")
@@ -70,6 +145,8 @@ def main():
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-budget", type=float, default=10.0)
+    ap.add_argument("--no-strong", action="store_true", help="skip the configs[4]-shape strong-scaling field")
+    ap.add_argument("--no-ordered", action="store_true", help="skip the ORDERED-mode field")
     args = ap.parse_args()
 
     import torch
@@ -99,11 +176,11 @@ def main():
     plan.upload(P0, Q0, np.zeros(n_users), np.zeros(n_items), float(np.mean(r)))
     stream = torch.cuda.current_stream(dev).cuda_stream
 
-    if world > 1:
-        import rsgpu.multi as multi
-        w, total = multi.user_weights(u, n_users, dist, device=f"cuda:{dev}")
-        step = multi.ItemShardedStep(plan, dist, w, total, device=f"cuda:{dev}", stream=stream)
-        run = lambda n: step.run(n, LR, REG)
+    if world > 1:  # the library's own RCCL communicator (csrc/multi.hip), id sent over torch.distributed
+        uid = [rsgpu.comm_unique_id() if rank == 0 else None]
+        dist.broadcast_object_list(uid, src=0)
+        plan.join(uid[0], rank, world)
+        run = lambda n: plan.epochs_sharded(n, LR, REG, stream)
     else:
         run = lambda n: plan.epochs(n, LR, REG, stream)
 
@@ -125,17 +202,17 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         dt = float(t.item())
 
-    # kernel-only timing of the SGD kernel (HIP events on the launch stream), separate pass
+    P, Q, bu, bi, gb = plan.download()
+    finite = bool(np.isfinite(P).all() and np.isfinite(Q).all() and np.isfinite(gb))
+    # kernel-only timing of the SGD kernel (HIP events on the launch stream), separate pass: plain
+    # single-GPU epochs of this rank's shard (the dominant kernel; no exchange)
     plan.set_timing(True)
-    if world > 1:
-        step.run(5, LR, REG)
-    else:
-        plan.epochs(5, LR, REG, stream)
+    plan.epochs(5, LR, REG, stream)
     kms, nl = plan.last_kernel_ms()
     plan.set_timing(False)
     avg_kernel_s = kms / 1e3 / nl
-    P, Q, bu, bi, gb = plan.download()
-    finite = bool(np.isfinite(P).all() and np.isfinite(Q).all() and np.isfinite(gb))
+    plan.close()
+    strong = None if args.no_strong else strong_scaling(ctx, rank, world, dist, dev, stream)
 
     if rank == 0:
         total_updates = nnz * world * args.steps
@@ -157,12 +234,14 @@ def main():
             "storage": "P rows int32 fixed point 2^-24 in LDS during the epoch; Q int32 fixed point 2^-24 "
                        "in HBM during a call (fp32 outside); the deltas are integer LDS / memory-side atomics",
             "data": "synthetic ML-1M-shaped ratings (rsgpu/synth.py: 6040 users x 3706 items, "
-                    "1,000,209 ratings per rank, seed 20250824+rank); random-init factors N(0,0.1)",
+                    "1,000,209 ratings per rank, seed 20250824+rank); random-init factors N(0,0.1); "
+                    "strong_scaling: rs_synth generator (csrc/synth.cpp)",
             "config": {"workload": "SVD nFactors=100 fast-mode SGD, 1 epoch over ML-1M-shaped set "
                                    "per step (BASELINE configs[1])",
                        "n_users": n_users, "n_items_per_rank": n_items, "nnz_per_rank": nnz,
                        "n_factors": K, "lr": LR, "reg": REG,
-                       "parallelism": f"item-sharded x{world}" if world > 1 else "single GPU"},
+                       "parallelism": f"item-sharded x{world} (RCCL all-reduce of user deltas, "
+                                      "pipelined per user block)" if world > 1 else "single GPU"},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
                          "traffic": traffic,
@@ -175,10 +254,13 @@ def main():
                          "algorithmic_bytes_per_launch": ab},
             "finite": finite,
         }
+        if strong is not None:
+            line["strong_scaling"] = strong
+        if world == 1 and not args.no_ordered:
+            line["ordered"] = ordered_throughput(ctx, u, i, r, n_users, n_items)
         if not args.no_cpu_baseline and world == 1:
             line["cpu_baseline"] = cpu_baseline(u, i, r, n_users, n_items, args.cpu_budget)
         print(json.dumps(line), flush=True)
-    plan.close()
     ctx.close()
     if dist:
         dist.destroy_process_group()

@@ -336,9 +336,12 @@ int rs_comm_unique_id(void* id /* RS_COMM_ID_BYTES */);
 int rs_svd_plan_join(rs_svd_plan* plan, const void* id, int32_t rank, int32_t n_ranks, int32_t n_blocks);
 int rs_svd_plan_epochs_sharded(rs_svd_plan* plan, int32_t n_epochs, float lr, float reg, void* stream);
 int rs_svd_plan_leave(rs_svd_plan* plan);
-/* User blocks of the tile schedule (default 1): the visit order becomes block by block.  Set by
- * rs_svd_plan_join; settable on its own so that a single plan reproduces a joined plan's order. */
-int rs_svd_plan_set_user_blocks(rs_svd_plan* plan, int32_t n_blocks);
+/* User blocks of the tile schedule (default 1): the visit order becomes block by block.  bounds
+ * (n_blocks + 1 user ids from 0 to n_users, or NULL: from this plan's ratings, the b-th bound being the
+ * first user whose ratings start at or past b / n_blocks of them).  A joined plan uses the same rule on
+ * every user's ratings over all shards, so the blocks agree across shards; passing those bounds here
+ * lets a single plan reproduce a joined plan's visit order. */
+int rs_svd_plan_set_user_blocks(rs_svd_plan* plan, int32_t n_blocks, const int32_t* bounds);
 /* One process driving n shards (one host thread per shard): RCCL when every plan has its own device,
  * otherwise (shards sharing a device: tests) an in-process exchange that sums the shards' deltas in
  * shard order after a host barrier (same arithmetic, no overlap).  The plans stay owned by the caller;

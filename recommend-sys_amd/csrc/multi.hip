@@ -172,13 +172,17 @@ void set_weights(rs_svd_plan* pl, const std::vector<double>& tot) {
     RS_HIP(hipStreamSynchronize(pl->ctx->stream));
 }
 
-// buffers, blocks and (RCCL) the comm stream of a shard whose comm / local group is set
-void shard_setup(rs_svd_plan* pl, ShardComm& c, int32_t n_blocks) {
+// buffers, blocks and (RCCL) the comm stream of a shard whose comm / local group is set; tot: every
+// user's ratings over all shards (the user blocks must be the same on every shard)
+void shard_setup(rs_svd_plan* pl, ShardComm& c, int32_t n_blocks, const std::vector<double>& tot) {
     if (pl->write_back != RS_SGD_WB_TILE)
         throw std::invalid_argument("the item-sharded epoch runs the tile schedule (RS_SGD_WB_TILE)");
     c.device = pl->ctx->device;
     c.ldd = round_up4(pl->k + 1);
     pl->tile_ublocks = n_blocks > 0 ? n_blocks : auto_blocks(pl, c.nranks, c.ldd);
+    std::vector<int64_t> cum(static_cast<size_t>(pl->n_users) + 1, 0);
+    for (int32_t u = 0; u < pl->n_users; ++u) cum[u + 1] = cum[u] + static_cast<int64_t>(tot[u]);
+    pl->ublock_bounds = user_block_bounds(cum.data(), pl->n_users, std::max(1, std::min(pl->tile_ublocks, std::max(1, pl->n_users))));
     if (c.nccl && c.nranks > 1 && pl->tile_wg == 0) {  // leave CUs to the collective's workgroups
         int cus = 0;
         RS_HIP(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, c.device));
@@ -335,7 +339,7 @@ void group_join(rs_svd_group* g, int32_t n_blocks) {
         c->local = g->local;
         c->total_nnz = total;
         rs::set_weights(pl, tot);
-        rs::shard_setup(pl, *c, n_blocks);
+        rs::shard_setup(pl, *c, n_blocks, tot);
         pl->shard = std::move(c);
     }
     if (g->local) {
@@ -359,13 +363,21 @@ extern "C" int rs_comm_unique_id(void* id) {
     });
 }
 
-extern "C" int rs_svd_plan_set_user_blocks(rs_svd_plan* pl, int32_t n_blocks) {
+extern "C" int rs_svd_plan_set_user_blocks(rs_svd_plan* pl, int32_t n_blocks, const int32_t* bounds) {
     if (!pl) return rs::set_error(nullptr, RS_ERR_INVALID, "plan is NULL");
     if (n_blocks < 1) return rs::set_error(pl->ctx, RS_ERR_INVALID, "n_blocks must be >= 1");
+    if (bounds) {
+        if (bounds[0] != 0 || bounds[n_blocks] != pl->n_users)
+            return rs::set_error(pl->ctx, RS_ERR_INVALID, "bounds must run from 0 to n_users");
+        for (int32_t b = 0; b < n_blocks; ++b)
+            if (bounds[b + 1] < bounds[b]) return rs::set_error(pl->ctx, RS_ERR_INVALID, "bounds must not decrease");
+    }
     return rs_guard(pl->ctx, [&]() -> int {
         if (pl->shard) return rs::set_error(pl->ctx, RS_ERR_INVALID, "plan is joined to a group (leave first)");
         rs::plan_sync_last(pl);
         pl->tile_ublocks = n_blocks;
+        if (bounds) pl->ublock_bounds.assign(bounds, bounds + n_blocks + 1);
+        else pl->ublock_bounds.clear();
         if (pl->write_back == RS_SGD_WB_TILE) {
             rs::tile_build(pl);
             pl->n_blocks = rs::tile_partials(pl);
@@ -408,7 +420,7 @@ extern "C" int rs_svd_plan_join(rs_svd_plan* pl, const void* id, int32_t rank, i
         c->total_nnz = cnt.back();
         cnt.pop_back();
         rs::set_weights(pl, cnt);
-        rs::shard_setup(pl, *c, n_blocks);
+        rs::shard_setup(pl, *c, n_blocks, cnt);
         pl->shard = std::move(c);
         return RS_OK;
     });
@@ -418,7 +430,7 @@ extern "C" int rs_svd_plan_leave(rs_svd_plan* pl) {
     if (!pl) return rs::set_error(nullptr, RS_ERR_INVALID, "plan is NULL");
     return rs_guard(pl->ctx, [&]() -> int {
         rs::plan_sync_last(pl);
-        pl->shard.reset();
+        pl->shard.reset();  // the tiles keep the group's blocks until the next rs_svd_plan_set_user_blocks
         return RS_OK;
     });
 }

@@ -93,6 +93,7 @@ struct rs_svd_plan {
     // [t_block_tile[b], t_block_tile[b+1]) hold users [t_block_user[b], t_block_user[b+1])); the
     // item-sharded multi-GPU epoch all-reduces a block's user deltas while the next block computes
     int32_t tile_ublocks = 1;
+    std::vector<int32_t> ublock_bounds;  // caller's block bounds (tile_ublocks + 1), or empty: own ratings
     std::vector<int32_t> t_block_tile, t_block_user;
     std::shared_ptr<rs::ShardComm> shard;  // item-sharded multi-GPU state (multi.hip), or empty
     ~rs_svd_plan() {
@@ -156,6 +157,7 @@ void gb_sum(const double* partial, int64_t n, double* out, hipStream_t s);  // f
 
 // sgd_tile.hip
 void tile_build(rs_svd_plan* pl);  // (re)builds the tile schedule from the host CSR
+std::vector<int32_t> user_block_bounds(const int64_t* cum, int32_t n_users, int32_t nb);
 void tile_launch(rs_svd_plan* pl, float lr, float reg, hipStream_t s, float* dP);  // one epoch (Q int32)
 // tiles [t0, t1) only (one user block), delta mode into dP (row stride ldd); returns the number of
 // GlobalBias partials written to pl->partial

@@ -628,19 +628,35 @@ int64_t tile_target_of(const rs_svd_plan* pl, int32_t grid, int32_t u_begin, int
     return std::max<int64_t>({64, dmax, (n + grid - 1) / std::max(1, grid)});
 }
 
+}  // namespace
+
+// b-th bound = the first user whose ratings start at or past b/nb of all ratings (cum: n_users + 1
+// cumulative counts); the same rule on every shard's global counts gives common bounds
+std::vector<int32_t> user_block_bounds(const int64_t* cum, int32_t n_users, int32_t nb) {
+    std::vector<int32_t> out(1, 0);
+    for (int32_t b = 1; b < nb; ++b) {
+        const int64_t want = cum[n_users] * b / nb;
+        const int32_t u = static_cast<int32_t>(std::lower_bound(cum, cum + n_users + 1, want) - cum);
+        out.push_back(std::max(out.back(), std::min(u, n_users)));
+    }
+    out.push_back(n_users);
+    return out;
+}
+
+namespace {
+
 // User blocks: tile_ublocks consecutive user ranges of near-equal ratings, tiled one after the other
 // (block b's tiles are [block_tile[b], block_tile[b+1])).  One block: the plain tile schedule.
 void build_tile_blocks(const rs_svd_plan* pl, int32_t grid0, bool want_pos, TileHost& th,
                        std::vector<int32_t>& block_tile, std::vector<int32_t>& block_user) {
-    const int32_t nb = std::max(1, std::min(pl->tile_ublocks, std::max(1, pl->n_users)));
     const std::vector<int64_t>& rp = pl->h_rowptr;
-    block_user.assign(1, 0);
-    for (int32_t b = 1; b < nb; ++b) {  // first user whose ratings start at or past b/nb of nnz
-        const int64_t want = pl->nnz * b / nb;
-        const int32_t u = static_cast<int32_t>(std::lower_bound(rp.begin(), rp.begin() + pl->n_users + 1, want) - rp.begin());
-        block_user.push_back(std::max(block_user.back(), std::min(u, pl->n_users)));
+    if (!pl->ublock_bounds.empty()) {  // common bounds of the shards of a multi-GPU fit
+        block_user = pl->ublock_bounds;
+    } else {
+        const int32_t nb = std::max(1, std::min(pl->tile_ublocks, std::max(1, pl->n_users)));
+        block_user = user_block_bounds(rp.data(), pl->n_users, nb);
     }
-    block_user.push_back(pl->n_users);
+    const int32_t nb = static_cast<int32_t>(block_user.size()) - 1;
     const int32_t cap = pl->tile_run_cap > 0 ? pl->tile_run_cap : auto_run_cap(pl, grid0, pl->tile_waves);
     block_tile.assign(1, 0);
     for (int32_t b = 0; b < nb; ++b) {

@@ -150,7 +150,7 @@ def lib():
             "rs_svd_plan_join": (C.c_int, [_vp, _vp, _i32, _i32, _i32]),
             "rs_svd_plan_epochs_sharded": (C.c_int, [_vp, _i32, _flt, _flt, _vp]),
             "rs_svd_plan_leave": (C.c_int, [_vp]),
-            "rs_svd_plan_set_user_blocks": (C.c_int, [_vp, _i32]),
+            "rs_svd_plan_set_user_blocks": (C.c_int, [_vp, _i32, _vp]),
             "rs_svd_group_create": (C.c_int, [_vp, _i32, _i32, C.POINTER(_vp)]),
             "rs_svd_group_epochs": (C.c_int, [_vp, _i32, _flt, _flt]),
             "rs_svd_group_destroy": (None, [_vp]),
@@ -439,9 +439,11 @@ class SvdPlan:
     def set_mode(self, write_back=WB_TILE, ring_depth=16):
         self.ctx.check(lib().rs_svd_plan_set_mode(self.h, write_back, ring_depth))
 
-    def set_user_blocks(self, n_blocks):
-        """Tile schedule in n_blocks consecutive user blocks (rs_svd_plan_set_user_blocks)."""
-        self.ctx.check(lib().rs_svd_plan_set_user_blocks(self.h, n_blocks))
+    def set_user_blocks(self, n_blocks, bounds=None):
+        """Tile schedule in n_blocks consecutive user blocks (rs_svd_plan_set_user_blocks); bounds:
+        n_blocks + 1 user ids (None: from this plan's ratings)."""
+        b = None if bounds is None else np.ascontiguousarray(bounds, np.int32)
+        self.ctx.check(lib().rs_svd_plan_set_user_blocks(self.h, n_blocks, _ptr(b)))
 
     def join(self, comm_id: bytes, rank: int, n_ranks: int, n_blocks: int = 0):
         """Item-sharded multi-GPU (rs_svd_plan_join; collective over the ranks): comm_id from

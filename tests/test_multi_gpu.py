@@ -35,12 +35,21 @@ def _shards(u, i, r, nu, ni, n):
     return out
 
 
+def _bounds(shards, nu, blocks):
+    """The library's common user-block bounds: from every user's ratings over all shards, the b-th
+    bound is the first user whose ratings start at or past b/blocks of them."""
+    cnt = sum(np.bincount(su, minlength=nu) for su, *_ in shards)
+    cum = np.concatenate([[0], np.cumsum(cnt)])
+    return np.array([np.searchsorted(cum, cum[-1] * b // blocks, side="left") for b in range(blocks)] + [nu])
+
+
 def _plans(ctx, shards, k, P0, Q0, blocks, waves=1, wg=1):
     plans = []
+    bounds = _bounds(shards, shards[0][3], blocks)
     for su, si, sr, nu, ni_s, lo in shards:
         pl = ctx.svd_plan(rsgpu.Ratings(su, si, sr, nu, ni_s), k)
         pl.set_tiles(workgroups=wg, waves=waves)
-        pl.set_user_blocks(blocks)
+        pl.set_user_blocks(blocks, bounds)
         pl.upload(P0, Q0[lo:lo + ni_s], np.zeros(nu), np.zeros(ni_s), 3.5)
         plans.append(pl)
     return plans
