@@ -37,7 +37,10 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <atomic>
+#include <chrono>
 #include <cmath>
+#include <cstdio>
 #include <cstdlib>
 #include <cstring>
 #include <numeric>
@@ -382,6 +385,14 @@ void build_tile_host(const rs_svd_plan* pl, int32_t u_begin, int32_t u_end, int3
     // near-equal ratings per tile -- the epoch is its slowest workgroup, and a workgroup's time tracks
     // its tile's ratings (measured: correlation 0.90 on the ML-1M shape).  The tile count is the
     // larger of nnz / target and what the LDS needs; entries of a tile keep user order.
+    static const bool ttrace = std::getenv("RSGPU_TILE_TRACE") != nullptr;
+    auto tprev = std::chrono::steady_clock::now();
+    auto tmark = [&](const char* what) {
+        if (!ttrace) return;
+        const auto t1 = std::chrono::steady_clock::now();
+        std::fprintf(stderr, "tile-build %-8s %8.3f ms\n", what, std::chrono::duration<double, std::milli>(t1 - tprev).count());
+        tprev = t1;
+    };
     std::vector<size_t> tb{0};
     {
         int64_t total = 0;
@@ -429,6 +440,7 @@ void build_tile_host(const rs_svd_plan* pl, int32_t u_begin, int32_t u_end, int3
             bn.ents.push_back(x);
             heap.push({bn.recs, pick});
         }
+        tmark("lpt");
         // Refinement by cost: a workgroup's time is ~ ratings + kRunCost * runs (one run per distinct item
         // of the tile; measured on the ML-1M shape: ~120 cycles per run against ~34 per rating, so
         // tiles of many light users -- more shared items -- are cheaper than tiles of one heavy user).
@@ -497,107 +509,168 @@ void build_tile_host(const rs_svd_plan* pl, int32_t u_begin, int32_t u_end, int3
         }
         ents.swap(sorted);
     }
+    tmark("refine");
     const size_t nt = tb.size() - 1;
-    // per tile: runs grouped by item in a per-tile pseudo-random item order, dealt to nw streams
+    // per tile: runs grouped by item in a per-tile pseudo-random item order, dealt to nw streams.
+    // Two parallel passes over the tiles: (1) group each tile's records by item without a comparison
+    // sort over records (distinct items through a per-thread item -> slot map, the distinct items put
+    // in key order by an LSD radix sort of their 32-bit keys, records scattered in entry = user order),
+    // cut and deal the runs; (2) write the records straight into the schedule's arrays at the tiles'
+    // offsets.  One-shot Fit pays this on every call.
     struct Local {
-        std::vector<int32_t> st;   // nw + 1 run offsets
-        std::vector<int2> runs;    // + sentinel
-        std::vector<int2> recs;
-        std::vector<int64_t> pos;
+        std::vector<int32_t> st;    // nw + 1 run offsets
+        std::vector<int2> runs;     // {item, first record (tile-local)} + sentinel
+        std::vector<int32_t> vul;   // grouped records: tile-local user entry
+        std::vector<int64_t> vp;    //                  CSR position
+        std::vector<int32_t> rb;    // per run (stream order): first grouped record
     };
     std::vector<Local> loc(nt);
     const std::vector<int32_t>& cols = pl->h_cols;
     const std::vector<float>& vals = pl->h_vals;
-    auto build_one = [&](size_t t) {
+    const size_t cap = (run_cap > 0 && nw > 1) ? static_cast<size_t>(run_cap) : 0;
+    auto group_one = [&](size_t t, std::vector<int32_t>& slot) {
         Local& L = loc[t];
-        struct R { uint32_t key; int32_t item; int32_t ul; int64_t p; };
-        std::vector<R> v;
+        std::vector<int32_t> ditem, dcnt;
         for (size_t x = tb[t]; x < tb[t + 1]; ++x)
-            for (int64_t p = ents[x].b; p < ents[x].e; ++p)
-                v.push_back({mix32((static_cast<uint64_t>(cols[p]) << 20) ^ (t * 0x9E3779B1ULL)), cols[p],
-                             static_cast<int32_t>(x - tb[t]), p});
-        std::sort(v.begin(), v.end(), [](const R& x, const R& y) {
-            return x.key != y.key ? x.key < y.key : (x.item != y.item ? x.item < y.item : x.ul < y.ul);
-        });
-        // runs: maximal equal-item groups; with run_cap (and more than one wave) cut into pieces that
-        // go to different waves (two pieces in one wave's ring reach would read q_i before the
-        // earlier piece's atomic landed)
-        struct Run { size_t b, e; int32_t piece; };
-        std::vector<Run> rs_;
-        const size_t cap = (run_cap > 0 && nw > 1) ? static_cast<size_t>(run_cap) : 0;
-        for (size_t x = 0; x < v.size();) {
-            size_t y = x;
-            while (y < v.size() && v[y].item == v[x].item) ++y;
-            const size_t pieces = cap ? std::min<size_t>((y - x + cap - 1) / cap, static_cast<size_t>(nw)) : 1;
-            for (size_t c = 0; c < pieces; ++c)
-                rs_.push_back({x + (y - x) * c / pieces, x + (y - x) * (c + 1) / pieces, static_cast<int32_t>(c)});
-            x = y;
+            for (int64_t p = ents[x].b; p < ents[x].e; ++p) {
+                const int32_t it = cols[p];
+                if (slot[it] < 0) {
+                    slot[it] = static_cast<int32_t>(ditem.size());
+                    ditem.push_back(it);
+                    dcnt.push_back(0);
+                }
+                dcnt[slot[it]]++;
+            }
+        const size_t nd = ditem.size();
+        std::vector<uint32_t> key(nd), ord(nd), tmp(nd);
+        for (size_t d = 0; d < nd; ++d) {
+            key[d] = mix32((static_cast<uint64_t>(ditem[d]) << 20) ^ (t * 0x9E3779B1ULL));
+            ord[d] = static_cast<uint32_t>(d);
         }
-        // deal (in key order) to the least-loaded stream; cost ~ ratings + a run start.  The pieces
-        // of one item take distinct streams.
+        for (int sh = 0; sh < 32; sh += 8) {  // LSD radix by key (ties: first appearance)
+            uint32_t cnt[257] = {0};
+            for (size_t d = 0; d < nd; ++d) cnt[((key[ord[d]] >> sh) & 255u) + 1]++;
+            for (int b2 = 0; b2 < 256; ++b2) cnt[b2 + 1] += cnt[b2];
+            for (size_t d = 0; d < nd; ++d) tmp[cnt[(key[ord[d]] >> sh) & 255u]++] = ord[d];
+            ord.swap(tmp);
+        }
+        std::vector<int32_t> off(nd);  // grouped offset of each slot
+        {
+            int32_t acc = 0;
+            for (size_t d = 0; d < nd; ++d) {
+                off[ord[d]] = acc;
+                acc += dcnt[ord[d]];
+            }
+        }
+        size_t nrec = 0;
+        for (int32_t c : dcnt) nrec += static_cast<size_t>(c);
+        L.vul.resize(nrec);
+        L.vp.resize(nrec);
+        {
+            std::vector<int32_t> fill(off);
+            for (size_t x = tb[t]; x < tb[t + 1]; ++x)
+                for (int64_t p = ents[x].b; p < ents[x].e; ++p) {
+                    const int32_t o = fill[slot[cols[p]]]++;
+                    L.vul[o] = static_cast<int32_t>(x - tb[t]);
+                    L.vp[o] = p;
+                }
+        }
+        for (int32_t it : ditem) slot[it] = -1;
+        // runs in key order; with run_cap (and more than one wave) an item's records are cut into
+        // pieces that go to different waves (two pieces in one wave's ring reach would read q_i
+        // before the earlier piece's atomic landed).  Dealt to the least-loaded stream (cost ~
+        // ratings + a run start); the pieces of one item take distinct streams.
         std::vector<int64_t> load(nw, 0);
-        std::vector<std::vector<size_t>> sr(nw);
+        std::vector<std::vector<std::pair<int32_t, int32_t>>> sr(nw);  // per stream: (slot, piece)
         std::vector<uint8_t> used(nw, 0);
-        for (size_t r = 0; r < rs_.size(); ++r) {
-            if (rs_[r].piece == 0) std::fill(used.begin(), used.end(), 0);
-            int best = -1;
-            for (int s = 0; s < nw; ++s)
-                if (!used[s] && (best < 0 || load[s] < load[best])) best = s;
-            used[best] = 1;
-            load[best] += static_cast<int64_t>(rs_[r].e - rs_[r].b) + 2;
-            sr[best].push_back(r);
+        for (size_t d = 0; d < nd; ++d) {
+            const int32_t sl = static_cast<int32_t>(ord[d]);
+            const size_t c = static_cast<size_t>(dcnt[sl]);
+            const int32_t pieces = static_cast<int32_t>(cap ? std::min<size_t>((c + cap - 1) / cap, static_cast<size_t>(nw)) : 1);
+            if (pieces > 1) std::fill(used.begin(), used.end(), 0);
+            for (int32_t pc = 0; pc < pieces; ++pc) {
+                int best = -1;
+                for (int s2 = 0; s2 < nw; ++s2)
+                    if (!used[s2] && (best < 0 || load[s2] < load[best])) best = s2;
+                if (pieces > 1) used[best] = 1;
+                load[best] += static_cast<int64_t>(c * (pc + 1) / pieces - c * pc / pieces) + 2;
+                sr[best].push_back({sl, pc | (pieces << 16)});
+            }
         }
         L.st.assign(nw + 1, 0);
-        for (int s = 0; s < nw; ++s) {
-            L.st[s] = static_cast<int32_t>(L.runs.size());
-            for (size_t r : sr[s]) {
-                L.runs.push_back(make_int2(v[rs_[r].b].item, static_cast<int32_t>(L.recs.size())));
-                for (size_t x = rs_[r].b; x < rs_[r].e; ++x) {
-                    int32_t bits;
-                    std::memcpy(&bits, &vals[v[x].p], 4);
-                    L.recs.push_back(make_int2(v[x].ul, bits));
-                    if (want_pos) L.pos.push_back(v[x].p);
-                }
+        int32_t rec = 0;
+        for (int s2 = 0; s2 < nw; ++s2) {
+            L.st[s2] = static_cast<int32_t>(L.runs.size());
+            for (const auto& e : sr[s2]) {
+                const int32_t sl = e.first, pc = e.second & 0xffff, pieces = e.second >> 16;
+                const int64_t c = dcnt[sl];
+                const int32_t b = off[sl] + static_cast<int32_t>(c * pc / pieces);
+                const int32_t n = static_cast<int32_t>(c * (pc + 1) / pieces - c * pc / pieces);
+                L.runs.push_back(make_int2(ditem[sl], rec));
+                L.rb.push_back(b);
+                rec += n;
             }
         }
         L.st[nw] = static_cast<int32_t>(L.runs.size());
-        L.runs.push_back(make_int2(-1, static_cast<int32_t>(L.recs.size())));  // sentinel
+        L.runs.push_back(make_int2(-1, rec));  // sentinel
     };
-    {
-        const int nth = static_cast<int>(std::min<size_t>(16, std::max<size_t>(1, nt / 64)));
-        std::vector<std::thread> th;
+    auto parallel_tiles = [&](auto&& fn, bool with_slot) {
+        static const int want_th = std::getenv("RSGPU_TILE_THREADS") ? std::atoi(std::getenv("RSGPU_TILE_THREADS")) : 16;
+        const int nth = static_cast<int>(std::min<size_t>(static_cast<size_t>(std::max(1, want_th)), std::max<size_t>(1, nt / 8)));
+        std::vector<std::thread> th2;
         for (int c = 0; c < nth; ++c)
-            th.emplace_back([&, c] {
-                for (size_t t = c; t < nt; t += nth) build_one(t);
+            th2.emplace_back([&, c] {
+                std::vector<int32_t> slot(with_slot ? static_cast<size_t>(std::max(1, pl->n_items)) : 0, -1);
+                for (size_t t = c; t < nt; t += nth) fn(t, slot);
             });
-        for (std::thread& x : th) x.join();
-    }
+        for (std::thread& x : th2) x.join();
+    };
+    parallel_tiles(group_one, true);
+    tmark("group");
+    // offsets, then the records written in place
     th.tiles.resize(nt);
-    th.streams.reserve(nt * (nw + 1));
-    int64_t run_off = 0, rec_off = 0;
+    std::vector<int64_t> rec_at(nt + 1, 0), run_at(nt + 1, 0);
     for (size_t t = 0; t < nt; ++t) {
-        const Local& L = loc[t];
-        if (run_off + static_cast<int64_t>(L.runs.size()) >= (int64_t{1} << 31) ||
-            rec_off + static_cast<int64_t>(L.recs.size()) >= (int64_t{1} << 31))
-            throw std::invalid_argument("tile schedule: more than 2^31 runs or ratings");
-        th.tiles[t] = make_int4(static_cast<int32_t>(tb[t]), static_cast<int32_t>(tb[t + 1] - tb[t]),
-                                static_cast<int32_t>(run_off), static_cast<int32_t>(rec_off));
-        th.streams.insert(th.streams.end(), L.st.begin(), L.st.end());
-        th.runs.insert(th.runs.end(), L.runs.begin(), L.runs.end());
-        th.recs.insert(th.recs.end(), L.recs.begin(), L.recs.end());
-        if (want_pos) th.pos.insert(th.pos.end(), L.pos.begin(), L.pos.end());
-        th.lds = std::max(th.lds, tile_bytes(static_cast<int64_t>(tb[t + 1] - tb[t]), static_cast<int64_t>(L.recs.size()),
-                                             static_cast<int64_t>(L.runs.size()) - 1, ld));
-        run_off += static_cast<int64_t>(L.runs.size());
-        rec_off += static_cast<int64_t>(L.recs.size());
-        loc[t] = Local();
+        rec_at[t + 1] = rec_at[t] + static_cast<int64_t>(loc[t].vp.size());
+        run_at[t + 1] = run_at[t] + static_cast<int64_t>(loc[t].runs.size());
     }
+    if (run_at[nt] >= (int64_t{1} << 31) || rec_at[nt] >= (int64_t{1} << 31))
+        throw std::invalid_argument("tile schedule: more than 2^31 runs or ratings");
+    th.recs.resize(static_cast<size_t>(rec_at[nt]));
+    th.runs.resize(static_cast<size_t>(run_at[nt]));
+    th.streams.resize(nt * (nw + 1));
+    if (want_pos) th.pos.resize(static_cast<size_t>(rec_at[nt]));
+    parallel_tiles([&](size_t t, std::vector<int32_t>&) {
+        Local& L = loc[t];
+        int2* out = th.recs.data() + rec_at[t];
+        int64_t* po = want_pos ? th.pos.data() + rec_at[t] : nullptr;
+        const size_t nr = L.runs.size() - 1;
+        for (size_t r = 0; r < nr; ++r) {
+            const int32_t n = L.runs[r + 1].y - L.runs[r].y;
+            for (int32_t x = 0; x < n; ++x) {
+                const size_t g = static_cast<size_t>(L.rb[r] + x);
+                int32_t bits;
+                std::memcpy(&bits, &vals[L.vp[g]], 4);
+                *out++ = make_int2(L.vul[g], bits);
+                if (po) *po++ = L.vp[g];
+            }
+        }
+        std::copy(L.runs.begin(), L.runs.end(), th.runs.begin() + run_at[t]);
+        std::copy(L.st.begin(), L.st.end(), th.streams.begin() + static_cast<std::ptrdiff_t>(t * (nw + 1)));
+        th.tiles[t] = make_int4(static_cast<int32_t>(tb[t]), static_cast<int32_t>(tb[t + 1] - tb[t]),
+                                static_cast<int32_t>(run_at[t]), static_cast<int32_t>(rec_at[t]));
+        loc[t] = Local();
+    }, false);
+    for (size_t t = 0; t < nt; ++t)
+        th.lds = std::max(th.lds, tile_bytes(static_cast<int64_t>(tb[t + 1] - tb[t]), rec_at[t + 1] - rec_at[t],
+                                             run_at[t + 1] - run_at[t] - 1, ld));
     th.users.resize(ents.size());
     for (size_t x = 0; x < ents.size(); ++x) {
         int32_t bits;
         std::memcpy(&bits, &ents[x].frac, 4);
         th.users[x] = make_int2(ents[x].u, bits);
     }
+    tmark("emit");
     if (th.lds > kTileLdsBudget) throw std::logic_error("tile schedule exceeds the LDS");
 }
 
@@ -864,3 +937,34 @@ int32_t tile_launch_range(rs_svd_plan* pl, float lr, float reg, hipStream_t s, f
 }
 
 }  // namespace rs
+
+// Host-only diagnostic (no device): the tile schedule's host build for a user-CSR, timed.  Used to
+// profile one-shot Fit's host share on the CPU and by the CPU tests.
+extern "C" int rs_tile_schedule_host(int32_t n_users, int32_t n_items, const int64_t* rowptr, const int32_t* cols,
+                                     const float* vals, int32_t n_factors, int32_t workgroups, int32_t waves,
+                                     int32_t n_blocks, int64_t* pos, int32_t* n_tiles, double* ms) {
+    if (n_users < 0 || n_items < 0 || !rowptr || n_factors < 1 || n_factors > 510 || workgroups < 1 ||
+        (waves != 1 && waves != 2 && waves != 4 && waves != 8 && waves != 16) || n_blocks < 1)
+        return rs::set_error(nullptr, RS_ERR_INVALID, "bad tile schedule arguments");
+    return rs_guard(nullptr, [&]() -> int {
+        rs_svd_plan pl;
+        pl.n_users = n_users;
+        pl.n_items = n_items;
+        pl.k = n_factors;
+        pl.nnz = rowptr[n_users];
+        pl.h_rowptr.assign(rowptr, rowptr + n_users + 1);
+        pl.h_cols.assign(cols, cols + pl.nnz);
+        pl.h_vals.assign(vals, vals + pl.nnz);
+        pl.tile_waves = waves;
+        pl.tile_ublocks = n_blocks;
+        const auto t0 = std::chrono::steady_clock::now();
+        rs::TileHost th;
+        std::vector<int32_t> bt, bu;
+        rs::build_tile_blocks(&pl, workgroups, pos != nullptr, th, bt, bu);
+        const auto t1 = std::chrono::steady_clock::now();
+        if (ms) *ms = std::chrono::duration<double, std::milli>(t1 - t0).count();
+        if (n_tiles) *n_tiles = static_cast<int32_t>(th.tiles.size());
+        if (pos) std::copy(th.pos.begin(), th.pos.end(), pos);
+        return RS_OK;
+    });
+}

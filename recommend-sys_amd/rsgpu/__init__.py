@@ -42,7 +42,7 @@ HEADER_SYMBOLS = (
     "rs_svd_plan_tile_order", "rs_svd_plan_tile_clocks",
     "rs_comm_unique_id", "rs_svd_plan_join", "rs_svd_plan_epochs_sharded", "rs_svd_plan_leave",
     "rs_svd_plan_set_user_blocks", "rs_svd_group_create", "rs_svd_group_epochs", "rs_svd_group_destroy",
-    "rs_item_shards", "rs_svd_fit_multi",
+    "rs_item_shards", "rs_svd_fit_multi", "rs_tile_schedule_host",
 )
 COMM_ID_BYTES = 128
 
@@ -155,6 +155,8 @@ def lib():
             "rs_svd_group_epochs": (C.c_int, [_vp, _i32, _flt, _flt]),
             "rs_svd_group_destroy": (None, [_vp]),
             "rs_item_shards": (C.c_int, [_i64, _vp, _i32, _i32, _vp]),
+            "rs_tile_schedule_host": (C.c_int, [_i32, _i32, _vp, _vp, _vp, _i32, _i32, _i32, _i32, _vp,
+                                                C.POINTER(_i32), C.POINTER(_dbl)]),
             "rs_svd_fit_multi": (C.c_int, [_vp, _i32, C.POINTER(_Ratings), C.POINTER(_SgdParams), _i32,
                                            _vp, _vp, _vp, _vp, _vp]),
         }
@@ -593,6 +595,19 @@ def comm_unique_id() -> bytes:
     buf = C.create_string_buffer(COMM_ID_BYTES)
     _check(lib().rs_comm_unique_id(buf))
     return buf.raw
+
+
+def tile_schedule_host(n_users, n_items, rowptr, cols, vals, n_factors, workgroups=256, waves=16,
+                       n_blocks=1, want_pos=False):
+    """Host-only tile schedule build (rs_tile_schedule_host): (ms, n_tiles, pos or None)."""
+    rowptr = np.ascontiguousarray(rowptr, np.int64)
+    cols = np.ascontiguousarray(cols, np.int32)
+    vals = np.ascontiguousarray(vals, np.float32)
+    pos = np.empty(int(rowptr[-1]), np.int64) if want_pos else None
+    nt, ms = _i32(0), _dbl(0)
+    _check(lib().rs_tile_schedule_host(n_users, n_items, _ptr(rowptr), _ptr(cols), _ptr(vals), n_factors,
+                                       workgroups, waves, n_blocks, _ptr(pos), C.byref(nt), C.byref(ms)))
+    return ms.value, nt.value, pos
 
 
 def item_shards(items, n_items, n_shards):
