@@ -5,6 +5,7 @@
 
 #include <cstdint>
 #include <cstdio>
+#include <memory>
 #include <string>
 #include <vector>
 
@@ -16,6 +17,7 @@ struct rs_ctx {
     std::string err;
     hipEvent_t k0 = nullptr, k1 = nullptr;  // bracket the main kernels of the last estimator call
     double last_kernel_ms = 0.0;
+    std::shared_ptr<void> svd_fit_cache;  // rs_svd_fit: the last FAST plan and the COO it was built from
 };
 
 namespace rs {

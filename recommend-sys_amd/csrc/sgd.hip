@@ -36,6 +36,8 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cstring>
+#include <memory>
 #include <chrono>
 #include <cstdio>
 #include <cmath>
@@ -1972,6 +1974,32 @@ extern "C" int rs_svd_plan_last_kernel_ms(rs_svd_plan* pl, double* ms, int32_t* 
     });
 }
 
+namespace rs {
+// One-shot Fit keeps its plan (CSR, tile schedule, device buffers) for the next rs_svd_fit on the same
+// ctx with the same ratings -- GridSearchCV (eval.go:78-230) and repeated CrossValidate runs refit the
+// same folds -- verified by comparing the whole COO (no hash: an exact match or a rebuild).
+struct SvdFitCache {
+    int64_t nnz = -1;
+    int32_t n_users = 0, n_items = 0, k = 0, write_back = 0;
+    std::vector<int32_t> users, items;
+    std::vector<double> ratings;
+    std::unique_ptr<rs_svd_plan> plan;
+    bool matches(const rs_ratings* r, int32_t k2, int32_t wb) const {
+        if (!plan || nnz != r->nnz || n_users != r->n_users || n_items != r->n_items || k != k2 || write_back != wb)
+            return false;
+        const size_t n = static_cast<size_t>(nnz);
+        return n == 0 || (std::memcmp(users.data(), r->users, n * 4) == 0 &&
+                          std::memcmp(items.data(), r->items, n * 4) == 0 &&
+                          std::memcmp(ratings.data(), r->ratings, n * 8) == 0);
+    }
+};
+
+static bool fit_cache_on() {
+    static const bool on = !(std::getenv("RSGPU_FIT_CACHE") && std::atoi(std::getenv("RSGPU_FIT_CACHE")) == 0);
+    return on;
+}
+}  // namespace rs
+
 extern "C" int rs_svd_fit(rs_ctx* ctx, const rs_ratings* r, const rs_sgd_params* p, double* P,
                           double* Q, double* bu, double* bi, double* gb) {
     if (!ctx) return rs::set_error(ctx, RS_ERR_INVALID, "ctx is NULL");
@@ -1994,15 +2022,34 @@ extern "C" int rs_svd_fit(rs_ctx* ctx, const rs_ratings* r, const rs_sgd_params*
                              std::chrono::duration<double, std::milli>(t1 - t).count());
                 t = t1;
             };
-            rs_svd_plan pl;
-            pl.write_back = p->write_back >= RS_SGD_WB_TILE && p->write_back <= RS_SGD_WB_ATOMIC ? p->write_back : RS_SGD_WB_TILE;
-            {
+            const int32_t wb = p->write_back >= RS_SGD_WB_TILE && p->write_back <= RS_SGD_WB_ATOMIC ? p->write_back : RS_SGD_WB_TILE;
+            auto cache = std::static_pointer_cast<rs::SvdFitCache>(ctx->svd_fit_cache);
+            const bool hit = rs::fit_cache_on() && cache && cache->matches(r, p->n_factors, wb);
+            mark(hit ? "cache-hit" : "cache-miss");
+            if (!hit) {
+                ctx->svd_fit_cache.reset();  // free the old plan's device buffers first
+                cache = std::make_shared<rs::SvdFitCache>();
+                cache->plan = std::make_unique<rs_svd_plan>();
+                cache->plan->write_back = wb;
                 rs::UserCSR csr;
                 rs::build_csr(r->nnz, r->n_users, r->users, r->items, r->ratings, csr);
                 mark("csr");
-                rs::plan_build_csr(ctx, r->n_users, r->n_items, std::move(csr), p->n_factors, &pl);
+                rs::plan_build_csr(ctx, r->n_users, r->n_items, std::move(csr), p->n_factors, cache->plan.get());
                 mark("plan");
+                if (rs::fit_cache_on()) {
+                    const size_t n = static_cast<size_t>(r->nnz);
+                    cache->nnz = r->nnz;
+                    cache->n_users = r->n_users;
+                    cache->n_items = r->n_items;
+                    cache->k = p->n_factors;
+                    cache->write_back = wb;
+                    cache->users.assign(r->users, r->users + n);
+                    cache->items.assign(r->items, r->items + n);
+                    cache->ratings.assign(r->ratings, r->ratings + n);
+                    ctx->svd_fit_cache = cache;
+                }
             }
+            rs_svd_plan& pl = *cache->plan;
             if (p->n_epochs > 0) *gb = rs::gb_warm_start(r, bu, bi);
             mark("warm");
             rs::plan_upload(&pl, P, Q, bu, bi, gb);
