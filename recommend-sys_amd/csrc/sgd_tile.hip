@@ -587,12 +587,12 @@ void build_tile_host(const rs_svd_plan* pl, int32_t u_begin, int32_t u_end, int3
             const int32_t sl = static_cast<int32_t>(ord[d]);
             const size_t c = static_cast<size_t>(dcnt[sl]);
             const int32_t pieces = static_cast<int32_t>(cap ? std::min<size_t>((c + cap - 1) / cap, static_cast<size_t>(nw)) : 1);
-            if (pieces > 1) std::fill(used.begin(), used.end(), 0);
+            std::fill(used.begin(), used.end(), 0);
             for (int32_t pc = 0; pc < pieces; ++pc) {
                 int best = -1;
                 for (int s2 = 0; s2 < nw; ++s2)
                     if (!used[s2] && (best < 0 || load[s2] < load[best])) best = s2;
-                if (pieces > 1) used[best] = 1;
+                used[best] = 1;
                 load[best] += static_cast<int64_t>(c * (pc + 1) / pieces - c * pc / pieces) + 2;
                 sr[best].push_back({sl, pc | (pieces << 16)});
             }
