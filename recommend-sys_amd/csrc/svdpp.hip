@@ -29,6 +29,7 @@
 #include <vector>
 
 #include "common.hpp"
+#include "sgd_plan.hpp"
 #include "wave.hpp"
 
 namespace rs {
@@ -653,9 +654,43 @@ extern "C" int rs_svdpp_fit(rs_ctx* ctx, const rs_ratings* r, const rs_sgd_param
         dQ.upload(hQ.data(), hQ.size(), s);
         dY.upload(hY.data(), hY.size(), s);
         const double inv_nnz = r->nnz > 0 ? 1.0 / static_cast<double>(r->nnz) : 0.0;
+        // The tile schedule (svdpp_tile.hip, write_back RS_SGD_WB_TILE, the default) unless a user is too
+        // heavy for one tile's LDS, k > 254, fp32 rows were asked for or RSGPU_PP_TILE=0; otherwise (and
+        // for any other write_back) the user-major lazy kernel below
+        bool tile = fx && k <= 254 && p->write_back == RS_SGD_WB_TILE;
+        if (const char* env = std::getenv("RSGPU_PP_TILE")) tile = tile && std::atoi(env) != 0;
+        rs_svd_plan sh;
+        if (tile) {
+            sh.ctx = ctx;
+            sh.n_users = r->n_users;
+            sh.n_items = r->n_items;
+            sh.k = k;
+            sh.ld = ld;
+            sh.nnz = r->nnz;
+            sh.h_rowptr = csr.rowptr;
+            sh.h_cols = csr.cols;
+            sh.h_vals = csr.vals;
+            sh.tile_pp = true;
+            sh.tile_user_lds = rs::pp_tile_user_lds(k);
+            if (const char* env = std::getenv("RSGPU_PP_TILE_WG")) sh.tile_wg = std::max(0, std::atoi(env));
+            try {
+                rs::tile_build(&sh);
+            } catch (const std::invalid_argument&) {
+                tile = false;  // a user whose ratings do not fit one tile
+            }
+        }
+        rs::DevBuf<double> tpart(tile ? static_cast<size_t>(sh.tile_grid) * 16 : 1);
         RS_HIP(hipStreamSynchronize(s));
         rs::kernel_span_begin(ctx);
-        for (int32_t ep = 0; ep < p->n_epochs; ++ep) {
+        for (int32_t ep = 0; tile && ep < p->n_epochs; ++ep) {
+            rs::pp_tile_launch(sh, reinterpret_cast<int32_t*>(dQ.p), static_cast<int32_t>(dQ.n * 4),
+                               reinterpret_cast<int32_t*>(dY.p), static_cast<int32_t>(dY.n * 4), dP.p, dgb.p, tpart.p,
+                               lr, reg, k, ld, s);
+            hipLaunchKernelGGL(rs::pp_gb_fold_kernel, dim3(1), dim3(256), 0, s, tpart.p,
+                               static_cast<int64_t>(sh.tile_grid) * 16, dgb.p, inv_nnz);
+            RS_HIP(hipGetLastError());
+        }
+        for (int32_t ep = 0; !tile && ep < p->n_epochs; ++ep) {
             switch (E) {
                 case 1: rs::launch_pp_fast<1>(n_blocks, dwork, n_work, n_heavy, drow, dcol, dval, dP, dQ, dY, dgb, dpart, lr, reg, k, fx, s); break;
                 case 2: rs::launch_pp_fast<2>(n_blocks, dwork, n_work, n_heavy, drow, dcol, dval, dP, dQ, dY, dgb, dpart, lr, reg, k, fx, s); break;

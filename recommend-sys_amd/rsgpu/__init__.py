@@ -325,15 +325,16 @@ class Context:
         return P, Q, bu, bi, float(g[0])
 
     def svdpp_fit(self, r: Ratings, P, Q, Y, bu=None, bi=None, gb=0.0, n_epochs=20, lr=0.007,
-                  reg=0.02, mode=SGD_FAST):
-        """core/svd.go:316-427 (ORDERED: literal per-rating y updates; FAST: lazy-y user-CSR)."""
+                  reg=0.02, mode=SGD_FAST, write_back=WB_TILE):
+        """core/svd.go:316-427 (ORDERED: literal per-rating y updates; FAST: the tile schedule with
+        the order-free lazy y state (write_back WB_TILE), or the user-major lazy kernel (WB_ATOMIC))."""
         P = np.array(P, dtype=np.float64, order="C")
         Q = np.array(Q, dtype=np.float64, order="C")
         Y = np.array(Y, dtype=np.float64, order="C")
         bu = np.zeros(r.n_users) if bu is None else np.array(bu, dtype=np.float64)
         bi = np.zeros(r.n_items) if bi is None else np.array(bi, dtype=np.float64)
         g = np.array([gb], dtype=np.float64)
-        prm = _SgdParams(P.shape[1], n_epochs, lr, reg, mode, 0)
+        prm = _SgdParams(P.shape[1], n_epochs, lr, reg, mode, write_back)
         rc = r.c()
         self.check(lib().rs_svdpp_fit(self.h, C.byref(rc), C.byref(prm), _ptr(P), _ptr(Q), _ptr(Y),
                                       _ptr(bu), _ptr(bi), _ptr(g)))

@@ -54,7 +54,8 @@ def test_svdpp_fast_lazy_matches_literal_race_free(ctx, k):
     rowptr, items, rr = O.csr_by(u, nu, i, r)
     for epochs in (1, 3):
         ref = O.svdpp_fit_userwise(rowptr, items, rr, P0, Q0, Y0, epochs=epochs)
-        got = ctx.svdpp_fit(rsgpu.Ratings(u, i, r, nu, ni), P0, Q0, Y0, n_epochs=epochs)
+        got = ctx.svdpp_fit(rsgpu.Ratings(u, i, r, nu, ni), P0, Q0, Y0, n_epochs=epochs,
+                            write_back=rsgpu.WB_ATOMIC)
         assert _maxdiff(ref[:5], got[:5]) <= TOL, (k, epochs)
         assert abs(ref[5] - got[5]) <= TOL
 
@@ -77,20 +78,22 @@ def test_svdpp_fast_heavy_blocks_race_free(ctx, monkeypatch, heavy, k):
     monkeypatch.setenv("RSGPU_PP_HEAVY", str(heavy))
     for epochs in (1, 2):
         ref = O.svdpp_fit_userwise(rowptr, it, rr, P0, Q0, Y0, epochs=epochs)
-        got = ctx.svdpp_fit(rsgpu.Ratings(u, i, r, nu, ni), P0, Q0, Y0, n_epochs=epochs)
+        got = ctx.svdpp_fit(rsgpu.Ratings(u, i, r, nu, ni), P0, Q0, Y0, n_epochs=epochs,
+                            write_back=rsgpu.WB_ATOMIC)
         assert _maxdiff(ref[:5], got[:5]) <= TOL, (heavy, k, epochs)
         assert abs(ref[5] - got[5]) <= TOL
 
 
-def test_svdpp_fast_rmse_near_literal(ctx, fold0):
-    """Fast (lazy, user-major, Hogwild) vs the literal reference order on ML-100K fold 1, defaults
-    (k=20, 20 epochs, lr 0.007, reg 0.02)."""
+@pytest.mark.parametrize("wb", [rsgpu.WB_TILE, rsgpu.WB_ATOMIC])
+def test_svdpp_fast_rmse_near_literal(ctx, fold0, wb):
+    """Fast (tile schedule / user-major lazy kernel, Hogwild) vs the literal reference order on ML-100K
+    fold 1, defaults (k=20, 20 epochs, lr 0.007, reg 0.02)."""
     f, k = fold0, 20
     rng = np.random.default_rng(4)
     P0, Q0, Y0 = (rng.normal(0, 0.1, (m, k)) for m in (f.nu, f.ni, f.ni))
     a = O.svdpp_fit(f.iu, f.ii, f.r, f.nu, P0, Q0, Y0)
     ref = rmse(O.svdpp_predict(f.iu, f.ii, f.nu, f.tu, f.ti, *a), f.te_r)
-    b = ctx.svdpp_fit(rsgpu.Ratings(f.iu, f.ii, f.r, f.nu, f.ni), P0, Q0, Y0)
+    b = ctx.svdpp_fit(rsgpu.Ratings(f.iu, f.ii, f.r, f.nu, f.ni), P0, Q0, Y0, write_back=wb)
     got = rmse(O.svdpp_predict(f.iu, f.ii, f.nu, f.tu, f.ti, *b), f.te_r)
     assert abs(got - ref) <= 0.005, (got, ref)
     assert got <= 0.92 + 0.008 + 0.01  # the reference's (disabled) bound, base_test.go:38-40
