@@ -974,7 +974,8 @@ int32_t tile_launch_range(rs_svd_plan* pl, float lr, float reg, hipStream_t s, f
 // profile one-shot Fit's host share on the CPU and by the CPU tests.
 extern "C" int rs_tile_schedule_host(int32_t n_users, int32_t n_items, const int64_t* rowptr, const int32_t* cols,
                                      const float* vals, int32_t n_factors, int32_t workgroups, int32_t waves,
-                                     int32_t n_blocks, int64_t* pos, int32_t* n_tiles, double* ms) {
+                                     int32_t n_blocks, int32_t svdpp, int64_t* pos, int64_t* tile_off,
+                                     int32_t* rank, int32_t* n_tiles, double* ms) {
     if (n_users < 0 || n_items < 0 || !rowptr || n_factors < 1 || n_factors > 510 || workgroups < 1 ||
         (waves != 1 && waves != 2 && waves != 4 && waves != 8 && waves != 16) || n_blocks < 1)
         return rs::set_error(nullptr, RS_ERR_INVALID, "bad tile schedule arguments");
@@ -989,6 +990,10 @@ extern "C" int rs_tile_schedule_host(int32_t n_users, int32_t n_items, const int
         pl.h_vals.assign(vals, vals + pl.nnz);
         pl.tile_waves = waves;
         pl.tile_ublocks = n_blocks;
+        if (svdpp) {
+            pl.tile_pp = true;
+            pl.tile_user_lds = rs::pp_tile_user_lds(n_factors);
+        }
         const auto t0 = std::chrono::steady_clock::now();
         rs::TileHost th;
         std::vector<int32_t> bt, bu;
@@ -997,6 +1002,12 @@ extern "C" int rs_tile_schedule_host(int32_t n_users, int32_t n_items, const int
         if (ms) *ms = std::chrono::duration<double, std::milli>(t1 - t0).count();
         if (n_tiles) *n_tiles = static_cast<int32_t>(th.tiles.size());
         if (pos) std::copy(th.pos.begin(), th.pos.end(), pos);
+        if (tile_off) {
+            for (size_t t = 0; t < th.tiles.size(); ++t) tile_off[t] = th.tiles[t].w;
+            tile_off[th.tiles.size()] = static_cast<int64_t>(th.recs.size());
+        }
+        if (rank)
+            for (size_t x = 0; x < th.recs.size(); ++x) rank[x] = svdpp ? (th.recs[x].x >> 16) : 0;
         return RS_OK;
     });
 }

@@ -673,13 +673,14 @@ extern "C" int rs_svdpp_fit(rs_ctx* ctx, const rs_ratings* r, const rs_sgd_param
             sh.tile_pp = true;
             sh.tile_user_lds = rs::pp_tile_user_lds(k);
             if (const char* env = std::getenv("RSGPU_PP_TILE_WG")) sh.tile_wg = std::max(0, std::atoi(env));
+            if (const char* env = std::getenv("RSGPU_PP_TILE_WAVES")) sh.tile_waves = std::atoi(env) == 1 ? 1 : 16;
             try {
                 rs::tile_build(&sh);
             } catch (const std::invalid_argument&) {
                 tile = false;  // a user whose ratings do not fit one tile
             }
         }
-        rs::DevBuf<double> tpart(tile ? static_cast<size_t>(sh.tile_grid) * 16 : 1);
+        rs::DevBuf<double> tpart(tile ? static_cast<size_t>(sh.tile_grid) * sh.tile_waves : 1);
         RS_HIP(hipStreamSynchronize(s));
         rs::kernel_span_begin(ctx);
         for (int32_t ep = 0; tile && ep < p->n_epochs; ++ep) {
@@ -687,7 +688,7 @@ extern "C" int rs_svdpp_fit(rs_ctx* ctx, const rs_ratings* r, const rs_sgd_param
                                reinterpret_cast<int32_t*>(dY.p), static_cast<int32_t>(dY.n * 4), dP.p, dgb.p, tpart.p,
                                lr, reg, k, ld, s);
             hipLaunchKernelGGL(rs::pp_gb_fold_kernel, dim3(1), dim3(256), 0, s, tpart.p,
-                               static_cast<int64_t>(sh.tile_grid) * 16, dgb.p, inv_nnz);
+                               static_cast<int64_t>(sh.tile_grid) * sh.tile_waves, dgb.p, inv_nnz);
             RS_HIP(hipGetLastError());
         }
         for (int32_t ep = 0; !tile && ep < p->n_epochs; ++ep) {

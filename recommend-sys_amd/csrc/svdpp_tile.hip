@@ -52,8 +52,8 @@ __global__ __launch_bounds__(NW * 64) void svdpp_epoch_tile_kernel(
     const int4* __restrict__ tiles, int32_t n_tiles, const int2* __restrict__ tile_users,
     const int32_t* __restrict__ streams, const int2* __restrict__ runs, const int2* __restrict__ recs,
     float* __restrict__ P, int32_t* Q, int32_t q_bytes, int32_t* Y, int32_t y_bytes,
-    const double* __restrict__ gb_in, double* __restrict__ gb_partial, float lr, float reg, int32_t kf,
-    int32_t ldm) {
+    const double* __restrict__ gb_in, double* __restrict__ gb_partial, float lr, float reg, float la,
+    int32_t kf, int32_t ldm) {
 #pragma clang fp contract(fast)
     constexpr int LD = 64 * E, NT = NW * 64;
     static_assert(2 * E * RQ <= 60, "ring loads and atomics must fit the 63-op vmcnt");
@@ -63,7 +63,7 @@ __global__ __launch_bounds__(NW * 64) void svdpp_epoch_tile_kernel(
     const __amdgpu_buffer_rsrc_t rq = __builtin_amdgcn_make_buffer_rsrc(Q, 0, q_bytes, 0x00020000);
     const __amdgpu_buffer_rsrc_t ry = __builtin_amdgcn_make_buffer_rsrc(Y, 0, y_bytes, 0x00020000);
     const double gb0 = gb_in[0];
-    const float a = 1.f - lr * reg, am1 = -lr * reg, la = __log2f(a);
+    const float a = 1.f - lr * reg, am1 = -lr * reg;  // la = log2(a), from the host in double
     int32_t qoff[E], yoff[E];
     bool qone[E], pone[E], fac[E];
 #pragma unroll
@@ -255,18 +255,20 @@ __global__ __launch_bounds__(NW * 64) void svdpp_epoch_tile_kernel(
 
 namespace {
 
-template <int E>
+template <int E, int NW>
 void pp_tile_launch_e(const rs_svd_plan& sh, int32_t* Q, int32_t q_bytes, int32_t* Y, int32_t y_bytes, float* P,
                       const double* gb, double* partial, float lr, float reg, int32_t kf, int32_t ldm, hipStream_t s) {
-    auto kern = svdpp_epoch_tile_kernel<E, 16, 2>;
+    auto kern = svdpp_epoch_tile_kernel<E, NW, 2>;
     static bool attr = false;
     if (!attr) {
         RS_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize,
                                    static_cast<int>(160 * 1024 - 512)));
         attr = true;
     }
-    hipLaunchKernelGGL(kern, dim3(sh.tile_grid), dim3(16 * 64), sh.tile_lds, s, sh.t_tiles.p, sh.n_tiles, sh.t_users.p,
-                       sh.t_streams.p, sh.t_runs.p, sh.t_recs.p, P, Q, q_bytes, Y, y_bytes, gb, partial, lr, reg, kf, ldm);
+    const float la = static_cast<float>(std::log2(1.0 - static_cast<double>(lr) * static_cast<double>(reg)));
+    hipLaunchKernelGGL(kern, dim3(sh.tile_grid), dim3(NW * 64), sh.tile_lds, s, sh.t_tiles.p, sh.n_tiles, sh.t_users.p,
+                       sh.t_streams.p, sh.t_runs.p, sh.t_recs.p, P, Q, q_bytes, Y, y_bytes, gb, partial, lr, reg, la,
+                       kf, ldm);
 }
 
 }  // namespace
@@ -279,14 +281,19 @@ int32_t pp_tile_user_lds(int32_t k) {
 void pp_tile_launch(const rs_svd_plan& sh, int32_t* Q, int32_t q_bytes, int32_t* Y, int32_t y_bytes, float* P,
                     const double* gb, double* partial, float lr, float reg, int32_t kf, int32_t ldm, hipStream_t s) {
     if (sh.n_tiles == 0) {
-        RS_HIP(hipMemsetAsync(partial, 0, static_cast<size_t>(sh.tile_grid) * 16 * sizeof(double), s));
+        RS_HIP(hipMemsetAsync(partial, 0, static_cast<size_t>(sh.tile_grid) * sh.tile_waves * sizeof(double), s));
         return;
     }
+    const bool one = sh.tile_waves == 1;  // one wave per tile: the exact form (tests)
     switch ((kf + 2 + 63) / 64) {
-        case 1: pp_tile_launch_e<1>(sh, Q, q_bytes, Y, y_bytes, P, gb, partial, lr, reg, kf, ldm, s); break;
-        case 2: pp_tile_launch_e<2>(sh, Q, q_bytes, Y, y_bytes, P, gb, partial, lr, reg, kf, ldm, s); break;
-        case 3: pp_tile_launch_e<3>(sh, Q, q_bytes, Y, y_bytes, P, gb, partial, lr, reg, kf, ldm, s); break;
-        case 4: pp_tile_launch_e<4>(sh, Q, q_bytes, Y, y_bytes, P, gb, partial, lr, reg, kf, ldm, s); break;
+        case 1: one ? pp_tile_launch_e<1, 1>(sh, Q, q_bytes, Y, y_bytes, P, gb, partial, lr, reg, kf, ldm, s)
+                    : pp_tile_launch_e<1, 16>(sh, Q, q_bytes, Y, y_bytes, P, gb, partial, lr, reg, kf, ldm, s); break;
+        case 2: one ? pp_tile_launch_e<2, 1>(sh, Q, q_bytes, Y, y_bytes, P, gb, partial, lr, reg, kf, ldm, s)
+                    : pp_tile_launch_e<2, 16>(sh, Q, q_bytes, Y, y_bytes, P, gb, partial, lr, reg, kf, ldm, s); break;
+        case 3: one ? pp_tile_launch_e<3, 1>(sh, Q, q_bytes, Y, y_bytes, P, gb, partial, lr, reg, kf, ldm, s)
+                    : pp_tile_launch_e<3, 16>(sh, Q, q_bytes, Y, y_bytes, P, gb, partial, lr, reg, kf, ldm, s); break;
+        case 4: one ? pp_tile_launch_e<4, 1>(sh, Q, q_bytes, Y, y_bytes, P, gb, partial, lr, reg, kf, ldm, s)
+                    : pp_tile_launch_e<4, 16>(sh, Q, q_bytes, Y, y_bytes, P, gb, partial, lr, reg, kf, ldm, s); break;
         default: throw std::invalid_argument("SVD++ tile schedule: n_factors <= 254");
     }
     RS_HIP(hipGetLastError());

@@ -155,8 +155,8 @@ def lib():
             "rs_svd_group_epochs": (C.c_int, [_vp, _i32, _flt, _flt]),
             "rs_svd_group_destroy": (None, [_vp]),
             "rs_item_shards": (C.c_int, [_i64, _vp, _i32, _i32, _vp]),
-            "rs_tile_schedule_host": (C.c_int, [_i32, _i32, _vp, _vp, _vp, _i32, _i32, _i32, _i32, _vp,
-                                                C.POINTER(_i32), C.POINTER(_dbl)]),
+            "rs_tile_schedule_host": (C.c_int, [_i32, _i32, _vp, _vp, _vp, _i32, _i32, _i32, _i32, _i32, _vp,
+                                                _vp, _vp, C.POINTER(_i32), C.POINTER(_dbl)]),
             "rs_svd_fit_multi": (C.c_int, [_vp, _i32, C.POINTER(_Ratings), C.POINTER(_SgdParams), _i32,
                                            _vp, _vp, _vp, _vp, _vp]),
         }
@@ -599,16 +599,26 @@ def comm_unique_id() -> bytes:
 
 
 def tile_schedule_host(n_users, n_items, rowptr, cols, vals, n_factors, workgroups=256, waves=16,
-                       n_blocks=1, want_pos=False):
-    """Host-only tile schedule build (rs_tile_schedule_host): (ms, n_tiles, pos or None)."""
+                       n_blocks=1, want_pos=False, svdpp=False):
+    """Host-only tile schedule build (rs_tile_schedule_host): (ms, n_tiles, pos or None); with
+    svdpp=True (ms, n_tiles, pos, tile_off, rank) of the SVD++ variant."""
     rowptr = np.ascontiguousarray(rowptr, np.int64)
     cols = np.ascontiguousarray(cols, np.int32)
     vals = np.ascontiguousarray(vals, np.float32)
-    pos = np.empty(int(rowptr[-1]), np.int64) if want_pos else None
+    nnz = int(rowptr[-1])
+    pos = np.empty(nnz, np.int64) if (want_pos or svdpp) else None
     nt, ms = _i32(0), _dbl(0)
     _check(lib().rs_tile_schedule_host(n_users, n_items, _ptr(rowptr), _ptr(cols), _ptr(vals), n_factors,
-                                       workgroups, waves, n_blocks, _ptr(pos), C.byref(nt), C.byref(ms)))
-    return ms.value, nt.value, pos
+                                       workgroups, waves, n_blocks, int(svdpp), _ptr(pos), None, None,
+                                       C.byref(nt), C.byref(ms)))
+    if not svdpp:
+        return ms.value, nt.value, pos
+    off = np.empty(nt.value + 1, np.int64)
+    rank = np.empty(nnz, np.int32)
+    _check(lib().rs_tile_schedule_host(n_users, n_items, _ptr(rowptr), _ptr(cols), _ptr(vals), n_factors,
+                                       workgroups, waves, n_blocks, 1, _ptr(pos), _ptr(off), _ptr(rank),
+                                       C.byref(nt), C.byref(ms)))
+    return ms.value, nt.value, pos, off, rank
 
 
 def item_shards(items, n_items, n_shards):
