@@ -654,11 +654,12 @@ extern "C" int rs_svdpp_fit(rs_ctx* ctx, const rs_ratings* r, const rs_sgd_param
         dQ.upload(hQ.data(), hQ.size(), s);
         dY.upload(hY.data(), hY.size(), s);
         const double inv_nnz = r->nnz > 0 ? 1.0 / static_cast<double>(r->nnz) : 0.0;
-        // The tile schedule (svdpp_tile.hip, write_back RS_SGD_WB_TILE, the default) unless a user is too
-        // heavy for one tile's LDS, k > 254, fp32 rows were asked for or RSGPU_PP_TILE=0; otherwise (and
-        // for any other write_back) the user-major lazy kernel below
-        bool tile = fx && k <= 254 && p->write_back == RS_SGD_WB_TILE;
-        if (const char* env = std::getenv("RSGPU_PP_TILE")) tile = tile && std::atoi(env) != 0;
+        // The tile schedule (svdpp_tile.hip) is an experiment, selected by RSGPU_PP_TILE=1: exact with one
+        // workgroup (tests), 2.7x faster, but unstable under inter-workgroup concurrency (the y_j decays of
+        // concurrent tiles add up from one snapshot: NaN on the ML-1M shape).  The default is
+        // the user-major lazy kernel below.
+        bool tile = false;
+        if (const char* env = std::getenv("RSGPU_PP_TILE")) tile = fx && k <= 254 && std::atoi(env) == 1;
         rs_svd_plan sh;
         if (tile) {
             sh.ctx = ctx;
@@ -673,7 +674,10 @@ extern "C" int rs_svdpp_fit(rs_ctx* ctx, const rs_ratings* r, const rs_sgd_param
             sh.tile_pp = true;
             sh.tile_user_lds = rs::pp_tile_user_lds(k);
             if (const char* env = std::getenv("RSGPU_PP_TILE_WG")) sh.tile_wg = std::max(0, std::atoi(env));
-            if (const char* env = std::getenv("RSGPU_PP_TILE_WAVES")) sh.tile_waves = std::atoi(env) == 1 ? 1 : 16;
+            if (const char* env = std::getenv("RSGPU_PP_TILE_WAVES")) {
+                const int wv = std::atoi(env);
+                sh.tile_waves = (wv == 1 || wv == 4 || wv == 8) ? wv : 16;
+            }
             try {
                 rs::tile_build(&sh);
             } catch (const std::invalid_argument&) {

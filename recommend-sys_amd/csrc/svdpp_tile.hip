@@ -22,6 +22,7 @@
 #include <cmath>
 #include <cstdlib>
 #include <stdexcept>
+#include <type_traits>
 #include <vector>
 
 #include "common.hpp"
@@ -284,16 +285,20 @@ void pp_tile_launch(const rs_svd_plan& sh, int32_t* Q, int32_t q_bytes, int32_t*
         RS_HIP(hipMemsetAsync(partial, 0, static_cast<size_t>(sh.tile_grid) * sh.tile_waves * sizeof(double), s));
         return;
     }
-    const bool one = sh.tile_waves == 1;  // one wave per tile: the exact form (tests)
+    auto launch = [&](auto e_tag) {
+        constexpr int E = decltype(e_tag)::value;
+        switch (sh.tile_waves) {
+            case 1: pp_tile_launch_e<E, 1>(sh, Q, q_bytes, Y, y_bytes, P, gb, partial, lr, reg, kf, ldm, s); break;
+            case 4: pp_tile_launch_e<E, 4>(sh, Q, q_bytes, Y, y_bytes, P, gb, partial, lr, reg, kf, ldm, s); break;
+            case 8: pp_tile_launch_e<E, 8>(sh, Q, q_bytes, Y, y_bytes, P, gb, partial, lr, reg, kf, ldm, s); break;
+            default: pp_tile_launch_e<E, 16>(sh, Q, q_bytes, Y, y_bytes, P, gb, partial, lr, reg, kf, ldm, s); break;
+        }
+    };
     switch ((kf + 2 + 63) / 64) {
-        case 1: one ? pp_tile_launch_e<1, 1>(sh, Q, q_bytes, Y, y_bytes, P, gb, partial, lr, reg, kf, ldm, s)
-                    : pp_tile_launch_e<1, 16>(sh, Q, q_bytes, Y, y_bytes, P, gb, partial, lr, reg, kf, ldm, s); break;
-        case 2: one ? pp_tile_launch_e<2, 1>(sh, Q, q_bytes, Y, y_bytes, P, gb, partial, lr, reg, kf, ldm, s)
-                    : pp_tile_launch_e<2, 16>(sh, Q, q_bytes, Y, y_bytes, P, gb, partial, lr, reg, kf, ldm, s); break;
-        case 3: one ? pp_tile_launch_e<3, 1>(sh, Q, q_bytes, Y, y_bytes, P, gb, partial, lr, reg, kf, ldm, s)
-                    : pp_tile_launch_e<3, 16>(sh, Q, q_bytes, Y, y_bytes, P, gb, partial, lr, reg, kf, ldm, s); break;
-        case 4: one ? pp_tile_launch_e<4, 1>(sh, Q, q_bytes, Y, y_bytes, P, gb, partial, lr, reg, kf, ldm, s)
-                    : pp_tile_launch_e<4, 16>(sh, Q, q_bytes, Y, y_bytes, P, gb, partial, lr, reg, kf, ldm, s); break;
+        case 1: launch(std::integral_constant<int, 1>{}); break;
+        case 2: launch(std::integral_constant<int, 2>{}); break;
+        case 3: launch(std::integral_constant<int, 3>{}); break;
+        case 4: launch(std::integral_constant<int, 4>{}); break;
         default: throw std::invalid_argument("SVD++ tile schedule: n_factors <= 254");
     }
     RS_HIP(hipGetLastError());

@@ -326,8 +326,8 @@ class Context:
 
     def svdpp_fit(self, r: Ratings, P, Q, Y, bu=None, bi=None, gb=0.0, n_epochs=20, lr=0.007,
                   reg=0.02, mode=SGD_FAST, write_back=WB_TILE):
-        """core/svd.go:316-427 (ORDERED: literal per-rating y updates; FAST: the tile schedule with
-        the order-free lazy y state (write_back WB_TILE), or the user-major lazy kernel (WB_ATOMIC))."""
+        """core/svd.go:316-427 (ORDERED: literal per-rating y updates; FAST: the user-major lazy-y
+        kernel; RSGPU_PP_TILE=1 selects the experimental tile schedule)."""
         P = np.array(P, dtype=np.float64, order="C")
         Q = np.array(Q, dtype=np.float64, order="C")
         Y = np.array(Y, dtype=np.float64, order="C")
