@@ -3,10 +3,12 @@
 
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cstdint>
 #include <cstdio>
 #include <memory>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "rsgpu.h"
@@ -18,6 +20,7 @@ struct rs_ctx {
     hipEvent_t k0 = nullptr, k1 = nullptr;  // bracket the main kernels of the last estimator call
     double last_kernel_ms = 0.0;
     std::shared_ptr<void> svd_fit_cache;  // rs_svd_fit: the last FAST plan and the COO it was built from
+    std::shared_ptr<void> staging;        // pinned host ring of the streamed Sims download (sim.hip)
 };
 
 namespace rs {
@@ -89,6 +92,23 @@ struct DevBuf {
 };
 
 inline int32_t round_up4(int32_t k) { return (k + 3) & ~3; }
+
+// Host threads for an index range: f(begin, end) on up to `max_threads` contiguous slices (the
+// caller's thread takes the first).  For host-side preparation passes that do not touch the GPU.
+template <typename F>
+void parallel_ranges(int64_t n, int max_threads, F&& f) {
+    const unsigned hw = std::max(1u, std::thread::hardware_concurrency());
+    const int64_t nt = std::max<int64_t>(1, std::min<int64_t>({static_cast<int64_t>(max_threads),
+                                                               static_cast<int64_t>(hw), (n + 4095) / 4096}));
+    if (nt == 1) {
+        f(int64_t{0}, n);
+        return;
+    }
+    std::vector<std::thread> th;
+    for (int64_t t = 1; t < nt; ++t) th.emplace_back([&, t] { f(n * t / nt, n * (t + 1) / nt); });
+    f(int64_t{0}, n / nt);
+    for (std::thread& x : th) x.join();
+}
 
 // f64 host rows (stride k) <-> f32 padded rows (stride ld) with zero padding.
 void pack_rows_f32(const double* src, int64_t rows, int32_t k, int32_t ld, std::vector<float>& dst);

@@ -129,6 +129,7 @@ extern "C" void rs_close(rs_ctx* ctx) {
     if (ctx->k0) (void)hipEventDestroy(ctx->k0);
     if (ctx->k1) (void)hipEventDestroy(ctx->k1);
     ctx->svd_fit_cache.reset();  // a cached plan frees its device buffers on this device
+    ctx->staging.reset();
     delete ctx;
 }
 

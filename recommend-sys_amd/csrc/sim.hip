@@ -22,7 +22,9 @@
 
 #include <algorithm>
 #include <cmath>
+#include <atomic>
 #include <cstdlib>
+#include <cstring>
 #include <limits>
 #include <numeric>
 #include <vector>
@@ -86,7 +88,7 @@ __device__ __forceinline__ void lds_barrier() {
     __builtin_amdgcn_s_barrier();
 }
 
-template <int KIND>
+template <int KIND, int PIPE>
 __global__ __launch_bounds__(256) void knn_sims_mfma_kernel(const int8_t* __restrict__ X,
                                                             int64_t ldk, int32_t L,
                                                             const int2* __restrict__ tiles,
@@ -158,6 +160,9 @@ __global__ __launch_bounds__(256) void knn_sims_mfma_kernel(const int8_t* __rest
         const int8_t* b = smem + buf * kStageBytes;
 #pragma unroll
         for (int s = 0; s < 2; ++s) {
+            if constexpr (PIPE) {
+                if (s == 1) break;
+            }
             i32x4 fa[3][2], fb[3][2];
 #pragma unroll
             for (int m = 0; m < 3; ++m)
@@ -185,6 +190,84 @@ __global__ __launch_bounds__(256) void knn_sims_mfma_kernel(const int8_t* __rest
         }
     };
 
+    // One K step of the software pipeline (PIPE): all 24 fragment reads up front, then the MFMAs
+    // of both 32-deep halves with the next step's X2 / M derivation and staging writes woven
+    // between them.  One wave per SIMD (192 accumulator AGPRs) cannot hide the VALU, LDS and MFMA
+    // phases behind other waves, so the wave has to overlap them itself: an MFMA occupies the
+    // matrix pipe for 32 cycles while the wave issues the independent VALU / LDS work behind it.
+    // The body is one basic block (the last step reloads its own chunk and stages it into the
+    // buffer nobody reads again), so the scheduler can apply the group pattern.
+    auto pipe_step = [&](int buf, i32x4 (&st)[kXPerThread]) {
+        const int8_t* b = smem + buf * kStageBytes;
+        int8_t* nb = smem + (buf ^ 1) * kStageBytes;  // last read in the previous step (barrier between)
+        i32x4 fa[2][3][2], fb[2][3][2];
+        auto read = [&](int s, int x) {  // fragment x of 12: matrix x >> 2, side (x >> 1) & 1, tile x & 1
+            const int m = x >> 2, side = (x >> 1) & 1, i = x & 1;
+            if (PIPE == 2 && m == 2) {  // M = [x > 0] of the X fragment read at the same place
+                i32x4& d = side ? fb[s][2][i] : fa[s][2][i];
+                const i32x4& src = side ? fb[s][0][i] : fa[s][0][i];
+#pragma unroll
+                for (int e = 0; e < 4; ++e) d[e] = static_cast<int>(mask_bytes(static_cast<uint32_t>(src[e])));
+            } else if (side) {
+                fb[s][m][i] = frag(b, m, 1, i, s);
+            } else {
+                fa[s][m][i] = frag(b, m, 0, i, s);
+            }
+        };
+        constexpr int NM = 4 * NC;  // MFMAs per half
+        auto mfma = [&](int s, int x) {  // x = c * 4 + i * 2 + j
+            const int c = x >> 2, i = (x >> 1) & 1, j = x & 1;
+            // operands per contraction c: Cosine/MSD (X,X) (X2,M) (M,X2) (M,M); SlopeOne (X,M) (M,X) (M,M)
+            const int ma = KIND == 2 ? (c == 0 ? 0 : 2) : (c == 0 ? 0 : c == 1 ? 1 : 2);
+            const int mb = KIND == 2 ? (c == 1 ? 0 : 2) : (c == 0 ? 0 : c == 1 ? 2 : c == 2 ? 1 : 2);
+            acc[c][i][j] = __builtin_amdgcn_mfma_i32_32x32x32_i8(fa[s][ma][i], fb[s][mb][j], acc[c][i][j], 0, 0, 0);
+        };
+        i32x4 sq[kXPerThread], mk[kXPerThread];
+        auto stage = [&](int x) {  // slice x of the next step's staging (x in [0, NM))
+            constexpr int per = (3 * kXPerThread + NM - 1) / NM;  // (chunk, part) units per slice
+#pragma unroll
+            for (int u = 0; u < per; ++u) {
+                const int w = x * per + u;
+                if (w >= 3 * kXPerThread) break;
+                const int j = w / 3, part = w % 3;
+                if (part == 0) {
+                    *reinterpret_cast<i32x4*>(nb + dst[j]) = st[j];
+                } else if (part == 1) {
+                    if constexpr (KIND != 2) {
+#pragma unroll
+                        for (int d = 0; d < 4; ++d) sq[j][d] = static_cast<int>(sq_bytes(static_cast<uint32_t>(st[j][d])));
+                        *reinterpret_cast<i32x4*>(nb + 1 * 2 * kStageMat + dst[j]) = sq[j];
+                    }
+                } else if (PIPE != 2) {  // PIPE 2 derives M from the X fragments instead
+#pragma unroll
+                    for (int d = 0; d < 4; ++d) mk[j][d] = static_cast<int>(mask_bytes(static_cast<uint32_t>(st[j][d])));
+                    *reinterpret_cast<i32x4*>(nb + 2 * 2 * kStageMat + dst[j]) = mk[j];
+                }
+            }
+        };
+        // half 0's fragments; then its MFMAs, each followed by one of half 1's fragment reads;
+        // then half 1's MFMAs, each followed by a slice of the next step's X2 / M derivation and
+        // staging writes.  sched_barrier(0) keeps this order: an MFMA holds the matrix pipe for 32
+        // cycles while the wave issues the independent LDS / VALU work behind it.
+        // (PIPE 2: half 0's M fragments are derived behind its first four MFMAs, the X X^T ones)
+#pragma unroll
+        for (int x = 0; x < (PIPE == 2 ? 8 : 12); ++x) read(0, x);
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int x = 0; x < NM; ++x) {
+            mfma(0, x);
+            if (PIPE == 2 && x < 4) read(0, 8 + x);
+            if (x < 12) read(1, x);
+            __builtin_amdgcn_sched_barrier(0);
+        }
+#pragma unroll
+        for (int x = 0; x < NM; ++x) {
+            mfma(1, x);
+            stage(x);
+            __builtin_amdgcn_sched_barrier(0);
+        }
+    };
+
     // the next step's X loads are in flight during this step's MFMAs (a second set in flight
     // spills: 153 VGPRs, 3x slower -- measured)
     const int64_t nsteps = ldk / kKBlock;
@@ -192,12 +275,21 @@ __global__ __launch_bounds__(256) void knn_sims_mfma_kernel(const int8_t* __rest
     gload(st, 0);
     lstore(st, 0);
     lds_barrier();
-    for (int64_t step = 0; step < nsteps; ++step) {
-        const int buf = static_cast<int>(step & 1);
-        if (step + 1 < nsteps) gload(st, (step + 1) * kKBlock);
-        compute(buf);
-        if (step + 1 < nsteps) lstore(st, buf ^ 1);  // buf ^ 1 was last read in step - 1
-        lds_barrier();
+    if constexpr (PIPE) {
+        for (int64_t step = 0; step < nsteps; ++step) {
+            const int buf = static_cast<int>(step & 1);
+            gload(st, std::min<int64_t>(step + 1, nsteps - 1) * kKBlock);
+            pipe_step(buf, st);
+            lds_barrier();
+        }
+    } else {
+        for (int64_t step = 0; step < nsteps; ++step) {
+            const int buf = static_cast<int>(step & 1);
+            if (step + 1 < nsteps) gload(st, (step + 1) * kKBlock);
+            compute(buf);
+            if (step + 1 < nsteps) lstore(st, buf ^ 1);  // buf ^ 1 was last read in step - 1
+            lds_barrier();
+        }
     }
     if (!live) return;
     const int32_t r0 = ta * kTile + 64 * wa;  // left rows (a)
@@ -250,17 +342,25 @@ __global__ __launch_bounds__(256) void knn_sims_mfma_kernel(const int8_t* __rest
 
 // Upper-triangle tiles (ta <= tb < T) in 16 x 16 super-tile groups, super-tiles column-major
 // (measured on the ML-20M shape: 10 % less time than plain column-major order; an XCD-striped
-// variant of the groups was slower).
-static std::vector<int2> tile_order(int32_t T) {
-    constexpr int32_t G = 16;
+// variant of the groups was slower).  The super-tile columns run from the last to the first:
+// once every column group >= g is done, the rows of group g are complete (their entries right of
+// the diagonal come from tiles (r, tb >= r), those left of it from the mirrored tiles (ta, r) of
+// group g itself), which is what the streamed download (sims_streamed) relies on.  group_off[j]
+// is the first tile of column group NS - 1 - j; group_off[NS] = the tile count.
+constexpr int32_t kGroup = 16;
+static std::vector<int2> tile_order(int32_t T, std::vector<size_t>* group_off = nullptr) {
     std::vector<int2> t;
     t.reserve(static_cast<size_t>(T) * (T + 1) / 2);
-    const int32_t NS = (T + G - 1) / G;
-    for (int32_t sj = 0; sj < NS; ++sj)
+    const int32_t NS = (T + kGroup - 1) / kGroup;
+    if (group_off) group_off->clear();
+    for (int32_t sj = NS - 1; sj >= 0; --sj) {
+        if (group_off) group_off->push_back(t.size());
         for (int32_t si = 0; si <= sj; ++si)
-            for (int32_t b = sj * G; b < std::min(T, (sj + 1) * G); ++b)
-                for (int32_t a = si * G; a < std::min(T, (si + 1) * G); ++a)
+            for (int32_t b = sj * kGroup; b < std::min(T, (sj + 1) * kGroup); ++b)
+                for (int32_t a = si * kGroup; a < std::min(T, (si + 1) * kGroup); ++a)
                     if (a <= b) t.push_back(make_int2(a, b));
+    }
+    if (group_off) group_off->push_back(t.size());
     return t;
 }
 
@@ -391,56 +491,213 @@ struct SortedRows {
     std::vector<double> r;
 };
 
-// data.go:236-243 sorts(): each row ID-ascending (stable, so duplicates keep data order)
+// data.go:236-243 sorts(): each row ID-ascending (stable, so duplicates keep data order).  Rows
+// already in order are copied as they are; rows are independent, so host threads split them.
 static void sort_rows(int32_t L, const int64_t* rowptr, const int32_t* ids, const double* r,
                       SortedRows& out) {
     out.rowptr.assign(rowptr, rowptr + L + 1);
     const int64_t nnz = rowptr[L] - rowptr[0];
     out.ids.resize(nnz);
     out.r.resize(nnz);
-    std::vector<int64_t> idx;
-    for (int32_t a = 0; a < L; ++a) {
-        const int64_t b = rowptr[a], e = rowptr[a + 1];
-        idx.resize(e - b);
-        std::iota(idx.begin(), idx.end(), b);
-        std::stable_sort(idx.begin(), idx.end(), [&](int64_t x, int64_t y) { return ids[x] < ids[y]; });
-        for (int64_t t = b; t < e; ++t) {
-            out.ids[t - rowptr[0]] = ids[idx[t - b]];
-            out.r[t - rowptr[0]] = r[idx[t - b]];
+    const int64_t o = rowptr[0];
+    parallel_ranges(L, 16, [&](int64_t a0, int64_t a1) {
+        std::vector<int64_t> idx;
+        for (int64_t a = a0; a < a1; ++a) {
+            const int64_t b = rowptr[a], e = rowptr[a + 1];
+            if (std::is_sorted(ids + b, ids + e)) {
+                std::copy(ids + b, ids + e, out.ids.begin() + (b - o));
+                std::copy(r + b, r + e, out.r.begin() + (b - o));
+                continue;
+            }
+            idx.resize(e - b);
+            std::iota(idx.begin(), idx.end(), b);
+            std::stable_sort(idx.begin(), idx.end(), [&](int64_t x, int64_t y) { return ids[x] < ids[y]; });
+            for (int64_t t = b; t < e; ++t) {
+                out.ids[t - o] = ids[idx[t - b]];
+                out.r[t - o] = r[idx[t - b]];
+            }
         }
-    }
-    for (auto& p : out.rowptr) p -= rowptr[0];
+    });
+    for (auto& p : out.rowptr) p -= o;
 }
 
 // ratings exactly x / s, s in {1, 2}, |x| <= 11, and no repeated id inside a row -> MFMA path
-static int int8_scale(const SortedRows& sr) {
-    for (int s = 1; s <= 2; ++s) {
-        bool ok = true;
-        for (double v : sr.r) {
-            const double x = v * s;
+static bool scale_ok(const SortedRows& sr, int s) {
+    const int64_t n = static_cast<int64_t>(sr.r.size());
+    std::atomic<bool> any{false};
+    parallel_ranges(n, 16, [&](int64_t t0, int64_t t1) {
+        for (int64_t t = t0; t < t1 && !any.load(std::memory_order_relaxed); ++t) {
+            const double x = sr.r[t] * s;
             if (!(x == std::floor(x)) || x < 1.0 || x > 11.0) {  // 0 marks "not rated"
-                ok = false;
-                break;
+                any.store(true, std::memory_order_relaxed);
+                return;
             }
         }
-        if (ok) return s;
-    }
+    });
+    return !any.load();
+}
+static int int8_scale(const SortedRows& sr) {
+    for (int s = 1; s <= 2; ++s)
+        if (scale_ok(sr, s)) return s;
     return 0;
 }
 
 static bool has_repeats(int32_t L, const SortedRows& sr) {
-    for (int32_t a = 0; a < L; ++a)
-        for (int64_t t = sr.rowptr[a] + 1; t < sr.rowptr[a + 1]; ++t)
-            if (sr.ids[t] == sr.ids[t - 1]) return true;
-    return false;
+    std::atomic<bool> any{false};
+    parallel_ranges(L, 16, [&](int64_t a0, int64_t a1) {
+        for (int64_t a = a0; a < a1 && !any.load(std::memory_order_relaxed); ++a)
+            for (int64_t t = sr.rowptr[a] + 1; t < sr.rowptr[a + 1]; ++t)
+                if (sr.ids[t] == sr.ids[t - 1]) {
+                    any.store(true, std::memory_order_relaxed);
+                    return;
+                }
+    });
+    return any.load();
 }
 
-static void sims_device(rs_ctx* ctx, int32_t kind, int32_t L, int32_t R, const SortedRows& sr,
-                        bool allow_mfma, DevBuf<double>& dS, int32_t part = 0, int32_t n_parts = 1) {
+// ---------------------------------------------------------------------------------------------
+// Streamed download of the MFMA path's Sims (rs_knn_sims, one part).  The tiles run as one launch
+// per super-tile column group, last group first, alternating over two streams (the groups write
+// disjoint entries, so consecutive launches overlap at their tails); after groups >= g are done,
+// the rows of group g are complete (tile_order) and the copy engine moves them, in chunks of whole
+// rows, into a pinned ring held by the ctx while the next groups compute.  Host threads copy each
+// chunk from the ring into the caller's buffer as its DMA completes.  Only the first group's rows
+// (the last to finish) are exposed after the kernels.
+constexpr int kDlSlots = 16;
+constexpr size_t kDlSlotBytes = size_t(16) << 20;
+constexpr int kDlWorkers = 8;
+
+static uint8_t* ctx_staging(rs_ctx* ctx) {
+    if (!ctx->staging) {
+        void* p = nullptr;
+        RS_HIP(hipHostMalloc(&p, kDlSlots * kDlSlotBytes, hipHostMallocDefault));
+        ctx->staging = std::shared_ptr<void>(p, [](void* q) { (void)hipHostFree(q); });
+    }
+    return static_cast<uint8_t*>(ctx->staging.get());
+}
+
+struct StreamSet {  // per-call streams and events, released on every path
+    std::vector<hipStream_t> st;
+    std::vector<hipEvent_t> ev;
+    ~StreamSet() {
+        for (hipStream_t s : st) {
+            (void)hipStreamSynchronize(s);
+            (void)hipStreamDestroy(s);
+        }
+        for (hipEvent_t e : ev) (void)hipEventDestroy(e);
+    }
+    hipStream_t stream() {
+        hipStream_t s;
+        RS_HIP(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
+        st.push_back(s);
+        return s;
+    }
+    hipEvent_t event() {
+        hipEvent_t e;
+        RS_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+        ev.push_back(e);
+        return e;
+    }
+};
+
+template <typename Launch>
+static void sims_streamed(rs_ctx* ctx, int32_t L, const std::vector<size_t>& group_off, Launch launch,
+                          const double* dS, double* host) {
+    const int32_t NG = static_cast<int32_t>(group_off.size()) - 1;
+    const int64_t group_rows = static_cast<int64_t>(kGroup) * kTile;
+    StreamSet ss;
+    hipStream_t sA = ctx->stream, sB = ss.stream(), sC = ss.stream();
+    std::vector<hipEvent_t> ev_g(NG);
+    for (auto& e : ev_g) e = ss.event();
+    hipEvent_t ev_b = ss.event();
+    kernel_span_begin(ctx);
+    RS_HIP(hipStreamWaitEvent(sB, ctx->k0, 0));
+    for (int32_t j = 0; j < NG; ++j) {  // launch j = column group NG - 1 - j
+        hipStream_t s = (j & 1) ? sB : sA;
+        launch(group_off[j], group_off[j + 1] - group_off[j], s);
+        RS_HIP(hipEventRecord(ev_g[NG - 1 - j], s));
+    }
+    RS_HIP(hipEventRecord(ev_b, sB));
+    RS_HIP(hipStreamWaitEvent(sA, ev_b, 0));
+    (void)hipEventRecord(ctx->k1, sA);
+
+    // chunks of whole rows, never crossing a group: groups NG-1 .. 0, rows ascending within
+    struct Chunk { int64_t row0, rows; int32_t group; };
+    std::vector<Chunk> chunks;
+    const int64_t row_bytes = static_cast<int64_t>(L) * sizeof(double);
+    const int64_t per = std::max<int64_t>(1, static_cast<int64_t>(kDlSlotBytes) / row_bytes);
+    for (int32_t g = NG - 1; g >= 0; --g) {
+        const int64_t r1 = std::min<int64_t>(L, (g + 1) * group_rows);
+        for (int64_t r = g * group_rows; r < r1; r += per) chunks.push_back({r, std::min(per, r1 - r), g});
+    }
+    uint8_t* ring = ctx_staging(ctx);
+    std::vector<hipEvent_t> ev_slot(kDlSlots);
+    for (auto& e : ev_slot) e = ss.event();
+    const int64_t NC = static_cast<int64_t>(chunks.size());
+    std::atomic<int64_t> issued{0};                       // chunks whose DMA is enqueued
+    std::vector<std::atomic<int64_t>> freed(kDlSlots);    // per slot: chunks copied out of it
+    for (auto& f : freed) f.store(0);
+    std::atomic<bool> failed{false};
+    const unsigned hw = std::max(1u, std::thread::hardware_concurrency());
+    const int W = static_cast<int>(std::min<unsigned>(kDlWorkers, hw));
+    auto worker = [&](int w) {
+        for (int64_t c = w; c < NC; c += W) {
+            while (issued.load(std::memory_order_acquire) <= c) {
+                if (failed.load()) return;
+                std::this_thread::yield();
+            }
+            const int slot = static_cast<int>(c % kDlSlots);
+            if (hipEventSynchronize(ev_slot[slot]) != hipSuccess) {
+                failed.store(true);
+                return;
+            }
+            std::memcpy(host + chunks[c].row0 * L, ring + slot * kDlSlotBytes,
+                        static_cast<size_t>(chunks[c].rows * row_bytes));
+            freed[slot].store(c / kDlSlots + 1, std::memory_order_release);
+        }
+    };
+    std::vector<std::thread> th;
+    for (int w = 0; w < W; ++w) th.emplace_back(worker, w);
+    std::string err;
+    try {
+        int32_t waited = NG;
+        for (int64_t c = 0; c < NC; ++c) {
+            const int slot = static_cast<int>(c % kDlSlots);
+            while (freed[slot].load(std::memory_order_acquire) < c / kDlSlots) {
+                if (failed.load()) throw HipError{hipErrorUnknown, "streamed download: event wait failed"};
+                std::this_thread::yield();
+            }
+            const int32_t g = chunks[c].group;
+            if (g < waited) {  // every group >= g is done: its own event and the next group's
+                RS_HIP(hipStreamWaitEvent(sC, ev_g[g], 0));
+                if (g + 1 < NG) RS_HIP(hipStreamWaitEvent(sC, ev_g[g + 1], 0));
+                waited = g;
+            }
+            RS_HIP(hipMemcpyAsync(ring + slot * kDlSlotBytes, dS + chunks[c].row0 * L,
+                                  static_cast<size_t>(chunks[c].rows * row_bytes), hipMemcpyDeviceToHost, sC));
+            RS_HIP(hipEventRecord(ev_slot[slot], sC));
+            issued.store(c + 1, std::memory_order_release);
+        }
+    } catch (const HipError& e) {
+        failed.store(true);
+        err = e.what;
+    }
+    for (std::thread& x : th) x.join();
+    if (!err.empty() || failed.load()) throw HipError{hipErrorUnknown, err.empty() ? "streamed download failed" : err};
+    float ms = 0.f;
+    if (hipEventSynchronize(ctx->k1) == hipSuccess && hipEventElapsedTime(&ms, ctx->k0, ctx->k1) == hipSuccess)
+        ctx->last_kernel_ms = ms;
+}
+
+// Returns true when the Sims already reached `host` (the streamed MFMA path, one part only);
+// otherwise they are in dS for the caller to copy.
+static bool sims_device(rs_ctx* ctx, int32_t kind, int32_t L, int32_t R, const SortedRows& sr,
+                        bool allow_mfma, DevBuf<double>& dS, int32_t part = 0, int32_t n_parts = 1,
+                        double* host = nullptr) {
     hipStream_t s = ctx->stream;
     const int64_t nnz = static_cast<int64_t>(sr.ids.size());
     dS.alloc(std::max<int64_t>(1, static_cast<int64_t>(L) * L));
-    if (L == 0) return;
+    if (L == 0) return false;
     const int scale = (kind != RS_SIM_PEARSON && allow_mfma && !has_repeats(L, sr)) ? int8_scale(sr) : 0;
     DevBuf<int64_t> drow(sr.rowptr.size());
     DevBuf<int32_t> dids(std::max<int64_t>(1, nnz));
@@ -450,7 +707,9 @@ static void sims_device(rs_ctx* ctx, int32_t kind, int32_t L, int32_t R, const S
         const int64_t ldk = ((static_cast<int64_t>(R) + kKBlock - 1) / kKBlock) * kKBlock;
         const int64_t Lp = ((static_cast<int64_t>(L) + kTile - 1) / kTile) * kTile;
         std::vector<int8_t> hx(nnz);
-        for (int64_t t = 0; t < nnz; ++t) hx[t] = static_cast<int8_t>(sr.r[t] * scale);
+        parallel_ranges(nnz, 16, [&](int64_t t0, int64_t t1) {
+            for (int64_t t = t0; t < t1; ++t) hx[t] = static_cast<int8_t>(sr.r[t] * scale);
+        });
         DevBuf<int8_t> dx(std::max<int64_t>(1, nnz));
         dx.upload(hx.data(), nnz, s);
         DevBuf<int8_t> X(Lp * ldk);
@@ -460,38 +719,57 @@ static void sims_device(rs_ctx* ctx, int32_t kind, int32_t L, int32_t R, const S
         RS_HIP(hipGetLastError());
         RS_HIP(hipStreamSynchronize(s));
         const int32_t T = static_cast<int32_t>(Lp / kTile);
-        std::vector<int2> order = tile_order(T);
+        std::vector<size_t> group_off;
+        std::vector<int2> order = tile_order(T, &group_off);
         if (n_parts > 1) {
             std::vector<int2> mine;
             for (const int2& t : order)
                 if (part_owns(t.x, part, n_parts)) mine.push_back(t);
             order.swap(mine);
-            if (order.empty()) return;
+            if (order.empty()) return false;
         }
         DevBuf<int2> dtiles(order.size());
         dtiles.upload(order.data(), order.size(), s);
         // Cosine / MSD scale the sums by 1 / s^2; SlopeOne's differences by 1 / s
         const double inv_s2 = kind == RS_DEV_SLOPE_ONE ? 1.0 / scale : 1.0 / static_cast<double>(scale * scale);
         const size_t lds = 2 * kStageBytes;
-        RS_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(&knn_sims_mfma_kernel<0>),
-                                   hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(lds)));
-        RS_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(&knn_sims_mfma_kernel<1>),
-                                   hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(lds)));
-        RS_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(&knn_sims_mfma_kernel<2>),
-                                   hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(lds)));
+        // K loop: 0 = round 1 (phases in sequence), 1 = software pipeline, 2 = pipeline with M
+        // derived from the X fragments in registers (one staged matrix less)
+        const char* pipe_env = std::getenv("RSGPU_KNN_PIPE");
+        const int pipe = (pipe_env && pipe_env[0] >= '0' && pipe_env[0] <= '2') ? pipe_env[0] - '0' : 1;
+        for (const void* f : {reinterpret_cast<const void*>(&knn_sims_mfma_kernel<0, 0>),
+                              reinterpret_cast<const void*>(&knn_sims_mfma_kernel<1, 0>),
+                              reinterpret_cast<const void*>(&knn_sims_mfma_kernel<2, 0>),
+                              reinterpret_cast<const void*>(&knn_sims_mfma_kernel<0, 1>),
+                              reinterpret_cast<const void*>(&knn_sims_mfma_kernel<1, 1>),
+                              reinterpret_cast<const void*>(&knn_sims_mfma_kernel<2, 1>),
+                              reinterpret_cast<const void*>(&knn_sims_mfma_kernel<0, 2>),
+                              reinterpret_cast<const void*>(&knn_sims_mfma_kernel<1, 2>),
+                              reinterpret_cast<const void*>(&knn_sims_mfma_kernel<2, 2>)})
+            RS_HIP(hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(lds)));
+        auto launch = [&](size_t first, size_t count, hipStream_t st) {
+            if (!count) return;
+            const dim3 grid(static_cast<uint32_t>(count));
+            auto go = [&](auto kern) {
+                hipLaunchKernelGGL(kern, grid, dim3(256), lds, st, X.p, ldk, L, dtiles.p + first, inv_s2, dS.p);
+            };
+            auto by_pipe = [&](auto k0, auto k1, auto k2) { pipe == 0 ? go(k0) : pipe == 1 ? go(k1) : go(k2); };
+            if (kind == RS_SIM_COSINE)
+                by_pipe(knn_sims_mfma_kernel<0, 0>, knn_sims_mfma_kernel<0, 1>, knn_sims_mfma_kernel<0, 2>);
+            else if (kind == RS_SIM_MSD)
+                by_pipe(knn_sims_mfma_kernel<1, 0>, knn_sims_mfma_kernel<1, 1>, knn_sims_mfma_kernel<1, 2>);
+            else
+                by_pipe(knn_sims_mfma_kernel<2, 0>, knn_sims_mfma_kernel<2, 1>, knn_sims_mfma_kernel<2, 2>);
+            RS_HIP(hipGetLastError());
+        };
+        if (host && n_parts == 1) {
+            sims_streamed(ctx, L, group_off, launch, dS.p, host);
+            return true;
+        }
         kernel_span_begin(ctx);
-        if (kind == RS_SIM_COSINE)
-            hipLaunchKernelGGL(knn_sims_mfma_kernel<0>, dim3(order.size()), dim3(256), lds, s, X.p,
-                               ldk, L, dtiles.p, inv_s2, dS.p);
-        else if (kind == RS_SIM_MSD)
-            hipLaunchKernelGGL(knn_sims_mfma_kernel<1>, dim3(order.size()), dim3(256), lds, s, X.p,
-                               ldk, L, dtiles.p, inv_s2, dS.p);
-        else
-            hipLaunchKernelGGL(knn_sims_mfma_kernel<2>, dim3(order.size()), dim3(256), lds, s, X.p,
-                               ldk, L, dtiles.p, inv_s2, dS.p);
-        RS_HIP(hipGetLastError());
+        launch(0, order.size(), s);
         kernel_span_end(ctx);
-        return;
+        return false;
     }
     DevBuf<double> dr(std::max<int64_t>(1, nnz)), dmean(L);
     dr.upload(sr.r.data(), nnz, s);
@@ -500,7 +778,7 @@ static void sims_device(rs_ctx* ctx, int32_t kind, int32_t L, int32_t R, const S
     std::vector<int32_t> rows;
     for (int32_t a = 0; a < L; ++a)
         if (n_parts == 1 || part_owns(a / kTile, part, n_parts)) rows.push_back(a);
-    if (rows.empty()) return;
+    if (rows.empty()) return false;
     DevBuf<int32_t> drows(rows.size());
     drows.upload(rows.data(), rows.size(), s);
     const int32_t n_rows = static_cast<int32_t>(rows.size());
@@ -520,6 +798,7 @@ static void sims_device(rs_ctx* ctx, int32_t kind, int32_t L, int32_t R, const S
         hipLaunchKernelGGL(sims_merge_kernel<3>, dim3(grid), dim3(256), 0, s, L, R, drow.p, dids.p, dr.p, dmean.p, scratch.p, scratch_has.p, dS.p, drows.p, n_rows);
     RS_HIP(hipGetLastError());
     kernel_span_end(ctx);
+    return false;
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -671,9 +950,12 @@ extern "C" int rs_knn_sims_part(rs_ctx* ctx, int32_t kind, int32_t n_left, int32
         rs::sort_rows(n_left, rowptr, ids, ratings, sr);
         rs::DevBuf<double> dS;
         const char* env = std::getenv("RSGPU_KNN_NO_MFMA");
-        rs::sims_device(ctx, kind, n_left, n_right, sr, !(env && env[0] == '1'), dS, part, n_parts);
+        const char* nostream = std::getenv("RSGPU_KNN_NO_STREAM");  // A/B switch: one launch, one copy
+        const bool done = rs::sims_device(ctx, kind, n_left, n_right, sr, !(env && env[0] == '1'), dS, part,
+                                          n_parts, (nostream && nostream[0] == '1') ? nullptr : sims);
         hipStream_t s = ctx->stream;
-        if (n_parts == 1) {
+        if (done) {
+        } else if (n_parts == 1) {
             dS.download(sims, static_cast<int64_t>(n_left) * n_left, s);
         } else {  // the part's rows from their diagonal block rightwards, and the mirrored columns
             const size_t pitch = static_cast<size_t>(n_left) * sizeof(double);

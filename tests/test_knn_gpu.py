@@ -187,3 +187,35 @@ def test_knn_plan_predict_bitwise(ctx, ml100k, kind, user_based):
             ref = O.knn_predict(t, S, rrp, rids, rr, means, stds, bias, gm, k, mink, ql, qr)
             assert bitwise_equal(got, ref), (name, k, mink)
     plan.close()
+
+
+@pytest.mark.parametrize("kind", [rsgpu.SIM_COSINE, rsgpu.SIM_MSD, rsgpu.DEV_SLOPE_ONE])
+def test_knn_streamed_download_multi_group(ctx, kind, monkeypatch):
+    """rs_knn_sims streams the Sims to the host while later column groups still compute (one launch
+    per 2048-row super-tile column group, rows copied as their groups complete).  With L = 4700
+    (3 groups, a ragged last block) the streamed result equals, bit for bit: the device plan's
+    one-launch Sims, the same call with the round-1 K loop (RSGPU_KNN_PIPE=0) and without streaming
+    (RSGPU_KNN_NO_STREAM=1), and the oracle's restatement (knn.go:190-216) on rows from every group."""
+    rng = np.random.default_rng(11)
+    L, R, nnz = 4700, 900, 120_000
+    left = rng.integers(0, L, nnz)
+    right = rng.integers(0, R, nnz)
+    key = np.unique(left.astype(np.int64) * R + right)  # no repeated (left, right) pair
+    left, right = (key // R).astype(np.int32), (key % R).astype(np.int32)
+    perm = rng.permutation(len(key))                     # rows arrive unsorted by id
+    left, right = left[perm], right[perm]
+    r = rng.integers(1, 11, len(key)) / 2.0              # half stars: the s = 2 int8 path
+    rowptr, ids, rr = O.csr_by(left, L, right, r)
+    S = ctx.knn_sims(kind, rowptr, ids, rr, R)
+    plan = ctx.knn_plan(kind, rowptr, ids, rr, R)
+    assert bitwise_equal(S, plan.sims())
+    plan.close()
+    monkeypatch.setenv("RSGPU_KNN_NO_STREAM", "1")
+    monkeypatch.setenv("RSGPU_KNN_PIPE", "0")
+    assert bitwise_equal(S, ctx.knn_sims(kind, rowptr, ids, rr, R))
+    if kind == rsgpu.DEV_SLOPE_ONE:
+        return  # the dev matrix is pinned against slope_one.go in test_slope_one_gpu.py
+    srt = np.lexsort((ids, np.repeat(np.arange(L), np.diff(rowptr))))
+    for a0 in (0, 2040, 4090, 4690):
+        ref = O.knn_sims_rows(kind, rowptr, ids[srt], rr[srt], a0, min(L, a0 + 10))
+        assert bitwise_equal(S[a0:a0 + 10], ref), a0
