@@ -23,6 +23,8 @@
 #include <algorithm>
 #include <cmath>
 #include <atomic>
+#include <chrono>
+#include <cstdio>
 #include <cstdlib>
 #include <cstring>
 #include <limits>
@@ -69,7 +71,6 @@ constexpr int kRowPad = 64;                             // bytes per staged row
 constexpr int kStageMat = kTile * kRowPad;              // one matrix, one side
 constexpr int kStageBytes = 3 * 2 * kStageMat;          // X, X2, M for A and B
 constexpr int kXChunks = 2 * kTile * (kKBlock / 16);    // 16-byte X chunks per step (A and B)
-constexpr int kXPerThread = kXChunks / 256;
 
 typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
 
@@ -88,32 +89,41 @@ __device__ __forceinline__ void lds_barrier() {
     __builtin_amdgcn_s_barrier();
 }
 
-template <int KIND, int PIPE>
-__global__ __launch_bounds__(256) void knn_sims_mfma_kernel(const int8_t* __restrict__ X,
+// NWJ = 32-column MFMA tiles per wave along b: 2 -> four waves of 64 x 64 (one wave per SIMD,
+// 192 accumulator AGPRs); 1 -> eight waves of 64 x 32 (two waves per SIMD, 96 AGPRs each, so the
+// SIMD interleaves two waves' phases; PIPE 2 only).
+template <int KIND, int PIPE, int NWJ = 2>
+__global__ __launch_bounds__(NWJ == 2 ? 256 : 512) void knn_sims_mfma_kernel(const int8_t* __restrict__ X,
                                                             int64_t ldk, int32_t L,
                                                             const int2* __restrict__ tiles,
                                                             double inv_s2, double* __restrict__ S) {
     constexpr int NC = KIND == 1 ? 4 : 3;
+    static_assert(NWJ == 2 || PIPE == 2, "the eight-wave tiling exists for the PIPE 2 loop only");
+    constexpr int NT = NWJ == 2 ? 256 : 512;      // threads
+    constexpr int kXPerThread = kXChunks / NT;    // 16-byte X chunks staged per thread and step
+    constexpr int FPM = 2 + NWJ;                  // fragments per matrix and half: 2 a-tiles, NWJ b-tiles
     extern __shared__ __attribute__((aligned(16))) int8_t smem[];
     const int2 tile = tiles[blockIdx.x];
     const int32_t ta = tile.x, tb = tile.y;
     const int tid = threadIdx.x;
     const int lane = tid & 63;
     const int wave = tid >> 6;
-    const int wa = wave >> 1, wb = wave & 1;
-    const bool live = !(ta == tb && wa > wb);  // strictly below the diagonal: its mirror covers it
+    const int wa = NWJ == 2 ? wave >> 1 : wave >> 2, wb = NWJ == 2 ? wave & 1 : wave & 3;
+    // strictly below the diagonal (a rows start at or after the b columns end): the mirror covers it
+    const bool live = !(ta == tb && 64 * wa >= 32 * NWJ * (wb + 1));
     const int row = lane & 31, half = lane >> 5;
 
-    i32x16 acc[NC][2][2];
+    i32x16 acc[NC][2][NWJ];
 #pragma unroll
     for (int c = 0; c < NC; ++c)
 #pragma unroll
         for (int i = 0; i < 2; ++i)
 #pragma unroll
-            for (int j = 0; j < 2; ++j) acc[c][i][j] = i32x16{};
+            for (int j = 0; j < NWJ; ++j) acc[c][i][j] = i32x16{};
 
     // staging map: chunk j of thread tid = side j >> 1, row (tid >> 2) + 64 (j & 1), 16-byte
-    // column tid & 3 -- a wave-uniform base per (side, j) plus one 32-bit lane offset
+    // column tid & 3 -- a wave-uniform base per (side, j) plus one 32-bit lane offset (eight
+    // waves: chunk j = side j, row tid >> 2)
     const int8_t* baseA = X + static_cast<int64_t>(ta) * kTile * ldk;
     const int8_t* baseB = X + static_cast<int64_t>(tb) * kTile * ldk;
     const uint32_t loff = static_cast<uint32_t>((tid >> 2) * ldk + 16 * (tid & 3));
@@ -122,13 +132,14 @@ __global__ __launch_bounds__(256) void knn_sims_mfma_kernel(const int8_t* __rest
     int32_t dst[kXPerThread];
 #pragma unroll
     for (int j = 0; j < kXPerThread; ++j) {
-        const int side = j >> 1, r = r_lo + 64 * (j & 1), c = tid & 3;
+        const int side = NWJ == 2 ? j >> 1 : j, r = r_lo + (NWJ == 2 ? 64 * (j & 1) : 0), c = tid & 3;
         dst[j] = side * kStageMat + r * kRowPad + 16 * (c ^ ((r >> 2) & 3));
     }
     auto gload = [&](i32x4 (&st)[kXPerThread], int64_t k0) {
 #pragma unroll
         for (int j = 0; j < kXPerThread; ++j) {
-            const int8_t* base = ((j >> 1) ? baseB : baseA) + (j & 1) * half_rows + k0;
+            const int8_t* base = NWJ == 2 ? ((j >> 1) ? baseB : baseA) + (j & 1) * half_rows + k0
+                                          : (j ? baseB : baseA) + k0;
             st[j] = *reinterpret_cast<const i32x4*>(base + loff);
         }
     };
@@ -152,11 +163,12 @@ __global__ __launch_bounds__(256) void knn_sims_mfma_kernel(const int8_t* __rest
     // bytes [32 s + 16 half, +16) of its row -- the same k bijection for both operands, so
     // sum_k A[a][k] B[b][k] is exact whatever the MFMA's internal k order.
     auto frag = [&](const int8_t* b, int m, int side, int i, int s) {
-        const int r = (side ? 64 * wb : 64 * wa) + 32 * i + row;
+        const int r = (side ? 32 * NWJ * wb : 64 * wa) + 32 * i + row;
         const int c = (2 * s + half) ^ ((r >> 2) & 3);
         return *reinterpret_cast<const i32x4*>(b + (m * 2 + side) * kStageMat + r * kRowPad + 16 * c);
     };
     auto compute = [&](int buf) {
+        if constexpr (NWJ != 2) return;
         const int8_t* b = smem + buf * kStageBytes;
 #pragma unroll
         for (int s = 0; s < 2; ++s) {
@@ -200,9 +212,9 @@ __global__ __launch_bounds__(256) void knn_sims_mfma_kernel(const int8_t* __rest
     auto pipe_step = [&](int buf, i32x4 (&st)[kXPerThread]) {
         const int8_t* b = smem + buf * kStageBytes;
         int8_t* nb = smem + (buf ^ 1) * kStageBytes;  // last read in the previous step (barrier between)
-        i32x4 fa[2][3][2], fb[2][3][2];
-        auto read = [&](int s, int x) {  // fragment x of 12: matrix x >> 2, side (x >> 1) & 1, tile x & 1
-            const int m = x >> 2, side = (x >> 1) & 1, i = x & 1;
+        i32x4 fa[2][3][2], fb[2][3][NWJ];
+        auto read = [&](int s, int x) {  // fragment x of 3 FPM: matrix x / FPM, then a-tiles 0-1, b-tiles
+            const int m = x / FPM, r = x % FPM, side = r >= 2, i = side ? r - 2 : r;
             if (PIPE == 2 && m == 2) {  // M = [x > 0] of the X fragment read at the same place
                 i32x4& d = side ? fb[s][2][i] : fa[s][2][i];
                 const i32x4& src = side ? fb[s][0][i] : fa[s][0][i];
@@ -214,9 +226,9 @@ __global__ __launch_bounds__(256) void knn_sims_mfma_kernel(const int8_t* __rest
                 fa[s][m][i] = frag(b, m, 0, i, s);
             }
         };
-        constexpr int NM = 4 * NC;  // MFMAs per half
-        auto mfma = [&](int s, int x) {  // x = c * 4 + i * 2 + j
-            const int c = x >> 2, i = (x >> 1) & 1, j = x & 1;
+        constexpr int NM = 2 * NWJ * NC;  // MFMAs per half
+        auto mfma = [&](int s, int x) {  // x = (c * 2 + i) * NWJ + j
+            const int c = x / (2 * NWJ), i = (x / NWJ) & 1, j = x % NWJ;
             // operands per contraction c: Cosine/MSD (X,X) (X2,M) (M,X2) (M,M); SlopeOne (X,M) (M,X) (M,M)
             const int ma = KIND == 2 ? (c == 0 ? 0 : 2) : (c == 0 ? 0 : c == 1 ? 1 : 2);
             const int mb = KIND == 2 ? (c == 1 ? 0 : 2) : (c == 0 ? 0 : c == 1 ? 2 : c == 2 ? 1 : 2);
@@ -249,17 +261,27 @@ __global__ __launch_bounds__(256) void knn_sims_mfma_kernel(const int8_t* __rest
         // then half 1's MFMAs, each followed by a slice of the next step's X2 / M derivation and
         // staging writes.  sched_barrier(0) keeps this order: an MFMA holds the matrix pipe for 32
         // cycles while the wave issues the independent LDS / VALU work behind it.
-        // (PIPE 2: half 0's M fragments are derived behind its first four MFMAs, the X X^T ones)
+        // (PIPE 2: half 0's M fragments are derived behind its first four MFMAs, the X X^T ones;
+        // SlopeOne never reads X2 and its first contraction, X M^T, needs M at once)
+        // The late M fragments go b-side first: the second contraction (X2_a, M_b) needs them.
+        constexpr bool m_late = PIPE == 2 && KIND != 2;
+        constexpr int NF = 3 * FPM;
+        auto needed = [](int x) { return !(KIND == 2 && x / FPM == 1); };
+        auto late = [](int k) { return k < NWJ ? 2 * FPM + 2 + k : 2 * FPM + k - NWJ; };
 #pragma unroll
-        for (int x = 0; x < (PIPE == 2 ? 8 : 12); ++x) read(0, x);
+        for (int x = 0; x < NF; ++x)
+            if (needed(x) && !(m_late && x >= 2 * FPM)) read(0, x);
         __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
         for (int x = 0; x < NM; ++x) {
             mfma(0, x);
-            if (PIPE == 2 && x < 4) read(0, 8 + x);
-            if (x < 12) read(1, x);
+            if (m_late && x < FPM) read(0, late(x));
+            if (x < NF && needed(x)) read(1, x);
             __builtin_amdgcn_sched_barrier(0);
         }
+#pragma unroll
+        for (int x = NM; x < NF; ++x)
+            if (needed(x)) read(1, x);
 #pragma unroll
         for (int x = 0; x < NM; ++x) {
             mfma(1, x);
@@ -293,13 +315,13 @@ __global__ __launch_bounds__(256) void knn_sims_mfma_kernel(const int8_t* __rest
     }
     if (!live) return;
     const int32_t r0 = ta * kTile + 64 * wa;  // left rows (a)
-    const int32_t c0 = tb * kTile + 64 * wb;  // partner rows (b)
+    const int32_t c0 = tb * kTile + 32 * NWJ * wb;  // partner rows (b)
     // epilogue: C/D layout of 32x32 MFMA: col = lane & 31, row = (q & 3) + 8 (q >> 2) + 4 (lane >> 5)
     const double nan = __builtin_nan("");
 #pragma unroll
     for (int i = 0; i < 2; ++i)
 #pragma unroll
-        for (int j = 0; j < 2; ++j)
+        for (int j = 0; j < NWJ; ++j)
 #pragma unroll
             for (int q = 0; q < 16; ++q) {
                 const int32_t a = r0 + 32 * i + (q & 3) + 8 * (q >> 2) + 4 * half;
@@ -485,14 +507,41 @@ __global__ __launch_bounds__(256) void sims_merge_kernel(
 // ---------------------------------------------------------------------------------------------
 // host side
 
+// RSGPU_KNN_TRACE=1: host-side phase times of rs_knn_sims on stderr (end-to-end study)
+struct PhaseTrace {
+    bool on = std::getenv("RSGPU_KNN_TRACE") != nullptr;
+    std::chrono::steady_clock::time_point t = std::chrono::steady_clock::now();
+    void mark(const char* what) {
+        if (!on) return;
+        const auto t1 = std::chrono::steady_clock::now();
+        std::fprintf(stderr, "knn-trace %-12s %9.3f ms\n", what, std::chrono::duration<double, std::milli>(t1 - t).count());
+        t = t1;
+    }
+};
+static thread_local PhaseTrace* g_trace = nullptr;  // set for the duration of one traced rs_knn_sims_part call
+static void trace_mark(const char* what) {
+    if (g_trace) g_trace->mark(what);
+}
+
+// The left rows handed to the kernels: rowptr rebased to 0, and the ids / ratings either the
+// caller's own arrays (the MFMA path scatters them densely, so row order does not matter) or the
+// ID-sorted copies of sort_rows (the merge path walks them in order).  scale: the int8 path's s
+// (0 = not applicable), -1 = not decided yet.
 struct SortedRows {
     std::vector<int64_t> rowptr;
     std::vector<int32_t> ids;
     std::vector<double> r;
+    const int32_t* pid = nullptr;
+    const double* pr = nullptr;
+    int64_t nnz = 0;
+    int scale = -1;
+    void own() { pid = ids.data(); pr = r.data(); nnz = static_cast<int64_t>(ids.size()); }
 };
 
 // data.go:236-243 sorts(): each row ID-ascending (stable, so duplicates keep data order).  Rows
-// already in order are copied as they are; rows are independent, so host threads split them.
+// already in order are copied as they are; the others sort 64-bit keys (id, position in the row),
+// which are unique, so the order is the stable one.  Host threads take row ranges of near-equal
+// rating counts.
 static void sort_rows(int32_t L, const int64_t* rowptr, const int32_t* ids, const double* r,
                       SortedRows& out) {
     out.rowptr.assign(rowptr, rowptr + L + 1);
@@ -500,34 +549,47 @@ static void sort_rows(int32_t L, const int64_t* rowptr, const int32_t* ids, cons
     out.ids.resize(nnz);
     out.r.resize(nnz);
     const int64_t o = rowptr[0];
-    parallel_ranges(L, 16, [&](int64_t a0, int64_t a1) {
-        std::vector<int64_t> idx;
-        for (int64_t a = a0; a < a1; ++a) {
+    const unsigned hw = std::max(1u, std::thread::hardware_concurrency());
+    const int nt = static_cast<int>(std::max<int64_t>(1, std::min<int64_t>({16, hw, nnz / 65536 + 1})));
+    std::vector<int32_t> cut(nt + 1, L);
+    cut[0] = 0;
+    for (int t = 1; t < nt; ++t)
+        cut[t] = static_cast<int32_t>(std::lower_bound(rowptr, rowptr + L + 1, o + nnz * t / nt) - rowptr);
+    auto work = [&](int t) {
+        std::vector<uint64_t> key;
+        for (int64_t a = cut[t]; a < cut[t + 1]; ++a) {
             const int64_t b = rowptr[a], e = rowptr[a + 1];
             if (std::is_sorted(ids + b, ids + e)) {
                 std::copy(ids + b, ids + e, out.ids.begin() + (b - o));
                 std::copy(r + b, r + e, out.r.begin() + (b - o));
                 continue;
             }
-            idx.resize(e - b);
-            std::iota(idx.begin(), idx.end(), b);
-            std::stable_sort(idx.begin(), idx.end(), [&](int64_t x, int64_t y) { return ids[x] < ids[y]; });
-            for (int64_t t = b; t < e; ++t) {
-                out.ids[t - o] = ids[idx[t - b]];
-                out.r[t - o] = r[idx[t - b]];
+            key.resize(e - b);
+            for (int64_t x = b; x < e; ++x)  // ids are >= 0 (check_knn_csr)
+                key[x - b] = (static_cast<uint64_t>(static_cast<uint32_t>(ids[x])) << 32) | static_cast<uint64_t>(x - b);
+            std::sort(key.begin(), key.end());
+            for (int64_t x = b; x < e; ++x) {
+                const int64_t src = b + static_cast<int64_t>(key[x - b] & 0xFFFFFFFFu);
+                out.ids[x - o] = ids[src];
+                out.r[x - o] = r[src];
             }
         }
-    });
+    };
+    std::vector<std::thread> th;
+    for (int t = 1; t < nt; ++t) th.emplace_back(work, t);
+    work(0);
+    for (std::thread& x : th) x.join();
     for (auto& p : out.rowptr) p -= o;
+    out.own();
 }
 
 // ratings exactly x / s, s in {1, 2}, |x| <= 11, and no repeated id inside a row -> MFMA path
 static bool scale_ok(const SortedRows& sr, int s) {
-    const int64_t n = static_cast<int64_t>(sr.r.size());
+    const int64_t n = sr.nnz;
     std::atomic<bool> any{false};
     parallel_ranges(n, 16, [&](int64_t t0, int64_t t1) {
         for (int64_t t = t0; t < t1 && !any.load(std::memory_order_relaxed); ++t) {
-            const double x = sr.r[t] * s;
+            const double x = sr.pr[t] * s;
             if (!(x == std::floor(x)) || x < 1.0 || x > 11.0) {  // 0 marks "not rated"
                 any.store(true, std::memory_order_relaxed);
                 return;
@@ -542,17 +604,53 @@ static int int8_scale(const SortedRows& sr) {
     return 0;
 }
 
-static bool has_repeats(int32_t L, const SortedRows& sr) {
+// A repeated id inside a row (any row order): one bitmap of the right ids per host thread, marked
+// and cleared row by row.
+static bool has_repeats(int32_t L, int32_t R, const SortedRows& sr) {
     std::atomic<bool> any{false};
     parallel_ranges(L, 16, [&](int64_t a0, int64_t a1) {
-        for (int64_t a = a0; a < a1 && !any.load(std::memory_order_relaxed); ++a)
-            for (int64_t t = sr.rowptr[a] + 1; t < sr.rowptr[a + 1]; ++t)
-                if (sr.ids[t] == sr.ids[t - 1]) {
-                    any.store(true, std::memory_order_relaxed);
-                    return;
-                }
+        std::vector<uint64_t> seen((static_cast<size_t>(R) + 63) / 64, 0);
+        for (int64_t a = a0; a < a1 && !any.load(std::memory_order_relaxed); ++a) {
+            const int64_t b = sr.rowptr[a], e = sr.rowptr[a + 1];
+            int64_t t = b;
+            for (; t < e; ++t) {
+                const uint32_t id = static_cast<uint32_t>(sr.pid[t]);
+                const uint64_t bit = uint64_t{1} << (id & 63);
+                if (seen[id >> 6] & bit) break;
+                seen[id >> 6] |= bit;
+            }
+            for (int64_t x = b; x < t; ++x) seen[static_cast<uint32_t>(sr.pid[x]) >> 6] = 0;
+            if (t < e) {
+                any.store(true, std::memory_order_relaxed);
+                return;
+            }
+        }
     });
     return any.load();
+}
+
+// The rows for sims_device: the caller's arrays as they are when the int8 MFMA path applies
+// (Cosine / MSD / SlopeOne on x / s ratings without repeated ids), the ID-sorted copy otherwise.
+static void prepare_rows(int32_t kind, bool allow_mfma, int32_t L, int32_t R, const int64_t* rowptr,
+                         const int32_t* ids, const double* r, SortedRows& out) {
+    out.rowptr.assign(rowptr, rowptr + L + 1);
+    for (auto& p : out.rowptr) p -= rowptr[0];
+    out.pid = ids + rowptr[0];
+    out.pr = r + rowptr[0];
+    out.nnz = rowptr[L] - rowptr[0];
+    out.scale = 0;
+    if (kind != RS_SIM_PEARSON && allow_mfma) {
+        const int sc = int8_scale(out);
+        if (sc && !has_repeats(L, R, out)) {
+            out.scale = sc;
+            trace_mark("scale-check");
+            return;
+        }
+    }
+    trace_mark("scale-check");
+    sort_rows(L, rowptr, ids, r, out);
+    out.scale = 0;
+    trace_mark("sort");
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -695,20 +793,21 @@ static bool sims_device(rs_ctx* ctx, int32_t kind, int32_t L, int32_t R, const S
                         bool allow_mfma, DevBuf<double>& dS, int32_t part = 0, int32_t n_parts = 1,
                         double* host = nullptr) {
     hipStream_t s = ctx->stream;
-    const int64_t nnz = static_cast<int64_t>(sr.ids.size());
+    const int64_t nnz = sr.nnz;
     dS.alloc(std::max<int64_t>(1, static_cast<int64_t>(L) * L));
     if (L == 0) return false;
-    const int scale = (kind != RS_SIM_PEARSON && allow_mfma && !has_repeats(L, sr)) ? int8_scale(sr) : 0;
+    const int scale = sr.scale >= 0 ? sr.scale
+                    : (kind != RS_SIM_PEARSON && allow_mfma && !has_repeats(L, R, sr)) ? int8_scale(sr) : 0;
     DevBuf<int64_t> drow(sr.rowptr.size());
     DevBuf<int32_t> dids(std::max<int64_t>(1, nnz));
     drow.upload(sr.rowptr.data(), sr.rowptr.size(), s);
-    dids.upload(sr.ids.data(), nnz, s);
+    dids.upload(sr.pid, nnz, s);
     if (scale) {
         const int64_t ldk = ((static_cast<int64_t>(R) + kKBlock - 1) / kKBlock) * kKBlock;
         const int64_t Lp = ((static_cast<int64_t>(L) + kTile - 1) / kTile) * kTile;
         std::vector<int8_t> hx(nnz);
         parallel_ranges(nnz, 16, [&](int64_t t0, int64_t t1) {
-            for (int64_t t = t0; t < t1; ++t) hx[t] = static_cast<int8_t>(sr.r[t] * scale);
+            for (int64_t t = t0; t < t1; ++t) hx[t] = static_cast<int8_t>(sr.pr[t] * scale);
         });
         DevBuf<int8_t> dx(std::max<int64_t>(1, nnz));
         dx.upload(hx.data(), nnz, s);
@@ -718,6 +817,7 @@ static bool sims_device(rs_ctx* ctx, int32_t kind, int32_t L, int32_t R, const S
                            ldk, X.p);
         RS_HIP(hipGetLastError());
         RS_HIP(hipStreamSynchronize(s));
+        trace_mark("dense-X");
         const int32_t T = static_cast<int32_t>(Lp / kTile);
         std::vector<size_t> group_off;
         std::vector<int2> order = tile_order(T, &group_off);
@@ -735,8 +835,10 @@ static bool sims_device(rs_ctx* ctx, int32_t kind, int32_t L, int32_t R, const S
         const size_t lds = 2 * kStageBytes;
         // K loop: 0 = round 1 (phases in sequence), 1 = software pipeline, 2 = pipeline with M
         // derived from the X fragments in registers (one staged matrix less)
+        // K loop: 0 = round 1 (phases in sequence), 1 = software pipeline, 2 = pipeline with M
+        // derived in registers, 3 = PIPE 2 on eight waves (two per SIMD, 64 x 32 each; default)
         const char* pipe_env = std::getenv("RSGPU_KNN_PIPE");
-        const int pipe = (pipe_env && pipe_env[0] >= '0' && pipe_env[0] <= '2') ? pipe_env[0] - '0' : 1;
+        const int pipe = (pipe_env && pipe_env[0] >= '0' && pipe_env[0] <= '3') ? pipe_env[0] - '0' : 3;
         for (const void* f : {reinterpret_cast<const void*>(&knn_sims_mfma_kernel<0, 0>),
                               reinterpret_cast<const void*>(&knn_sims_mfma_kernel<1, 0>),
                               reinterpret_cast<const void*>(&knn_sims_mfma_kernel<2, 0>),
@@ -745,25 +847,35 @@ static bool sims_device(rs_ctx* ctx, int32_t kind, int32_t L, int32_t R, const S
                               reinterpret_cast<const void*>(&knn_sims_mfma_kernel<2, 1>),
                               reinterpret_cast<const void*>(&knn_sims_mfma_kernel<0, 2>),
                               reinterpret_cast<const void*>(&knn_sims_mfma_kernel<1, 2>),
-                              reinterpret_cast<const void*>(&knn_sims_mfma_kernel<2, 2>)})
+                              reinterpret_cast<const void*>(&knn_sims_mfma_kernel<2, 2>),
+                              reinterpret_cast<const void*>(&knn_sims_mfma_kernel<0, 2, 1>),
+                              reinterpret_cast<const void*>(&knn_sims_mfma_kernel<1, 2, 1>),
+                              reinterpret_cast<const void*>(&knn_sims_mfma_kernel<2, 2, 1>)})
             RS_HIP(hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(lds)));
         auto launch = [&](size_t first, size_t count, hipStream_t st) {
             if (!count) return;
             const dim3 grid(static_cast<uint32_t>(count));
-            auto go = [&](auto kern) {
-                hipLaunchKernelGGL(kern, grid, dim3(256), lds, st, X.p, ldk, L, dtiles.p + first, inv_s2, dS.p);
+            auto go = [&](auto kern, int threads) {
+                hipLaunchKernelGGL(kern, grid, dim3(threads), lds, st, X.p, ldk, L, dtiles.p + first, inv_s2, dS.p);
             };
-            auto by_pipe = [&](auto k0, auto k1, auto k2) { pipe == 0 ? go(k0) : pipe == 1 ? go(k1) : go(k2); };
+            auto by_pipe = [&](auto k0, auto k1, auto k2, auto k3) {
+                pipe == 0 ? go(k0, 256) : pipe == 1 ? go(k1, 256) : pipe == 2 ? go(k2, 256) : go(k3, 512);
+            };
             if (kind == RS_SIM_COSINE)
-                by_pipe(knn_sims_mfma_kernel<0, 0>, knn_sims_mfma_kernel<0, 1>, knn_sims_mfma_kernel<0, 2>);
+                by_pipe(knn_sims_mfma_kernel<0, 0>, knn_sims_mfma_kernel<0, 1>, knn_sims_mfma_kernel<0, 2>,
+                        knn_sims_mfma_kernel<0, 2, 1>);
             else if (kind == RS_SIM_MSD)
-                by_pipe(knn_sims_mfma_kernel<1, 0>, knn_sims_mfma_kernel<1, 1>, knn_sims_mfma_kernel<1, 2>);
+                by_pipe(knn_sims_mfma_kernel<1, 0>, knn_sims_mfma_kernel<1, 1>, knn_sims_mfma_kernel<1, 2>,
+                        knn_sims_mfma_kernel<1, 2, 1>);
             else
-                by_pipe(knn_sims_mfma_kernel<2, 0>, knn_sims_mfma_kernel<2, 1>, knn_sims_mfma_kernel<2, 2>);
+                by_pipe(knn_sims_mfma_kernel<2, 0>, knn_sims_mfma_kernel<2, 1>, knn_sims_mfma_kernel<2, 2>,
+                        knn_sims_mfma_kernel<2, 2, 1>);
             RS_HIP(hipGetLastError());
         };
         if (host && n_parts == 1) {
+            trace_mark("tiles");
             sims_streamed(ctx, L, group_off, launch, dS.p, host);
+            trace_mark("streamed");
             return true;
         }
         kernel_span_begin(ctx);
@@ -772,7 +884,7 @@ static bool sims_device(rs_ctx* ctx, int32_t kind, int32_t L, int32_t R, const S
         return false;
     }
     DevBuf<double> dr(std::max<int64_t>(1, nnz)), dmean(L);
-    dr.upload(sr.r.data(), nnz, s);
+    dr.upload(sr.pr, nnz, s);
     hipLaunchKernelGGL(row_mean_kernel, dim3((L + 255) / 256), dim3(256), 0, s, L, drow.p, dr.p,
                        dmean.p);
     std::vector<int32_t> rows;
@@ -944,12 +1056,16 @@ extern "C" int rs_knn_sims_part(rs_ctx* ctx, int32_t kind, int32_t n_left, int32
         if (n_parts < 1 || part < 0 || part >= n_parts)
             return rs::set_error(ctx, RS_ERR_INVALID, "part must be in [0, n_parts)");
         if (n_left > 0 && !sims) return rs::set_error(ctx, RS_ERR_INVALID, "sims is NULL");
+        rs::PhaseTrace tr;
+        rs::g_trace = tr.on ? &tr : nullptr;
+        struct Reset { ~Reset() { rs::g_trace = nullptr; } } reset_trace;
         const int st = rs::check_knn_csr(ctx, n_left, n_right, rowptr, ids, ratings);
         if (st != RS_OK) return st;
         rs::SortedRows sr;
-        rs::sort_rows(n_left, rowptr, ids, ratings, sr);
-        rs::DevBuf<double> dS;
+        tr.mark("check");
         const char* env = std::getenv("RSGPU_KNN_NO_MFMA");
+        rs::prepare_rows(kind, !(env && env[0] == '1'), n_left, n_right, rowptr, ids, ratings, sr);
+        rs::DevBuf<double> dS;
         const char* nostream = std::getenv("RSGPU_KNN_NO_STREAM");  // A/B switch: one launch, one copy
         const bool done = rs::sims_device(ctx, kind, n_left, n_right, sr, !(env && env[0] == '1'), dS, part,
                                           n_parts, (nostream && nostream[0] == '1') ? nullptr : sims);
@@ -970,6 +1086,9 @@ extern "C" int rs_knn_sims_part(rs_ctx* ctx, int32_t kind, int32_t n_left, int32
             }
         }
         RS_HIP(hipStreamSynchronize(s));
+        tr.mark("download");
+        dS.release();
+        tr.mark("free");
         return RS_OK;
     });
 }
@@ -1011,6 +1130,7 @@ extern "C" int rs_sim_pair(rs_ctx* ctx, int32_t kind, int64_t na, const int32_t*
         sr.rowptr = rowptr;
         sr.ids = ids;
         sr.r = r;  // inputs are ID-ascending already (SortedIdRatings)
+        sr.own();
         rs::DevBuf<double> dS;
         rs::sims_device(ctx, kind, 2, R, sr, false, dS);
         double S[4];
@@ -1048,8 +1168,8 @@ extern "C" int rs_knn_plan_create(rs_ctx* ctx, int32_t kind, int32_t n_left, int
             pl->L = n_left;
             pl->kind = kind;
             rs::SortedRows sr;
-            rs::sort_rows(n_left, rowptr, ids, ratings, sr);
             const char* env = std::getenv("RSGPU_KNN_NO_MFMA");
+            rs::prepare_rows(kind, !(env && env[0] == '1'), n_left, n_right, rowptr, ids, ratings, sr);
             rs::sims_device(ctx, kind, n_left, n_right, sr, !(env && env[0] == '1'), pl->S);
             RS_HIP(hipStreamSynchronize(ctx->stream));
         } catch (...) {
