@@ -655,7 +655,7 @@ static void prepare_rows(int32_t kind, bool allow_mfma, int32_t L, int32_t R, co
 
 // ---------------------------------------------------------------------------------------------
 // Streamed download of the MFMA path's Sims (rs_knn_sims, one part).  The tiles run as one launch
-// per super-tile column group, last group first, alternating over two streams (the groups write
+// per super-tile column group, last group first, round robin over two streams (the groups write
 // disjoint entries, so consecutive launches overlap at their tails); after groups >= g are done,
 // the rows of group g are complete (tile_order) and the copy engine moves them, in chunks of whole
 // rows, into a pinned ring held by the ctx while the next groups compute.  Host threads copy each
@@ -664,6 +664,9 @@ static void prepare_rows(int32_t kind, bool allow_mfma, int32_t L, int32_t R, co
 constexpr int kDlSlots = 16;
 constexpr size_t kDlSlotBytes = size_t(16) << 20;
 constexpr int kDlWorkers = 8;
+// compute streams of the group launches: 3 measured 166 ms of kernels but 0.29 s of Fit wall
+// against 170 ms / 0.26 s for 2 (rows complete later when more groups run at once)
+constexpr int kDlCompute = 2;
 
 static uint8_t* ctx_staging(rs_ctx* ctx) {
     if (!ctx->staging) {
@@ -704,20 +707,26 @@ static void sims_streamed(rs_ctx* ctx, int32_t L, const std::vector<size_t>& gro
     const int32_t NG = static_cast<int32_t>(group_off.size()) - 1;
     const int64_t group_rows = static_cast<int64_t>(kGroup) * kTile;
     StreamSet ss;
-    hipStream_t sA = ctx->stream, sB = ss.stream(), sC = ss.stream();
+    // kDlCompute compute streams (the ctx stream first) take the launches round robin
+    const int NS = std::max(1, std::min(kDlCompute, NG));
+    std::vector<hipStream_t> sk(NS, ctx->stream);
+    for (int i = 1; i < NS; ++i) sk[i] = ss.stream();
+    hipStream_t sC = ss.stream();
     std::vector<hipEvent_t> ev_g(NG);
     for (auto& e : ev_g) e = ss.event();
-    hipEvent_t ev_b = ss.event();
     kernel_span_begin(ctx);
-    RS_HIP(hipStreamWaitEvent(sB, ctx->k0, 0));
+    for (int i = 1; i < NS; ++i) RS_HIP(hipStreamWaitEvent(sk[i], ctx->k0, 0));
     for (int32_t j = 0; j < NG; ++j) {  // launch j = column group NG - 1 - j
-        hipStream_t s = (j & 1) ? sB : sA;
+        hipStream_t s = sk[j % NS];
         launch(group_off[j], group_off[j + 1] - group_off[j], s);
         RS_HIP(hipEventRecord(ev_g[NG - 1 - j], s));
     }
-    RS_HIP(hipEventRecord(ev_b, sB));
-    RS_HIP(hipStreamWaitEvent(sA, ev_b, 0));
-    (void)hipEventRecord(ctx->k1, sA);
+    for (int i = 1; i < NS; ++i) {
+        hipEvent_t e = ss.event();
+        RS_HIP(hipEventRecord(e, sk[i]));
+        RS_HIP(hipStreamWaitEvent(sk[0], e, 0));
+    }
+    (void)hipEventRecord(ctx->k1, sk[0]);
 
     // chunks of whole rows, never crossing a group: groups NG-1 .. 0, rows ascending within
     struct Chunk { int64_t row0, rows; int32_t group; };
@@ -766,9 +775,8 @@ static void sims_streamed(rs_ctx* ctx, int32_t L, const std::vector<size_t>& gro
                 std::this_thread::yield();
             }
             const int32_t g = chunks[c].group;
-            if (g < waited) {  // every group >= g is done: its own event and the next group's
-                RS_HIP(hipStreamWaitEvent(sC, ev_g[g], 0));
-                if (g + 1 < NG) RS_HIP(hipStreamWaitEvent(sC, ev_g[g + 1], 0));
+            if (g < waited) {  // every group >= g is done: the last one on each compute stream
+                for (int32_t h = g; h < std::min(NG, g + NS); ++h) RS_HIP(hipStreamWaitEvent(sC, ev_g[h], 0));
                 waited = g;
             }
             RS_HIP(hipMemcpyAsync(ring + slot * kDlSlotBytes, dS + chunks[c].row0 * L,
