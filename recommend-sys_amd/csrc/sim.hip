@@ -98,7 +98,7 @@ __global__ __launch_bounds__(NWJ == 2 ? 256 : 512) void knn_sims_mfma_kernel(con
                                                             const int2* __restrict__ tiles,
                                                             double inv_s2, double* __restrict__ S) {
     constexpr int NC = KIND == 1 ? 4 : 3;
-    static_assert(NWJ == 2 || PIPE == 2, "the eight-wave tiling exists for the PIPE 2 loop only");
+    static_assert(NWJ == 2 || PIPE >= 1, "the eight-wave tiling exists for the pipelined loops only");
     constexpr int NT = NWJ == 2 ? 256 : 512;      // threads
     constexpr int kXPerThread = kXChunks / NT;    // 16-byte X chunks staged per thread and step
     constexpr int FPM = 2 + NWJ;                  // fragments per matrix and half: 2 a-tiles, NWJ b-tiles
@@ -844,9 +844,10 @@ static bool sims_device(rs_ctx* ctx, int32_t kind, int32_t L, int32_t R, const S
         // K loop: 0 = round 1 (phases in sequence), 1 = software pipeline, 2 = pipeline with M
         // derived from the X fragments in registers (one staged matrix less)
         // K loop: 0 = round 1 (phases in sequence), 1 = software pipeline, 2 = pipeline with M
-        // derived in registers, 3 = PIPE 2 on eight waves (two per SIMD, 64 x 32 each; default)
+        // derived in registers, 3 = PIPE 2 on eight waves (two per SIMD, 64 x 32 each; default),
+        // 4 = PIPE 1 on eight waves (M staged: fewer VALU, more LDS reads)
         const char* pipe_env = std::getenv("RSGPU_KNN_PIPE");
-        const int pipe = (pipe_env && pipe_env[0] >= '0' && pipe_env[0] <= '3') ? pipe_env[0] - '0' : 3;
+        const int pipe = (pipe_env && pipe_env[0] >= '0' && pipe_env[0] <= '4') ? pipe_env[0] - '0' : 3;
         for (const void* f : {reinterpret_cast<const void*>(&knn_sims_mfma_kernel<0, 0>),
                               reinterpret_cast<const void*>(&knn_sims_mfma_kernel<1, 0>),
                               reinterpret_cast<const void*>(&knn_sims_mfma_kernel<2, 0>),
@@ -858,7 +859,10 @@ static bool sims_device(rs_ctx* ctx, int32_t kind, int32_t L, int32_t R, const S
                               reinterpret_cast<const void*>(&knn_sims_mfma_kernel<2, 2>),
                               reinterpret_cast<const void*>(&knn_sims_mfma_kernel<0, 2, 1>),
                               reinterpret_cast<const void*>(&knn_sims_mfma_kernel<1, 2, 1>),
-                              reinterpret_cast<const void*>(&knn_sims_mfma_kernel<2, 2, 1>)})
+                              reinterpret_cast<const void*>(&knn_sims_mfma_kernel<2, 2, 1>),
+                              reinterpret_cast<const void*>(&knn_sims_mfma_kernel<0, 1, 1>),
+                              reinterpret_cast<const void*>(&knn_sims_mfma_kernel<1, 1, 1>),
+                              reinterpret_cast<const void*>(&knn_sims_mfma_kernel<2, 1, 1>)})
             RS_HIP(hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(lds)));
         auto launch = [&](size_t first, size_t count, hipStream_t st) {
             if (!count) return;
@@ -866,18 +870,19 @@ static bool sims_device(rs_ctx* ctx, int32_t kind, int32_t L, int32_t R, const S
             auto go = [&](auto kern, int threads) {
                 hipLaunchKernelGGL(kern, grid, dim3(threads), lds, st, X.p, ldk, L, dtiles.p + first, inv_s2, dS.p);
             };
-            auto by_pipe = [&](auto k0, auto k1, auto k2, auto k3) {
-                pipe == 0 ? go(k0, 256) : pipe == 1 ? go(k1, 256) : pipe == 2 ? go(k2, 256) : go(k3, 512);
+            auto by_pipe = [&](auto k0, auto k1, auto k2, auto k3, auto k4) {
+                pipe == 0 ? go(k0, 256) : pipe == 1 ? go(k1, 256) : pipe == 2 ? go(k2, 256)
+                          : pipe == 3 ? go(k3, 512) : go(k4, 512);
             };
             if (kind == RS_SIM_COSINE)
                 by_pipe(knn_sims_mfma_kernel<0, 0>, knn_sims_mfma_kernel<0, 1>, knn_sims_mfma_kernel<0, 2>,
-                        knn_sims_mfma_kernel<0, 2, 1>);
+                        knn_sims_mfma_kernel<0, 2, 1>, knn_sims_mfma_kernel<0, 1, 1>);
             else if (kind == RS_SIM_MSD)
                 by_pipe(knn_sims_mfma_kernel<1, 0>, knn_sims_mfma_kernel<1, 1>, knn_sims_mfma_kernel<1, 2>,
-                        knn_sims_mfma_kernel<1, 2, 1>);
+                        knn_sims_mfma_kernel<1, 2, 1>, knn_sims_mfma_kernel<1, 1, 1>);
             else
                 by_pipe(knn_sims_mfma_kernel<2, 0>, knn_sims_mfma_kernel<2, 1>, knn_sims_mfma_kernel<2, 2>,
-                        knn_sims_mfma_kernel<2, 2, 1>);
+                        knn_sims_mfma_kernel<2, 2, 1>, knn_sims_mfma_kernel<2, 1, 1>);
             RS_HIP(hipGetLastError());
         };
         if (host && n_parts == 1) {
