@@ -92,7 +92,7 @@ __device__ __forceinline__ void lds_barrier() {
 // NWJ = 32-column MFMA tiles per wave along b: 2 -> four waves of 64 x 64 (one wave per SIMD,
 // 192 accumulator AGPRs); 1 -> eight waves of 64 x 32 (two waves per SIMD, 96 AGPRs each, so the
 // SIMD interleaves two waves' phases; PIPE 2 only).
-template <int KIND, int PIPE, int NWJ = 2>
+template <int KIND, int PIPE, int NWJ = 2, bool ROT = false>
 __global__ __launch_bounds__(NWJ == 2 ? 256 : 512) void knn_sims_mfma_kernel(const int8_t* __restrict__ X,
                                                             int64_t ldk, int32_t L,
                                                             const int2* __restrict__ tiles,
@@ -297,7 +297,21 @@ __global__ __launch_bounds__(NWJ == 2 ? 256 : 512) void knn_sims_mfma_kernel(con
     gload(st, 0);
     lstore(st, 0);
     lds_barrier();
-    if constexpr (PIPE) {
+    if constexpr (ROT) {
+        // loads one step further ahead through a rotation: st (step t + 1, loaded during step
+        // t - 1) is staged while st2 loads step t + 2; st = st2 at the end of the step, so a load
+        // has a whole step to land before anything waits on it
+        i32x4 st2[kXPerThread];
+        gload(st, std::min<int64_t>(1, nsteps - 1) * kKBlock);
+        for (int64_t step = 0; step < nsteps; ++step) {
+            const int buf = static_cast<int>(step & 1);
+            gload(st2, std::min<int64_t>(step + 2, nsteps - 1) * kKBlock);
+            pipe_step(buf, st);
+#pragma unroll
+            for (int j = 0; j < kXPerThread; ++j) st[j] = st2[j];
+            lds_barrier();
+        }
+    } else if constexpr (PIPE) {
         for (int64_t step = 0; step < nsteps; ++step) {
             const int buf = static_cast<int>(step & 1);
             gload(st, std::min<int64_t>(step + 1, nsteps - 1) * kKBlock);
@@ -844,10 +858,11 @@ static bool sims_device(rs_ctx* ctx, int32_t kind, int32_t L, int32_t R, const S
         // K loop: 0 = round 1 (phases in sequence), 1 = software pipeline, 2 = pipeline with M
         // derived from the X fragments in registers (one staged matrix less)
         // K loop: 0 = round 1 (phases in sequence), 1 = software pipeline, 2 = pipeline with M
-        // derived in registers, 3 = PIPE 2 on eight waves (two per SIMD, 64 x 32 each; default),
-        // 4 = PIPE 1 on eight waves (M staged: fewer VALU, more LDS reads)
+        // derived in registers, 3 = PIPE 2 on eight waves (two per SIMD, 64 x 32 each),
+        // 4 = PIPE 1 on eight waves (M staged: fewer VALU, more LDS reads), 5 = PIPE 3 with the X
+        // loads rotated one step further ahead (default)
         const char* pipe_env = std::getenv("RSGPU_KNN_PIPE");
-        const int pipe = (pipe_env && pipe_env[0] >= '0' && pipe_env[0] <= '4') ? pipe_env[0] - '0' : 3;
+        const int pipe = (pipe_env && pipe_env[0] >= '0' && pipe_env[0] <= '5') ? pipe_env[0] - '0' : 5;
         for (const void* f : {reinterpret_cast<const void*>(&knn_sims_mfma_kernel<0, 0>),
                               reinterpret_cast<const void*>(&knn_sims_mfma_kernel<1, 0>),
                               reinterpret_cast<const void*>(&knn_sims_mfma_kernel<2, 0>),
@@ -862,7 +877,10 @@ static bool sims_device(rs_ctx* ctx, int32_t kind, int32_t L, int32_t R, const S
                               reinterpret_cast<const void*>(&knn_sims_mfma_kernel<2, 2, 1>),
                               reinterpret_cast<const void*>(&knn_sims_mfma_kernel<0, 1, 1>),
                               reinterpret_cast<const void*>(&knn_sims_mfma_kernel<1, 1, 1>),
-                              reinterpret_cast<const void*>(&knn_sims_mfma_kernel<2, 1, 1>)})
+                              reinterpret_cast<const void*>(&knn_sims_mfma_kernel<2, 1, 1>),
+                              reinterpret_cast<const void*>(&knn_sims_mfma_kernel<0, 2, 1, true>),
+                              reinterpret_cast<const void*>(&knn_sims_mfma_kernel<1, 2, 1, true>),
+                              reinterpret_cast<const void*>(&knn_sims_mfma_kernel<2, 2, 1, true>)})
             RS_HIP(hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(lds)));
         auto launch = [&](size_t first, size_t count, hipStream_t st) {
             if (!count) return;
@@ -870,19 +888,22 @@ static bool sims_device(rs_ctx* ctx, int32_t kind, int32_t L, int32_t R, const S
             auto go = [&](auto kern, int threads) {
                 hipLaunchKernelGGL(kern, grid, dim3(threads), lds, st, X.p, ldk, L, dtiles.p + first, inv_s2, dS.p);
             };
-            auto by_pipe = [&](auto k0, auto k1, auto k2, auto k3, auto k4) {
+            auto by_pipe = [&](auto k0, auto k1, auto k2, auto k3, auto k4, auto k5) {
                 pipe == 0 ? go(k0, 256) : pipe == 1 ? go(k1, 256) : pipe == 2 ? go(k2, 256)
-                          : pipe == 3 ? go(k3, 512) : go(k4, 512);
+                          : pipe == 3 ? go(k3, 512) : pipe == 4 ? go(k4, 512) : go(k5, 512);
             };
             if (kind == RS_SIM_COSINE)
                 by_pipe(knn_sims_mfma_kernel<0, 0>, knn_sims_mfma_kernel<0, 1>, knn_sims_mfma_kernel<0, 2>,
-                        knn_sims_mfma_kernel<0, 2, 1>, knn_sims_mfma_kernel<0, 1, 1>);
+                        knn_sims_mfma_kernel<0, 2, 1>, knn_sims_mfma_kernel<0, 1, 1>,
+                        knn_sims_mfma_kernel<0, 2, 1, true>);
             else if (kind == RS_SIM_MSD)
                 by_pipe(knn_sims_mfma_kernel<1, 0>, knn_sims_mfma_kernel<1, 1>, knn_sims_mfma_kernel<1, 2>,
-                        knn_sims_mfma_kernel<1, 2, 1>, knn_sims_mfma_kernel<1, 1, 1>);
+                        knn_sims_mfma_kernel<1, 2, 1>, knn_sims_mfma_kernel<1, 1, 1>,
+                        knn_sims_mfma_kernel<1, 2, 1, true>);
             else
                 by_pipe(knn_sims_mfma_kernel<2, 0>, knn_sims_mfma_kernel<2, 1>, knn_sims_mfma_kernel<2, 2>,
-                        knn_sims_mfma_kernel<2, 2, 1>, knn_sims_mfma_kernel<2, 1, 1>);
+                        knn_sims_mfma_kernel<2, 2, 1>, knn_sims_mfma_kernel<2, 1, 1>,
+                        knn_sims_mfma_kernel<2, 2, 1, true>);
             RS_HIP(hipGetLastError());
         };
         if (host && n_parts == 1) {

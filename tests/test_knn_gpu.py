@@ -210,7 +210,7 @@ def test_knn_streamed_download_multi_group(ctx, kind, monkeypatch):
     plan = ctx.knn_plan(kind, rowptr, ids, rr, R)
     assert bitwise_equal(S, plan.sims())
     plan.close()
-    for pipe in ("3", "4"):  # eight waves of 64 x 32 (two per SIMD), M in registers / staged
+    for pipe in ("3", "4", "5"):  # eight waves of 64 x 32 (two per SIMD): M in registers / staged / rotated loads
         monkeypatch.setenv("RSGPU_KNN_PIPE", pipe)
         assert bitwise_equal(S, ctx.knn_sims(kind, rowptr, ids, rr, R)), pipe
     monkeypatch.setenv("RSGPU_KNN_NO_STREAM", "1")
