@@ -328,18 +328,41 @@ int rs_svd_plan_epoch_delta(rs_svd_plan* plan, float lr, float reg, void* dP, vo
 int rs_svd_plan_apply_delta(rs_svd_plan* plan, const void* dP, const void* gbsum,
                             double inv_total_nnz, void* stream);
 /* ---- item-sharded multi-GPU behind the library (RCCL over xGMI; multi.hip) ------------------- *
- * The protocol above with the collective inside the library, pipelined per user block: the users are
- * cut into n_blocks ranges of near-equal ratings, each with its own tiles; while block b + 1's SGD
- * kernel runs, block b's dP rows are all-reduced (RCCL, in place) and applied to P on a second
- * stream, so only the last block's exchange is exposed per epoch.  The user
- * weights and the total are computed by the library.  Tile schedule only (RS_SGD_WB_TILE).
+ * Q and b_i are sharded by item range (one plan per rank over its shard; same users, same n_factors).
+ * Two exchanges, chosen per plan before the join (rs_svd_plan_set_exchange):
+ *
+ * RS_EXCHANGE_ROTATE (default) -- the stratum rotation, exact.  The users are cut into n_ranks
+ * rank-blocks of near-equal ratings (from every user's ratings over all shards, so the blocks agree on
+ * every rank), each of `pieces` user blocks with their own tiles.  An epoch is n_ranks sub-epochs: in
+ * sub-epoch s rank g trains its shard against rank-block (g + s) mod n_ranks with P updated in place,
+ * then sends those rows to rank g - 1 and receives rank-block (g + s + 1) from rank g + 1 (RCCL
+ * send/recv on a library comm stream, piece by piece while the next piece computes).  Every rating is
+ * trained once per epoch against the current p_u and q_i; no rows are averaged.  GlobalBias is folded
+ * once per epoch from every stratum's work-local partials (all-reduced).  After the call the
+ * rank-blocks are broadcast, so P, b_u and GlobalBias are identical on every rank again.  n_blocks =
+ * user blocks in all (rounded up to a multiple of n_ranks; 0 = automatic: pieces of ~64 MiB of P).
+ * This replaces north_star's per-epoch all-reduce of user-factor deltas, which RS_EXCHANGE_AVERAGE
+ * keeps (the averaged deltas miss the reference's RMSE).
+ *
+ * RS_EXCHANGE_AVERAGE -- round 2's protocol: the epoch of every rank in delta mode from the same P, the
+ * count-weighted user deltas all-reduced per user block while the next block computes and applied
+ * (n_blocks 0 = automatic: about 256 MiB of deltas per block, 2..32).
  *
  * One process per GPU (the Go host's one-process-per-GPU mode, bench.py --gpus N): rank 0 calls
  * rs_comm_unique_id and sends the RS_COMM_ID_BYTES bytes to every rank (any channel); every rank
- * builds a plan over its item shard (same users, same n_factors), uploads the same P / b_u / GlobalBias
- * and calls rs_svd_plan_join (collective: all ranks together), then rs_svd_plan_epochs_sharded on every
- * rank with the same arguments.  n_blocks 0 = automatic (1 for one rank, else about 256 MiB of deltas
- * per block, 2..32).  rs_svd_plan_leave frees the communicator (rs_svd_plan_destroy does too). */
+ * builds a plan over its item shard, uploads the same P / b_u / GlobalBias and calls rs_svd_plan_join
+ * (collective: all ranks together), then rs_svd_plan_epochs_sharded on every rank with the same
+ * arguments.  rs_svd_plan_leave frees the communicator (rs_svd_plan_destroy does too).
+ * rs_comm_info reports the RCCL library the process runs against (its version code and the path of
+ * the one librccl mapped; path_len bytes incl. the terminating NUL; either pointer may be NULL). */
+#define RS_EXCHANGE_ROTATE 0
+#define RS_EXCHANGE_AVERAGE 1
+int rs_svd_plan_set_exchange(rs_svd_plan* plan, int32_t mode);
+/* Host only: RS_EXCHANGE_ROTATE's sub-epoch `sub_epoch` of `rank` -- out[0] the rank-block it trains,
+ * out[1] the rank its rows are sent to, out[2] the rank-block it receives, out[3] the rank that sends
+ * it.  The schedule rs_svd_plan_epochs_sharded runs. */
+int rs_rotation_step(int32_t rank, int32_t n_ranks, int32_t sub_epoch, int32_t* out /* 4 */);
+int rs_comm_info(int32_t* version, char* path, int32_t path_len);
 #define RS_COMM_ID_BYTES 128
 int rs_comm_unique_id(void* id /* RS_COMM_ID_BYTES */);
 int rs_svd_plan_join(rs_svd_plan* plan, const void* id, int32_t rank, int32_t n_ranks, int32_t n_blocks);
@@ -352,9 +375,10 @@ int rs_svd_plan_leave(rs_svd_plan* plan);
  * lets a single plan reproduce a joined plan's visit order. */
 int rs_svd_plan_set_user_blocks(rs_svd_plan* plan, int32_t n_blocks, const int32_t* bounds);
 /* One process driving n shards (one host thread per shard): RCCL when every plan has its own device,
- * otherwise (shards sharing a device: tests) an in-process exchange that sums the shards' deltas in
- * shard order after a host barrier (same arithmetic, no overlap).  The plans stay owned by the caller;
- * rs_svd_group_destroy detaches them. */
+ * otherwise (shards sharing a device: tests) an in-process exchange behind host barriers (ROTATE: the
+ * rank-blocks copied between the shards' P; AVERAGE: the deltas summed in shard order; same arithmetic,
+ * no overlap).  If a shard fails, the others are released (barrier failure, ncclCommAbort) and the
+ * call returns its error.  The plans stay owned by the caller; rs_svd_group_destroy detaches them. */
 typedef struct rs_svd_group rs_svd_group;
 int rs_svd_group_create(rs_svd_plan* const* plans, int32_t n, int32_t n_blocks, rs_svd_group** out);
 int rs_svd_group_epochs(rs_svd_group* group, int32_t n_epochs, float lr, float reg);
@@ -362,7 +386,8 @@ void rs_svd_group_destroy(rs_svd_group* group);
 /* Item shards of near-equal ratings over contiguous inner item ids: bounds (n_shards + 1 entries). */
 int rs_item_shards(int64_t nnz, const int32_t* items, int32_t n_items, int32_t n_shards, int32_t* bounds);
 /* core/svd.go:63-132 (FAST tile schedule) on n_devices GPUs of this process, items sharded by
- * rs_item_shards, as rs_svd_fit otherwise (GlobalBias warm start, host buffers in / out). */
+ * rs_item_shards, RS_EXCHANGE_ROTATE, as rs_svd_fit otherwise (GlobalBias warm start, host buffers in /
+ * out; RS_ERR_NUMERIC after every shard's values are written). */
 int rs_svd_fit_multi(const int32_t* devices, int32_t n_devices, const rs_ratings* r, const rs_sgd_params* p,
                      int32_t n_blocks, double* P, double* Q, double* bu, double* bi, double* gb);
 /* ---- user-sharded multi-GPU (the dual partition, SURVEY §8e "measured alternative") ---------- *

@@ -1,27 +1,34 @@
 // multi.hip -- item-sharded multi-GPU SGD behind the C-ABI (north_star), the epoch of
-// core/svd.go:92-130 over Q sharded by item range, P / b_u / GlobalBias replicated.
+// core/svd.go:92-130 over Q sharded by item range across the ranks.
 //
-// Protocol.  Every shard's plan runs the tile schedule in delta mode: P stays
-// at the epoch start and the kernel writes dP[u] = w_u (p_u(end) - p_u(start)) (bias column
-// included), w_u = the shard's share of u's ratings (a plain sum of shard deltas overshoots for users
-// split over shards).  The ranks sum dP and the GlobalBias partials and every rank applies the same
-// sum, so the replicated state stays bitwise identical.
+// Two exchanges (rs_svd_plan_set_exchange):
 //
-// Pipelining.  The users are cut into B blocks of consecutive users with near-equal ratings, each
-// with its own tiles (rs_svd_plan_set_user_blocks).  Block b's kernel is launched on the compute
-// stream; when it ends, the comm stream all-reduces block b's dP rows (RCCL over xGMI, in place) and
-// applies them to P while the compute stream runs block b + 1 -- block b + 1 touches other P rows,
-// and the shard's own Q rows never leave the device.  Only the last block's all-reduce and the
-// GlobalBias fold are exposed at the epoch boundary (the next epoch's kernels read the new
-// GlobalBias).  RCCL is limited to kCommCTAs workgroups and the tile launch leaves that many CUs free,
-// so the collective's kernels run beside the SGD kernel instead of queueing behind its 160-KiB-LDS
-// workgroups.
+// ROTATE (default; the exact one).  The users are cut into N rank-blocks (N = ranks), each of
+// `pieces` user blocks of near-equal ratings with their own tiles.  An epoch is N sub-epochs: in
+// sub-epoch s rank g trains its item shard against rank-block (g + s) mod N with P written in place,
+// then sends those P rows (b_u rides in column k) to rank g - 1, which trains them against its own
+// shard in sub-epoch s + 1, and receives rank-block (g + s + 1) from rank g + 1.  Every (user block,
+// item shard) stratum is trained by exactly one rank, once per epoch, with exclusive P and Q rows:
+// no rows are averaged, and each rating sees the current p_u and q_i as in the sequential epoch
+// (the DSGD stratum rotation).  The strata of one sub-epoch touch disjoint rows, so with one wave
+// per tile the epoch equals the sequential SGD over the strata in rotation order
+// (tests/test_multi_gpu.py restates it with the oracle).  Piece j of a rank-block is sent as soon as
+// its kernel ends (RCCL send/recv on a comm stream) while piece j + 1 computes; the receiver's piece j
+// waits only for that transfer.  GlobalBias is the FAST schedules' work-local copy folded once per
+// epoch (the partials of every stratum summed and all-reduced).  After the call the rank-blocks are
+// broadcast, so P is replicated again on every rank.
 //
-// Two exchanges share this code: RCCL (ncclComm per rank: rs_svd_plan_join for one process per GPU,
-// rs_svd_group_create for one process driving several GPUs) and an in-process host-barrier exchange
-// for shards that share a device (tests; no overlap: a fixed-order sum over the shards' buffers).
+// AVERAGE (round 2's protocol, kept selectable).  Every rank trains all users against its shard in
+// delta mode from the same P; the count-weighted average of the shards' user deltas is all-reduced
+// per user block and applied.  It under-trains users split over shards (5-fold ML-100K held-out RMSE
+// 0.9422 against 0.9367 with two shards), which is why ROTATE is the default.
+//
+// Both exchanges run over RCCL (ncclComm per rank: rs_svd_plan_join for one process per GPU,
+// rs_svd_group_create for one process driving several GPUs) or, for shards that share a device
+// (tests), over an in-process host-barrier exchange (no overlap).
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
+#include <dlfcn.h>
 
 #include <algorithm>
 #include <atomic>
@@ -52,6 +59,8 @@ struct LocalGroup {  // host-barrier exchange between the shards of one process
     bool failed = false;
     std::vector<float*> dP;
     std::vector<double*> gbs;
+    std::vector<float*> P;    // ROTATE: every shard's P (rank-blocks are pulled from the neighbour)
+    std::vector<int> dev;
     void barrier() {
         std::unique_lock<std::mutex> l(m);
         if (failed) throw std::runtime_error("another shard of the group failed");
@@ -74,22 +83,34 @@ struct LocalGroup {  // host-barrier exchange between the shards of one process
 
 struct ShardComm {
     int rank = 0, nranks = 1, device = 0;
+    int32_t mode = RS_EXCHANGE_ROTATE;
+    int32_t pieces = 1;  // ROTATE: user blocks per rank-block
     ncclComm_t nccl = nullptr;
     bool own_nccl = true;
+    std::atomic<bool> aborted{false};
     std::shared_ptr<LocalGroup> local;
     hipStream_t cs = nullptr;  // comm stream (RCCL exchange)
-    hipEvent_t ev_epoch = nullptr;
-    std::vector<hipEvent_t> ev_done;
-    DevBuf<float> dP, sum;      // n_users x ldd; sum: the in-process exchange's result
+    hipEvent_t ev_epoch = nullptr, ev_gb = nullptr;
+    std::vector<hipEvent_t> ev_done;  // per user block: its kernel ended (compute stream)
+    std::vector<hipEvent_t> ev_recv;  // ROTATE, per user block: its rows arrived (comm stream)
+    std::vector<uint8_t> pending;     // ROTATE: ev_recv[b] recorded and not yet waited on
+    DevBuf<float> dP, sum;      // AVERAGE: n_users x ldd; sum: the in-process exchange's result
     DevBuf<double> gbs, gbs_sum;  // per block
     int32_t ldd = 0;
     double total_nnz = 0.0;
+    // ROTATE: ncclCommAbort once (any thread) so that ranks blocked on a collective return
+    void abort_comm() {
+        bool was = false;
+        if (nccl && aborted.compare_exchange_strong(was, true)) (void)ncclCommAbort(nccl);
+    }
     ~ShardComm() {
         (void)hipSetDevice(device);
-        if (cs) (void)hipStreamSynchronize(cs);
-        if (nccl && own_nccl) (void)ncclCommDestroy(nccl);
+        if (cs && !aborted) (void)hipStreamSynchronize(cs);
+        if (nccl && own_nccl && !aborted) (void)ncclCommDestroy(nccl);
         for (hipEvent_t e : ev_done) (void)hipEventDestroy(e);
+        for (hipEvent_t e : ev_recv) (void)hipEventDestroy(e);
         if (ev_epoch) (void)hipEventDestroy(ev_epoch);
+        if (ev_gb) (void)hipEventDestroy(ev_gb);
         if (cs) (void)hipStreamDestroy(cs);
     }
 };
@@ -151,6 +172,18 @@ __global__ void gb_fold_blocks_kernel(double* __restrict__ gb, const double* __r
     }
 }
 
+// ROTATE, in-process exchange: gb += (sum over shards in shard order of their per-block partial sums) /
+// total ratings -- the same bits on every shard
+__global__ void local_gb_fold_kernel(Srcs src, int32_t n_src, int32_t nb, double* __restrict__ gb,
+                                     double inv_total) {
+    if (threadIdx.x == 0 && blockIdx.x == 0) {
+        double t = 0.0;
+        for (int32_t r = 0; r < n_src; ++r)
+            for (int32_t b = 0; b < nb; ++b) t += src.g[r][b];
+        gb[0] += t * inv_total;
+    }
+}
+
 int grid_for(int64_t n) { return static_cast<int>(std::max<int64_t>(1, std::min<int64_t>(4096, (n + 255) / 256))); }
 
 int32_t auto_blocks(const rs_svd_plan* pl, int32_t nranks, int32_t ldd) {
@@ -158,6 +191,23 @@ int32_t auto_blocks(const rs_svd_plan* pl, int32_t nranks, int32_t ldd) {
     const double bytes = static_cast<double>(pl->n_users) * ldd * 4.0;
     const int32_t b = static_cast<int32_t>(bytes / (256.0 * 1024 * 1024) + 0.5);
     return std::max(2, std::min(32, b));
+}
+
+// ROTATE, sub-epoch st of rank g: the rank-block it trains, the rank its rows go to, the rank-block that
+// comes in and the rank it comes from (rs_rotation_step exports it to host models of the protocol)
+struct RotStep {
+    int32_t train, send_to, recv, recv_from;
+};
+RotStep rotation_step(int32_t g, int32_t n, int32_t st) {
+    return {(g + st) % n, (g + n - 1) % n, (g + st + 1) % n, (g + 1) % n};
+}
+
+// ROTATE: user blocks per rank-block.  A piece's rows are sent while the next piece computes, so only
+// the last piece's transfer is exposed per sub-epoch; pieces of about 64 MiB of P rows (1..16).
+int32_t auto_pieces(const rs_svd_plan* pl, int32_t nranks) {
+    if (nranks <= 1) return 1;
+    const double bytes = static_cast<double>(pl->n_users) / nranks * pl->ld * 4.0;
+    return std::max(1, std::min(16, static_cast<int32_t>(bytes / (64.0 * 1024 * 1024) + 0.5)));
 }
 
 // weights w_u = local / total ratings of u; totals from the caller (host, n_users)
@@ -179,7 +229,13 @@ void shard_setup(rs_svd_plan* pl, ShardComm& c, int32_t n_blocks, const std::vec
         throw std::invalid_argument("the item-sharded epoch runs the tile schedule (RS_SGD_WB_TILE)");
     c.device = pl->ctx->device;
     c.ldd = round_up4(pl->k + 1);
-    pl->tile_ublocks = n_blocks > 0 ? n_blocks : auto_blocks(pl, c.nranks, c.ldd);
+    c.mode = pl->exchange;
+    if (c.mode == RS_EXCHANGE_ROTATE) {  // n_blocks: user blocks in all, rounded up to whole rank-blocks
+        c.pieces = n_blocks > 0 ? (n_blocks + c.nranks - 1) / c.nranks : auto_pieces(pl, c.nranks);
+        pl->tile_ublocks = c.pieces * c.nranks;
+    } else {
+        pl->tile_ublocks = n_blocks > 0 ? n_blocks : auto_blocks(pl, c.nranks, c.ldd);
+    }
     std::vector<int64_t> cum(static_cast<size_t>(pl->n_users) + 1, 0);
     for (int32_t u = 0; u < pl->n_users; ++u) cum[u + 1] = cum[u] + static_cast<int64_t>(tot[u]);
     pl->ublock_bounds = user_block_bounds(cum.data(), pl->n_users, std::max(1, std::min(pl->tile_ublocks, std::max(1, pl->n_users))));
@@ -190,32 +246,39 @@ void shard_setup(rs_svd_plan* pl, ShardComm& c, int32_t n_blocks, const std::vec
     }
     tile_build(pl);
     const int32_t nb = static_cast<int32_t>(pl->t_block_tile.size()) - 1;
-    c.dP.alloc(static_cast<size_t>(std::max(1, pl->n_users)) * c.ldd);
-    RS_HIP(hipMemsetAsync(c.dP.p, 0, c.dP.n * sizeof(float), pl->ctx->stream));
-    c.gbs.alloc(static_cast<size_t>(nb));
-    if (c.local) {
-        c.sum.alloc(c.dP.n);
-        c.gbs_sum.alloc(static_cast<size_t>(nb));
+    if (c.mode == RS_EXCHANGE_ROTATE && nb != c.pieces * c.nranks)
+        throw std::logic_error("rotation: user blocks do not match the rank-blocks");
+    if (c.mode == RS_EXCHANGE_AVERAGE) {
+        c.dP.alloc(static_cast<size_t>(std::max(1, pl->n_users)) * c.ldd);
+        RS_HIP(hipMemsetAsync(c.dP.p, 0, c.dP.n * sizeof(float), pl->ctx->stream));
+        if (c.local) c.sum.alloc(c.dP.n);
     }
+    c.gbs.alloc(static_cast<size_t>(nb));
+    if (c.local) c.gbs_sum.alloc(static_cast<size_t>(nb));
     if (c.nccl) {
         RS_HIP(hipStreamCreateWithFlags(&c.cs, hipStreamNonBlocking));
         RS_HIP(hipEventCreateWithFlags(&c.ev_epoch, hipEventDisableTiming));
+        RS_HIP(hipEventCreateWithFlags(&c.ev_gb, hipEventDisableTiming));
         c.ev_done.resize(static_cast<size_t>(nb), nullptr);
         for (hipEvent_t& e : c.ev_done) RS_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+        if (c.mode == RS_EXCHANGE_ROTATE) {
+            c.ev_recv.resize(static_cast<size_t>(nb), nullptr);
+            for (hipEvent_t& e : c.ev_recv) RS_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+        }
     }
+    c.pending.assign(static_cast<size_t>(nb), 0);
     RS_HIP(hipStreamSynchronize(pl->ctx->stream));
 }
 
 }  // namespace
 
-// n_epochs of the item-sharded schedule on stream s (every rank calls it with the same arguments)
-void epochs_sharded(rs_svd_plan* pl, int32_t n_epochs, float lr, float reg, hipStream_t s) {
+namespace {
+
+// AVERAGE: n_epochs of the delta protocol on stream s
+void epochs_average(rs_svd_plan* pl, int32_t n_epochs, float lr, float reg, hipStream_t s) {
     ShardComm& c = *pl->shard;
-    if (!pl->tiles_built) tile_build(pl);
     const int32_t nb = static_cast<int32_t>(pl->t_block_tile.size()) - 1;
-    if (static_cast<int32_t>(c.gbs.n) != nb) throw std::logic_error("user blocks changed after the join");
     const double inv_total = c.total_nnz > 0 ? 1.0 / c.total_nnz : 0.0;
-    RS_HIP(hipEventRecord(pl->ev0, s));
     q_convert(pl, s, 1);
     for (int32_t e = 0; e < n_epochs; ++e) {
         for (int32_t b = 0; b < nb; ++b) {
@@ -268,6 +331,135 @@ void epochs_sharded(rs_svd_plan* pl, int32_t n_epochs, float lr, float reg, hipS
         RS_HIP(hipGetLastError());
     }
     q_convert(pl, s, 0);
+}
+
+// rows [u0, u1) of P (whole rows, the bias in column k) as one contiguous range
+struct RowRange {
+    float* p;
+    size_t n;
+};
+RowRange block_rows(rs_svd_plan* pl, float* P, int32_t b) {
+    const int32_t u0 = pl->t_block_user[b], u1 = pl->t_block_user[b + 1];
+    return {P + static_cast<int64_t>(u0) * pl->ld, static_cast<size_t>(u1 - u0) * pl->ld};
+}
+
+// ROTATE: n_epochs of the stratum rotation on stream s (the comm stream carries the transfers)
+void epochs_rotate(rs_svd_plan* pl, int32_t n_epochs, float lr, float reg, hipStream_t s) {
+    ShardComm& c = *pl->shard;
+    const int32_t N = c.nranks, h = c.pieces, nb = N * h, g = c.rank;
+    const double inv_total = c.total_nnz > 0 ? 1.0 / c.total_nnz : 0.0;
+    // test hook: the shard of this rank throws in the last sub-epoch (the others must be released)
+    const int fault = std::getenv("RSGPU_FAULT_SHARD") ? std::atoi(std::getenv("RSGPU_FAULT_SHARD")) : -1;
+    q_convert(pl, s, 1);
+    for (int32_t e = 0; e < n_epochs; ++e) {
+        for (int32_t st = 0; st < N; ++st) {
+            const RotStep rs = rotation_step(g, N, st);
+            const int32_t rb = rs.train, rb_in = rs.recv, prev = rs.send_to, next = rs.recv_from;
+            for (int32_t j = 0; j < h; ++j) {
+                const int32_t b = rb * h + j;
+                if (c.nccl && c.pending[b]) {  // this piece's rows arrive from rank g + 1
+                    RS_HIP(hipStreamWaitEvent(s, c.ev_recv[b], 0));
+                    c.pending[b] = 0;
+                }
+                const int32_t parts = tile_launch_range(pl, lr, reg, s, nullptr, 0, pl->t_block_tile[b],
+                                                        pl->t_block_tile[b + 1]);
+                merge_tile_split_rows(pl, pl->t_block_split[b], pl->t_block_split[b + 1], s);
+                gb_sum(pl->partial.p, parts, c.gbs.p + b, s);
+                if (g == fault && st == N - 1) throw std::runtime_error("injected shard fault (RSGPU_FAULT_SHARD)");
+                if (c.nccl && N > 1) {  // piece j goes to rank g - 1, piece j of the next rank-block comes in
+                    const int32_t b_in = rb_in * h + j;
+                    const RowRange out = block_rows(pl, pl->P.p, b), in = block_rows(pl, pl->P.p, b_in);
+                    RS_HIP(hipEventRecord(c.ev_done[b], s));
+                    RS_HIP(hipStreamWaitEvent(c.cs, c.ev_done[b], 0));
+                    check_nccl(ncclGroupStart(), "ncclGroupStart");
+                    if (out.n) check_nccl(ncclSend(out.p, out.n, ncclFloat32, prev, c.nccl, c.cs), "ncclSend(P block)");
+                    if (in.n) check_nccl(ncclRecv(in.p, in.n, ncclFloat32, next, c.nccl, c.cs), "ncclRecv(P block)");
+                    check_nccl(ncclGroupEnd(), "ncclGroupEnd");
+                    RS_HIP(hipEventRecord(c.ev_recv[b_in], c.cs));
+                    c.pending[b_in] = 1;
+                }
+            }
+            if (c.local && N > 1) {  // in-process: pull rank-block rb_in from shard g + 1
+                LocalGroup& lg = *c.local;
+                RS_HIP(hipStreamSynchronize(s));
+                lg.barrier();  // every shard finished sub-epoch st
+                const RowRange in0 = block_rows(pl, pl->P.p, rb_in * h), in1 = block_rows(pl, pl->P.p, rb_in * h + h - 1);
+                const size_t n = static_cast<size_t>(in1.p + in1.n - in0.p);
+                const float* src = lg.P[next] + (in0.p - pl->P.p);
+                if (n) RS_HIP(hipMemcpyPeerAsync(in0.p, lg.dev[g], src, lg.dev[next], n * sizeof(float), s));
+                RS_HIP(hipStreamSynchronize(s));
+                lg.barrier();  // every pull done: the next sub-epoch may write these rows
+            }
+        }
+        // GlobalBias: every stratum's partial, folded once per epoch on every rank
+        if (c.nccl && N > 1) {
+            RS_HIP(hipEventRecord(c.ev_gb, s));
+            RS_HIP(hipStreamWaitEvent(c.cs, c.ev_gb, 0));
+            check_nccl(ncclAllReduce(c.gbs.p, c.gbs.p, static_cast<size_t>(nb), ncclFloat64, ncclSum, c.nccl, c.cs),
+                       "ncclAllReduce(GlobalBias)");
+            hipLaunchKernelGGL(gb_fold_blocks_kernel, dim3(1), dim3(64), 0, c.cs, pl->gb.p, c.gbs.p, nb, inv_total);
+            RS_HIP(hipEventRecord(c.ev_epoch, c.cs));
+            RS_HIP(hipStreamWaitEvent(s, c.ev_epoch, 0));  // the next epoch reads the new GlobalBias
+        } else if (c.local && N > 1) {
+            LocalGroup& lg = *c.local;
+            RS_HIP(hipStreamSynchronize(s));
+            lg.barrier();
+            Srcs src{};
+            for (int r = 0; r < lg.n; ++r) src.g[r] = lg.gbs[r];
+            hipLaunchKernelGGL(local_gb_fold_kernel, dim3(1), dim3(64), 0, s, src, lg.n, nb, pl->gb.p, inv_total);
+            RS_HIP(hipGetLastError());
+            RS_HIP(hipStreamSynchronize(s));
+            lg.barrier();  // every shard read every partial: the next epoch may overwrite them
+        } else {
+            hipLaunchKernelGGL(gb_fold_blocks_kernel, dim3(1), dim3(64), 0, s, pl->gb.p, c.gbs.p, nb, inv_total);
+        }
+        RS_HIP(hipGetLastError());
+    }
+    // rank-block r is current on rank r: broadcast them so P is replicated again
+    if (n_epochs > 0 && N > 1) {
+        if (c.nccl) {
+            for (int32_t b = 0; b < nb; ++b)
+                if (c.pending[b]) {
+                    RS_HIP(hipStreamWaitEvent(s, c.ev_recv[b], 0));
+                    c.pending[b] = 0;
+                }
+            RS_HIP(hipEventRecord(c.ev_gb, s));
+            RS_HIP(hipStreamWaitEvent(c.cs, c.ev_gb, 0));
+            check_nccl(ncclGroupStart(), "ncclGroupStart");
+            for (int32_t r = 0; r < N; ++r) {
+                const RowRange a = block_rows(pl, pl->P.p, r * h), z = block_rows(pl, pl->P.p, r * h + h - 1);
+                const size_t n = static_cast<size_t>(z.p + z.n - a.p);
+                if (n) check_nccl(ncclBroadcast(a.p, a.p, n, ncclFloat32, r, c.nccl, c.cs), "ncclBroadcast(P)");
+            }
+            check_nccl(ncclGroupEnd(), "ncclGroupEnd");
+            RS_HIP(hipEventRecord(c.ev_epoch, c.cs));
+            RS_HIP(hipStreamWaitEvent(s, c.ev_epoch, 0));
+        } else {
+            LocalGroup& lg = *c.local;
+            for (int32_t r = 0; r < N; ++r) {
+                if (r == g) continue;
+                const RowRange a = block_rows(pl, pl->P.p, r * h), z = block_rows(pl, pl->P.p, r * h + h - 1);
+                const size_t n = static_cast<size_t>(z.p + z.n - a.p);
+                if (n)
+                    RS_HIP(hipMemcpyPeerAsync(a.p, lg.dev[g], lg.P[r] + (a.p - pl->P.p), lg.dev[r], n * sizeof(float), s));
+            }
+            RS_HIP(hipStreamSynchronize(s));
+            lg.barrier();  // nobody trains on (or is read from) before every shard has its copy
+        }
+    }
+    q_convert(pl, s, 0);
+}
+
+}  // namespace
+
+// n_epochs of the item-sharded schedule on stream s (every rank calls it with the same arguments)
+void epochs_sharded(rs_svd_plan* pl, int32_t n_epochs, float lr, float reg, hipStream_t s) {
+    if (!pl->tiles_built) tile_build(pl);
+    if (static_cast<int32_t>(pl->shard->gbs.n) != static_cast<int32_t>(pl->t_block_tile.size()) - 1)
+        throw std::logic_error("user blocks changed after the join");
+    RS_HIP(hipEventRecord(pl->ev0, s));
+    if (pl->shard->mode == RS_EXCHANGE_ROTATE) epochs_rotate(pl, n_epochs, lr, reg, s);
+    else epochs_average(pl, n_epochs, lr, reg, s);
     RS_HIP(hipEventRecord(pl->ev1, s));
     pl->last_launches = n_epochs;  // rs_svd_plan_last_kernel_ms: the call's device span per epoch
     pl->last_stream = s;
@@ -301,6 +493,7 @@ void group_join(rs_svd_group* g, int32_t n_blocks) {
     for (rs_svd_plan* pl : g->plans) {
         if (pl->n_users != nu || pl->k != g->plans[0]->k)
             throw std::invalid_argument("shards must have the same users and n_factors");
+        if (pl->exchange != g->plans[0]->exchange) throw std::invalid_argument("shards must use the same exchange");
         for (int32_t u = 0; u < nu; ++u) tot[u] += static_cast<double>(pl->h_rowptr[u + 1] - pl->h_rowptr[u]);
         total += static_cast<double>(pl->nnz);
     }
@@ -338,7 +531,7 @@ void group_join(rs_svd_group* g, int32_t n_blocks) {
         c->nccl = comms[r];
         c->local = g->local;
         c->total_nnz = total;
-        rs::set_weights(pl, tot);
+        if (pl->exchange == RS_EXCHANGE_AVERAGE) rs::set_weights(pl, tot);
         rs::shard_setup(pl, *c, n_blocks, tot);
         pl->shard = std::move(c);
     }
@@ -346,6 +539,8 @@ void group_join(rs_svd_group* g, int32_t n_blocks) {
         for (rs_svd_plan* pl : g->plans) {
             g->local->dP.push_back(pl->shard->dP.p);
             g->local->gbs.push_back(pl->shard->gbs.p);
+            g->local->P.push_back(pl->P.p);
+            g->local->dev.push_back(pl->ctx->device);
         }
     }
 }
@@ -359,6 +554,34 @@ extern "C" int rs_comm_unique_id(void* id) {
         rs::check_nccl(ncclGetUniqueId(&u), "ncclGetUniqueId");
         static_assert(sizeof(u) == RS_COMM_ID_BYTES, "RCCL unique id size");
         std::memcpy(id, &u, sizeof(u));
+        return RS_OK;
+    });
+}
+
+extern "C" int rs_rotation_step(int32_t rank, int32_t n_ranks, int32_t sub_epoch, int32_t* out) {
+    if (!out || n_ranks < 1 || rank < 0 || rank >= n_ranks || sub_epoch < 0 || sub_epoch >= n_ranks)
+        return rs::set_error(nullptr, RS_ERR_INVALID, "bad rotation step arguments");
+    const rs::RotStep r = rs::rotation_step(rank, n_ranks, sub_epoch);
+    out[0] = r.train;
+    out[1] = r.send_to;
+    out[2] = r.recv;
+    out[3] = r.recv_from;
+    return RS_OK;
+}
+
+extern "C" int rs_comm_info(int32_t* version, char* path, int32_t path_len) {
+    return rs_guard(nullptr, [&]() -> int {
+        if (version) {
+            int v = 0;
+            rs::check_nccl(ncclGetVersion(&v), "ncclGetVersion");
+            *version = v;
+        }
+        if (path && path_len > 0) {  // the object that defines the symbol this library calls
+            Dl_info info{};
+            const char* p = dladdr(reinterpret_cast<void*>(&ncclGetVersion), &info) && info.dli_fname ? info.dli_fname : "";
+            std::strncpy(path, p, static_cast<size_t>(path_len) - 1);
+            path[path_len - 1] = 0;
+        }
         return RS_OK;
     });
 }
@@ -386,6 +609,15 @@ extern "C" int rs_svd_plan_set_user_blocks(rs_svd_plan* pl, int32_t n_blocks, co
         }
         return RS_OK;
     });
+}
+
+extern "C" int rs_svd_plan_set_exchange(rs_svd_plan* pl, int32_t mode) {
+    if (!pl) return rs::set_error(nullptr, RS_ERR_INVALID, "plan is NULL");
+    if (mode != RS_EXCHANGE_ROTATE && mode != RS_EXCHANGE_AVERAGE)
+        return rs::set_error(pl->ctx, RS_ERR_INVALID, "unknown exchange");
+    if (pl->shard) return rs::set_error(pl->ctx, RS_ERR_INVALID, "plan is joined to a group (leave first)");
+    pl->exchange = mode;
+    return RS_OK;
 }
 
 extern "C" int rs_svd_plan_join(rs_svd_plan* pl, const void* id, int32_t rank, int32_t n_ranks, int32_t n_blocks) {
@@ -419,7 +651,7 @@ extern "C" int rs_svd_plan_join(rs_svd_plan* pl, const void* id, int32_t rank, i
         RS_HIP(hipStreamSynchronize(s));
         c->total_nnz = cnt.back();
         cnt.pop_back();
-        rs::set_weights(pl, cnt);
+        if (pl->exchange == RS_EXCHANGE_AVERAGE) rs::set_weights(pl, cnt);
         rs::shard_setup(pl, *c, n_blocks, cnt);
         pl->shard = std::move(c);
         return RS_OK;
@@ -486,7 +718,11 @@ extern "C" int rs_svd_group_epochs(rs_svd_group* g, int32_t n_epochs, float lr, 
             } catch (const std::exception& e) {
                 errs[r] = e.what();
             }
-            if (!errs[r].empty() && g->local) g->local->fail();
+            if (!errs[r].empty()) {  // release the other shards: host barrier or pending collectives
+                if (g->local) g->local->fail();
+                for (rs_svd_plan* q : g->plans)
+                    if (q->shard) q->shard->abort_comm();
+            }
         });
     for (std::thread& t : th) t.join();
     for (size_t r = 0; r < n; ++r)
@@ -569,13 +805,15 @@ extern "C" int rs_svd_fit_multi(const int32_t* devices, int32_t n_devices, const
         if (e != RS_OK) return e;
         e = rs_svd_group_epochs(g, p->n_epochs, static_cast<float>(p->lr), static_cast<float>(p->reg));
         if (e != RS_OK) return e;
+        int numeric = RS_OK;  // every shard's values are returned before RS_ERR_NUMERIC is
         for (int32_t s = 0; s < n; ++s) {  // P, b_u, GlobalBias are identical on every shard: take shard 0's
             const int32_t lo = bounds[s];
             e = rs_svd_plan_download(plans[s], s == 0 ? P : nullptr, Q + static_cast<int64_t>(lo) * k,
                                      s == 0 ? bu : nullptr, bi + lo, s == 0 ? gb : nullptr);
-            if (e != RS_OK) return e;
+            if (e == RS_ERR_NUMERIC && numeric == RS_OK) numeric = e;
+            else if (e != RS_OK && e != RS_ERR_NUMERIC) return e;
         }
-        return RS_OK;
+        return numeric;
     });
     std::string err = st != RS_OK ? std::string(rs_last_error(nullptr)) : std::string();
     for (int32_t s = 0; s < n && st != RS_OK && err.empty(); ++s)

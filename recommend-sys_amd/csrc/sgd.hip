@@ -1076,6 +1076,13 @@ void q_convert(rs_svd_plan* pl, hipStream_t s, int32_t to_fixed) {
     RS_HIP(hipGetLastError());
 }
 
+void merge_tile_split_rows(rs_svd_plan* pl, int32_t r0, int32_t r1, hipStream_t s) {
+    if (r1 <= r0) return;
+    hipLaunchKernelGGL(svd_merge_rows_kernel, dim3(r1 - r0), dim3(64), 0, s, pl->P.p, pl->dPs.p,
+                       pl->t_split_rows.p + r0, pl->ld);
+    RS_HIP(hipGetLastError());
+}
+
 void gb_sum(const double* partial, int64_t n, double* out, hipStream_t s) {
     hipLaunchKernelGGL(gb_sum_kernel, dim3(1), dim3(256), 0, s, partial, n, out);
     RS_HIP(hipGetLastError());

@@ -100,7 +100,9 @@ struct rs_svd_plan {
     bool tile_pp = false;
     std::vector<int32_t> ublock_bounds;  // caller's block bounds (tile_ublocks + 1), or empty: own ratings
     std::vector<int32_t> t_block_tile, t_block_user;
+    std::vector<int32_t> t_block_split;  // block b's split users: t_split_rows[t_block_split[b], t_block_split[b+1])
     std::shared_ptr<rs::ShardComm> shard;  // item-sharded multi-GPU state (multi.hip), or empty
+    int32_t exchange = RS_EXCHANGE_ROTATE;  // the multi-GPU exchange a join sets up
     ~rs_svd_plan() {
         if (ev0) (void)hipEventDestroy(ev0);
         if (ev1) (void)hipEventDestroy(ev1);
@@ -159,6 +161,8 @@ void plan_sync_last(rs_svd_plan* pl);  // waits for the stream of the last enque
 int32_t* numflag(rs_svd_plan* pl);  // the RS_ERR_NUMERIC device flag (allocated on first use)
 void q_convert(rs_svd_plan* pl, hipStream_t s, int32_t to_fixed);  // Q <-> int32 fixed point in place
 void gb_sum(const double* partial, int64_t n, double* out, hipStream_t s);  // fixed-order sum
+// split users t_split_rows[r0, r1) of the tile schedule: P += dPs, dPs = 0 (the pieces' merge)
+void merge_tile_split_rows(rs_svd_plan* pl, int32_t r0, int32_t r1, hipStream_t s);
 
 // sgd_tile.hip
 void tile_build(rs_svd_plan* pl);  // (re)builds the tile schedule from the host CSR

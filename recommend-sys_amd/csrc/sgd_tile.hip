@@ -753,7 +753,8 @@ namespace {
 // User blocks: tile_ublocks consecutive user ranges of near-equal ratings, tiled one after the other
 // (block b's tiles are [block_tile[b], block_tile[b+1])).  One block: the plain tile schedule.
 void build_tile_blocks(const rs_svd_plan* pl, int32_t grid0, bool want_pos, TileHost& th,
-                       std::vector<int32_t>& block_tile, std::vector<int32_t>& block_user) {
+                       std::vector<int32_t>& block_tile, std::vector<int32_t>& block_user,
+                       std::vector<int32_t>* block_split = nullptr) {
     const std::vector<int64_t>& rp = pl->h_rowptr;
     if (!pl->ublock_bounds.empty()) {  // common bounds of the shards of a multi-GPU fit
         block_user = pl->ublock_bounds;
@@ -764,6 +765,7 @@ void build_tile_blocks(const rs_svd_plan* pl, int32_t grid0, bool want_pos, Tile
     const int32_t nb = static_cast<int32_t>(block_user.size()) - 1;
     const int32_t cap = pl->tile_run_cap > 0 ? pl->tile_run_cap : auto_run_cap(pl, grid0, pl->tile_waves);
     block_tile.assign(1, 0);
+    if (block_split) block_split->assign(1, 0);
     for (int32_t b = 0; b < nb; ++b) {
         const int32_t u0 = block_user[b], u1 = block_user[b + 1];
         TileHost part;
@@ -787,6 +789,7 @@ void build_tile_blocks(const rs_svd_plan* pl, int32_t grid0, bool want_pos, Tile
             th.lds = std::max(th.lds, part.lds);
         }
         block_tile.push_back(static_cast<int32_t>(th.tiles.size()));
+        if (block_split) block_split->push_back(static_cast<int32_t>(th.split.size()));  // users ascend by block
     }
 }
 
@@ -799,7 +802,7 @@ void tile_build(rs_svd_plan* pl) {
     const int32_t cus = device_cus(pl->ctx);
     const int32_t grid0 = pl->tile_wg > 0 ? pl->tile_wg : cus;
     TileHost th;
-    build_tile_blocks(pl, grid0, false, th, pl->t_block_tile, pl->t_block_user);
+    build_tile_blocks(pl, grid0, false, th, pl->t_block_tile, pl->t_block_user, &pl->t_block_split);
     plan_sync_last(pl);
     pl->n_tiles = static_cast<int32_t>(th.tiles.size());
     pl->tile_grid = std::max(1, std::min(grid0, pl->n_tiles));

@@ -22,6 +22,7 @@ SGD_FAST, SGD_ORDERED = 0, 1
 WB_TILE, WB_STORE, WB_ATOMIC_DIRECT, WB_ATOMIC = 0, 1, 2, 3  # WB_TILE: the default schedule
 SIM_COSINE, SIM_MSD, SIM_PEARSON = 0, 1, 2
 DEV_SLOPE_ONE = 3  # rs_knn_sims kind: SlopeOne deviation matrix (slope_one.go:64-92)
+EXCHANGE_ROTATE, EXCHANGE_AVERAGE = 0, 1  # multi-GPU exchange of the item-sharded fit (rsgpu.h)
 
 HEADER_SYMBOLS = (
     "rs_version", "rs_device_count", "rs_open", "rs_close", "rs_last_error", "rs_synchronize",
@@ -42,7 +43,8 @@ HEADER_SYMBOLS = (
     "rs_svd_plan_tile_order", "rs_svd_plan_tile_clocks",
     "rs_comm_unique_id", "rs_svd_plan_join", "rs_svd_plan_epochs_sharded", "rs_svd_plan_leave",
     "rs_svd_plan_set_user_blocks", "rs_svd_group_create", "rs_svd_group_epochs", "rs_svd_group_destroy",
-    "rs_item_shards", "rs_svd_fit_multi", "rs_tile_schedule_host",
+    "rs_item_shards", "rs_svd_fit_multi", "rs_tile_schedule_host", "rs_svd_plan_set_exchange",
+    "rs_comm_info", "rs_rotation_step",
 )
 COMM_ID_BYTES = 128
 
@@ -159,6 +161,9 @@ def lib():
                                                 _vp, _vp, C.POINTER(_i32), C.POINTER(_dbl)]),
             "rs_svd_fit_multi": (C.c_int, [_vp, _i32, C.POINTER(_Ratings), C.POINTER(_SgdParams), _i32,
                                            _vp, _vp, _vp, _vp, _vp]),
+            "rs_svd_plan_set_exchange": (C.c_int, [_vp, _i32]),
+            "rs_comm_info": (C.c_int, [C.POINTER(_i32), _vp, _i32]),
+            "rs_rotation_step": (C.c_int, [_i32, _i32, _i32, _vp]),
         }
         for name, (res, args) in sig.items():
             f = getattr(L, name)
@@ -448,6 +453,10 @@ class SvdPlan:
         b = None if bounds is None else np.ascontiguousarray(bounds, np.int32)
         self.ctx.check(lib().rs_svd_plan_set_user_blocks(self.h, n_blocks, _ptr(b)))
 
+    def set_exchange(self, mode=EXCHANGE_ROTATE):
+        """Multi-GPU exchange a later join / group sets up (rs_svd_plan_set_exchange)."""
+        self.ctx.check(lib().rs_svd_plan_set_exchange(self.h, mode))
+
     def join(self, comm_id: bytes, rank: int, n_ranks: int, n_blocks: int = 0):
         """Item-sharded multi-GPU (rs_svd_plan_join; collective over the ranks): comm_id from
         comm_unique_id() on rank 0, sent to every rank."""
@@ -596,6 +605,22 @@ def comm_unique_id() -> bytes:
     buf = C.create_string_buffer(COMM_ID_BYTES)
     _check(lib().rs_comm_unique_id(buf))
     return buf.raw
+
+
+def rotation_step(rank, n_ranks, sub_epoch):
+    """(rank-block trained, send-to rank, rank-block received, recv-from rank) of the ROTATE exchange's
+    sub-epoch (rs_rotation_step; host only)."""
+    out = np.zeros(4, np.int32)
+    _check(lib().rs_rotation_step(rank, n_ranks, sub_epoch, _ptr(out)))
+    return tuple(int(x) for x in out)
+
+
+def comm_info():
+    """(RCCL version code, path of the librccl this process runs against) (rs_comm_info)."""
+    v = _i32(0)
+    buf = C.create_string_buffer(4096)
+    _check(lib().rs_comm_info(C.byref(v), buf, 4096))
+    return v.value, buf.value.decode()
 
 
 def tile_schedule_host(n_users, n_items, rowptr, cols, vals, n_factors, workgroups=256, waves=16,

@@ -1,6 +1,7 @@
-"""Item-sharded and user-sharded multi-GPU schedules (rsgpu.multi): world_size-2 gloo tests on CPU
-with a host model of the plan (the shard's epoch is the oracle's restatement of the fast kernel's
-schedule), checked against a single-process computation of the same merge rule."""
+"""Multi-GPU schedules on CPU: world_size-2/3 gloo tests with a host model of the plan (a shard's epoch is
+the oracle's restatement of the kernel's schedule), checked against a single-process computation of the
+same rule -- the ROTATE exchange (the library's default, its schedule from rs_rotation_step), the
+AVERAGE delta protocol, the user-sharded dual partition and the KNN part split."""
 import os
 import socket
 
@@ -129,6 +130,127 @@ def test_two_rank_gloo_matches_single_process_merge():
         # each rank's item shard equals the shard trained in the single-process run
         mine = multi.item_shard_of(ni, 2) == rank
         np.testing.assert_allclose(Q[mine], plans[rank].Q[mine], atol=1e-6)
+
+
+# ---- ROTATE (the library's default exchange): strata rotation with P rank-blocks sent around ------
+# Host model of rs_svd_plan_epochs_sharded's ROTATE path (csrc/multi.hip) on world_size 2 and 3 over
+# gloo: the schedule is the library's own (rs_rotation_step, host-only C-ABI); a stratum's epoch is the
+# oracle's per-rating SGD (svd.go:93-129) with one work-local GlobalBias; P rank-blocks go to rank g-1
+# by send/recv, GlobalBias partials are all-reduced once per epoch, the rank-blocks broadcast at the end.
+
+def _rot_blocks(u, nu, n):
+    """Rank-blocks of near-equal ratings over all users (the library's user_block_bounds rule)."""
+    cum = np.concatenate([[0], np.cumsum(np.bincount(u, minlength=nu))])
+    return np.array([np.searchsorted(cum, cum[-1] * b // n, side="left") for b in range(n)] + [nu])
+
+
+def _stratum(u, i, r, ub, lo, hi, b):
+    """Ratings of users in rank-block b and items in [lo, hi), user-CSR order (data order per user)."""
+    m = (u >= ub[b]) & (u < ub[b + 1]) & (i >= lo) & (i < hi)
+    order = np.argsort(u[m], kind="stable")
+    return u[m][order], i[m][order], r[m][order]
+
+
+def _train_stratum(P, Q, bu, bi, gb, su, si, sr):
+    """One stratum: the sequential SGD with a work-local GlobalBias; returns its fold partial."""
+    if len(sr) == 0:
+        return P, Q, bu, bi, 0.0
+    P, Q, bu, bi, g = O.svd_fit_works(su, si, sr, np.array([0, len(sr)], np.int64), P, Q, bu, bi, gb, epochs=1)
+    return P, Q, bu, bi, len(sr) * (g - gb)
+
+
+def _rot_worker(rank, world, port, out):
+    import rsgpu
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    u, i, r, nu, ni = make_data(seed=5)
+    rng = np.random.default_rng(4)
+    P, Q = rng.normal(0, 0.1, (nu, K)), rng.normal(0, 0.1, (ni, K))
+    bu, bi, gb = np.zeros(nu), np.zeros(ni), 3.0
+    lo, hi = ni * rank // world, ni * (rank + 1) // world  # this rank's item shard
+    ub = _rot_blocks(u, nu, world)
+    for _ in range(EPOCHS):
+        part = 0.0
+        for st in range(world):
+            train, send_to, recv, recv_from = rsgpu.rotation_step(rank, world, st)
+            P, Q, bu, bi, p = _train_stratum(P, Q, bu, bi, gb, *_stratum(u, i, r, ub, lo, hi, train))
+            part += p
+            a, z = ub[train], ub[train + 1]
+            blk = torch.from_numpy(np.concatenate([P[a:z], bu[a:z, None]], 1).copy())
+            ra, rz = ub[recv], ub[recv + 1]
+            inc = torch.zeros((rz - ra, K + 1), dtype=torch.float64)
+            reqs = [dist.isend(blk, send_to), dist.irecv(inc, recv_from)]
+            for q in reqs:
+                q.wait()
+            P[ra:rz], bu[ra:rz] = inc[:, :K].numpy(), inc[:, K].numpy()
+        t = torch.tensor([part], dtype=torch.float64)
+        dist.all_reduce(t)
+        gb += float(t.item()) / len(r)
+    for b in range(world):  # rank-block b is current on rank b
+        blk = torch.from_numpy(np.concatenate([P[ub[b]:ub[b + 1]], bu[ub[b]:ub[b + 1], None]], 1).copy())
+        dist.broadcast(blk, b)
+        P[ub[b]:ub[b + 1]], bu[ub[b]:ub[b + 1]] = blk[:, :K].numpy(), blk[:, K].numpy()
+    out[rank] = (P, Q[lo:hi], bu, bi[lo:hi], gb)
+    dist.destroy_process_group()
+
+
+def _rot_reference(world):
+    """Single process: the strata in rotation order (sub-epoch, then rank), one GlobalBias fold per epoch."""
+    u, i, r, nu, ni = make_data(seed=5)
+    rng = np.random.default_rng(4)
+    P, Q = rng.normal(0, 0.1, (nu, K)), rng.normal(0, 0.1, (ni, K))
+    bu, bi, gb = np.zeros(nu), np.zeros(ni), 3.0
+    ub = _rot_blocks(u, nu, world)
+    for _ in range(EPOCHS):
+        part = 0.0
+        for st in range(world):
+            for g in range(world):
+                lo, hi = ni * g // world, ni * (g + 1) // world
+                P, Q, bu, bi, p = _train_stratum(P, Q, bu, bi, gb, *_stratum(u, i, r, ub, lo, hi, (g + st) % world))
+                part += p
+        gb += part / len(r)
+    return P, Q, bu, bi, gb, ni
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_gloo_rotation_matches_single_process(world):
+    port = _free_port()
+    with mp.Manager() as m:
+        out = m.dict()
+        mp.spawn(_rot_worker, args=(world, port, out), nprocs=world, join=True)
+        res = dict(out)
+    P, Q, bu, bi, gb, ni = _rot_reference(world)
+    for rank in range(world):
+        rP, rQ, rbu, rbi, rgb = res[rank]
+        lo, hi = ni * rank // world, ni * (rank + 1) // world
+        np.testing.assert_allclose(rP, P, atol=1e-12)
+        np.testing.assert_allclose(rbu, bu, atol=1e-12)
+        np.testing.assert_allclose(rQ, Q[lo:hi], atol=1e-12)
+        np.testing.assert_allclose(rbi, bi[lo:hi], atol=1e-12)
+        assert abs(rgb - gb) < 1e-12
+        np.testing.assert_array_equal(res[0][0], rP)  # P replicated bit for bit after the broadcast
+
+
+def test_rotation_step_covers_every_stratum_once():
+    """rs_rotation_step (the library's schedule): over an epoch every (rank, rank-block) stratum is
+    trained exactly once, no two ranks train one rank-block in the same sub-epoch, and the block a rank
+    receives is the one it trains next (sent by the rank that just trained it)."""
+    import rsgpu
+    for n in (1, 2, 3, 8):
+        seen = set()
+        for st in range(n):
+            trained = set()
+            for g in range(n):
+                train, send_to, recv, recv_from = rsgpu.rotation_step(g, n, st)
+                assert (g, train) not in seen
+                seen.add((g, train))
+                trained.add(train)
+                if st + 1 < n:
+                    assert rsgpu.rotation_step(g, n, st + 1)[0] == recv
+                assert rsgpu.rotation_step(recv_from, n, st)[0] == recv
+                assert rsgpu.rotation_step(send_to, n, st)[3] == g
+            assert len(trained) == n
+        assert len(seen) == n * n
 
 
 # ---- user-sharded (dual) partition: users split by range, item deltas all-reduced ---------------

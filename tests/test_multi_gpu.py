@@ -1,22 +1,30 @@
 """GPU tests of the item-sharded multi-GPU path behind the C-ABI (csrc/multi.hip; north_star's item
-sharding with an all-reduce of user-factor deltas once per epoch, core/svd.go:92-130 per shard).
+sharding, core/svd.go:92-130 per shard).
 
 The one-GPU box runs N shards of one device through the in-process exchange (rs_svd_group with plans
 sharing a device) and the RCCL code with a single rank (rs_svd_group of one device, rs_svd_plan_join
-with n_ranks = 1): the block pipeline, the user weights, the GlobalBias fold and the apply are the
-same code as with 8 GPUs; only the RCCL ring itself is unexercised ("unmeasured on hardware").
+with n_ranks = 1): the schedule, the GlobalBias fold and the final broadcast are the same code as with
+8 GPUs; only RCCL's p2p transfers between two devices are unexercised ("unmeasured on hardware").
 
-Checker: the delta protocol run by hand on plans of the same schedule (one workgroup of one wave:
-deterministic) -- rs_svd_plan_epoch_delta per shard, the shard deltas summed in shard order, and
-rs_svd_plan_apply_delta on every shard -- which test_tile_gpu.py::test_delta_mode_equals_direct pins
-to the plain epoch, itself pinned to the oracle (or_svd_fit_works).
+ROTATE (the default exchange) checker: with one workgroup of one wave per shard the epoch is the
+sequential SGD of svd.go:93-129 over the strata in rotation order -- sub-epoch s, shard g, rank-block
+(g + s) mod N, its tiles in the exported order -- with the work-local GlobalBias fold of the FAST
+schedules; the oracle restates exactly that (or_svd_fit_works).  The strata of one sub-epoch share no
+P or Q row, so their order inside the sub-epoch is immaterial.  Accuracy with the default schedule
+(16 waves): P2, RMSE within 0.003 of the reference visit order at 2, 4 and 8 shards.
+
+AVERAGE (round 2's protocol, selectable): the delta protocol run by hand on plans of the same
+schedule, as before.
 """
+import os
+
 import numpy as np
 import pytest
 
 import oracle as O
 import rsgpu
 from helpers import folds, rmse
+from rsgpu import synth
 
 pytestmark = pytest.mark.gpu
 TOL = 1e-5
@@ -43,17 +51,177 @@ def _bounds(shards, nu, blocks):
     return np.array([np.searchsorted(cum, cum[-1] * b // blocks, side="left") for b in range(blocks)] + [nu])
 
 
-def _plans(ctx, shards, k, P0, Q0, blocks, waves=1, wg=1):
+def _plans(ctx, shards, k, P0, Q0, blocks, waves=1, wg=1, mode=rsgpu.EXCHANGE_ROTATE, gb0=3.5):
     plans = []
     bounds = _bounds(shards, shards[0][3], blocks)
     for su, si, sr, nu, ni_s, lo in shards:
         pl = ctx.svd_plan(rsgpu.Ratings(su, si, sr, nu, ni_s), k)
         pl.set_tiles(workgroups=wg, waves=waves)
         pl.set_user_blocks(blocks, bounds)
-        pl.upload(P0, Q0[lo:lo + ni_s], np.zeros(nu), np.zeros(ni_s), 3.5)
+        pl.set_exchange(mode)
+        pl.upload(P0, Q0[lo:lo + ni_s], np.zeros(nu), np.zeros(ni_s), gb0)
         plans.append(pl)
     return plans
 
+
+def _rotation_oracle(plans, shards, bounds, pieces, P0, Q0, gb0, epochs):
+    """or_svd_fit_works over the strata in rotation order (global user / item ids)."""
+    n = len(plans)
+    strata = {}  # (shard, user block) -> (u, i, r, works)
+    for g, (pl, (su, si, sr, nu, ni_s, lo)) in enumerate(zip(plans, shards)):
+        rowptr, items, rr = O.csr_by(su, nu, si, sr)
+        cu = np.repeat(np.arange(nu, dtype=np.int32), np.diff(rowptr))
+        pos, off = pl.tile_order()
+        uu, ii, r_ = cu[pos], np.asarray(items, np.int32)[pos] + lo, np.asarray(rr)[pos]
+        for w in range(len(off) - 1):
+            if off[w + 1] == off[w]:
+                continue
+            b = int(np.searchsorted(bounds, uu[off[w]], side="right") - 1)
+            strata.setdefault((g, b), []).append((off[w], off[w + 1], uu, ii, r_))
+    U, I, R, W = [], [], [], [0]
+    for st in range(n):
+        for g in range(n):
+            for j in range(pieces):
+                b = ((g + st) % n) * pieces + j
+                for a, z, uu, ii, r_ in strata.get((g, b), []):
+                    U.append(uu[a:z])
+                    I.append(ii[a:z])
+                    R.append(r_[a:z])
+                    W.append(W[-1] + (z - a))
+    U, I, R = np.concatenate(U), np.concatenate(I), np.concatenate(R)
+    return O.svd_fit_works(U, I, R, np.array(W, np.int64), P0, Q0, np.zeros(P0.shape[0]),
+                           np.zeros(Q0.shape[0]), gb0, epochs=epochs)
+
+
+@pytest.mark.parametrize("n_shards,pieces", [(2, 1), (2, 2), (3, 1), (4, 2), (8, 1)])
+def test_rotation_one_wave_equals_oracle(ctx, ml100k, n_shards, pieces):
+    """ROTATE through the in-process exchange (shards on device 0), one wave per shard: equal to the
+    sequential SGD over the strata in rotation order (1e-5), P / b_u / GlobalBias bitwise identical on
+    every shard after the call (the final broadcast)."""
+    f = folds(*ml100k)[2]
+    n = 30000
+    u, i, r, nu, ni = f.iu[:n], f.ii[:n], f.r[:n], f.nu, f.ni
+    k = 24
+    rng = np.random.default_rng(n_shards + 10 * pieces)
+    P0, Q0 = rng.normal(0, 0.1, (nu, k)), rng.normal(0, 0.1, (ni, k))
+    sh = _shards(u, i, r, nu, ni, n_shards)
+    blocks = n_shards * pieces
+    got = _plans(ctx, sh, k, P0, Q0, blocks)
+    g = rsgpu.SvdGroup(got, n_blocks=blocks)
+    g.epochs(2)
+    ref = _rotation_oracle(got, sh, _bounds(sh, nu, blocks), pieces, P0, Q0, 3.5, 2)
+    g.close()
+    b = [pl.download() for pl in got]
+    for pl in got:
+        pl.close()
+    Qg = np.concatenate([x[1] for x in b])
+    big = np.concatenate([x[3] for x in b])
+    assert _maxdiff((ref[0], ref[1], ref[2], ref[3]), (b[0][0], Qg, b[0][2], big)) <= TOL
+    assert abs(ref[4] - b[0][4]) <= 1e-9
+    for y in b[1:]:  # the replicated state is bitwise identical across shards
+        assert np.array_equal(b[0][0], y[0]) and np.array_equal(b[0][2], y[2]) and b[0][4] == y[4]
+
+
+@pytest.mark.parametrize("api", ["group", "join"])
+def test_rccl_single_rank_rotation_equals_oracle(ctx, ml100k, api):
+    """The RCCL exchange (communicator, comm stream, events, GlobalBias fold) with one rank: the
+    rotation degenerates to the user blocks in order, equal to the oracle in tile order (1e-5)."""
+    f = folds(*ml100k)[3]
+    n = 30000
+    u, i, r, nu, ni = f.iu[:n], f.ii[:n], f.r[:n], f.nu, f.ni
+    k = 40
+    rng = np.random.default_rng(11)
+    P0, Q0 = rng.normal(0, 0.1, (nu, k)), rng.normal(0, 0.1, (ni, k))
+    sh = _shards(u, i, r, nu, ni, 1)
+    got = _plans(ctx, sh, k, P0, Q0, 3)
+    if api == "group":
+        g = rsgpu.SvdGroup(got, n_blocks=3)
+        g.epochs(3)
+        ref = _rotation_oracle(got, sh, _bounds(sh, nu, 3), 3, P0, Q0, 3.5, 3)
+        g.close()
+    else:
+        got[0].join(rsgpu.comm_unique_id(), 0, 1, 3)
+        got[0].epochs_sharded(3)
+        ref = _rotation_oracle(got, sh, _bounds(sh, nu, 3), 3, P0, Q0, 3.5, 3)
+        got[0].leave()
+    b = got[0].download()
+    got[0].close()
+    assert _maxdiff(ref[:4], b[:4]) <= TOL and abs(ref[4] - b[4]) <= 1e-9
+
+
+def test_rotation_shard_failure_releases_the_others(ctx, ml100k):
+    """A shard that throws mid-epoch (test hook RSGPU_FAULT_SHARD) makes rs_svd_group_epochs return its
+    error instead of leaving the other shards blocked at the exchange."""
+    f = folds(*ml100k)[0]
+    k = 16
+    rng = np.random.default_rng(3)
+    P0, Q0 = rng.normal(0, 0.1, (f.nu, k)), rng.normal(0, 0.1, (f.ni, k))
+    sh = _shards(f.iu, f.ii, f.r, f.nu, f.ni, 3)
+    plans = _plans(ctx, sh, k, P0, Q0, 3)
+    g = rsgpu.SvdGroup(plans, n_blocks=3)
+    os.environ["RSGPU_FAULT_SHARD"] = "1"
+    try:
+        with pytest.raises(rsgpu.RsError) as e:
+            g.epochs(1)
+    finally:
+        del os.environ["RSGPU_FAULT_SHARD"]
+    assert "shard 1" in str(e.value) or "another shard" in str(e.value)
+    g.close()
+    for pl in plans:
+        pl.close()
+
+
+@pytest.mark.parametrize("n_dev", [2, 8])
+def test_fit_multi_rmse_parity_ml100k(ctx, ml100k, n_dev):
+    """P2 for rs_svd_fit_multi (ROTATE, default tile schedule, 16 waves) with 2 and 8 item shards on
+    device 0: 5-fold ML-100K held-out RMSE within 0.003 of the reference visit order and under
+    core/base_test.go:35's bound (0.934 + 0.008)."""
+    k = 100
+    ref_r, gpu_r = [], []
+    for f in folds(*ml100k):
+        rng = np.random.default_rng(7)
+        P0, Q0 = rng.normal(0, 0.1, (f.nu, k)), rng.normal(0, 0.1, (f.ni, k))
+        ref_r.append(rmse(O.svd_predict(f.tu, f.ti, *O.svd_fit(f.iu, f.ii, f.r, P0, Q0)), f.te_r))
+        got = rsgpu.svd_fit_multi([0] * n_dev, rsgpu.Ratings(f.iu, f.ii, f.r, f.nu, f.ni), P0, Q0)
+        assert all(np.all(np.isfinite(x)) for x in got[:4])
+        gpu_r.append(rmse(O.svd_predict(f.tu, f.ti, *got), f.te_r))
+    g, ref = float(np.mean(gpu_r)), float(np.mean(ref_r))
+    print(f"n_dev={n_dev}: fit_multi RMSE {g:.4f} vs reference order {ref:.4f}")
+    assert abs(g - ref) <= 0.003, (g, ref)
+    assert g <= 0.934 + 0.008
+
+
+_ML1M = {}
+
+
+def _ml1m_holdout():
+    if not _ML1M:
+        u, i, r, nu, ni = synth.ml1m_like()
+        n = len(r)
+        te = np.zeros(n, bool)
+        te[np.random.default_rng(9).permutation(n)[: n // 10]] = True
+        tr = ~te
+        rng = np.random.default_rng(5)
+        P0, Q0 = rng.normal(0, 0.1, (nu, 100)), rng.normal(0, 0.1, (ni, 100))
+        ref = O.svd_fit(u[tr], i[tr], r[tr], P0, Q0, epochs=20)
+        _ML1M.update(u=u, i=i, r=r, nu=nu, ni=ni, tr=tr, te=te, P0=P0, Q0=Q0,
+                     e_ref=rmse(O.svd_predict(u[te], i[te], *ref), r[te]))
+    return _ML1M
+
+
+@pytest.mark.parametrize("n_dev", [2, 4, 8])
+def test_fit_multi_rmse_parity_ml1m_holdout(ctx, n_dev):
+    """P2 at config-2 scale for the sharded fit: ML-1M-shaped set, 90/10 split, k=100, 20 epochs, 2/4/8
+    item shards on device 0; held-out RMSE within 0.003 of the reference visit order's."""
+    d = _ml1m_holdout()
+    u, i, r, tr, te = d["u"], d["i"], d["r"], d["tr"], d["te"]
+    got = rsgpu.svd_fit_multi([0] * n_dev, rsgpu.Ratings(u[tr], i[tr], r[tr], d["nu"], d["ni"]), d["P0"], d["Q0"])
+    e = rmse(rsgpu.svd_predict(u[te], i[te], *got), r[te])
+    print(f"n_dev={n_dev}: ML-1M held-out RMSE {e:.4f} vs reference order {d['e_ref']:.4f}")
+    assert abs(e - d["e_ref"]) <= 0.003, (e, d["e_ref"])
+
+
+# ---- AVERAGE (round 2's delta protocol, selectable) ---------------------------------------------
 
 def _manual(plans, shards, nu, epochs):
     """The delta protocol by hand (torch buffers, sum in shard order)."""
@@ -82,16 +250,16 @@ def _manual(plans, shards, nu, epochs):
 
 
 @pytest.mark.parametrize("n_shards,blocks", [(2, 1), (2, 3), (3, 4)])
-def test_group_on_one_device_equals_manual_protocol(ctx, ml100k, n_shards, blocks):
+def test_average_group_on_one_device_equals_manual_protocol(ctx, ml100k, n_shards, blocks):
     f = folds(*ml100k)[2]
     u, i, r, nu, ni = f.iu, f.ii, f.r, f.nu, f.ni
     k = 24
     rng = np.random.default_rng(n_shards + blocks)
     P0, Q0 = rng.normal(0, 0.1, (nu, k)), rng.normal(0, 0.1, (ni, k))
     sh = _shards(u, i, r, nu, ni, n_shards)
-    ref = _plans(ctx, sh, k, P0, Q0, blocks)
+    ref = _plans(ctx, sh, k, P0, Q0, blocks, mode=rsgpu.EXCHANGE_AVERAGE)
     _manual(ref, sh, nu, epochs=2)
-    got = _plans(ctx, sh, k, P0, Q0, blocks)
+    got = _plans(ctx, sh, k, P0, Q0, blocks, mode=rsgpu.EXCHANGE_AVERAGE)
     g = rsgpu.SvdGroup(got, n_blocks=blocks)
     g.epochs(2)
     g.close()
@@ -101,50 +269,33 @@ def test_group_on_one_device_equals_manual_protocol(ctx, ml100k, n_shards, block
         pl.close()
     for x, y in zip(a, b):
         assert _maxdiff(x[:4], y[:4]) <= TOL and abs(x[4] - y[4]) <= 1e-9
-    for y in b[1:]:  # the replicated state is bitwise identical across shards
+    for y in b[1:]:
         assert np.array_equal(b[0][0], y[0]) and np.array_equal(b[0][2], y[2]) and b[0][4] == y[4]
 
 
-@pytest.mark.parametrize("api", ["group", "join"])
-def test_rccl_single_rank_equals_manual_protocol(ctx, ml100k, api):
-    """The RCCL exchange (communicator, block all-reduces on the comm stream, events) with one rank."""
+def test_average_rccl_single_rank_equals_manual_protocol(ctx, ml100k):
     f = folds(*ml100k)[3]
     u, i, r, nu, ni = f.iu, f.ii, f.r, f.nu, f.ni
     k = 40
     rng = np.random.default_rng(11)
     P0, Q0 = rng.normal(0, 0.1, (nu, k)), rng.normal(0, 0.1, (ni, k))
     sh = _shards(u, i, r, nu, ni, 1)
-    ref = _plans(ctx, sh, k, P0, Q0, 3)
+    ref = _plans(ctx, sh, k, P0, Q0, 3, mode=rsgpu.EXCHANGE_AVERAGE)
     _manual(ref, sh, nu, epochs=3)
-    got = _plans(ctx, sh, k, P0, Q0, 3)
-    if api == "group":
-        g = rsgpu.SvdGroup(got, n_blocks=3)
-        g.epochs(3)
-        g.close()
-    else:
-        got[0].join(rsgpu.comm_unique_id(), 0, 1, 3)
-        got[0].epochs_sharded(3)
-        got[0].leave()
+    got = _plans(ctx, sh, k, P0, Q0, 3, mode=rsgpu.EXCHANGE_AVERAGE)
+    got[0].join(rsgpu.comm_unique_id(), 0, 1, 3)
+    got[0].epochs_sharded(3)
+    got[0].leave()
     a, b = ref[0].download(), got[0].download()
     for pl in ref + got:
         pl.close()
     assert _maxdiff(a[:4], b[:4]) <= TOL and abs(a[4] - b[4]) <= 1e-9
 
 
-def test_fit_multi_rmse_parity_ml100k(ctx, ml100k):
-    """rs_svd_fit_multi with two item shards on device 0 (default tile schedule, 16 waves), 5-fold
-    ML-100K held-out RMSE (core/base_test.go:34-36 data) within 0.01 of the reference visit order.
-    Wider than P2's 0.003 because the north_star protocol itself departs from the sequential epoch:
-    each shard moves p_u over its own ratings only and the count-weighted average of the shard deltas
-    moves a user split over K shards by about 1/K of a sequential epoch's step on its shard-specific
-    part (measured: 0.9422 against 0.9367 with two shards; DESIGN.md "Multi-GPU")."""
-    k = 100
-    ref_r, gpu_r = [], []
-    for f in folds(*ml100k):
-        rng = np.random.default_rng(7)
-        P0, Q0 = rng.normal(0, 0.1, (f.nu, k)), rng.normal(0, 0.1, (f.ni, k))
-        ref_r.append(rmse(O.svd_predict(f.tu, f.ti, *O.svd_fit(f.iu, f.ii, f.r, P0, Q0)), f.te_r))
-        got = rsgpu.svd_fit_multi([0, 0], rsgpu.Ratings(f.iu, f.ii, f.r, f.nu, f.ni), P0, Q0, n_blocks=2)
-        assert all(np.all(np.isfinite(x)) for x in got[:4])
-        gpu_r.append(rmse(O.svd_predict(f.tu, f.ti, *got), f.te_r))
-    assert abs(np.mean(gpu_r) - np.mean(ref_r)) <= 0.01, (np.mean(gpu_r), np.mean(ref_r))
+def test_one_librccl_mapped(ctx):
+    """Exactly one librccl is mapped into the process and the library runs against it."""
+    ver, path = rsgpu.comm_info()
+    maps = open("/proc/self/maps").read().split("\n")
+    libs = {ln.split()[-1] for ln in maps if "librccl" in ln and ln.split()[-1].startswith("/")}
+    assert len(libs) == 1, libs
+    assert os.path.realpath(path) == os.path.realpath(libs.pop()) and ver > 0
