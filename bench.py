@@ -3,10 +3,14 @@
 
 One step = one fast-mode SGD epoch (core/svd.go:92-130) over all 1,000,209 ratings, inputs resident
 in HBM (user-CSR + factors uploaded before the timed region).  N>1 GPUs: one process per GPU
-(torch.distributed for the launch, barriers and the max-over-ranks clock); each rank owns its own
-item-range shard of ML-1M size (weak scaling, the 6040 users replicated) and the library's own RCCL
-communicator (rs_svd_plan_join) all-reduces the user-factor / user-bias / global-bias deltas once
-per epoch, pipelined per user block (north_star item sharding, csrc/multi.hip).
+(torch.distributed for the barriers and the max-over-ranks clock); each rank owns its own item-range
+shard of ML-1M size (weak scaling, the 6040 users shared) and the library's own RCCL communicator
+(rs_svd_plan_join) runs the stratum rotation: N sub-epochs per epoch, P rank-blocks sent to the
+neighbour rank after each (north_star item sharding with the exact exchange, csrc/multi.hip).
+
+Launch: under torch.distributed.run (WORLD_SIZE set) every process is one rank.  `--gpus N` with
+N > 1 and no WORLD_SIZE starts the N rank processes itself from a parent that makes no GPU call, and
+fails when fewer than N GPUs are visible.
 
 Extra fields of the same line:
   strong_scaling  BASELINE configs[4]'s shape at 1/8 scale (1.25M users x 125k items x ~125M ratings,
@@ -110,8 +114,8 @@ def strong_scaling(ctx, rank, world, dist, dev, stream, epochs=3, warmup=1):
                         f"{world} GPU(s)", "scaling": "strong", "n_gpus": world, "epochs": epochs,
             "value": total * epochs / dt, "unit": "updates/s", "ms_per_epoch": dt / epochs * 1e3,
             "setup_s_rank0": setup_s, "finite": finite,
-            "exchange": "rs_svd_plan_join + rs_svd_plan_epochs_sharded (RCCL all-reduce of user deltas, "
-                        "pipelined per user block)" if world > 1 else "none (one GPU)"}
+            "exchange": "rs_svd_plan_join + rs_svd_plan_epochs_sharded (stratum rotation: RCCL send/recv "
+                        "of P rank-blocks, piece by piece)" if world > 1 else "none (one GPU)"}
 
 
 def ordered_throughput(ctx, u, i, r, n_users, n_items):
@@ -138,6 +142,46 @@ def load_traffic():
     return None
 
 
+def spawn_ranks(n, argv, need_gpus=True):
+    """`--gpus n` without a launcher: n rank processes (RANK / LOCAL_RANK / WORLD_SIZE / MASTER_*),
+    started from this parent, which touches no GPU (device_count does not initialise HIP here)."""
+    import socket
+    import subprocess
+    if need_gpus:
+        import torch
+        visible = torch.cuda.device_count()
+        if visible < n:
+            sys.exit(f"bench.py --gpus {n}: only {visible} GPU(s) visible")
+    with socket.socket() as so:
+        so.bind(("127.0.0.1", 0))
+        port = so.getsockname()[1]
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), HSA_ENABLE_IPC_MODE_LEGACY="0")
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + argv, env=env))
+    rcs = [p.wait() for p in procs]
+    sys.exit(next((c for c in rcs if c != 0), 0))
+
+
+def launch_check(gpus):
+    """Every rank joins a gloo group and all-reduces its rank; rank 0 prints what the group saw."""
+    import torch
+    import torch.distributed as dist
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    if world > 1:
+        dist.init_process_group("gloo")
+    t = torch.tensor([float(rank), 1.0], dtype=torch.float64)
+    if world > 1:
+        dist.all_reduce(t)
+    if rank == 0:
+        print(json.dumps({"gpus": gpus, "world": world, "rank_sum": int(t[0]), "ranks": int(t[1]),
+                          "local_rank0": int(os.environ.get("LOCAL_RANK", "0"))}), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -147,7 +191,14 @@ def main():
     ap.add_argument("--cpu-budget", type=float, default=10.0)
     ap.add_argument("--no-strong", action="store_true", help="skip the configs[4]-shape strong-scaling field")
     ap.add_argument("--no-ordered", action="store_true", help="skip the ORDERED-mode field")
+    ap.add_argument("--launch-check", action="store_true",
+                    help="CPU check of the N-rank launch: gloo ranks report themselves, no GPU work")
     args = ap.parse_args()
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        spawn_ranks(args.gpus, sys.argv[1:], need_gpus=not args.launch_check)
+    if args.launch_check:
+        launch_check(args.gpus)
+        return
 
     import torch
     import rsgpu
@@ -156,6 +207,8 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        sys.exit(f"bench.py --gpus {args.gpus} launched with WORLD_SIZE={world}")
     dist = None
     if world > 1:
         import torch.distributed as dist
@@ -180,9 +233,12 @@ def main():
         uid = [rsgpu.comm_unique_id() if rank == 0 else None]
         dist.broadcast_object_list(uid, src=0)
         plan.join(uid[0], rank, world)
+        comm_rank, comm_ranks, _, comm_blocks = plan.shard_info()
         run = lambda n: plan.epochs_sharded(n, LR, REG, stream)
     else:
+        comm_ranks, comm_blocks = 1, 1
         run = lambda n: plan.epochs(n, LR, REG, stream)
+    rccl_version, rccl_path = rsgpu.comm_info()
 
     for _ in range(args.warmup):
         run(1)
@@ -224,6 +280,8 @@ def main():
             "value": total_updates / dt,
             "unit": "updates/s",
             "n_gpus": world,
+            "nranks": comm_ranks,  # as the library's RCCL communicator reports it (1: no communicator)
+            "rccl": {"version": rccl_version, "path": rccl_path},
             "steps": args.steps,
             "warmup": args.warmup,
             "ms_per_step": dt / args.steps * 1e3,
@@ -240,8 +298,9 @@ def main():
                                    "per step (BASELINE configs[1])",
                        "n_users": n_users, "n_items_per_rank": n_items, "nnz_per_rank": nnz,
                        "n_factors": K, "lr": LR, "reg": REG,
-                       "parallelism": f"item-sharded x{world} (RCCL all-reduce of user deltas, "
-                                      "pipelined per user block)" if world > 1 else "single GPU"},
+                       "parallelism": f"item-sharded x{world}: stratum rotation, {comm_blocks} user blocks "
+                                      "(RCCL send/recv of P rank-blocks per sub-epoch)" if world > 1
+                                      else "single GPU"},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
                          "traffic": traffic,

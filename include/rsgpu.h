@@ -363,6 +363,10 @@ int rs_svd_plan_set_exchange(rs_svd_plan* plan, int32_t mode);
  * it.  The schedule rs_svd_plan_epochs_sharded runs. */
 int rs_rotation_step(int32_t rank, int32_t n_ranks, int32_t sub_epoch, int32_t* out /* 4 */);
 int rs_comm_info(int32_t* version, char* path, int32_t path_len);
+/* A joined plan's rank and rank count (from the RCCL communicator when there is one), its exchange and
+ * its user blocks in all (any pointer may be NULL). */
+int rs_svd_plan_shard_info(rs_svd_plan* plan, int32_t* rank, int32_t* n_ranks, int32_t* exchange,
+                           int32_t* n_blocks);
 #define RS_COMM_ID_BYTES 128
 int rs_comm_unique_id(void* id /* RS_COMM_ID_BYTES */);
 int rs_svd_plan_join(rs_svd_plan* plan, const void* id, int32_t rank, int32_t n_ranks, int32_t n_blocks);

@@ -277,6 +277,69 @@ void or_svdpp_fit(int64_t n, const int32_t* u, const int32_t* i, const double* r
     free(pos);
 }
 
+/* or_svdpp_fit with the reference's own parallelism (CPU baseline only): svd.go:399-422 splits the
+ * y-update loop of EVERY rating over nJobs goroutines (contiguous ranges [nRating*j/nJobs,
+ * nRating*(j+1)/nJobs)) and waits for them (wg.Wait) before the next rating; restated as one OpenMP
+ * fork/join per rating with the same static contiguous split.  Same arithmetic per element.  Each epoch
+ * visits the first n_visit ratings (n_visit = n: the whole epoch; less: a timed slice of it, N(u) still
+ * over all n ratings). */
+void or_svdpp_fit_jobs(int64_t n, const int32_t* u, const int32_t* i, const double* r,
+                       int32_t n_users, int32_t k, int32_t epochs, double lr, double reg, double* P,
+                       double* Q, double* Y, double* bu, double* bi, double* gb, int32_t n_jobs,
+                       int64_t n_visit) {
+    int64_t *rowptr, *pos;
+    build_user_csr(n, u, n_users, &rowptr, &pos);
+    double* e = (double*)malloc((size_t)k * sizeof(double));
+    double GB = *gb;
+    if (n_visit > n) n_visit = n;
+    for (int32_t epoch = 0; epoch < epochs; epoch++) {
+        for (int64_t t = 0; t < n_visit; t++) {
+            const int32_t uu = u[t], ii = i[t];
+            const double userBias = bu[uu], itemBias = bi[ii];
+            double* pu = P + (int64_t)uu * k;
+            double* qi = Q + (int64_t)ii * k;
+            double pred = GB;
+            pred += bu[uu];
+            pred += bi[ii];
+            ensemble(rowptr, pos, i, uu, k, Y, e);
+            double s = 0.0;
+            for (int32_t f = 0; f < k; f++) {
+                double tmp = 0.0;
+                tmp = tmp + pu[f];
+                tmp = tmp + e[f];
+                s += tmp * qi[f];
+            }
+            pred += s;
+            const double diff = pred - r[t];
+            GB -= lr * diff;
+            bu[uu] -= lr * (diff + reg * userBias);
+            bi[ii] -= lr * (diff + reg * itemBias);
+            for (int32_t f = 0; f < k; f++) pu[f] = pu[f] - (qi[f] * diff + pu[f] * reg) * lr;
+            for (int32_t f = 0; f < k; f++) qi[f] = qi[f] - ((pu[f] + e[f]) * diff + qi[f] * reg) * lr;
+            const int64_t b0 = rowptr[uu], nr = rowptr[uu + 1] - b0;
+            const double sq = sqrt((double)nr);
+#pragma omp parallel for num_threads(n_jobs) schedule(static)
+            for (int32_t j = 0; j < n_jobs; j++) {          /* svd.go:402-420: one goroutine per job */
+                for (int64_t x = b0 + nr * j / n_jobs; x < b0 + nr * (j + 1) / n_jobs; x++) {
+                    double* y = Y + (int64_t)i[pos[x]] * k;
+                    for (int32_t f = 0; f < k; f++) {
+                        double a = qi[f] * diff;
+                        a = a / sq;
+                        double b = y[f] * reg;
+                        a = a + b;
+                        a = a * lr;
+                        y[f] = y[f] - a;
+                    }
+                }
+            }
+        }
+    }
+    *gb = GB;
+    free(e);
+    free(rowptr);
+    free(pos);
+}
+
 void or_svdpp_predict(int64_t n_train, const int32_t* tu, const int32_t* ti, int32_t n_users,
                       int64_t n, const int32_t* u, const int32_t* i, int32_t k, const double* P,
                       const double* Q, const double* Y, const double* bu, const double* bi,
@@ -503,6 +566,19 @@ void or_knn_sims(int32_t kind, int32_t L, const int64_t* rowptr, const int32_t* 
 
 void or_knn_sims_rows(int32_t kind, int32_t L, const int64_t* rowptr, const int32_t* sid,
                       const double* sr, int32_t row_begin, int32_t row_end, double* out) {
+    for (int32_t a = row_begin; a < row_end; a++)
+        for (int32_t b = 0; b < L; b++)
+            out[(int64_t)(a - row_begin) * L + b] =
+                a == b ? NAN
+                       : or_sim(kind, rowptr[a + 1] - rowptr[a], sid + rowptr[a], sr + rowptr[a],
+                                rowptr[b + 1] - rowptr[b], sid + rowptr[b], sr + rowptr[b]);
+}
+
+/* or_knn_sims_rows on n_jobs threads (CPU baseline only): the rows split into contiguous ranges as
+ * knn.go:192-216 splits them over its nJobs goroutines, every row against every partner. */
+void or_knn_sims_rows_mt(int32_t kind, int32_t L, const int64_t* rowptr, const int32_t* sid,
+                         const double* sr, int32_t row_begin, int32_t row_end, int32_t n_jobs, double* out) {
+#pragma omp parallel for num_threads(n_jobs) schedule(static)
     for (int32_t a = row_begin; a < row_end; a++)
         for (int32_t b = 0; b < L; b++)
             out[(int64_t)(a - row_begin) * L + b] =

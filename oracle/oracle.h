@@ -141,6 +141,14 @@ void or_svdpp_fit_userwise(int32_t n_users, const int64_t* rowptr, const int32_t
                            const double* r, int32_t k, int32_t epochs, double lr, double reg,
                            double* P, double* Q, double* Y, double* bu, double* bi, double* gb);
 
+/* CPU baselines with the reference's own goroutine fan-out, restated with OpenMP (bench only). */
+void or_svdpp_fit_jobs(int64_t n, const int32_t* u, const int32_t* i, const double* r,
+                       int32_t n_users, int32_t k, int32_t epochs, double lr, double reg, double* P,
+                       double* Q, double* Y, double* bu, double* bi, double* gb, int32_t n_jobs,
+                       int64_t n_visit);
+void or_knn_sims_rows_mt(int32_t kind, int32_t L, const int64_t* rowptr, const int32_t* sid,
+                         const double* sr, int32_t row_begin, int32_t row_end, int32_t n_jobs, double* out);
+
 #ifdef __cplusplus
 }
 #endif

@@ -76,6 +76,11 @@ def lib():
                                          _f64p, _dp]
         L.or_knn_sims_rows.argtypes = [C.c_int32, C.c_int32, _i64p, _i32p, _f64p, C.c_int32,
                                        C.c_int32, _f64p]
+        L.or_knn_sims_rows_mt.argtypes = [C.c_int32, C.c_int32, _i64p, _i32p, _f64p, C.c_int32,
+                                          C.c_int32, C.c_int32, _f64p]
+        L.or_svdpp_fit_jobs.argtypes = [C.c_int64, _i32p, _i32p, _f64p, C.c_int32, C.c_int32,
+                                        C.c_int32, C.c_double, C.c_double, _f64p, _f64p, _f64p,
+                                        _f64p, _f64p, _dp, C.c_int32, C.c_int64]
         L.or_gb_warm_start.argtypes = [C.c_int32, _i64p, _i32p, _f64p, _f64p, _f64p]
         L.or_gb_warm_start.restype = C.c_double
         L.or_slope_one_fit.argtypes = [C.c_int32, _i64p, _i32p, _f64p, _f64p]
@@ -265,6 +270,34 @@ def knn_sims(kind, rowptr, ids, ratings):
     out = np.empty((L, L))
     lib().or_knn_sims(kind, L, _i64(rowptr), _i32(ids), _f64(ratings), out)
     return out
+
+
+def knn_sims_rows_mt(kind, rowptr, sorted_ids, sorted_r, row_begin, row_end, n_jobs):
+    """knn_sims_rows on n_jobs threads, rows split as knn.go:192-216 splits them (CPU baseline)."""
+    L = len(rowptr) - 1
+    out = np.empty((row_end - row_begin, L))
+    lib().or_knn_sims_rows_mt(kind, L, _i64(rowptr), _i32(sorted_ids), _f64(sorted_r), row_begin,
+                              row_end, n_jobs, out)
+    return out
+
+
+def svdpp_fit_jobs(u, i, r, n_users, P, Q, Y, epochs=1, lr=0.007, reg=0.02, n_jobs=1):
+    """svdpp_fit with svd.go:399-422's per-rating nJobs split of the y-update (CPU baseline)."""
+    P, Q, Y = _f64(P).copy(), _f64(Q).copy(), _f64(Y).copy()
+    bu, bi = np.zeros(P.shape[0]), np.zeros(Q.shape[0])
+    g = C.c_double(0.0)
+    lib().or_svdpp_fit_jobs(len(r), _i32(u), _i32(i), _f64(r), n_users, P.shape[1], epochs, lr, reg,
+                            P, Q, Y, bu, bi, C.byref(g), n_jobs, len(r))
+    return P, Q, Y, bu, bi, g.value
+
+
+def svdpp_fit_sample(u, i, r, n_users, P, Q, Y, n_visit, lr=0.007, reg=0.02, n_jobs=1):
+    """The first n_visit ratings of one svdpp_fit_jobs epoch, N(u) over all ratings (a timed slice)."""
+    P, Q, Y = _f64(P).copy(), _f64(Q).copy(), _f64(Y).copy()
+    bu, bi = np.zeros(P.shape[0]), np.zeros(Q.shape[0])
+    g = C.c_double(0.0)
+    lib().or_svdpp_fit_jobs(len(r), _i32(u), _i32(i), _f64(r), n_users, P.shape[1], 1, lr, reg,
+                            P, Q, Y, bu, bi, C.byref(g), n_jobs, n_visit)
 
 
 def knn_sims_rows(kind, rowptr, sorted_ids, sorted_r, row_begin, row_end):

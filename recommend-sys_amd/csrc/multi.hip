@@ -569,6 +569,25 @@ extern "C" int rs_rotation_step(int32_t rank, int32_t n_ranks, int32_t sub_epoch
     return RS_OK;
 }
 
+extern "C" int rs_svd_plan_shard_info(rs_svd_plan* pl, int32_t* rank, int32_t* n_ranks, int32_t* exchange,
+                                      int32_t* n_blocks) {
+    if (!pl) return rs::set_error(nullptr, RS_ERR_INVALID, "plan is NULL");
+    return rs_guard(pl->ctx, [&]() -> int {
+        if (!pl->shard) return rs::set_error(pl->ctx, RS_ERR_INVALID, "plan is not joined");
+        const rs::ShardComm& c = *pl->shard;
+        int r = c.rank, n = c.nranks;
+        if (c.nccl) {  // what the communicator itself reports
+            rs::check_nccl(ncclCommUserRank(c.nccl, &r), "ncclCommUserRank");
+            rs::check_nccl(ncclCommCount(c.nccl, &n), "ncclCommCount");
+        }
+        if (rank) *rank = r;
+        if (n_ranks) *n_ranks = n;
+        if (exchange) *exchange = c.mode;
+        if (n_blocks) *n_blocks = static_cast<int32_t>(pl->t_block_tile.size()) - 1;
+        return RS_OK;
+    });
+}
+
 extern "C" int rs_comm_info(int32_t* version, char* path, int32_t path_len) {
     return rs_guard(nullptr, [&]() -> int {
         if (version) {

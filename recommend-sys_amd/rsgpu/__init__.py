@@ -44,7 +44,7 @@ HEADER_SYMBOLS = (
     "rs_comm_unique_id", "rs_svd_plan_join", "rs_svd_plan_epochs_sharded", "rs_svd_plan_leave",
     "rs_svd_plan_set_user_blocks", "rs_svd_group_create", "rs_svd_group_epochs", "rs_svd_group_destroy",
     "rs_item_shards", "rs_svd_fit_multi", "rs_tile_schedule_host", "rs_svd_plan_set_exchange",
-    "rs_comm_info", "rs_rotation_step",
+    "rs_comm_info", "rs_rotation_step", "rs_svd_plan_shard_info",
 )
 COMM_ID_BYTES = 128
 
@@ -164,6 +164,8 @@ def lib():
             "rs_svd_plan_set_exchange": (C.c_int, [_vp, _i32]),
             "rs_comm_info": (C.c_int, [C.POINTER(_i32), _vp, _i32]),
             "rs_rotation_step": (C.c_int, [_i32, _i32, _i32, _vp]),
+            "rs_svd_plan_shard_info": (C.c_int, [_vp, C.POINTER(_i32), C.POINTER(_i32), C.POINTER(_i32),
+                                                 C.POINTER(_i32)]),
         }
         for name, (res, args) in sig.items():
             f = getattr(L, name)
@@ -463,6 +465,12 @@ class SvdPlan:
         assert len(comm_id) == COMM_ID_BYTES
         buf = C.create_string_buffer(bytes(comm_id), COMM_ID_BYTES)
         self.ctx.check(lib().rs_svd_plan_join(self.h, buf, rank, n_ranks, n_blocks))
+
+    def shard_info(self):
+        """(rank, n_ranks, exchange, user blocks) of a joined plan; ranks from the RCCL communicator."""
+        v = [_i32(0) for _ in range(4)]
+        self.ctx.check(lib().rs_svd_plan_shard_info(self.h, *[C.byref(x) for x in v]))
+        return tuple(x.value for x in v)
 
     def epochs_sharded(self, n, lr=0.005, reg=0.02, stream=None):
         self.ctx.check(lib().rs_svd_plan_epochs_sharded(self.h, n, lr, reg, stream))

@@ -26,6 +26,9 @@ import time
 import numpy as np
 
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+# the oracle's nJobs restatements fork/join once per rating (svd.go:399-422): spinning OpenMP workers
+# stand in for Go's spinning scheduler threads (a sleeping pool would charge a wake-up per rating)
+os.environ.setdefault("OMP_WAIT_POLICY", "ACTIVE")
 sys.path[:0] = [os.path.join(REPO, "recommend-sys_amd"), os.path.join(REPO, "oracle")]
 
 HBM_PEAK = 8000.0      # GB/s, MI355X_MICROARCH.md chip table
@@ -50,6 +53,13 @@ def host_info():
     except OSError:
         pass
     return {"nproc": os.cpu_count(), "cpu_model": model}
+
+
+def cpu_jobs():
+    """Threads for the reference's nJobs = runtime.NumCPU() fan-out: the CPUs this process may use,
+    capped at the box's per-GPU share (OMP_NUM_THREADS, 16 on the GPU box)."""
+    avail = len(os.sched_getaffinity(0))
+    return max(1, min(avail, int(os.environ.get("OMP_NUM_THREADS", "16") or 16)))
 
 
 def config0(ctx, out, k=20, epochs=20):
@@ -103,22 +113,28 @@ def config2(ctx, out, epochs=5):
     ms = ctx.last_kernel_ms() / epochs
     nnz = len(r)
     ab = nnz * (16 + 8 * k) + nu * (16 + 8 * k) + nnz * (4 + 12 * k)
-    # CPU: literal svd.go:316-427 restatement on the first 3000 ratings (cost per rating depends on
-    # |N(u)| of the rated user; the shuffled prefix is a uniform sample), extrapolated to an epoch
-    m = 3000
+    # CPU: the literal svd.go:316-427 restatement with the reference's own parallelism -- the y-update
+    # of every rating split over nJobs threads (svd.go:399-422, one fork/join per rating) -- on a
+    # uniform sample of the epoch: ratings of the shuffled set with their FULL N(u) (the epoch's
+    # per-rating cost depends only on |N(u)|), timed as a slice of a real epoch
+    jobs = cpu_jobs()
+    m = 4000
     t0 = time.perf_counter()
-    O.svdpp_fit(u[:m], i[:m], r[:m], nu, P0, Q0, Y0, epochs=1)
-    # the prefix's N(u) are the prefix's own ratings: rescale by the full-set |N(u)| ratio
-    deg_full = np.bincount(u, minlength=nu)[u[:m]].mean()
-    deg_pref = np.bincount(u[:m], minlength=nu)[u[:m]].mean()
-    t_rating = (time.perf_counter() - t0) / m * (deg_full / deg_pref)
+    O.svdpp_fit_sample(u, i, r, nu, P0, Q0, Y0, m, n_jobs=jobs)
+    t_rating = (time.perf_counter() - t0) / m
+    t0 = time.perf_counter()
+    O.svdpp_fit_sample(u, i, r, nu, P0, Q0, Y0, m // 4, n_jobs=1)
+    t_rating1 = (time.perf_counter() - t0) / (m // 4)
     emit({"config": "SVD++ nFactors=128 ML-1M-shaped (BASELINE configs[2])", "kernel": "svdpp_epoch_fast_kernel<E=3,D=8>",
           "updates_per_s": nnz / (ms / 1e3), "epoch_ms_kernel": ms, "fit_wall_s": wall,
           "roofline": {"bound": "hbm", "achieved_GBs": ab / (ms / 1e3) / 1e9, "peak_GBs": HBM_PEAK,
                        "frac": ab / (ms / 1e3) / 1e9 / HBM_PEAK, "algorithmic_bytes": ab},
-          "cpu_baseline": {"value": 1.0 / t_rating, "unit": "updates/s", "cores": 1, "kind": "port",
-                           "sample": f"literal svd.go:352-424 restatement, {m} ratings, cost scaled to "
-                                     f"full-set |N(u)| (x{deg_full / deg_pref:.1f})"}}, out)
+          "cpu_baseline": {"value": 1.0 / t_rating, "unit": "updates/s", "cores": jobs, "kind": "port",
+                           "sample": f"literal svd.go:352-424 restatement with svd.go:399-422's nJobs = {jobs} "
+                                     f"split of every rating's y-update (OpenMP fork/join per rating), the first "
+                                     f"{m} ratings of the shuffled ML-1M-shaped epoch against the full N(u); "
+                                     f"1 thread: {1.0 / t_rating1:.3g} updates/s",
+                           **host_info()}}, out)
 
 
 def config3(ctx, out):
@@ -141,13 +157,14 @@ def config3(ctx, out):
     kpad = (R + 63) // 64 * 64
     executed = 3 * 2 * (T * (T + 1) // 2) * 128 * 128 * kpad     # 3 int8 contractions, triangle tiles
     algorithmic = 2 * 2 * L * (L + 1) // 2 * R                    # G=2, unique pairs
-    # CPU: the reference-style merge (sim.go:10-25) for rows [0, 64) against every partner,
-    # extrapolated to the unique pairs of the full matrix (knn.go skips computed mirrors)
+    # CPU: the reference-style merge (sim.go:10-25) on nJobs threads over a 512-row block (knn.go:192-216
+    # splits the rows into contiguous ranges, one per goroutine), every row against every partner,
+    # extrapolated to the unique pairs of the full matrix (knn.go skips computed mirrors) -- BASELINE.md
     srt = np.lexsort((ids, np.repeat(np.arange(L), np.diff(rowptr))))
     sid, sr = ids[srt], rr[srt]
-    rows = 64
+    rows, jobs = 512, cpu_jobs()
     t0 = time.perf_counter()
-    blk = O.knn_sims_rows(O.COSINE, rowptr, sid, sr, 0, rows)
+    blk = O.knn_sims_rows_mt(O.COSINE, rowptr, sid, sr, 0, rows, jobs)
     t_blk = time.perf_counter() - t0
     t_full = t_blk * (L / rows) / 2
     same = np.array_equal(np.isnan(blk), np.isnan(S[:rows])) and np.array_equal(
@@ -161,11 +178,12 @@ def config3(ctx, out):
                        "peak_TOPs": I8_PEAK, "frac": algorithmic / (ms / 1e3) / 1e12 / I8_PEAK,
                        "frac_executed": executed / (ms / 1e3) / 1e12 / I8_PEAK,
                        "executed_int8_ops": executed, "algorithmic_int8_ops": algorithmic},
-          "parity_rows_0_63_bitwise": bool(same),
-          "cpu_baseline": {"value": L * (L - 1) / 2 / t_full, "unit": "pairs/s", "cores": 1,
+          "parity_rows_0_511_bitwise": bool(same),
+          "cpu_baseline": {"value": L * (L - 1) / 2 / t_full, "unit": "pairs/s", "cores": jobs,
                            "kind": "port", "sample": f"rows 0-{rows - 1} x {L} partners, merge "
-                           f"restatement {t_blk:.1f} s, extrapolated x{L / rows / 2:.0f} to the "
-                           f"unique pairs ({t_full:.0f} s)"}}, out)
+                           f"restatement on {jobs} threads (knn.go:192-216's contiguous row split) "
+                           f"{t_blk:.1f} s, extrapolated x{L / rows / 2:.1f} to the unique pairs "
+                           f"({t_full:.0f} s)", **host_info()}}, out)
 
 
 def config4(ctx, out, epochs=5):

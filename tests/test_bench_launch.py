@@ -1,0 +1,38 @@
+"""bench.py's multi-GPU launch on CPU: `--gpus N` without a launcher starts N rank processes (RANK /
+LOCAL_RANK / WORLD_SIZE / MASTER_* set by the parent, which makes no GPU call); --launch-check makes
+every rank join a gloo group instead of running the GPU bench."""
+import json
+import os
+import subprocess
+import sys
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _run(args, env=None):
+    e = dict(os.environ)
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT"):
+        e.pop(k, None)
+    e.update(env or {})
+    return subprocess.run([sys.executable, os.path.join(REPO, "bench.py")] + args, capture_output=True, text=True,
+                          timeout=300, env=e, cwd=REPO)
+
+
+def test_two_rank_self_launch():
+    r = _run(["--gpus", "2", "--launch-check"])
+    assert r.returncode == 0, r.stderr
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1  # rank 0 only
+    d = json.loads(lines[0])
+    assert d == {"gpus": 2, "world": 2, "rank_sum": 1, "ranks": 2, "local_rank0": 0}
+
+
+def test_too_few_gpus_fails_loudly():
+    """No GPU in this container: --gpus 2 (a real run) must refuse, not fall back to one device."""
+    r = _run(["--gpus", "2"])
+    assert r.returncode != 0 and "GPU(s) visible" in r.stderr
+
+
+def test_world_size_must_match_gpus():
+    r = _run(["--gpus", "2"], env={"WORLD_SIZE": "1", "RANK": "0", "LOCAL_RANK": "0"})
+    assert r.returncode != 0 and "WORLD_SIZE=1" in r.stderr

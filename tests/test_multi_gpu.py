@@ -117,7 +117,7 @@ def test_rotation_one_wave_equals_oracle(ctx, ml100k, n_shards, pieces):
     Qg = np.concatenate([x[1] for x in b])
     big = np.concatenate([x[3] for x in b])
     assert _maxdiff((ref[0], ref[1], ref[2], ref[3]), (b[0][0], Qg, b[0][2], big)) <= TOL
-    assert abs(ref[4] - b[0][4]) <= 1e-9
+    assert abs(ref[4] - b[0][4]) <= TOL  # a run's GlobalBias steps are summed in fp32 (sgd_tile.hip)
     for y in b[1:]:  # the replicated state is bitwise identical across shards
         assert np.array_equal(b[0][0], y[0]) and np.array_equal(b[0][2], y[2]) and b[0][4] == y[4]
 
@@ -146,7 +146,7 @@ def test_rccl_single_rank_rotation_equals_oracle(ctx, ml100k, api):
         got[0].leave()
     b = got[0].download()
     got[0].close()
-    assert _maxdiff(ref[:4], b[:4]) <= TOL and abs(ref[4] - b[4]) <= 1e-9
+    assert _maxdiff(ref[:4], b[:4]) <= TOL and abs(ref[4] - b[4]) <= TOL
 
 
 def test_rotation_shard_failure_releases_the_others(ctx, ml100k):
