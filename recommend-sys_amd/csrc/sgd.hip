@@ -2069,46 +2069,58 @@ extern "C" int rs_svd_fit(rs_ctx* ctx, const rs_ratings* r, const rs_sgd_params*
             mark("download");
             return RS_OK;
         }
-        // ORDERED: COO in train-set order, one group, all epochs in one launch.
+        // ORDERED: COO in train-set order, one wave, all epochs in one launch (sgd_ordered.hip), rows in the
+        // folded layout P [p, b_u, 1], Q [q, 1, b_i]
         hipStream_t s = ctx->stream;
-        const int32_t k = p->n_factors, ld = rs::round_up4(k);
+        const int32_t k = p->n_factors, ld = rs::round_up4(k + 2);
         const int64_t nnz = r->nnz;
-        rs::DevBuf<int32_t> du(std::max<int64_t>(1, nnz)), di(std::max<int64_t>(1, nnz));
-        rs::DevBuf<float> dr(std::max<int64_t>(1, nnz));
-        std::vector<float> rf(static_cast<size_t>(nnz));
+        const int64_t npad = rs::ordered_padded(nnz);  // whole blocks for the kernel's scalar id loads
+        rs::DevBuf<int32_t> du(npad), di(npad);
+        rs::DevBuf<float> dr(npad);
+        std::vector<float> rf(static_cast<size_t>(npad), 0.f);
         for (int64_t t = 0; t < nnz; ++t) rf[t] = static_cast<float>(r->ratings[t]);
+        RS_HIP(hipMemsetAsync(du.p, 0, npad * sizeof(int32_t), s));
+        RS_HIP(hipMemsetAsync(di.p, 0, npad * sizeof(int32_t), s));
         du.upload(r->users, nnz, s);
         di.upload(r->items, nnz, s);
-        dr.upload(rf.data(), nnz, s);
-        rs::DevBuf<float> dP(static_cast<size_t>(std::max(1, r->n_users)) * ld);
-        rs::DevBuf<float> dQ(static_cast<size_t>(std::max(1, r->n_items)) * ld);
-        rs::DevBuf<float> dbu(std::max(1, r->n_users)), dbi(std::max(1, r->n_items));
+        dr.upload(rf.data(), npad, s);
+        const int64_t pn = static_cast<int64_t>(std::max(1, r->n_users)) * ld, qn = static_cast<int64_t>(std::max(1, r->n_items)) * ld;
+        rs::DevBuf<float> dP(pn), dQ(qn);
         rs::DevBuf<double> dgb(1);
-        std::vector<float> hP, hQ, hbu, hbi;
-        rs::pack_rows_f32(P, r->n_users, k, ld, hP);
-        rs::pack_rows_f32(Q, r->n_items, k, ld, hQ);
-        rs::pack_rows_f32(bu, r->n_users, 1, 1, hbu);
-        rs::pack_rows_f32(bi, r->n_items, 1, 1, hbi);
+        std::vector<float> hP(static_cast<size_t>(pn), 0.f), hQ(static_cast<size_t>(qn), 0.f);
+        for (int32_t x = 0; x < r->n_users; ++x) {
+            float* row = hP.data() + static_cast<int64_t>(x) * ld;
+            for (int32_t f = 0; f < k; ++f) row[f] = static_cast<float>(P[static_cast<int64_t>(x) * k + f]);
+            row[k] = static_cast<float>(bu[x]);
+            row[k + 1] = 1.f;
+        }
+        for (int32_t x = 0; x < r->n_items; ++x) {
+            float* row = hQ.data() + static_cast<int64_t>(x) * ld;
+            for (int32_t f = 0; f < k; ++f) row[f] = static_cast<float>(Q[static_cast<int64_t>(x) * k + f]);
+            row[k] = 1.f;
+            row[k + 1] = static_cast<float>(bi[x]);
+        }
         dP.upload(hP.data(), hP.size(), s);
         dQ.upload(hQ.data(), hQ.size(), s);
-        dbu.upload(hbu.data(), hbu.size(), s);
-        dbi.upload(hbi.data(), hbi.size(), s);
         dgb.upload(gb, 1, s);
         rs::kernel_span_begin(ctx);
         if (nnz > 0 && p->n_epochs > 0)
-            rs::launch_ordered(nnz, du.p, di.p, dr.p, dP.p, dQ.p, dbu.p, dbi.p, ld, dgb.p,
-                               p->n_epochs, lr, reg, s);
+            rs::ordered_epochs(du.p, di.p, dr.p, nnz, dP.p, pn, dQ.p, qn, ld, k, dgb.p, p->n_epochs, lr, reg, s);
         rs::kernel_span_end(ctx);
         dP.download(hP.data(), hP.size(), s);
         dQ.download(hQ.data(), hQ.size(), s);
-        dbu.download(hbu.data(), hbu.size(), s);
-        dbi.download(hbi.data(), hbi.size(), s);
         dgb.download(gb, 1, s);
         RS_HIP(hipStreamSynchronize(s));
-        rs::unpack_rows_f64(hP, r->n_users, k, ld, P);
-        rs::unpack_rows_f64(hQ, r->n_items, k, ld, Q);
-        rs::unpack_rows_f64(hbu, r->n_users, 1, 1, bu);
-        rs::unpack_rows_f64(hbi, r->n_items, 1, 1, bi);
+        for (int32_t x = 0; x < r->n_users; ++x) {
+            const float* row = hP.data() + static_cast<int64_t>(x) * ld;
+            for (int32_t f = 0; f < k; ++f) P[static_cast<int64_t>(x) * k + f] = row[f];
+            bu[x] = row[k];
+        }
+        for (int32_t x = 0; x < r->n_items; ++x) {
+            const float* row = hQ.data() + static_cast<int64_t>(x) * ld;
+            for (int32_t f = 0; f < k; ++f) Q[static_cast<int64_t>(x) * k + f] = row[f];
+            bi[x] = row[k + 1];
+        }
         return RS_OK;
     });
 }

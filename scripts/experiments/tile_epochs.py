@@ -50,6 +50,15 @@ if os.environ.get("RSGPU_TILE_DIAG") == "16":  # per-wave phase clocks of the la
     if nt == 256:
         for name, col in zip(("ratings", "runs", "users", "max user"), st.T):
             print(f"corr(WG time, {name}) = {np.corrcoef(wg, col)[0, 1]:+.2f}   range {col.min():.0f}..{col.max():.0f}")
+    # per-wave ratings and runs of the schedule beside the clocks (cost-model fit)
+    wr, wn = [], []
+    for w in range(len(off) - 1):
+        a, b = off[w], off[w + 1]
+        wr.append(b - a)
+        wn.append(int(np.count_nonzero(np.diff(ci[a:b]) != 0)) + (1 if b > a else 0))
+    out = os.environ.get("CLOCKS_NPZ")
+    if out:
+        np.savez(out, clocks=buf.reshape(-1, 4), ratings=np.array(wr), runs=np.array(wn))
     for b in np.argsort(-wg)[:4]:
         print("slow WG", b, "waves busy:", busy[b].astype(int).tolist())
         print("   ring:", d.reshape(256, 16, 4)[b, :, 1].astype(int).tolist())

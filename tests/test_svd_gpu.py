@@ -44,6 +44,21 @@ def test_ordered_matches_oracle(ctx, fold0, k, epochs, n):
     assert abs(ref[4] - got[4]) <= TOL
 
 
+@pytest.mark.parametrize("k", [1, 62, 100, 254, 300, 510])
+def test_ordered_collisions_and_widths(ctx, k):
+    """ORDERED with rows reused within the kernel's prefetch window all the time (3 users x 5 items: a
+    rating's user or item was usually rewritten by one of the previous 8, the forwarding path) and row
+    widths over both register layouts (k + 2 <= 256 and > 256 columns): equal to the restatement."""
+    rng = np.random.default_rng(k)
+    n = 700
+    u, i = rng.integers(0, 3, n), rng.integers(0, 5, n)
+    r = rng.integers(1, 6, n).astype(float)
+    P0, Q0 = rng.normal(0, 0.1, (3, k)), rng.normal(0, 0.1, (5, k))
+    ref = O.svd_fit(u, i, r, P0, Q0, epochs=2)
+    got = ctx.svd_fit(rsgpu.Ratings(u, i, r, 3, 5), P0, Q0, n_epochs=2, mode=rsgpu.SGD_ORDERED)
+    assert _maxdiff(ref[:4], got[:4]) <= TOL and abs(ref[4] - got[4]) <= TOL
+
+
 def test_ordered_permuted_order(ctx, fold0):
     """Visit order is the caller's (Q3): a fixed permutation of the same ratings also matches."""
     f = fold0
