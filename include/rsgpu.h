@@ -52,8 +52,9 @@ extern "C" {
                                    the values are still returned                                   */
 
 /* SGD visit schedule (SURVEY §8a parity contract P1/P2) */
-#define RS_SGD_FAST 0    /* user-CSR, one wave per user, atomic q_i deltas, deferred global bias */
-#define RS_SGD_ORDERED 1 /* single group, exact train-set order and update order of svd.go:93-129 */
+#define RS_SGD_FAST 0    /* the FAST schedule of rs_sgd_params.write_back (default RS_SGD_WB_TILE: user
+                            tiles in LDS, one memory-side atomic per (item, tile) run), work-local global bias */
+#define RS_SGD_ORDERED 1 /* one wave, exact train-set order and update order of svd.go:93-129 */
 
 /* FAST-mode schedule / write-back of the item rows (rs_sgd_params.write_back, rs_svd_plan_set_mode) */
 #define RS_SGD_WB_TILE 0          /* default: user tiles in LDS (integer LDS atomics), one memory-side
@@ -144,7 +145,11 @@ int rs_last_kernel_ms(const rs_ctx* ctx, double* ms);
 
 /* core/svd.go:63-132.  P (n_users x n_factors), Q (n_items x n_factors): injected initial factors
  * in (svd.go:80-85 draws them; the draw is unseeded in the reference, Q4), fitted factors out.
- * bu, bi, gb: in/out (the reference starts them at zero). */
+ * bu, bi, gb: in/out (the reference starts them at zero).
+ * FAST mode keeps its plan (user-CSR, tile schedule, device buffers) and a host copy of the COO
+ * (16 bytes per rating) on the ctx for the next rs_svd_fit of the same ratings (an exact comparison;
+ * GridSearchCV / CrossValidate refit the same folds); sets of more than 2^26 ratings are not kept, any
+ * other estimator call on the ctx (or rs_close) frees it, RSGPU_FIT_CACHE=0 turns it off. */
 int rs_svd_fit(rs_ctx* ctx, const rs_ratings* r, const rs_sgd_params* p, double* P, double* Q,
                double* bu, double* bi, double* gb);
 

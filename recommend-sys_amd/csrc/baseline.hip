@@ -74,6 +74,7 @@ extern "C" int rs_baseline_fit(rs_ctx* ctx, const rs_ratings* r, int32_t n_epoch
                                double reg, double* bu, double* bi, double* gb) {
     if (!ctx) return rs::set_error(ctx, RS_ERR_INVALID, "ctx is NULL");
     return rs_guard(ctx, [&]() -> int {
+        rs::drop_fit_cache(ctx);
         int st = rs::check_ratings(ctx, r);
         if (st != RS_OK) return st;
         if (n_epochs < 0 || !bu || !bi || !gb) return rs::set_error(ctx, RS_ERR_INVALID, "bad arguments");

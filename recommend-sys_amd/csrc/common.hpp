@@ -25,6 +25,9 @@ struct rs_ctx {
 
 namespace rs {
 // Device-time bracket of an estimator call's kernels (HIP events on the ctx stream).
+// rs_svd_fit's cached plan (sgd.hip) is freed when another estimator runs on the ctx (advisor round 2:
+// its host COO copy and device buffers would otherwise outlive their use)
+inline void drop_fit_cache(rs_ctx* c) { c->svd_fit_cache.reset(); }
 inline void kernel_span_begin(rs_ctx* c) { (void)hipEventRecord(c->k0, c->stream); }
 inline void kernel_span_end(rs_ctx* c) {
     (void)hipEventRecord(c->k1, c->stream);

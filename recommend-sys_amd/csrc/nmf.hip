@@ -242,6 +242,7 @@ extern "C" int rs_nmf_fit(rs_ctx* ctx, const rs_ratings* r, int32_t n_factors, i
                           double reg, int32_t as_written, double* P, double* Q) {
     if (!ctx) return rs::set_error(ctx, RS_ERR_INVALID, "ctx is NULL");
     return rs_guard(ctx, [&]() -> int {
+        rs::drop_fit_cache(ctx);
         int st = rs::check_ratings(ctx, r);
         if (st != RS_OK) return st;
         if (n_factors < 1 || n_factors > 512)

@@ -913,7 +913,7 @@ int32_t default_light_blocks(const rs_ctx* ctx) {
 // Blocks of the FAST launch: four work items per block (direct write-back), or one block per heavy
 // work item plus four light items per block (hybrid).  gb partials are one per block.
 int32_t fast_blocks(const rs_svd_plan* pl) {
-    if (pl->write_back == RS_SGD_WB_ATOMIC || pl->write_back == 101) {
+    if (pl->write_back == RS_SGD_WB_ATOMIC) {
         int32_t light = (pl->n_work - pl->n_heavy + 3) / 4;
         if (pl->light_blocks > 0) light = std::min(light, pl->light_blocks);
         return std::max<int32_t>(1, pl->n_heavy + light) + (pl->n_live + 3) / 4;  // + live mergers
@@ -923,7 +923,7 @@ int32_t fast_blocks(const rs_svd_plan* pl) {
 
 template <int E, int D, int WB>
 static void launch_fast_t(rs_svd_plan* pl, float lr, float reg, hipStream_t s, float* dP) {
-    const int32_t q_bytes = static_cast<int32_t>(pl->Q.n * sizeof(float));
+    const int32_t q_bytes = buffer_bytes32(pl->Q.n, sizeof(float), "item factor matrix");
     // multi-GPU delta mode (caller's dP, shard weights): every item adds its weighted delta;
     // single GPU: whole rows store P directly, pieces of split users add into the plan's dPs
     const bool multi = dP != nullptr;
@@ -1016,8 +1016,6 @@ static void launch_fast(rs_svd_plan* pl, float lr, float reg, hipStream_t s, flo
     switch (pl->write_back) {
         case RS_SGD_WB_STORE: launch_fast_d<0>(pl, lr, reg, s, dP); break;          // write-through stores
         case RS_SGD_WB_ATOMIC_DIRECT: launch_fast_d<1>(pl, lr, reg, s, dP); break;  // per-wave atomics
-        case 100: launch_fast_d<4>(pl, lr, reg, s, dP); break;                      // DIAG: no write-back
-        case 101: launch_fast_d<5>(pl, lr, reg, s, dP); break;                      // DIAG: writer drops
         default: launch_fast_d<2>(pl, lr, reg, s, dP); break;                       // hybrid
     }
     if (fx) {  // final live round on the int32 rows, then back to fp32 (live_merge_after skips)
@@ -1340,6 +1338,7 @@ static void plan_build_csr(rs_ctx* ctx, int32_t n_users, int32_t n_items, UserCS
     pl->h_vals = std::move(csr.vals);
     pl->P.alloc(static_cast<size_t>(std::max(1, n_users)) * pl->ld);
     RS_HIP(hipMemsetAsync(pl->P.p, 0, pl->P.n * sizeof(float), s));
+    (void)buffer_bytes32(static_cast<size_t>(std::max(1, n_items)) * pl->ld, sizeof(float), "item factor matrix");
     pl->Q.alloc(static_cast<size_t>(std::max(1, n_items)) * pl->ld);
     RS_HIP(hipMemsetAsync(pl->Q.p, 0, pl->Q.n * sizeof(float), s));
     pl->n_qrows = n_items;
@@ -1775,7 +1774,7 @@ extern "C" int rs_svd_plan_apply_delta(rs_svd_plan* pl, const void* dP, const vo
 
 extern "C" int rs_svd_plan_set_mode(rs_svd_plan* pl, int32_t write_back, int32_t ring_depth) {
     if (!pl) return rs::set_error(nullptr, RS_ERR_INVALID, "plan is NULL");
-    if ((write_back < RS_SGD_WB_TILE || write_back > RS_SGD_WB_ATOMIC) && write_back != 100 && write_back != 101)
+    if (write_back < RS_SGD_WB_TILE || write_back > RS_SGD_WB_ATOMIC)
         return rs::set_error(pl->ctx, RS_ERR_INVALID, "unknown write-back mode");
     if (ring_depth != 4 && ring_depth != 8 && ring_depth != 16)
         return rs::set_error(pl->ctx, RS_ERR_INVALID, "ring depth must be 4, 8 or 16");
@@ -2005,6 +2004,9 @@ static bool fit_cache_on() {
     static const bool on = !(std::getenv("RSGPU_FIT_CACHE") && std::atoi(std::getenv("RSGPU_FIT_CACHE")) == 0);
     return on;
 }
+// Sets larger than this are not cached (the cache holds a 16-byte-per-rating host copy of the COO and the
+// plan's device buffers): 2^26 ratings = 1 GiB of host memory at most.
+constexpr int64_t kFitCacheMaxNnz = int64_t{1} << 26;
 }  // namespace rs
 
 extern "C" int rs_svd_fit(rs_ctx* ctx, const rs_ratings* r, const rs_sgd_params* p, double* P,
@@ -2043,7 +2045,7 @@ extern "C" int rs_svd_fit(rs_ctx* ctx, const rs_ratings* r, const rs_sgd_params*
                 mark("csr");
                 rs::plan_build_csr(ctx, r->n_users, r->n_items, std::move(csr), p->n_factors, cache->plan.get());
                 mark("plan");
-                if (rs::fit_cache_on()) {
+                if (rs::fit_cache_on() && r->nnz <= rs::kFitCacheMaxNnz) {
                     const size_t n = static_cast<size_t>(r->nnz);
                     cache->nnz = r->nnz;
                     cache->n_users = r->n_users;
@@ -2071,6 +2073,7 @@ extern "C" int rs_svd_fit(rs_ctx* ctx, const rs_ratings* r, const rs_sgd_params*
         }
         // ORDERED: COO in train-set order, one wave, all epochs in one launch (sgd_ordered.hip), rows in the
         // folded layout P [p, b_u, 1], Q [q, 1, b_i]
+        rs::drop_fit_cache(ctx);
         hipStream_t s = ctx->stream;
         const int32_t k = p->n_factors, ld = rs::round_up4(k + 2);
         const int64_t nnz = r->nnz;

@@ -5,6 +5,8 @@
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
+#include <stdexcept>
+#include <string>
 #include <memory>
 #include <vector>
 
@@ -154,6 +156,15 @@ __device__ __forceinline__ int32_t roff(int32_t row, int x, int32_t lane4, int32
 
 __device__ __forceinline__ float lane63(float x) {
     return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(x), 63));
+}
+
+// byte size of a buffer the kernels address through a buffer resource with 32-bit offsets (the row
+// offsets are int32 too): 2 GiB or more is rejected instead of silently dropping loads and atomics
+inline int32_t buffer_bytes32(size_t elems, size_t elem_size, const char* what) {
+    const size_t b = elems * elem_size;
+    if (b >= (size_t{1} << 31))
+        throw std::invalid_argument(std::string(what) + " of 2 GiB or more: beyond the kernels' 32-bit buffer offsets");
+    return static_cast<int32_t>(b);
 }
 
 // sgd.hip

@@ -863,7 +863,7 @@ static void tile_launch_t(rs_svd_plan* pl, float lr, float reg, hipStream_t s, f
                                    hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(kTileLdsBudget)));
         attr = true;
     }
-    const int32_t q_bytes = static_cast<int32_t>(pl->Q.n * sizeof(float));
+    const int32_t q_bytes = buffer_bytes32(pl->Q.n, sizeof(float), "item factor matrix");
     hipLaunchKernelGGL(kern, dim3(tr.grid), dim3(NW * 64), pl->tile_lds, s, pl->t_tiles.p + tr.t0, tr.t1 - tr.t0,
                        pl->t_users.p, pl->t_streams.p + static_cast<int64_t>(tr.t0) * (NW + 1), pl->t_runs.p,
                        pl->t_recs.p, pl->P.p, reinterpret_cast<int32_t*>(pl->Q.p), q_bytes, pl->gb.p, pl->partial.p,

@@ -855,23 +855,16 @@ static bool sims_device(rs_ctx* ctx, int32_t kind, int32_t L, int32_t R, const S
         // Cosine / MSD scale the sums by 1 / s^2; SlopeOne's differences by 1 / s
         const double inv_s2 = kind == RS_DEV_SLOPE_ONE ? 1.0 / scale : 1.0 / static_cast<double>(scale * scale);
         const size_t lds = 2 * kStageBytes;
-        // K loop: 0 = round 1 (phases in sequence), 1 = software pipeline, 2 = pipeline with M
-        // derived from the X fragments in registers (one staged matrix less)
-        // K loop: 0 = round 1 (phases in sequence), 1 = software pipeline, 2 = pipeline with M
-        // derived in registers, 3 = PIPE 2 on eight waves (two per SIMD, 64 x 32 each),
-        // 4 = PIPE 1 on eight waves (M staged: fewer VALU, more LDS reads), 5 = PIPE 3 with the X
-        // loads rotated one step further ahead (default)
+        // K loop (RSGPU_KNN_PIPE, the variants the tests cross-check against each other):
+        // 5 = default: software pipeline on eight waves (two per SIMD, 64 x 32 each), M derived from the X
+        // fragments in registers, X loads rotated one step further ahead; 3 = the same without the
+        // rotation; 4 = the pipeline on eight waves with M staged in LDS; 0 = round 1 (four waves, phases
+        // in sequence).  (The four-wave pipelined loops of round 2, 1 and 2, were slower and are gone.)
         const char* pipe_env = std::getenv("RSGPU_KNN_PIPE");
-        const int pipe = (pipe_env && pipe_env[0] >= '0' && pipe_env[0] <= '5') ? pipe_env[0] - '0' : 5;
+        const int pipe = (pipe_env && (pipe_env[0] == '0' || pipe_env[0] == '3' || pipe_env[0] == '4')) ? pipe_env[0] - '0' : 5;
         for (const void* f : {reinterpret_cast<const void*>(&knn_sims_mfma_kernel<0, 0>),
                               reinterpret_cast<const void*>(&knn_sims_mfma_kernel<1, 0>),
                               reinterpret_cast<const void*>(&knn_sims_mfma_kernel<2, 0>),
-                              reinterpret_cast<const void*>(&knn_sims_mfma_kernel<0, 1>),
-                              reinterpret_cast<const void*>(&knn_sims_mfma_kernel<1, 1>),
-                              reinterpret_cast<const void*>(&knn_sims_mfma_kernel<2, 1>),
-                              reinterpret_cast<const void*>(&knn_sims_mfma_kernel<0, 2>),
-                              reinterpret_cast<const void*>(&knn_sims_mfma_kernel<1, 2>),
-                              reinterpret_cast<const void*>(&knn_sims_mfma_kernel<2, 2>),
                               reinterpret_cast<const void*>(&knn_sims_mfma_kernel<0, 2, 1>),
                               reinterpret_cast<const void*>(&knn_sims_mfma_kernel<1, 2, 1>),
                               reinterpret_cast<const void*>(&knn_sims_mfma_kernel<2, 2, 1>),
@@ -888,20 +881,19 @@ static bool sims_device(rs_ctx* ctx, int32_t kind, int32_t L, int32_t R, const S
             auto go = [&](auto kern, int threads) {
                 hipLaunchKernelGGL(kern, grid, dim3(threads), lds, st, X.p, ldk, L, dtiles.p + first, inv_s2, dS.p);
             };
-            auto by_pipe = [&](auto k0, auto k1, auto k2, auto k3, auto k4, auto k5) {
-                pipe == 0 ? go(k0, 256) : pipe == 1 ? go(k1, 256) : pipe == 2 ? go(k2, 256)
-                          : pipe == 3 ? go(k3, 512) : pipe == 4 ? go(k4, 512) : go(k5, 512);
+            auto by_pipe = [&](auto k0, auto k3, auto k4, auto k5) {
+                pipe == 0 ? go(k0, 256) : pipe == 3 ? go(k3, 512) : pipe == 4 ? go(k4, 512) : go(k5, 512);
             };
             if (kind == RS_SIM_COSINE)
-                by_pipe(knn_sims_mfma_kernel<0, 0>, knn_sims_mfma_kernel<0, 1>, knn_sims_mfma_kernel<0, 2>,
+                by_pipe(knn_sims_mfma_kernel<0, 0>,
                         knn_sims_mfma_kernel<0, 2, 1>, knn_sims_mfma_kernel<0, 1, 1>,
                         knn_sims_mfma_kernel<0, 2, 1, true>);
             else if (kind == RS_SIM_MSD)
-                by_pipe(knn_sims_mfma_kernel<1, 0>, knn_sims_mfma_kernel<1, 1>, knn_sims_mfma_kernel<1, 2>,
+                by_pipe(knn_sims_mfma_kernel<1, 0>,
                         knn_sims_mfma_kernel<1, 2, 1>, knn_sims_mfma_kernel<1, 1, 1>,
                         knn_sims_mfma_kernel<1, 2, 1, true>);
             else
-                by_pipe(knn_sims_mfma_kernel<2, 0>, knn_sims_mfma_kernel<2, 1>, knn_sims_mfma_kernel<2, 2>,
+                by_pipe(knn_sims_mfma_kernel<2, 0>,
                         knn_sims_mfma_kernel<2, 2, 1>, knn_sims_mfma_kernel<2, 1, 1>,
                         knn_sims_mfma_kernel<2, 2, 1, true>);
             RS_HIP(hipGetLastError());
@@ -1085,6 +1077,7 @@ extern "C" int rs_knn_sims_part(rs_ctx* ctx, int32_t kind, int32_t n_left, int32
                                 int32_t part, int32_t n_parts, double* sims) {
     if (!ctx) return rs::set_error(ctx, RS_ERR_INVALID, "ctx is NULL");
     return rs_guard(ctx, [&]() -> int {
+        rs::drop_fit_cache(ctx);
         if (kind < RS_SIM_COSINE || kind > RS_DEV_SLOPE_ONE)
             return rs::set_error(ctx, RS_ERR_INVALID, "unknown similarity kind");
         if (n_parts < 1 || part < 0 || part >= n_parts)
@@ -1190,6 +1183,7 @@ extern "C" int rs_knn_plan_create(rs_ctx* ctx, int32_t kind, int32_t n_left, int
                                   rs_knn_plan** out) {
     if (!ctx) return rs::set_error(ctx, RS_ERR_INVALID, "ctx is NULL");
     return rs_guard(ctx, [&]() -> int {
+        rs::drop_fit_cache(ctx);
         if (!out) return rs::set_error(ctx, RS_ERR_INVALID, "out is NULL");
         *out = nullptr;
         if (kind < RS_SIM_COSINE || kind > RS_DEV_SLOPE_ONE)

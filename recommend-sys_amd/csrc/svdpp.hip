@@ -530,7 +530,7 @@ static void launch_pp_fast(int32_t n_blocks, const DevBuf<int32_t>& work, int32_
     auto kern = fx ? svdpp_epoch_fast_kernel<E, 8, true> : svdpp_epoch_fast_kernel<E, 8, false>;
     hipLaunchKernelGGL(kern, dim3(n_blocks), dim3(256), 0, s, work.p,
                        n_work, n_heavy, rowptr.p, items.p, ratings.p, P.p, Q.p, Y.p,
-                       static_cast<int32_t>(Q.n * 4), static_cast<int32_t>(Y.n * 4), gb.p,
+                       rs::buffer_bytes32(Q.n, 4, "item factor matrix"), rs::buffer_bytes32(Y.n, 4, "implicit factor matrix"), gb.p,
                        partial.p, lr, reg, kf);
 }
 
@@ -540,6 +540,7 @@ extern "C" int rs_svdpp_fit(rs_ctx* ctx, const rs_ratings* r, const rs_sgd_param
                             double* Q, double* Y, double* bu, double* bi, double* gb) {
     if (!ctx) return rs::set_error(ctx, RS_ERR_INVALID, "ctx is NULL");
     return rs_guard(ctx, [&]() -> int {
+        rs::drop_fit_cache(ctx);
         int st = rs::check_ratings(ctx, r);
         if (st != RS_OK) return st;
         if (!p || !P || !Q || !Y || !bu || !bi || !gb)
@@ -688,8 +689,8 @@ extern "C" int rs_svdpp_fit(rs_ctx* ctx, const rs_ratings* r, const rs_sgd_param
         RS_HIP(hipStreamSynchronize(s));
         rs::kernel_span_begin(ctx);
         for (int32_t ep = 0; tile && ep < p->n_epochs; ++ep) {
-            rs::pp_tile_launch(sh, reinterpret_cast<int32_t*>(dQ.p), static_cast<int32_t>(dQ.n * 4),
-                               reinterpret_cast<int32_t*>(dY.p), static_cast<int32_t>(dY.n * 4), dP.p, dgb.p, tpart.p,
+            rs::pp_tile_launch(sh, reinterpret_cast<int32_t*>(dQ.p), rs::buffer_bytes32(dQ.n, 4, "item factor matrix"),
+                               reinterpret_cast<int32_t*>(dY.p), rs::buffer_bytes32(dY.n, 4, "implicit factor matrix"), dP.p, dgb.p, tpart.p,
                                lr, reg, k, ld, s);
             hipLaunchKernelGGL(rs::pp_gb_fold_kernel, dim3(1), dim3(256), 0, s, tpart.p,
                                static_cast<int64_t>(sh.tile_grid) * sh.tile_waves, dgb.p, inv_nnz);

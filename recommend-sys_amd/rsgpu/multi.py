@@ -1,10 +1,15 @@
-"""Item-sharded multi-GPU SGD (north_star): one process per GPU, torch.distributed (backend "nccl"
-= RCCL over xGMI on ROCm), Q and b_i sharded by item range, P and b_u replicated.
+"""Host-driven multi-GPU building blocks over torch.distributed (backend "nccl" = RCCL over xGMI on ROCm).
 
-Per epoch every rank runs its shard's fast SGD kernel in delta mode (rs_svd_plan_epoch_delta), the
-ranks all-reduce the count-weighted user deltas (n_users x ld fp32, one collective) and the
-global-bias sum (one float64), and every rank applies the same sum (rs_svd_plan_apply_delta), so P,
-b_u and GlobalBias stay bitwise identical across ranks.
+The library's own multi-GPU fit (csrc/multi.hip: rs_svd_plan_join / rs_svd_plan_epochs_sharded,
+rs_svd_fit_multi) runs the exact stratum rotation with its own RCCL communicator and is what bench.py
+and a Go host use.  This module keeps round 2's AVERAGE protocol as a host loop around the delta
+C-ABI (ItemShardedStep: every rank's shard epoch in delta mode, the count-weighted user deltas and the
+global-bias sum all-reduced, the same sum applied on every rank), its user-sharded dual
+(UserShardedStep), and the KNN part split.
+
+Streams: the steps pass `stream` to the plan; None means torch's current stream on the tensors'
+device (SvdPlan.epoch_delta_t / apply_delta_t resolve it), the stream torch's collectives are enqueued
+on, so kernels and all-reduces are ordered without a host sync.
 """
 from __future__ import annotations
 

@@ -59,6 +59,16 @@ def test_ordered_collisions_and_widths(ctx, k):
     assert _maxdiff(ref[:4], got[:4]) <= TOL and abs(ref[4] - got[4]) <= TOL
 
 
+def test_item_matrix_beyond_32bit_offsets_is_rejected(ctx):
+    """The kernels address Q through buffer resources with 32-bit offsets: a plan whose item matrix is
+    2 GiB or more (k = 510: 2 KiB rows, 2^20 items) is refused at creation instead of silently dropping
+    loads and atomics (advisor round 2)."""
+    ni = 1 << 20
+    with pytest.raises(rsgpu.RsError) as e:
+        ctx.svd_plan(rsgpu.Ratings([0], [ni - 1], [3.0], 1, ni), 510)
+    assert e.value.code == rsgpu.RS_ERR_INVALID and "2 GiB" in str(e.value)
+
+
 def test_ordered_permuted_order(ctx, fold0):
     """Visit order is the caller's (Q3): a fixed permutation of the same ratings also matches."""
     f = fold0
