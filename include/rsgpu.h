@@ -345,7 +345,8 @@ int rs_svd_plan_apply_delta(rs_svd_plan* plan, const void* dP, const void* gbsum
  * trained once per epoch against the current p_u and q_i; no rows are averaged.  GlobalBias is folded
  * once per epoch from every stratum's work-local partials (all-reduced).  After the call the
  * rank-blocks are broadcast, so P, b_u and GlobalBias are identical on every rank again.  n_blocks =
- * user blocks in all (rounded up to a multiple of n_ranks; 0 = automatic: pieces of ~64 MiB of P).
+ * user blocks in all (rounded up to a multiple of n_ranks; 0 = automatic: 2..16 pieces of ~64 MiB of
+ * P per rank-block).
  * This replaces north_star's per-epoch all-reduce of user-factor deltas, which RS_EXCHANGE_AVERAGE
  * keeps (the averaged deltas miss the reference's RMSE).
  *

@@ -203,11 +203,12 @@ RotStep rotation_step(int32_t g, int32_t n, int32_t st) {
 }
 
 // ROTATE: user blocks per rank-block.  A piece's rows are sent while the next piece computes, so only
-// the last piece's transfer is exposed per sub-epoch; pieces of about 64 MiB of P rows (1..16).
+// the last piece's transfer is exposed per sub-epoch: at least two pieces, about 64 MiB of P rows each
+// (2..16).
 int32_t auto_pieces(const rs_svd_plan* pl, int32_t nranks) {
     if (nranks <= 1) return 1;
     const double bytes = static_cast<double>(pl->n_users) / nranks * pl->ld * 4.0;
-    return std::max(1, std::min(16, static_cast<int32_t>(bytes / (64.0 * 1024 * 1024) + 0.5)));
+    return std::max(2, std::min(16, static_cast<int32_t>(bytes / (64.0 * 1024 * 1024) + 0.5)));
 }
 
 // weights w_u = local / total ratings of u; totals from the caller (host, n_users)

@@ -163,8 +163,10 @@ int main(int argc, char** argv) {
         auto s = NewSVD({{"mode", std::string("ordered")}, {"seed", 3}, {"nEpochs", 2}, {"nFactors", 8}});
         s->Fit(t);
         const double p = s->Predict(data.Users[0], data.Items[0]);
-        double want = s->GlobalBias + s->UserBias[0] + s->ItemBias[0];
-        for (int f = 0; f < 8; ++f) want += s->UserFactor[0][f] * s->ItemFactor[0][f];
+        // svd.go:35-48: ((GlobalBias + b_u) + b_i) + Dot(p, q), the dot product summed first
+        double dotpq = 0.0;
+        for (int f = 0; f < 8; ++f) dotpq += s->UserFactor[0][f] * s->ItemFactor[0][f];
+        const double want = s->GlobalBias + s->UserBias[0] + s->ItemBias[0] + dotpq;
         CHECK(p == want && s->Predict(-5, data.Items[0]) == s->GlobalBias + s->ItemBias[0]);
     });
     std::printf("%d/%d passed\n", g_run - g_failed, g_run);
