@@ -271,10 +271,11 @@ int rs_svd_plan_tile_order(rs_svd_plan* plan, int64_t* pos, int64_t* work_off, i
  * {staging, q-ring waits, rating loops, write-back} shader cycles per wave, up to n int64 values. */
 int rs_svd_plan_tile_clocks(rs_svd_plan* plan, int64_t* out, int64_t n);
 /* Diagnostic, host only (no device needed): builds the tile schedule of a user-CSR the way a plan
- * would (workgroups, waves, user blocks; svdpp != 0: the SVD++ variant rs_svdpp_fit uses) and reports
+ * would (workgroups, waves, user blocks) and reports
  * its host time in ms, the tile count and, for non-NULL outputs, the visit order pos (nnz user-CSR
- * positions, as rs_svd_plan_tile_order), the tiles' first records tile_off (n_tiles + 1) and, SVD++,
- * every record's rank among its user's records (nnz). */
+ * positions, as rs_svd_plan_tile_order) and the tiles' first records tile_off (n_tiles + 1); rank (nnz)
+ * is zero-filled.  svdpp must be 0: the SVD++ tile schedule it selected was removed in round 3
+ * (RS_ERR_UNSUPPORTED). */
 int rs_tile_schedule_host(int32_t n_users, int32_t n_items, const int64_t* rowptr, const int32_t* cols,
                           const float* vals, int32_t n_factors, int32_t workgroups, int32_t waves,
                           int32_t n_blocks, int32_t svdpp, int64_t* pos, int64_t* tile_off, int32_t* rank,

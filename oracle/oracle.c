@@ -864,98 +864,6 @@ void or_svdpp_fit_lazy(int32_t n_users, const int64_t* rowptr, const int32_t* it
     free(e);
 }
 
-/* The SVD++ tile schedule's own semantics (repo csrc/svdpp_tile.hip with one wave per tile), the
- * lazy form of svd.go:352-424 reorganised by tile: records pos[tile_off[t] .. tile_off[t+1]) (user-CSR
- * positions) in this order; every user of a tile has all its ratings there.  Per tile: W_u = sum over
- * N(u) of y_j / sqrt(n_u); a record of rank m (its user's m-th) predicts with e = a^m W_u and, after
- * the svd.go updates, W_u -= c q_i a^-(m+1) (c = lr diff); at the tile's end
- * y_j += sum over the tile's users u of j of (a^n_u - 1) y_j - a^n_u (W_u(start) - W_u) / sqrt(n_u).
- * GlobalBias: a tile-local copy, folded after the epoch (gb += sum n_t (gb_t - gb) / nnz). */
-void or_svdpp_fit_tiles(int32_t n_users, int32_t n_items, const int64_t* rowptr, const int32_t* items,
-                        const double* r, const int64_t* pos, int64_t n_tiles, const int64_t* tile_off,
-                        const int32_t* rank, int32_t k, int32_t epochs, double lr, double reg, double* P,
-                        double* Q, double* Y, double* bu, double* bi, double* gb) {
-    const int64_t nnz = rowptr[n_users];
-    const double al = 1.0 - lr * reg;
-    int32_t* uof = (int32_t*)malloc((size_t)(nnz > 0 ? nnz : 1) * sizeof(int32_t));
-    for (int32_t x = 0; x < n_users; x++)
-        for (int64_t t = rowptr[x]; t < rowptr[x + 1]; t++) uof[t] = x;
-    double* W = (double*)calloc((size_t)(n_users > 0 ? n_users : 1) * (size_t)k, sizeof(double));
-    double* W0 = (double*)calloc((size_t)(n_users > 0 ? n_users : 1) * (size_t)k, sizeof(double));
-    double* dY = (double*)calloc((size_t)(n_items > 0 ? n_items : 1) * (size_t)k, sizeof(double));
-    double* e = (double*)malloc((size_t)k * sizeof(double));
-    double GB = *gb;
-    for (int32_t epoch = 0; epoch < epochs; epoch++) {
-        double gsum = 0.0;
-        for (int64_t t = 0; t < n_tiles; t++) {
-            const int64_t a0 = tile_off[t], a1 = tile_off[t + 1];
-            for (int64_t z = a0; z < a1; z++) { /* the tile's users' start state (once per user) */
-                if (rank[z] != 0) continue;
-                const int32_t x = uof[pos[z]];
-                const double sq = sqrt((double)(rowptr[x + 1] - rowptr[x]));
-                double* w = W + (int64_t)x * k;
-                for (int32_t f = 0; f < k; f++) w[f] = 0.0;
-                for (int64_t q = rowptr[x]; q < rowptr[x + 1]; q++)
-                    for (int32_t f = 0; f < k; f++) w[f] += Y[(int64_t)items[q] * k + f] / sq;
-                for (int32_t f = 0; f < k; f++) W0[(int64_t)x * k + f] = w[f];
-            }
-            double g = GB;
-            for (int64_t z = a0; z < a1; z++) {
-                const int64_t p = pos[z];
-                const int32_t x = uof[p], ii = items[p], m = rank[z];
-                double* pu = P + (int64_t)x * k;
-                double* qi = Q + (int64_t)ii * k;
-                double* wu = W + (int64_t)x * k;
-                const double Ab = pow(al, (double)m), Ai = pow(al, -(double)(m + 1));
-                const double userBias = bu[x], itemBias = bi[ii];
-                double pred = g;
-                pred += bu[x];
-                pred += bi[ii];
-                double s = 0.0;
-                for (int32_t f = 0; f < k; f++) {
-                    e[f] = Ab * wu[f];
-                    s += (pu[f] + e[f]) * qi[f];
-                }
-                pred += s;
-                const double diff = pred - r[p];
-                g -= lr * diff;
-                bu[x] -= lr * (diff + reg * userBias);
-                bi[ii] -= lr * (diff + reg * itemBias);
-                for (int32_t f = 0; f < k; f++) pu[f] = pu[f] - (qi[f] * diff + pu[f] * reg) * lr;
-                for (int32_t f = 0; f < k; f++) qi[f] = qi[f] - ((pu[f] + e[f]) * diff + qi[f] * reg) * lr;
-                for (int32_t f = 0; f < k; f++) wu[f] -= lr * diff * qi[f] * Ai;
-            }
-            /* the tile's end: every term uses y_j as it was before the tile's sum */
-            for (int64_t z = a0; z < a1; z++) {
-                if (rank[z] != 0) continue;
-                const int32_t x = uof[pos[z]];
-                const int64_t n = rowptr[x + 1] - rowptr[x];
-                const double An = pow(al, (double)n), sq = sqrt((double)n);
-                for (int64_t q = rowptr[x]; q < rowptr[x + 1]; q++) {
-                    const int64_t j = (int64_t)items[q] * k;
-                    for (int32_t f = 0; f < k; f++)
-                        dY[j + f] += (An - 1.0) * Y[j + f] - An * (W0[(int64_t)x * k + f] - W[(int64_t)x * k + f]) / sq;
-                }
-            }
-            for (int64_t z = a0; z < a1; z++) {
-                const int64_t j = (int64_t)items[pos[z]] * k;
-                for (int32_t f = 0; f < k; f++) {
-                    Y[j + f] += dY[j + f];
-                    dY[j + f] = 0.0;
-                }
-            }
-            gsum += (double)(a1 - a0) * (g - GB);
-        }
-        if (nnz > 0) GB += gsum / (double)nnz;
-    }
-    *gb = GB;
-    free(uof);
-    free(W);
-    free(W0);
-    free(dY);
-    free(e);
-}
-
 double or_gb_warm_start(int32_t n_users, const int64_t* rowptr, const int32_t* items,
                         const double* r, const double* bu, const double* bi) {
     const int64_t nnz = rowptr[n_users];

@@ -126,10 +126,6 @@ double or_gb_warm_start(int32_t n_users, const int64_t* rowptr, const int32_t* i
                         const double* r, const double* bu, const double* bi);
 
 /* or_svdpp_fit_userwise in its O(nnz k) lazy affine form (rows without repeated items). */
-void or_svdpp_fit_tiles(int32_t n_users, int32_t n_items, const int64_t* rowptr, const int32_t* items,
-                        const double* r, const int64_t* pos, int64_t n_tiles, const int64_t* tile_off,
-                        const int32_t* rank, int32_t k, int32_t epochs, double lr, double reg, double* P,
-                        double* Q, double* Y, double* bu, double* bi, double* gb);
 void or_svdpp_fit_lazy(int32_t n_users, const int64_t* rowptr, const int32_t* items, const double* r,
                        int32_t k, int32_t epochs, double lr, double reg, double* P, double* Q, double* Y,
                        double* bu, double* bi, double* gb);

@@ -95,11 +95,7 @@ struct rs_svd_plan {
     // [t_block_tile[b], t_block_tile[b+1]) hold users [t_block_user[b], t_block_user[b+1])); the
     // item-sharded multi-GPU epoch all-reduces a block's user deltas while the next block computes
     int32_t tile_ublocks = 1;
-    // SVD++ tile schedule (svdpp_tile.hip) reuses this builder: LDS ints per user (0 = one row) and the
-    // SVD++ record format (no user pieces; tile_users.y = the user's rating count; records carry the
-    // rating's rank m among its user's ratings in the schedule, records.x = user | m << 16)
-    int32_t tile_user_lds = 0;
-    bool tile_pp = false;
+    int32_t tile_user_lds = 0;  // LDS ints per user (0 = one row of k + 2)
     std::vector<int32_t> ublock_bounds;  // caller's block bounds (tile_ublocks + 1), or empty: own ratings
     std::vector<int32_t> t_block_tile, t_block_user;
     std::vector<int32_t> t_block_split;  // block b's split users: t_split_rows[t_block_split[b], t_block_split[b+1])
@@ -192,10 +188,6 @@ void tile_launch(rs_svd_plan* pl, float lr, float reg, hipStream_t s, float* dP)
 int32_t tile_launch_range(rs_svd_plan* pl, float lr, float reg, hipStream_t s, float* dP, int32_t ldd,
                           int32_t t0, int32_t t1);
 int32_t tile_partials(const rs_svd_plan* pl);  // GlobalBias partials the launch writes
-// svdpp_tile.hip: K2 on the tile schedule (a plan used as the schedule's container: tile_pp set)
-int32_t pp_tile_user_lds(int32_t k);
-void pp_tile_launch(const rs_svd_plan& sh, int32_t* Q, int32_t q_bytes, int32_t* Y, int32_t y_bytes, float* P,
-                    const double* gb, double* partial, float lr, float reg, int32_t kf, int32_t ldm, hipStream_t s);
 // visit order of the tile schedule (user-CSR positions, nnz entries) and its GlobalBias work items
 // (one per tile and wave: n_works + 1 offsets into pos); any pointer may be NULL
 void tile_order(rs_svd_plan* pl, int64_t* pos, int64_t* work_off, int32_t* n_works);

@@ -376,7 +376,6 @@ void build_tile_host(const rs_svd_plan* pl, int32_t u_begin, int32_t u_end, int3
         if (d == 0) continue;
         const int64_t cap = std::min<int64_t>(rec_cap, std::max<int64_t>(target, 1));
         const int64_t pieces = d > rec_cap ? (d + cap - 1) / cap : 1;
-        if (pieces > 1 && pl->tile_pp) throw std::invalid_argument("a user too heavy for the SVD++ tile schedule");
         if (pieces > 1) th.split.push_back(u);
         for (int64_t x = 0; x < pieces; ++x) {
             const int64_t b = rp[u] + d * x / pieces, e = rp[u] + d * (x + 1) / pieces;
@@ -647,35 +646,6 @@ void build_tile_host(const rs_svd_plan* pl, int32_t u_begin, int32_t u_end, int3
         int2* out = th.recs.data() + rec_at[t];
         int64_t* po = want_pos ? th.pos.data() + rec_at[t] : nullptr;
         const size_t nr = L.runs.size() - 1;
-        std::vector<int32_t> mrank;  // SVD++: each record's rank among its user's records
-        if (pl->tile_pp) {
-            // ranks by progress through the record's stream ((index + 1/2) / stream length): the order
-            // the concurrent waves reach them; with one wave, exactly the visit order
-            const size_t n = L.vp.size();
-            const int32_t nusr = static_cast<int32_t>(tb[t + 1] - tb[t]);
-            std::vector<double> prog(n);
-            std::vector<int32_t> who(n);
-            size_t at = 0;
-            for (int s2 = 0; s2 < nw; ++s2) {
-                const int32_t a0 = L.runs[L.st[s2]].y, a1 = L.runs[L.st[s2 + 1]].y;
-                for (int32_t r = L.st[s2]; r < L.st[s2 + 1]; ++r)
-                    for (int32_t x = 0; x < L.runs[r + 1].y - L.runs[r].y; ++x, ++at) {
-                        prog[at] = (static_cast<double>(L.runs[r].y + x - a0) + 0.5) / std::max(1, a1 - a0);
-                        who[at] = L.vul[static_cast<size_t>(L.rb[r] + x)];
-                    }
-            }
-            std::vector<int32_t> first(static_cast<size_t>(nusr) + 1, 0), idx(n);
-            for (size_t x = 0; x < n; ++x) first[who[x] + 1]++;
-            for (int32_t u = 0; u < nusr; ++u) first[u + 1] += first[u];
-            std::vector<int32_t> fill(first.begin(), first.end() - 1);
-            for (size_t x = 0; x < n; ++x) idx[fill[who[x]]++] = static_cast<int32_t>(x);
-            mrank.assign(n, 0);
-            for (int32_t u = 0; u < nusr; ++u) {
-                std::stable_sort(idx.begin() + first[u], idx.begin() + first[u + 1],
-                                 [&](int32_t a, int32_t b) { return prog[a] < prog[b]; });
-                for (int32_t x = first[u]; x < first[u + 1]; ++x) mrank[idx[x]] = x - first[u];
-            }
-        }
         size_t at = 0;
         for (size_t r = 0; r < nr; ++r) {
             const int32_t n = L.runs[r + 1].y - L.runs[r].y;
@@ -683,7 +653,7 @@ void build_tile_host(const rs_svd_plan* pl, int32_t u_begin, int32_t u_end, int3
                 const size_t g = static_cast<size_t>(L.rb[r] + x);
                 int32_t bits;
                 std::memcpy(&bits, &vals[L.vp[g]], 4);
-                *out++ = make_int2(pl->tile_pp ? (L.vul[g] | (mrank[at] << 16)) : L.vul[g], bits);
+                *out++ = make_int2(L.vul[g], bits);
                 if (po) *po++ = L.vp[g];
             }
         }
@@ -700,7 +670,7 @@ void build_tile_host(const rs_svd_plan* pl, int32_t u_begin, int32_t u_end, int3
     for (size_t x = 0; x < ents.size(); ++x) {
         int32_t bits;
         std::memcpy(&bits, &ents[x].frac, 4);
-        th.users[x] = make_int2(ents[x].u, pl->tile_pp ? static_cast<int32_t>(ents[x].e - ents[x].b) : bits);
+        th.users[x] = make_int2(ents[x].u, bits);
     }
     tmark("emit");
     if (th.lds > kTileLdsBudget) throw std::logic_error("tile schedule exceeds the LDS");
@@ -982,6 +952,7 @@ extern "C" int rs_tile_schedule_host(int32_t n_users, int32_t n_items, const int
     if (n_users < 0 || n_items < 0 || !rowptr || n_factors < 1 || n_factors > 510 || workgroups < 1 ||
         (waves != 1 && waves != 2 && waves != 4 && waves != 8 && waves != 16) || n_blocks < 1)
         return rs::set_error(nullptr, RS_ERR_INVALID, "bad tile schedule arguments");
+    if (svdpp) return rs::set_error(nullptr, RS_ERR_UNSUPPORTED, "the SVD++ tile schedule was removed (round 3)");
     return rs_guard(nullptr, [&]() -> int {
         rs_svd_plan pl;
         pl.n_users = n_users;
@@ -993,10 +964,6 @@ extern "C" int rs_tile_schedule_host(int32_t n_users, int32_t n_items, const int
         pl.h_vals.assign(vals, vals + pl.nnz);
         pl.tile_waves = waves;
         pl.tile_ublocks = n_blocks;
-        if (svdpp) {
-            pl.tile_pp = true;
-            pl.tile_user_lds = rs::pp_tile_user_lds(n_factors);
-        }
         const auto t0 = std::chrono::steady_clock::now();
         rs::TileHost th;
         std::vector<int32_t> bt, bu;
@@ -1009,8 +976,7 @@ extern "C" int rs_tile_schedule_host(int32_t n_users, int32_t n_items, const int
             for (size_t t = 0; t < th.tiles.size(); ++t) tile_off[t] = th.tiles[t].w;
             tile_off[th.tiles.size()] = static_cast<int64_t>(th.recs.size());
         }
-        if (rank)
-            for (size_t x = 0; x < th.recs.size(); ++x) rank[x] = svdpp ? (th.recs[x].x >> 16) : 0;
+        if (rank) std::fill(rank, rank + th.recs.size(), 0);
         return RS_OK;
     });
 }

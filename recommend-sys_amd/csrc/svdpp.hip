@@ -212,11 +212,12 @@ __device__ __forceinline__ void pp_chain(__amdgpu_buffer_rsrc_t rq, const int32_
     }
 }
 
-// FAST epoch.  Blocks [0, n_heavy) take one heavy user each (the first, heaviest work items):
-// pass 1 and pass 3 split over the block's four waves (rows j = 4 t YB + w YB ...), pass 2 on wave
-// 0 with its q_i deltas written to an LDS ring that waves 1..3 drain into the float atomics (the
-// K1 hybrid scheme: the chain's vmcnt then holds only its own loads).  The other blocks' waves
-// stride over the light users, each wave running all three passes itself with direct atomics.
+// FAST epoch.  Blocks [0, n_hblocks) stride over the heavy users (the first n_heavy work items, LPT
+// order), one user at a time per block: pass 1 and pass 3 split over the block's four waves (rows
+// j = 4 t YB + w YB ...), pass 2 on wave 0 with its q_i deltas written to an LDS ring that waves 1..3
+// drain into the atomics (the K1 hybrid scheme: the chain's vmcnt then holds only its own loads, not
+// the atomics' memory-side latency).  The other blocks' waves stride over the light users, each wave
+// running all three passes itself with direct atomics.
 template <int E>
 struct PPRing {
     static constexpr int kRing = E <= 2 ? 32 : (E <= 4 ? 16 : 8);
@@ -232,7 +233,8 @@ __device__ __forceinline__ void pp_lds_store(int32_t* p, int32_t v) {
 
 template <int E, int D, bool FX>
 __global__ __launch_bounds__(256) void svdpp_epoch_fast_kernel(
-    const int32_t* __restrict__ work, int32_t n_work, int32_t n_heavy, const int64_t* __restrict__ rowptr,
+    const int32_t* __restrict__ work, int32_t n_work, int32_t n_heavy, int32_t n_hblocks,
+    const int64_t* __restrict__ rowptr,
     const int32_t* __restrict__ items, const float* __restrict__ ratings, float* __restrict__ P,
     float* Q, float* Y, int32_t row_bytes_q, int32_t row_bytes_y, const double* __restrict__ gb_in,
     double* __restrict__ gb_partial, float lr, float reg, int32_t kf) {
@@ -259,9 +261,9 @@ __global__ __launch_bounds__(256) void svdpp_epoch_fast_kernel(
     const int blk = static_cast<int>(blockIdx.x);
     double contrib = 0.0;
 
-    if (blk >= n_heavy) {  // light blocks
-        const int stride = (static_cast<int>(gridDim.x) - n_heavy) * 4;
-        for (int w = n_heavy + (blk - n_heavy) * 4 + wib; w < n_work; w += stride) {
+    if (blk >= n_hblocks) {  // light blocks
+        const int stride = (static_cast<int>(gridDim.x) - n_hblocks) * 4;
+        for (int w = n_heavy + (blk - n_hblocks) * 4 + wib; w < n_work; w += stride) {
             const int32_t u = work[w];
             const int64_t b = rowptr[u], e = rowptr[u + 1];
             float p[E];
@@ -293,108 +295,111 @@ __global__ __launch_bounds__(256) void svdpp_epoch_fast_kernel(
         return;
     }
 
-    // heavy block (block-uniform branch): user work[blk]
-    const int32_t u = work[blk];
-    const int64_t b = rowptr[u], e = rowptr[u + 1];
-    if (threadIdx.x == 0) {
-        s_tail = 0;
-        s_done = 0;
-    }
-    if (threadIdx.x < NW) s_head[threadIdx.x] = static_cast<int32_t>(threadIdx.x);
-    // pass 1 split over the four waves, the partial sums added in wave order (identical everywhere)
-    {
-        float S0w[E];
-        pp_sum_y<E, YB, FX>(ry, items, b, e, wib * YB, 4 * YB, lane4, lcy, S0w);
-#pragma unroll
-        for (int x = 0; x < E; ++x) s_red[wib][lane + 64 * x] = S0w[x];
-    }
-    __syncthreads();
-    float Cv[E];
-#pragma unroll
-    for (int x = 0; x < E; ++x) Cv[x] = 0.f;
-    if (wib == 0) {
-        float S0[E], p[E];
-#pragma unroll
-        for (int x = 0; x < E; ++x)
-            S0[x] = ((s_red[0][lane + 64 * x] + s_red[1][lane + 64 * x]) + s_red[2][lane + 64 * x]) +
-                    s_red[3][lane + 64 * x];
-        float* prow = P + static_cast<int64_t>(u) * LD;
-#pragma unroll
-        for (int x = 0; x < E; ++x) p[x] = pcol(x) >= 0 ? prow[pcol(x)] : 0.f;
-        float ub = pp_lane63(p[E - 1]);
-        float gb = gb0, A = 1.f;
-        int32_t tail = 0, free_end = R;
-        pp_chain<E, DH, FX>(rq, items, ratings, b, e, lane, lcq, lr, a, S0, p, ub, gb, A, Cv,
-                        [&](int32_t row, const float (&qw)[E], const float (&q)[E]) {
-                            if (tail >= free_end) {  // ring full: wait for the writers
-                                for (;;) {
-                                    const int32_t h = min(min(pp_lds_load(&s_head[0]), pp_lds_load(&s_head[1])),
-                                                          pp_lds_load(&s_head[2]));
-                                    free_end = h + R;
-                                    if (tail < free_end) break;
-                                    __builtin_amdgcn_s_sleep(1);
-                                }
-                            }
-                            const int slot = tail & (R - 1);
-#pragma unroll
-                            for (int x = 0; x < E; ++x) s_q[slot][lane + 64 * x] = qw[x] - q[x];
-                            if (lane == 0) s_row[slot] = row;
-                            __atomic_signal_fence(__ATOMIC_SEQ_CST);  // entry before tail, in issue order
-                            ++tail;
-                            if (lane == 0) pp_lds_store(&s_tail, tail);
-                        });
-#pragma unroll
-        for (int x = 0; x < E; ++x) {
-            if (pcol(x) >= 0) prow[pcol(x)] = p[x];
-            s_red[0][lane + 64 * x] = Cv[x];  // pass 3 reads C and A from LDS
+    // heavy block (block-uniform branch): users work[blk], work[blk + n_hblocks], ...
+    for (int32_t hw = blk; hw < n_heavy; hw += n_hblocks) {
+        const int32_t u = work[hw];
+        const int64_t b = rowptr[u], e = rowptr[u + 1];
+        if (threadIdx.x == 0) {
+            s_tail = 0;
+            s_done = 0;
         }
-        if (lane == 0) s_A = A;
-        contrib = static_cast<double>(e - b) * (static_cast<double>(gb) - static_cast<double>(gb0));
-        __atomic_signal_fence(__ATOMIC_SEQ_CST);
-        if (lane == 0) pp_lds_store(&s_done, 1);
-    } else {
-        const int wr = wib - 1;
-        int32_t next = wr;
-        for (;;) {
-            const int32_t done = pp_lds_load(&s_done);
+        if (threadIdx.x < NW) s_head[threadIdx.x] = static_cast<int32_t>(threadIdx.x);
+        // pass 1 split over the four waves, the partial sums added in wave order (identical everywhere)
+        {
+            float S0w[E];
+            pp_sum_y<E, YB, FX>(ry, items, b, e, wib * YB, 4 * YB, lane4, lcy, S0w);
+#pragma unroll
+            for (int x = 0; x < E; ++x) s_red[wib][lane + 64 * x] = S0w[x];
+        }
+        __syncthreads();
+        float Cv[E];
+#pragma unroll
+        for (int x = 0; x < E; ++x) Cv[x] = 0.f;
+        if (wib == 0) {
+            float S0[E], p[E];
+#pragma unroll
+            for (int x = 0; x < E; ++x)
+                S0[x] = ((s_red[0][lane + 64 * x] + s_red[1][lane + 64 * x]) + s_red[2][lane + 64 * x]) +
+                        s_red[3][lane + 64 * x];
+            float* prow = P + static_cast<int64_t>(u) * LD;
+#pragma unroll
+            for (int x = 0; x < E; ++x) p[x] = pcol(x) >= 0 ? prow[pcol(x)] : 0.f;
+            float ub = pp_lane63(p[E - 1]);
+            float gb = gb0, A = 1.f;
+            int32_t tail = 0, free_end = R;
+            pp_chain<E, DH, FX>(rq, items, ratings, b, e, lane, lcq, lr, a, S0, p, ub, gb, A, Cv,
+                            [&](int32_t row, const float (&qw)[E], const float (&q)[E]) {
+                                if (tail >= free_end) {  // ring full: wait for the writers
+                                    for (;;) {
+                                        const int32_t h = min(min(pp_lds_load(&s_head[0]), pp_lds_load(&s_head[1])),
+                                                              pp_lds_load(&s_head[2]));
+                                        free_end = h + R;
+                                        if (tail < free_end) break;
+                                        __builtin_amdgcn_s_sleep(1);
+                                    }
+                                }
+                                const int slot = tail & (R - 1);
+#pragma unroll
+                                for (int x = 0; x < E; ++x) s_q[slot][lane + 64 * x] = qw[x] - q[x];
+                                if (lane == 0) s_row[slot] = row;
+                                __atomic_signal_fence(__ATOMIC_SEQ_CST);  // entry before tail, in issue order
+                                ++tail;
+                                if (lane == 0) pp_lds_store(&s_tail, tail);
+                            });
+#pragma unroll
+            for (int x = 0; x < E; ++x) {
+                if (pcol(x) >= 0) prow[pcol(x)] = p[x];
+                s_red[0][lane + 64 * x] = Cv[x];  // pass 3 reads C and A from LDS
+            }
+            if (lane == 0) s_A = A;
+            contrib += static_cast<double>(e - b) * (static_cast<double>(gb) - static_cast<double>(gb0));
             __atomic_signal_fence(__ATOMIC_SEQ_CST);
-            const int32_t tail = pp_lds_load(&s_tail);
-            __atomic_signal_fence(__ATOMIC_SEQ_CST);
-            if (next < tail) {
-                while (next < tail) {
-                    const int32_t n = min((tail - next + NW - 1) / NW, NB);
-                    const int32_t myrow = s_row[(next + NW * (lane & (NB - 1))) & (R - 1)];
-                    float v[NB][E];
-#pragma unroll
-                    for (int j = 0; j < NB; ++j)
-#pragma unroll
-                        for (int x = 0; x < E; ++x) v[j][x] = s_q[(next + NW * j) & (R - 1)][lane + 64 * x];
-#pragma unroll
-                    for (int j = 0; j < NB; ++j) {
-                        if (j < n) {
-                            const int32_t row = __builtin_amdgcn_readlane(myrow, j);
-#pragma unroll
-                            for (int x = 0; x < E; ++x)
-                                pp_atomic_add<FX>(v[j][x], rq, pp_roff<E>(row, x, lane4, lcq));
-                        }
-                    }
-                    next += NW * n;
-                }
+            if (lane == 0) pp_lds_store(&s_done, 1);
+        } else {
+            const int wr = wib - 1;
+            int32_t next = wr;
+            for (;;) {
+                const int32_t done = pp_lds_load(&s_done);
                 __atomic_signal_fence(__ATOMIC_SEQ_CST);
-                if (lane == 0) pp_lds_store(&s_head[wr], next);
-            } else if (done) {
-                break;
-            } else {
-                __builtin_amdgcn_s_sleep(1);
+                const int32_t tail = pp_lds_load(&s_tail);
+                __atomic_signal_fence(__ATOMIC_SEQ_CST);
+                if (next < tail) {
+                    while (next < tail) {
+                        const int32_t n = min((tail - next + NW - 1) / NW, NB);
+                        const int32_t myrow = s_row[(next + NW * (lane & (NB - 1))) & (R - 1)];
+                        float v[NB][E];
+#pragma unroll
+                        for (int j = 0; j < NB; ++j)
+#pragma unroll
+                            for (int x = 0; x < E; ++x) v[j][x] = s_q[(next + NW * j) & (R - 1)][lane + 64 * x];
+#pragma unroll
+                        for (int j = 0; j < NB; ++j) {
+                            if (j < n) {
+                                const int32_t row = __builtin_amdgcn_readlane(myrow, j);
+#pragma unroll
+                                for (int x = 0; x < E; ++x)
+                                    pp_atomic_add<FX>(v[j][x], rq, pp_roff<E>(row, x, lane4, lcq));
+                            }
+                        }
+                        next += NW * n;
+                    }
+                    __atomic_signal_fence(__ATOMIC_SEQ_CST);
+                    if (lane == 0) pp_lds_store(&s_head[wr], next);
+                } else if (done) {
+                    break;
+                } else {
+                    __builtin_amdgcn_s_sleep(1);
+                }
             }
         }
-    }
-    __syncthreads();  // A and C in LDS; every q delta issued
-    {
-        float C[E];
+        __syncthreads();  // A and C in LDS; every q delta issued
+        {
+            float C[E];
 #pragma unroll
-        for (int x = 0; x < E; ++x) C[x] = s_red[0][lane + 64 * x];
-        pp_update_y<E, YB, FX>(ry, items, b, e, wib * YB, 4 * YB, lane4, lcy, s_A - 1.f, C);
+            for (int x = 0; x < E; ++x) C[x] = s_red[0][lane + 64 * x];
+            pp_update_y<E, YB, FX>(ry, items, b, e, wib * YB, 4 * YB, lane4, lcy, s_A - 1.f, C);
+        }
+        __syncthreads();  // s_red, s_A and the ring are reset by the next user
     }
     if (threadIdx.x == 0) gb_partial[blk] = contrib;
 }
@@ -522,14 +527,14 @@ static void unpack_bias_rows(const std::vector<float>& src, int64_t rows, int32_
 }
 
 template <int E>
-static void launch_pp_fast(int32_t n_blocks, const DevBuf<int32_t>& work, int32_t n_work, int32_t n_heavy,
+static void launch_pp_fast(int32_t n_blocks, const DevBuf<int32_t>& work, int32_t n_work, int32_t n_heavy, int32_t n_hblocks,
                            const DevBuf<int64_t>& rowptr, const DevBuf<int32_t>& items,
                            const DevBuf<float>& ratings, DevBuf<float>& P, DevBuf<float>& Q,
                            DevBuf<float>& Y, DevBuf<double>& gb, DevBuf<double>& partial, float lr,
                            float reg, int32_t kf, bool fx, hipStream_t s) {
     auto kern = fx ? svdpp_epoch_fast_kernel<E, 8, true> : svdpp_epoch_fast_kernel<E, 8, false>;
     hipLaunchKernelGGL(kern, dim3(n_blocks), dim3(256), 0, s, work.p,
-                       n_work, n_heavy, rowptr.p, items.p, ratings.p, P.p, Q.p, Y.p,
+                       n_work, n_heavy, n_hblocks, rowptr.p, items.p, ratings.p, P.p, Q.p, Y.p,
                        rs::buffer_bytes32(Q.n, 4, "item factor matrix"), rs::buffer_bytes32(Y.n, 4, "implicit factor matrix"), gb.p,
                        partial.p, lr, reg, kf);
 }
@@ -623,23 +628,33 @@ extern "C" int rs_svdpp_fit(rs_ctx* ctx, const rs_ratings* r, const rs_sgd_param
         if (static_cast<int64_t>(std::max(1, r->n_items)) * ld * 4 >= (int64_t{1} << 31) - 64)
             return rs::set_error(ctx, RS_ERR_UNSUPPORTED, "n_items * n_factors too large");
         const int32_t n_work = static_cast<int32_t>(order.size());
-        // blocks of four waves striding over the LPT-ordered users: at most 1.5 blocks per CU (the
-        // K1 measurement: fewer waves keep the memory-side atomic queues, which every q_i / y_j load
-        // waits behind, short); RSGPU_PP_BLOCKS overrides (experiments)
+        // blocks of four waves striding over the LPT-ordered users: at most one block per CU.  The
+        // number of users in flight sets the Hogwild error (every in-flight user trains on implicit
+        // sums S0 read when its row started, while the others decay the same y_j): on the ML-1M shape
+        // (k = 128, 20 epochs) 512 blocks give held-out RMSE 0.672-0.684, 384 give 0.649-0.656 run to
+        // run, 128-320 give 0.6463-0.6475 on every run against the sequential restatement's 0.6470
+        // (heaviest-first order) and 0.6493 (user-id order), at the same epoch time (1.27 ms: the
+        // heaviest user's chain bounds it); profiles/r03_experiments/pp_accuracy.log.
+        // RSGPU_PP_BLOCKS overrides (experiments)
         int cus = 256;
         if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, ctx->device) != hipSuccess || cus <= 0)
             cus = 256;
-        int32_t cap = (3 * cus) / 2;
+        int32_t cap = cus;
         if (const char* env = std::getenv("RSGPU_PP_BLOCKS")) cap = std::max(1, std::atoi(env));
-        // users with >= 1024 ratings (LPT order: the first n_heavy work items) get a block each
+        // users with >= heavy_min ratings (LPT order: the first n_heavy work items) run on the heavy
+        // blocks, n_hblocks of them striding over those users
         int32_t n_heavy = 0;
         int32_t heavy_min = 1024;
         if (const char* env = std::getenv("RSGPU_PP_HEAVY")) heavy_min = std::atoi(env);
         while (heavy_min > 0 && n_heavy < n_work &&
                csr.rowptr[order[n_heavy] + 1] - csr.rowptr[order[n_heavy]] >= heavy_min)
             ++n_heavy;
-        const int32_t n_blocks =
-            n_heavy + std::max<int32_t>(1, std::min<int32_t>((n_work - n_heavy + 3) / 4, cap));
+        // one block per heavy user: fewer blocks striding over them (or every user on the block path,
+        // heavy_min = 1) measured slower at equal or worse RMSE (profiles/r03_experiments/pp_accuracy.log)
+        const int32_t n_hblocks = n_heavy;
+        const int32_t n_light_blocks =
+            n_work > n_heavy || n_hblocks == 0 ? std::max<int32_t>(1, std::min<int32_t>((n_work - n_heavy + 3) / 4, cap)) : 0;
+        const int32_t n_blocks = n_hblocks + n_light_blocks;
         rs::DevBuf<int32_t> dwork(std::max<size_t>(1, order.size()));
         dwork.upload(order.data(), order.size(), s);
         std::vector<float> hP, hQ, hY;
@@ -655,57 +670,18 @@ extern "C" int rs_svdpp_fit(rs_ctx* ctx, const rs_ratings* r, const rs_sgd_param
         dQ.upload(hQ.data(), hQ.size(), s);
         dY.upload(hY.data(), hY.size(), s);
         const double inv_nnz = r->nnz > 0 ? 1.0 / static_cast<double>(r->nnz) : 0.0;
-        // The tile schedule (svdpp_tile.hip) is an experiment, selected by RSGPU_PP_TILE=1: exact with one
-        // workgroup (tests), 2.7x faster, but unstable under inter-workgroup concurrency (the y_j decays of
-        // concurrent tiles add up from one snapshot: NaN on the ML-1M shape).  The default is
-        // the user-major lazy kernel below.
-        bool tile = false;
-        if (const char* env = std::getenv("RSGPU_PP_TILE")) tile = fx && k <= 254 && std::atoi(env) == 1;
-        rs_svd_plan sh;
-        if (tile) {
-            sh.ctx = ctx;
-            sh.n_users = r->n_users;
-            sh.n_items = r->n_items;
-            sh.k = k;
-            sh.ld = ld;
-            sh.nnz = r->nnz;
-            sh.h_rowptr = csr.rowptr;
-            sh.h_cols = csr.cols;
-            sh.h_vals = csr.vals;
-            sh.tile_pp = true;
-            sh.tile_user_lds = rs::pp_tile_user_lds(k);
-            if (const char* env = std::getenv("RSGPU_PP_TILE_WG")) sh.tile_wg = std::max(0, std::atoi(env));
-            if (const char* env = std::getenv("RSGPU_PP_TILE_WAVES")) {
-                const int wv = std::atoi(env);
-                sh.tile_waves = (wv == 1 || wv == 4 || wv == 8) ? wv : 16;
-            }
-            try {
-                rs::tile_build(&sh);
-            } catch (const std::invalid_argument&) {
-                tile = false;  // a user whose ratings do not fit one tile
-            }
-        }
-        rs::DevBuf<double> tpart(tile ? static_cast<size_t>(sh.tile_grid) * sh.tile_waves : 1);
         RS_HIP(hipStreamSynchronize(s));
         rs::kernel_span_begin(ctx);
-        for (int32_t ep = 0; tile && ep < p->n_epochs; ++ep) {
-            rs::pp_tile_launch(sh, reinterpret_cast<int32_t*>(dQ.p), rs::buffer_bytes32(dQ.n, 4, "item factor matrix"),
-                               reinterpret_cast<int32_t*>(dY.p), rs::buffer_bytes32(dY.n, 4, "implicit factor matrix"), dP.p, dgb.p, tpart.p,
-                               lr, reg, k, ld, s);
-            hipLaunchKernelGGL(rs::pp_gb_fold_kernel, dim3(1), dim3(256), 0, s, tpart.p,
-                               static_cast<int64_t>(sh.tile_grid) * sh.tile_waves, dgb.p, inv_nnz);
-            RS_HIP(hipGetLastError());
-        }
-        for (int32_t ep = 0; !tile && ep < p->n_epochs; ++ep) {
+        for (int32_t ep = 0; ep < p->n_epochs; ++ep) {
             switch (E) {
-                case 1: rs::launch_pp_fast<1>(n_blocks, dwork, n_work, n_heavy, drow, dcol, dval, dP, dQ, dY, dgb, dpart, lr, reg, k, fx, s); break;
-                case 2: rs::launch_pp_fast<2>(n_blocks, dwork, n_work, n_heavy, drow, dcol, dval, dP, dQ, dY, dgb, dpart, lr, reg, k, fx, s); break;
-                case 3: rs::launch_pp_fast<3>(n_blocks, dwork, n_work, n_heavy, drow, dcol, dval, dP, dQ, dY, dgb, dpart, lr, reg, k, fx, s); break;
-                case 4: rs::launch_pp_fast<4>(n_blocks, dwork, n_work, n_heavy, drow, dcol, dval, dP, dQ, dY, dgb, dpart, lr, reg, k, fx, s); break;
-                case 5: rs::launch_pp_fast<5>(n_blocks, dwork, n_work, n_heavy, drow, dcol, dval, dP, dQ, dY, dgb, dpart, lr, reg, k, fx, s); break;
-                case 6: rs::launch_pp_fast<6>(n_blocks, dwork, n_work, n_heavy, drow, dcol, dval, dP, dQ, dY, dgb, dpart, lr, reg, k, fx, s); break;
-                case 7: rs::launch_pp_fast<7>(n_blocks, dwork, n_work, n_heavy, drow, dcol, dval, dP, dQ, dY, dgb, dpart, lr, reg, k, fx, s); break;
-                default: rs::launch_pp_fast<8>(n_blocks, dwork, n_work, n_heavy, drow, dcol, dval, dP, dQ, dY, dgb, dpart, lr, reg, k, fx, s); break;
+                case 1: rs::launch_pp_fast<1>(n_blocks, dwork, n_work, n_heavy, n_hblocks, drow, dcol, dval, dP, dQ, dY, dgb, dpart, lr, reg, k, fx, s); break;
+                case 2: rs::launch_pp_fast<2>(n_blocks, dwork, n_work, n_heavy, n_hblocks, drow, dcol, dval, dP, dQ, dY, dgb, dpart, lr, reg, k, fx, s); break;
+                case 3: rs::launch_pp_fast<3>(n_blocks, dwork, n_work, n_heavy, n_hblocks, drow, dcol, dval, dP, dQ, dY, dgb, dpart, lr, reg, k, fx, s); break;
+                case 4: rs::launch_pp_fast<4>(n_blocks, dwork, n_work, n_heavy, n_hblocks, drow, dcol, dval, dP, dQ, dY, dgb, dpart, lr, reg, k, fx, s); break;
+                case 5: rs::launch_pp_fast<5>(n_blocks, dwork, n_work, n_heavy, n_hblocks, drow, dcol, dval, dP, dQ, dY, dgb, dpart, lr, reg, k, fx, s); break;
+                case 6: rs::launch_pp_fast<6>(n_blocks, dwork, n_work, n_heavy, n_hblocks, drow, dcol, dval, dP, dQ, dY, dgb, dpart, lr, reg, k, fx, s); break;
+                case 7: rs::launch_pp_fast<7>(n_blocks, dwork, n_work, n_heavy, n_hblocks, drow, dcol, dval, dP, dQ, dY, dgb, dpart, lr, reg, k, fx, s); break;
+                default: rs::launch_pp_fast<8>(n_blocks, dwork, n_work, n_heavy, n_hblocks, drow, dcol, dval, dP, dQ, dY, dgb, dpart, lr, reg, k, fx, s); break;
             }
             RS_HIP(hipGetLastError());
             hipLaunchKernelGGL(rs::pp_gb_fold_kernel, dim3(1), dim3(256), 0, s, dpart.p,

@@ -334,7 +334,7 @@ class Context:
     def svdpp_fit(self, r: Ratings, P, Q, Y, bu=None, bi=None, gb=0.0, n_epochs=20, lr=0.007,
                   reg=0.02, mode=SGD_FAST, write_back=WB_TILE):
         """core/svd.go:316-427 (ORDERED: literal per-rating y updates; FAST: the user-major lazy-y
-        kernel; RSGPU_PP_TILE=1 selects the experimental tile schedule)."""
+        kernel)."""
         P = np.array(P, dtype=np.float64, order="C")
         Q = np.array(Q, dtype=np.float64, order="C")
         Y = np.array(Y, dtype=np.float64, order="C")
@@ -632,26 +632,18 @@ def comm_info():
 
 
 def tile_schedule_host(n_users, n_items, rowptr, cols, vals, n_factors, workgroups=256, waves=16,
-                       n_blocks=1, want_pos=False, svdpp=False):
-    """Host-only tile schedule build (rs_tile_schedule_host): (ms, n_tiles, pos or None); with
-    svdpp=True (ms, n_tiles, pos, tile_off, rank) of the SVD++ variant."""
+                       n_blocks=1, want_pos=False):
+    """Host-only tile schedule build (rs_tile_schedule_host): (ms, n_tiles, pos or None)."""
     rowptr = np.ascontiguousarray(rowptr, np.int64)
     cols = np.ascontiguousarray(cols, np.int32)
     vals = np.ascontiguousarray(vals, np.float32)
     nnz = int(rowptr[-1])
-    pos = np.empty(nnz, np.int64) if (want_pos or svdpp) else None
+    pos = np.empty(nnz, np.int64) if want_pos else None
     nt, ms = _i32(0), _dbl(0)
     _check(lib().rs_tile_schedule_host(n_users, n_items, _ptr(rowptr), _ptr(cols), _ptr(vals), n_factors,
-                                       workgroups, waves, n_blocks, int(svdpp), _ptr(pos), None, None,
+                                       workgroups, waves, n_blocks, 0, _ptr(pos), None, None,
                                        C.byref(nt), C.byref(ms)))
-    if not svdpp:
-        return ms.value, nt.value, pos
-    off = np.empty(nt.value + 1, np.int64)
-    rank = np.empty(nnz, np.int32)
-    _check(lib().rs_tile_schedule_host(n_users, n_items, _ptr(rowptr), _ptr(cols), _ptr(vals), n_factors,
-                                       workgroups, waves, n_blocks, 1, _ptr(pos), _ptr(off), _ptr(rank),
-                                       C.byref(nt), C.byref(ms)))
-    return ms.value, nt.value, pos, off, rank
+    return ms.value, nt.value, pos
 
 
 def item_shards(items, n_items, n_shards):

@@ -1,7 +1,7 @@
 """Experiment: SVD++ FAST (K2) held-out RMSE spread vs the sequential lazy restatement on the ML-1M
 shape (k=128, 20 epochs; the test_config2 setup) for several launch shapes, with the epoch time.
-Each configuration runs REPS fits; the oracle runs once.  Env CFGS = "blocks:heavy,..." ("d" keeps the
-library default)."""
+Each configuration runs REPS fits; the oracle runs once.  Env CFGS = "blocks:heavy[:heavy_blocks],..."
+(RSGPU_PP_BLOCKS, RSGPU_PP_HEAVY, RSGPU_PP_HBLOCKS (removed); "d" keeps the library default)."""
 import os
 import sys
 import time
@@ -43,8 +43,8 @@ print(f"oracle, LPT user order: held-out {e_lpt:.4f}", flush=True)
 ctx = rsgpu.Context(0)
 reps = int(os.environ.get("REPS", "3"))
 for cfg in os.environ.get("CFGS", "d:d,256:d,128:d,64:d,d:0").split(","):
-    nb, hv = cfg.split(":")
-    for key, v in (("RSGPU_PP_BLOCKS", nb), ("RSGPU_PP_HEAVY", hv)):
+    nb, hv, hb = (cfg.split(":") + ["d"])[:3]
+    for key, v in (("RSGPU_PP_BLOCKS", nb), ("RSGPU_PP_HEAVY", hv), ("RSGPU_PP_HBLOCKS", hb)):
         if v == "d":
             os.environ.pop(key, None)
         else:
@@ -56,5 +56,5 @@ for cfg in os.environ.get("CFGS", "d:d,256:d,128:d,64:d,d:0").split(","):
         errs.append(rmse(O.svdpp_predict(u[tr], i[tr], nu, u[te], i[te], *got), r[te]))
     gap = max(abs(e - e_ref) for e in errs)
     gap2 = max(abs(e - e_lpt) for e in errs)
-    print(f"blocks {nb:>4} heavy {hv:>5}: held-out {' '.join(f'{e:.4f}' for e in errs)} "
+    print(f"blocks {nb:>4} heavy {hv:>5} heavy blocks {hb:>4}: held-out {' '.join(f'{e:.4f}' for e in errs)} "
           f"max gap {gap:.4f} (LPT order {gap2:.4f}); epoch {ms:.3f} ms", flush=True)

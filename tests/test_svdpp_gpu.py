@@ -96,26 +96,3 @@ def test_svdpp_fast_rmse_near_literal(ctx, fold0):
     got = rmse(O.svdpp_predict(f.iu, f.ii, f.nu, f.tu, f.ti, *b), f.te_r)
     assert abs(got - ref) <= 0.005, (got, ref)
     assert got <= 0.92 + 0.008 + 0.01  # the reference's (disabled) bound, base_test.go:38-40
-
-
-@pytest.mark.parametrize("k,epochs", [(20, 1), (20, 2), (128, 1)])
-def test_svdpp_tile_one_wave_matches_oracle(ctx, fold0, monkeypatch, k, epochs):
-    """The SVD++ tile schedule (experimental, RSGPU_PP_TILE=1) with one workgroup of one wave is the lazy SGD of
-    svd.go:352-424 reorganised by tile -- or_svdpp_fit_tiles in the schedule's own visit order
-    (rs_tile_schedule_host exports it) -- to 1e-5, on a 20k-rating ML-100K prefix."""
-    f = fold0
-    n = 20000
-    u, i, r = f.iu[:n], f.ii[:n], f.r[:n]
-    nu, ni = int(u.max()) + 1, int(i.max()) + 1
-    rng = np.random.default_rng(k + epochs)
-    P0, Q0, Y0 = (rng.normal(0, 0.1, (m, k)) for m in (nu, ni, ni))
-    rowptr, items, rr = O.csr_by(u, nu, i, r)
-    _, nt, pos, off, rank = rsgpu.tile_schedule_host(nu, ni, rowptr, items, rr, k, workgroups=1, waves=1,
-                                                     svdpp=True)
-    ref = O.svdpp_fit_tiles(rowptr, items, rr, pos, off, rank, P0, Q0, Y0, epochs=epochs)
-    monkeypatch.setenv("RSGPU_PP_TILE", "1")
-    monkeypatch.setenv("RSGPU_PP_TILE_WG", "1")
-    monkeypatch.setenv("RSGPU_PP_TILE_WAVES", "1")
-    got = ctx.svdpp_fit(rsgpu.Ratings(u, i, r, nu, ni), P0, Q0, Y0, n_epochs=epochs)
-    assert _maxdiff(ref[:5], got[:5]) <= TOL, (k, epochs, nt)
-    assert abs(ref[5] - got[5]) <= TOL

@@ -38,3 +38,15 @@ def test_item_shard_shape():
     n = s.nnz
     s.close()
     assert np.array_equal(np.sort(pos), np.arange(n))
+
+
+def test_svdpp_variant_is_rejected():
+    """svdpp != 0 selected the SVD++ tile schedule, removed in round 3 (it diverged across
+    workgroups): the call fails loudly instead of building a schedule nothing runs."""
+    rowptr = np.array([0, 2], np.int64)
+    cols = np.array([0, 1], np.int32)
+    vals = np.array([3.0, 4.0], np.float32)
+    nt, ms = rsgpu._i32(0), rsgpu._dbl(0)
+    rc = rsgpu.lib().rs_tile_schedule_host(1, 2, rsgpu._ptr(rowptr), rsgpu._ptr(cols), rsgpu._ptr(vals), 8,
+                                           1, 1, 1, 1, None, None, None, rsgpu.C.byref(nt), rsgpu.C.byref(ms))
+    assert rc == rsgpu.RS_ERR_UNSUPPORTED
