@@ -80,6 +80,17 @@ __device__ __forceinline__ uint32_t sq_bytes(uint32_t w) {  // per byte x^2 (x <
     const u16x2 o2 = __builtin_bit_cast(u16x2, o) * __builtin_bit_cast(u16x2, o);
     return __builtin_bit_cast(uint32_t, e2) | (__builtin_bit_cast(uint32_t, o2) << 8);
 }
+__device__ __forceinline__ uint32_t sq_bytes_perm(uint32_t w) {  // sq_bytes in five operations
+    const uint32_t e = w & 0x00FF00FFu;                         // bytes 0, 2 as u16 lanes
+    const uint32_t o = __builtin_amdgcn_perm(0u, w, 0x0C030C01u);  // bytes 1, 3 as u16 lanes
+    const u16x2 e2 = __builtin_bit_cast(u16x2, e) * __builtin_bit_cast(u16x2, e);
+    const u16x2 o2 = __builtin_bit_cast(u16x2, o) * __builtin_bit_cast(u16x2, o);
+    // bytes [e2.lo, o2.lo, e2.hi, o2.hi]: selector picks byte 0 of e2 (4), byte 0 of o2 (0), ...
+    return __builtin_amdgcn_perm(__builtin_bit_cast(uint32_t, e2), __builtin_bit_cast(uint32_t, o2), 0x02060004u);
+}
+__device__ __forceinline__ uint32_t mask128_bytes(uint32_t w) {  // per byte 0x80 (= -128) where x > 0
+    return (w + 0x7F7F7F7Fu) & 0x80808080u;
+}
 __device__ __forceinline__ uint32_t mask_bytes(uint32_t w) {  // per byte [x > 0] (x <= 127)
     return ((w + 0x7F7F7F7Fu) & 0x80808080u) >> 7;
 }
@@ -92,7 +103,7 @@ __device__ __forceinline__ void lds_barrier() {
 // NWJ = 32-column MFMA tiles per wave along b: 2 -> four waves of 64 x 64 (one wave per SIMD,
 // 192 accumulator AGPRs); 1 -> eight waves of 64 x 32 (two waves per SIMD, 96 AGPRs each, so the
 // SIMD interleaves two waves' phases; PIPE 2 only).
-template <int KIND, int PIPE, int NWJ = 2, bool ROT = false>
+template <int KIND, int PIPE, int NWJ = 2, int ROT = 0, bool LEAN = false>
 __global__ __launch_bounds__(NWJ == 2 ? 256 : 512) void knn_sims_mfma_kernel(const int8_t* __restrict__ X,
                                                             int64_t ldk, int32_t L,
                                                             const int2* __restrict__ tiles,
@@ -219,7 +230,8 @@ __global__ __launch_bounds__(NWJ == 2 ? 256 : 512) void knn_sims_mfma_kernel(con
                 i32x4& d = side ? fb[s][2][i] : fa[s][2][i];
                 const i32x4& src = side ? fb[s][0][i] : fa[s][0][i];
 #pragma unroll
-                for (int e = 0; e < 4; ++e) d[e] = static_cast<int>(mask_bytes(static_cast<uint32_t>(src[e])));
+                for (int e = 0; e < 4; ++e)
+                    d[e] = static_cast<int>(LEAN ? mask128_bytes(static_cast<uint32_t>(src[e])) : mask_bytes(static_cast<uint32_t>(src[e])));
             } else if (side) {
                 fb[s][m][i] = frag(b, m, 1, i, s);
             } else {
@@ -247,7 +259,8 @@ __global__ __launch_bounds__(NWJ == 2 ? 256 : 512) void knn_sims_mfma_kernel(con
                 } else if (part == 1) {
                     if constexpr (KIND != 2) {
 #pragma unroll
-                        for (int d = 0; d < 4; ++d) sq[j][d] = static_cast<int>(sq_bytes(static_cast<uint32_t>(st[j][d])));
+                        for (int d = 0; d < 4; ++d)
+                            sq[j][d] = static_cast<int>(LEAN ? sq_bytes_perm(static_cast<uint32_t>(st[j][d])) : sq_bytes(static_cast<uint32_t>(st[j][d])));
                         *reinterpret_cast<i32x4*>(nb + 1 * 2 * kStageMat + dst[j]) = sq[j];
                     }
                 } else if (PIPE != 2) {  // PIPE 2 derives M from the X fragments instead
@@ -297,7 +310,7 @@ __global__ __launch_bounds__(NWJ == 2 ? 256 : 512) void knn_sims_mfma_kernel(con
     gload(st, 0);
     lstore(st, 0);
     lds_barrier();
-    if constexpr (ROT) {
+    if constexpr (ROT == 1) {
         // loads one step further ahead through a rotation: st (step t + 1, loaded during step
         // t - 1) is staged while st2 loads step t + 2; st = st2 at the end of the step, so a load
         // has a whole step to land before anything waits on it
@@ -346,7 +359,12 @@ __global__ __launch_bounds__(NWJ == 2 ? 256 : 512) void knn_sims_mfma_kernel(con
                     continue;
                 }
                 if (ta == tb && a > bb) continue;
-                const int64_t li = acc[0][i][j][q], mi = acc[1][i][j][q], ni = acc[2][i][j][q];
+                // LEAN: the M operand is -128 where rated, so its contractions carry a factor -128 (count:
+                // 16384); exact while a co-rated count stays below 2^17 (the host checks the row degrees)
+                constexpr bool m128 = LEAN && PIPE == 2;
+                const int64_t li = m128 && KIND == 2 ? -(acc[0][i][j][q] >> 7) : acc[0][i][j][q];
+                const int64_t mi = m128 ? -(acc[1][i][j][q] >> 7) : acc[1][i][j][q];
+                const int64_t ni = m128 ? (KIND == 2 ? acc[2][i][j][q] >> 14 : -(acc[2][i][j][q] >> 7)) : acc[2][i][j][q];
                 double v;
                 if constexpr (KIND == 2) {
                     // slope_one.go:68-88 for the pair i = bb > j = a: sum of (r_bb - r_a) over the
@@ -368,7 +386,7 @@ __global__ __launch_bounds__(NWJ == 2 ? 256 : 512) void knn_sims_mfma_kernel(con
                     v = l / (sqrt(m) * sqrt(n));
                 } else {
                     const double sum = static_cast<double>(mi + ni - 2 * li) * inv_s2;
-                    const double count = static_cast<double>(acc[3][i][j][q]);
+                    const double count = static_cast<double>(m128 ? (acc[3][i][j][q] >> 14) : acc[3][i][j][q]);
                     v = 1.0 / (sum / count + 1.0);
                 }
                 S[static_cast<int64_t>(a) * L + bb] = v;
@@ -857,11 +875,22 @@ static bool sims_device(rs_ctx* ctx, int32_t kind, int32_t L, int32_t R, const S
         const size_t lds = 2 * kStageBytes;
         // K loop (RSGPU_KNN_PIPE, the variants the tests cross-check against each other):
         // 5 = default: software pipeline on eight waves (two per SIMD, 64 x 32 each), M derived from the X
-        // fragments in registers, X loads rotated one step further ahead; 3 = the same without the
-        // rotation; 4 = the pipeline on eight waves with M staged in LDS; 0 = round 1 (four waves, phases
-        // in sequence).  (The four-wave pipelined loops of round 2, 1 and 2, were slower and are gone.)
+        // fragments in registers, X loads rotated one step further ahead, and the LEAN operand forms
+        // (M = -128 where rated: two VALU operations per dword instead of three; x^2 by two byte
+        // permutes around the packed multiplies: five instead of six) -- 107 VALU per 12 MFMAs instead of
+        // 139, 155 -> 148 ms on the ML-20M shape; 6 = the same without LEAN (also the default when a row
+        // has 2^17 or more ratings: a co-rated count times 16384 must fit int32); 3 = without the
+        // rotation; 4 = M staged in LDS; 0 = round 1 (four waves, phases in sequence).  Measured and
+        // dropped in round 3 (profiles/r03_experiments/knn_k4.log): a third register set (loads two
+        // whole steps ahead: no change), s_setprio for the second half of the waves (no change), x^2
+        // stored in HBM beside X (196 ms: the doubled operand traffic costs more than the VALU it saves).
+        int64_t max_deg = 0;
+        for (int32_t a = 0; a < L; ++a) max_deg = std::max(max_deg, sr.rowptr[a + 1] - sr.rowptr[a]);
+        const bool lean_ok = max_deg < (int64_t{1} << 17);
         const char* pipe_env = std::getenv("RSGPU_KNN_PIPE");
-        const int pipe = (pipe_env && (pipe_env[0] == '0' || pipe_env[0] == '3' || pipe_env[0] == '4')) ? pipe_env[0] - '0' : 5;
+        int pipe = (pipe_env && (pipe_env[0] == '0' || pipe_env[0] == '3' || pipe_env[0] == '4' || pipe_env[0] == '6'))
+                       ? pipe_env[0] - '0' : 5;
+        if (pipe == 5 && !lean_ok) pipe = 6;
         for (const void* f : {reinterpret_cast<const void*>(&knn_sims_mfma_kernel<0, 0>),
                               reinterpret_cast<const void*>(&knn_sims_mfma_kernel<1, 0>),
                               reinterpret_cast<const void*>(&knn_sims_mfma_kernel<2, 0>),
@@ -871,9 +900,12 @@ static bool sims_device(rs_ctx* ctx, int32_t kind, int32_t L, int32_t R, const S
                               reinterpret_cast<const void*>(&knn_sims_mfma_kernel<0, 1, 1>),
                               reinterpret_cast<const void*>(&knn_sims_mfma_kernel<1, 1, 1>),
                               reinterpret_cast<const void*>(&knn_sims_mfma_kernel<2, 1, 1>),
-                              reinterpret_cast<const void*>(&knn_sims_mfma_kernel<0, 2, 1, true>),
-                              reinterpret_cast<const void*>(&knn_sims_mfma_kernel<1, 2, 1, true>),
-                              reinterpret_cast<const void*>(&knn_sims_mfma_kernel<2, 2, 1, true>)})
+                              reinterpret_cast<const void*>(&knn_sims_mfma_kernel<0, 2, 1, 1>),
+                              reinterpret_cast<const void*>(&knn_sims_mfma_kernel<1, 2, 1, 1>),
+                              reinterpret_cast<const void*>(&knn_sims_mfma_kernel<2, 2, 1, 1>),
+                              reinterpret_cast<const void*>(&knn_sims_mfma_kernel<0, 2, 1, 1, true>),
+                              reinterpret_cast<const void*>(&knn_sims_mfma_kernel<1, 2, 1, 1, true>),
+                              reinterpret_cast<const void*>(&knn_sims_mfma_kernel<2, 2, 1, 1, true>)})
             RS_HIP(hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(lds)));
         auto launch = [&](size_t first, size_t count, hipStream_t st) {
             if (!count) return;
@@ -881,21 +913,19 @@ static bool sims_device(rs_ctx* ctx, int32_t kind, int32_t L, int32_t R, const S
             auto go = [&](auto kern, int threads) {
                 hipLaunchKernelGGL(kern, grid, dim3(threads), lds, st, X.p, ldk, L, dtiles.p + first, inv_s2, dS.p);
             };
-            auto by_pipe = [&](auto k0, auto k3, auto k4, auto k5) {
-                pipe == 0 ? go(k0, 256) : pipe == 3 ? go(k3, 512) : pipe == 4 ? go(k4, 512) : go(k5, 512);
+            auto by_pipe = [&](auto k0, auto k3, auto k4, auto k5, auto k6) {
+                pipe == 0 ? go(k0, 256) : pipe == 3 ? go(k3, 512) : pipe == 4 ? go(k4, 512) : pipe == 6 ? go(k6, 512)
+                          : go(k5, 512);
             };
             if (kind == RS_SIM_COSINE)
-                by_pipe(knn_sims_mfma_kernel<0, 0>,
-                        knn_sims_mfma_kernel<0, 2, 1>, knn_sims_mfma_kernel<0, 1, 1>,
-                        knn_sims_mfma_kernel<0, 2, 1, true>);
+                by_pipe(knn_sims_mfma_kernel<0, 0>, knn_sims_mfma_kernel<0, 2, 1>, knn_sims_mfma_kernel<0, 1, 1>,
+                        knn_sims_mfma_kernel<0, 2, 1, 1, true>, knn_sims_mfma_kernel<0, 2, 1, 1>);
             else if (kind == RS_SIM_MSD)
-                by_pipe(knn_sims_mfma_kernel<1, 0>,
-                        knn_sims_mfma_kernel<1, 2, 1>, knn_sims_mfma_kernel<1, 1, 1>,
-                        knn_sims_mfma_kernel<1, 2, 1, true>);
+                by_pipe(knn_sims_mfma_kernel<1, 0>, knn_sims_mfma_kernel<1, 2, 1>, knn_sims_mfma_kernel<1, 1, 1>,
+                        knn_sims_mfma_kernel<1, 2, 1, 1, true>, knn_sims_mfma_kernel<1, 2, 1, 1>);
             else
-                by_pipe(knn_sims_mfma_kernel<2, 0>,
-                        knn_sims_mfma_kernel<2, 2, 1>, knn_sims_mfma_kernel<2, 1, 1>,
-                        knn_sims_mfma_kernel<2, 2, 1, true>);
+                by_pipe(knn_sims_mfma_kernel<2, 0>, knn_sims_mfma_kernel<2, 2, 1>, knn_sims_mfma_kernel<2, 1, 1>,
+                        knn_sims_mfma_kernel<2, 2, 1, 1, true>, knn_sims_mfma_kernel<2, 2, 1, 1>);
             RS_HIP(hipGetLastError());
         };
         if (host && n_parts == 1) {

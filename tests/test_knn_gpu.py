@@ -194,7 +194,8 @@ def test_knn_streamed_download_multi_group(ctx, kind, monkeypatch):
     """rs_knn_sims streams the Sims to the host while later column groups still compute (one launch
     per 2048-row super-tile column group, rows copied as their groups complete).  With L = 4700
     (3 groups, a ragged last block) the streamed result equals, bit for bit: the device plan's
-    one-launch Sims, the eight-wave tilings (RSGPU_KNN_PIPE=3, 4), the same call with the round-1 K loop (RSGPU_KNN_PIPE=0) and without streaming
+    one-launch Sims, the eight-wave tilings (RSGPU_KNN_PIPE=3, 4, 5 and 6: the default with and without
+    the LEAN operand forms), the same call with the round-1 K loop (RSGPU_KNN_PIPE=0) and without streaming
     (RSGPU_KNN_NO_STREAM=1), and the oracle's restatement (knn.go:190-216) on rows from every group."""
     rng = np.random.default_rng(11)
     L, R, nnz = 4700, 900, 120_000
@@ -210,7 +211,7 @@ def test_knn_streamed_download_multi_group(ctx, kind, monkeypatch):
     plan = ctx.knn_plan(kind, rowptr, ids, rr, R)
     assert bitwise_equal(S, plan.sims())
     plan.close()
-    for pipe in ("3", "4", "5"):  # eight waves of 64 x 32 (two per SIMD): M in registers / staged / rotated loads
+    for pipe in ("3", "4", "5", "6"):  # eight waves of 64 x 32 (two per SIMD): M in registers / staged / rotated loads (LEAN / not)
         monkeypatch.setenv("RSGPU_KNN_PIPE", pipe)
         assert bitwise_equal(S, ctx.knn_sims(kind, rowptr, ids, rr, R)), pipe
     monkeypatch.setenv("RSGPU_KNN_NO_STREAM", "1")
