@@ -682,6 +682,13 @@ void build_tile_host(const rs_svd_plan* pl, int32_t u_begin, int32_t u_end, int3
 // d * grid * waves / nnz runs at a time, each c/2 updates ahead of memory on average, so about
 // S = d * grid * waves * c / (2 nnz); uncut runs (c = d / grid) give S = waves * d^2 / (2 nnz) -- 290 for
 // ML-1M's hottest item at 16 waves, where 20-epoch training diverged; 8-rating pieces give ~100.
+// The cap is at least dmax * 256 / nnz: every piece of a run ends in one atomic row on the item's
+// single q_i row, and those atomics serialise at the memory side, so the hottest row gets at most
+// about nnz / 256 of them per epoch -- the ratings one CU trains.  On configs[4]'s shard (k = 256,
+// hottest item 3.4M of 126M ratings) the staleness model alone gives 2 and the hottest row's 1.7M
+// atomic rows bound the epoch at 143 ms; caps 4 / 6 / 8 / 10 / 12 give 92 / 80 / 76 / 74 / 75 ms at the
+// same held-out RMSE after five epochs (0.8815-0.8818; profiles/r03_experiments/cfg4_ring.log), and 7
+// is what this rule picks.  On ML-1M (dmax 3428) it is 1 and changes nothing.
 constexpr double kStaleTarget = 100.0;
 int32_t auto_run_cap(const rs_svd_plan* pl, int32_t grid, int32_t waves) {
     if (waves <= 1 || pl->nnz == 0) return 0;
@@ -690,7 +697,8 @@ int32_t auto_run_cap(const rs_svd_plan* pl, int32_t grid, int32_t waves) {
     const int64_t dmax = *std::max_element(deg.begin(), deg.end());
     const double c = 2.0 * kStaleTarget * static_cast<double>(pl->nnz) /
                      (static_cast<double>(dmax) * grid * waves);
-    return c >= 1e6 ? 0 : std::max(2, static_cast<int32_t>(c));
+    const int64_t c_hot = (dmax * 256 + pl->nnz - 1) / pl->nnz;
+    return c >= 1e6 ? 0 : static_cast<int32_t>(std::max<int64_t>({2, static_cast<int64_t>(c), c_hot}));
 }
 
 // Ratings per tile: nnz / workgroups, but at least the heaviest user's ratings (cutting users into
