@@ -276,7 +276,7 @@ __global__ __launch_bounds__(256) void svdpp_epoch_fast_kernel(
             pp_sum_y<E, YB, FX>(ry, items, b, e, 0, YB, lane4, lcy, S0);
 #pragma unroll
             for (int x = 0; x < E; ++x) Cv[x] = 0.f;
-            pp_chain<E, 8, FX>(rq, items, ratings, b, e, lane, lcq, lr, a, S0, p, ub, gb, A, Cv,
+            pp_chain<E, D, FX>(rq, items, ratings, b, e, lane, lcq, lr, a, S0, p, ub, gb, A, Cv,
                                [&](int32_t row, const float (&qw)[E], const float (&q)[E]) {
 #pragma unroll
                                    for (int x = 0; x < E; ++x)
@@ -532,6 +532,7 @@ static void launch_pp_fast(int32_t n_blocks, const DevBuf<int32_t>& work, int32_
                            const DevBuf<float>& ratings, DevBuf<float>& P, DevBuf<float>& Q,
                            DevBuf<float>& Y, DevBuf<double>& gb, DevBuf<double>& partial, float lr,
                            float reg, int32_t kf, bool fx, hipStream_t s) {
+    // light ring depth 8: 16 and 32 measured slower (1.33 / 1.34 against 1.28 ms per ML-1M epoch, k = 128)
     auto kern = fx ? svdpp_epoch_fast_kernel<E, 8, true> : svdpp_epoch_fast_kernel<E, 8, false>;
     hipLaunchKernelGGL(kern, dim3(n_blocks), dim3(256), 0, s, work.p,
                        n_work, n_heavy, n_hblocks, rowptr.p, items.p, ratings.p, P.p, Q.p, Y.p,
@@ -557,7 +558,7 @@ extern "C" int rs_svdpp_fit(rs_ctx* ctx, const rs_ratings* r, const rs_sgd_param
         const float lr = static_cast<float>(p->lr), reg = static_cast<float>(p->reg);
         rs::UserCSR csr;  // N(u) = TrainSet.UserRatings() (data.go:185-199), data order
         rs::build_csr(r->nnz, r->n_users, r->users, r->items, r->ratings, csr);
-        csr.cols.resize(csr.cols.size() + 64, 0);
+        csr.cols.resize(csr.cols.size() + 64, 0);  // pp_chain reads ids up to 3 batches (<= 48) ahead
         csr.vals.resize(csr.vals.size() + 64, 0.f);
         rs::DevBuf<int64_t> drow(csr.rowptr.size());
         rs::DevBuf<int32_t> dcol(csr.cols.size());
