@@ -127,8 +127,10 @@ def ordered_throughput(ctx, u, i, r, n_users, n_items):
     ctx.svd_fit(R, P0[:, :K], Q0, n_epochs=1, mode=rsgpu.SGD_ORDERED)
     ms = ctx.last_kernel_ms()
     return {"value": len(r) / (ms / 1e3), "unit": "updates/s", "epoch_ms_kernel": ms,
-            "note": "one wave walks the ratings in the reference order with a 14-deep row prefetch ring "
-                    "(factors within 1e-5 of the oracle; csrc/sgd_ordered.hip); kernel-only time of one epoch"}
+            "note": "one workgroup walks the ratings in the reference order in conflict-free batches (no user "
+                    "or item twice, <= 64 ratings; rows prefetched a batch ahead, the previous batch's rows "
+                    "forwarded through LDS, the GlobalBias chain as a lane-parallel scan; factors within 1e-5 "
+                    "of the oracle; csrc/sgd_ordered.hip); kernel-only time of one epoch"}
 
 
 def load_traffic():

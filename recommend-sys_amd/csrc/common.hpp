@@ -3,6 +3,8 @@
 
 #include <hip/hip_runtime.h>
 
+#include <functional>
+
 #include <algorithm>
 #include <cstdint>
 #include <cstdio>
@@ -125,6 +127,14 @@ struct UserCSR {
 };
 void build_csr(int64_t nnz, int32_t n_rows, const int32_t* rows, const int32_t* cols,
                const double* vals, UserCSR& out);
+
+// ingest.cpp: host threads (n_threads <= 0: min(hardware threads, 16)); parallel_run(n, fn) runs fn(t),
+// t < n, on n threads (the caller's included) and rethrows the first exception; csr_build is the stable
+// COO -> CSR of build_csr on T threads
+int32_t clamp_threads(int32_t n_threads);
+void parallel_run(int32_t n, const std::function<void(int32_t)>& fn);
+void csr_build(int64_t nnz, int32_t n_rows, const int32_t* rows, const int32_t* cols, const double* vals,
+               int32_t n_threads, int64_t* rowptr, int32_t* cols_out, float* vals_out);
 
 // FAST-mode GlobalBias warm start: the least-squares bias given the current b_u, b_i (factors
 // ignored), i.e. mean(r - b_u - b_i).  The sequential reference reaches this value within its first

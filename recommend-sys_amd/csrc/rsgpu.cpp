@@ -32,24 +32,30 @@ void unpack_rows_f64(const std::vector<float>& src, int64_t rows, int32_t k, int
 }
 
 void build_csr(int64_t nnz, int32_t n_rows, const int32_t* rows, const int32_t* cols,
-               const double* vals, UserCSR& out) {
-    out.rowptr.assign(static_cast<size_t>(n_rows) + 1, 0);
-    for (int64_t t = 0; t < nnz; ++t) out.rowptr[rows[t] + 1]++;
-    for (int32_t x = 0; x < n_rows; ++x) out.rowptr[x + 1] += out.rowptr[x];
-    std::vector<int64_t> fill(out.rowptr.begin(), out.rowptr.end() - 1);
+               const double* vals, UserCSR& out) {  // stable: data order within a row (ingest.cpp)
+    out.rowptr.resize(static_cast<size_t>(n_rows) + 1);
     out.cols.resize(static_cast<size_t>(nnz));
     out.vals.resize(static_cast<size_t>(nnz));
-    for (int64_t t = 0; t < nnz; ++t) {  // stable: data order within a row
-        const int64_t d = fill[rows[t]]++;
-        out.cols[d] = cols[t];
-        out.vals[d] = static_cast<float>(vals[t]);
-    }
+    csr_build(nnz, n_rows, rows, cols, vals, 0, out.rowptr.data(), out.cols.data(), out.vals.data());
 }
 
+// mean(r - b_u - b_i) over fixed 2^16-rating chunks summed in order (independent of the thread count)
 double gb_warm_start(const rs_ratings* r, const double* bu, const double* bi) {
     if (r->nnz <= 0) return 0.0;
+    constexpr int64_t kChunk = int64_t{1} << 16;
+    const int64_t nc = (r->nnz + kChunk - 1) / kChunk;
+    std::vector<double> part(static_cast<size_t>(nc), 0.0);
+    const int32_t T = static_cast<int32_t>(std::min<int64_t>(clamp_threads(0), nc));
+    parallel_run(T, [&](int32_t th) {
+        for (int64_t c = th; c < nc; c += T) {
+            double s = 0.0;
+            for (int64_t t = c * kChunk, e = std::min(r->nnz, (c + 1) * kChunk); t < e; ++t)
+                s += r->ratings[t] - bu[r->users[t]] - bi[r->items[t]];
+            part[c] = s;
+        }
+    });
     double s = 0.0;
-    for (int64_t t = 0; t < r->nnz; ++t) s += r->ratings[t] - bu[r->users[t]] - bi[r->items[t]];
+    for (double x : part) s += x;
     return s / static_cast<double>(r->nnz);
 }
 
@@ -59,11 +65,22 @@ int check_ratings(rs_ctx* ctx, const rs_ratings* r) {
         return set_error(ctx, RS_ERR_INVALID, "negative size");
     if (r->nnz > 0 && (!r->users || !r->items || !r->ratings))
         return set_error(ctx, RS_ERR_INVALID, "ratings arrays are NULL");
-    for (int64_t t = 0; t < r->nnz; ++t) {
+    // the first offending position (the same message whatever the thread count)
+    const int32_t T = static_cast<int32_t>(std::max<int64_t>(1, std::min<int64_t>(clamp_threads(0), r->nnz >> 16)));
+    std::vector<int64_t> bad(static_cast<size_t>(T), -1);
+    parallel_run(T, [&](int32_t th) {
+        for (int64_t t = r->nnz * th / T, e = r->nnz * (th + 1) / T; t < e; ++t)
+            if (static_cast<uint32_t>(r->users[t]) >= static_cast<uint32_t>(r->n_users) ||
+                static_cast<uint32_t>(r->items[t]) >= static_cast<uint32_t>(r->n_items)) {
+                bad[th] = t;
+                return;
+            }
+    });
+    for (int64_t t : bad) {
+        if (t < 0) continue;
         if (r->users[t] < 0 || r->users[t] >= r->n_users)
             return set_error(ctx, RS_ERR_INVALID, "user id out of range at " + std::to_string(t));
-        if (r->items[t] < 0 || r->items[t] >= r->n_items)
-            return set_error(ctx, RS_ERR_INVALID, "item id out of range at " + std::to_string(t));
+        return set_error(ctx, RS_ERR_INVALID, "item id out of range at " + std::to_string(t));
     }
     return RS_OK;
 }

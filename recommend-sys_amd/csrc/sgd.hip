@@ -2071,7 +2071,7 @@ extern "C" int rs_svd_fit(rs_ctx* ctx, const rs_ratings* r, const rs_sgd_params*
             mark("download");
             return RS_OK;
         }
-        // ORDERED: COO in train-set order, one wave, all epochs in one launch (sgd_ordered.hip), rows in the
+        // ORDERED: COO in train-set order, conflict-free batches on one workgroup, all epochs in one launch (sgd_ordered.hip), rows in the
         // folded layout P [p, b_u, 1], Q [q, 1, b_i]
         rs::drop_fit_cache(ctx);
         hipStream_t s = ctx->stream;
@@ -2106,9 +2106,18 @@ extern "C" int rs_svd_fit(rs_ctx* ctx, const rs_ratings* r, const rs_sgd_params*
         dP.upload(hP.data(), hP.size(), s);
         dQ.upload(hQ.data(), hQ.size(), s);
         dgb.upload(gb, 1, s);
+        const rs::OrderedSchedule os = rs::ordered_batches(r->users, r->items, nnz, r->n_users, r->n_items,
+                                                           rs::ordered_wmax(ld));
+        const int64_t nbs = static_cast<int64_t>(os.start.size());
+        rs::DevBuf<int64_t> dbs(nbs);
+        rs::DevBuf<int32_t> dfw(npad);
+        dbs.upload(os.start.data(), nbs, s);
+        RS_HIP(hipMemsetAsync(dfw.p, 0, npad * sizeof(int32_t), s));
+        dfw.upload(os.fwd.data(), nnz, s);
         rs::kernel_span_begin(ctx);
         if (nnz > 0 && p->n_epochs > 0)
-            rs::ordered_epochs(du.p, di.p, dr.p, nnz, dP.p, pn, dQ.p, qn, ld, k, dgb.p, p->n_epochs, lr, reg, s);
+            rs::ordered_epochs(du.p, di.p, dr.p, dfw.p, nnz, dbs.p, nbs - 1, dP.p, pn, dQ.p, qn, ld, k, dgb.p,
+                               p->n_epochs, lr, reg, s);
         rs::kernel_span_end(ctx);
         dP.download(hP.data(), hP.size(), s);
         dQ.download(hQ.data(), hQ.size(), s);

@@ -4,25 +4,24 @@
 //
 // The serial dependence of that loop is narrower than it looks: rating t needs the rows rating t - d
 // wrote only when it shares the user or the item, and the only state EVERY rating shares is the scalar
-// GlobalBias chain gb <- gb - lr ((gb + b_u + b_i + p.q) - r) (svd.go:102-106).  So one wave walks the
-// ratings with
-//   * the rows of rating t + D loaded while rating t computes (a D-deep register ring), ids read by
-//     scalar loads two blocks of D ahead;
-//   * a prefetched row that one of the last D ratings rewrote after its load was issued loaded again
-//     (a uniform branch that rarely runs);
+// GlobalBias chain gb <- gb - lr ((gb + b_u + b_i + p.q) - r) (svd.go:102-106), a first-order linear
+// recurrence.  So the ratings are cut into batches in which no user and no item repeats, a batch's
+// ratings run in parallel, and the chain runs as a scan (svd_ordered_batch_kernel below).  Also:
 //   * the biases folded into the rows -- P row [p_0 .. p_{k-1}, b_u, 1], Q row [q_0 .. q_{k-1}, 1, b_i]
 //     -- so p.q over all columns is the prediction minus gb, and the one update p <- a p - c q,
 //     q <- a q - c p_new also performs svd.go:108-112 (the constant columns are held at 1);
 //   * gb, the prediction and diff in float64 (the chain), the row arithmetic in float32.
-// The result is the sequential epoch exactly (no reordering), within float32 rounding of the fp64
-// restatement (tests/test_svd_gpu.py::test_ordered_matches_oracle, 1e-5).  One rating costs about 85
-// instructions, most of them on its own dependency chain (DPP reduction, the f64 chain, the updates):
-// 222 ms per ML-1M epoch (4.5e6 updates/s) against 515 ms for round 2's 16-lane group.
+// The result is the sequential epoch (no reordering), within float32 rounding of the fp64 restatement
+// (tests/test_svd_gpu.py::test_ordered_*, 1e-5).  ML-1M shape, k = 100: 76.5 ms per epoch
+// (1.31e7 updates/s); round 3's one-wave ring kernel took 222 ms, round 2's 16-lane group 515 ms.
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cstdio>
+#include <cstdlib>
 #include <stdexcept>
 #include <type_traits>
+#include <vector>
 
 #include "common.hpp"
 #include "sgd_plan.hpp"
@@ -31,40 +30,57 @@ namespace rs {
 
 namespace {
 
-// sum over the wave, valid in lane 63 (DPP row sums, then row_bcast:15 / row_bcast:31)
-__device__ __forceinline__ float ordered_wave_sum(float x) {
-    x = group_sum<16>(x);
-    x += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(x), 0x142, 0xA, 0xF, false));
-    x += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(x), 0x143, 0xC, 0xF, false));
-    return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(x), 63));
+// DPP move of a double (both halves; lanes without a source read 0, rows outside row_mask keep 0)
+template <int C, int RM>
+__device__ __forceinline__ double dpp_f64(double v) {
+    const uint64_t b = __builtin_bit_cast(uint64_t, v);
+    const uint32_t lo = __builtin_amdgcn_update_dpp(0u, static_cast<uint32_t>(b), C, RM, 0xF, false);
+    const uint32_t hi = __builtin_amdgcn_update_dpp(0u, static_cast<uint32_t>(b >> 32), C, RM, 0xF, false);
+    return __builtin_bit_cast(double, (static_cast<uint64_t>(hi) << 32) | lo);
+}
+
+__device__ __forceinline__ double readlane_f64(double x, int j) {
+    const uint64_t b = __builtin_bit_cast(uint64_t, x);
+    const uint32_t lo = __builtin_amdgcn_readlane(static_cast<uint32_t>(b), j);
+    const uint32_t hi = __builtin_amdgcn_readlane(static_cast<uint32_t>(b >> 32), j);
+    return __builtin_bit_cast(double, (static_cast<uint64_t>(hi) << 32) | lo);
 }
 
 }  // namespace
 
-// One wave; lane l holds the column pairs (128 h + 2 l, 128 h + 2 l + 1), h < H, of a row: one 8-byte
-// load / store and one packed-math op per pair.  Rows are ld floats (ld even, ld >= k + 2,
-// ld <= 128 H); the id and rating arrays hold whole blocks of D entries (padded).  All epochs in one
-// launch.
-//
-// Rating t's rows are loaded when rating t - D ends (ring slot t mod D).  If one of the ratings in
-// between wrote the same user or item row (a rare, uniform branch: about one rating in seventy on the
-// ML-1M shape), the row is loaded again.  The loop body is D ratings with every slot issuing the same
-// loads and stores (an empty slot's go to out-of-range offsets), so the compiler's vmcnt waits keep the
-// whole ring in flight.  Measured alternatives (DESIGN.md K1 ORDERED): a float4-per-lane layout with the
-// rewritten rows forwarded from registers (277 ms per ML-1M epoch), blocks of 4 ratings run as one
-// group with interleaved reductions (288-309 ms), against 222 ms for this loop.
-template <int H, int D>
-__global__ __launch_bounds__(64) void svd_ordered_wave_kernel(
+// One workgroup of NW waves walks the ratings in BATCHES: maximal runs of consecutive ratings (at most
+// W = NW * R) in which no user and no item repeats (ordered_batches, on the host; 30.5 ratings on
+// average on the ML-1M shape at W = 64).  Inside a batch the ratings touch disjoint rows, so their row
+// updates commute; what they share is the GlobalBias chain gb <- gb - lr (gb + d_j) (svd.go:102-106,
+// d_j = p.q + b_u + b_i - r_j), a first-order linear recurrence gb_{j+1} = a gb_j - lr d_j with a = 1 - lr:
+//   1. wave w holds the rows of ratings w, w + NW, ... of batch c in registers (prefetched during batch
+//      c - 1), except rows batch c - 1 rewrote, which it reads from the LDS copy that batch left;
+//      it reduces d_j (biases folded into the rows) into LDS;
+//   2. after one barrier every wave runs the chain as a lane-parallel scan of the affine maps (lane j:
+//      gb after rating j, in six DPP steps), and issues the loads of batch c + 1's rows;
+//   3. each wave applies svd.go:108-128 to its rows (p first, then q with the new p: Q1), stores them
+//      and leaves a copy in LDS for batch c + 1.
+// A row batch c + 1 loads from memory was last written by batch c - 1 or earlier; every wave drains its
+// stores of batch c - 1 before batch c's first barrier, and batch c + 1's loads are issued after it.
+// The result is the sequential epoch (the same rows meet the same updates in the same order); the
+// GlobalBias values are the reference's recurrence evaluated in scan order (fp64; within 1e-15).
+template <int H, int NW, int R>
+__global__ __launch_bounds__(NW * 64) void svd_ordered_batch_kernel(
     const int32_t* __restrict__ users, const int32_t* __restrict__ items, const float* __restrict__ ratings,
-    int64_t nnz, int64_t n_blocks /* per epoch, of D ratings */, float* P, int32_t p_bytes, float* Q,
-    int32_t q_bytes, int32_t ld, int32_t kf, double* gb_io, int32_t epochs, float lr, float reg) {
+    const int32_t* __restrict__ fwd, const int64_t* __restrict__ bstart, int64_t n_batches, float* P,
+    int32_t p_bytes, float* Q, int32_t q_bytes, int32_t ld, int32_t kf, double* gb_io, int32_t epochs, float lr,
+    float reg, uint64_t* prof /* diagnostics (RSGPU_ORDERED_PROF): wave 0's cycles per phase, or NULL */) {
 #pragma clang fp contract(fast)
+    constexpr int W = NW * R;
+    static_assert(W <= 64, "a batch spans at most one wave's lanes");
     typedef float f2 __attribute__((ext_vector_type(2)));
-    const int lane = static_cast<int>(threadIdx.x);
+    typedef uint32_t u2 __attribute__((ext_vector_type(2)));
+    __shared__ double sd[W];
+    __shared__ f2 fp[W][H][64], fq[W][H][64];  // the rows batch c wrote, for batch c + 1
+    const int lane = static_cast<int>(threadIdx.x & 63);
+    const int w = __builtin_amdgcn_readfirstlane(static_cast<int>(threadIdx.x >> 6));
     const __amdgpu_buffer_rsrc_t rp = __builtin_amdgcn_make_buffer_rsrc(P, 0, p_bytes, 0x00020000);
     const __amdgpu_buffer_rsrc_t rq = __builtin_amdgcn_make_buffer_rsrc(Q, 0, q_bytes, 0x00020000);
-    // per pair: byte offset inside a row (kOutOfRange past it: 2^31 lies past every buffer) and the update's
-    // multipliers, which hold the constant columns at 1 (P: k + 1, Q: k): x <- x * am - y * (c * cm)
     int32_t coff[H];
     f2 amp[H], cmp[H], amq[H], cmq[H];
     const float a = 1.f - lr * reg;
@@ -81,140 +97,257 @@ __global__ __launch_bounds__(64) void svd_ordered_wave_kernel(
             cmq[h][e] = kq ? 0.f : 1.f;
         }
     }
-    const double lrd = lr;
+    const double lrd = lr, al = 1.0 - lrd;
+    // powers of a for the scan: a^(lane+1), a^(lane mod 16 + 1), a^(lane mod 32 + 1), a^1,2,4,8
+    double pw1 = al, pw16 = al, pw32 = al;
+    {
+        double x = al;
+        for (int j = 1; j < 64; ++j) {
+            x *= al;
+            pw1 = lane == j ? x : pw1;
+            pw16 = (lane & 15) == j ? x : pw16;
+            pw32 = (lane & 31) == j ? x : pw32;
+        }
+    }
+    const double a2 = al * al, a4 = a2 * a2, a8 = a4 * a4;
     double gb = gb_io[0];
-    const int64_t total = n_blocks * static_cast<int64_t>(epochs);
-    auto rl = [](int32_t x, int j) { return __builtin_amdgcn_readlane(x, j); };
-    // byte offset of pair h of `row`: no branch on the row (a uniform condition would become a branch
-    // around the memory operation and the vmcnt waits would lose count); row -1 and the pairs past the
-    // row wrap to offsets past the buffer's end, which load 0 and drop the store
     auto off = [&](int32_t row, int h) {
         return static_cast<int32_t>(static_cast<uint32_t>(row) * static_cast<uint32_t>(ld * 4) + static_cast<uint32_t>(coff[h]));
     };
-    auto load_row = [&](__amdgpu_buffer_rsrc_t r, int32_t row, f2 (&dst)[H]) {
-#pragma unroll
-        for (int h = 0; h < H; ++h)
-            dst[h] = __builtin_bit_cast(f2, __builtin_amdgcn_raw_buffer_load_b64(r, off(row, h), 0, kSgdAux));
+    const int64_t total = n_batches * static_cast<int64_t>(epochs);
+    // A batch's ids live in VGPRs, lane x holding slot x (rating w + NW x): user, item, forward word (bits
+    // 0-7: 1 + the slot of the previous batch that wrote this user's row, 0: none; bits 8-15 the same for
+    // the item), rating.  Everything the loop reads from memory is a VECTOR load (vmcnt) issued a batch or
+    // two ahead -- scalar loads would share lgkmcnt with the LDS traffic, and every LDS wait would then
+    // wait for them too.  The arrays are padded by 64 entries past nnz; lanes x >= R repeat slot R - 1.
+    struct Ids {
+        int32_t u, i, f;
+        float r;
     };
-    auto store_row = [&](__amdgpu_buffer_rsrc_t r, int32_t row, const f2 (&src)[H]) {
-#pragma unroll
-        for (int h = 0; h < H; ++h)
-            __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(__attribute__((ext_vector_type(2))) uint32_t, src[h]),
-                                                  r, off(row, h), 0, 0);
+    const int xl = lane < R ? lane : R - 1;
+    auto fetch_ids = [&](int64_t s0, Ids& d) {
+        const int64_t e = s0 + w + NW * xl;
+        d.u = users[e];
+        d.i = items[e];
+        d.f = fwd[e];
+        d.r = ratings[e];
     };
-
-    auto dot = [&](const f2 (&p)[H], const f2 (&q)[H]) {  // p.q over all columns: the prediction minus gb
-        f2 acc = p[0] * q[0];
-#pragma unroll
-        for (int h = 1; h < H; ++h) acc = __builtin_elementwise_fma(p[h], q[h], acc);
-        return acc.x + acc.y;
+    // batch bounds: lane 0 the start, lane 1 the end
+    auto fetch_bounds = [&](int64_t b) { return bstart[b + (lane & 1)]; };
+    auto s0_of = [](int64_t v) {
+        return static_cast<int64_t>((static_cast<uint64_t>(__builtin_amdgcn_readlane(static_cast<uint32_t>(static_cast<uint64_t>(v) >> 32), 0)) << 32) |
+                                    __builtin_amdgcn_readlane(static_cast<uint32_t>(v), 0));
     };
-    // svd.go:114-128: p <- p - (q diff + p reg) lr, then q with the NEW p (Q1); c = lr diff
-    auto update = [&](f2 (&p)[H], f2 (&q)[H], float c) {
-        const f2 cc = {c, c};
-#pragma unroll
-        for (int h = 0; h < H; ++h) {
-            p[h] = __builtin_elementwise_fma(-q[h], cc * cmp[h], p[h] * amp[h]);
-            q[h] = __builtin_elementwise_fma(-p[h], cc * cmq[h], q[h] * amq[h]);
-        }
+    auto n_of = [](int64_t v) {
+        return static_cast<int32_t>(__builtin_amdgcn_readlane(static_cast<uint32_t>(v), 1) - __builtin_amdgcn_readlane(static_cast<uint32_t>(v), 0));
     };
-    // ids of block B, lane j < D holding rating j of the block (-1: none, also for B < 0 or past the
-    // last epoch); rating index base (B mod n_blocks) D.  Scalar loads (lgkmcnt: the ids never stall the
-    // row ring's vmcnt), then spread over the lanes; the arrays are padded to whole blocks.
-    auto ids = [&](int64_t B, int32_t& u, int32_t& i, float& r) {
-        const int64_t Bc = B < 0 ? 0 : B;
-        const int64_t base = (Bc % n_blocks) * D;
-        const int32_t ok_n = (B >= 0 && B < total) ? static_cast<int32_t>(min(static_cast<int64_t>(D), nnz - base)) : 0;
-        u = -1;
-        i = -1;
-        r = 0.f;
+    auto next_b = [&](int64_t b) { return b + 1 == n_batches ? int64_t{0} : b + 1; };
+    auto rl = [](int32_t v, int x) { return static_cast<int32_t>(__builtin_amdgcn_readlane(v, x)); };
+    // rows of a batch from memory; a slot past n, or a row the previous batch rewrote (forwarded through
+    // LDS instead), loads from row -1: past the buffer, 0
+    auto load_rows = [&](const Ids& d, int32_t n, bool first, f2 (&p)[R][H], f2 (&q)[R][H]) {
 #pragma unroll
-        for (int j = 0; j < D; ++j) {
-            const int32_t uj = users[base + j], ij = items[base + j];
-            const float rj = ratings[base + j];
-            u = (lane == j && j < ok_n) ? uj : u;
-            i = (lane == j && j < ok_n) ? ij : i;
-            r = (lane == j && j < ok_n) ? rj : r;
-        }
-    };
-    int32_t cu, ci, nu, ni;  // this block's and the next block's ids (lane j: slot j)
-    float cr, nr;
-    int32_t ou = -1, oi = -1;  // lane s < D: ids of the rating slot s last processed
-    f2 lp[D][H], lq[D][H];     // the ring: rows of the next D ratings
+        for (int x = 0; x < R; ++x) {
+            if (w + NW * x >= n) continue;  // (uniform: slots past the batch are not touched at all)
+            const int32_t f = rl(d.f, x);
+            const int32_t ur = first || (f & 0xff) == 0 ? rl(d.u, x) : -1;
+            const int32_t ir = first || (f & 0xff00) == 0 ? rl(d.i, x) : -1;
 #pragma unroll
-    for (int j = 0; j < D; ++j)
-#pragma unroll
-        for (int h = 0; h < H; ++h) lp[j][h] = lq[j][h] = f2{0.f, 0.f};
-    ids(-1, cu, ci, cr);
-    ids(0, nu, ni, nr);
-    // The loop starts at an empty block -1 (nothing updated, its stores dropped) whose slots issue block
-    // 0's loads in the loop's own order.
-    for (int64_t B = -1; B < total; ++B) {
-        int32_t fu, fi;
-        float fr;
-        ids(B + 2, fu, fi, fr);  // two blocks ahead
-#pragma unroll
-        for (int j = 0; j < D; ++j) {
-            const int32_t u = rl(cu, j), i = rl(ci, j);
-            f2 p[H], q[H];
-#pragma unroll
-            for (int h = 0; h < H; ++h)  // real copies: the refill below lands in the ring's own registers
-#pragma unroll
-                for (int e = 0; e < 2; ++e) {
-                    asm volatile("v_mov_b32 %0, %1" : "=v"(p[h][e]) : "v"(lp[j][h][e]));
-                    asm volatile("v_mov_b32 %0, %1" : "=v"(q[h][e]) : "v"(lq[j][h][e]));
-                }
-            // a row one of the last D ratings rewrote after this load was issued: load it again
-            const bool su = __ballot(lane < D && ou == u) != 0, si = __ballot(lane < D && oi == i) != 0;
-            if (u >= 0 && (su || si)) {  // (a load after this lane's own store of the address sees it)
-                if (su) load_row(rp, u, p);
-                if (si) load_row(rq, i, q);
-                __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0), as the compiler's wait tracking knows
+            for (int h = 0; h < H; ++h) {
+                p[x][h] = __builtin_bit_cast(f2, __builtin_amdgcn_raw_buffer_load_b64(rp, off(ur, h), 0, kSgdAux));
+                q[x][h] = __builtin_bit_cast(f2, __builtin_amdgcn_raw_buffer_load_b64(rq, off(ir, h), 0, kSgdAux));
             }
-            const float sp = ordered_wave_sum(dot(p, q));
-            const float rt = __int_as_float(rl(__float_as_int(cr), j));
-            const double diff = gb + (static_cast<double>(sp) - static_cast<double>(rt));  // svd.go:102
-            gb = u >= 0 ? gb - lrd * diff : gb;                                             // svd.go:105-106
-            update(p, q, static_cast<float>(lrd * diff));
-            store_row(rp, u, p);  // (an empty slot's stores go to out-of-range offsets and are dropped)
-            store_row(rq, i, q);
-            ou = lane == j ? u : ou;
-            oi = lane == j ? i : oi;
-            load_row(rp, rl(nu, j), lp[j]);  // rating D ahead into the freed slot
-            load_row(rq, rl(ni, j), lq[j]);
         }
-        cu = nu;
-        ci = ni;
-        cr = nr;
-        nu = fu;
-        ni = fi;
-        nr = fr;
+    };
+    uint64_t pc[6] = {0, 0, 0, 0, 0, 0}, tp = prof ? __builtin_amdgcn_s_memtime() : 0;
+    auto ptick = [&](int ph) {
+        if (prof) {
+            const uint64_t tn = __builtin_amdgcn_s_memtime();
+            pc[ph] += tn - tp;
+            tp = tn;
+        }
+    };
+    // prologue: batch 0's ids and rows, batch 1's ids, batch 2's bounds
+    Ids cur, nxt;
+    int64_t b1 = next_b(0), b2 = next_b(b1);
+    const int64_t v0 = fetch_bounds(0), v1 = fetch_bounds(b1);
+    int64_t vb = fetch_bounds(b2);  // bounds of batch t + 2
+    int32_t n = n_of(v0), n1 = n_of(v1);
+    fetch_ids(s0_of(v0), cur);
+    fetch_ids(s0_of(v1), nxt);
+    f2 p[R][H], q[R][H];
+    load_rows(cur, n, true, p, q);
+    for (int64_t t = 0; t < total; ++t) {
+        // rows batch t - 1 rewrote: its LDS copies (the first batch of the launch has none)
+        if (t > 0) {
+#pragma unroll
+            for (int x = 0; x < R; ++x) {
+                if (w + NW * x >= n) continue;
+                const int32_t f = rl(cur.f, x);
+                const int32_t fu = (f & 0xff) - 1, fi = ((f >> 8) & 0xff) - 1;
+                if (fu >= 0)
+#pragma unroll
+                    for (int h = 0; h < H; ++h) p[x][h] = fp[fu][h][lane];
+                if (fi >= 0)
+#pragma unroll
+                    for (int h = 0; h < H; ++h) q[x][h] = fq[fi][h][lane];
+            }
+        }
+        double dx[R];
+#pragma unroll
+        for (int x = 0; x < R; ++x) {
+            dx[x] = 0.0;
+            if (w + NW * x >= n) continue;
+            f2 acc = p[x][0] * q[x][0];
+#pragma unroll
+            for (int h = 1; h < H; ++h) acc = __builtin_elementwise_fma(p[x][h], q[x][h], acc);
+            const float sp = wave_sum(acc.x + acc.y);
+            const float rx = __builtin_bit_cast(float, rl(__builtin_bit_cast(int32_t, cur.r), x));
+            dx[x] = static_cast<double>(sp) - static_cast<double>(rx);  // svd.go:102 (minus gb)
+            if (lane == 0) sd[w + NW * x] = dx[x];
+        }
+        ptick(0);
+        __builtin_amdgcn_s_waitcnt(0);  // this wave's stores of batch t - 1 are done (see above)
+        __syncthreads();
+        ptick(1);
+        double T = lane < n ? -lrd * sd[lane] : 0.0;
+        // batch t + 1's rows (not rewritten by batch t), batch t + 2's ids, batch t + 3's bounds
+        f2 pn[R][H], qn[R][H];
+        load_rows(nxt, n1, false, pn, qn);
+        Ids nn;
+        fetch_ids(s0_of(vb), nn);
+        const int32_t n2 = n_of(vb);
+        b1 = b2;
+        b2 = next_b(b2);
+        const int64_t vbn = fetch_bounds(b2);
+        // GlobalBias: T_j = sum_{i <= j} a^(j-i) (-lr d_i) by a Hillis-Steele scan (DPP row shifts inside
+        // the 16-lane rows, then row_bcast:15 / row_bcast:31), G_j = a^(j+1) gb + T_j = gb after rating j
+        T = __builtin_fma(al, dpp_f64<0x111, 0xF>(T), T);    // row_shr:1
+        T = __builtin_fma(a2, dpp_f64<0x112, 0xF>(T), T);    // row_shr:2
+        T = __builtin_fma(a4, dpp_f64<0x114, 0xF>(T), T);    // row_shr:4
+        T = __builtin_fma(a8, dpp_f64<0x118, 0xF>(T), T);    // row_shr:8
+        T = __builtin_fma(pw16, dpp_f64<0x142, 0xA>(T), T);  // row_bcast:15 into rows 1 and 3
+        T = __builtin_fma(pw32, dpp_f64<0x143, 0xC>(T), T);  // row_bcast:31 into rows 2 and 3
+        const double G = __builtin_fma(pw1, gb, T);
+        ptick(2);
+#pragma unroll
+        for (int x = 0; x < R; ++x) {
+            const int j = w + NW * x;
+            if (j >= n) continue;
+            const double g = j == 0 ? gb : readlane_f64(G, j > 0 ? j - 1 : 0);
+            const float c = static_cast<float>(lrd * (g + dx[x]));  // lr diff
+            const f2 cc = {c, c};
+            const int32_t ur = rl(cur.u, x), ir = rl(cur.i, x);
+#pragma unroll
+            for (int h = 0; h < H; ++h) {  // svd.go:114-128: p first, then q with the NEW p (Q1)
+                p[x][h] = __builtin_elementwise_fma(-q[x][h], cc * cmp[h], p[x][h] * amp[h]);
+                q[x][h] = __builtin_elementwise_fma(-p[x][h], cc * cmq[h], q[x][h] * amq[h]);
+                fp[j][h][lane] = p[x][h];
+                fq[j][h][lane] = q[x][h];
+                __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u2, p[x][h]), rp, off(ur, h), 0, 0);
+                __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u2, q[x][h]), rq, off(ir, h), 0, 0);
+            }
+        }
+        gb = readlane_f64(G, n - 1);
+        ptick(3);
+        __syncthreads();  // the LDS copies are complete (the memory stores drain before the next barrier)
+        ptick(4);
+#pragma unroll
+        for (int x = 0; x < R; ++x)
+#pragma unroll
+            for (int h = 0; h < H; ++h) {
+                p[x][h] = pn[x][h];
+                q[x][h] = qn[x][h];
+            }
+        cur = nxt;
+        nxt = nn;
+        n = n1;
+        n1 = n2;
+        vb = vbn;
     }
-    if (lane == 0) gb_io[0] = gb;
+    __builtin_amdgcn_s_waitcnt(0);
+    if (threadIdx.x == 0) gb_io[0] = gb;
+    if (prof && threadIdx.x == 0)
+        for (int ph = 0; ph < 5; ++ph) prof[ph] = pc[ph];
 }
 
 // ORDERED epochs on the folded layout (rows of ld floats: P [p, b_u, 1], Q [q, 1, b_i]); users / items /
 // ratings in train-set order, allocated for ordered_padded(nnz) entries.
-int64_t ordered_padded(int64_t nnz) { return (nnz + 7) / 8 * 8 + 16; }
+int64_t ordered_padded(int64_t nnz) { return (nnz + 7) / 8 * 8 + 64; }
 
-void ordered_epochs(const int32_t* users, const int32_t* items, const float* ratings, int64_t nnz, float* P,
-                    int64_t p_floats, float* Q, int64_t q_floats, int32_t ld, int32_t kf, double* gb,
-                    int32_t epochs, float lr, float reg, hipStream_t s) {
+// Batches of the batched ORDERED kernel: a batch ends before the first rating whose user or item already
+// occurs in it, or after wmax ratings.  start: n_batches + 1 offsets (the last one nnz).  fwd, per rating:
+// 1 + the slot (position) in the previous batch that wrote its user's row (bits 0-7; 0: none) and its
+// item's row (bits 8-15); batch 0's previous batch is the last one (the epochs repeat the sequence).
+OrderedSchedule ordered_batches(const int32_t* users, const int32_t* items, int64_t nnz, int32_t n_users,
+                                int32_t n_items, int32_t wmax) {
+    OrderedSchedule o;
+    o.start.reserve(static_cast<size_t>(nnz / 16 + 2));
+    o.fwd.assign(static_cast<size_t>(nnz), 0);
+    std::vector<int64_t> bu(static_cast<size_t>(std::max(1, n_users)), -2), bi(static_cast<size_t>(std::max(1, n_items)), -2);
+    std::vector<int32_t> pu(bu.size(), 0), pi(bi.size(), 0);
+    int64_t b = -1;
+    int32_t n = wmax;
+    for (int64_t t = 0; t < nnz; ++t) {
+        const int32_t u = users[t], i = items[t];
+        if (n == wmax || bu[u] == b || bi[i] == b) {
+            o.start.push_back(t);
+            ++b;
+            n = 0;
+        }
+        o.fwd[t] = (bu[u] == b - 1 ? pu[u] + 1 : 0) | (bi[i] == b - 1 ? pi[i] + 1 : 0) << 8;
+        bu[u] = bi[i] = b;
+        pu[u] = pi[i] = n++;
+    }
+    o.start.push_back(nnz);
+    const int64_t last = b;
+    for (int64_t t = 0; t < (o.start.size() > 1 ? o.start[1] : 0); ++t) {
+        const int32_t u = users[t], i = items[t];
+        o.fwd[t] = (bu[u] == last ? pu[u] + 1 : 0) | (bi[i] == last ? pi[i] + 1 : 0) << 8;
+    }
+    return o;
+}
+
+int32_t ordered_wmax(int32_t ld) { return ld <= 256 ? 64 : 32; }
+
+void ordered_epochs(const int32_t* users, const int32_t* items, const float* ratings, const int32_t* fwd,
+                    int64_t nnz, const int64_t* bstart, int64_t n_batches, float* P, int64_t p_floats, float* Q,
+                    int64_t q_floats, int32_t ld, int32_t kf, double* gb, int32_t epochs, float lr, float reg,
+                    hipStream_t s) {
     if (nnz == 0 || epochs <= 0) return;
     if (p_floats * 4 >= (int64_t{1} << 31) || q_floats * 4 >= (int64_t{1} << 31))
         throw std::invalid_argument("ORDERED mode: factor matrices of 2 GiB or more");
+    if (ld > 512) throw std::invalid_argument("ORDERED mode: rows of more than 512 floats");
     const int32_t pb = static_cast<int32_t>(p_floats * 4), qb = static_cast<int32_t>(q_floats * 4);
-    // ring depth: every slot keeps 4 H memory operations in flight, the vmcnt counter holds 63
-    auto go = [&](auto h_c, auto d_c) {
-        constexpr int H = decltype(h_c)::value, D = decltype(d_c)::value;
-        hipLaunchKernelGGL((svd_ordered_wave_kernel<H, D>), dim3(1), dim3(64), 0, s, users, items, ratings, nnz,
-                           (nnz + D - 1) / D, P, pb, Q, qb, ld, kf, gb, epochs, lr, reg);
+    const int nw = [] { const char* e = std::getenv("RSGPU_ORDERED_NW"); return e ? std::atoi(e) : 16; }();
+    // diagnostics: RSGPU_ORDERED_PROF=1 prints wave 0's cycles per phase of a batch
+    const bool diag = [] { const char* e = std::getenv("RSGPU_ORDERED_PROF"); return e && std::atoi(e) != 0; }();
+    DevBuf<uint64_t> dprof(diag ? 8 : 0);
+    uint64_t* prof = diag ? dprof.p : nullptr;
+    auto go = [&](auto h_c, auto nw_c) {
+        constexpr int H = decltype(h_c)::value, NW = decltype(nw_c)::value;
+        constexpr int W = H <= 2 ? 64 : 32;
+        hipLaunchKernelGGL((svd_ordered_batch_kernel<H, NW, W / NW>), dim3(1), dim3(NW * 64), 0, s, users, items,
+                           ratings, fwd, bstart, n_batches, P, pb, Q, qb, ld, kf, gb, epochs, lr, reg, prof);
     };
     using std::integral_constant;
-    if (ld <= 128) go(integral_constant<int, 1>{}, integral_constant<int, 14>{});
-    else if (ld <= 256) go(integral_constant<int, 2>{}, integral_constant<int, 7>{});
-    else go(integral_constant<int, 4>{}, integral_constant<int, 3>{});
+    auto by_h = [&](auto nw_c) {
+        if (ld <= 128) go(integral_constant<int, 1>{}, nw_c);
+        else if (ld <= 256) go(integral_constant<int, 2>{}, nw_c);
+        else go(integral_constant<int, 4>{}, nw_c);
+    };
+    if (nw == 8) by_h(integral_constant<int, 8>{});
+    else by_h(integral_constant<int, 16>{});
     RS_HIP(hipGetLastError());
+    if (diag) {
+        uint64_t h[8] = {0};
+        RS_HIP(hipMemcpyAsync(h, prof, 5 * sizeof(uint64_t), hipMemcpyDeviceToHost, s));
+        RS_HIP(hipStreamSynchronize(s));
+        const double nb = static_cast<double>(n_batches) * epochs;
+        std::fprintf(stderr, "ordered-prof NW=%d batches=%.0f cycles/batch: forward+dot %.0f drain+barrier1 %.0f "
+                     "prefetch+scan %.0f update+store %.0f barrier2 %.0f\n", nw, nb, h[0] / nb, h[1] / nb, h[2] / nb,
+                     h[3] / nb, h[4] / nb);
+    }
 }
 
 }  // namespace rs

@@ -171,13 +171,23 @@ void gb_sum(const double* partial, int64_t n, double* out, hipStream_t s);  // f
 // split users t_split_rows[r0, r1) of the tile schedule: P += dPs, dPs = 0 (the pieces' merge)
 void merge_tile_split_rows(rs_svd_plan* pl, int32_t r0, int32_t r1, hipStream_t s);
 
-// sgd_ordered.hip: RS_SGD_ORDERED epochs, one wave, rows of ld floats in the folded layout
+// sgd_ordered.hip: RS_SGD_ORDERED epochs, one workgroup over conflict-free batches, rows of ld floats in the folded layout
 // P [p_0 .. p_{k-1}, b_u, 1, 0 ..], Q [q_0 .. q_{k-1}, 1, b_i, 0 ..] (ld % 4 == 0, k + 2 <= ld <= 512);
 // the id / rating arrays allocated for ordered_padded(nnz) entries
 int64_t ordered_padded(int64_t nnz);
-void ordered_epochs(const int32_t* users, const int32_t* items, const float* ratings, int64_t nnz, float* P,
-                    int64_t p_floats, float* Q, int64_t q_floats, int32_t ld, int32_t kf, double* gb,
-                    int32_t epochs, float lr, float reg, hipStream_t s);
+// the batched ORDERED kernel's schedule: batch starts (n_batches + 1 offsets; no user or item twice in a
+// batch, at most wmax ratings) and per rating the slots of the previous batch that wrote its rows
+struct OrderedSchedule {
+    std::vector<int64_t> start;
+    std::vector<int32_t> fwd;
+};
+OrderedSchedule ordered_batches(const int32_t* users, const int32_t* items, int64_t nnz, int32_t n_users,
+                                int32_t n_items, int32_t wmax);
+int32_t ordered_wmax(int32_t ld);  // the kernel's batch size limit for rows of ld floats
+void ordered_epochs(const int32_t* users, const int32_t* items, const float* ratings, const int32_t* fwd,
+                    int64_t nnz, const int64_t* bstart, int64_t n_batches, float* P, int64_t p_floats, float* Q,
+                    int64_t q_floats, int32_t ld, int32_t kf, double* gb, int32_t epochs, float lr, float reg,
+                    hipStream_t s);
 
 // sgd_tile.hip
 void tile_build(rs_svd_plan* pl);  // (re)builds the tile schedule from the host CSR

@@ -518,3 +518,18 @@ def test_hot_replicas_rmse_parity_ml100k(ctx, ml100k):
         gpu_r.append(plan.evaluate(f.tu, f.ti, f.te_r)[0])
         plan.close()
     assert abs(np.mean(gpu_r) - np.mean(ref_r)) <= 0.003, (np.mean(gpu_r), np.mean(ref_r))
+
+
+@pytest.mark.parametrize("k", [8, 100, 300])
+def test_ordered_full_batches(ctx, k):
+    """ORDERED on ratings whose conflict-free batches reach the kernel's 64-rating maximum (4000 users x
+    3000 items, uniform): every wave carries several ratings of a batch and the GlobalBias chain runs
+    over 64 entries; equal to the sequential restatement (svd.go:93-129)."""
+    rng = np.random.default_rng(100 + k)
+    n, nu, ni = 30000, 4000, 3000
+    u, i = rng.integers(0, nu, n), rng.integers(0, ni, n)
+    r = rng.integers(1, 6, n).astype(float)
+    P0, Q0 = rng.normal(0, 0.1, (nu, k)), rng.normal(0, 0.1, (ni, k))
+    ref = O.svd_fit(u, i, r, P0, Q0, epochs=2)
+    got = ctx.svd_fit(rsgpu.Ratings(u, i, r, nu, ni), P0, Q0, n_epochs=2, mode=rsgpu.SGD_ORDERED)
+    assert _maxdiff(ref[:4], got[:4]) <= TOL and abs(ref[4] - got[4]) <= TOL
