@@ -54,7 +54,7 @@ extern "C" {
 /* SGD visit schedule (SURVEY §8a parity contract P1/P2) */
 #define RS_SGD_FAST 0    /* the FAST schedule of rs_sgd_params.write_back (default RS_SGD_WB_TILE: user
                             tiles in LDS, one memory-side atomic per (item, tile) run), work-local global bias */
-#define RS_SGD_ORDERED 1 /* one wave, exact train-set order and update order of svd.go:93-129 */
+#define RS_SGD_ORDERED 1 /* exact train-set order and update order of svd.go:93-129 (conflict-free batches, one workgroup) */
 
 /* FAST-mode schedule / write-back of the item rows (rs_sgd_params.write_back, rs_svd_plan_set_mode) */
 #define RS_SGD_WB_TILE 0          /* default: user tiles in LDS (integer LDS atomics), one memory-side
