@@ -453,12 +453,15 @@ void build_tile_host(const rs_svd_plan* pl, int32_t u_begin, int32_t u_end, int3
             std::vector<int64_t> runs(nb, 0), cost(nb, 0);
             auto row = [&](size_t b) { return cnt.data() + b * static_cast<size_t>(pl->n_items); };
             const std::vector<int32_t>& cols0 = pl->h_cols;
-            for (size_t b = 0; b < nb; ++b) {
-                int32_t* c = row(b);
-                for (size_t x : bins[b].ents)
-                    for (int64_t q = ents[x].b; q < ents[x].e; ++q) runs[b] += c[cols0[q]]++ == 0;
-                cost[b] = bins[b].recs + kRunCost * runs[b];
-            }
+            const int32_t nth = static_cast<int32_t>(std::min<size_t>(static_cast<size_t>(clamp_threads(0)), nb / 8 + 1));
+            parallel_run(nth, [&](int32_t th) {  // per-tile item counts (pooled threads)
+                for (size_t b = static_cast<size_t>(th); b < nb; b += static_cast<size_t>(nth)) {
+                    int32_t* c = row(b);
+                    for (size_t x : bins[b].ents)
+                        for (int64_t q = ents[x].b; q < ents[x].e; ++q) runs[b] += c[cols0[q]]++ == 0;
+                    cost[b] = bins[b].recs + kRunCost * runs[b];
+                }
+            });
             for (size_t it = 0; it < 4 * nb; ++it) {
                 const size_t hi = static_cast<size_t>(std::max_element(cost.begin(), cost.end()) - cost.begin());
                 const size_t lo = static_cast<size_t>(std::min_element(cost.begin(), cost.end()) - cost.begin());
@@ -618,13 +621,10 @@ void build_tile_host(const rs_svd_plan* pl, int32_t u_begin, int32_t u_end, int3
     auto parallel_tiles = [&](auto&& fn, bool with_slot) {
         static const int want_th = std::getenv("RSGPU_TILE_THREADS") ? std::atoi(std::getenv("RSGPU_TILE_THREADS")) : 16;
         const int nth = static_cast<int>(std::min<size_t>(static_cast<size_t>(std::max(1, want_th)), std::max<size_t>(1, nt / 8)));
-        std::vector<std::thread> th2;
-        for (int c = 0; c < nth; ++c)
-            th2.emplace_back([&, c] {
-                std::vector<int32_t> slot(with_slot ? static_cast<size_t>(std::max(1, pl->n_items)) : 0, -1);
-                for (size_t t = c; t < nt; t += nth) fn(t, slot);
-            });
-        for (std::thread& x : th2) x.join();
+        parallel_run(nth, [&](int32_t c) {  // (pooled threads, ingest.cpp)
+            std::vector<int32_t> slot(with_slot ? static_cast<size_t>(std::max(1, pl->n_items)) : 0, -1);
+            for (size_t t = static_cast<size_t>(c); t < nt; t += static_cast<size_t>(nth)) fn(t, slot);
+        });
     };
     parallel_tiles(group_one, true);
     tmark("group");
@@ -688,8 +688,13 @@ void build_tile_host(const rs_svd_plan* pl, int32_t u_begin, int32_t u_end, int3
 // hottest item 3.4M of 126M ratings) the staleness model alone gives 2 and the hottest row's 1.7M
 // atomic rows bound the epoch at 143 ms; caps 4 / 6 / 8 / 10 / 12 give 92 / 80 / 76 / 74 / 75 ms at the
 // same held-out RMSE after five epochs (0.8815-0.8818; profiles/r03_experiments/cfg4_ring.log), and 7
-// is what this rule picks.  On ML-1M (dmax 3428) it is 1 and changes nothing.
+// is what this rule picks.  On ML-1M (dmax 3428) it is 1 and changes nothing.  The floor applies from
+// 2^25 ratings on: below that it buys little time and its staleness can diverge -- the 1.13M-rating,
+// k = 64 set of tests/test_csr_plan_gpu.py (hottest item 16271 ratings) trains at the model's cap 3
+// (held-out 1.005 -> 0.729 in 10 epochs) and goes NaN at the floor's 4 within 1-3 epochs
+// (scripts/experiments/exp_synth_cap.py, profiles/r03_experiments/synth_cap.log).
 constexpr double kStaleTarget = 100.0;
+constexpr int64_t kHotFloorMinNnz = int64_t{1} << 25;
 int32_t auto_run_cap(const rs_svd_plan* pl, int32_t grid, int32_t waves) {
     if (waves <= 1 || pl->nnz == 0) return 0;
     std::vector<int64_t> deg(std::max(1, pl->n_items), 0);
@@ -697,7 +702,7 @@ int32_t auto_run_cap(const rs_svd_plan* pl, int32_t grid, int32_t waves) {
     const int64_t dmax = *std::max_element(deg.begin(), deg.end());
     const double c = 2.0 * kStaleTarget * static_cast<double>(pl->nnz) /
                      (static_cast<double>(dmax) * grid * waves);
-    const int64_t c_hot = (dmax * 256 + pl->nnz - 1) / pl->nnz;
+    const int64_t c_hot = pl->nnz >= kHotFloorMinNnz ? (dmax * 256 + pl->nnz - 1) / pl->nnz : 0;
     return c >= 1e6 ? 0 : static_cast<int32_t>(std::max<int64_t>({2, static_cast<int64_t>(c), c_hot}));
 }
 
