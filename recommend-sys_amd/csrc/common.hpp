@@ -98,8 +98,17 @@ struct DevBuf {
 
 inline int32_t round_up4(int32_t k) { return (k + 3) & ~3; }
 
+// ingest.cpp: host threads (n_threads <= 0: min(hardware threads, 16)); parallel_run(n, fn) runs fn(t),
+// t < n, on n threads (the caller's included) and rethrows the first exception; csr_build is the stable
+// COO -> CSR of build_csr on T threads
+int32_t clamp_threads(int32_t n_threads);
+void parallel_run(int32_t n, const std::function<void(int32_t)>& fn);
+void csr_build(int64_t nnz, int32_t n_rows, const int32_t* rows, const int32_t* cols, const double* vals,
+               int32_t n_threads, int64_t* rowptr, int32_t* cols_out, float* vals_out);
+
 // Host threads for an index range: f(begin, end) on up to `max_threads` contiguous slices (the
-// caller's thread takes the first).  For host-side preparation passes that do not touch the GPU.
+// caller's thread takes the first; pooled threads, ingest.cpp).  For host-side preparation passes
+// that do not touch the GPU.
 template <typename F>
 void parallel_ranges(int64_t n, int max_threads, F&& f) {
     const unsigned hw = std::max(1u, std::thread::hardware_concurrency());
@@ -109,11 +118,12 @@ void parallel_ranges(int64_t n, int max_threads, F&& f) {
         f(int64_t{0}, n);
         return;
     }
-    std::vector<std::thread> th;
-    for (int64_t t = 1; t < nt; ++t) th.emplace_back([&, t] { f(n * t / nt, n * (t + 1) / nt); });
-    f(int64_t{0}, n / nt);
-    for (std::thread& x : th) x.join();
+    parallel_run(static_cast<int32_t>(nt), [&](int32_t t) { f(n * t / nt, n * (t + 1) / nt); });
 }
+
+// Pinned host staging for large uploads: a per-thread page-locked buffer (grown on demand, kept for the
+// process) that the caller fills and DMAs from; the caller synchronises the stream before reuse.
+void* pinned_staging(size_t bytes);
 
 // f64 host rows (stride k) <-> f32 padded rows (stride ld) with zero padding.
 void pack_rows_f32(const double* src, int64_t rows, int32_t k, int32_t ld, std::vector<float>& dst);
@@ -127,14 +137,6 @@ struct UserCSR {
 };
 void build_csr(int64_t nnz, int32_t n_rows, const int32_t* rows, const int32_t* cols,
                const double* vals, UserCSR& out);
-
-// ingest.cpp: host threads (n_threads <= 0: min(hardware threads, 16)); parallel_run(n, fn) runs fn(t),
-// t < n, on n threads (the caller's included) and rethrows the first exception; csr_build is the stable
-// COO -> CSR of build_csr on T threads
-int32_t clamp_threads(int32_t n_threads);
-void parallel_run(int32_t n, const std::function<void(int32_t)>& fn);
-void csr_build(int64_t nnz, int32_t n_rows, const int32_t* rows, const int32_t* cols, const double* vals,
-               int32_t n_threads, int64_t* rowptr, int32_t* cols_out, float* vals_out);
 
 // FAST-mode GlobalBias warm start: the least-squares bias given the current b_u, b_i (factors
 // ignored), i.e. mean(r - b_u - b_i).  The sequential reference reaches this value within its first

@@ -40,6 +40,23 @@ void build_csr(int64_t nnz, int32_t n_rows, const int32_t* rows, const int32_t* 
 }
 
 // mean(r - b_u - b_i) over fixed 2^16-rating chunks summed in order (independent of the thread count)
+void* pinned_staging(size_t bytes) {
+    struct Buf {
+        void* p = nullptr;
+        size_t n = 0;
+    };
+    thread_local Buf b;  // (never freed: the process may outlive the HIP runtime's teardown order)
+    if (b.n < bytes) {
+        if (b.p) (void)hipHostFree(b.p);
+        b.p = nullptr;
+        b.n = 0;
+        const size_t n = std::max(bytes, size_t{1} << 20) * 5 / 4;
+        RS_HIP(hipHostMalloc(&b.p, n, hipHostMallocPortable));
+        b.n = n;
+    }
+    return b.p;
+}
+
 double gb_warm_start(const rs_ratings* r, const double* bu, const double* bi) {
     if (r->nnz <= 0) return 0.0;
     constexpr int64_t kChunk = int64_t{1} << 16;

@@ -36,6 +36,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <atomic>
 #include <cstring>
 #include <memory>
 #include <chrono>
@@ -1993,10 +1994,16 @@ struct SvdFitCache {
     bool matches(const rs_ratings* r, int32_t k2, int32_t wb) const {
         if (!plan || nnz != r->nnz || n_users != r->n_users || n_items != r->n_items || k != k2 || write_back != wb)
             return false;
-        const size_t n = static_cast<size_t>(nnz);
-        return n == 0 || (std::memcmp(users.data(), r->users, n * 4) == 0 &&
-                          std::memcmp(items.data(), r->items, n * 4) == 0 &&
-                          std::memcmp(ratings.data(), r->ratings, n * 8) == 0);
+        // exact comparison of the COO (16 B per rating), on pooled threads
+        std::atomic<bool> same{true};
+        parallel_ranges(nnz, 16, [&](int64_t b, int64_t e) {
+            const size_t o = static_cast<size_t>(b), n = static_cast<size_t>(e - b);
+            if (std::memcmp(users.data() + o, r->users + o, n * 4) != 0 ||
+                std::memcmp(items.data() + o, r->items + o, n * 4) != 0 ||
+                std::memcmp(ratings.data() + o, r->ratings + o, n * 8) != 0)
+                same = false;
+        });
+        return same;
     }
 };
 
@@ -2052,9 +2059,15 @@ extern "C" int rs_svd_fit(rs_ctx* ctx, const rs_ratings* r, const rs_sgd_params*
                     cache->n_items = r->n_items;
                     cache->k = p->n_factors;
                     cache->write_back = wb;
-                    cache->users.assign(r->users, r->users + n);
-                    cache->items.assign(r->items, r->items + n);
-                    cache->ratings.assign(r->ratings, r->ratings + n);
+                    cache->users.resize(n);
+                    cache->items.resize(n);
+                    cache->ratings.resize(n);
+                    rs::parallel_ranges(r->nnz, 16, [&](int64_t b, int64_t e) {  // the COO copy, pooled threads
+                        const size_t o = static_cast<size_t>(b), m = static_cast<size_t>(e - b);
+                        std::memcpy(cache->users.data() + o, r->users + o, m * 4);
+                        std::memcpy(cache->items.data() + o, r->items + o, m * 4);
+                        std::memcpy(cache->ratings.data() + o, r->ratings + o, m * 8);
+                    });
                     ctx->svd_fit_cache = cache;
                 }
             }
