@@ -128,7 +128,8 @@ def ordered_throughput(ctx, u, i, r, n_users, n_items):
     ms = ctx.last_kernel_ms()
     return {"value": len(r) / (ms / 1e3), "unit": "updates/s", "epoch_ms_kernel": ms,
             "note": "one workgroup walks the ratings in the reference order in conflict-free batches (no user "
-                    "or item twice, <= 64 ratings; rows prefetched a batch ahead, the previous batch's rows "
+                    "or item twice, <= 64 ratings, a 16-lane group per rating; rows prefetched a batch ahead, the "
+                    "previous batch's rows "
                     "forwarded through LDS, the GlobalBias chain as a lane-parallel scan; factors within 1e-5 "
                     "of the oracle; csrc/sgd_ordered.hip); kernel-only time of one epoch"}
 

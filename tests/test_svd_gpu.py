@@ -533,3 +533,18 @@ def test_ordered_full_batches(ctx, k):
     ref = O.svd_fit(u, i, r, P0, Q0, epochs=2)
     got = ctx.svd_fit(rsgpu.Ratings(u, i, r, nu, ni), P0, Q0, n_epochs=2, mode=rsgpu.SGD_ORDERED)
     assert _maxdiff(ref[:4], got[:4]) <= TOL and abs(ref[4] - got[4]) <= TOL
+
+
+@pytest.mark.parametrize("gnw", ["4", "8", "0"])
+def test_ordered_group_kernel_widths(ctx, gnw, monkeypatch):
+    """The ORDERED group kernel (rows <= 128 floats: a 16-lane group per rating) at 4 and 8 waves, and the
+    wave-per-rating kernel (RSGPU_ORDERED_GNW=0) on the same rows: each equal to the restatement."""
+    monkeypatch.setenv("RSGPU_ORDERED_GNW", gnw)
+    rng = np.random.default_rng(7)
+    n, nu, ni, k = 20000, 3000, 2000, 100
+    u, i = rng.integers(0, nu, n), rng.integers(0, ni, n)
+    r = rng.integers(1, 6, n).astype(float)
+    P0, Q0 = rng.normal(0, 0.1, (nu, k)), rng.normal(0, 0.1, (ni, k))
+    ref = O.svd_fit(u, i, r, P0, Q0, epochs=2)
+    got = ctx.svd_fit(rsgpu.Ratings(u, i, r, nu, ni), P0, Q0, n_epochs=2, mode=rsgpu.SGD_ORDERED)
+    assert _maxdiff(ref[:4], got[:4]) <= TOL and abs(ref[4] - got[4]) <= TOL
