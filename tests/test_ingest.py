@@ -94,3 +94,42 @@ def test_synth_deterministic_and_shards_are_filters():
     assert np.array_equal(np.diff(s.rowptr), np.bincount(users[keep], minlength=3000))
     for x in (a, b, s):
         x.close()
+
+
+def test_csr_build_concurrent_callers_share_the_worker_pool():
+    """The host passes run on a pool of persistent threads (ingest.cpp) that serves one job at a time; a
+    caller that finds it busy (another host thread -- CrossValidate's goroutines, the shards of a
+    multi-GPU fit) spawns its own threads.  Six Python threads (ctypes releases the GIL) building CSRs
+    at once, several times over, each equal to the single-threaded build; an out-of-range id raises in
+    its own caller only."""
+    import threading
+
+    rng = np.random.default_rng(5)
+    sets = []
+    for s in range(6):
+        n, nr = 200000 + 1000 * s, 3000 + s
+        rows, cols = rng.integers(0, nr, n), rng.integers(0, 5000, n)
+        vals = rng.integers(1, 6, n).astype(float)
+        sets.append((rows, cols, vals, nr, rsgpu.csr_build(rows, cols, vals, nr, n_threads=1)))
+    errors = []
+
+    def work(x):
+        rows, cols, vals, nr, ref = sets[x]
+        try:
+            for _ in range(4):
+                got = rsgpu.csr_build(rows, cols, vals, nr, n_threads=8)
+                for a, b in zip(got, ref):
+                    assert np.array_equal(a, b)
+            bad = rows.copy()
+            bad[len(bad) // 2] = nr  # out of range
+            with pytest.raises(rsgpu.RsError):
+                rsgpu.csr_build(bad, cols, vals, nr, n_threads=8)
+        except BaseException as e:  # noqa: BLE001 -- reported below
+            errors.append(e)
+
+    th = [threading.Thread(target=work, args=(x,)) for x in range(6)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join()
+    assert not errors, errors
