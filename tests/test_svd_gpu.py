@@ -44,7 +44,7 @@ def test_ordered_matches_oracle(ctx, fold0, k, epochs, n):
     assert abs(ref[4] - got[4]) <= TOL
 
 
-@pytest.mark.parametrize("k", [1, 62, 100, 254, 300, 510])
+@pytest.mark.parametrize("k", [1, 62, 100, 126, 127, 254, 300, 510])
 def test_ordered_collisions_and_widths(ctx, k):
     """ORDERED with rows reused within the kernel's prefetch window all the time (3 users x 5 items: a
     rating's user or item was usually rewritten by one of the previous 8, the forwarding path) and row
