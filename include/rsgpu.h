@@ -259,10 +259,17 @@ int rs_svd_plan_set_mode(rs_svd_plan* plan, int32_t write_back, int32_t ring_dep
  * for wide rows; deeper rings read hot rows earlier, i.e. staler).  Rebuilds the schedule. */
 int rs_svd_plan_set_tiles(rs_svd_plan* plan, int32_t workgroups, int32_t waves, int32_t target,
                           int32_t run_cap, int32_t ring);
+/* Work distribution inside a tile: runs_per_claim = 4 (default) or 8 -- the tile's runs form one queue
+ * and each wave claims that many consecutive runs at a time from an LDS counter (a workgroup ends about
+ * one claim after its average wave); 0 -- the runs are dealt to the waves on the host (round-3
+ * schedule).  Rebuilds the schedule. */
+int rs_svd_plan_set_tile_claim(rs_svd_plan* plan, int32_t runs_per_claim);
 /* Visit order of the tile schedule: pos[n] = user-CSR position (rowptr order, data order inside a row)
  * of the n-th rating (nnz entries) as the kernel's streams walk it -- tile by tile, a tile's waves in
  * order, a wave's runs in order --, and work_off (n_works + 1 entries) the boundaries of the (tile,
- * wave) streams, the kernel's GlobalBias work items; n_works = tiles x waves.  Any pointer may be
+ * wave) streams, the kernel's GlobalBias work items; n_works = tiles x waves.  With claimed runs the
+ * whole queue is stream 0 of its tile (the other streams empty): with one wave it is the visit order,
+ * with several the waves' shares are decided at run time.  Any pointer may be
  * NULL (call once with pos = work_off = NULL for n_works).  With one workgroup of one wave an epoch
  * is exactly the sequential SGD of svd.go:93-129 in this order with the work-local GlobalBias fold
  * (the oracle's or_svd_fit_works restates it). */
@@ -364,7 +371,24 @@ int rs_svd_plan_apply_delta(rs_svd_plan* plan, const void* dP, const void* gbsum
  * the one librccl mapped; path_len bytes incl. the terminating NUL; either pointer may be NULL). */
 #define RS_EXCHANGE_ROTATE 0
 #define RS_EXCHANGE_AVERAGE 1
+/* RS_EXCHANGE_ROTATE_Q -- the dual rotation (round 4), exact like ROTATE, for U > I (configs[4]: 10M users,
+ * 1M items): the factor matrix that travels is the smaller one.  Rank g's plan holds the ratings of its
+ * user range (global user and item ids, all items: each rank's users a contiguous range, ascending by
+ * rank).  The items are cut into n_ranks item rank-blocks of near-equal ratings (from every item's ratings
+ * over all ranks), each of `pieces` item blocks, and the plan's tiles are built per stratum (its users x
+ * one item block).  In sub-epoch s rank g trains its users against item rank-block (g + s) mod n_ranks,
+ * then sends those Q rows (b_i in column k) to rank g - 1 and receives item rank-block (g + s + 1) from
+ * rank g + 1, piece by piece; P rows never move during the call.  At configs[4] a sub-epoch moves
+ * 1M / 8 Q rows (160 MB at k = 256) instead of 10M / 8 P rows (1.6 GB).  After the call the item
+ * rank-blocks and every rank's user range are broadcast, so P, Q, the biases and GlobalBias are identical
+ * on every rank.  n_blocks = item blocks in all (rounded up to a multiple of n_ranks; 0 = automatic: 2..16
+ * pieces of ~64 MiB of Q per rank-block).  rs_svd_fit_multi picks it when n_items < n_users. */
+#define RS_EXCHANGE_ROTATE_Q 2
 int rs_svd_plan_set_exchange(rs_svd_plan* plan, int32_t mode);
+/* Test hook (fault injection): the next rs_svd_plan_epochs_sharded / rs_svd_group_epochs call on this
+ * plan throws at the start of its sub-epoch `sub_epoch` (once), so tests can check that the other ranks
+ * are released.  -1 clears it.  Nothing else reads it. */
+int rs_svd_plan_inject_fault(rs_svd_plan* plan, int32_t sub_epoch);
 /* Host only: RS_EXCHANGE_ROTATE's sub-epoch `sub_epoch` of `rank` -- out[0] the rank-block it trains,
  * out[1] the rank its rows are sent to, out[2] the rank-block it receives, out[3] the rank that sends
  * it.  The schedule rs_svd_plan_epochs_sharded runs. */
@@ -377,6 +401,9 @@ int rs_svd_plan_shard_info(rs_svd_plan* plan, int32_t* rank, int32_t* n_ranks, i
 #define RS_COMM_ID_BYTES 128
 int rs_comm_unique_id(void* id /* RS_COMM_ID_BYTES */);
 int rs_svd_plan_join(rs_svd_plan* plan, const void* id, int32_t rank, int32_t n_ranks, int32_t n_blocks);
+/* On an error inside the call the plan aborts its communicator (ncclCommAbort) and stays unusable until
+ * rs_svd_plan_leave; its peers may be blocked in a transfer with it, which RCCL does not cancel across
+ * processes -- a one-process-per-GPU host needs its own watchdog (e.g. the launcher's timeout). */
 int rs_svd_plan_epochs_sharded(rs_svd_plan* plan, int32_t n_epochs, float lr, float reg, void* stream);
 int rs_svd_plan_leave(rs_svd_plan* plan);
 /* User blocks of the tile schedule (default 1): the visit order becomes block by block.  bounds
@@ -396,9 +423,11 @@ int rs_svd_group_epochs(rs_svd_group* group, int32_t n_epochs, float lr, float r
 void rs_svd_group_destroy(rs_svd_group* group);
 /* Item shards of near-equal ratings over contiguous inner item ids: bounds (n_shards + 1 entries). */
 int rs_item_shards(int64_t nnz, const int32_t* items, int32_t n_items, int32_t n_shards, int32_t* bounds);
-/* core/svd.go:63-132 (FAST tile schedule) on n_devices GPUs of this process, items sharded by
- * rs_item_shards, RS_EXCHANGE_ROTATE, as rs_svd_fit otherwise (GlobalBias warm start, host buffers in /
- * out; RS_ERR_NUMERIC after every shard's values are written). */
+/* core/svd.go:63-132 (FAST tile schedule) on n_devices GPUs of this process: with n_items >= n_users the
+ * items are sharded by rs_item_shards and P rank-blocks rotate (RS_EXCHANGE_ROTATE); with fewer items than
+ * users the users are cut into ranges of near-equal ratings and Q item blocks rotate
+ * (RS_EXCHANGE_ROTATE_Q).  As rs_svd_fit otherwise (GlobalBias warm start, host buffers in / out;
+ * RS_ERR_NUMERIC after every shard's values are written). */
 int rs_svd_fit_multi(const int32_t* devices, int32_t n_devices, const rs_ratings* r, const rs_sgd_params* p,
                      int32_t n_blocks, double* P, double* Q, double* bu, double* bi, double* gb);
 /* ---- user-sharded multi-GPU (the dual partition, SURVEY §8e "measured alternative") ---------- *

@@ -37,11 +37,16 @@ namespace {
 // Persistent workers for parallel_run: creating threads costs tens of microseconds each on the GPU boxes'
 // hosts, which made a 16-thread, four-pass CSR build slower than one thread (3.0 ms against 2.0 ms for
 // 1M ratings).  Workers are created on first use, then sleep on a condition variable between jobs.  One
-// job at a time: a caller that finds the pool busy (another host thread, e.g. a shard of a multi-GPU fit,
-// or a nested call) spawns its own threads as before.
+// job at a time: a caller that finds the pool busy (another host thread, e.g. a shard of a multi-GPU fit)
+// spawns its own threads as before.  A nested call -- from inside a pool job, on a worker or on the
+// caller's own t = 0 -- never touches the pool's mutex (try_lock on a mutex the thread already holds is
+// undefined behaviour): the thread-local flag sends it to the spawned-threads path.
+thread_local bool in_pool_job = false;
+
 class WorkerPool {
   public:
     bool try_run(int32_t n, const std::function<void(int32_t)>& fn, std::vector<std::exception_ptr>& err) {
+        if (in_pool_job) return false;
         std::unique_lock<std::mutex> busy(busy_, std::try_to_lock);
         if (!busy.owns_lock()) return false;
         {
@@ -57,11 +62,13 @@ class WorkerPool {
             ++gen_;
         }
         cv_.notify_all();
+        in_pool_job = true;
         try {
             fn(0);
         } catch (...) {
             err[0] = std::current_exception();
         }
+        in_pool_job = false;
         std::unique_lock<std::mutex> l(m_);
         done_.wait(l, [&] { return left_ == 0; });
         job_ = nullptr;
@@ -78,6 +85,7 @@ class WorkerPool {
 
   private:
     void loop(int32_t id) {
+        in_pool_job = true;  // a worker only ever runs pool jobs
         uint64_t seen = 0;
         std::unique_lock<std::mutex> l(m_);
         for (;;) {

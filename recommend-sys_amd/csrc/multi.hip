@@ -1,7 +1,7 @@
 // multi.hip -- item-sharded multi-GPU SGD behind the C-ABI (north_star), the epoch of
 // core/svd.go:92-130 over Q sharded by item range across the ranks.
 //
-// Two exchanges (rs_svd_plan_set_exchange):
+// Three exchanges (rs_svd_plan_set_exchange):
 //
 // ROTATE (default; the exact one).  The users are cut into N rank-blocks (N = ranks), each of
 // `pieces` user blocks of near-equal ratings with their own tiles.  An epoch is N sub-epochs: in
@@ -17,6 +17,13 @@
 // waits only for that transfer.  GlobalBias is the FAST schedules' work-local copy folded once per
 // epoch (the partials of every stratum summed and all-reduced).  After the call the rank-blocks are
 // broadcast, so P is replicated again on every rank.
+//
+// ROTATE_Q (round 4; the dual of ROTATE, for U > I).  The ranks hold user ranges (all items); the items are
+// cut into N item rank-blocks and the plan's tiles per stratum (its users x one item block).  In sub-epoch s
+// rank g trains item rank-block (g + s) mod N and passes those Q rows to rank g - 1: the same schedule with
+// the roles of P and Q swapped, so the rows that travel are the smaller factor matrix (configs[4]: 1M / 8
+// item rows per sub-epoch instead of 10M / 8 user rows).  After the call the item rank-blocks and the ranks'
+// user ranges are broadcast.
 //
 // AVERAGE (round 2's protocol, kept selectable).  Every rank trains all users against its shard in
 // delta mode from the same P; the count-weighted average of the shards' user deltas is all-reduced
@@ -41,6 +48,8 @@
 #include <stdexcept>
 #include <string>
 #include <thread>
+#include <tuple>
+#include <utility>
 #include <vector>
 
 #include "common.hpp"
@@ -60,6 +69,7 @@ struct LocalGroup {  // host-barrier exchange between the shards of one process
     std::vector<float*> dP;
     std::vector<double*> gbs;
     std::vector<float*> P;    // ROTATE: every shard's P (rank-blocks are pulled from the neighbour)
+    std::vector<float*> Q;    // ROTATE_Q: every shard's Q
     std::vector<int> dev;
     void barrier() {
         std::unique_lock<std::mutex> l(m);
@@ -84,7 +94,8 @@ struct LocalGroup {  // host-barrier exchange between the shards of one process
 struct ShardComm {
     int rank = 0, nranks = 1, device = 0;
     int32_t mode = RS_EXCHANGE_ROTATE;
-    int32_t pieces = 1;  // ROTATE: user blocks per rank-block
+    int32_t pieces = 1;  // ROTATE / ROTATE_Q: user / item blocks per rank-block
+    std::vector<int32_t> owner;  // ROTATE_Q: the ranks' user ranges [owner[r], owner[r + 1])
     ncclComm_t nccl = nullptr;
     bool own_nccl = true;
     std::atomic<bool> aborted{false};
@@ -205,9 +216,9 @@ RotStep rotation_step(int32_t g, int32_t n, int32_t st) {
 // ROTATE: user blocks per rank-block.  A piece's rows are sent while the next piece computes, so only
 // the last piece's transfer is exposed per sub-epoch: at least two pieces, about 64 MiB of P rows each
 // (2..16).
-int32_t auto_pieces(const rs_svd_plan* pl, int32_t nranks) {
+int32_t auto_pieces(const rs_svd_plan* pl, int32_t nranks, bool items) {
     if (nranks <= 1) return 1;
-    const double bytes = static_cast<double>(pl->n_users) / nranks * pl->ld * 4.0;
+    const double bytes = static_cast<double>(items ? pl->n_items : pl->n_users) / nranks * pl->ld * 4.0;
     return std::max(2, std::min(16, static_cast<int32_t>(bytes / (64.0 * 1024 * 1024) + 0.5)));
 }
 
@@ -223,23 +234,68 @@ void set_weights(rs_svd_plan* pl, const std::vector<double>& tot) {
     RS_HIP(hipStreamSynchronize(pl->ctx->stream));
 }
 
+// ROTATE_Q: the ranks' user ranges from each rank's first user with ratings and one past its last
+// (first < 0: no ratings); every rank's users must form a contiguous range, ascending by rank
+std::vector<int32_t> owner_ranges(const std::vector<int64_t>& first, const std::vector<int64_t>& end,
+                                  int32_t n_users) {
+    const size_t n = first.size();
+    std::vector<int32_t> owner(n + 1, 0);
+    int64_t prev_end = 0;
+    for (size_t r = 0; r < n; ++r) {
+        if (first[r] >= 0) {
+            if (first[r] < prev_end)
+                throw std::invalid_argument("RS_EXCHANGE_ROTATE_Q: each rank's users must be one contiguous range, "
+                                            "ascending by rank");
+            if (r > 0) owner[r] = static_cast<int32_t>(first[r]);
+            prev_end = end[r];
+        } else if (r > 0) {
+            owner[r] = static_cast<int32_t>(prev_end);
+        }
+    }
+    owner[n] = n_users;
+    return owner;
+}
+
+// first user with ratings in this plan and one past its last (-1, -1: none)
+std::pair<int64_t, int64_t> user_span(const rs_svd_plan* pl) {
+    int64_t f = -1, e = -1;
+    for (int32_t u = 0; u < pl->n_users; ++u)
+        if (pl->h_rowptr[u + 1] > pl->h_rowptr[u]) {
+            if (f < 0) f = u;
+            e = u + 1;
+        }
+    return {f, e};
+}
+
 // buffers, blocks and (RCCL) the comm stream of a shard whose comm / local group is set; tot: every
-// user's ratings over all shards (the user blocks must be the same on every shard)
+// user's ratings over all shards (ROTATE, AVERAGE: the user blocks must be the same on every shard) or
+// every item's (ROTATE_Q: the item blocks)
 void shard_setup(rs_svd_plan* pl, ShardComm& c, int32_t n_blocks, const std::vector<double>& tot) {
     if (pl->write_back != RS_SGD_WB_TILE)
         throw std::invalid_argument("the item-sharded epoch runs the tile schedule (RS_SGD_WB_TILE)");
     c.device = pl->ctx->device;
     c.ldd = round_up4(pl->k + 1);
     c.mode = pl->exchange;
-    if (c.mode == RS_EXCHANGE_ROTATE) {  // n_blocks: user blocks in all, rounded up to whole rank-blocks
-        c.pieces = n_blocks > 0 ? (n_blocks + c.nranks - 1) / c.nranks : auto_pieces(pl, c.nranks);
-        pl->tile_ublocks = c.pieces * c.nranks;
+    const bool rq = c.mode == RS_EXCHANGE_ROTATE_Q;
+    int32_t nbk = 0;  // blocks of the rows `tot` counts
+    if (c.mode != RS_EXCHANGE_AVERAGE) {  // n_blocks: blocks in all, rounded up to whole rank-blocks
+        c.pieces = n_blocks > 0 ? (n_blocks + c.nranks - 1) / c.nranks : auto_pieces(pl, c.nranks, rq);
+        nbk = c.pieces * c.nranks;  // empty blocks (fewer rows than blocks) send and receive nothing
+        pl->tile_ublocks = rq ? 1 : nbk;
     } else {
         pl->tile_ublocks = n_blocks > 0 ? n_blocks : auto_blocks(pl, c.nranks, c.ldd);
+        nbk = std::max(1, std::min(pl->tile_ublocks, std::max(1, pl->n_users)));
     }
-    std::vector<int64_t> cum(static_cast<size_t>(pl->n_users) + 1, 0);
-    for (int32_t u = 0; u < pl->n_users; ++u) cum[u + 1] = cum[u] + static_cast<int64_t>(tot[u]);
-    pl->ublock_bounds = user_block_bounds(cum.data(), pl->n_users, std::max(1, std::min(pl->tile_ublocks, std::max(1, pl->n_users))));
+    const int32_t n_rows = rq ? pl->n_items : pl->n_users;
+    std::vector<int64_t> cum(static_cast<size_t>(n_rows) + 1, 0);
+    for (int32_t x = 0; x < n_rows; ++x) cum[x + 1] = cum[x] + static_cast<int64_t>(tot[x]);
+    if (rq) {
+        pl->iblock_bounds = user_block_bounds(cum.data(), n_rows, nbk);
+        pl->ublock_bounds.clear();
+    } else {
+        pl->ublock_bounds = user_block_bounds(cum.data(), n_rows, nbk);
+        pl->iblock_bounds.clear();
+    }
     if (c.nccl && c.nranks > 1 && pl->tile_wg == 0) {  // leave CUs to the collective's workgroups
         int cus = 0;
         RS_HIP(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, c.device));
@@ -247,8 +303,8 @@ void shard_setup(rs_svd_plan* pl, ShardComm& c, int32_t n_blocks, const std::vec
     }
     tile_build(pl);
     const int32_t nb = static_cast<int32_t>(pl->t_block_tile.size()) - 1;
-    if (c.mode == RS_EXCHANGE_ROTATE && nb != c.pieces * c.nranks)
-        throw std::logic_error("rotation: user blocks do not match the rank-blocks");
+    if (c.mode != RS_EXCHANGE_AVERAGE && nb != c.pieces * c.nranks)
+        throw std::logic_error("rotation: blocks do not match the rank-blocks");
     if (c.mode == RS_EXCHANGE_AVERAGE) {
         c.dP.alloc(static_cast<size_t>(std::max(1, pl->n_users)) * c.ldd);
         RS_HIP(hipMemsetAsync(c.dP.p, 0, c.dP.n * sizeof(float), pl->ctx->stream));
@@ -262,7 +318,7 @@ void shard_setup(rs_svd_plan* pl, ShardComm& c, int32_t n_blocks, const std::vec
         RS_HIP(hipEventCreateWithFlags(&c.ev_gb, hipEventDisableTiming));
         c.ev_done.resize(static_cast<size_t>(nb), nullptr);
         for (hipEvent_t& e : c.ev_done) RS_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
-        if (c.mode == RS_EXCHANGE_ROTATE) {
+        if (c.mode != RS_EXCHANGE_AVERAGE) {
             c.ev_recv.resize(static_cast<size_t>(nb), nullptr);
             for (hipEvent_t& e : c.ev_recv) RS_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
         }
@@ -334,23 +390,32 @@ void epochs_average(rs_svd_plan* pl, int32_t n_epochs, float lr, float reg, hipS
     q_convert(pl, s, 0);
 }
 
-// rows [u0, u1) of P (whole rows, the bias in column k) as one contiguous range
+// whole rows [r0, r1) of a factor matrix (the bias in column k) as one contiguous range
 struct RowRange {
     float* p;
     size_t n;
 };
-RowRange block_rows(rs_svd_plan* pl, float* P, int32_t b) {
-    const int32_t u0 = pl->t_block_user[b], u1 = pl->t_block_user[b + 1];
-    return {P + static_cast<int64_t>(u0) * pl->ld, static_cast<size_t>(u1 - u0) * pl->ld};
+RowRange rows_of(const rs_svd_plan* pl, float* base, int32_t r0, int32_t r1) {
+    return {base + static_cast<int64_t>(r0) * pl->ld, static_cast<size_t>(r1 - r0) * pl->ld};
+}
+// the rows of block b that travel: P user rows (ROTATE) or Q item rows (ROTATE_Q); base = that matrix
+RowRange block_rows(const rs_svd_plan* pl, float* base, int32_t b) {
+    const std::vector<int32_t>& bd = pl->shard->mode == RS_EXCHANGE_ROTATE_Q ? pl->iblock_bounds : pl->t_block_user;
+    return rows_of(pl, base, bd[b], bd[b + 1]);
+}
+// rank-block r (pieces r h .. r h + h - 1) as one range
+RowRange rank_block_rows(const rs_svd_plan* pl, float* base, int32_t r, int32_t h) {
+    const RowRange a = block_rows(pl, base, r * h), z = block_rows(pl, base, r * h + h - 1);
+    return {a.p, static_cast<size_t>(z.p + z.n - a.p)};
 }
 
-// ROTATE: n_epochs of the stratum rotation on stream s (the comm stream carries the transfers)
+// ROTATE / ROTATE_Q: n_epochs of the stratum rotation on stream s (the comm stream carries the transfers)
 void epochs_rotate(rs_svd_plan* pl, int32_t n_epochs, float lr, float reg, hipStream_t s) {
     ShardComm& c = *pl->shard;
     const int32_t N = c.nranks, h = c.pieces, nb = N * h, g = c.rank;
+    const bool rq = c.mode == RS_EXCHANGE_ROTATE_Q;
+    float* const M = rq ? pl->Q.p : pl->P.p;  // the factor matrix whose blocks rotate (Q: int32 bits in a call)
     const double inv_total = c.total_nnz > 0 ? 1.0 / c.total_nnz : 0.0;
-    // test hook: the shard of this rank throws in the last sub-epoch (the others must be released)
-    const int fault = std::getenv("RSGPU_FAULT_SHARD") ? std::atoi(std::getenv("RSGPU_FAULT_SHARD")) : -1;
     q_convert(pl, s, 1);
     for (int32_t e = 0; e < n_epochs; ++e) {
         for (int32_t st = 0; st < N; ++st) {
@@ -366,15 +431,18 @@ void epochs_rotate(rs_svd_plan* pl, int32_t n_epochs, float lr, float reg, hipSt
                                                         pl->t_block_tile[b + 1]);
                 merge_tile_split_rows(pl, pl->t_block_split[b], pl->t_block_split[b + 1], s);
                 gb_sum(pl->partial.p, parts, c.gbs.p + b, s);
-                if (g == fault && st == N - 1) throw std::runtime_error("injected shard fault (RSGPU_FAULT_SHARD)");
+                if (pl->fault_sub_epoch == st) {  // test hook (rs_svd_plan_inject_fault), once
+                    pl->fault_sub_epoch = -1;
+                    throw std::runtime_error("injected shard fault (rs_svd_plan_inject_fault)");
+                }
                 if (c.nccl && N > 1) {  // piece j goes to rank g - 1, piece j of the next rank-block comes in
                     const int32_t b_in = rb_in * h + j;
-                    const RowRange out = block_rows(pl, pl->P.p, b), in = block_rows(pl, pl->P.p, b_in);
+                    const RowRange out = block_rows(pl, M, b), in = block_rows(pl, M, b_in);
                     RS_HIP(hipEventRecord(c.ev_done[b], s));
                     RS_HIP(hipStreamWaitEvent(c.cs, c.ev_done[b], 0));
                     check_nccl(ncclGroupStart(), "ncclGroupStart");
-                    if (out.n) check_nccl(ncclSend(out.p, out.n, ncclFloat32, prev, c.nccl, c.cs), "ncclSend(P block)");
-                    if (in.n) check_nccl(ncclRecv(in.p, in.n, ncclFloat32, next, c.nccl, c.cs), "ncclRecv(P block)");
+                    if (out.n) check_nccl(ncclSend(out.p, out.n, ncclFloat32, prev, c.nccl, c.cs), "ncclSend(block)");
+                    if (in.n) check_nccl(ncclRecv(in.p, in.n, ncclFloat32, next, c.nccl, c.cs), "ncclRecv(block)");
                     check_nccl(ncclGroupEnd(), "ncclGroupEnd");
                     RS_HIP(hipEventRecord(c.ev_recv[b_in], c.cs));
                     c.pending[b_in] = 1;
@@ -384,10 +452,9 @@ void epochs_rotate(rs_svd_plan* pl, int32_t n_epochs, float lr, float reg, hipSt
                 LocalGroup& lg = *c.local;
                 RS_HIP(hipStreamSynchronize(s));
                 lg.barrier();  // every shard finished sub-epoch st
-                const RowRange in0 = block_rows(pl, pl->P.p, rb_in * h), in1 = block_rows(pl, pl->P.p, rb_in * h + h - 1);
-                const size_t n = static_cast<size_t>(in1.p + in1.n - in0.p);
-                const float* src = lg.P[next] + (in0.p - pl->P.p);
-                if (n) RS_HIP(hipMemcpyPeerAsync(in0.p, lg.dev[g], src, lg.dev[next], n * sizeof(float), s));
+                const RowRange in = rank_block_rows(pl, M, rb_in, h);
+                const float* src = (rq ? lg.Q : lg.P)[next] + (in.p - M);
+                if (in.n) RS_HIP(hipMemcpyPeerAsync(in.p, lg.dev[g], src, lg.dev[next], in.n * sizeof(float), s));
                 RS_HIP(hipStreamSynchronize(s));
                 lg.barrier();  // every pull done: the next sub-epoch may write these rows
             }
@@ -416,7 +483,8 @@ void epochs_rotate(rs_svd_plan* pl, int32_t n_epochs, float lr, float reg, hipSt
         }
         RS_HIP(hipGetLastError());
     }
-    // rank-block r is current on rank r: broadcast them so P is replicated again
+    // rank-block r is current on rank r: broadcast them so the matrix is replicated again (ROTATE_Q: and the
+    // P rows of every rank's user range)
     if (n_epochs > 0 && N > 1) {
         if (c.nccl) {
             for (int32_t b = 0; b < nb; ++b)
@@ -428,9 +496,12 @@ void epochs_rotate(rs_svd_plan* pl, int32_t n_epochs, float lr, float reg, hipSt
             RS_HIP(hipStreamWaitEvent(c.cs, c.ev_gb, 0));
             check_nccl(ncclGroupStart(), "ncclGroupStart");
             for (int32_t r = 0; r < N; ++r) {
-                const RowRange a = block_rows(pl, pl->P.p, r * h), z = block_rows(pl, pl->P.p, r * h + h - 1);
-                const size_t n = static_cast<size_t>(z.p + z.n - a.p);
-                if (n) check_nccl(ncclBroadcast(a.p, a.p, n, ncclFloat32, r, c.nccl, c.cs), "ncclBroadcast(P)");
+                const RowRange a = rank_block_rows(pl, M, r, h);
+                if (a.n) check_nccl(ncclBroadcast(a.p, a.p, a.n, ncclFloat32, r, c.nccl, c.cs), "ncclBroadcast(block)");
+                if (rq) {
+                    const RowRange u = rows_of(pl, pl->P.p, c.owner[r], c.owner[r + 1]);
+                    if (u.n) check_nccl(ncclBroadcast(u.p, u.p, u.n, ncclFloat32, r, c.nccl, c.cs), "ncclBroadcast(P range)");
+                }
             }
             check_nccl(ncclGroupEnd(), "ncclGroupEnd");
             RS_HIP(hipEventRecord(c.ev_epoch, c.cs));
@@ -439,10 +510,16 @@ void epochs_rotate(rs_svd_plan* pl, int32_t n_epochs, float lr, float reg, hipSt
             LocalGroup& lg = *c.local;
             for (int32_t r = 0; r < N; ++r) {
                 if (r == g) continue;
-                const RowRange a = block_rows(pl, pl->P.p, r * h), z = block_rows(pl, pl->P.p, r * h + h - 1);
-                const size_t n = static_cast<size_t>(z.p + z.n - a.p);
-                if (n)
-                    RS_HIP(hipMemcpyPeerAsync(a.p, lg.dev[g], lg.P[r] + (a.p - pl->P.p), lg.dev[r], n * sizeof(float), s));
+                const RowRange a = rank_block_rows(pl, M, r, h);
+                if (a.n)
+                    RS_HIP(hipMemcpyPeerAsync(a.p, lg.dev[g], (rq ? lg.Q : lg.P)[r] + (a.p - M), lg.dev[r],
+                                              a.n * sizeof(float), s));
+                if (rq) {
+                    const RowRange u = rows_of(pl, pl->P.p, c.owner[r], c.owner[r + 1]);
+                    if (u.n)
+                        RS_HIP(hipMemcpyPeerAsync(u.p, lg.dev[g], lg.P[r] + (u.p - pl->P.p), lg.dev[r],
+                                                  u.n * sizeof(float), s));
+                }
             }
             RS_HIP(hipStreamSynchronize(s));
             lg.barrier();  // nobody trains on (or is read from) before every shard has its copy
@@ -459,8 +536,8 @@ void epochs_sharded(rs_svd_plan* pl, int32_t n_epochs, float lr, float reg, hipS
     if (static_cast<int32_t>(pl->shard->gbs.n) != static_cast<int32_t>(pl->t_block_tile.size()) - 1)
         throw std::logic_error("user blocks changed after the join");
     RS_HIP(hipEventRecord(pl->ev0, s));
-    if (pl->shard->mode == RS_EXCHANGE_ROTATE) epochs_rotate(pl, n_epochs, lr, reg, s);
-    else epochs_average(pl, n_epochs, lr, reg, s);
+    if (pl->shard->mode == RS_EXCHANGE_AVERAGE) epochs_average(pl, n_epochs, lr, reg, s);
+    else epochs_rotate(pl, n_epochs, lr, reg, s);
     RS_HIP(hipEventRecord(pl->ev1, s));
     pl->last_launches = n_epochs;  // rs_svd_plan_last_kernel_ms: the call's device span per epoch
     pl->last_stream = s;
@@ -487,17 +564,28 @@ void group_join(rs_svd_group* g, int32_t n_blocks) {
     std::sort(sorted.begin(), sorted.end());
     const bool distinct = std::adjacent_find(sorted.begin(), sorted.end()) == sorted.end();
     if (!distinct && n > rs::kMaxLocal) throw std::invalid_argument("at most 16 shards share devices");
-    // user weights and the total from the shards' host CSRs (no collective needed in one process)
-    const int32_t nu = g->plans[0]->n_users;
-    std::vector<double> tot(static_cast<size_t>(std::max(1, nu)), 0.0);
+    // user (ROTATE_Q: item) totals, the user ranges and the total from the shards' host CSRs (no
+    // collective needed in one process)
+    const int32_t nu = g->plans[0]->n_users, ni = g->plans[0]->n_items;
+    const bool rq = g->plans[0]->exchange == RS_EXCHANGE_ROTATE_Q;
+    std::vector<double> tot(static_cast<size_t>(std::max(1, rq ? ni : nu)), 0.0);
+    std::vector<int64_t> first(n), end(n);
     double total = 0.0;
-    for (rs_svd_plan* pl : g->plans) {
+    for (int r = 0; r < n; ++r) {
+        const rs_svd_plan* pl = g->plans[r];
         if (pl->n_users != nu || pl->k != g->plans[0]->k)
             throw std::invalid_argument("shards must have the same users and n_factors");
         if (pl->exchange != g->plans[0]->exchange) throw std::invalid_argument("shards must use the same exchange");
-        for (int32_t u = 0; u < nu; ++u) tot[u] += static_cast<double>(pl->h_rowptr[u + 1] - pl->h_rowptr[u]);
+        if (rq) {
+            if (pl->n_items != ni) throw std::invalid_argument("RS_EXCHANGE_ROTATE_Q shards must have the same items");
+            for (int32_t c : pl->h_cols) tot[c] += 1.0;
+            std::tie(first[r], end[r]) = rs::user_span(pl);
+        } else {
+            for (int32_t u = 0; u < nu; ++u) tot[u] += static_cast<double>(pl->h_rowptr[u + 1] - pl->h_rowptr[u]);
+        }
         total += static_cast<double>(pl->nnz);
     }
+    const std::vector<int32_t> owner = rq ? rs::owner_ranges(first, end, nu) : std::vector<int32_t>();
     std::vector<ncclComm_t> comms(static_cast<size_t>(n), nullptr);
     if (distinct) {
         ncclUniqueId id;
@@ -532,6 +620,7 @@ void group_join(rs_svd_group* g, int32_t n_blocks) {
         c->nccl = comms[r];
         c->local = g->local;
         c->total_nnz = total;
+        c->owner = owner;
         if (pl->exchange == RS_EXCHANGE_AVERAGE) rs::set_weights(pl, tot);
         rs::shard_setup(pl, *c, n_blocks, tot);
         pl->shard = std::move(c);
@@ -541,6 +630,7 @@ void group_join(rs_svd_group* g, int32_t n_blocks) {
             g->local->dP.push_back(pl->shard->dP.p);
             g->local->gbs.push_back(pl->shard->gbs.p);
             g->local->P.push_back(pl->P.p);
+            g->local->Q.push_back(pl->Q.p);
             g->local->dev.push_back(pl->ctx->device);
         }
     }
@@ -633,10 +723,16 @@ extern "C" int rs_svd_plan_set_user_blocks(rs_svd_plan* pl, int32_t n_blocks, co
 
 extern "C" int rs_svd_plan_set_exchange(rs_svd_plan* pl, int32_t mode) {
     if (!pl) return rs::set_error(nullptr, RS_ERR_INVALID, "plan is NULL");
-    if (mode != RS_EXCHANGE_ROTATE && mode != RS_EXCHANGE_AVERAGE)
+    if (mode != RS_EXCHANGE_ROTATE && mode != RS_EXCHANGE_AVERAGE && mode != RS_EXCHANGE_ROTATE_Q)
         return rs::set_error(pl->ctx, RS_ERR_INVALID, "unknown exchange");
     if (pl->shard) return rs::set_error(pl->ctx, RS_ERR_INVALID, "plan is joined to a group (leave first)");
     pl->exchange = mode;
+    return RS_OK;
+}
+
+extern "C" int rs_svd_plan_inject_fault(rs_svd_plan* pl, int32_t sub_epoch) {
+    if (!pl || sub_epoch < -1) return rs::set_error(pl ? pl->ctx : nullptr, RS_ERR_INVALID, "bad arguments");
+    pl->fault_sub_epoch = sub_epoch;
     return RS_OK;
 }
 
@@ -658,11 +754,25 @@ extern "C" int rs_svd_plan_join(rs_svd_plan* pl, const void* id, int32_t rank, i
         ncclConfig_t cfg = NCCL_CONFIG_INITIALIZER;
         cfg.maxCTAs = rs::comm_ctas();
         rs::check_nccl(ncclCommInitRankConfig(&c->nccl, n_ranks, u, rank, &cfg), "ncclCommInitRankConfig");
-        // per-user rating counts and the total over all shards (one all-reduce each)
+        // per-user (ROTATE_Q: per-item) rating counts over all shards, the total and (ROTATE_Q) every rank's
+        // user span, in one all-reduce
         hipStream_t s = pl->ctx->stream;
         const int32_t nu = pl->n_users;
-        std::vector<double> cnt(static_cast<size_t>(std::max(1, nu)), 0.0);
-        for (int32_t u2 = 0; u2 < nu; ++u2) cnt[u2] = static_cast<double>(pl->h_rowptr[u2 + 1] - pl->h_rowptr[u2]);
+        const bool rq = pl->exchange == RS_EXCHANGE_ROTATE_Q;
+        const int32_t n_rows = rq ? pl->n_items : nu;
+        std::vector<double> cnt(static_cast<size_t>(std::max(1, n_rows)), 0.0);
+        if (rq) {
+            for (int32_t c2 : pl->h_cols) cnt[c2] += 1.0;
+        } else {
+            for (int32_t u2 = 0; u2 < nu; ++u2) cnt[u2] = static_cast<double>(pl->h_rowptr[u2 + 1] - pl->h_rowptr[u2]);
+        }
+        const size_t span_at = cnt.size();
+        cnt.resize(span_at + 2 * static_cast<size_t>(n_ranks), 0.0);
+        if (rq) {  // slot of this rank: first + 1 (0: no ratings), end
+            const std::pair<int64_t, int64_t> sp = rs::user_span(pl);
+            cnt[span_at + 2 * rank] = static_cast<double>(sp.first + 1);
+            cnt[span_at + 2 * rank + 1] = static_cast<double>(sp.second);
+        }
         cnt.push_back(static_cast<double>(pl->nnz));
         rs::DevBuf<double> d(cnt.size());
         d.upload(cnt.data(), cnt.size(), s);
@@ -670,7 +780,15 @@ extern "C" int rs_svd_plan_join(rs_svd_plan* pl, const void* id, int32_t rank, i
         d.download(cnt.data(), cnt.size(), s);
         RS_HIP(hipStreamSynchronize(s));
         c->total_nnz = cnt.back();
-        cnt.pop_back();
+        if (rq) {
+            std::vector<int64_t> first(n_ranks), end(n_ranks);
+            for (int32_t r = 0; r < n_ranks; ++r) {
+                first[r] = static_cast<int64_t>(cnt[span_at + 2 * r]) - 1;
+                end[r] = static_cast<int64_t>(cnt[span_at + 2 * r + 1]);
+            }
+            c->owner = rs::owner_ranges(first, end, nu);
+        }
+        cnt.resize(span_at);
         if (pl->exchange == RS_EXCHANGE_AVERAGE) rs::set_weights(pl, cnt);
         rs::shard_setup(pl, *c, n_blocks, cnt);
         pl->shard = std::move(c);
@@ -693,7 +811,14 @@ extern "C" int rs_svd_plan_epochs_sharded(rs_svd_plan* pl, int32_t n_epochs, flo
         if (!pl->shard) return rs::set_error(pl->ctx, RS_ERR_INVALID, "plan is not joined (rs_svd_plan_join)");
         if (n_epochs < 0) return rs::set_error(pl->ctx, RS_ERR_INVALID, "n_epochs < 0");
         if (pl->shard->local) return rs::set_error(pl->ctx, RS_ERR_INVALID, "group shards run through rs_svd_group_epochs");
-        rs::epochs_sharded(pl, n_epochs, lr, reg, stream ? static_cast<hipStream_t>(stream) : pl->ctx->stream);
+        if (pl->shard->aborted)
+            return rs::set_error(pl->ctx, RS_ERR_INVALID, "the shard's communicator was aborted after an error (leave, then join again)");
+        try {
+            rs::epochs_sharded(pl, n_epochs, lr, reg, stream ? static_cast<hipStream_t>(stream) : pl->ctx->stream);
+        } catch (...) {  // sends of this sub-epoch will never be posted: abort so nothing waits on this rank
+            pl->shard->abort_comm();
+            throw;
+        }
         return RS_OK;
     });
 }
@@ -790,9 +915,21 @@ extern "C" int rs_svd_fit_multi(const int32_t* devices, int32_t n_devices, const
     if (r->nnz < 0 || r->n_users < 0 || r->n_items < 0 || (r->nnz > 0 && (!r->users || !r->items || !r->ratings)))
         return rs::set_error(nullptr, RS_ERR_INVALID, "bad ratings");
     const int32_t n = n_devices, k = p->n_factors;
+    // the smaller factor matrix travels: item shards + P rotation, or user ranges + Q rotation
+    const bool rq = r->n_items < r->n_users;
     std::vector<int32_t> bounds(static_cast<size_t>(n) + 1);
-    int st = rs_item_shards(r->nnz, r->items, r->n_items, n, bounds.data());
-    if (st != RS_OK) return st;
+    if (rq) {
+        std::vector<int64_t> cum(static_cast<size_t>(r->n_users) + 1, 0);
+        for (int64_t t = 0; t < r->nnz; ++t) {
+            if (r->users[t] < 0 || r->users[t] >= r->n_users) return rs::set_error(nullptr, RS_ERR_INVALID, "user id out of range");
+            cum[r->users[t] + 1]++;
+        }
+        for (int32_t u = 0; u < r->n_users; ++u) cum[u + 1] += cum[u];
+        bounds = rs::user_block_bounds(cum.data(), r->n_users, n);
+    } else {
+        int st = rs_item_shards(r->nnz, r->items, r->n_items, n, bounds.data());
+        if (st != RS_OK) return st;
+    }
     std::vector<rs_ctx*> ctxs(n, nullptr);
     std::vector<rs_svd_plan*> plans(n, nullptr);
     rs_svd_group* g = nullptr;
@@ -801,7 +938,7 @@ extern "C" int rs_svd_fit_multi(const int32_t* devices, int32_t n_devices, const
         for (rs_svd_plan* pl : plans) rs_svd_plan_destroy(pl);
         for (rs_ctx* c : ctxs) rs_close(c);
     };
-    st = rs_guard(nullptr, [&]() -> int {
+    int st = rs_guard(nullptr, [&]() -> int {
         *gb = p->n_epochs > 0 ? rs::gb_warm_start(r, bu, bi) : *gb;  // as rs_svd_fit (FAST)
         for (int32_t s = 0; s < n; ++s) {
             int e = rs_open(devices[s], &ctxs[s]);
@@ -809,16 +946,25 @@ extern "C" int rs_svd_fit_multi(const int32_t* devices, int32_t n_devices, const
             const int32_t lo = bounds[s], hi = bounds[s + 1];
             std::vector<int32_t> su, si;
             std::vector<double> sr;
-            for (int64_t t = 0; t < r->nnz; ++t)
-                if (r->items[t] >= lo && r->items[t] < hi) {
+            for (int64_t t = 0; t < r->nnz; ++t) {
+                const int32_t key = rq ? r->users[t] : r->items[t];
+                if (key >= lo && key < hi) {
                     su.push_back(r->users[t]);
-                    si.push_back(r->items[t] - lo);
+                    si.push_back(rq ? r->items[t] : r->items[t] - lo);
                     sr.push_back(r->ratings[t]);
                 }
-            rs_ratings sh{static_cast<int64_t>(su.size()), r->n_users, hi - lo, su.data(), si.data(), sr.data()};
+            }
+            rs_ratings sh{static_cast<int64_t>(su.size()), r->n_users, rq ? r->n_items : hi - lo, su.data(), si.data(),
+                          sr.data()};
             e = rs_svd_plan_create(ctxs[s], &sh, k, &plans[s]);
             if (e != RS_OK) return e;
-            e = rs_svd_plan_upload(plans[s], P, Q + static_cast<int64_t>(lo) * k, bu, bi + lo, gb);
+            if (rq) {
+                e = rs_svd_plan_set_exchange(plans[s], RS_EXCHANGE_ROTATE_Q);
+                if (e != RS_OK) return e;
+                e = rs_svd_plan_upload(plans[s], P, Q, bu, bi, gb);
+            } else {
+                e = rs_svd_plan_upload(plans[s], P, Q + static_cast<int64_t>(lo) * k, bu, bi + lo, gb);
+            }
             if (e != RS_OK) return e;
         }
         int e = rs_svd_group_create(plans.data(), n, n_blocks, &g);
@@ -826,8 +972,9 @@ extern "C" int rs_svd_fit_multi(const int32_t* devices, int32_t n_devices, const
         e = rs_svd_group_epochs(g, p->n_epochs, static_cast<float>(p->lr), static_cast<float>(p->reg));
         if (e != RS_OK) return e;
         int numeric = RS_OK;  // every shard's values are returned before RS_ERR_NUMERIC is
-        for (int32_t s = 0; s < n; ++s) {  // P, b_u, GlobalBias are identical on every shard: take shard 0's
-            const int32_t lo = bounds[s];
+        for (int32_t s = 0; s < n; ++s) {  // P, b_u, GlobalBias (ROTATE_Q: everything) identical on every shard
+            if (rq && s > 0) break;
+            const int32_t lo = rq ? 0 : bounds[s];
             e = rs_svd_plan_download(plans[s], s == 0 ? P : nullptr, Q + static_cast<int64_t>(lo) * k,
                                      s == 0 ? bu : nullptr, bi + lo, s == 0 ? gb : nullptr);
             if (e == RS_ERR_NUMERIC && numeric == RS_OK) numeric = e;

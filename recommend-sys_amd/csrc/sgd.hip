@@ -1818,6 +1818,21 @@ extern "C" int rs_svd_plan_set_tiles(rs_svd_plan* pl, int32_t workgroups, int32_
     });
 }
 
+// Claimed runs inside a tile (include/rsgpu.h): 0 = runs dealt to the waves on the host, 4 or 8 = runs
+// per claim from the tile's run queue (the default 4).  Rebuilds the schedule.
+extern "C" int rs_svd_plan_set_tile_claim(rs_svd_plan* pl, int32_t runs_per_claim) {
+    if (!pl) return rs::set_error(nullptr, RS_ERR_INVALID, "plan is NULL");
+    if (runs_per_claim != 0 && runs_per_claim != 4 && runs_per_claim != 8)
+        return rs::set_error(pl->ctx, RS_ERR_INVALID, "runs per claim must be 0, 4 or 8");
+    return rs_guard(pl->ctx, [&]() -> int {
+        rs::plan_sync_last(pl);
+        pl->tile_claim = runs_per_claim;
+        rs::tile_build(pl);
+        if (pl->write_back == RS_SGD_WB_TILE) pl->n_blocks = rs::tile_partials(pl);
+        return RS_OK;
+    });
+}
+
 extern "C" int rs_svd_plan_tile_clocks(rs_svd_plan* pl, int64_t* out, int64_t n) {
     if (!pl || !out || n < 0) return rs::set_error(pl ? pl->ctx : nullptr, RS_ERR_INVALID, "bad arguments");
     return rs_guard(pl->ctx, [&]() -> int {

@@ -79,7 +79,8 @@ struct rs_svd_plan {
     int32_t tile_waves = 16;  // waves per workgroup (1, 2, 4, 8 or 16)
     int32_t tile_target = 0;  // ratings per tile (0 = nnz / workgroups, bounded by the LDS)
     int32_t tile_run_cap = 0; // runs longer than this are cut over waves (0 = never)
-    int32_t tile_ring = 0;    // q_i rows prefetched per wave (0 = auto: 12, fewer for wide rows)
+    int32_t tile_ring = 0;    // q_i rows prefetched per wave (0 = auto: 2)
+    int32_t tile_claim = 4;   // runs per claim from the tile's run queue (4 or 8; 0 = runs dealt on the host)
     int32_t n_tiles = 0, tile_grid = 0;
     size_t tile_lds = 0;      // dynamic LDS bytes of the launch (the largest tile)
     bool tiles_built = false, hybrid_built = false;
@@ -98,9 +99,14 @@ struct rs_svd_plan {
     int32_t tile_user_lds = 0;  // LDS ints per user (0 = one row of k + 2)
     std::vector<int32_t> ublock_bounds;  // caller's block bounds (tile_ublocks + 1), or empty: own ratings
     std::vector<int32_t> t_block_tile, t_block_user;
+    // item blocks (RS_EXCHANGE_ROTATE_Q, multi.hip): when set (n_blocks + 1 item ids from 0 to n_items) the
+    // tiles are built per stratum -- block b's tiles hold this plan's ratings of items
+    // [iblock_bounds[b], iblock_bounds[b+1]) over all its users -- instead of per user block
+    std::vector<int32_t> iblock_bounds;
     std::vector<int32_t> t_block_split;  // block b's split users: t_split_rows[t_block_split[b], t_block_split[b+1])
     std::shared_ptr<rs::ShardComm> shard;  // item-sharded multi-GPU state (multi.hip), or empty
     int32_t exchange = RS_EXCHANGE_ROTATE;  // the multi-GPU exchange a join sets up
+    int32_t fault_sub_epoch = -1;  // test hook (rs_svd_plan_inject_fault): the next sharded call throws there
     ~rs_svd_plan() {
         if (ev0) (void)hipEventDestroy(ev0);
         if (ev1) (void)hipEventDestroy(ev1);

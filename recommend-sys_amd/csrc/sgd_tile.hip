@@ -82,7 +82,17 @@ __device__ __forceinline__ int32_t cvt_rpi(float x) {
 // q <- a q - c p_new gives b_u <- a b_u - c and b_i <- a b_i - c (svd.go:108-112); only the two
 // constant columns are held at 1 by a select.  In memory the bias sits in column k of both rows
 // (the 64-B line budget of the global atomics, sgd.hip) and nothing is stored past it.
-template <int E, int NW, int RQ, int DIAG = 0>
+//
+// Work distribution inside a tile (CH, round 4).  CH = 0: the runs are dealt to the NW waves on the host
+// (streams of near-equal ratings).  CH > 0: the tile's runs form ONE queue and a wave claims CH
+// consecutive runs at a time from an LDS counter.  Round 3's per-wave clocks showed that a
+// wave's time does not follow its ratings or runs (R^2 = 0.04) but the memory side, so no static deal can
+// balance it: the slowest of 16 waves was 8 % above the mean.  With claims a workgroup ends about one
+// chunk after its mean wave.  The claim for the chunk after next is issued when a chunk starts and its
+// headers / first record window are read after the chunk's first / second run, so no LDS round trip
+// waits on the critical path.  With one wave the claims come in queue order: the visit order is the
+// queue, as rs_svd_plan_tile_order exports it.
+template <int E, int NW, int RQ, int CH, int DIAG = 0>
 __global__ __launch_bounds__(NW * 64) void svd_epoch_tile_kernel(
     const int4* __restrict__ tiles, int32_t n_tiles, const int2* __restrict__ tile_users,
     const int32_t* __restrict__ streams, const int2* __restrict__ runs, const int2* __restrict__ recs,
@@ -93,11 +103,13 @@ __global__ __launch_bounds__(NW * 64) void svd_epoch_tile_kernel(
 #pragma clang fp contract(fast)
     constexpr int LD = 64 * E, NT = NW * 64;  // LD: LDS row (k + 2 columns fit); ldm: the rows in HBM
     constexpr bool TIMED = (DIAG & 16) != 0;  // per-wave phase clocks into dbg (experiments)
+    static_assert(CH == 0 || (CH > RQ && CH >= 2 && CH < 64), "a claimed chunk must outlast the ring");
     int64_t tm_stage = 0, tm_ring = 0, tm_loop = 0, tm_tail = 0, tm_c = 0;
     auto clk = [] { return static_cast<int64_t>(__builtin_amdgcn_s_memtime()); };
     static_assert(2 * E * RQ <= 60, "ring loads and atomics must fit the 63-op vmcnt");
     typedef float f2 __attribute__((ext_vector_type(2)));
     extern __shared__ __align__(16) int32_t lds[];
+    __shared__ int32_t s_claim;  // CH > 0: next unclaimed chunk of the tile's run queue
     const int tid = static_cast<int>(threadIdx.x), lane = tid & 63;
     const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
     const __amdgpu_buffer_rsrc_t rq = __builtin_amdgcn_make_buffer_rsrc(Q, 0, q_bytes, 0x00020000);
@@ -137,6 +149,7 @@ __global__ __launch_bounds__(NW * 64) void svd_epoch_tile_kernel(
         }
         for (int32_t x = tid; x < n_rec; x += NT) Rl[x] = recs[tm.w + x];
         for (int32_t x = tid; x <= n_runs; x += NT) Ul[x] = tr[x];
+        if (CH > 0 && tid == 0) s_claim = NW;  // chunk w is wave w's without a claim
         __syncthreads();
         if constexpr (TIMED) {
             const int64_t c = clk();
@@ -144,21 +157,15 @@ __global__ __launch_bounds__(NW * 64) void svd_epoch_tile_kernel(
             tm_c = c;
         }
 
-        const int32_t r0 = sp[w], r1 = sp[w + 1];
-        // Run headers and records are read from LDS in 64-entry windows (one lane-parallel read per 64
-        // runs / ratings, then v_readlane with an SGPR index): no LDS round trip per run or rating.
-        int32_t hb = r0;  // run window base: lane l of (hw0, hw1) holds run hb + l, hb + 64 + l
-        int2 hw0 = Ul[min(hb + lane, n_runs)], hw1 = Ul[min(hb + 64 + lane, n_runs)];
-        auto run_hdr = [&](int32_t r, bool want_begin) -> int32_t {  // item or first record of run r
-            const int32_t o = r - hb;
-            const int32_t v = o < 64 ? (want_begin ? hw0.y : hw0.x) : (want_begin ? hw1.y : hw1.x);
-            return __builtin_amdgcn_readlane(v, o & 63);
+        // Records are read from LDS in 64-entry windows (one lane-parallel read per 64 ratings, then
+        // v_readlane with an SGPR index): no LDS round trip per rating.
+        int32_t rb = 0, j = 0;  // record window base, next record (tile-local)
+        int2 rw0, rw1;
+        auto set_window = [&](int32_t first) {
+            rb = j = first;
+            rw0 = Rl[min(rb + lane, n_rec - 1)];
+            rw1 = Rl[min(rb + 64 + lane, n_rec - 1)];
         };
-        auto item_of = [&](int32_t r) -> int32_t { return r < r1 ? run_hdr(r, false) : -1; };
-        const int32_t s_end = __builtin_amdgcn_readfirstlane(Ul[r1].y);  // records [first of r0, first of r1)
-        const int32_t s_begin = run_hdr(r0, true);
-        int32_t rb = s_begin;  // record window base (tile-local)
-        int2 rw0 = Rl[min(rb + lane, n_rec - 1)], rw1 = Rl[min(rb + 64 + lane, n_rec - 1)];
         auto load_q = [&](int32_t (&q)[E], int32_t item) {
             const int32_t row = item >= 0 ? item * (ldm * 4) : -1;  // SGPR arithmetic
 #pragma unroll
@@ -167,129 +174,189 @@ __global__ __launch_bounds__(NW * 64) void svd_epoch_tile_kernel(
                                   : static_cast<int32_t>(__builtin_amdgcn_raw_buffer_load_b32(rq, qaddr(row, x), 0, kSgdAux));
         };
         int32_t ring[RQ][E];
-#pragma unroll
-        for (int s = 0; s < RQ; ++s) {
-            load_q(ring[s], item_of(r0 + s));
-            // dropped atomics (out-of-range offsets): the loop is entered with the same pattern of
-            // loads and atomics in flight as its back edge carries, so the compiler's vmcnt waits
-            // keep the whole ring in flight instead of draining to the prologue's count
-#pragma unroll
-            for (int x = 0; x < E; ++x) {  // per-lane offsets and value: not folded into one lane
-                int32_t z;
-                asm volatile("v_mov_b32 %0, 0" : "=v"(z));
-                __builtin_amdgcn_raw_ptr_buffer_atomic_add_i32(z, rq, kOutOfRange + lane * 4 + 256 * x, 0, 0);
-            }
-        }
-        double gb = gb0;
-        const float klr = lr * kFxInv * kFxInv;  // c = lr (s 2^-48 + gb - r): p and q in 2^-24 units
-        int32_t j = rb;                 // next record
-        for (int32_t r = r0; r < r1; r += RQ) {
+        auto prefill = [&](auto&& item_at) {
 #pragma unroll
             for (int s = 0; s < RQ; ++s) {
-                const int32_t rr = r + s;
-                const bool live = rr < r1;  // wave-uniform
-                if (live && rr - hb >= 64) {  // slide the run window (every 64 runs)
-                    hb += 64;
-                    hw0 = hw1;
-                    hw1 = Ul[min(hb + 64 + lane, n_runs)];
-                }
-                int64_t c0 = 0;
-                if constexpr (TIMED) c0 = clk();
-                int32_t q0[E];
-                float q[E];
+                load_q(ring[s], item_at(s));
+                // dropped atomics (out-of-range offsets): the loop is entered with the same pattern of
+                // loads and atomics in flight as its back edge carries, so the compiler's vmcnt waits
+                // keep the whole ring in flight instead of draining to the prologue's count
 #pragma unroll
-                for (int x = 0; x < E; ++x) {
-                    // a real copy: ring[s] is then dead and its refill lands in the same registers (a
-                    // coalesced copy would keep both live and the compiler would rotate the ring with
-                    // moves at the loop back edge, waiting for every load in flight there)
-                    asm volatile("v_mov_b32 %0, %1" : "=v"(q0[x]) : "v"(ring[s][x]));
-                    q[x] = qone[x] ? kFx : static_cast<float>(q0[x]);  // q in 2^-24 units too
+                for (int x = 0; x < E; ++x) {  // per-lane offsets and value: not folded into one lane
+                    int32_t z;
+                    asm volatile("v_mov_b32 %0, 0" : "=v"(z));
+                    __builtin_amdgcn_raw_ptr_buffer_atomic_add_i32(z, rq, kOutOfRange + lane * 4 + 256 * x, 0, 0);
                 }
-                if constexpr (TIMED) {
-                    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // (timed variant only) honest split
-                    const int64_t c1 = clk();
-                    tm_ring += c1 - c0;
-                    c0 = c1;
+            }
+        };
+        double gb = gb0;
+        const float klr = lr * kFxInv * kFxInv;  // c = lr (s 2^-48 + gb - r): p and q in 2^-24 units
+        // One run: its q_i row comes out of ring slot `slot`, which is refilled with the row of `next`;
+        // records [j, e) are trained in order with q_i in registers, then the run's delta goes to memory.
+        auto run = [&](int32_t (&slot)[E], int32_t item, int32_t e, int32_t next) {
+            int64_t c0 = 0;
+            if constexpr (TIMED) c0 = clk();
+            int32_t q0[E];
+            float q[E];
+#pragma unroll
+            for (int x = 0; x < E; ++x) {
+                // a real copy: the slot is then dead and its refill lands in the same registers (a
+                // coalesced copy would keep both live and the compiler would rotate the ring with
+                // moves at the loop back edge, waiting for every load in flight there)
+                asm volatile("v_mov_b32 %0, %1" : "=v"(q0[x]) : "v"(slot[x]));
+                q[x] = qone[x] ? kFx : static_cast<float>(q0[x]);  // q in 2^-24 units too
+            }
+            if constexpr (TIMED) {
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // (timed variant only) honest split
+                const int64_t c1 = clk();
+                tm_ring += c1 - c0;
+                c0 = c1;
+            }
+            load_q(slot, next);  // refill: every slot issues E loads + E atomics
+            const float gbf = static_cast<float>(gb);
+            float cs = 0.f;  // sum of this run's c: GlobalBias moves by -cs (folded in double)
+            for (; j < e; ++j) {
+                if (j - rb >= 64) {  // slide the record window (every 64 ratings)
+                    rb += 64;
+                    rw0 = rw1;
+                    rw1 = Rl[min(rb + 64 + lane, n_rec - 1)];
                 }
-                const int32_t item = live ? run_hdr(rr, false) : -1;
-                const int32_t e = live ? run_hdr(rr + 1, true) : j;
-                load_q(ring[s], item_of(rr + RQ));  // refill: every slot issues E loads + E atomics
-                const float gbf = static_cast<float>(gb);
-                float cs = 0.f;  // sum of this run's c: GlobalBias moves by -cs (folded in double)
-                for (; j < e; ++j) {
-                    if (j - rb >= 64) {  // slide the record window (every 64 ratings)
-                        rb += 64;
-                        rw0 = rw1;
-                        rw1 = Rl[min(rb + 64 + lane, n_rec - 1)];
+                const int32_t o = j - rb;
+                const int32_t ul = __builtin_amdgcn_readlane(rw0.x, o);
+                const float rt = __int_as_float(__builtin_amdgcn_readlane(rw0.y, o));
+                int32_t* prow = Pl + ul * LD + lane;
+                float pu[E];  // p in 2^-24 units
+#pragma unroll
+                for (int x = 0; x < E; ++x)
+                    pu[x] = (DIAG & 8) ? 1e5f * ul : static_cast<float>(prow[64 * x]);
+                // dot over all columns (biases included), two columns per packed op
+                float sd;
+                {
+                    f2 acc = {0.f, 0.f};
+#pragma unroll
+                    for (int x = 0; x + 1 < E; x += 2) {
+                        const f2 pv = {pu[x], pu[x + 1]}, qv = {q[x], q[x + 1]};
+                        acc = __builtin_elementwise_fma(pv, qv, acc);
                     }
-                    const int32_t o = j - rb;
-                    const int32_t ul = __builtin_amdgcn_readlane(rw0.x, o);
-                    const float rt = __int_as_float(__builtin_amdgcn_readlane(rw0.y, o));
-                    int32_t* prow = Pl + ul * LD + lane;
-                    float pu[E];  // p in 2^-24 units
-#pragma unroll
-                    for (int x = 0; x < E; ++x)
-                        pu[x] = (DIAG & 8) ? 1e5f * ul : static_cast<float>(prow[64 * x]);
-                    // dot over all columns (biases included), two columns per packed op
-                    float sd;
-                    {
-                        f2 acc = {0.f, 0.f};
-#pragma unroll
-                        for (int x = 0; x + 1 < E; x += 2) {
-                            const f2 pv = {pu[x], pu[x + 1]}, qv = {q[x], q[x + 1]};
-                            acc = __builtin_elementwise_fma(pv, qv, acc);
-                        }
-                        sd = acc.x + acc.y;
-                        if constexpr (E & 1) sd = __builtin_fmaf(pu[E - 1], q[E - 1], sd);
-                    }
-                    sd = wave_sum_l63(sd);
-                    // svd.go:102-128: diff = (gb + b_u + b_i + p.q) - r, c = lr diff;
-                    // p <- a p - c q ; q <- a q - c p_new (Q1) ; gb <- gb - c
-                    const float c = __builtin_fmaf(sd, klr, lr * ((gbf - cs) - rt));
-                    cs += c;
+                    sd = acc.x + acc.y;
+                    if constexpr (E & 1) sd = __builtin_fmaf(pu[E - 1], q[E - 1], sd);
+                }
+                sd = wave_sum_l63(sd);
+                // svd.go:102-128: diff = (gb + b_u + b_i + p.q) - r, c = lr diff;
+                // p <- a p - c q ; q <- a q - c p_new (Q1) ; gb <- gb - c
+                const float c = __builtin_fmaf(sd, klr, lr * ((gbf - cs) - rt));
+                cs += c;
 
-                    float pn[E];
+                float pn[E];
 #pragma unroll
-                    for (int x = 0; x + 1 < E + 1; x += 2) {
-                        if (x + 1 < E) {  // d = (a - 1) p - c q in 2^-24 units; p_new = p + d
-                            const f2 pv = {pu[x], pu[x + 1]}, qv = {q[x], q[x + 1]};
-                            f2 d = __builtin_elementwise_fma(qv, f2{-c, -c}, pv * f2{am1, am1});
-                            if (pone[x]) d.x = 0.f;  // P's constant column stays 1 (b_i's partner)
-                            if (pone[x + 1]) d.y = 0.f;
-                            const f2 np = pv + d;
-                            const f2 nq = __builtin_elementwise_fma(np, f2{-c, -c}, qv * f2{a, a});
-                            pn[x] = d.x;
-                            pn[x + 1] = d.y;
-                            q[x] = nq.x;
-                            q[x + 1] = nq.y;
-                        } else {
-                            const float d = pone[x] ? 0.f : __builtin_fmaf(q[x], -c, pu[x] * am1);
-                            pn[x] = d;
-                            q[x] = __builtin_fmaf(pu[x] + d, -c, q[x] * a);
-                        }
-                    }
-#pragma unroll
-                    for (int x = 0; x < E; ++x) {
-                        if (qone[x]) q[x] = kFx;
-                        const int32_t di = cvt_rpi(pn[x]);
-                        if (!(DIAG & 4))
-                            __hip_atomic_fetch_add(prow + 64 * x, di, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                for (int x = 0; x + 1 < E + 1; x += 2) {
+                    if (x + 1 < E) {  // d = (a - 1) p - c q in 2^-24 units; p_new = p + d
+                        const f2 pv = {pu[x], pu[x + 1]}, qv = {q[x], q[x + 1]};
+                        f2 d = __builtin_elementwise_fma(qv, f2{-c, -c}, pv * f2{am1, am1});
+                        if (pone[x]) d.x = 0.f;  // P's constant column stays 1 (b_i's partner)
+                        if (pone[x + 1]) d.y = 0.f;
+                        const f2 np = pv + d;
+                        const f2 nq = __builtin_elementwise_fma(np, f2{-c, -c}, qv * f2{a, a});
+                        pn[x] = d.x;
+                        pn[x + 1] = d.y;
+                        q[x] = nq.x;
+                        q[x + 1] = nq.y;
+                    } else {
+                        const float d = pone[x] ? 0.f : __builtin_fmaf(q[x], -c, pu[x] * am1);
+                        pn[x] = d;
+                        q[x] = __builtin_fmaf(pu[x] + d, -c, q[x] * a);
                     }
                 }
-                gb -= static_cast<double>(cs);
-                if constexpr (TIMED) tm_loop += clk() - c0;
-                const int32_t row = live ? item * (ldm * 4) : -1;
 #pragma unroll
                 for (int x = 0; x < E; ++x) {
-                    const int32_t dq = cvt_rpi(q[x]) - q0[x];
-                    if constexpr (DIAG & 1)  // diagnostic: the atomic goes nowhere (same issue count)
-                        __builtin_amdgcn_raw_ptr_buffer_atomic_add_i32(dq, rq, kOutOfRange + lane * 4 + 256 * x, 0, 0);
-                    else
-                        __builtin_amdgcn_raw_ptr_buffer_atomic_add_i32(dq, rq, qaddr(row, x), 0, 0);
+                    if (qone[x]) q[x] = kFx;
+                    const int32_t di = cvt_rpi(pn[x]);
+                    if (!(DIAG & 4))
+                        __hip_atomic_fetch_add(prow + 64 * x, di, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                }
+            }
+            gb -= static_cast<double>(cs);
+            if constexpr (TIMED) tm_loop += clk() - c0;
+            const int32_t row = item >= 0 ? item * (ldm * 4) : -1;
+#pragma unroll
+            for (int x = 0; x < E; ++x) {
+                const int32_t dq = cvt_rpi(q[x]) - q0[x];
+                if constexpr (DIAG & 1)  // diagnostic: the atomic goes nowhere (same issue count)
+                    __builtin_amdgcn_raw_ptr_buffer_atomic_add_i32(dq, rq, kOutOfRange + lane * 4 + 256 * x, 0, 0);
+                else
+                    __builtin_amdgcn_raw_ptr_buffer_atomic_add_i32(dq, rq, qaddr(row, x), 0, 0);
+            }
+        };
+
+        int32_t nr = 0;  // ratings this wave trained in this tile (the GlobalBias fold's weight)
+        if constexpr (CH == 0) {
+            const int32_t r0 = sp[w], r1 = sp[w + 1];
+            // Run headers are read from LDS in 64-entry windows like the records
+            int32_t hb = r0;  // run window base: lane l of (hw0, hw1) holds run hb + l, hb + 64 + l
+            int2 hw0 = Ul[min(hb + lane, n_runs)], hw1 = Ul[min(hb + 64 + lane, n_runs)];
+            auto run_hdr = [&](int32_t r, bool want_begin) -> int32_t {  // item or first record of run r
+                const int32_t o = r - hb;
+                const int32_t v = o < 64 ? (want_begin ? hw0.y : hw0.x) : (want_begin ? hw1.y : hw1.x);
+                return __builtin_amdgcn_readlane(v, o & 63);
+            };
+            auto item_of = [&](int32_t r) -> int32_t { return r < r1 ? run_hdr(r, false) : -1; };
+            const int32_t s_end = __builtin_amdgcn_readfirstlane(Ul[r1].y);  // records [first of r0, first of r1)
+            const int32_t s_begin = run_hdr(r0, true);
+            set_window(s_begin);
+            prefill([&](int s) { return item_of(r0 + s); });
+            for (int32_t r = r0; r < r1; r += RQ) {
+#pragma unroll
+                for (int s = 0; s < RQ; ++s) {
+                    const int32_t rr = r + s;
+                    const bool live = rr < r1;  // wave-uniform
+                    if (live && rr - hb >= 64) {  // slide the run window (every 64 runs)
+                        hb += 64;
+                        hw0 = hw1;
+                        hw1 = Ul[min(hb + 64 + lane, n_runs)];
+                    }
+                    const int32_t item = live ? run_hdr(rr, false) : -1;
+                    const int32_t e = live ? run_hdr(rr + 1, true) : j;
+                    run(ring[s], item, e, item_of(rr + RQ));
+                }
+            }
+            nr = s_end - s_begin;
+        } else {
+            // chunk c holds runs [c CH, c CH + CH) of the queue; lane l of a header window holds run c CH + l
+            // (the sentinel past the last run: item -1, first record n_rec -- an empty run)
+            const int32_t n_chunks = (n_runs + CH - 1) / CH;
+            auto hdr = [&](int32_t c) { return Ul[min(c * CH + lane, n_runs)]; };
+            auto hx = [](const int2& h, int i) { return __builtin_amdgcn_readlane(h.x, i); };
+            auto hy = [](const int2& h, int i) { return __builtin_amdgcn_readlane(h.y, i); };
+            int32_t cn = w, claim = 0;
+            int2 hn = hdr(cn);
+            int2 rwn = Rl[min(hy(hn, 0) + lane, n_rec - 1)];  // the next chunk's first record window
+            prefill([&](int s) { return hx(hn, s); });
+            while (true) {
+                const int32_t cc = cn;
+                const int2 hc = hn;
+                if (cc >= n_chunks) break;
+                rb = j = hy(hc, 0);
+                rw0 = rwn;
+                rw1 = Rl[min(rb + 64 + lane, n_rec - 1)];
+                nr += hy(hc, CH) - j;
+                if (lane == 0) claim = atomicAdd(&s_claim, 1);  // the chunk after this one
+#pragma unroll
+                for (int p0 = 0; p0 < CH; p0 += RQ) {
+#pragma unroll
+                    for (int s = 0; s < RQ; ++s) {
+                        const int p = p0 + s;
+                        const int32_t nxt = p + RQ < CH ? hx(hc, p + RQ) : hx(hn, p + RQ - CH);
+                        run(ring[s], hx(hc, p), hy(hc, p + 1), nxt);
+                        if (p == 0) {  // the claim has landed behind this run's LDS traffic
+                            cn = __builtin_amdgcn_readfirstlane(claim);
+                            hn = hdr(cn);
+                        } else if (p == 1) {
+                            rwn = Rl[min(hy(hn, 0) + lane, n_rec - 1)];
+                        }
+                    }
                 }
             }
         }
-        const int32_t nr = s_end - s_begin;
         if constexpr (TIMED) tm_c = clk();
         contrib += static_cast<double>(nr) * (gb - gb0);
         __syncthreads();
@@ -363,6 +430,7 @@ size_t tile_bytes(int64_t users, int64_t recs, int64_t runs, int32_t ld) {  // l
 // do not fit one tile's LDS is cut into near-equal pieces (count-weighted merge after the epoch).
 void build_tile_host(const rs_svd_plan* pl, int32_t u_begin, int32_t u_end, int32_t nw, int64_t target,
                      int32_t run_cap, bool want_pos, TileHost& th) {
+    const bool claim = pl->tile_claim > 0;  // one run queue per tile, claimed by the waves
     const std::vector<int64_t>& rp = pl->h_rowptr;
     const int32_t ld = pl->tile_user_lds > 0 ? pl->tile_user_lds
                                              : 64 * ((pl->k + 2 + 63) / 64);  // LDS per user: k factors + two bias columns
@@ -583,8 +651,37 @@ void build_tile_host(const rs_svd_plan* pl, int32_t u_begin, int32_t u_end, int3
         for (int32_t it : ditem) slot[it] = -1;
         // runs in key order; with run_cap (and more than one wave) an item's records are cut into
         // pieces that go to different waves (two pieces in one wave's ring reach would read q_i
-        // before the earlier piece's atomic landed).  Dealt to the least-loaded stream (cost ~
-        // ratings + a run start); the pieces of one item take distinct streams.
+        // before the earlier piece's atomic landed).
+        if (claim) {
+            // Claimed runs: one queue.  Piece pc of an item of `pieces` sits at queue position
+            // (pc + key / 2^32) / pieces, so an item's pieces are n_runs / pieces apart (the waves take
+            // them at different times, far outside one wave's ring reach) and single runs keep their
+            // pseudo-random key order.
+            struct QE { uint64_t at; int32_t sl, pc, pieces; };
+            std::vector<QE> qv;
+            qv.reserve(nd);
+            for (size_t d = 0; d < nd; ++d) {
+                const int32_t sl = static_cast<int32_t>(ord[d]);
+                const size_t c = static_cast<size_t>(dcnt[sl]);
+                const int32_t pieces = static_cast<int32_t>(cap ? std::min<size_t>((c + cap - 1) / cap, static_cast<size_t>(nw)) : 1);
+                for (int32_t pc = 0; pc < pieces; ++pc)
+                    qv.push_back({((static_cast<uint64_t>(pc) << 32) + key[sl]) / static_cast<uint64_t>(pieces), sl, pc, pieces});
+            }
+            std::stable_sort(qv.begin(), qv.end(), [](const QE& x, const QE& y) { return x.at < y.at; });
+            int32_t rec = 0;
+            for (const QE& e : qv) {
+                const int64_t c = dcnt[e.sl];
+                L.runs.push_back(make_int2(ditem[e.sl], rec));
+                L.rb.push_back(off[e.sl] + static_cast<int32_t>(c * e.pc / e.pieces));
+                rec += static_cast<int32_t>(c * (e.pc + 1) / e.pieces - c * e.pc / e.pieces);
+            }
+            L.st.assign(nw + 1, static_cast<int32_t>(L.runs.size()));
+            L.st[0] = 0;
+            L.runs.push_back(make_int2(-1, rec));  // sentinel
+            return;
+        }
+        // Static deal: to the least-loaded stream (cost ~ ratings + a run start); the pieces of one item
+        // take distinct streams.
         std::vector<int64_t> load(nw, 0);
         std::vector<std::vector<std::pair<int32_t, int32_t>>> sr(nw);  // per stream: (slot, piece)
         std::vector<uint8_t> used(nw, 0);
@@ -736,10 +833,92 @@ namespace {
 
 // User blocks: tile_ublocks consecutive user ranges of near-equal ratings, tiled one after the other
 // (block b's tiles are [block_tile[b], block_tile[b+1])).  One block: the plain tile schedule.
+void append_tiles(TileHost& th, TileHost&& part, bool first) {
+    if (first) {
+        th = std::move(part);
+        return;
+    }
+    const int32_t e0 = static_cast<int32_t>(th.users.size());
+    const int64_t r0 = static_cast<int64_t>(th.runs.size()), c0 = static_cast<int64_t>(th.recs.size());
+    if (r0 + static_cast<int64_t>(part.runs.size()) >= (int64_t{1} << 31) ||
+        c0 + static_cast<int64_t>(part.recs.size()) >= (int64_t{1} << 31))
+        throw std::invalid_argument("tile schedule: more than 2^31 runs or ratings");
+    for (int4 t : part.tiles)
+        th.tiles.push_back(make_int4(t.x + e0, t.y, t.z + static_cast<int32_t>(r0), t.w + static_cast<int32_t>(c0)));
+    th.users.insert(th.users.end(), part.users.begin(), part.users.end());
+    th.streams.insert(th.streams.end(), part.streams.begin(), part.streams.end());
+    th.runs.insert(th.runs.end(), part.runs.begin(), part.runs.end());
+    th.recs.insert(th.recs.end(), part.recs.begin(), part.recs.end());
+    th.pos.insert(th.pos.end(), part.pos.begin(), part.pos.end());
+    th.split.insert(th.split.end(), part.split.begin(), part.split.end());
+    th.lds = std::max(th.lds, part.lds);
+}
+
+// Strata (RS_EXCHANGE_ROTATE_Q): block b = this plan's ratings of items [ib[b], ib[b+1]) over all its users,
+// tiled like a plan of its own (the item ids stay global: the kernel addresses the plan's whole Q).  Each
+// block's user-CSR is filtered out of the plan's on pooled threads; positions map back to the plan's CSR.
+void build_tile_strata(const rs_svd_plan* pl, int32_t grid0, bool want_pos, TileHost& th,
+                       std::vector<int32_t>& block_tile, std::vector<int32_t>* block_split) {
+    const std::vector<int32_t>& ib = pl->iblock_bounds;
+    const int32_t nb = static_cast<int32_t>(ib.size()) - 1, nu = pl->n_users;
+    std::vector<int32_t> blk(static_cast<size_t>(std::max(1, pl->n_items)), 0);
+    for (int32_t b = 0; b < nb; ++b)
+        for (int32_t x = ib[b]; x < ib[b + 1]; ++x) blk[x] = b;
+    block_tile.assign(1, 0);
+    if (block_split) block_split->assign(1, 0);
+    const std::vector<int64_t>& rp = pl->h_rowptr;
+    for (int32_t b = 0; b < nb; ++b) {
+        rs_svd_plan sub;
+        sub.n_users = nu;
+        sub.n_items = pl->n_items;
+        sub.k = pl->k;
+        sub.tile_waves = pl->tile_waves;
+        sub.tile_claim = pl->tile_claim;
+        sub.tile_user_lds = pl->tile_user_lds;
+        sub.tile_target = pl->tile_target;
+        sub.h_rowptr.assign(static_cast<size_t>(nu) + 1, 0);
+        parallel_ranges(nu, 16, [&](int64_t u0, int64_t u1) {
+            for (int64_t u = u0; u < u1; ++u) {
+                int64_t c = 0;
+                for (int64_t q = rp[u]; q < rp[u + 1]; ++q) c += blk[pl->h_cols[q]] == b;
+                sub.h_rowptr[u + 1] = c;
+            }
+        });
+        for (int32_t u = 0; u < nu; ++u) sub.h_rowptr[u + 1] += sub.h_rowptr[u];
+        sub.nnz = sub.h_rowptr[nu];
+        sub.h_cols.resize(static_cast<size_t>(sub.nnz));
+        sub.h_vals.resize(static_cast<size_t>(sub.nnz));
+        std::vector<int64_t> orig(want_pos ? static_cast<size_t>(sub.nnz) : 0);
+        parallel_ranges(nu, 16, [&](int64_t u0, int64_t u1) {
+            for (int64_t u = u0; u < u1; ++u) {
+                int64_t o = sub.h_rowptr[u];
+                for (int64_t q = rp[u]; q < rp[u + 1]; ++q)
+                    if (blk[pl->h_cols[q]] == b) {
+                        sub.h_cols[o] = pl->h_cols[q];
+                        sub.h_vals[o] = pl->h_vals[q];
+                        if (want_pos) orig[o] = q;
+                        ++o;
+                    }
+            }
+        });
+        const int32_t cap = pl->tile_run_cap > 0 ? pl->tile_run_cap : auto_run_cap(&sub, grid0, pl->tile_waves);
+        TileHost part;
+        build_tile_host(&sub, 0, nu, pl->tile_waves, tile_target_of(&sub, grid0, 0, nu), cap, want_pos, part);
+        for (int64_t& x : part.pos) x = orig[x];
+        append_tiles(th, std::move(part), b == 0);
+        block_tile.push_back(static_cast<int32_t>(th.tiles.size()));
+        if (block_split) block_split->push_back(static_cast<int32_t>(th.split.size()));
+    }
+}
+
 void build_tile_blocks(const rs_svd_plan* pl, int32_t grid0, bool want_pos, TileHost& th,
                        std::vector<int32_t>& block_tile, std::vector<int32_t>& block_user,
                        std::vector<int32_t>* block_split = nullptr) {
     const std::vector<int64_t>& rp = pl->h_rowptr;
+    if (!pl->iblock_bounds.empty()) {  // strata of a Q-rotation shard
+        block_user = {0, pl->n_users};
+        return build_tile_strata(pl, grid0, want_pos, th, block_tile, block_split);
+    }
     if (!pl->ublock_bounds.empty()) {  // common bounds of the shards of a multi-GPU fit
         block_user = pl->ublock_bounds;
     } else {
@@ -754,24 +933,7 @@ void build_tile_blocks(const rs_svd_plan* pl, int32_t grid0, bool want_pos, Tile
         const int32_t u0 = block_user[b], u1 = block_user[b + 1];
         TileHost part;
         build_tile_host(pl, u0, u1, pl->tile_waves, tile_target_of(pl, grid0, u0, u1), cap, want_pos, part);
-        if (b == 0) {
-            th = std::move(part);
-        } else {
-            const int32_t e0 = static_cast<int32_t>(th.users.size());
-            const int64_t r0 = static_cast<int64_t>(th.runs.size()), c0 = static_cast<int64_t>(th.recs.size());
-            if (r0 + static_cast<int64_t>(part.runs.size()) >= (int64_t{1} << 31) ||
-                c0 + static_cast<int64_t>(part.recs.size()) >= (int64_t{1} << 31))
-                throw std::invalid_argument("tile schedule: more than 2^31 runs or ratings");
-            for (int4 t : part.tiles)
-                th.tiles.push_back(make_int4(t.x + e0, t.y, t.z + static_cast<int32_t>(r0), t.w + static_cast<int32_t>(c0)));
-            th.users.insert(th.users.end(), part.users.begin(), part.users.end());
-            th.streams.insert(th.streams.end(), part.streams.begin(), part.streams.end());
-            th.runs.insert(th.runs.end(), part.runs.begin(), part.runs.end());
-            th.recs.insert(th.recs.end(), part.recs.begin(), part.recs.end());
-            th.pos.insert(th.pos.end(), part.pos.begin(), part.pos.end());
-            th.split.insert(th.split.end(), part.split.begin(), part.split.end());
-            th.lds = std::max(th.lds, part.lds);
-        }
+        append_tiles(th, std::move(part), b == 0);
         block_tile.push_back(static_cast<int32_t>(th.tiles.size()));
         if (block_split) block_split->push_back(static_cast<int32_t>(th.split.size()));  // users ascend by block
     }
@@ -856,9 +1018,9 @@ struct TileRange {  // tiles [t0, t1) into dP rows of stride ldd (delta mode), g
     int32_t t0, t1, ldd, grid;
 };
 
-template <int E, int NW, int RQ, int DIAG = 0>
+template <int E, int NW, int RQ, int CH, int DIAG = 0>
 static void tile_launch_t(rs_svd_plan* pl, float lr, float reg, hipStream_t s, float* dP, const TileRange& tr) {
-    auto kern = svd_epoch_tile_kernel<E, NW, RQ, DIAG>;
+    auto kern = svd_epoch_tile_kernel<E, NW, RQ, CH, DIAG>;
     static bool attr = false;  // per instantiation
     if (!attr) {
         RS_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(kern),
@@ -874,44 +1036,52 @@ static void tile_launch_t(rs_svd_plan* pl, float lr, float reg, hipStream_t s, f
 
 // q_i rows in flight per wave (runs ahead): the ring's loads and the runs' atomics share the wave's
 // in-order vmcnt, so a slot's load also waits for every atomic issued before it; the deeper the ring,
-// the longer an atomic has to complete before a load behind it is needed
+// the longer an atomic has to complete before a load behind it is needed.  Claimed runs (the default,
+// pl->tile_claim > 0) take rings of 2 or 3 and chunks of 4 or 8 runs.
 template <int E, int NW>
 static void tile_launch_r(rs_svd_plan* pl, float lr, float reg, hipStream_t s, float* dP, const TileRange& tr) {
     constexpr int kMax = 60 / (2 * E);  // 15 at E = 2 (k <= 127), 6 at E = 5 (k <= 319), 3 at E = 8
     const int want = pl->tile_ring > 0 ? pl->tile_ring : 2;
+    const bool claim = pl->tile_claim > 0;
     if constexpr (E == 2 && NW == 16) {  // diagnostics (RSGPU_TILE_DIAG, experiments only): bits drop
         static const int diag = std::getenv("RSGPU_TILE_DIAG") ? std::atoi(std::getenv("RSGPU_TILE_DIAG")) : 0;
-        switch (diag) {  // 1 q atomics, 2 q loads, 4 p LDS atomics, 8 p LDS reads
-            case 1: return tile_launch_t<E, NW, 4, 1>(pl, lr, reg, s, dP, tr);
-            case 2: return tile_launch_t<E, NW, 4, 2>(pl, lr, reg, s, dP, tr);
-            case 3: return tile_launch_t<E, NW, 4, 3>(pl, lr, reg, s, dP, tr);
-            case 4: return tile_launch_t<E, NW, 4, 4>(pl, lr, reg, s, dP, tr);
-            case 12: return tile_launch_t<E, NW, 4, 12>(pl, lr, reg, s, dP, tr);
-            case 15: return tile_launch_t<E, NW, 4, 15>(pl, lr, reg, s, dP, tr);
-            case 16:
-                if (pl->trace.n < static_cast<size_t>(pl->tile_grid) * NW * 4) {
-                    pl->trace.alloc(static_cast<size_t>(pl->tile_grid) * NW * 4);
-                    RS_HIP(hipMemsetAsync(pl->trace.p, 0, pl->trace.n * 8, s));
-                }
-                return tile_launch_t<E, NW, 4, 16>(pl, lr, reg, s, dP, tr);
+        if (diag == 16 && pl->trace.n < static_cast<size_t>(pl->tile_grid) * NW * 4) {
+            pl->trace.alloc(static_cast<size_t>(pl->tile_grid) * NW * 4);
+            RS_HIP(hipMemsetAsync(pl->trace.p, 0, pl->trace.n * 8, s));
+        }
+        switch (diag * (claim ? -1 : 1)) {  // 1 q atomics, 2 q loads, 4 p LDS atomics, 8 p LDS reads, 16 clocks
+            case 1: return tile_launch_t<E, NW, 4, 0, 1>(pl, lr, reg, s, dP, tr);
+            case 2: return tile_launch_t<E, NW, 4, 0, 2>(pl, lr, reg, s, dP, tr);
+            case 3: return tile_launch_t<E, NW, 4, 0, 3>(pl, lr, reg, s, dP, tr);
+            case 4: return tile_launch_t<E, NW, 4, 0, 4>(pl, lr, reg, s, dP, tr);
+            case 16: return tile_launch_t<E, NW, 4, 0, 16>(pl, lr, reg, s, dP, tr);
+            case -1: return tile_launch_t<E, NW, 2, 4, 1>(pl, lr, reg, s, dP, tr);
+            case -3: return tile_launch_t<E, NW, 2, 4, 3>(pl, lr, reg, s, dP, tr);
+            case -16: return tile_launch_t<E, NW, 2, 4, 16>(pl, lr, reg, s, dP, tr);
             default: break;
         }
     }
+    if (claim) {
+        const bool big = pl->tile_claim >= 8;
+        if (want <= 2) return big ? tile_launch_t<E, NW, 2, 8>(pl, lr, reg, s, dP, tr)
+                                  : tile_launch_t<E, NW, 2, 4>(pl, lr, reg, s, dP, tr);
+        return big ? tile_launch_t<E, NW, 3, 8>(pl, lr, reg, s, dP, tr) : tile_launch_t<E, NW, 3, 4>(pl, lr, reg, s, dP, tr);
+    }
     if constexpr (kMax >= 12) {
-        if (want >= 12) return tile_launch_t<E, NW, 12>(pl, lr, reg, s, dP, tr);
+        if (want >= 12) return tile_launch_t<E, NW, 12, 0>(pl, lr, reg, s, dP, tr);
     }
     if constexpr (kMax >= 8) {
-        if (want >= 8) return tile_launch_t<E, NW, 8>(pl, lr, reg, s, dP, tr);
+        if (want >= 8) return tile_launch_t<E, NW, 8, 0>(pl, lr, reg, s, dP, tr);
     }
     if constexpr (kMax >= 6) {
-        if (want >= 6) return tile_launch_t<E, NW, 6>(pl, lr, reg, s, dP, tr);
+        if (want >= 6) return tile_launch_t<E, NW, 6, 0>(pl, lr, reg, s, dP, tr);
     }
-    if (want <= 2) return tile_launch_t<E, NW, 2>(pl, lr, reg, s, dP, tr);
-    if (want == 3) return tile_launch_t<E, NW, 3>(pl, lr, reg, s, dP, tr);
+    if (want <= 2) return tile_launch_t<E, NW, 2, 0>(pl, lr, reg, s, dP, tr);
+    if (want == 3) return tile_launch_t<E, NW, 3, 0>(pl, lr, reg, s, dP, tr);
     if constexpr (kMax >= 4) {
-        return tile_launch_t<E, NW, 4>(pl, lr, reg, s, dP, tr);
+        return tile_launch_t<E, NW, 4, 0>(pl, lr, reg, s, dP, tr);
     } else {
-        return tile_launch_t<E, NW, kMax>(pl, lr, reg, s, dP, tr);
+        return tile_launch_t<E, NW, kMax, 0>(pl, lr, reg, s, dP, tr);
     }
 }
 

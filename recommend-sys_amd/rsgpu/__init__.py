@@ -22,7 +22,7 @@ SGD_FAST, SGD_ORDERED = 0, 1
 WB_TILE, WB_STORE, WB_ATOMIC_DIRECT, WB_ATOMIC = 0, 1, 2, 3  # WB_TILE: the default schedule
 SIM_COSINE, SIM_MSD, SIM_PEARSON = 0, 1, 2
 DEV_SLOPE_ONE = 3  # rs_knn_sims kind: SlopeOne deviation matrix (slope_one.go:64-92)
-EXCHANGE_ROTATE, EXCHANGE_AVERAGE = 0, 1  # multi-GPU exchange of the item-sharded fit (rsgpu.h)
+EXCHANGE_ROTATE, EXCHANGE_AVERAGE, EXCHANGE_ROTATE_Q = 0, 1, 2  # multi-GPU exchange of the sharded fit (rsgpu.h)
 
 HEADER_SYMBOLS = (
     "rs_version", "rs_device_count", "rs_open", "rs_close", "rs_last_error", "rs_synchronize",
@@ -40,11 +40,11 @@ HEADER_SYMBOLS = (
     "rs_synth_create", "rs_synth_csr", "rs_synth_destroy",
     "rs_svd_plan_set_item_weights", "rs_svd_plan_epoch_qdelta", "rs_svd_plan_apply_qdelta",
     "rs_svd_plan_set_hot_replicas", "rs_svd_plan_set_fixed_q", "rs_svd_plan_set_tiles",
-    "rs_svd_plan_tile_order", "rs_svd_plan_tile_clocks",
+    "rs_svd_plan_set_tile_claim", "rs_svd_plan_tile_order", "rs_svd_plan_tile_clocks",
     "rs_comm_unique_id", "rs_svd_plan_join", "rs_svd_plan_epochs_sharded", "rs_svd_plan_leave",
     "rs_svd_plan_set_user_blocks", "rs_svd_group_create", "rs_svd_group_epochs", "rs_svd_group_destroy",
     "rs_item_shards", "rs_svd_fit_multi", "rs_tile_schedule_host", "rs_svd_plan_set_exchange",
-    "rs_comm_info", "rs_rotation_step", "rs_svd_plan_shard_info",
+    "rs_comm_info", "rs_rotation_step", "rs_svd_plan_shard_info", "rs_svd_plan_inject_fault",
 )
 COMM_ID_BYTES = 128
 
@@ -141,6 +141,7 @@ def lib():
             "rs_svd_plan_set_hot_replicas": (C.c_int, [_vp, _i32, _i32]),
             "rs_svd_plan_set_fixed_q": (C.c_int, [_vp, _i32]),
             "rs_svd_plan_set_tiles": (C.c_int, [_vp, _i32, _i32, _i32, _i32, _i32]),
+            "rs_svd_plan_set_tile_claim": (C.c_int, [_vp, _i32]),
             "rs_svd_plan_tile_order": (C.c_int, [_vp, _vp, _vp, C.POINTER(_i32)]),
             "rs_svd_plan_tile_clocks": (C.c_int, [_vp, _vp, _i64]),
             "rs_svd_plan_epoch_qdelta": (C.c_int, [_vp, _flt, _flt, _vp, _vp, _vp]),
@@ -162,6 +163,7 @@ def lib():
             "rs_svd_fit_multi": (C.c_int, [_vp, _i32, C.POINTER(_Ratings), C.POINTER(_SgdParams), _i32,
                                            _vp, _vp, _vp, _vp, _vp]),
             "rs_svd_plan_set_exchange": (C.c_int, [_vp, _i32]),
+            "rs_svd_plan_inject_fault": (C.c_int, [_vp, _i32]),
             "rs_comm_info": (C.c_int, [C.POINTER(_i32), _vp, _i32]),
             "rs_rotation_step": (C.c_int, [_i32, _i32, _i32, _vp]),
             "rs_svd_plan_shard_info": (C.c_int, [_vp, C.POINTER(_i32), C.POINTER(_i32), C.POINTER(_i32),
@@ -459,6 +461,10 @@ class SvdPlan:
         """Multi-GPU exchange a later join / group sets up (rs_svd_plan_set_exchange)."""
         self.ctx.check(lib().rs_svd_plan_set_exchange(self.h, mode))
 
+    def inject_fault(self, sub_epoch):
+        """Test hook: the next sharded call throws at that sub-epoch, once (rs_svd_plan_inject_fault)."""
+        self.ctx.check(lib().rs_svd_plan_inject_fault(self.h, sub_epoch))
+
     def join(self, comm_id: bytes, rank: int, n_ranks: int, n_blocks: int = 0):
         """Item-sharded multi-GPU (rs_svd_plan_join; collective over the ranks): comm_id from
         comm_unique_id() on rank 0, sent to every rank."""
@@ -481,6 +487,11 @@ class SvdPlan:
     def set_tiles(self, workgroups=0, waves=16, target=0, run_cap=0, ring=0):
         """WB_TILE schedule parameters (rs_svd_plan_set_tiles); rebuilds the tiles."""
         self.ctx.check(lib().rs_svd_plan_set_tiles(self.h, workgroups, waves, target, run_cap, ring))
+
+    def set_tile_claim(self, runs_per_claim=4):
+        """Runs per claim from a tile's run queue (4, 8), or 0: runs dealt on the host
+        (rs_svd_plan_set_tile_claim); rebuilds the tiles."""
+        self.ctx.check(lib().rs_svd_plan_set_tile_claim(self.h, runs_per_claim))
 
     def tile_order(self):
         """(pos, work_off): user-CSR positions in the tile schedule's visit order and the boundaries

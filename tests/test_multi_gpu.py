@@ -122,6 +122,98 @@ def test_rotation_one_wave_equals_oracle(ctx, ml100k, n_shards, pieces):
         assert np.array_equal(b[0][0], y[0]) and np.array_equal(b[0][2], y[2]) and b[0][4] == y[4]
 
 
+def _block_bounds(keys, n, blocks):
+    """The library's block bounds over rows counted by `keys` (user_block_bounds): the b-th bound is the
+    first row whose ratings start at or past b/blocks of them."""
+    cum = np.concatenate([[0], np.cumsum(np.bincount(keys, minlength=n))])
+    return np.array([np.searchsorted(cum, cum[-1] * b // blocks, side="left") for b in range(blocks)] + [n])
+
+
+def _user_shards(u, i, r, nu, n):
+    """ROTATE_Q shards: the ratings of contiguous user ranges of near-equal ratings, global ids."""
+    b = _block_bounds(u, nu, n)
+    return [(u[(u >= b[s]) & (u < b[s + 1])], i[(u >= b[s]) & (u < b[s + 1])], r[(u >= b[s]) & (u < b[s + 1])])
+            for s in range(n)]
+
+
+@pytest.mark.parametrize("n_shards,pieces", [(2, 1), (2, 2), (3, 1), (4, 2), (8, 1)])
+def test_rotation_q_one_wave_equals_oracle(ctx, ml100k, n_shards, pieces):
+    """ROTATE_Q (user ranges stay, item rank-blocks rotate) through the in-process exchange, one wave per
+    shard: equal to the sequential SGD over the strata in rotation order -- sub-epoch s, shard g, item
+    blocks of rank-block (g + s) mod N, each stratum's tiles in the exported order -- (1e-5), and P, Q,
+    the biases and GlobalBias bitwise identical on every shard after the call (the final broadcast)."""
+    f = folds(*ml100k)[2]
+    n = 30000
+    u, i, r, nu, ni = f.iu[:n], f.ii[:n], f.r[:n], f.nu, f.ni
+    k = 24
+    rng = np.random.default_rng(50 + n_shards + 10 * pieces)
+    P0, Q0 = rng.normal(0, 0.1, (nu, k)), rng.normal(0, 0.1, (ni, k))
+    sh = _user_shards(u, i, r, nu, n_shards)
+    blocks = n_shards * pieces
+    ib = _block_bounds(i, ni, blocks)
+    plans = []
+    for su, si, sr in sh:
+        pl = ctx.svd_plan(rsgpu.Ratings(su, si, sr, nu, ni), k)
+        pl.set_tiles(workgroups=1, waves=1)
+        pl.set_exchange(rsgpu.EXCHANGE_ROTATE_Q)
+        pl.upload(P0, Q0, np.zeros(nu), np.zeros(ni), 3.5)
+        plans.append(pl)
+    g = rsgpu.SvdGroup(plans, n_blocks=blocks)
+    assert all(pl.shard_info()[2:] == (rsgpu.EXCHANGE_ROTATE_Q, blocks) for pl in plans)
+    g.epochs(2)
+    strata = {}  # (shard, item block) -> works
+    for gi, (pl, (su, si, sr)) in enumerate(zip(plans, sh)):
+        rowptr, items, rr = O.csr_by(su, nu, si, sr)
+        cu = np.repeat(np.arange(nu, dtype=np.int32), np.diff(rowptr))
+        pos, off = pl.tile_order()
+        assert np.array_equal(np.sort(pos), np.arange(len(sr)))
+        uu, ii, r_ = cu[pos], np.asarray(items, np.int32)[pos], np.asarray(rr)[pos]
+        for w in range(len(off) - 1):
+            if off[w + 1] > off[w]:
+                b = int(np.searchsorted(ib, ii[off[w]], side="right") - 1)
+                assert np.all((ii[off[w]:off[w + 1]] >= ib[b]) & (ii[off[w]:off[w + 1]] < ib[b + 1]))
+                strata.setdefault((gi, b), []).append((off[w], off[w + 1], uu, ii, r_))
+    U, I, R, W = [], [], [], [0]
+    for st in range(n_shards):
+        for gi in range(n_shards):
+            for j in range(pieces):
+                for a, z, uu, ii, r_ in strata.get((gi, ((gi + st) % n_shards) * pieces + j), []):
+                    U.append(uu[a:z])
+                    I.append(ii[a:z])
+                    R.append(r_[a:z])
+                    W.append(W[-1] + (z - a))
+    ref = O.svd_fit_works(np.concatenate(U), np.concatenate(I), np.concatenate(R), np.array(W, np.int64), P0, Q0,
+                          np.zeros(nu), np.zeros(ni), 3.5, epochs=2)
+    g.close()
+    b = [pl.download() for pl in plans]
+    for pl in plans:
+        pl.close()
+    assert _maxdiff(ref[:4], b[0][:4]) <= TOL and abs(ref[4] - b[0][4]) <= TOL
+    for y in b[1:]:
+        assert all(np.array_equal(b[0][x], y[x]) for x in range(4)) and b[0][4] == y[4]
+
+
+def test_rotation_fewer_users_than_blocks(ctx):
+    """ROTATE with more user blocks than users (4 shards x 2 pieces, 5 users): empty blocks send and
+    receive nothing and the fit still equals a single plan's users trained (finite, every rating seen)."""
+    rng = np.random.default_rng(4)
+    nu, ni, k = 5, 40, 8
+    u = rng.integers(0, nu, 300).astype(np.int32)
+    i = rng.integers(0, ni, 300).astype(np.int32)
+    r = rng.integers(1, 6, 300).astype(float)
+    P0, Q0 = rng.normal(0, 0.1, (nu, k)), rng.normal(0, 0.1, (ni, k))
+    sh = _shards(u, i, r, nu, ni, 4)
+    plans = _plans(ctx, sh, k, P0, Q0, 8)
+    g = rsgpu.SvdGroup(plans, n_blocks=8)
+    g.epochs(3)
+    g.close()
+    b = [pl.download() for pl in plans]
+    for pl in plans:
+        pl.close()
+    assert all(np.all(np.isfinite(x)) for y in b for x in y[:4])
+    assert not np.array_equal(b[0][0], P0)
+
+
 @pytest.mark.parametrize("api", ["group", "join"])
 def test_rccl_single_rank_rotation_equals_oracle(ctx, ml100k, api):
     """The RCCL exchange (communicator, comm stream, events, GlobalBias fold) with one rank: the
@@ -150,8 +242,8 @@ def test_rccl_single_rank_rotation_equals_oracle(ctx, ml100k, api):
 
 
 def test_rotation_shard_failure_releases_the_others(ctx, ml100k):
-    """A shard that throws mid-epoch (test hook RSGPU_FAULT_SHARD) makes rs_svd_group_epochs return its
-    error instead of leaving the other shards blocked at the exchange."""
+    """A shard that throws mid-epoch (test hook rs_svd_plan_inject_fault) makes rs_svd_group_epochs return
+    its error instead of leaving the other shards blocked at the exchange."""
     f = folds(*ml100k)[0]
     k = 16
     rng = np.random.default_rng(3)
@@ -159,12 +251,9 @@ def test_rotation_shard_failure_releases_the_others(ctx, ml100k):
     sh = _shards(f.iu, f.ii, f.r, f.nu, f.ni, 3)
     plans = _plans(ctx, sh, k, P0, Q0, 3)
     g = rsgpu.SvdGroup(plans, n_blocks=3)
-    os.environ["RSGPU_FAULT_SHARD"] = "1"
-    try:
-        with pytest.raises(rsgpu.RsError) as e:
-            g.epochs(1)
-    finally:
-        del os.environ["RSGPU_FAULT_SHARD"]
+    plans[1].inject_fault(2)  # the last sub-epoch
+    with pytest.raises(rsgpu.RsError) as e:
+        g.epochs(1)
     assert "shard 1" in str(e.value) or "another shard" in str(e.value)
     g.close()
     for pl in plans:
