@@ -385,6 +385,11 @@ int rs_svd_plan_apply_delta(rs_svd_plan* plan, const void* dP, const void* gbsum
  * pieces of ~64 MiB of Q per rank-block).  rs_svd_fit_multi picks it when n_items < n_users. */
 #define RS_EXCHANGE_ROTATE_Q 2
 int rs_svd_plan_set_exchange(rs_svd_plan* plan, int32_t mode);
+/* Diagnostic: one epoch of the plan with each user block / stratum of its tile schedule (a joined plan's,
+ * or rs_svd_plan_set_user_blocks') launched alone and timed -- ms[b] = block b's SGD kernel in
+ * milliseconds (n >= the plan's blocks).  It trains the model like an epoch.  Used to table the
+ * per-stratum times the sub-epochs of a sharded run wait on (DESIGN.md Multi-GPU). */
+int rs_svd_plan_time_blocks(rs_svd_plan* plan, float lr, float reg, double* ms, int32_t n);
 /* Test hook (fault injection): the next rs_svd_plan_epochs_sharded / rs_svd_group_epochs call on this
  * plan throws at the start of its sub-epoch `sub_epoch` (once), so tests can check that the other ranks
  * are released.  -1 clears it.  Nothing else reads it. */

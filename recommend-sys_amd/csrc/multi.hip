@@ -711,6 +711,7 @@ extern "C" int rs_svd_plan_set_user_blocks(rs_svd_plan* pl, int32_t n_blocks, co
         pl->tile_ublocks = n_blocks;
         if (bounds) pl->ublock_bounds.assign(bounds, bounds + n_blocks + 1);
         else pl->ublock_bounds.clear();
+        pl->iblock_bounds.clear();  // a ROTATE_Q group's strata end here too
         if (pl->write_back == RS_SGD_WB_TILE) {
             rs::tile_build(pl);
             pl->n_blocks = rs::tile_partials(pl);
@@ -728,6 +729,44 @@ extern "C" int rs_svd_plan_set_exchange(rs_svd_plan* pl, int32_t mode) {
     if (pl->shard) return rs::set_error(pl->ctx, RS_ERR_INVALID, "plan is joined to a group (leave first)");
     pl->exchange = mode;
     return RS_OK;
+}
+
+// Diagnostic (DESIGN.md Multi-GPU, configs[4]): one epoch of this plan with each user block / stratum of its
+// tile schedule launched on its own and timed (HIP events on the ctx stream) -- the per-stratum kernel
+// times a sharded run's sub-epochs wait on.  Trains the model like an epoch (blocks in order).
+extern "C" int rs_svd_plan_time_blocks(rs_svd_plan* pl, float lr, float reg, double* ms, int32_t n) {
+    if (!pl || !ms || n < 0) return rs::set_error(pl ? pl->ctx : nullptr, RS_ERR_INVALID, "bad arguments");
+    return rs_guard(pl->ctx, [&]() -> int {
+        if (pl->write_back != RS_SGD_WB_TILE) return rs::set_error(pl->ctx, RS_ERR_UNSUPPORTED, "tile schedule only");
+        rs::plan_sync_last(pl);
+        if (!pl->tiles_built) rs::tile_build(pl);
+        const int32_t nb = static_cast<int32_t>(pl->t_block_tile.size()) - 1;
+        if (n < nb) return rs::set_error(pl->ctx, RS_ERR_INVALID, "ms holds fewer entries than the plan's blocks");
+        hipStream_t s = pl->ctx->stream;
+        std::vector<hipEvent_t> ev(2 * static_cast<size_t>(nb), nullptr);
+        for (hipEvent_t& e : ev) RS_HIP(hipEventCreate(&e));
+        rs::DevBuf<double> gbs(static_cast<size_t>(std::max(1, nb)));
+        rs::q_convert(pl, s, 1);
+        for (int32_t b = 0; b < nb; ++b) {
+            RS_HIP(hipEventRecord(ev[2 * b], s));
+            const int32_t parts = rs::tile_launch_range(pl, lr, reg, s, nullptr, 0, pl->t_block_tile[b], pl->t_block_tile[b + 1]);
+            RS_HIP(hipEventRecord(ev[2 * b + 1], s));
+            rs::merge_tile_split_rows(pl, pl->t_block_split[b], pl->t_block_split[b + 1], s);
+            rs::gb_sum(pl->partial.p, parts, gbs.p + b, s);
+        }
+        hipLaunchKernelGGL(rs::gb_fold_blocks_kernel, dim3(1), dim3(64), 0, s, pl->gb.p, gbs.p, nb,
+                           pl->nnz > 0 ? 1.0 / static_cast<double>(pl->nnz) : 0.0);
+        RS_HIP(hipGetLastError());
+        rs::q_convert(pl, s, 0);
+        RS_HIP(hipStreamSynchronize(s));
+        for (int32_t b = 0; b < nb; ++b) {
+            float t = 0.f;
+            RS_HIP(hipEventElapsedTime(&t, ev[2 * b], ev[2 * b + 1]));
+            ms[b] = t;
+        }
+        for (hipEvent_t e : ev) (void)hipEventDestroy(e);
+        return RS_OK;
+    });
 }
 
 extern "C" int rs_svd_plan_inject_fault(rs_svd_plan* pl, int32_t sub_epoch) {

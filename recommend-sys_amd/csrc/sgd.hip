@@ -1481,6 +1481,23 @@ static void plan_download(rs_svd_plan* pl, double* P, double* Q, double* bu, dou
     }
 }
 
+// After a call's epochs: did the model leave the fixed-point range or go non-finite (the Q conversion's flag,
+// a non-finite GlobalBias)?  Waits for the stream; clears the flag when it is raised.
+static bool plan_diverged(rs_svd_plan* pl) {
+    plan_sync_last(pl);
+    hipStream_t s = pl->ctx->stream;
+    double g = 0.0;
+    pl->gb.download(&g, 1, s);
+    int32_t f = 0;
+    if (pl->numflag.p) pl->numflag.download(&f, 1, s);
+    RS_HIP(hipStreamSynchronize(s));
+    if (f) {
+        RS_HIP(hipMemsetAsync(pl->numflag.p, 0, sizeof(int32_t), s));
+        RS_HIP(hipStreamSynchronize(s));
+    }
+    return f != 0 || !std::isfinite(g);
+}
+
 static void plan_epochs(rs_svd_plan* pl, int32_t epochs, float lr, float reg, hipStream_t s) {
     const double inv_nnz = pl->nnz > 0 ? 1.0 / static_cast<double>(pl->nnz) : 0.0;
     if (pl->timing) {
@@ -2087,14 +2104,28 @@ extern "C" int rs_svd_fit(rs_ctx* ctx, const rs_ratings* r, const rs_sgd_params*
                 }
             }
             rs_svd_plan& pl = *cache->plan;
-            if (p->n_epochs > 0) *gb = rs::gb_warm_start(r, bu, bi);
-            mark("warm");
-            rs::plan_upload(&pl, P, Q, bu, bi, gb);
-            mark("upload");
-            rs::kernel_span_begin(ctx);
-            rs::plan_epochs(&pl, p->n_epochs, lr, reg, ctx->stream);
-            rs::kernel_span_end(ctx);
-            mark("epochs");
+            // Divergence guard (tile schedule): a fit that leaves the fixed-point range or goes non-finite is
+            // redone from the caller's inputs (still intact: nothing is written back before the check) with
+            // the run cap halved -- shorter runs of the hot items, less staleness -- up to
+            // three times; the plan keeps the lower cap for later fits of the same ratings.  Only then does
+            // the caller see RS_ERR_NUMERIC (a Go Fit that panics on an error never gets a NaN model first).
+            for (int attempt = 0;; ++attempt) {
+                if (p->n_epochs > 0) *gb = rs::gb_warm_start(r, bu, bi);
+                mark("warm");
+                rs::plan_upload(&pl, P, Q, bu, bi, gb);
+                mark("upload");
+                rs::kernel_span_begin(ctx);
+                rs::plan_epochs(&pl, p->n_epochs, lr, reg, ctx->stream);
+                rs::kernel_span_end(ctx);
+                mark("epochs");
+                if (wb != RS_SGD_WB_TILE || attempt == 3 || pl.tile_waves <= 1 || !rs::plan_diverged(&pl)) break;
+                const int32_t cap = rs::tile_cap_in_use(&pl);
+                if (cap <= 1) break;
+                pl.tile_run_cap = cap / 2;
+                rs::tile_build(&pl);
+                pl.n_blocks = rs::tile_partials(&pl);
+                if (trace) std::fprintf(stderr, "fit-trace diverged: refit with run cap %d\n", pl.tile_run_cap);
+            }
             rs::plan_download(&pl, P, Q, bu, bi, gb);
             mark("download");
             return RS_OK;

@@ -204,6 +204,7 @@ void tile_launch(rs_svd_plan* pl, float lr, float reg, hipStream_t s, float* dP)
 int32_t tile_launch_range(rs_svd_plan* pl, float lr, float reg, hipStream_t s, float* dP, int32_t ldd,
                           int32_t t0, int32_t t1);
 int32_t tile_partials(const rs_svd_plan* pl);  // GlobalBias partials the launch writes
+int32_t tile_cap_in_use(const rs_svd_plan* pl);  // the run cap the schedule is built with (uncut: the max degree)
 // visit order of the tile schedule (user-CSR positions, nnz entries) and its GlobalBias work items
 // (one per tile and wave: n_works + 1 offsets into pos); any pointer may be NULL
 void tile_order(rs_svd_plan* pl, int64_t* pos, int64_t* work_off, int32_t* n_works);

@@ -943,6 +943,16 @@ void build_tile_blocks(const rs_svd_plan* pl, int32_t grid0, bool want_pos, Tile
 
 int32_t tile_partials(const rs_svd_plan* pl) { return std::max(1, pl->tile_grid) * pl->tile_waves; }
 
+int32_t tile_cap_in_use(const rs_svd_plan* pl) {
+    if (pl->tile_run_cap > 0) return pl->tile_run_cap;
+    const int32_t grid0 = pl->tile_wg > 0 ? pl->tile_wg : device_cus(pl->ctx);
+    const int32_t c = auto_run_cap(pl, grid0, pl->tile_waves);
+    if (c > 0) return c;
+    std::vector<int64_t> deg(std::max(1, pl->n_items), 0);  // uncut: the longest run is at most an item's degree
+    for (int32_t x : pl->h_cols) deg[x]++;
+    return static_cast<int32_t>(std::min<int64_t>(*std::max_element(deg.begin(), deg.end()), 1 << 30));
+}
+
 void tile_build(rs_svd_plan* pl) {
     hipStream_t s = pl->ctx->stream;
     const int32_t cus = device_cus(pl->ctx);

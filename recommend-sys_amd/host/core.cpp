@@ -6,6 +6,7 @@
 #include <fstream>
 #include <numeric>
 #include <sstream>
+#include <thread>
 
 namespace core {
 
@@ -475,7 +476,7 @@ double MAE(Estimator& e, const DataSet& test) {
 
 std::vector<CrossValidateResult> CrossValidate(const Estimator& estimator, const DataSet& dataSet,
                                                const std::vector<Evaluator>& metrics, int cv,
-                                               uint64_t seed, const Parameters& params) {
+                                               uint64_t seed, const Parameters& params, int nJobs) {
     std::vector<CrossValidateResult> ret(metrics.size());
     for (auto& r : ret) {
         r.Trains.assign(cv, 0.0);
@@ -488,12 +489,25 @@ std::vector<CrossValidateResult> CrossValidate(const Estimator& estimator, const
     std::vector<TrainSet> trains;
     std::vector<DataSet> tests;
     dataSet.KFold(cv, perm, trains, tests);
-    for (int i = 0; i < cv; ++i) {
-        std::unique_ptr<Estimator> cp = estimator.Clone();  // eval.go:29-30
-        cp->SetParams(params);                               // eval.go:34: params replace the copy's
-        cp->Fit(trains[i]);
-        for (size_t j = 0; j < metrics.size(); ++j) ret[j].Tests[i] = metrics[j](*cp, tests[i]);
-    }
+    const int jobs = nJobs > 0 ? std::min(nJobs, cv) : cv;
+    std::vector<std::exception_ptr> err(static_cast<size_t>(jobs));
+    std::vector<std::thread> th;
+    for (int job = 0; job < jobs; ++job)
+        th.emplace_back([&, job] {  // utils.go:145-157: one goroutine per job
+            try {
+                std::unique_ptr<Estimator> cp = estimator.Clone();  // eval.go:29-30
+                for (int i = cv * job / jobs; i < cv * (job + 1) / jobs; ++i) {
+                    cp->SetParams(params);  // eval.go:34: params replace the copy's
+                    cp->Fit(trains[i]);
+                    for (size_t j = 0; j < metrics.size(); ++j) ret[j].Tests[i] = metrics[j](*cp, tests[i]);
+                }
+            } catch (...) {
+                err[job] = std::current_exception();
+            }
+        });
+    for (std::thread& t : th) t.join();
+    for (auto& e : err)
+        if (e) std::rethrow_exception(e);
     return ret;
 }
 

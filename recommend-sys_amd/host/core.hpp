@@ -185,9 +185,11 @@ double MAE(Estimator& e, const DataSet& test);
 struct CrossValidateResult {  // eval.go:12-15
     std::vector<double> Trains, Tests;
 };
-// eval.go:18-67 (folds run sequentially here; each fold fits a Clone, as eval.go:29-30 does)
+// eval.go:18-67: the cv folds split over nJobs host threads (utils.go:145-157 `parallel`: job j takes folds
+// [cv j / nJobs, cv (j + 1) / nJobs)); each job fits its own Clone (eval.go:29-30), which opens its own
+// rs_ctx, so the folds' Fits run concurrently on the device (nJobs <= 0: one job per fold)
 std::vector<CrossValidateResult> CrossValidate(const Estimator& estimator, const DataSet& dataSet,
                                                const std::vector<Evaluator>& metrics, int cv,
-                                               uint64_t seed, const Parameters& params);
+                                               uint64_t seed, const Parameters& params, int nJobs = 0);
 
 }  // namespace core

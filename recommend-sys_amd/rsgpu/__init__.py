@@ -45,6 +45,7 @@ HEADER_SYMBOLS = (
     "rs_svd_plan_set_user_blocks", "rs_svd_group_create", "rs_svd_group_epochs", "rs_svd_group_destroy",
     "rs_item_shards", "rs_svd_fit_multi", "rs_tile_schedule_host", "rs_svd_plan_set_exchange",
     "rs_comm_info", "rs_rotation_step", "rs_svd_plan_shard_info", "rs_svd_plan_inject_fault",
+    "rs_svd_plan_time_blocks",
 )
 COMM_ID_BYTES = 128
 
@@ -164,6 +165,7 @@ def lib():
                                            _vp, _vp, _vp, _vp, _vp]),
             "rs_svd_plan_set_exchange": (C.c_int, [_vp, _i32]),
             "rs_svd_plan_inject_fault": (C.c_int, [_vp, _i32]),
+            "rs_svd_plan_time_blocks": (C.c_int, [_vp, _flt, _flt, _vp, _i32]),
             "rs_comm_info": (C.c_int, [C.POINTER(_i32), _vp, _i32]),
             "rs_rotation_step": (C.c_int, [_i32, _i32, _i32, _vp]),
             "rs_svd_plan_shard_info": (C.c_int, [_vp, C.POINTER(_i32), C.POINTER(_i32), C.POINTER(_i32),
@@ -460,6 +462,13 @@ class SvdPlan:
     def set_exchange(self, mode=EXCHANGE_ROTATE):
         """Multi-GPU exchange a later join / group sets up (rs_svd_plan_set_exchange)."""
         self.ctx.check(lib().rs_svd_plan_set_exchange(self.h, mode))
+
+    def time_blocks(self, n_blocks, lr=0.005, reg=0.02):
+        """One epoch with every user block / stratum launched alone and timed: ms per block
+        (rs_svd_plan_time_blocks; trains the model like an epoch)."""
+        ms = np.zeros(n_blocks)
+        self.ctx.check(lib().rs_svd_plan_time_blocks(self.h, lr, reg, _ptr(ms), n_blocks))
+        return ms
 
     def inject_fault(self, sub_epoch):
         """Test hook: the next sharded call throws at that sub-epoch, once (rs_svd_plan_inject_fault)."""

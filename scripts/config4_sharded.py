@@ -1,0 +1,180 @@
+#!/usr/bin/env python3
+"""BASELINE configs[4] as a sharded fit at full size on ONE MI355X: SVD nFactors=256 on the synthetic
+10M users x 1M items x ~1e9 ratings set (rs_synth, seed 20250826), library defaults, 8 shards through
+the in-process group (rs_svd_group on plans sharing device 0), next to the whole set fitted by one plan.
+
+The exchange is RS_EXCHANGE_ROTATE_Q (U > I: the Q item rank-blocks rotate, the users stay; the shards
+are user ranges of near-equal ratings, as rs_svd_fit_multi cuts them).  Both fits start from the same
+factors (rs_svd_plan_init_normal draws rows by row id, so every shard's P / Q equal the single plan's)
+and the same GlobalBias (the training mean).  0.1 % of the ratings (every 1024th of each user range's
+CSR) are held out.  Reports the held-out RMSE after every epoch for both fits, the epoch times, and --
+with --strata -- one extra epoch per shard with every stratum launched alone (rs_svd_plan_time_blocks):
+the per-stratum kernel times an 8-GPU run's sub-epochs wait on, and the Q bytes each sub-epoch moves.
+
+    python scripts/config4_sharded.py [--epochs 5] [--shards 8] [--strata] [--users U --items I]
+Prints JSON lines (progress on stderr).  Reference: core/svd.go:92-130.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [os.path.join(REPO, "recommend-sys_amd")]
+import rsgpu  # noqa: E402
+
+LR, REG = 0.005, 0.02
+
+
+def log(*a):
+    print(f"[{time.strftime('%H:%M:%S')}]", *a, file=sys.stderr, flush=True)
+
+
+def generate(U, I, n, seed, threads=16):
+    """n user ranges of near-equal users (rs_synth rows [lo, hi)), each with every 1024th rating held out."""
+    parts = []
+    for p in range(n):
+        lo, hi = U * p // n, U * (p + 1) // n
+        s = rsgpu.Synth(U, I, mean_deg=100.0, sigma=1.0, min_deg=1, max_deg=I // 2, zipf_s=0.9, seed=seed,
+                        user_lo=lo, user_hi=hi, n_threads=threads)
+        deg = np.diff(s.rowptr)
+        hold = np.zeros(s.nnz, bool)
+        hold[::1024] = True
+        rows = np.repeat(np.arange(hi - lo, dtype=np.int32), deg)
+        hu, hi_, hr = rows[hold] + lo, s.cols[hold].copy(), s.vals[hold].astype(np.float64)
+        keep = ~hold
+        rp = np.zeros(hi - lo + 1, np.int64)
+        np.cumsum(np.bincount(rows[keep], minlength=hi - lo), out=rp[1:])
+        parts.append(dict(lo=lo, hi=hi, rowptr=rp, cols=s.cols[keep].copy(), vals=s.vals[keep].copy(),
+                          hu=hu, hi_=hi_, hr=hr))
+        s.close()
+        log(f"range {p}: users [{lo}, {hi}) {int(rp[-1])} training ratings")
+    return parts
+
+
+def padded_rowptr(part, U):
+    """A user range's CSR as rows 0..U-1 (empty rows outside the range)."""
+    rp = np.zeros(U + 1, np.int64)
+    rp[part["lo"] + 1:part["hi"] + 1] = part["rowptr"][1:]
+    rp[part["hi"] + 1:] = part["rowptr"][-1]
+    return rp
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--users", type=int, default=10_000_000)
+    ap.add_argument("--items", type=int, default=1_000_000)
+    ap.add_argument("--k", type=int, default=256)
+    ap.add_argument("--epochs", type=int, default=5)
+    ap.add_argument("--shards", type=int, default=8)
+    ap.add_argument("--seed", type=int, default=20250826)
+    ap.add_argument("--strata", action="store_true", help="time every stratum alone (one extra epoch per shard)")
+    ap.add_argument("--no-whole", action="store_true", help="skip the single-plan fit")
+    args = ap.parse_args()
+    U, I, k, n = args.users, args.items, args.k, args.shards
+
+    ctx = rsgpu.Context(0)
+    t0 = time.perf_counter()
+    parts = generate(U, I, n, args.seed)
+    t_gen = time.perf_counter() - t0
+    hu = np.concatenate([p["hu"] for p in parts])
+    hi_ = np.concatenate([p["hi_"] for p in parts])
+    hr = np.concatenate([p["hr"] for p in parts])
+    nnz = int(sum(int(p["rowptr"][-1]) for p in parts))
+    gb0 = float(sum(float(np.sum(p["vals"], dtype=np.float64)) for p in parts) / nnz)
+    log(f"generated {nnz} training + {len(hr)} held-out ratings in {t_gen:.1f} s, mean {gb0:.4f}")
+    out = {"config": "BASELINE configs[4]: SVD nFactors=256, synthetic 10M x 1M x ~1e9 (rs_synth seed "
+                     f"{args.seed}), library defaults", "n_users": U, "n_items": I, "nnz_train": nnz,
+           "n_holdout": int(len(hr)), "epochs": args.epochs, "lr": LR, "reg": REG, "gen_s": t_gen}
+
+    whole = None
+    if not args.no_whole:  # the same set as one plan: one CSR over all users
+        t0 = time.perf_counter()
+        rp = np.concatenate([[0]] + [p["rowptr"][1:] + sum(int(q["rowptr"][-1]) for q in parts[:x])
+                                     for x, p in enumerate(parts)]).astype(np.int64)
+        cols = np.concatenate([p["cols"] for p in parts])
+        vals = np.concatenate([p["vals"] for p in parts])
+        plan = ctx.svd_plan_csr(U, I, rp, cols, vals, k)
+        del cols, vals, rp
+        plan.init_normal(0.0, 0.1, seed=1)
+        plan.upload(gb=gb0)
+        t_plan = time.perf_counter() - t0
+        r0 = plan.evaluate(hu, hi_, hr)[0]
+        curve, ep_s = [], []
+        for e in range(args.epochs):
+            t = time.perf_counter()
+            plan.epochs(1, LR, REG)
+            ctx.check(rsgpu.lib().rs_synchronize(ctx.h))
+            ep_s.append(time.perf_counter() - t)
+            curve.append(plan.evaluate(hu, hi_, hr)[0])
+            log(f"whole set epoch {e + 1}: {ep_s[-1]:.3f} s, held-out RMSE {curve[-1]:.4f}")
+        plan.close()
+        whole = {"plan_build_s": t_plan, "rmse_init": r0, "rmse_per_epoch": curve, "epoch_s": ep_s}
+        out["whole"] = whole
+        print(json.dumps({"whole": whole}), flush=True)
+
+    # the sharded fit: n plans over user ranges (global ids, all items), Q item blocks rotate
+    t0 = time.perf_counter()
+    plans = []
+    for p in parts:
+        pl = ctx.svd_plan_csr(U, I, padded_rowptr(p, U), p["cols"], p["vals"], k)
+        pl.set_exchange(rsgpu.EXCHANGE_ROTATE_Q)
+        pl.init_normal(0.0, 0.1, seed=1)
+        pl.upload(gb=gb0)
+        plans.append(pl)
+    g = rsgpu.SvdGroup(plans, n_blocks=0)
+    t_join = time.perf_counter() - t0
+    _, _, exch, nblk = plans[0].shard_info()
+    log(f"{n} shard plans + group in {t_join:.1f} s: exchange {exch}, {nblk} item blocks")
+    r0 = plans[0].evaluate(hu, hi_, hr)[0]
+    curve, ep_s = [], []
+    for e in range(args.epochs):
+        t = time.perf_counter()
+        g.epochs(1, LR, REG)
+        ep_s.append(time.perf_counter() - t)
+        curve.append(plans[0].evaluate(hu, hi_, hr)[0])
+        log(f"sharded epoch {e + 1}: {ep_s[-1]:.3f} s, held-out RMSE {curve[-1]:.4f}")
+    sh = {"n_shards": n, "exchange": "RS_EXCHANGE_ROTATE_Q", "item_blocks": nblk, "setup_s": t_join,
+          "rmse_init": r0, "rmse_per_epoch": curve, "epoch_s_one_gpu": ep_s}
+    if whole:
+        sh["rmse_diff_vs_whole"] = curve[-1] - whole["rmse_per_epoch"][-1]
+    g.close()
+    if args.strata:  # per-stratum kernel times: shard g trains item rank-block (g + s) mod n in sub-epoch s
+        pieces = nblk // n
+        t = np.array([pl.time_blocks(nblk, LR, REG) for pl in plans])  # [shard, item block] ms
+        rb = t.reshape(n, n, pieces).sum(2)  # [shard, item rank-block]
+        sub = np.array([[rb[gg, (gg + s) % n] for gg in range(n)] for s in range(n)])  # [sub-epoch, shard]
+        ld = plans[0].ld
+        sh["stratum_ms"] = t.tolist()
+        sh["sub_epoch_ms_per_shard"] = sub.tolist()
+        sh["sub_epoch_max_ms"] = sub.max(1).tolist()
+        sh["sub_epoch_mean_ms"] = sub.mean(1).tolist()
+        sh["imbalance_max_over_mean"] = float((sub.max(1) / sub.mean(1)).mean())
+        sh["q_bytes_per_sub_epoch"] = int(I / n * ld * 4)
+        sh["p_bytes_per_sub_epoch_if_p_rotated"] = int(U / n * ld * 4)
+        log(f"sub-epoch max/mean stratum time {sh['imbalance_max_over_mean']:.3f}; "
+            f"epoch on {n} GPUs ~ {sum(sh['sub_epoch_max_ms']):.1f} ms of SGD")
+    # finite: the download's fixed-point / non-finite check of Q (RS_ERR_NUMERIC) and the RMSE of every shard
+    # (P of 10M x 256 doubles is not brought to the host)
+    finite = all(np.isfinite(x) for x in curve)
+    for pl in plans:
+        try:
+            e = pl.evaluate(hu[:1000], hi_[:1000], hr[:1000])[0]
+            finite = finite and bool(np.isfinite(e))
+        except rsgpu.RsError:
+            finite = False
+        pl.close()
+    sh["finite"] = finite
+    out["sharded"] = sh
+    print(json.dumps({"sharded": sh}), flush=True)
+    print(json.dumps(out), flush=True)
+    ctx.close()
+
+
+if __name__ == "__main__":
+    main()
