@@ -310,8 +310,12 @@ def main():
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
                          "traffic": traffic,
-                         "kernel": "svd_epoch_tile_kernel<E=2,NW=16,RQ=2> (tile schedule: user tiles in LDS, "
-                                   "integer LDS atomics, one memory-side atomic per (item, tile) run)",
+                         "traffic_source": "committed PMC figure, not measured in this run: FETCH_SIZE x 2 + "
+                                           "WRITE_SIZE per launch from separate rocprofv3 --pmc passes over the "
+                                           "same workload (scripts/pmc_sgd.sh -> profiles/sgd_traffic.json)",
+                         "kernel": "svd_epoch_tile_kernel<E=2,NW=16,RQ=2,CH=4> (tile schedule: user tiles in "
+                                   "LDS, integer LDS atomics, one memory-side atomic per (item, tile) run, waves "
+                                   "claim 4 runs at a time from the tile's run queue)",
                          "avg_kernel_us": avg_kernel_s * 1e6,
                          "timed_span": "HIP events around each epoch's SGD kernel on the launch stream "
                                        "(the per-epoch epilogue and the per-call Q fixed-point conversions "

@@ -205,9 +205,14 @@ void rs_knn_plan_destroy(rs_knn_plan* plan);
 int rs_knn_plan_sims(rs_knn_plan* plan, double* sims /* host, n_left x n_left */);
 /* core/knn.go:75-141 KNN.Predict for n (left, right) inner-id pairs (-1 / out of range = unknown):
  * candidates RightRatings[right] (right CSR over n_right rows, data order, ids are left ids) with a
- * non-NaN Sims[left][id]; top-k by (sim desc, position asc) -- the documented tie rule for the
- * reference's unstable sort.Sort (knn.go:107-108) --; type 0 basic, 1 centered (means), 2 zscore
- * (means, stddevs), 3 baseline (bias), arrays over left ids.  Bitwise equal to the restatement. */
+ * non-NaN Sims[left][id], ordered as knn.go:107-108's sort.Sort orders them (RS_TIE_GO_SORT, default:
+ * Go 1.24's pdqsort restated call for call, so equal similarities end in the reference's order), or by
+ * (sim desc, position asc) (RS_TIE_STABLE, rs_knn_plan_set_tie_order); the first k summed in that order;
+ * type 0 basic, 1 centered (means), 2 zscore (means, stddevs), 3 baseline (bias), arrays over left ids.
+ * Bitwise equal to the restatement (oracle or_knn_predict / or_knn_predict_stable). */
+#define RS_TIE_GO_SORT 0
+#define RS_TIE_STABLE 1
+int rs_knn_plan_set_tie_order(rs_knn_plan* plan, int32_t tie);
 int rs_knn_plan_predict(rs_knn_plan* plan, int32_t type, int32_t n_right, const int64_t* right_rowptr,
                         const int32_t* right_ids, const double* right_r, const double* means,
                         const double* stddevs, const double* bias, double global_mean, int32_t k,

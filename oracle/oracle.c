@@ -607,11 +607,230 @@ static int cmp_cand(const void* x, const void* y) {
     return (a->pos > b->pos) - (a->pos < b->pos);           /* documented tie rule */
 }
 
-void or_knn_predict(int32_t type, int32_t L, const double* sims, const int64_t* right_rowptr,
-                    const int32_t* right_ids, const double* right_r, const double* means,
-                    const double* stddevs, const double* bias, double global_mean, int32_t k,
-                    int32_t min_k, int64_t n, const int32_t* left, const int32_t* right,
-                    double* out) {
+/* Go 1.24 sort.Sort (knn.go:107-108 sorts the CandidateSet with it; go.mod:3 pins go 1.24): pdqsort as in
+ * the standard library's sort/zsortinterface.go, restated here call for call -- the same Less / Swap
+ * sequence, so the same permutation of tied candidates (sort.Sort is not stable).  Less(i, j) =
+ * sims[c_i] > sims[c_j] (knn.go:43-45), Swap exchanges two candidates (knn.go:46-48).  Restated from the
+ * published algorithm of that release; no Go toolchain exists here or on the GPU boxes to run the
+ * original, so the tie order is pinned by this restatement only. */
+typedef struct {
+    cand* c;
+    const double* s;
+} gosort;
+static int g_less(const gosort* d, int64_t i, int64_t j) { return d->s[d->c[i].id] > d->s[d->c[j].id]; }
+static void g_swap(gosort* d, int64_t i, int64_t j) {
+    const cand t = d->c[i];
+    d->c[i] = d->c[j];
+    d->c[j] = t;
+}
+static int g_bits_len(uint64_t x) { /* math/bits.Len */
+    int n = 0;
+    while (x) {
+        n++;
+        x >>= 1;
+    }
+    return n;
+}
+static void g_insertion(gosort* d, int64_t a, int64_t b) {
+    for (int64_t i = a + 1; i < b; i++)
+        for (int64_t j = i; j > a && g_less(d, j, j - 1); j--) g_swap(d, j, j - 1);
+}
+static void g_sift_down(gosort* d, int64_t lo, int64_t hi, int64_t first) {
+    int64_t root = lo;
+    for (;;) {
+        int64_t child = 2 * root + 1;
+        if (child >= hi) return;
+        if (child + 1 < hi && g_less(d, first + child, first + child + 1)) child++;
+        if (!g_less(d, first + root, first + child)) return;
+        g_swap(d, first + root, first + child);
+        root = child;
+    }
+}
+static void g_heap_sort(gosort* d, int64_t a, int64_t b) {
+    const int64_t first = a, lo = 0, hi = b - a;
+    for (int64_t i = (hi - 1) / 2; i >= 0; i--) g_sift_down(d, i, hi, first);
+    for (int64_t i = hi - 1; i >= 0; i--) {
+        g_swap(d, first, first + i);
+        g_sift_down(d, lo, i, first);
+    }
+}
+enum { G_UNKNOWN = 0, G_INCREASING = 1, G_DECREASING = 2 };
+static void g_order2(gosort* d, int64_t* a, int64_t* b, int* swaps) {
+    if (g_less(d, *b, *a)) {
+        const int64_t t = *a;
+        *a = *b;
+        *b = t;
+        (*swaps)++;
+    }
+}
+static int64_t g_median(gosort* d, int64_t a, int64_t b, int64_t c, int* swaps) {
+    g_order2(d, &a, &b, swaps);
+    g_order2(d, &b, &c, swaps);
+    g_order2(d, &a, &b, swaps);
+    return b;
+}
+static int64_t g_median_adjacent(gosort* d, int64_t a, int* swaps) { return g_median(d, a - 1, a, a + 1, swaps); }
+static int64_t g_choose_pivot(gosort* d, int64_t a, int64_t b, int* hint) {
+    const int64_t l = b - a;
+    int swaps = 0;
+    int64_t i = a + l / 4 * 1, j = a + l / 4 * 2, k = a + l / 4 * 3;
+    if (l >= 8) {
+        if (l >= 50) { /* Tukey ninther */
+            i = g_median_adjacent(d, i, &swaps);
+            j = g_median_adjacent(d, j, &swaps);
+            k = g_median_adjacent(d, k, &swaps);
+        }
+        j = g_median(d, i, j, k, &swaps);
+    }
+    *hint = swaps == 0 ? G_INCREASING : (swaps == 12 ? G_DECREASING : G_UNKNOWN);
+    return j;
+}
+static void g_reverse(gosort* d, int64_t a, int64_t b) {
+    for (int64_t i = a, j = b - 1; i < j; i++, j--) g_swap(d, i, j);
+}
+static int g_partial_insertion(gosort* d, int64_t a, int64_t b) {
+    int64_t i = a + 1;
+    for (int step = 0; step < 5; step++) {
+        while (i < b && !g_less(d, i, i - 1)) i++;
+        if (i == b) return 1;
+        if (b - a < 50) return 0;
+        g_swap(d, i, i - 1);
+        if (i - a >= 2)
+            for (int64_t j = i - 1; j >= 1; j--) {
+                if (!g_less(d, j, j - 1)) break;
+                g_swap(d, j, j - 1);
+            }
+        if (b - i >= 2)
+            for (int64_t j = i + 1; j < b; j++) {
+                if (!g_less(d, j, j - 1)) break;
+                g_swap(d, j, j - 1);
+            }
+    }
+    return 0;
+}
+static void g_break_patterns(gosort* d, int64_t a, int64_t b) {
+    const int64_t length = b - a;
+    if (length >= 8) {
+        uint64_t r = (uint64_t)length; /* xorshift seeded with the length */
+        const uint64_t modulus = (uint64_t)1 << g_bits_len((uint64_t)length);
+        const int64_t idx = a + (length / 4) * 2 - 1;
+        for (int t = 0; t < 3; t++) {
+            r ^= r << 13;
+            r ^= r >> 7;
+            r ^= r << 17;
+            int64_t other = (int64_t)(r & (modulus - 1));
+            if (other >= length) other -= length;
+            g_swap(d, idx - 1 + t, a + other);
+        }
+    }
+}
+static int64_t g_partition_equal(gosort* d, int64_t a, int64_t b, int64_t pivot) {
+    g_swap(d, a, pivot);
+    int64_t i = a + 1, j = b - 1;
+    for (;;) {
+        while (i <= j && !g_less(d, a, i)) i++;
+        while (i <= j && g_less(d, a, j)) j--;
+        if (i > j) break;
+        g_swap(d, i, j);
+        i++;
+        j--;
+    }
+    return i;
+}
+static int64_t g_partition(gosort* d, int64_t a, int64_t b, int64_t pivot, int* already) {
+    g_swap(d, a, pivot);
+    int64_t i = a + 1, j = b - 1;
+    while (i <= j && g_less(d, i, a)) i++;
+    while (i <= j && !g_less(d, j, a)) j--;
+    if (i > j) {
+        g_swap(d, j, a);
+        *already = 1;
+        return j;
+    }
+    g_swap(d, i, j);
+    i++;
+    j--;
+    for (;;) {
+        while (i <= j && g_less(d, i, a)) i++;
+        while (i <= j && !g_less(d, j, a)) j--;
+        if (i > j) break;
+        g_swap(d, i, j);
+        i++;
+        j--;
+    }
+    g_swap(d, j, a);
+    *already = 0;
+    return j;
+}
+static void g_pdqsort(gosort* d, int64_t a, int64_t b, int limit) {
+    int was_balanced = 1, was_partitioned = 1;
+    for (;;) {
+        const int64_t length = b - a;
+        if (length <= 12) {
+            g_insertion(d, a, b);
+            return;
+        }
+        if (limit == 0) {
+            g_heap_sort(d, a, b);
+            return;
+        }
+        if (!was_balanced) {
+            g_break_patterns(d, a, b);
+            limit--;
+        }
+        int hint;
+        int64_t pivot = g_choose_pivot(d, a, b, &hint);
+        if (hint == G_DECREASING) {
+            g_reverse(d, a, b);
+            pivot = (b - 1) - (pivot - a);
+            hint = G_INCREASING;
+        }
+        if (was_balanced && was_partitioned && hint == G_INCREASING)
+            if (g_partial_insertion(d, a, b)) return;
+        if (a > 0 && !g_less(d, a - 1, pivot)) {
+            a = g_partition_equal(d, a, b, pivot);
+            continue;
+        }
+        int already = 0;
+        const int64_t mid = g_partition(d, a, b, pivot, &already);
+        was_partitioned = already;
+        const int64_t left_len = mid - a, right_len = b - mid, threshold = length / 8;
+        if (left_len < right_len) {
+            was_balanced = left_len >= threshold;
+            g_pdqsort(d, a, mid, limit);
+            a = mid + 1;
+        } else {
+            was_balanced = right_len >= threshold;
+            g_pdqsort(d, mid + 1, b, limit);
+            b = mid;
+        }
+    }
+}
+static void go_sort_candidates(cand* c, int64_t n, const double* srow) {
+    if (n <= 1) return;
+    gosort d = {c, srow};
+    g_pdqsort(&d, 0, n, g_bits_len((uint64_t)n));
+}
+
+/* Test helper: the permutation Go's sort.Sort leaves for keys under Less(i, j) = key_i > key_j (perm[t] =
+ * the input position at output t). */
+void or_go_sort_desc(int64_t n, const double* keys, int64_t* perm) {
+    cand* c = (cand*)malloc((size_t)(n > 0 ? n : 1) * sizeof(cand));
+    for (int64_t t = 0; t < n; t++) {
+        c[t].id = (int32_t)t;
+        c[t].r = 0.0;
+        c[t].pos = t;
+    }
+    go_sort_candidates(c, n, keys);
+    for (int64_t t = 0; t < n; t++) perm[t] = c[t].pos;
+    free(c);
+}
+
+static void knn_predict_impl(int go_order, int32_t type, int32_t L, const double* sims, const int64_t* right_rowptr,
+                             const int32_t* right_ids, const double* right_r, const double* means,
+                             const double* stddevs, const double* bias, double global_mean, int32_t k,
+                             int32_t min_k, int64_t n, const int32_t* left, const int32_t* right,
+                             double* out) {
     int64_t maxdeg = 1;
     for (int64_t x = 0; x < n; x++) {
         if (right[x] < 0) continue;
@@ -639,8 +858,12 @@ void or_knn_predict(int32_t type, int32_t L, const double* sims, const int64_t* 
             out[x] = global_mean;
             continue;
         }
-        g_sim_row = srow;
-        qsort(c, (size_t)nc, sizeof(cand), cmp_cand);       /* knn.go:107-108 */
+        if (go_order) {
+            go_sort_candidates(c, nc, srow);                /* knn.go:107-108: sort.Sort */
+        } else {
+            g_sim_row = srow;
+            qsort(c, (size_t)nc, sizeof(cand), cmp_cand);   /* stable tie rule (position) */
+        }
         const int64_t nn = nc < k ? nc : k;                 /* knn.go:111-114 */
         double weightSum = 0.0, weightRating = 0.0;
         for (int64_t t = 0; t < nn; t++) {                  /* knn.go:118-130 */
@@ -661,6 +884,26 @@ void or_knn_predict(int32_t type, int32_t L, const double* sims, const int64_t* 
         out[x] = prediction;
     }
     free(c);
+}
+
+/* KNN.Predict (knn.go:75-141) with the reference's tie order (Go sort.Sort, restated above) */
+void or_knn_predict(int32_t type, int32_t L, const double* sims, const int64_t* right_rowptr,
+                    const int32_t* right_ids, const double* right_r, const double* means,
+                    const double* stddevs, const double* bias, double global_mean, int32_t k,
+                    int32_t min_k, int64_t n, const int32_t* left, const int32_t* right,
+                    double* out) {
+    knn_predict_impl(1, type, L, sims, right_rowptr, right_ids, right_r, means, stddevs, bias, global_mean, k,
+                     min_k, n, left, right, out);
+}
+
+/* The same with ties kept in candidate (RightRatings) order: the library's RS_TIE_STABLE option */
+void or_knn_predict_stable(int32_t type, int32_t L, const double* sims, const int64_t* right_rowptr,
+                           const int32_t* right_ids, const double* right_r, const double* means,
+                           const double* stddevs, const double* bias, double global_mean, int32_t k,
+                           int32_t min_k, int64_t n, const int32_t* left, const int32_t* right,
+                           double* out) {
+    knn_predict_impl(0, type, L, sims, right_rowptr, right_ids, right_r, means, stddevs, bias, global_mean, k,
+                     min_k, n, left, right, out);
 }
 
 void or_baseline_fit(int64_t n, const int32_t* u, const int32_t* i, const double* r,

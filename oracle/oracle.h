@@ -84,14 +84,24 @@ void or_knn_sims(int32_t kind, int32_t L, const int64_t* rowptr, const int32_t* 
 void or_knn_sims_rows(int32_t kind, int32_t L, const int64_t* rowptr, const int32_t* sorted_ids,
                       const double* sorted_r, int32_t row_begin, int32_t row_end, double* out);
 
-/* knn.go:75-141 KNN.Predict with ties broken by (sim desc, position asc) -- the reference uses
- * Go's unstable sort.Sort (knn.go:108), so tie order is the one documented deviation.
+/* knn.go:75-141 KNN.Predict.  The candidates are ordered as Go 1.24's sort.Sort (pdqsort, unstable)
+ * orders them (knn.go:107-108), restated call for call in oracle.c -- the tie order among equal
+ * similarities, and so the top-k boundary and the summation order, are the reference's.
  * type: 0 basic, 1 centered, 2 zscore, 3 baseline.  right_* is RightRatings CSR in data order. */
 void or_knn_predict(int32_t type, int32_t L, const double* sims, const int64_t* right_rowptr,
                     const int32_t* right_ids, const double* right_r, const double* means,
                     const double* stddevs, const double* bias, double global_mean,
                     int32_t k, int32_t min_k, int64_t n, const int32_t* left, const int32_t* right,
                     double* out);
+/* The same with ties broken by candidate position (sim desc, position asc): the library's
+ * RS_TIE_STABLE option. */
+void or_knn_predict_stable(int32_t type, int32_t L, const double* sims, const int64_t* right_rowptr,
+                           const int32_t* right_ids, const double* right_r, const double* means,
+                           const double* stddevs, const double* bias, double global_mean,
+                           int32_t k, int32_t min_k, int64_t n, const int32_t* left, const int32_t* right,
+                           double* out);
+/* Go's sort.Sort permutation for keys under Less(i, j) = key_i > key_j (perm[t] = input position). */
+void or_go_sort_desc(int64_t n, const double* keys, int64_t* perm);
 
 /* base.go:135-163 BaseLine.Fit (bias-only SGD, used by KNN baseline knn.go:179-187). */
 void or_baseline_fit(int64_t n, const int32_t* u, const int32_t* i, const double* r,

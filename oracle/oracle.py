@@ -56,9 +56,11 @@ def lib():
         L.or_sim.argtypes = [C.c_int32, C.c_int64, _i32p, _f64p, C.c_int64, _i32p, _f64p]
         L.or_sim.restype = C.c_double
         L.or_knn_sims.argtypes = [C.c_int32, C.c_int32, _i64p, _i32p, _f64p, _f64p]
-        L.or_knn_predict.argtypes = [C.c_int32, C.c_int32, _f64p, _i64p, _i32p, _f64p, _f64p,
-                                     _f64p, _f64p, C.c_double, C.c_int32, C.c_int32, C.c_int64,
-                                     _i32p, _i32p, _f64p]
+        for fn in (L.or_knn_predict, L.or_knn_predict_stable):
+            fn.argtypes = [C.c_int32, C.c_int32, _f64p, _i64p, _i32p, _f64p, _f64p,
+                           _f64p, _f64p, C.c_double, C.c_int32, C.c_int32, C.c_int64,
+                           _i32p, _i32p, _f64p]
+        L.or_go_sort_desc.argtypes = [C.c_int64, _f64p, _i64p]
         L.or_baseline_fit.argtypes = [C.c_int64, _i32p, _i32p, _f64p, C.c_int32, C.c_double,
                                       C.c_double, _f64p, _f64p, _dp]
         L.or_svdpp_fit_userwise.argtypes = [C.c_int32, _i64p, _i32p, _f64p, C.c_int32, C.c_int32,
@@ -292,12 +294,22 @@ def knn_sims_rows(kind, rowptr, sorted_ids, sorted_r, row_begin, row_end):
     return out
 
 
+def go_sort_desc(keys):
+    """Go 1.24 sort.Sort's permutation under Less(i, j) = keys[i] > keys[j] (knn.go:43-45, 107-108)."""
+    keys = np.ascontiguousarray(keys, dtype=np.float64)
+    perm = np.empty(len(keys), np.int64)
+    lib().or_go_sort_desc(len(keys), _f64(keys), _i64(perm))
+    return perm
+
+
 def knn_predict(type_, sims, right_rowptr, right_ids, right_r, means, stddevs, bias,
-                global_mean, k, min_k, left, right):
+                global_mean, k, min_k, left, right, stable=False):
+    """knn.go:75-141; ties in Go sort.Sort's order (stable=True: candidate order)."""
     L = sims.shape[0]
     z = np.zeros(max(L, 1))
     out = np.empty(len(left))
-    lib().or_knn_predict(type_, L, _f64(sims), _i64(right_rowptr), _i32(right_ids),
+    fn = lib().or_knn_predict_stable if stable else lib().or_knn_predict
+    fn(type_, L, _f64(sims), _i64(right_rowptr), _i32(right_ids),
                          _f64(right_r), _f64(z if means is None else means),
                          _f64(z if stddevs is None else stddevs), _f64(z if bias is None else bias),
                          global_mean, k, min_k, len(left), _i32(left), _i32(right), out)

@@ -1062,6 +1062,288 @@ __global__ __launch_bounds__(64) void knn_predict_kernel(
     }
 }
 
+// ---- KNN.Predict with the reference's tie order (RS_TIE_GO_SORT, the default) --------------------------------
+// knn.go:107-108 orders the candidates with Go 1.24's sort.Sort -- pdqsort, not stable -- so among equal
+// similarities (ML-100K has ~293k pairs tied at exactly 1.0) the order, the top-k boundary and the
+// summation order of knn.go:118-130 are whatever its exact Less / Swap sequence leaves.  GoSort restates that
+// sequence (sort/zsortinterface.go) call for call on one lane; the recursion on the smaller part becomes an
+// explicit stack (depth <= log2 n).  Less(i, j) = sims_i > sims_j (knn.go:43-45); Swap moves a candidate's
+// similarity and position together.  oracle/oracle.c and host/gosort.hpp restate the same algorithm.
+struct GoSort {
+    double* s;
+    int32_t* p;
+    __device__ bool less(int32_t i, int32_t j) const { return s[i] > s[j]; }
+    __device__ void swap(int32_t i, int32_t j) const {
+        const double a = s[i];
+        s[i] = s[j];
+        s[j] = a;
+        const int32_t b = p[i];
+        p[i] = p[j];
+        p[j] = b;
+    }
+    __device__ static int bits_len(uint32_t x) { return x ? 32 - __clz(static_cast<int>(x)) : 0; }
+    __device__ void insertion(int32_t a, int32_t b) const {
+        for (int32_t i = a + 1; i < b; ++i)
+            for (int32_t j = i; j > a && less(j, j - 1); --j) swap(j, j - 1);
+    }
+    __device__ void sift_down(int32_t lo, int32_t hi, int32_t first) const {
+        int32_t root = lo;
+        for (;;) {
+            int32_t child = 2 * root + 1;
+            if (child >= hi) return;
+            if (child + 1 < hi && less(first + child, first + child + 1)) ++child;
+            if (!less(first + root, first + child)) return;
+            swap(first + root, first + child);
+            root = child;
+        }
+    }
+    __device__ void heap_sort(int32_t a, int32_t b) const {
+        const int32_t first = a, lo = 0, hi = b - a;
+        for (int32_t i = (hi - 1) / 2; i >= 0; --i) sift_down(i, hi, first);
+        for (int32_t i = hi - 1; i >= 0; --i) {
+            swap(first, first + i);
+            sift_down(lo, i, first);
+        }
+    }
+    __device__ void order2(int32_t& a, int32_t& b, int& swaps) const {
+        if (less(b, a)) {
+            const int32_t t = a;
+            a = b;
+            b = t;
+            ++swaps;
+        }
+    }
+    __device__ int32_t median(int32_t a, int32_t b, int32_t c, int& swaps) const {
+        order2(a, b, swaps);
+        order2(b, c, swaps);
+        order2(a, b, swaps);
+        return b;
+    }
+    __device__ int32_t choose_pivot(int32_t a, int32_t b, int& hint) const {  // hint: 0 unknown, 1 inc, 2 dec
+        const int32_t l = b - a;
+        int swaps = 0;
+        int32_t i = a + l / 4 * 1, j = a + l / 4 * 2, k = a + l / 4 * 3;
+        if (l >= 8) {
+            if (l >= 50) {  // Tukey ninther
+                i = median(i - 1, i, i + 1, swaps);
+                j = median(j - 1, j, j + 1, swaps);
+                k = median(k - 1, k, k + 1, swaps);
+            }
+            j = median(i, j, k, swaps);
+        }
+        hint = swaps == 0 ? 1 : (swaps == 12 ? 2 : 0);
+        return j;
+    }
+    __device__ bool partial_insertion(int32_t a, int32_t b) const {
+        int32_t i = a + 1;
+        for (int step = 0; step < 5; ++step) {
+            while (i < b && !less(i, i - 1)) ++i;
+            if (i == b) return true;
+            if (b - a < 50) return false;
+            swap(i, i - 1);
+            if (i - a >= 2)
+                for (int32_t j = i - 1; j >= 1; --j) {
+                    if (!less(j, j - 1)) break;
+                    swap(j, j - 1);
+                }
+            if (b - i >= 2)
+                for (int32_t j = i + 1; j < b; ++j) {
+                    if (!less(j, j - 1)) break;
+                    swap(j, j - 1);
+                }
+        }
+        return false;
+    }
+    __device__ void break_patterns(int32_t a, int32_t b) const {
+        const int32_t length = b - a;
+        if (length < 8) return;
+        uint64_t r = static_cast<uint64_t>(length);  // xorshift seeded with the length
+        const uint64_t modulus = uint64_t{1} << bits_len(static_cast<uint32_t>(length));
+        const int32_t idx = a + (length / 4) * 2 - 1;
+        for (int t = 0; t < 3; ++t) {
+            r ^= r << 13;
+            r ^= r >> 7;
+            r ^= r << 17;
+            int32_t other = static_cast<int32_t>(r & (modulus - 1));
+            if (other >= length) other -= length;
+            swap(idx - 1 + t, a + other);
+        }
+    }
+    __device__ int32_t partition_equal(int32_t a, int32_t b, int32_t pivot) const {
+        swap(a, pivot);
+        int32_t i = a + 1, j = b - 1;
+        for (;;) {
+            while (i <= j && !less(a, i)) ++i;
+            while (i <= j && less(a, j)) --j;
+            if (i > j) break;
+            swap(i, j);
+            ++i;
+            --j;
+        }
+        return i;
+    }
+    __device__ int32_t partition(int32_t a, int32_t b, int32_t pivot, bool& already) const {
+        swap(a, pivot);
+        int32_t i = a + 1, j = b - 1;
+        while (i <= j && less(i, a)) ++i;
+        while (i <= j && !less(j, a)) --j;
+        if (i > j) {
+            swap(j, a);
+            already = true;
+            return j;
+        }
+        swap(i, j);
+        ++i;
+        --j;
+        for (;;) {
+            while (i <= j && less(i, a)) ++i;
+            while (i <= j && !less(j, a)) --j;
+            if (i > j) break;
+            swap(i, j);
+            ++i;
+            --j;
+        }
+        swap(j, a);
+        already = false;
+        return j;
+    }
+    // sort.Sort over [0, n): pdqsort's loop, its recursive call on the smaller part as a pushed frame
+    __device__ void sort(int32_t n) const {
+        if (n <= 1) return;
+        struct Frame { int32_t a, b, limit; bool wb, wp; };
+        Frame st[40];
+        int sp = 0;
+        Frame f{0, n, bits_len(static_cast<uint32_t>(n)), true, true};
+        for (;;) {
+            bool done = false;
+            for (;;) {  // one pdqsort(data, a, b, limit) activation
+                const int32_t length = f.b - f.a;
+                if (length <= 12) {
+                    insertion(f.a, f.b);
+                    done = true;
+                    break;
+                }
+                if (f.limit == 0) {
+                    heap_sort(f.a, f.b);
+                    done = true;
+                    break;
+                }
+                if (!f.wb) {
+                    break_patterns(f.a, f.b);
+                    --f.limit;
+                }
+                int hint = 0;
+                int32_t pivot = choose_pivot(f.a, f.b, hint);
+                if (hint == 2) {
+                    for (int32_t i = f.a, j = f.b - 1; i < j; ++i, --j) swap(i, j);
+                    pivot = (f.b - 1) - (pivot - f.a);
+                    hint = 1;
+                }
+                if (f.wb && f.wp && hint == 1 && partial_insertion(f.a, f.b)) {
+                    done = true;
+                    break;
+                }
+                if (f.a > 0 && !less(f.a - 1, pivot)) {
+                    f.a = partition_equal(f.a, f.b, pivot);
+                    continue;
+                }
+                bool already = false;
+                const int32_t mid = partition(f.a, f.b, pivot, already);
+                f.wp = already;
+                const int32_t left_len = mid - f.a, right_len = f.b - mid, threshold = length / 8;
+                Frame child;
+                if (left_len < right_len) {
+                    f.wb = left_len >= threshold;
+                    child = Frame{f.a, mid, f.limit, true, true};
+                    f.a = mid + 1;
+                } else {
+                    f.wb = right_len >= threshold;
+                    child = Frame{mid + 1, f.b, f.limit, true, true};
+                    f.b = mid;
+                }
+                st[sp++] = f;  // the caller continues after the child returns
+                f = child;
+            }
+            if (done) {
+                if (sp == 0) return;
+                f = st[--sp];
+            }
+        }
+    }
+};
+
+constexpr int kGoSortLds = 4096;  // candidates sorted in LDS; more go to the per-block global scratch
+
+// One wave per query (grid-stride): the non-NaN candidates in RightRatings order (knn.go:95-99) are
+// compacted by ballot into (similarity, position) arrays, lane 0 runs GoSort on them, and the first
+// min(k, n) are accumulated in that order (knn.go:111-130), so the result is bitwise the reference's.
+__global__ __launch_bounds__(64) void knn_predict_gosort_kernel(
+    const double* __restrict__ S, int32_t L, int32_t n_right, const int64_t* __restrict__ rrp,
+    const int32_t* __restrict__ rids, const double* __restrict__ rr, const double* __restrict__ means,
+    const double* __restrict__ stddevs, const double* __restrict__ bias, double gmean, int32_t type,
+    int32_t k, int32_t min_k, int64_t n, const int32_t* __restrict__ left,
+    const int32_t* __restrict__ right, double* __restrict__ out, double* __restrict__ gs,
+    int32_t* __restrict__ gp, int64_t scratch) {
+    __shared__ double ls[kGoSortLds];
+    __shared__ int32_t lp[kGoSortLds];
+    const int lane = threadIdx.x;
+    for (int64_t qi = blockIdx.x; qi < n; qi += gridDim.x) {
+        const int32_t li = left[qi], ri = right[qi];
+        if (li < 0 || li >= L || ri < 0 || ri >= n_right) {  // knn.go:89-91
+            if (lane == 0) out[qi] = gmean;
+            continue;
+        }
+        const double* srow = S + static_cast<int64_t>(li) * L;
+        const int64_t b = rrp[ri];
+        const int32_t m = static_cast<int32_t>(rrp[ri + 1] - b);
+        const bool in_lds = m <= kGoSortLds;
+        double* sv = in_lds ? ls : gs + blockIdx.x * scratch;
+        int32_t* pv = in_lds ? lp : gp + blockIdx.x * scratch;
+        int32_t cnt = 0;  // wave-uniform
+        for (int32_t t0 = 0; t0 < m; t0 += 64) {
+            const int32_t t = t0 + lane;
+            const double v = t < m ? srow[rids[b + t]] : 0.0;
+            const bool ok = t < m && !isnan(v);
+            const uint64_t mask = __ballot(ok);
+            if (ok) {
+                const int32_t at = cnt + __popcll(mask & ((uint64_t{1} << lane) - 1));
+                sv[at] = v;
+                pv[at] = t;
+            }
+            cnt += __popcll(mask);
+        }
+        __syncthreads();
+        if (cnt <= min_k) {  // knn.go:102-104
+            if (lane == 0) out[qi] = gmean;
+            __syncthreads();
+            continue;
+        }
+        if (lane == 0) {
+            GoSort{sv, pv}.sort(cnt);  // knn.go:107-108
+            const int32_t nn = min(k, cnt);
+            double weightSum = 0.0, weightRating = 0.0;
+            for (int32_t j = 0; j < nn; ++j) {  // knn.go:118-130
+                const int32_t t = pv[j], id = rids[b + t];
+                weightSum += sv[j];
+                double rating = rr[b + t];
+                if (type == 1) rating -= means[id];
+                else if (type == 2) rating = (rating - means[id]) / stddevs[id];
+                else if (type == 3) rating -= bias[id];
+                weightRating += sv[j] * rating;
+            }
+            double prediction = weightRating / weightSum;  // knn.go:131-139
+            if (type == 1) prediction += means[li];
+            else if (type == 3) prediction += bias[li];
+            else if (type == 2) {
+                prediction *= stddevs[li];
+                prediction += means[li];
+            }
+            out[qi] = prediction;
+        }
+        __syncthreads();  // the next query overwrites the arrays
+    }
+}
+
 // SlopeOne.Predict (core/slope_one.go:21-45), one thread per query, bitwise: prediction = the user's
 // mean rating (means(), data.go:222-235, precomputed by row_mean_kernel in the same order) or the
 // global mean for an unknown user; for a known (user, item) the user's ratings are walked in data
@@ -1205,8 +1487,16 @@ struct rs_knn_plan {
     rs_ctx* ctx = nullptr;
     int32_t L = 0;
     int32_t kind = 0;
+    int32_t tie = RS_TIE_GO_SORT;  // rs_knn_plan_set_tie_order
     rs::DevBuf<double> S;
 };
+
+extern "C" int rs_knn_plan_set_tie_order(rs_knn_plan* pl, int32_t tie) {
+    if (!pl) return rs::set_error(nullptr, RS_ERR_INVALID, "plan is NULL");
+    if (tie != RS_TIE_GO_SORT && tie != RS_TIE_STABLE) return rs::set_error(pl->ctx, RS_ERR_INVALID, "unknown tie order");
+    pl->tie = tie;
+    return RS_OK;
+}
 
 extern "C" int rs_knn_plan_create(rs_ctx* ctx, int32_t kind, int32_t n_left, int32_t n_right,
                                   const int64_t* rowptr, const int32_t* ids, const double* ratings,
@@ -1290,9 +1580,23 @@ extern "C" int rs_knn_plan_predict(rs_knn_plan* pl, int32_t type, int32_t n_righ
         if (stddevs) dsd.upload(stddevs, pl->L, s);
         if (bias) db.upload(bias, pl->L, s);
         rs::kernel_span_begin(ctx);
-        hipLaunchKernelGGL(rs::knn_predict_kernel, dim3(static_cast<uint32_t>(n)), dim3(64), 0, s,
-                           pl->S.p, pl->L, n_right, drp.p, dids.p, drr.p, dm.p, dsd.p, db.p,
-                           global_mean, type, k, min_k, n, dl.p, dr.p, dout.p);
+        if (pl->tie == RS_TIE_GO_SORT) {
+            int64_t mmax = 0;  // rows past the LDS arrays sort in a per-block global scratch
+            for (int32_t x = 0; x < n_right; ++x) mmax = std::max(mmax, rp[x + 1] - rp[x]);
+            const int32_t grid = static_cast<int32_t>(std::min<int64_t>(n, 4096));
+            const int64_t scratch = mmax > rs::kGoSortLds ? mmax : 0;
+            rs::DevBuf<double> gs(std::max<int64_t>(1, scratch * grid));
+            rs::DevBuf<int32_t> gp(std::max<int64_t>(1, scratch * grid));
+            hipLaunchKernelGGL(rs::knn_predict_gosort_kernel, dim3(grid), dim3(64), 0, s, pl->S.p, pl->L, n_right,
+                               drp.p, dids.p, drr.p, dm.p, dsd.p, db.p, global_mean, type, k, min_k, n, dl.p, dr.p,
+                               dout.p, gs.p, gp.p, scratch);
+            RS_HIP(hipGetLastError());
+            RS_HIP(hipStreamSynchronize(s));  // the scratch dies with this scope
+        } else {
+            hipLaunchKernelGGL(rs::knn_predict_kernel, dim3(static_cast<uint32_t>(n)), dim3(64), 0, s,
+                               pl->S.p, pl->L, n_right, drp.p, dids.p, drr.p, dm.p, dsd.p, db.p,
+                               global_mean, type, k, min_k, n, dl.p, dr.p, dout.p);
+        }
         RS_HIP(hipGetLastError());
         rs::kernel_span_end(ctx);
         dout.download(out, n, s);

@@ -1,5 +1,6 @@
 // core.cpp -- C++ host mirror of the reference's Go `core` API over the C-ABI (see core.hpp).
 #include "core.hpp"
+#include "gosort.hpp"
 
 #include <algorithm>
 #include <cmath>
@@ -406,10 +407,11 @@ double KNN::Predict(int64_t userID, int64_t itemID) {  // knn.go:75-141
     for (const IDRating& ir : RightRatings[right])
         if (!std::isnan(srow[ir.ID])) cand.push_back(ir);
     if (static_cast<int>(cand.size()) <= minK) return GlobalMean;
-    // knn.go:107-108 sort.Sort (Go's unstable pdqsort) by similarity descending; ties here keep
-    // RightRatings order (stable) -- the one documented deviation of the host Predict.
-    std::stable_sort(cand.begin(), cand.end(),
-                     [&](const IDRating& a, const IDRating& b) { return srow[a.ID] > srow[b.ID]; });
+    // knn.go:107-108 sort.Sort: Go's pdqsort, restated call for call (gosort.hpp), so ties among equal
+    // similarities end in the reference's order
+    gosort::sort(static_cast<int64_t>(cand.size()),
+                 [&](int64_t a, int64_t b) { return srow[cand[a].ID] > srow[cand[b].ID]; },
+                 [&](int64_t a, int64_t b) { std::swap(cand[a], cand[b]); });
     const size_t nn = std::min<size_t>(k, cand.size());
     double weightSum = 0.0, weightRating = 0.0;
     for (size_t t = 0; t < nn; ++t) {

@@ -21,6 +21,7 @@ RS_ERR_INVALID, RS_ERR_HIP, RS_ERR_NOMEM, RS_ERR_UNSUPPORTED, RS_ERR_NO_DEVICE, 
 SGD_FAST, SGD_ORDERED = 0, 1
 WB_TILE, WB_STORE, WB_ATOMIC_DIRECT, WB_ATOMIC = 0, 1, 2, 3  # WB_TILE: the default schedule
 SIM_COSINE, SIM_MSD, SIM_PEARSON = 0, 1, 2
+TIE_GO_SORT, TIE_STABLE = 0, 1  # KNN.Predict tie order (rs_knn_plan_set_tie_order)
 DEV_SLOPE_ONE = 3  # rs_knn_sims kind: SlopeOne deviation matrix (slope_one.go:64-92)
 EXCHANGE_ROTATE, EXCHANGE_AVERAGE, EXCHANGE_ROTATE_Q = 0, 1, 2  # multi-GPU exchange of the sharded fit (rsgpu.h)
 
@@ -45,7 +46,7 @@ HEADER_SYMBOLS = (
     "rs_svd_plan_set_user_blocks", "rs_svd_group_create", "rs_svd_group_epochs", "rs_svd_group_destroy",
     "rs_item_shards", "rs_svd_fit_multi", "rs_tile_schedule_host", "rs_svd_plan_set_exchange",
     "rs_comm_info", "rs_rotation_step", "rs_svd_plan_shard_info", "rs_svd_plan_inject_fault",
-    "rs_svd_plan_time_blocks",
+    "rs_svd_plan_time_blocks", "rs_knn_plan_set_tie_order",
 )
 COMM_ID_BYTES = 128
 
@@ -166,6 +167,7 @@ def lib():
             "rs_svd_plan_set_exchange": (C.c_int, [_vp, _i32]),
             "rs_svd_plan_inject_fault": (C.c_int, [_vp, _i32]),
             "rs_svd_plan_time_blocks": (C.c_int, [_vp, _flt, _flt, _vp, _i32]),
+            "rs_knn_plan_set_tie_order": (C.c_int, [_vp, _i32]),
             "rs_comm_info": (C.c_int, [C.POINTER(_i32), _vp, _i32]),
             "rs_rotation_step": (C.c_int, [_i32, _i32, _i32, _vp]),
             "rs_svd_plan_shard_info": (C.c_int, [_vp, C.POINTER(_i32), C.POINTER(_i32), C.POINTER(_i32),
@@ -749,6 +751,10 @@ class KnnPlan:
         out = np.empty((self.L, self.L))
         self.ctx.check(lib().rs_knn_plan_sims(self.h, _ptr(out)))
         return out
+
+    def set_tie_order(self, tie=0):
+        """TIE_GO_SORT (default: knn.go:107-108's sort.Sort order) or TIE_STABLE (rs_knn_plan_set_tie_order)."""
+        self.ctx.check(lib().rs_knn_plan_set_tie_order(self.h, tie))
 
     def predict(self, knn_type, right_rowptr, right_ids, right_r, left, right, global_mean,
                 means=None, stddevs=None, bias=None, k=40, min_k=1):

@@ -116,7 +116,7 @@ def build_host(verbose: bool = False) -> str:
          [f"-L{HOST}", "-lrscore", f"-L{PKG_DIR}", "-lrsgpu",
           "-Wl,-rpath,$ORIGIN/..", "-Wl,-rpath,$ORIGIN/../../rsgpu"]),
     ]
-    deps = [os.path.join(HOST, "core.hpp"), os.path.join(INCLUDE, "rsgpu.h"), lib]
+    deps = [os.path.join(HOST, "core.hpp"), os.path.join(HOST, "gosort.hpp"), os.path.join(INCLUDE, "rsgpu.h"), lib]
     for srcs, out, extra in steps:
         newest = max(os.path.getmtime(p) for p in srcs + deps)
         if os.path.exists(out) and os.path.getmtime(out) >= newest:

@@ -181,11 +181,46 @@ def test_knn_plan_predict_bitwise(ctx, ml100k, kind, user_based):
     bias = bu if user_based else bi
     ql, qr = (f.tu, f.ti) if user_based else (f.ti, f.tu)
     gm = float(np.mean(r))
+    differ = 0
+    for stable in (False, True):  # knn.go:107-108's sort.Sort order (default), then RS_TIE_STABLE
+        plan.set_tie_order(rsgpu.TIE_STABLE if stable else rsgpu.TIE_GO_SORT)
+        for t, name in enumerate(["basic", "centered", "zscore", "baseline"]):
+            for k, mink in [(40, 1), (3, 5)]:
+                got = plan.predict(name, rrp, rids, rr, ql, qr, gm, means, stds, bias, k=k, min_k=mink)
+                ref = O.knn_predict(t, S, rrp, rids, rr, means, stds, bias, gm, k, mink, ql, qr, stable=stable)
+                assert bitwise_equal(got, ref), (name, k, mink, stable)
+                if not stable:
+                    alt = O.knn_predict(t, S, rrp, rids, rr, means, stds, bias, gm, k, mink, ql, qr, stable=True)
+                    differ += int(np.count_nonzero(~np.isclose(alt, ref, rtol=0, atol=0)))
+    plan.close()
+    print(f"predictions whose value depends on the tie order: {differ}")
+
+
+def test_knn_predict_go_order_long_rows(ctx):
+    """Candidate rows longer than the kernel's LDS arrays (5000 > 4096: the per-block global scratch) and
+    rows of exact ties (integer ratings, one co-rated item: Cosine 1.0 everywhere) through the Go-order
+    kernel: bitwise the restatement of sort.Sort's order, for every KNN type."""
+    rng = np.random.default_rng(21)
+    nl, nr = 6000, 12  # user-based: left = users, right = items; item 0 rated by 5000 users
+    users = [rng.choice(nl, 5000, replace=False)] + [rng.choice(nl, 300, replace=False) for _ in range(1, nr)]
+    u = np.concatenate(users).astype(np.int32)
+    i = np.concatenate([np.full(len(x), j) for j, x in enumerate(users)]).astype(np.int32)
+    r = rng.integers(1, 6, len(u)).astype(float)
+    lrp, lids, lr = O.csr_by(u, nl, i, r)
+    rrp, rids, rr = O.csr_by(i, nr, u, r)
+    plan = ctx.knn_plan(rsgpu.SIM_COSINE, lrp, lids, lr, nr)
+    S = plan.sims()
+    deg = np.diff(lrp).astype(float)
+    means = np.add.reduceat(lr, lrp[:-1]) / np.maximum(deg, 1)
+    stds = np.full(nl, 0.5)
+    bias = rng.normal(0, 0.1, nl)
+    ql = rng.integers(0, nl, 400).astype(np.int32)
+    qr = rng.integers(0, nr, 400).astype(np.int32)
+    qr[:100] = 0  # the 5000-candidate row
     for t, name in enumerate(["basic", "centered", "zscore", "baseline"]):
-        for k, mink in [(40, 1), (3, 5)]:
-            got = plan.predict(name, rrp, rids, rr, ql, qr, gm, means, stds, bias, k=k, min_k=mink)
-            ref = O.knn_predict(t, S, rrp, rids, rr, means, stds, bias, gm, k, mink, ql, qr)
-            assert bitwise_equal(got, ref), (name, k, mink)
+        got = plan.predict(name, rrp, rids, rr, ql, qr, 3.0, means, stds, bias, k=40, min_k=1)
+        ref = O.knn_predict(t, S, rrp, rids, rr, means, stds, bias, 3.0, 40, 1, ql, qr)
+        assert bitwise_equal(got, ref), name
     plan.close()
 
 

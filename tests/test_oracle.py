@@ -217,3 +217,50 @@ def test_slope_one_accuracy_regression(ml100k_folds):
 
     r, m = _cv(ml100k_folds, fp)
     assert r <= 0.946 + EPS and m <= 0.743 + EPS, (r, m)
+
+
+def test_go_sort_restatement():
+    """knn.go:107-108's sort.Sort (Go 1.24 pdqsort) as restated in oracle.c: a descending permutation for
+    random, sorted, reversed and tie-heavy keys; identity where pdqsort provably returns early (already
+    sorted input, all keys equal: partialInsertionSort finds no inversion); insertion sort, hence stable,
+    up to 12 elements; and the C++ mirror's template (host/gosort.hpp) leaves the same permutation."""
+    import subprocess
+    import tempfile
+    rng = np.random.default_rng(3)
+    cases = []
+    for n in (0, 1, 2, 5, 12, 13, 49, 50, 51, 200, 1000, 4097):
+        cases += [rng.integers(0, 3, n).astype(float), rng.random(n), np.sort(rng.integers(0, 5, n)).astype(float),
+                  np.sort(rng.integers(0, 5, n))[::-1].astype(float), np.ones(n)]
+    for k in cases:
+        p = O.go_sort_desc(k)
+        assert sorted(p.tolist()) == list(range(len(k)))
+        assert np.all(np.diff(k[p]) <= 0)
+        if len(k) and (np.all(k == k[0]) or np.all(np.diff(k) <= 0)):
+            assert np.array_equal(p, np.arange(len(k)))
+        if len(k) <= 12:
+            assert np.array_equal(p, np.argsort(-k, kind="stable"))
+    src = os.path.join(os.path.dirname(__file__), "..", "recommend-sys_amd", "host")
+    prog = r'''
+#include "gosort.hpp"
+#include <cstdio>
+#include <utility>
+#include <vector>
+int main() {
+    std::vector<double> k; double x;
+    while (std::scanf("%lf", &x) == 1) k.push_back(x);
+    std::vector<long> p(k.size());
+    for (size_t i = 0; i < k.size(); ++i) p[i] = static_cast<long>(i);
+    core::gosort::sort(static_cast<int64_t>(k.size()), [&](int64_t a, int64_t b) { return k[p[a]] > k[p[b]]; },
+                       [&](int64_t a, int64_t b) { std::swap(p[a], p[b]); });
+    for (long v : p) std::printf("%ld\n", v);
+}
+'''
+    with tempfile.TemporaryDirectory() as d:
+        with open(os.path.join(d, "t.cpp"), "w") as fh:
+            fh.write(prog)
+        exe = os.path.join(d, "t")
+        subprocess.run(["g++", "-O1", "-std=c++17", f"-I{src}", os.path.join(d, "t.cpp"), "-o", exe], check=True)
+        for k in cases[::3]:
+            out = subprocess.run([exe], input="\n".join(repr(float(v)) for v in k), capture_output=True,
+                                 text=True, check=True).stdout.split()
+            assert np.array_equal(np.array([int(v) for v in out], np.int64), O.go_sort_desc(k))
