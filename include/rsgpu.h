@@ -152,6 +152,10 @@ int rs_last_kernel_ms(const rs_ctx* ctx, double* ms);
  * other estimator call on the ctx (or rs_close) frees it, RSGPU_FIT_CACHE=0 turns it off. */
 int rs_svd_fit(rs_ctx* ctx, const rs_ratings* r, const rs_sgd_params* p, double* P, double* Q,
                double* bu, double* bi, double* gb);
+/* Divergence refits of the last rs_svd_fit on this ctx (FAST tile schedule): a fit whose model left the
+ * fixed-point range or went non-finite is redone from the caller's inputs on half the workgroups (less
+ * Hogwild staleness on the hot item rows), up to three times, before RS_ERR_NUMERIC is returned. */
+int rs_fit_refits(const rs_ctx* ctx, int32_t* n);
 
 /* core/svd.go:32-51 for n (inner user, inner item) pairs; -1 = unknown id (data.go:129). */
 int rs_svd_predict(rs_ctx* ctx, int64_t n, const int32_t* users, const int32_t* items,
@@ -260,8 +264,10 @@ int rs_svd_plan_set_mode(rs_svd_plan* plan, int32_t write_back, int32_t ring_dep
  * 8 or 16; default 16), ratings per tile (0 = nnz / workgroups, bounded by the 160 KiB LDS), run cap
  * (an item's run in a tile longer than this is cut into pieces on different waves; 0 = auto: hot items
  * cut so that ~100 of an item's updates are in flight; a huge value = never; ignored with
- * one wave), ring (q_i rows each wave loads ahead, in runs: 0 = auto = 2, else 2, 3, 4, 6, 8 or 12, clamped
- * for wide rows; deeper rings read hot rows earlier, i.e. staler).  Rebuilds the schedule. */
+ * one wave), ring (q_i rows each wave loads ahead, in runs: 0 = auto = 2; with claimed runs (the default,
+ * rs_svd_plan_set_tile_claim) 2, or 3 for k <= 126; with host-dealt runs 2 or 4, and 3, 6, 8, 12 for
+ * k <= 126; other values round down; deeper rings read hot rows earlier, i.e. staler).  Rebuilds the
+ * schedule. */
 int rs_svd_plan_set_tiles(rs_svd_plan* plan, int32_t workgroups, int32_t waves, int32_t target,
                           int32_t run_cap, int32_t ring);
 /* Work distribution inside a tile: runs_per_claim = 4 (default) or 8 -- the tile's runs form one queue
@@ -390,6 +396,22 @@ int rs_svd_plan_apply_delta(rs_svd_plan* plan, const void* dP, const void* gbsum
  * pieces of ~64 MiB of Q per rank-block).  rs_svd_fit_multi picks it when n_items < n_users. */
 #define RS_EXCHANGE_ROTATE_Q 2
 int rs_svd_plan_set_exchange(rs_svd_plan* plan, int32_t mode);
+/* RS_EXCHANGE_ROTATE_Q on Zipf-headed sets: a stratum (one rank's users x one item block) holds an item's
+ * ratings n_blocks-fold concentrated, so the head's rows get many concurrent runs in flight (Hogwild staleness
+ * that diverges at lr 0.005; configs[4]: the hottest item is 0.8 % of the set but 12.7 % of its stratum).  An
+ * item whose share of its stratum would pass `share` (default 0.02) -- when strata hold at least min_stratum
+ * ratings (default 2^17) -- is split: one row copy per item block, its ratings dealt to the copies by user
+ * hash (each copy trained in its block's strata, travelling with the block; as few copies as bring the
+ * item's share under `share`), the copies merged once per epoch into the item's row on every rank as the
+ * last merged value plus w x the sum of the copies' moves since: RS_HOT_SCALED (default) w = kappa / c with
+ * kappa = (1 - (1 - lr)^(c n)) / (1 - (1 - lr)^n), c copies of n ratings each per epoch (the ratio of what
+ * sequential SGD over all c n ratings and what one copy closes of a unit-curvature gap: c for lightly trained
+ * copies, 1 for converged ones); RS_HOT_AVERAGE w = 1 / c (the copies' mean); RS_HOT_SUM w = 1 (diverges on
+ * the Zipf head: measured).  share = 0 turns it off.  Set before the join. */
+#define RS_HOT_SCALED 0
+#define RS_HOT_AVERAGE 1
+#define RS_HOT_SUM 2
+int rs_svd_plan_set_hot_split(rs_svd_plan* plan, double share, int64_t min_stratum, int32_t merge);
 /* Diagnostic: one epoch of the plan with each user block / stratum of its tile schedule (a joined plan's,
  * or rs_svd_plan_set_user_blocks') launched alone and timed -- ms[b] = block b's SGD kernel in
  * milliseconds (n >= the plan's blocks).  It trains the model like an epoch.  Used to table the

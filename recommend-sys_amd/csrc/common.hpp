@@ -23,6 +23,7 @@ struct rs_ctx {
     double last_kernel_ms = 0.0;
     std::shared_ptr<void> svd_fit_cache;  // rs_svd_fit: the last FAST plan and the COO it was built from
     std::shared_ptr<void> staging;        // pinned host ring of the streamed Sims download (sim.hip)
+    int32_t fit_refits = 0;               // divergence refits of the last rs_svd_fit (rs_fit_refits)
 };
 
 namespace rs {

@@ -38,6 +38,7 @@
 #include <dlfcn.h>
 
 #include <algorithm>
+#include <cmath>
 #include <atomic>
 #include <condition_variable>
 #include <cstdlib>
@@ -70,6 +71,7 @@ struct LocalGroup {  // host-barrier exchange between the shards of one process
     std::vector<double*> gbs;
     std::vector<float*> P;    // ROTATE: every shard's P (rank-blocks are pulled from the neighbour)
     std::vector<float*> Q;    // ROTATE_Q: every shard's Q
+    std::vector<float*> hot;  // ROTATE_Q: every shard's partial hot-copy averages
     std::vector<int> dev;
     void barrier() {
         std::unique_lock<std::mutex> l(m);
@@ -96,6 +98,8 @@ struct ShardComm {
     int32_t mode = RS_EXCHANGE_ROTATE;
     int32_t pieces = 1;  // ROTATE / ROTATE_Q: user / item blocks per rank-block
     std::vector<int32_t> owner;  // ROTATE_Q: the ranks' user ranges [owner[r], owner[r + 1])
+    DevBuf<float> hot_part, hot_avg;  // ROTATE_Q hot copies: this rank's summed moves, over all ranks (H x ld)
+    DevBuf<float> hot_w;              // merge weight per hot item
     ncclComm_t nccl = nullptr;
     bool own_nccl = true;
     std::atomic<bool> aborted{false};
@@ -192,6 +196,64 @@ __global__ void local_gb_fold_kernel(Srcs src, int32_t n_src, int32_t nb, double
         for (int32_t r = 0; r < n_src; ++r)
             for (int32_t b = 0; b < nb; ++b) t += src.g[r][b];
         gb[0] += t * inv_total;
+    }
+}
+
+// ROTATE_Q hot copies (rows n_items + b H + h of Q, int32 fixed point during a call).  Seed: every copy takes
+// its item's canonical row.
+__global__ __launch_bounds__(256) void hot_seed_kernel(int32_t* __restrict__ Q, const int32_t* __restrict__ hot,
+                                                       int32_t H, int32_t nb, int32_t n_items, int32_t ld) {
+    const int64_t n = static_cast<int64_t>(nb) * H * ld;
+    for (int64_t t = static_cast<int64_t>(blockIdx.x) * 256 + threadIdx.x; t < n; t += static_cast<int64_t>(gridDim.x) * 256) {
+        const int64_t row = t / ld;  // b H + h
+        const int32_t c = static_cast<int32_t>(t - row * ld), h = static_cast<int32_t>(row % H);
+        Q[(n_items + row) * ld + c] = Q[static_cast<int64_t>(hot[h]) * ld + c];
+    }
+}
+// Partial merge of the copies of blocks [b0, b1): out[h][c] = the sum of the copies' moves since the last merge
+// (copy - the item's row, which holds the last merged value on every rank and is never trained), fp32 from
+// the fixed point; summed over the ranks, the merged row is the last value + w_h x that sum.
+// the copy of hot item h in block b is in use (hot_copy_used: its ratings are dealt there)
+__device__ __host__ inline bool hot_copy_used(int32_t b, int32_t nb, int2 meta) {
+    const int32_t stride = nb / meta.y, off = (b - meta.x + nb) % nb;
+    return off % stride == 0 && off / stride < meta.y;
+}
+__global__ __launch_bounds__(256) void hot_partial_kernel(const int32_t* __restrict__ Q, const int32_t* __restrict__ hot,
+                                                          const int2* __restrict__ meta, int32_t H, int32_t nb,
+                                                          int32_t n_items, int32_t ld, int32_t b0, int32_t b1,
+                                                          float* __restrict__ out) {
+    const int64_t n = static_cast<int64_t>(H) * ld;
+    for (int64_t t = static_cast<int64_t>(blockIdx.x) * 256 + threadIdx.x; t < n; t += static_cast<int64_t>(gridDim.x) * 256) {
+        const int64_t h = t / ld;
+        const int32_t c = static_cast<int32_t>(t - h * ld);
+        const int2 m = meta[h];
+        const int32_t base = Q[static_cast<int64_t>(hot[h]) * ld + c];
+        float acc = 0.f;
+        for (int32_t b = b0; b < b1; ++b)
+            if (hot_copy_used(b, nb, m)) acc += static_cast<float>(Q[(n_items + static_cast<int64_t>(b) * H + h) * ld + c] - base);
+        out[t] = acc * kFxInv;
+    }
+}
+// every copy of blocks [b0, b1) and the item's row take the merged value, last + w_h x the summed moves (back to
+// the fixed point)
+__global__ __launch_bounds__(256) void hot_write_kernel(int32_t* __restrict__ Q, const int32_t* __restrict__ hot,
+                                                        int32_t H, int32_t n_items, int32_t ld, int32_t b0, int32_t b1,
+                                                        const float* __restrict__ w, const float* __restrict__ moves) {
+    const int64_t n = static_cast<int64_t>(H) * ld;
+    for (int64_t t = static_cast<int64_t>(blockIdx.x) * 256 + threadIdx.x; t < n; t += static_cast<int64_t>(gridDim.x) * 256) {
+        const int64_t h = t / ld;
+        const int32_t c = static_cast<int32_t>(t - h * ld);
+        const int32_t v = __float2int_rn(w[h] * moves[t] * kFx) + Q[static_cast<int64_t>(hot[h]) * ld + c];
+        Q[static_cast<int64_t>(hot[h]) * ld + c] = v;
+        for (int32_t b = b0; b < b1; ++b) Q[(n_items + static_cast<int64_t>(b) * H + h) * ld + c] = v;
+    }
+}
+// in-process exchange: out = sum over the shards (shard order) of their partial averages
+__global__ __launch_bounds__(256) void hot_sum_kernel(Srcs src, int32_t n_src, int64_t n, float* __restrict__ out) {
+    for (int64_t t = static_cast<int64_t>(blockIdx.x) * 256 + threadIdx.x; t < n; t += static_cast<int64_t>(gridDim.x) * 256) {
+        float a = reinterpret_cast<const float*>(src.p[0])[t];
+        for (int32_t r = 1; r < n_src; ++r) a += reinterpret_cast<const float*>(src.p[r])[t];
+        out[t] = a;
     }
 }
 
@@ -292,9 +354,49 @@ void shard_setup(rs_svd_plan* pl, ShardComm& c, int32_t n_blocks, const std::vec
     if (rq) {
         pl->iblock_bounds = user_block_bounds(cum.data(), n_rows, nbk);
         pl->ublock_bounds.clear();
+        // hot items: share of their stratum (tot_i / N of the stratum's total / (N nbk)) above hot_share, when
+        // strata are large enough for it to matter (the same rule on every rank: global counts)
+        pl->hot_items.clear();
+        pl->hot_count.clear();
+        // copies per hot item: as few as bring its share of a stratum under hot_share (each copy takes
+        // 1 / copies of its ratings; averaged copies learn about copies-fold slower, so no more than needed)
+        const double stratum = c.total_nnz / (static_cast<double>(c.nranks) * nbk);
+        std::vector<int2> meta;
+        if (pl->hot_share > 0.0 && stratum >= static_cast<double>(pl->hot_min_stratum) && c.total_nnz > 0)
+            for (int32_t x = 0; x < n_rows; ++x) {
+                const double share = tot[x] * nbk / c.total_nnz;
+                if (share <= pl->hot_share) continue;
+                const int32_t copies = static_cast<int32_t>(std::min<double>(nbk, std::ceil(share / pl->hot_share)));
+                const int32_t nat = static_cast<int32_t>(std::upper_bound(pl->iblock_bounds.begin(), pl->iblock_bounds.end(), x) -
+                                                         pl->iblock_bounds.begin()) - 1;
+                pl->hot_items.push_back(x);
+                pl->hot_count.push_back(tot[x]);
+                meta.push_back(make_int2(nat, copies));
+            }
+        pl->hot_meta_h = meta;
+        const int32_t H = static_cast<int32_t>(pl->hot_items.size());
+        const size_t rows = static_cast<size_t>(std::max(1, pl->n_items)) + static_cast<size_t>(nbk) * H;
+        if (pl->Q.n != rows * pl->ld) {  // room for the copies after the item rows (item rows kept)
+            (void)buffer_bytes32(rows * pl->ld, sizeof(float), "item factor matrix with hot copies");
+            DevBuf<float> q2(rows * pl->ld);
+            const size_t keep = static_cast<size_t>(std::max(1, pl->n_items)) * pl->ld;
+            RS_HIP(hipMemcpyAsync(q2.p, pl->Q.p, keep * sizeof(float), hipMemcpyDeviceToDevice, pl->ctx->stream));
+            RS_HIP(hipMemsetAsync(q2.p + keep, 0, (q2.n - keep) * sizeof(float), pl->ctx->stream));
+            RS_HIP(hipStreamSynchronize(pl->ctx->stream));
+            pl->Q = std::move(q2);
+        }
+        pl->hot_rows.alloc(static_cast<size_t>(std::max(1, H)));
+        pl->hot_rows.upload(pl->hot_items.data(), static_cast<size_t>(H), pl->ctx->stream);
+        pl->hot_meta.alloc(static_cast<size_t>(std::max(1, H)));
+        pl->hot_meta.upload(meta.data(), static_cast<size_t>(H), pl->ctx->stream);
+        if (H > 0) {
+            c.hot_part.alloc(static_cast<size_t>(H) * pl->ld);
+            c.hot_avg.alloc(static_cast<size_t>(H) * pl->ld);
+        }
     } else {
         pl->ublock_bounds = user_block_bounds(cum.data(), n_rows, nbk);
         pl->iblock_bounds.clear();
+        pl->hot_items.clear();
     }
     if (c.nccl && c.nranks > 1 && pl->tile_wg == 0) {  // leave CUs to the collective's workgroups
         int cus = 0;
@@ -416,7 +518,32 @@ void epochs_rotate(rs_svd_plan* pl, int32_t n_epochs, float lr, float reg, hipSt
     const bool rq = c.mode == RS_EXCHANGE_ROTATE_Q;
     float* const M = rq ? pl->Q.p : pl->P.p;  // the factor matrix whose blocks rotate (Q: int32 bits in a call)
     const double inv_total = c.total_nnz > 0 ? 1.0 / c.total_nnz : 0.0;
+    const int32_t H = rq ? static_cast<int32_t>(pl->hot_items.size()) : 0;  // hot copies (sgd_plan.hpp)
+    int32_t* const Qi = reinterpret_cast<int32_t*>(pl->Q.p);
+    // the copy rows of blocks [b0, b1) (ROTATE_Q with hot items): they travel with their blocks
+    auto copy_rows = [&](int32_t b0, int32_t b1) {
+        return RowRange{pl->Q.p + (static_cast<int64_t>(pl->n_items) + static_cast<int64_t>(b0) * H) * pl->ld,
+                        static_cast<size_t>(b1 - b0) * H * pl->ld};
+    };
     q_convert(pl, s, 1);
+    if (H > 0) {  // merge weights of the summed moves (RS_HOT_*), then every copy starts from its item's row
+        // RS_HOT_SCALED: n = an item's ratings per copy and epoch; the copies each closed 1 - (1 - lr)^n of a unit-
+        // curvature gap (the bias column's, svd.go:108-112), sequential SGD over all c n ratings would close
+        // 1 - (1 - lr)^(c n): kappa = their ratio (c for few ratings per copy, 1 for copies that converged), w = kappa / c
+        std::vector<float> w(static_cast<size_t>(H));
+        for (int32_t x = 0; x < H; ++x) {
+            const double cp = pl->hot_meta_h[x].y, n = pl->hot_count[x] / cp, a = std::max(1e-12, 1.0 - static_cast<double>(lr));
+            const double kappa = (1.0 - std::pow(a, cp * n)) / std::max(1e-300, 1.0 - std::pow(a, n));
+            w[x] = static_cast<float>(pl->hot_merge == RS_HOT_SUM ? 1.0 : pl->hot_merge == RS_HOT_AVERAGE ? 1.0 / cp
+                                                                                                           : kappa / cp);
+        }
+        if (c.hot_w.n < static_cast<size_t>(H)) c.hot_w.alloc(static_cast<size_t>(H));
+        c.hot_w.upload(w.data(), w.size(), s);
+        RS_HIP(hipStreamSynchronize(s));  // w dies with this scope
+        hipLaunchKernelGGL(hot_seed_kernel, dim3(grid_for(static_cast<int64_t>(nb) * H * pl->ld)), dim3(256), 0, s, Qi,
+                           pl->hot_rows.p, H, nb, pl->n_items, pl->ld);
+        RS_HIP(hipGetLastError());
+    }
     for (int32_t e = 0; e < n_epochs; ++e) {
         for (int32_t st = 0; st < N; ++st) {
             const RotStep rs = rotation_step(g, N, st);
@@ -443,6 +570,11 @@ void epochs_rotate(rs_svd_plan* pl, int32_t n_epochs, float lr, float reg, hipSt
                     check_nccl(ncclGroupStart(), "ncclGroupStart");
                     if (out.n) check_nccl(ncclSend(out.p, out.n, ncclFloat32, prev, c.nccl, c.cs), "ncclSend(block)");
                     if (in.n) check_nccl(ncclRecv(in.p, in.n, ncclFloat32, next, c.nccl, c.cs), "ncclRecv(block)");
+                    if (H > 0) {  // the block's hot copies ride along
+                        const RowRange co = copy_rows(b, b + 1), ci = copy_rows(b_in, b_in + 1);
+                        check_nccl(ncclSend(co.p, co.n, ncclFloat32, prev, c.nccl, c.cs), "ncclSend(hot copies)");
+                        check_nccl(ncclRecv(ci.p, ci.n, ncclFloat32, next, c.nccl, c.cs), "ncclRecv(hot copies)");
+                    }
                     check_nccl(ncclGroupEnd(), "ncclGroupEnd");
                     RS_HIP(hipEventRecord(c.ev_recv[b_in], c.cs));
                     c.pending[b_in] = 1;
@@ -455,9 +587,52 @@ void epochs_rotate(rs_svd_plan* pl, int32_t n_epochs, float lr, float reg, hipSt
                 const RowRange in = rank_block_rows(pl, M, rb_in, h);
                 const float* src = (rq ? lg.Q : lg.P)[next] + (in.p - M);
                 if (in.n) RS_HIP(hipMemcpyPeerAsync(in.p, lg.dev[g], src, lg.dev[next], in.n * sizeof(float), s));
+                if (H > 0) {
+                    const RowRange ci = copy_rows(rb_in * h, rb_in * h + h);
+                    RS_HIP(hipMemcpyPeerAsync(ci.p, lg.dev[g], lg.Q[next] + (ci.p - M), lg.dev[next], ci.n * sizeof(float), s));
+                }
                 RS_HIP(hipStreamSynchronize(s));
                 lg.barrier();  // every pull done: the next sub-epoch may write these rows
             }
+        }
+        // hot copies: after N sub-epochs rank g holds item rank-block g again; its copies' partial average
+        // (1 / nb of each copy) is summed over the ranks and written to the copies it holds and to every hot
+        // item's own row (the row Predict and the download read)
+        if (H > 0) {
+            const int32_t b0 = g * h, b1 = g * h + h;
+            const int64_t hn = static_cast<int64_t>(H) * pl->ld;
+            for (int32_t b = b0; c.nccl && b < b1; ++b)
+                if (c.pending[b]) {
+                    RS_HIP(hipStreamWaitEvent(s, c.ev_recv[b], 0));
+                    c.pending[b] = 0;
+                }
+            hipLaunchKernelGGL(hot_partial_kernel, dim3(grid_for(hn)), dim3(256), 0, s, Qi, pl->hot_rows.p, pl->hot_meta.p,
+                               H, nb, pl->n_items, pl->ld, b0, b1, c.hot_part.p);
+            RS_HIP(hipGetLastError());
+            const float* avg = c.hot_part.p;
+            if (c.nccl && N > 1) {
+                RS_HIP(hipEventRecord(c.ev_gb, s));
+                RS_HIP(hipStreamWaitEvent(c.cs, c.ev_gb, 0));
+                check_nccl(ncclAllReduce(c.hot_part.p, c.hot_avg.p, static_cast<size_t>(hn), ncclFloat32, ncclSum, c.nccl,
+                                         c.cs), "ncclAllReduce(hot copies)");
+                RS_HIP(hipEventRecord(c.ev_epoch, c.cs));
+                RS_HIP(hipStreamWaitEvent(s, c.ev_epoch, 0));
+                avg = c.hot_avg.p;
+            } else if (c.local && N > 1) {
+                LocalGroup& lg = *c.local;
+                RS_HIP(hipStreamSynchronize(s));
+                lg.barrier();  // every shard's partial is in place
+                Srcs src{};
+                for (int r = 0; r < lg.n; ++r) src.p[r] = reinterpret_cast<const float4*>(lg.hot[r]);
+                hipLaunchKernelGGL(hot_sum_kernel, dim3(grid_for(hn)), dim3(256), 0, s, src, lg.n, hn, c.hot_avg.p);
+                RS_HIP(hipGetLastError());
+                RS_HIP(hipStreamSynchronize(s));
+                lg.barrier();  // every shard has read every partial
+                avg = c.hot_avg.p;
+            }
+            hipLaunchKernelGGL(hot_write_kernel, dim3(grid_for(hn)), dim3(256), 0, s, Qi, pl->hot_rows.p, H, pl->n_items,
+                               pl->ld, b0, b1, c.hot_w.p, avg);
+            RS_HIP(hipGetLastError());
         }
         // GlobalBias: every stratum's partial, folded once per epoch on every rank
         if (c.nccl && N > 1) {
@@ -631,6 +806,7 @@ void group_join(rs_svd_group* g, int32_t n_blocks) {
             g->local->gbs.push_back(pl->shard->gbs.p);
             g->local->P.push_back(pl->P.p);
             g->local->Q.push_back(pl->Q.p);
+            g->local->hot.push_back(pl->shard->hot_part.p);
             g->local->dev.push_back(pl->ctx->device);
         }
     }
@@ -712,6 +888,7 @@ extern "C" int rs_svd_plan_set_user_blocks(rs_svd_plan* pl, int32_t n_blocks, co
         if (bounds) pl->ublock_bounds.assign(bounds, bounds + n_blocks + 1);
         else pl->ublock_bounds.clear();
         pl->iblock_bounds.clear();  // a ROTATE_Q group's strata end here too
+        pl->hot_items.clear();
         if (pl->write_back == RS_SGD_WB_TILE) {
             rs::tile_build(pl);
             pl->n_blocks = rs::tile_partials(pl);
@@ -767,6 +944,16 @@ extern "C" int rs_svd_plan_time_blocks(rs_svd_plan* pl, float lr, float reg, dou
         for (hipEvent_t e : ev) (void)hipEventDestroy(e);
         return RS_OK;
     });
+}
+
+extern "C" int rs_svd_plan_set_hot_split(rs_svd_plan* pl, double share, int64_t min_stratum, int32_t merge) {
+    if (!pl || !(share >= 0.0) || min_stratum < 0 || merge < RS_HOT_SCALED || merge > RS_HOT_SUM)
+        return rs::set_error(pl ? pl->ctx : nullptr, RS_ERR_INVALID, "bad arguments");
+    if (pl->shard) return rs::set_error(pl->ctx, RS_ERR_INVALID, "plan is joined to a group (leave first)");
+    pl->hot_share = share;
+    pl->hot_min_stratum = min_stratum;
+    pl->hot_merge = merge;
+    return RS_OK;
 }
 
 extern "C" int rs_svd_plan_inject_fault(rs_svd_plan* pl, int32_t sub_epoch) {

@@ -2048,6 +2048,12 @@ static bool fit_cache_on() {
 constexpr int64_t kFitCacheMaxNnz = int64_t{1} << 26;
 }  // namespace rs
 
+extern "C" int rs_fit_refits(const rs_ctx* ctx, int32_t* n) {
+    if (!ctx || !n) return rs::set_error(nullptr, RS_ERR_INVALID, "bad arguments");
+    *n = ctx->fit_refits;
+    return RS_OK;
+}
+
 extern "C" int rs_svd_fit(rs_ctx* ctx, const rs_ratings* r, const rs_sgd_params* p, double* P,
                           double* Q, double* bu, double* bi, double* gb) {
     if (!ctx) return rs::set_error(ctx, RS_ERR_INVALID, "ctx is NULL");
@@ -2104,11 +2110,15 @@ extern "C" int rs_svd_fit(rs_ctx* ctx, const rs_ratings* r, const rs_sgd_params*
                 }
             }
             rs_svd_plan& pl = *cache->plan;
+            ctx->fit_refits = 0;
             // Divergence guard (tile schedule): a fit that leaves the fixed-point range or goes non-finite is
-            // redone from the caller's inputs (still intact: nothing is written back before the check) with
-            // the run cap halved -- shorter runs of the hot items, less staleness -- up to
-            // three times; the plan keeps the lower cap for later fits of the same ratings.  Only then does
-            // the caller see RS_ERR_NUMERIC (a Go Fit that panics on an error never gets a NaN model first).
+            // redone from the caller's inputs (still intact: nothing is written back before the check) on half
+            // the workgroups, up to three times.  What diverges is a hot item's q_i / b_i under Hogwild
+            // staleness: the updates other workgroups apply between a run's read of the row and its write
+            // grow with the chip-wide update rate, i.e. with the workgroups in flight,
+            // and halving them halves that staleness.  The plan keeps the smaller grid for later fits of the
+            // same ratings.  Only then does the caller see RS_ERR_NUMERIC (a Go Fit that panics on an error
+            // never gets a NaN model first).
             for (int attempt = 0;; ++attempt) {
                 if (p->n_epochs > 0) *gb = rs::gb_warm_start(r, bu, bi);
                 mark("warm");
@@ -2118,13 +2128,13 @@ extern "C" int rs_svd_fit(rs_ctx* ctx, const rs_ratings* r, const rs_sgd_params*
                 rs::plan_epochs(&pl, p->n_epochs, lr, reg, ctx->stream);
                 rs::kernel_span_end(ctx);
                 mark("epochs");
-                if (wb != RS_SGD_WB_TILE || attempt == 3 || pl.tile_waves <= 1 || !rs::plan_diverged(&pl)) break;
-                const int32_t cap = rs::tile_cap_in_use(&pl);
-                if (cap <= 1) break;
-                pl.tile_run_cap = cap / 2;
+                if (wb != RS_SGD_WB_TILE || attempt == 3 || !rs::plan_diverged(&pl)) break;
+                if (pl.tile_grid <= 1) break;
+                pl.tile_wg = std::max(1, pl.tile_grid / 2);
                 rs::tile_build(&pl);
                 pl.n_blocks = rs::tile_partials(&pl);
-                if (trace) std::fprintf(stderr, "fit-trace diverged: refit with run cap %d\n", pl.tile_run_cap);
+                ++ctx->fit_refits;
+                if (trace) std::fprintf(stderr, "fit-trace diverged: refit on %d workgroups\n", pl.tile_wg);
             }
             rs::plan_download(&pl, P, Q, bu, bi, gb);
             mark("download");

@@ -103,6 +103,18 @@ struct rs_svd_plan {
     // tiles are built per stratum -- block b's tiles hold this plan's ratings of items
     // [iblock_bounds[b], iblock_bounds[b+1]) over all its users -- instead of per user block
     std::vector<int32_t> iblock_bounds;
+    // hot items of a ROTATE_Q shard (multi.hip): a stratum concentrates an item's ratings n_blocks-fold, and a
+    // Zipf head then holds a large share of one stratum's runs in flight at once (Hogwild staleness beyond
+    // what lr tolerates).  Each hot item gets one row copy per item block (rows n_items + b * H + h, h < H),
+    // its ratings dealt to the copies by user hash, and the copies are averaged once per epoch.
+    std::vector<int32_t> hot_items;      // canonical ids (H = size)
+    rs::DevBuf<int32_t> hot_rows;        // the same on the device
+    std::vector<int2> hot_meta_h;        // per hot item {natural block, copies in use}
+    rs::DevBuf<int2> hot_meta;
+    double hot_share = 0.02;             // an item is hot above this share of its stratum's ratings ...
+    int64_t hot_min_stratum = int64_t{1} << 17;  // ... when strata hold at least this many ratings (0 share: off)
+    int32_t hot_merge = RS_HOT_SCALED;  // how the copies merge once per epoch
+    std::vector<double> hot_count;       // every hot item's ratings over all ranks
     std::vector<int32_t> t_block_split;  // block b's split users: t_split_rows[t_block_split[b], t_block_split[b+1])
     std::shared_ptr<rs::ShardComm> shard;  // item-sharded multi-GPU state (multi.hip), or empty
     int32_t exchange = RS_EXCHANGE_ROTATE;  // the multi-GPU exchange a join sets up

@@ -103,6 +103,7 @@ __global__ __launch_bounds__(NW * 64) void svd_epoch_tile_kernel(
 #pragma clang fp contract(fast)
     constexpr int LD = 64 * E, NT = NW * 64;  // LD: LDS row (k + 2 columns fit); ldm: the rows in HBM
     constexpr bool TIMED = (DIAG & 16) != 0;  // per-wave phase clocks into dbg (experiments)
+    constexpr bool SPAN = (DIAG & 32) != 0;   // per-wave start / end clocks only (no extra waits)
     static_assert(CH == 0 || (CH > RQ && CH >= 2 && CH < 64), "a claimed chunk must outlast the ring");
     int64_t tm_stage = 0, tm_ring = 0, tm_loop = 0, tm_tail = 0, tm_c = 0;
     auto clk = [] { return static_cast<int64_t>(__builtin_amdgcn_s_memtime()); };
@@ -127,6 +128,7 @@ __global__ __launch_bounds__(NW * 64) void svd_epoch_tile_kernel(
     }
     auto qaddr = [&](int32_t row, int x) { return (row >= 0 && qoff[x] >= 0) ? row + qoff[x] : kOutOfRange; };
     double contrib = 0.0;
+    const int64_t t_begin = SPAN ? clk() : 0;
 
     for (int32_t t = static_cast<int32_t>(blockIdx.x); t < n_tiles; t += static_cast<int32_t>(gridDim.x)) {
         if constexpr (TIMED) tm_c = clk();
@@ -384,6 +386,16 @@ __global__ __launch_bounds__(NW * 64) void svd_epoch_tile_kernel(
         if constexpr (TIMED) tm_tail += clk() - tm_c;
     }
     if (lane == 0) gb_partial[static_cast<int64_t>(blockIdx.x) * NW + w] = contrib;
+    if constexpr (SPAN) {
+        const int64_t t_end = clk();
+        if (lane == 0) {
+            int64_t* d = dbg + (static_cast<int64_t>(blockIdx.x) * NW + w) * 4;
+            d[0] = t_begin;
+            d[1] = t_end;
+            d[2] = static_cast<int64_t>(__builtin_amdgcn_s_getreg((20 << 0) | (0 << 6) | (3 << 11)));  // XCC_ID (XCD)
+            d[3] = static_cast<int64_t>(static_cast<uint32_t>(__builtin_amdgcn_s_getreg((4 << 0) | (0 << 6) | (31 << 11))));  // HW_ID
+        }
+    }
     if constexpr (TIMED) {
         if (lane == 0) {
             int64_t* d = dbg + (static_cast<int64_t>(blockIdx.x) * NW + w) * 4;
@@ -653,10 +665,13 @@ void build_tile_host(const rs_svd_plan* pl, int32_t u_begin, int32_t u_end, int3
         // pieces that go to different waves (two pieces in one wave's ring reach would read q_i
         // before the earlier piece's atomic landed).
         if (claim) {
-            // Claimed runs: one queue.  Piece pc of an item of `pieces` sits at queue position
-            // (pc + key / 2^32) / pieces, so an item's pieces are n_runs / pieces apart (the waves take
-            // them at different times, far outside one wave's ring reach) and single runs keep their
-            // pseudo-random key order.
+            // Claimed runs: one queue in the per-tile pseudo-random key order, an item's pieces next to each
+            // other (consecutive claims: the waves take them at about the same time, as the host deal's
+            // streams did).  Measured on a hot-headed set (942k ratings, hottest item 1.95 %, k = 100,
+            // scripts/experiments/exp_stability.py): pieces spread evenly over the queue instead -- each
+            // tile then holds one of the item's runs in flight most of the time -- diverged at epoch 3-4 with
+            // chunks of 4 and of 8; adjacent pieces train as the host deal does (10-epoch held-out 0.683 /
+            // 0.683 against 0.686 for the reference order), at the same ML-1M epoch time.
             struct QE { uint64_t at; int32_t sl, pc, pieces; };
             std::vector<QE> qv;
             qv.reserve(nd);
@@ -664,8 +679,7 @@ void build_tile_host(const rs_svd_plan* pl, int32_t u_begin, int32_t u_end, int3
                 const int32_t sl = static_cast<int32_t>(ord[d]);
                 const size_t c = static_cast<size_t>(dcnt[sl]);
                 const int32_t pieces = static_cast<int32_t>(cap ? std::min<size_t>((c + cap - 1) / cap, static_cast<size_t>(nw)) : 1);
-                for (int32_t pc = 0; pc < pieces; ++pc)
-                    qv.push_back({((static_cast<uint64_t>(pc) << 32) + key[sl]) / static_cast<uint64_t>(pieces), sl, pc, pieces});
+                for (int32_t pc = 0; pc < pieces; ++pc) qv.push_back({key[sl], sl, pc, pieces});
             }
             std::stable_sort(qv.begin(), qv.end(), [](const QE& x, const QE& y) { return x.at < y.at; });
             int32_t rec = 0;
@@ -861,16 +875,28 @@ void build_tile_strata(const rs_svd_plan* pl, int32_t grid0, bool want_pos, Tile
                        std::vector<int32_t>& block_tile, std::vector<int32_t>* block_split) {
     const std::vector<int32_t>& ib = pl->iblock_bounds;
     const int32_t nb = static_cast<int32_t>(ib.size()) - 1, nu = pl->n_users;
-    std::vector<int32_t> blk(static_cast<size_t>(std::max(1, pl->n_items)), 0);
+    const int32_t H = static_cast<int32_t>(pl->hot_items.size());
+    std::vector<int32_t> blk(static_cast<size_t>(std::max(1, pl->n_items)), 0), hidx(blk.size(), -1);
     for (int32_t b = 0; b < nb; ++b)
         for (int32_t x = ib[b]; x < ib[b + 1]; ++x) blk[x] = b;
+    for (int32_t h = 0; h < H; ++h) hidx[pl->hot_items[h]] = h;
+    // a rating's stratum, and the Q row it trains: a hot item's rating goes to block mix32(user) mod nb and to
+    // that block's copy of the item
+    auto block_of = [&](int32_t u, int32_t item) {  // copy j of `copies`, blocks nb / copies apart from the natural one
+        const int32_t h = hidx[item];
+        if (h < 0) return blk[item];
+        const int2 m = pl->hot_meta_h[h];
+        const int32_t j = static_cast<int32_t>(mix32(static_cast<uint64_t>(u) * 0x9E3779B97F4A7C15ULL) % static_cast<uint32_t>(m.y));
+        return (m.x + j * (nb / m.y)) % nb;
+    };
+    auto row_of = [&](int32_t b, int32_t item) { return hidx[item] < 0 ? item : pl->n_items + b * H + hidx[item]; };
     block_tile.assign(1, 0);
     if (block_split) block_split->assign(1, 0);
     const std::vector<int64_t>& rp = pl->h_rowptr;
     for (int32_t b = 0; b < nb; ++b) {
         rs_svd_plan sub;
         sub.n_users = nu;
-        sub.n_items = pl->n_items;
+        sub.n_items = pl->n_items + nb * H;  // the copies' rows
         sub.k = pl->k;
         sub.tile_waves = pl->tile_waves;
         sub.tile_claim = pl->tile_claim;
@@ -880,7 +906,7 @@ void build_tile_strata(const rs_svd_plan* pl, int32_t grid0, bool want_pos, Tile
         parallel_ranges(nu, 16, [&](int64_t u0, int64_t u1) {
             for (int64_t u = u0; u < u1; ++u) {
                 int64_t c = 0;
-                for (int64_t q = rp[u]; q < rp[u + 1]; ++q) c += blk[pl->h_cols[q]] == b;
+                for (int64_t q = rp[u]; q < rp[u + 1]; ++q) c += block_of(static_cast<int32_t>(u), pl->h_cols[q]) == b;
                 sub.h_rowptr[u + 1] = c;
             }
         });
@@ -893,8 +919,8 @@ void build_tile_strata(const rs_svd_plan* pl, int32_t grid0, bool want_pos, Tile
             for (int64_t u = u0; u < u1; ++u) {
                 int64_t o = sub.h_rowptr[u];
                 for (int64_t q = rp[u]; q < rp[u + 1]; ++q)
-                    if (blk[pl->h_cols[q]] == b) {
-                        sub.h_cols[o] = pl->h_cols[q];
+                    if (block_of(static_cast<int32_t>(u), pl->h_cols[q]) == b) {
+                        sub.h_cols[o] = row_of(b, pl->h_cols[q]);
                         sub.h_vals[o] = pl->h_vals[q];
                         if (want_pos) orig[o] = q;
                         ++o;
@@ -1055,7 +1081,7 @@ static void tile_launch_r(rs_svd_plan* pl, float lr, float reg, hipStream_t s, f
     const bool claim = pl->tile_claim > 0;
     if constexpr (E == 2 && NW == 16) {  // diagnostics (RSGPU_TILE_DIAG, experiments only): bits drop
         static const int diag = std::getenv("RSGPU_TILE_DIAG") ? std::atoi(std::getenv("RSGPU_TILE_DIAG")) : 0;
-        if (diag == 16 && pl->trace.n < static_cast<size_t>(pl->tile_grid) * NW * 4) {
+        if ((diag & 48) && pl->trace.n < static_cast<size_t>(pl->tile_grid) * NW * 4) {
             pl->trace.alloc(static_cast<size_t>(pl->tile_grid) * NW * 4);
             RS_HIP(hipMemsetAsync(pl->trace.p, 0, pl->trace.n * 8, s));
         }
@@ -1068,26 +1094,28 @@ static void tile_launch_r(rs_svd_plan* pl, float lr, float reg, hipStream_t s, f
             case -1: return tile_launch_t<E, NW, 2, 4, 1>(pl, lr, reg, s, dP, tr);
             case -3: return tile_launch_t<E, NW, 2, 4, 3>(pl, lr, reg, s, dP, tr);
             case -16: return tile_launch_t<E, NW, 2, 4, 16>(pl, lr, reg, s, dP, tr);
+            case -32: return tile_launch_t<E, NW, 2, 4, 32>(pl, lr, reg, s, dP, tr);
             default: break;
         }
     }
-    if (claim) {
-        const bool big = pl->tile_claim >= 8;
-        if (want <= 2) return big ? tile_launch_t<E, NW, 2, 8>(pl, lr, reg, s, dP, tr)
-                                  : tile_launch_t<E, NW, 2, 4>(pl, lr, reg, s, dP, tr);
-        return big ? tile_launch_t<E, NW, 3, 8>(pl, lr, reg, s, dP, tr) : tile_launch_t<E, NW, 3, 4>(pl, lr, reg, s, dP, tr);
+    if (claim) {  // chunks of 8 runs and rings of 3 are instantiated for the bench's rows (E <= 2) only
+        if constexpr (E <= 2) {
+            const bool big = pl->tile_claim >= 8;
+            if (want <= 2) return big ? tile_launch_t<E, NW, 2, 8>(pl, lr, reg, s, dP, tr)
+                                      : tile_launch_t<E, NW, 2, 4>(pl, lr, reg, s, dP, tr);
+            return big ? tile_launch_t<E, NW, 3, 8>(pl, lr, reg, s, dP, tr) : tile_launch_t<E, NW, 3, 4>(pl, lr, reg, s, dP, tr);
+        } else {
+            return tile_launch_t<E, NW, 2, 4>(pl, lr, reg, s, dP, tr);
+        }
     }
-    if constexpr (kMax >= 12) {
+    // the host-dealt schedule (round 3; tile_claim = 0): rings 2 and 4, and 3 / 6 / 8 / 12 for E = 2
+    if constexpr (E == 2) {
         if (want >= 12) return tile_launch_t<E, NW, 12, 0>(pl, lr, reg, s, dP, tr);
-    }
-    if constexpr (kMax >= 8) {
         if (want >= 8) return tile_launch_t<E, NW, 8, 0>(pl, lr, reg, s, dP, tr);
-    }
-    if constexpr (kMax >= 6) {
         if (want >= 6) return tile_launch_t<E, NW, 6, 0>(pl, lr, reg, s, dP, tr);
+        if (want == 3) return tile_launch_t<E, NW, 3, 0>(pl, lr, reg, s, dP, tr);
     }
-    if (want <= 2) return tile_launch_t<E, NW, 2, 0>(pl, lr, reg, s, dP, tr);
-    if (want == 3) return tile_launch_t<E, NW, 3, 0>(pl, lr, reg, s, dP, tr);
+    if (want <= 3) return tile_launch_t<E, NW, 2, 0>(pl, lr, reg, s, dP, tr);
     if constexpr (kMax >= 4) {
         return tile_launch_t<E, NW, 4, 0>(pl, lr, reg, s, dP, tr);
     } else {

@@ -46,7 +46,8 @@ HEADER_SYMBOLS = (
     "rs_svd_plan_set_user_blocks", "rs_svd_group_create", "rs_svd_group_epochs", "rs_svd_group_destroy",
     "rs_item_shards", "rs_svd_fit_multi", "rs_tile_schedule_host", "rs_svd_plan_set_exchange",
     "rs_comm_info", "rs_rotation_step", "rs_svd_plan_shard_info", "rs_svd_plan_inject_fault",
-    "rs_svd_plan_time_blocks", "rs_knn_plan_set_tie_order",
+    "rs_svd_plan_time_blocks", "rs_knn_plan_set_tie_order", "rs_fit_refits",
+    "rs_svd_plan_set_hot_split",
 )
 COMM_ID_BYTES = 128
 
@@ -168,6 +169,8 @@ def lib():
             "rs_svd_plan_inject_fault": (C.c_int, [_vp, _i32]),
             "rs_svd_plan_time_blocks": (C.c_int, [_vp, _flt, _flt, _vp, _i32]),
             "rs_knn_plan_set_tie_order": (C.c_int, [_vp, _i32]),
+            "rs_fit_refits": (C.c_int, [_vp, C.POINTER(_i32)]),
+            "rs_svd_plan_set_hot_split": (C.c_int, [_vp, _dbl, _i64, _i32]),
             "rs_comm_info": (C.c_int, [C.POINTER(_i32), _vp, _i32]),
             "rs_rotation_step": (C.c_int, [_i32, _i32, _i32, _vp]),
             "rs_svd_plan_shard_info": (C.c_int, [_vp, C.POINTER(_i32), C.POINTER(_i32), C.POINTER(_i32),
@@ -323,6 +326,12 @@ class Context:
 
     # ---- estimators --------------------------------------------------------------------------
 
+    def fit_refits(self):
+        """Divergence refits (half the workgroups each) the last svd_fit made (rs_fit_refits)."""
+        n = _i32(0)
+        self.check(lib().rs_fit_refits(self.h, C.byref(n)))
+        return n.value
+
     def svd_fit(self, r: Ratings, P, Q, bu=None, bi=None, gb=0.0, n_epochs=20, lr=0.005,
                 reg=0.02, mode=SGD_FAST, write_back=WB_TILE):
         P = np.array(P, dtype=np.float64, order="C")
@@ -471,6 +480,11 @@ class SvdPlan:
         ms = np.zeros(n_blocks)
         self.ctx.check(lib().rs_svd_plan_time_blocks(self.h, lr, reg, _ptr(ms), n_blocks))
         return ms
+
+    def set_hot_split(self, share=0.02, min_stratum=1 << 17, merge=0):
+        """ROTATE_Q hot items split into per-block copies (rs_svd_plan_set_hot_split; merge 0 scaled, 1 average,
+        2 sum of moves); before the join."""
+        self.ctx.check(lib().rs_svd_plan_set_hot_split(self.h, share, min_stratum, merge))
 
     def inject_fault(self, sub_epoch):
         """Test hook: the next sharded call throws at that sub-epoch, once (rs_svd_plan_inject_fault)."""

@@ -35,12 +35,12 @@ def log(*a):
     print(f"[{time.strftime('%H:%M:%S')}]", *a, file=sys.stderr, flush=True)
 
 
-def generate(U, I, n, seed, threads=16):
+def generate(U, I, n, seed, threads=16, zipf=0.9):
     """n user ranges of near-equal users (rs_synth rows [lo, hi)), each with every 1024th rating held out."""
     parts = []
     for p in range(n):
         lo, hi = U * p // n, U * (p + 1) // n
-        s = rsgpu.Synth(U, I, mean_deg=100.0, sigma=1.0, min_deg=1, max_deg=I // 2, zipf_s=0.9, seed=seed,
+        s = rsgpu.Synth(U, I, mean_deg=100.0, sigma=1.0, min_deg=1, max_deg=I // 2, zipf_s=zipf, seed=seed,
                         user_lo=lo, user_hi=hi, n_threads=threads)
         deg = np.diff(s.rowptr)
         hold = np.zeros(s.nnz, bool)
@@ -73,14 +73,20 @@ def main():
     ap.add_argument("--epochs", type=int, default=5)
     ap.add_argument("--shards", type=int, default=8)
     ap.add_argument("--seed", type=int, default=20250826)
+    ap.add_argument("--zipf", type=float, default=0.9, help="item popularity exponent (0: uniform items)")
     ap.add_argument("--strata", action="store_true", help="time every stratum alone (one extra epoch per shard)")
     ap.add_argument("--no-whole", action="store_true", help="skip the single-plan fit")
+    ap.add_argument("--wg", type=int, default=0, help="workgroups per shard launch (0: one per CU)")
+    ap.add_argument("--blocks", type=int, default=0, help="item blocks in all (0: automatic)")
+    ap.add_argument("--hot-share", type=float, default=None, help="rs_svd_plan_set_hot_split share (default: library)")
+    ap.add_argument("--hot-min", type=int, default=None, help="rs_svd_plan_set_hot_split min stratum ratings")
+    ap.add_argument("--hot-merge", type=int, default=None, help="0 scaled (default), 1 average, 2 sum")
     args = ap.parse_args()
     U, I, k, n = args.users, args.items, args.k, args.shards
 
     ctx = rsgpu.Context(0)
     t0 = time.perf_counter()
-    parts = generate(U, I, n, args.seed)
+    parts = generate(U, I, n, args.seed, zipf=args.zipf)
     t_gen = time.perf_counter() - t0
     hu = np.concatenate([p["hu"] for p in parts])
     hi_ = np.concatenate([p["hi_"] for p in parts])
@@ -124,10 +130,15 @@ def main():
     for p in parts:
         pl = ctx.svd_plan_csr(U, I, padded_rowptr(p, U), p["cols"], p["vals"], k)
         pl.set_exchange(rsgpu.EXCHANGE_ROTATE_Q)
+        if args.wg:
+            pl.set_tiles(workgroups=args.wg)
+        if args.hot_share is not None or args.hot_min is not None or args.hot_merge is not None:
+            pl.set_hot_split(0.02 if args.hot_share is None else args.hot_share,
+                             (1 << 17) if args.hot_min is None else args.hot_min, args.hot_merge or 0)
         pl.init_normal(0.0, 0.1, seed=1)
         pl.upload(gb=gb0)
         plans.append(pl)
-    g = rsgpu.SvdGroup(plans, n_blocks=0)
+    g = rsgpu.SvdGroup(plans, n_blocks=args.blocks)
     t_join = time.perf_counter() - t0
     _, _, exch, nblk = plans[0].shard_info()
     log(f"{n} shard plans + group in {t_join:.1f} s: exchange {exch}, {nblk} item blocks")

@@ -1,0 +1,125 @@
+"""Experiment (round 4): FAST tile schedule stability at library defaults across set sizes, hot-item shares
+and k (VERDICT r3 "make the FAST default stable by rule").  rs_synth sets (lognormal user degrees, Zipf
+items), 5 % held out, device init N(0, 0.1), GlobalBias = training mean; held-out RMSE after every epoch,
+the run cap the library chose, and -- where the oracle is affordable -- the sequential reference
+(core/svd.go:92-130, user-major CSR order, same init) beside it.
+
+    python scripts/experiments/exp_stability.py [case ...] [--claim 0|4|8] [--cap C]
+"""
+import argparse
+import os
+import sys
+import time
+
+import numpy as np
+
+REPO = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+sys.path[:0] = [os.path.join(REPO, "recommend-sys_amd"), os.path.join(REPO, "oracle")]
+import rsgpu  # noqa: E402
+
+# name: (users, items, mean degree, zipf s, k, epochs, oracle)
+CASES = {
+    "1m_k64": (20000, 4000, 60.0, 0.9, 64, 10, True),
+    "1m_k64_hot": (20000, 4000, 60.0, 1.1, 64, 10, True),
+    "1m_k100_hot": (20000, 2000, 50.0, 1.2, 100, 10, True),
+    "8m_k100": (100000, 20000, 80.0, 0.9, 100, 8, False),
+    "8m_k256_hot": (200000, 10000, 40.0, 1.1, 256, 5, False),
+    "32m_k100": (400000, 50000, 80.0, 1.0, 100, 5, False),
+    "128m_k256": (1250000, 125000, 100.0, 0.9, 256, 4, False),
+}
+
+
+def run(ctx, name, claim, cap, log, wg=0):
+    U, I, deg, zs, k, ep, with_oracle = CASES[name]
+    t0 = time.time()
+    s = rsgpu.Synth(U, I, mean_deg=deg, zipf_s=zs, seed=20250901, n_threads=16)
+    d = np.diff(s.rowptr)
+    users = np.repeat(np.arange(U, dtype=np.int32), d)
+    hold = np.random.default_rng(0).random(s.nnz) < 0.05
+    keep = ~hold
+    rp = np.concatenate([[0], np.cumsum(np.bincount(users[keep], minlength=U))]).astype(np.int64)
+    cols, vals = s.cols[keep].copy(), s.vals[keep].copy()
+    hu, hi, hr = users[hold], s.cols[hold].copy(), s.vals[hold].astype(np.float64)
+    s.close()
+    nnz = len(cols)
+    hot = int(np.bincount(cols, minlength=I).max())
+    plan = ctx.svd_plan_csr(U, I, rp, cols, vals, k)
+    plan.set_tile_claim(claim)
+    if cap or wg:
+        plan.set_tiles(workgroups=wg, run_cap=cap)
+    plan.init_normal(0.0, 0.1, seed=1)
+    gb0 = float(np.mean(vals, dtype=np.float64))
+    plan.upload(gb=gb0)
+    ref_curve = None
+    if with_oracle:
+        import oracle as O
+        P0, Q0, bu0, bi0, _ = plan.download()
+        uu = np.repeat(np.arange(U, dtype=np.int32), np.diff(rp))
+        P, Q, bu, bi, g = P0, Q0, bu0, bi0, gb0
+        ref_curve = []
+        for _ in range(ep):
+            P, Q, bu, bi, g = O.svd_fit(uu, cols.astype(np.int32), vals.astype(np.float64), P, Q, bu, bi, g, epochs=1)
+            ref_curve.append(float(np.sqrt(np.mean((O.svd_predict(hu, hi, P, Q, bu, bi, g) - hr) ** 2))))
+    r0 = plan.evaluate(hu, hi, hr)[0]
+    curve = []
+    plan.set_timing(True)
+    ms = 0.0
+    for _ in range(ep):
+        plan.epochs(1)
+        m, _n = plan.last_kernel_ms()
+        ms += m
+        curve.append(plan.evaluate(hu, hi, hr)[0])
+    try:
+        plan.download()
+        numeric = "ok"
+    except rsgpu.RsError as e:
+        numeric = f"RS_ERR {e.code}"
+    plan.close()
+    log(f"{name:12s} claim {claim} cap {cap or 'auto'} wg {wg or 'all'}: nnz {nnz} hottest {hot} ({100.0 * hot / nnz:.2f} %) k {k} "
+        f"epoch {ms / ep:.2f} ms  held-out {r0:.4f} -> " + " ".join(f"{x:.4f}" for x in curve) +
+        (("  | reference " + " ".join(f"{x:.4f}" for x in ref_curve)) if ref_curve else "") +
+        f"  [{numeric}, {time.time() - t0:.0f} s]")
+
+
+def run_fit(ctx, name, log):
+    """The Go drop-in (rs_svd_fit: host COO in, guarded refits) on the same set: held-out RMSE and refits."""
+    U, I, deg, zs, k, ep, _ = CASES[name]
+    s = rsgpu.Synth(U, I, mean_deg=deg, zipf_s=zs, seed=20250901, n_threads=16)
+    users = np.repeat(np.arange(U, dtype=np.int32), np.diff(s.rowptr))
+    hold = np.random.default_rng(0).random(s.nnz) < 0.05
+    keep = ~hold
+    u, i, r = users[keep], s.cols[keep].copy(), s.vals[keep].astype(np.float64)
+    hu, hi, hr = users[hold], s.cols[hold].copy(), s.vals[hold].astype(np.float64)
+    s.close()
+    rng = np.random.default_rng(1)
+    P0, Q0 = rng.normal(0, 0.1, (U, k)), rng.normal(0, 0.1, (I, k))
+    t0 = time.time()
+    try:
+        got = ctx.svd_fit(rsgpu.Ratings(u, i, r, U, I), P0, Q0, n_epochs=ep)
+        import oracle as O
+        e = float(np.sqrt(np.mean((O.svd_predict(hu, hi, *got) - hr) ** 2)))
+        res = f"held-out RMSE after {ep} epochs {e:.4f}"
+    except rsgpu.RsError as x:
+        res = f"RS_ERR {x.code}"
+    log(f"{name:12s} rs_svd_fit: {res}, refits {ctx.fit_refits()} ({time.time() - t0:.1f} s)")
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("cases", nargs="*", default=list(CASES))
+    ap.add_argument("--claim", type=int, default=4)
+    ap.add_argument("--cap", type=int, default=0)
+    ap.add_argument("--wg", type=int, default=0, help="workgroups (0: one per CU)")
+    ap.add_argument("--fit", action="store_true", help="through rs_svd_fit (the guarded Go drop-in)")
+    args = ap.parse_args()
+    ctx = rsgpu.Context(0)
+    for c in args.cases:
+        if args.fit:
+            run_fit(ctx, c, lambda m: print(m, flush=True))
+        else:
+            run(ctx, c, args.claim, args.cap, lambda m: print(m, flush=True), args.wg)
+    ctx.close()
+
+
+if __name__ == "__main__":
+    main()
