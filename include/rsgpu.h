@@ -289,7 +289,8 @@ int rs_svd_plan_tile_order(rs_svd_plan* plan, int64_t* pos, int64_t* work_off, i
  * {staging, q-ring waits, rating loops, write-back} shader cycles per wave, up to n int64 values. */
 int rs_svd_plan_tile_clocks(rs_svd_plan* plan, int64_t* out, int64_t n);
 /* Diagnostic, host only (no device needed): builds the tile schedule of a user-CSR the way a plan
- * would (workgroups, waves, user blocks) and reports
+ * would (workgroups, waves, user blocks; n_blocks < 0: -n_blocks item blocks, a ROTATE_Q shard's strata)
+ * and reports
  * its host time in ms, the tile count and, for non-NULL outputs, the visit order pos (nnz user-CSR
  * positions, as rs_svd_plan_tile_order) and the tiles' first records tile_off (n_tiles + 1); rank (nnz)
  * is zero-filled.  svdpp must be 0: the SVD++ tile schedule it selected was removed in round 3

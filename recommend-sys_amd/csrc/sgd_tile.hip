@@ -482,9 +482,25 @@ void build_tile_host(const rs_svd_plan* pl, int32_t u_begin, int32_t u_end, int3
             total += x.e - x.b;
             bytes += static_cast<double>(ld) * 4 + 16.0 * static_cast<double>(x.e - x.b);
         }
-        const int64_t n0 = std::max<int64_t>(
-            {1, (total + target - 1) / std::max<int64_t>(target, 1),
-             static_cast<int64_t>(std::ceil(bytes / (0.85 * static_cast<double>(kTileLdsBudget))))});
+        const int64_t n_target = (total + target - 1) / std::max<int64_t>(target, 1);
+        const int64_t n_lds = static_cast<int64_t>(std::ceil(bytes / (0.85 * static_cast<double>(kTileLdsBudget))));
+        const int64_t n0 = std::max<int64_t>({1, n_target, n_lds});
+        if (n_lds > 64 && n_lds >= 4 * n_target) {
+            // LDS-bound (many tiles per workgroup, e.g. a ROTATE_Q stratum of 10M users' ratings): the launch
+            // balances itself over the tiles, so fill tiles in user order to the LDS instead of LPT (which took
+            // ~1 s per configs[4] stratum for nothing)
+            int64_t users = 0, recs = 0;
+            for (size_t x = 0; x < ents.size(); ++x) {
+                const int64_t d = ents[x].e - ents[x].b;
+                if (users > 0 && tile_bytes(users + 1, recs + d, recs + d, ld) > kTileLdsBudget) {
+                    tb.push_back(x);
+                    users = recs = 0;
+                }
+                ++users;
+                recs += d;
+            }
+            if (!ents.empty()) tb.push_back(ents.size());
+        } else {
         std::vector<size_t> order(ents.size());
         std::iota(order.begin(), order.end(), size_t{0});
         std::stable_sort(order.begin(), order.end(), [&](size_t a, size_t b) {
@@ -593,6 +609,7 @@ void build_tile_host(const rs_svd_plan* pl, int32_t u_begin, int32_t u_end, int3
             tb.push_back(sorted.size());
         }
         ents.swap(sorted);
+        }
     }
     tmark("refine");
     const size_t nt = tb.size() - 1;
@@ -893,6 +910,12 @@ void build_tile_strata(const rs_svd_plan* pl, int32_t grid0, bool want_pos, Tile
     block_tile.assign(1, 0);
     if (block_split) block_split->assign(1, 0);
     const std::vector<int64_t>& rp = pl->h_rowptr;
+    if (nb > 65535) throw std::invalid_argument("ROTATE_Q: at most 65535 item blocks");
+    std::vector<uint16_t> rb(static_cast<size_t>(pl->nnz));  // every rating's block, one pass
+    parallel_ranges(nu, 16, [&](int64_t u0, int64_t u1) {
+        for (int64_t u = u0; u < u1; ++u)
+            for (int64_t q = rp[u]; q < rp[u + 1]; ++q) rb[q] = static_cast<uint16_t>(block_of(static_cast<int32_t>(u), pl->h_cols[q]));
+    });
     for (int32_t b = 0; b < nb; ++b) {
         rs_svd_plan sub;
         sub.n_users = nu;
@@ -906,7 +929,7 @@ void build_tile_strata(const rs_svd_plan* pl, int32_t grid0, bool want_pos, Tile
         parallel_ranges(nu, 16, [&](int64_t u0, int64_t u1) {
             for (int64_t u = u0; u < u1; ++u) {
                 int64_t c = 0;
-                for (int64_t q = rp[u]; q < rp[u + 1]; ++q) c += block_of(static_cast<int32_t>(u), pl->h_cols[q]) == b;
+                for (int64_t q = rp[u]; q < rp[u + 1]; ++q) c += rb[q] == b;
                 sub.h_rowptr[u + 1] = c;
             }
         });
@@ -919,7 +942,7 @@ void build_tile_strata(const rs_svd_plan* pl, int32_t grid0, bool want_pos, Tile
             for (int64_t u = u0; u < u1; ++u) {
                 int64_t o = sub.h_rowptr[u];
                 for (int64_t q = rp[u]; q < rp[u + 1]; ++q)
-                    if (block_of(static_cast<int32_t>(u), pl->h_cols[q]) == b) {
+                    if (rb[q] == b) {
                         sub.h_cols[o] = row_of(b, pl->h_cols[q]);
                         sub.h_vals[o] = pl->h_vals[q];
                         if (want_pos) orig[o] = q;
@@ -1190,7 +1213,7 @@ extern "C" int rs_tile_schedule_host(int32_t n_users, int32_t n_items, const int
                                      int32_t n_blocks, int32_t svdpp, int64_t* pos, int64_t* tile_off,
                                      int32_t* rank, int32_t* n_tiles, double* ms) {
     if (n_users < 0 || n_items < 0 || !rowptr || n_factors < 1 || n_factors > 510 || workgroups < 1 ||
-        (waves != 1 && waves != 2 && waves != 4 && waves != 8 && waves != 16) || n_blocks < 1)
+        (waves != 1 && waves != 2 && waves != 4 && waves != 8 && waves != 16) || n_blocks == 0)
         return rs::set_error(nullptr, RS_ERR_INVALID, "bad tile schedule arguments");
     if (svdpp) return rs::set_error(nullptr, RS_ERR_UNSUPPORTED, "the SVD++ tile schedule was removed (round 3)");
     return rs_guard(nullptr, [&]() -> int {
@@ -1203,7 +1226,14 @@ extern "C" int rs_tile_schedule_host(int32_t n_users, int32_t n_items, const int
         pl.h_cols.assign(cols, cols + pl.nnz);
         pl.h_vals.assign(vals, vals + pl.nnz);
         pl.tile_waves = waves;
-        pl.tile_ublocks = n_blocks;
+        if (n_blocks > 0) {
+            pl.tile_ublocks = n_blocks;
+        } else {  // -n item blocks of near-equal ratings: a ROTATE_Q shard's strata (no hot split)
+            std::vector<int64_t> cum(static_cast<size_t>(n_items) + 1, 0);
+            for (int64_t q = 0; q < pl.nnz; ++q) cum[cols[q] + 1]++;
+            for (int32_t x = 0; x < n_items; ++x) cum[x + 1] += cum[x];
+            pl.iblock_bounds = rs::user_block_bounds(cum.data(), n_items, -n_blocks);
+        }
         const auto t0 = std::chrono::steady_clock::now();
         rs::TileHost th;
         std::vector<int32_t> bt, bu;

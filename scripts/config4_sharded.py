@@ -65,7 +65,7 @@ def padded_rowptr(part, U):
     return rp
 
 
-def main():
+def parse(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--users", type=int, default=10_000_000)
     ap.add_argument("--items", type=int, default=1_000_000)
@@ -81,9 +81,14 @@ def main():
     ap.add_argument("--hot-share", type=float, default=None, help="rs_svd_plan_set_hot_split share (default: library)")
     ap.add_argument("--hot-min", type=int, default=None, help="rs_svd_plan_set_hot_split min stratum ratings")
     ap.add_argument("--hot-merge", type=int, default=None, help="0 scaled (default), 1 average, 2 sum")
-    args = ap.parse_args()
-    U, I, k, n = args.users, args.items, args.k, args.shards
+    return ap.parse_args(argv)
 
+
+def run(args, say=log):
+    """The whole-set fit and the sharded fit of the same set; returns the summary dict (tests/ call this)."""
+    U, I, k, n = args.users, args.items, args.k, args.shards
+    global log
+    log = say
     ctx = rsgpu.Context(0)
     t0 = time.perf_counter()
     parts = generate(U, I, n, args.seed, zipf=args.zipf)
@@ -183,9 +188,9 @@ def main():
     sh["finite"] = finite
     out["sharded"] = sh
     print(json.dumps({"sharded": sh}), flush=True)
-    print(json.dumps(out), flush=True)
     ctx.close()
+    return out
 
 
 if __name__ == "__main__":
-    main()
+    print(json.dumps(run(parse())), flush=True)
