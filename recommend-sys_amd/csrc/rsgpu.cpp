@@ -39,7 +39,7 @@ void build_csr(int64_t nnz, int32_t n_rows, const int32_t* rows, const int32_t* 
     csr_build(nnz, n_rows, rows, cols, vals, 0, out.rowptr.data(), out.cols.data(), out.vals.data());
 }
 
-// mean(r - b_u - b_i) over fixed 2^16-rating chunks summed in order (independent of the thread count)
+// The buffer is sized to the request rounded up to 1 MiB (callers cap requests at 256 MiB, sgd_tile.hip).
 void* pinned_staging(size_t bytes) {
     struct Buf {
         void* p = nullptr;
@@ -50,13 +50,14 @@ void* pinned_staging(size_t bytes) {
         if (b.p) (void)hipHostFree(b.p);
         b.p = nullptr;
         b.n = 0;
-        const size_t n = std::max(bytes, size_t{1} << 20) * 5 / 4;
+        const size_t n = (bytes + (size_t{1} << 20) - 1) & ~((size_t{1} << 20) - 1);
         RS_HIP(hipHostMalloc(&b.p, n, hipHostMallocPortable));
         b.n = n;
     }
     return b.p;
 }
 
+// mean(r - b_u - b_i) over fixed 2^16-rating chunks summed in order (independent of the thread count)
 double gb_warm_start(const rs_ratings* r, const double* bu, const double* bi) {
     if (r->nnz <= 0) return 0.0;
     constexpr int64_t kChunk = int64_t{1} << 16;

@@ -17,8 +17,10 @@
 //           ceil(deg / item_cap) row copies, merged by count-weighted average after the epoch and
 //           re-broadcast: the float atomics of a hot row are spread over several rows, which the
 //           memory-side atomic unit otherwise serialises.  Off by default for the same reason.
-//   ORDERED one 16-lane group walks the ratings in train-set order with the exact update order of
-//           svd.go:93-129 (aliasing Q1: q_i is updated with the NEW p_u) -- factor parity (P1).
+//   ORDERED the ratings in train-set order with the exact update order of svd.go:93-129 (aliasing Q1:
+//           q_i is updated with the NEW p_u) -- factor parity (P1): conflict-free batches on one
+//           workgroup, sgd_ordered.hip.
+//   TILE    the FAST default since round 2: user tiles in LDS, per-(item, tile) runs, sgd_tile.hip.
 //
 // Device layout of the FAST plan (HBM, fp32): P is n_users x ld, Q is n_items x ld with
 // ld = 64 * ceil((k + 1) / 64); columns [0, k) hold the factors, column k holds the bias
@@ -812,82 +814,6 @@ __global__ __launch_bounds__(256) void pair_sum_kernel(const double* __restrict_
     }
 }
 
-// --------------------------------------------------------------------------------------------
-// ORDERED kernel: one 16-lane group, all epochs, reference visit and update order.
-
-template <int V>
-__global__ __launch_bounds__(64) void svd_ordered_kernel(
-    int64_t nnz, const int32_t* __restrict__ users, const int32_t* __restrict__ items,
-    const float* __restrict__ ratings, float* P, float* Q, float* bu, float* bi, int32_t ld,
-    double* gb_io, int32_t epochs, float lr, float reg) {
-#pragma clang fp contract(off)
-    constexpr int G = 16;
-    const int gl = threadIdx.x;
-    if (gl >= G) return;
-    const double lrd = lr, regd = reg;
-    bool act[V];
-#pragma unroll
-    for (int v = 0; v < V; ++v) act[v] = 4 * (gl + G * v) < ld;
-    double gb = gb_io[0];
-    for (int32_t epoch = 0; epoch < epochs; ++epoch) {       // svd.go:92
-        for (int64_t n = 0; n < nnz; ++n) {                   // svd.go:93
-            const int32_t u = users[n], i = items[n];
-            const float r = ratings[n];
-            float* prow = P + static_cast<int64_t>(u) * ld;   // svd.go:99-100 aliases
-            float* qrow = Q + static_cast<int64_t>(i) * ld;
-            float4 p[V], q[V];
-#pragma unroll
-            for (int v = 0; v < V; ++v) {
-                const int c = 4 * (gl + G * v);
-                p[v] = act[v] ? *reinterpret_cast<const float4*>(prow + c) : make_float4(0, 0, 0, 0);
-                q[v] = act[v] ? *reinterpret_cast<const float4*>(qrow + c) : make_float4(0, 0, 0, 0);
-            }
-            const float ub = bu[u], ib = bi[i];               // svd.go:97-98
-            float s = 0.f;
-#pragma unroll
-            for (int v = 0; v < V; ++v) s += dot4(p[v], q[v]);
-            s = group_sum<G>(s);
-            double pred = gb;                                 // Predict svd.go:35-48
-            pred += static_cast<double>(ub);
-            pred += static_cast<double>(ib);
-            pred += static_cast<double>(s);
-            const double diff = pred - static_cast<double>(r);
-            gb -= lrd * diff;                                 // svd.go:105-106
-            const float ub_new = static_cast<float>(ub - lrd * (diff + regd * ub));  // 108-109
-            const float ib_new = static_cast<float>(ib - lrd * (diff + regd * ib));  // 111-112
-            const float df = static_cast<float>(diff);
-#pragma unroll
-            for (int v = 0; v < V; ++v) {                     // svd.go:114-120
-                float4 a;
-                a.x = (q[v].x * df + p[v].x * reg) * lr;
-                a.y = (q[v].y * df + p[v].y * reg) * lr;
-                a.z = (q[v].z * df + p[v].z * reg) * lr;
-                a.w = (q[v].w * df + p[v].w * reg) * lr;
-                p[v].x -= a.x; p[v].y -= a.y; p[v].z -= a.z; p[v].w -= a.w;
-            }
-#pragma unroll
-            for (int v = 0; v < V; ++v) {                     // svd.go:122-128 (new p: Q1)
-                float4 a;
-                a.x = (p[v].x * df + q[v].x * reg) * lr;
-                a.y = (p[v].y * df + q[v].y * reg) * lr;
-                a.z = (p[v].z * df + q[v].z * reg) * lr;
-                a.w = (p[v].w * df + q[v].w * reg) * lr;
-                q[v].x -= a.x; q[v].y -= a.y; q[v].z -= a.z; q[v].w -= a.w;
-            }
-#pragma unroll
-            for (int v = 0; v < V; ++v) {
-                const int c = 4 * (gl + G * v);
-                if (act[v]) {
-                    *reinterpret_cast<float4*>(prow + c) = p[v];
-                    *reinterpret_cast<float4*>(qrow + c) = q[v];
-                }
-            }
-            bu[u] = ub_new;  // all 16 lanes store identical bits: each lane re-reads its own write
-            bi[i] = ib_new;
-        }
-    }
-    if (gl == 0) gb_io[0] = gb;
-}
 
 }  // namespace rs
 
@@ -1051,19 +977,6 @@ static void merge_split_rows(rs_svd_plan* pl, hipStream_t s) {
                            tile ? pl->t_split_rows.p : pl->split_rows.p, pl->ld);
 }
 
-static void launch_ordered(int64_t nnz, const int32_t* u, const int32_t* i, const float* r,
-                           float* P, float* Q, float* bu, float* bi, int32_t ld, double* gb,
-                           int32_t epochs, float lr, float reg, hipStream_t s) {
-    if (ld <= 64)
-        hipLaunchKernelGGL((svd_ordered_kernel<1>), dim3(1), dim3(16), 0, s, nnz, u, i, r, P, Q, bu, bi, ld, gb, epochs, lr, reg);
-    else if (ld <= 128)
-        hipLaunchKernelGGL((svd_ordered_kernel<2>), dim3(1), dim3(16), 0, s, nnz, u, i, r, P, Q, bu, bi, ld, gb, epochs, lr, reg);
-    else if (ld <= 256)
-        hipLaunchKernelGGL((svd_ordered_kernel<4>), dim3(1), dim3(16), 0, s, nnz, u, i, r, P, Q, bu, bi, ld, gb, epochs, lr, reg);
-    else
-        hipLaunchKernelGGL((svd_ordered_kernel<8>), dim3(1), dim3(16), 0, s, nnz, u, i, r, P, Q, bu, bi, ld, gb, epochs, lr, reg);
-    RS_HIP(hipGetLastError());
-}
 
 int32_t fast_ld(int32_t k) { return 64 * ((k + 1 + 63) / 64); }
 

@@ -129,6 +129,7 @@ __global__ __launch_bounds__(NW * 64) void svd_epoch_tile_kernel(
     auto qaddr = [&](int32_t row, int x) { return (row >= 0 && qoff[x] >= 0) ? row + qoff[x] : kOutOfRange; };
     double contrib = 0.0;
     const int64_t t_begin = SPAN ? clk() : 0;
+    const int64_t rt_begin = SPAN ? static_cast<int64_t>(__builtin_amdgcn_s_memrealtime()) : 0;  // 100 MHz, chip-wide
 
     for (int32_t t = static_cast<int32_t>(blockIdx.x); t < n_tiles; t += static_cast<int32_t>(gridDim.x)) {
         if constexpr (TIMED) tm_c = clk();
@@ -141,6 +142,36 @@ __global__ __launch_bounds__(NW * 64) void svd_epoch_tile_kernel(
         int32_t* Pl = lds;
         int2* Rl = reinterpret_cast<int2*>(Pl + nu * LD);
         int2* Ul = Rl + n_rec;
+        auto load_q = [&](int32_t (&q)[E], int32_t item) {
+            const int32_t row = item >= 0 ? item * (ldm * 4) : -1;  // SGPR arithmetic
+#pragma unroll
+            for (int x = 0; x < E; ++x)
+                q[x] = (DIAG & 2) ? 0
+                                  : static_cast<int32_t>(__builtin_amdgcn_raw_buffer_load_b32(rq, qaddr(row, x), 0, kSgdAux));
+        };
+        int32_t ring[RQ][E];
+        auto prefill = [&](auto&& item_at) {
+#pragma unroll
+            for (int s = 0; s < RQ; ++s) {
+                load_q(ring[s], item_at(s));
+                // dropped atomics (out-of-range offsets): the loop is entered with the same pattern of
+                // loads and atomics in flight as its back edge carries, so the compiler's vmcnt waits
+                // keep the whole ring in flight instead of draining to the prologue's count
+#pragma unroll
+                for (int x = 0; x < E; ++x) {  // per-lane offsets and value: not folded into one lane
+                    int32_t z;
+                    asm volatile("v_mov_b32 %0, 0" : "=v"(z));
+                    __builtin_amdgcn_raw_ptr_buffer_atomic_add_i32(z, rq, kOutOfRange + lane * 4 + 256 * x, 0, 0);
+                }
+            }
+        };
+        // claimed runs: the wave's first chunk (chunk w) comes from the run headers in HBM, so its q_i rows
+        // load while the tile is staged (one memory latency instead of two before the first run)
+        int2 hn0 = make_int2(-1, 0);
+        if constexpr (CH > 0) {
+            hn0 = tr[min(w * CH + lane, n_runs)];
+            prefill([&](int s) { return __builtin_amdgcn_readlane(hn0.x, s); });
+        }
         // stage the tile: P rows as int32 fixed point in the register layout above, records, runs
         for (int32_t x = tid; x < nu * LD; x += NT) {
             const int32_t ul = x / LD, c = x - ul * LD;
@@ -167,29 +198,6 @@ __global__ __launch_bounds__(NW * 64) void svd_epoch_tile_kernel(
             rb = j = first;
             rw0 = Rl[min(rb + lane, n_rec - 1)];
             rw1 = Rl[min(rb + 64 + lane, n_rec - 1)];
-        };
-        auto load_q = [&](int32_t (&q)[E], int32_t item) {
-            const int32_t row = item >= 0 ? item * (ldm * 4) : -1;  // SGPR arithmetic
-#pragma unroll
-            for (int x = 0; x < E; ++x)
-                q[x] = (DIAG & 2) ? 0
-                                  : static_cast<int32_t>(__builtin_amdgcn_raw_buffer_load_b32(rq, qaddr(row, x), 0, kSgdAux));
-        };
-        int32_t ring[RQ][E];
-        auto prefill = [&](auto&& item_at) {
-#pragma unroll
-            for (int s = 0; s < RQ; ++s) {
-                load_q(ring[s], item_at(s));
-                // dropped atomics (out-of-range offsets): the loop is entered with the same pattern of
-                // loads and atomics in flight as its back edge carries, so the compiler's vmcnt waits
-                // keep the whole ring in flight instead of draining to the prologue's count
-#pragma unroll
-                for (int x = 0; x < E; ++x) {  // per-lane offsets and value: not folded into one lane
-                    int32_t z;
-                    asm volatile("v_mov_b32 %0, 0" : "=v"(z));
-                    __builtin_amdgcn_raw_ptr_buffer_atomic_add_i32(z, rq, kOutOfRange + lane * 4 + 256 * x, 0, 0);
-                }
-            }
         };
         double gb = gb0;
         const float klr = lr * kFxInv * kFxInv;  // c = lr (s 2^-48 + gb - r): p and q in 2^-24 units
@@ -330,9 +338,8 @@ __global__ __launch_bounds__(NW * 64) void svd_epoch_tile_kernel(
             auto hx = [](const int2& h, int i) { return __builtin_amdgcn_readlane(h.x, i); };
             auto hy = [](const int2& h, int i) { return __builtin_amdgcn_readlane(h.y, i); };
             int32_t cn = w, claim = 0;
-            int2 hn = hdr(cn);
+            int2 hn = hn0;  // = hdr(cn), read from HBM before the staging barrier (its ring is in flight)
             int2 rwn = Rl[min(hy(hn, 0) + lane, n_rec - 1)];  // the next chunk's first record window
-            prefill([&](int s) { return hx(hn, s); });
             while (true) {
                 const int32_t cc = cn;
                 const int2 hc = hn;
@@ -392,8 +399,10 @@ __global__ __launch_bounds__(NW * 64) void svd_epoch_tile_kernel(
             int64_t* d = dbg + (static_cast<int64_t>(blockIdx.x) * NW + w) * 4;
             d[0] = t_begin;
             d[1] = t_end;
-            d[2] = static_cast<int64_t>(__builtin_amdgcn_s_getreg((20 << 0) | (0 << 6) | (3 << 11)));  // XCC_ID (XCD)
-            d[3] = static_cast<int64_t>(static_cast<uint32_t>(__builtin_amdgcn_s_getreg((4 << 0) | (0 << 6) | (31 << 11))));  // HW_ID
+            const int64_t rt_end = static_cast<int64_t>(__builtin_amdgcn_s_memrealtime());
+            const int64_t xcc = __builtin_amdgcn_s_getreg((20 << 0) | (0 << 6) | (3 << 11));  // XCC_ID (XCD)
+            d[2] = rt_begin;
+            d[3] = (rt_end - rt_begin) | (xcc << 48);
         }
     }
     if constexpr (TIMED) {
@@ -543,7 +552,8 @@ void build_tile_host(const rs_svd_plan* pl, int32_t u_begin, int32_t u_end, int3
         // tiles of many light users -- more shared items -- are cheaper than tiles of one heavy user).
         // Move users from the costliest tile to the cheapest while that lowers the maximum.
         const size_t nb = bins.size();
-        if (nb > 1 && nb <= 8192 && static_cast<double>(nb) * std::max(1, pl->n_items) <= 6.4e7) {
+        static const bool no_refine = std::getenv("RSGPU_TILE_NO_REFINE") != nullptr;  // (experiment, round 4)
+        if (!no_refine && nb > 1 && nb <= 8192 && static_cast<double>(nb) * std::max(1, pl->n_items) <= 6.4e7) {
             constexpr int64_t kRunCost = 3;
             std::vector<int32_t> cnt(nb * static_cast<size_t>(std::max(1, pl->n_items)), 0);
             std::vector<int64_t> runs(nb, 0), cost(nb, 0);

@@ -30,13 +30,7 @@ def take_shard(users, items, ratings, shard_of_item, rank):
 
 def user_weights(local_users, n_users, dist, device=None):
     """w_u = (ratings of u on this rank) / (ratings of u on all ranks); one all-reduce of counts."""
-    import torch
-    cnt = np.bincount(np.asarray(local_users, dtype=np.int64), minlength=n_users).astype(np.float64)
-    t = torch.tensor(cnt, dtype=torch.float64, device=device)
-    dist.all_reduce(t)
-    tot = t.cpu().numpy()
-    w = np.divide(cnt, tot, out=np.zeros_like(cnt), where=tot > 0)
-    return w.astype(np.float32), float(tot.sum())
+    return count_weights(np.bincount(np.asarray(local_users, dtype=np.int64), minlength=n_users), dist, device)
 
 
 class ItemShardedStep:

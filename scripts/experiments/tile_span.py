@@ -22,12 +22,21 @@ n = 256 * 16 * 4
 buf = np.zeros(n, np.int64)
 ctx.check(rsgpu.lib().rs_svd_plan_tile_clocks(plan.h, buf.ctypes.data, n))
 d = buf.reshape(256, 16, 4)
-t0 = d[:, :, 0].min()
-start, end = d[:, :, 0] - t0, d[:, :, 1] - t0
-xcd = d[:, 0, 2] & 15
-cu = (d[:, 0, 3] >> 8) & 15
+cyc = d[:, :, 1] - d[:, :, 0]           # shader-clock cycles per wave (s_memtime, per XCD)
+rt0 = d[:, :, 2]                         # s_memrealtime (100 MHz) at the wave's start
+rtl = d[:, :, 3] & ((1 << 48) - 1)       # ... and its length
+xcd = (d[:, 0, 3] >> 48) & 15
+t0 = rt0.min()
+start, end = rt0 - t0, rt0 - t0 + rtl
+cu = xcd * 0
 wg_end = end.max(1)
 wg_len = wg_end - start.min(1)
+print("real time (100 MHz ticks): kernel", int(end.max()), " WG start max", int(start.min(1).max()))
+ghz = cyc.max(1) / np.maximum(1, rtl.max(1)) / 10.0
+for x in range(8):
+    m = xcd == x
+    print(f"XCD {x}: clock {ghz[m].mean():.2f} GHz, WG real length mean {wg_len[m].mean():.0f} max {wg_len[m].max():.0f} "
+          f"end max {wg_end[m].max():.0f}")
 pos, off = plan.tile_order()
 order = np.argsort(u, kind="stable")
 ci, cu_ = i[order][pos], u[order][pos]
