@@ -13,10 +13,10 @@ N > 1 and no WORLD_SIZE starts the N rank processes itself from a parent that ma
 fails when fewer than N GPUs are visible.
 
 Extra fields of the same line:
-  strong_scaling  BASELINE configs[4]'s shape at 1/8 scale (1.25M users x 125k items x ~125M ratings,
-                  k = 256: the same ratings-per-user and so the same exchange-to-compute ratio as the
-                  10M x 1M x 1e9 set) split over the N ranks by item range -- the north_star scaling
-                  question; the driver's N = 1, 2, 4, 8 lines give its curve.
+  strong_scaling  BASELINE configs[4] at full size (10M users x 1M items x ~1e9 ratings, k = 256), user
+                  ranges over the N ranks with the Q item rank-blocks rotating (RS_EXCHANGE_ROTATE_Q) --
+                  the north_star scaling question; the driver's N = 1, 2, 4, 8 lines give its curve.
+                  About a minute at N = 1 (generation ~35 s, plan ~10-30 s, 4 epochs of ~0.6 s).
   ordered         N = 1: throughput of the ORDERED mode (the reference visit order, the mode that
                   meets north_star's 1e-5 factor contract) on the same ML-1M-shaped set.
 
@@ -66,27 +66,43 @@ def cpu_baseline(u, i, r, n_users, n_items, budget_s=10.0):
 
 
 def strong_scaling(ctx, rank, world, dist, dev, stream, epochs=3, warmup=1):
-    """configs[4] shape at 1/8 scale, items split over the ranks (rs_svd_plan_join when world > 1)."""
+    """BASELINE configs[4] at its own size: SVD nFactors=256 on the synthetic 10M users x 1M items x ~1e9
+    ratings set (rs_synth, seed 20250826 -- the set tests/test_config4_gpu.py fits), library defaults.  Rank r
+    generates and holds users [U r / N, U (r + 1) / N) (global ids, every item); with N > 1 the library's RCCL
+    communicator runs RS_EXCHANGE_ROTATE_Q (user ranges stay, the Q item rank-blocks rotate, N sub-epochs per
+    epoch; the Zipf head's items split into per-block copies merged once per epoch, csrc/multi.hip)."""
     import torch
     import rsgpu
-    n_users, n_items, k = 1_250_000, 125_000, 256
-    lo, hi = n_items * rank // world, n_items * (rank + 1) // world
+    n_users, n_items, k = 10_000_000, 1_000_000, 256
+    lo, hi = n_users * rank // world, n_users * (rank + 1) // world
     t0 = time.perf_counter()
-    s = rsgpu.Synth(n_users, n_items, mean_deg=100.0, seed=20250827, item_lo=lo, item_hi=hi, n_threads=16)
-    plan = ctx.svd_plan_csr(n_users, hi - lo, s.rowptr, s.cols - lo, s.vals, k)
+    s = rsgpu.Synth(n_users, n_items, mean_deg=100.0, sigma=1.0, min_deg=1, max_deg=n_items // 2, zipf_s=0.9,
+                    seed=20250826, user_lo=lo, user_hi=hi, n_threads=16)
+    rp = np.empty(n_users + 1, np.int64)  # this range's CSR as rows 0..U-1 (empty rows elsewhere)
+    rp[:lo + 1] = 0
+    rp[lo + 1:hi + 1] = s.rowptr[1:]
+    rp[hi + 1:] = s.rowptr[-1]
     nnz, vsum = s.nnz, float(np.sum(s.vals, dtype=np.float64))
+    probe_u = np.repeat(np.arange(lo, hi, dtype=np.int32), np.diff(s.rowptr))[:4096]
+    probe_i, probe_r = s.cols[:len(probe_u)].copy(), s.vals[:len(probe_u)].astype(np.float64)
+    gen_s = time.perf_counter() - t0
+    plan = ctx.svd_plan_csr(n_users, n_items, rp, s.cols, s.vals, k)
     s.close()
-    plan.init_normal(0.0, 0.1, seed=3)  # P rows keyed by row id: identical on every rank
+    del rp
+    plan.init_normal(0.0, 0.1, seed=1)  # rows drawn by row id: every rank's P / Q equal one plan's
     tot = torch.tensor([float(nnz), vsum], dtype=torch.float64, device=f"cuda:{dev}")
     if dist:
         dist.all_reduce(tot)
+    plan.upload(gb=float(tot[1] / tot[0]))  # the training mean: the same GlobalBias on every rank
+    if dist:
+        plan.set_exchange(rsgpu.EXCHANGE_ROTATE_Q)
         uid = [rsgpu.comm_unique_id() if rank == 0 else None]
         dist.broadcast_object_list(uid, src=0)
-        plan.upload(gb=float(tot[1] / tot[0]))  # the same GlobalBias on every rank
         plan.join(uid[0], rank, world)
+        _, _, _, n_blocks = plan.shard_info()
         run = lambda n: plan.epochs_sharded(n, LR, REG, stream)
     else:
-        plan.upload(gb=float(tot[1] / tot[0]))
+        n_blocks = 1
         run = lambda n: plan.epochs(n, LR, REG, stream)
     setup_s = time.perf_counter() - t0
     run(warmup)
@@ -105,17 +121,21 @@ def strong_scaling(ctx, rank, world, dist, dev, stream, epochs=3, warmup=1):
         t = torch.tensor([dt], dtype=torch.float64, device=f"cuda:{dev}")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         dt = float(t.item())
-    P, Q, bu, bi, gb = plan.download()
-    finite = bool(np.isfinite(P).all() and np.isfinite(Q).all() and np.isfinite(gb))
+    try:  # RMSE over this rank's first ratings: the device's fixed-point / non-finite check of the factors
+        finite = bool(np.isfinite(plan.evaluate(probe_u, probe_i, probe_r)[0]))
+    except rsgpu.RsError:
+        finite = False
     plan.close()
     total = int(tot[0].item())
-    return {"workload": "SVD nFactors=256, configs[4] shape at 1/8 scale: 1.25M users x 125k items, "
-                        f"{total} ratings (mean 100 per user, Zipf items), split by item range over "
-                        f"{world} GPU(s)", "scaling": "strong", "n_gpus": world, "epochs": epochs,
+    return {"workload": "BASELINE configs[4]: SVD nFactors=256 on the synthetic 10M users x 1M items x "
+                        f"{total} ratings set (rs_synth seed 20250826, lognormal user degrees mean 100, Zipf 0.9 "
+                        f"items), library defaults, user ranges over {world} GPU(s)",
+            "scaling": "strong", "n_gpus": world, "epochs": epochs, "warmup": warmup,
             "value": total * epochs / dt, "unit": "updates/s", "ms_per_epoch": dt / epochs * 1e3,
-            "setup_s_rank0": setup_s, "finite": finite,
-            "exchange": "rs_svd_plan_join + rs_svd_plan_epochs_sharded (stratum rotation: RCCL send/recv "
-                        "of P rank-blocks, piece by piece)" if world > 1 else "none (one GPU)"}
+            "gen_s_rank0": gen_s, "setup_s_rank0": setup_s, "finite": finite, "item_blocks": n_blocks,
+            "exchange": "rs_svd_plan_join + rs_svd_plan_epochs_sharded, RS_EXCHANGE_ROTATE_Q (RCCL send/recv of "
+                        "Q item rank-blocks, piece by piece; hot-copy merge by one all-reduce per epoch)"
+                        if world > 1 else "none (one GPU, one plan over the whole set)"}
 
 
 def ordered_throughput(ctx, u, i, r, n_users, n_items):
@@ -195,7 +215,7 @@ def main():
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-budget", type=float, default=10.0)
-    ap.add_argument("--no-strong", action="store_true", help="skip the configs[4]-shape strong-scaling field")
+    ap.add_argument("--no-strong", action="store_true", help="skip the configs[4] strong-scaling field")
     ap.add_argument("--no-ordered", action="store_true", help="skip the ORDERED-mode field")
     ap.add_argument("--launch-check", action="store_true",
                     help="CPU check of the N-rank launch: gloo ranks report themselves, no GPU work")

@@ -32,6 +32,12 @@ namespace rs {
 // its host COO copy and device buffers would otherwise outlive their use)
 inline void drop_fit_cache(rs_ctx* c) { c->svd_fit_cache.reset(); }
 inline void kernel_span_begin(rs_ctx* c) { (void)hipEventRecord(c->k0, c->stream); }
+inline void kernel_span_record(rs_ctx* c) { (void)hipEventRecord(c->k1, c->stream); }
+inline void kernel_span_wait(rs_ctx* c) {  // after kernel_span_record: waits for the bracket's end
+    float ms = 0.f;
+    if (hipEventSynchronize(c->k1) == hipSuccess && hipEventElapsedTime(&ms, c->k0, c->k1) == hipSuccess)
+        c->last_kernel_ms = ms;
+}
 inline void kernel_span_end(rs_ctx* c) {
     (void)hipEventRecord(c->k1, c->stream);
     float ms = 0.f;
@@ -124,7 +130,7 @@ void parallel_ranges(int64_t n, int max_threads, F&& f) {
 
 // Pinned host staging for large uploads: a per-thread page-locked buffer (grown on demand, kept for the
 // process) that the caller fills and DMAs from; the caller synchronises the stream before reuse.
-void* pinned_staging(size_t bytes);
+void* pinned_staging(size_t bytes, int slot = 0);  // slots 0 and 1: independent buffers
 
 // f64 host rows (stride k) <-> f32 padded rows (stride ld) with zero padding.
 void pack_rows_f32(const double* src, int64_t rows, int32_t k, int32_t ld, std::vector<float>& dst);

@@ -40,12 +40,13 @@ void build_csr(int64_t nnz, int32_t n_rows, const int32_t* rows, const int32_t* 
 }
 
 // The buffer is sized to the request rounded up to 1 MiB (callers cap requests at 256 MiB, sgd_tile.hip).
-void* pinned_staging(size_t bytes) {
+void* pinned_staging(size_t bytes, int slot) {
     struct Buf {
         void* p = nullptr;
         size_t n = 0;
     };
-    thread_local Buf b;  // (never freed: the process may outlive the HIP runtime's teardown order)
+    thread_local Buf bufs[2];  // (never freed: the process may outlive the HIP runtime's teardown order)
+    Buf& b = bufs[slot & 1];
     if (b.n < bytes) {
         if (b.p) (void)hipHostFree(b.p);
         b.p = nullptr;

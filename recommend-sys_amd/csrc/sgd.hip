@@ -48,6 +48,7 @@
 #include <numeric>
 #include <thread>
 #include <stdexcept>
+#include <type_traits>
 #include <vector>
 
 #include "common.hpp"
@@ -1217,6 +1218,7 @@ static void build_work(rs_svd_plan* pl) {
 // modes (the tile schedule, the default, has its own arrays).
 static void ensure_hybrid(rs_svd_plan* pl) {
     if (pl->hybrid_built) return;
+    ensure_host_csr(pl);
     hipStream_t s = pl->ctx->stream;
     // items / ratings padded by 128 entries: the kernels read 32-entry chunks up to two ahead
     // (entries < e + 96 for a row ending at e)
@@ -1268,6 +1270,150 @@ static void plan_build_csr(rs_ctx* ctx, int32_t n_users, int32_t n_items, UserCS
     RS_HIP(hipEventCreate(&pl->ev0));
     RS_HIP(hipEventCreate(&pl->ev1));
     RS_HIP(hipStreamSynchronize(s));  // host CSR vectors die with this scope
+}
+
+// One-shot Fit's plan (RS_SGD_WB_TILE, at most kDeviceBuildMaxNnz ratings): the COO goes to the device as it
+// is (ratings rounded to f32 on the host threads, one pinned staging buffer, three DMAs) and the tile
+// schedule is built there (RS_TILE_RULE_SNAKE_DEVICE, sched_dev.hip): no host CSR, no host schedule.  Where
+// the rule does not apply, tile_build falls back to the host CSR (downloaded COO) and the LPT build.
+constexpr int64_t kDeviceBuildMaxNnz = int64_t{1} << 24;
+static void plan_build_coo_device(rs_ctx* ctx, const rs_ratings* r, int32_t k, rs_svd_plan* pl) {
+    hipStream_t s = ctx->stream;
+    pl->ctx = ctx;
+    pl->light_blocks = default_light_blocks(ctx);
+    pl->n_users = r->n_users;
+    pl->n_items = r->n_items;
+    pl->k = k;
+    pl->ld = fast_ld(k);
+    pl->nnz = r->nnz;
+    pl->tile_rule = RS_TILE_RULE_SNAKE_DEVICE;
+    const size_t n = static_cast<size_t>(r->nnz);
+    char* st = static_cast<char*>(pinned_staging(12 * n));
+    int32_t* su = reinterpret_cast<int32_t*>(st);
+    int32_t* si = su + n;
+    float* sv = reinterpret_cast<float*>(si + n);
+    parallel_ranges(r->nnz, 16, [&](int64_t b, int64_t e) {
+        std::memcpy(su + b, r->users + b, static_cast<size_t>(e - b) * 4);
+        std::memcpy(si + b, r->items + b, static_cast<size_t>(e - b) * 4);
+        for (int64_t t = b; t < e; ++t) sv[t] = static_cast<float>(r->ratings[t]);
+    });
+    // (buffers recycled from the previous Fit's plan are kept where large enough; P and Q must fit exactly)
+    if (pl->coo_users.n < n) pl->coo_users.alloc(n);
+    if (pl->coo_items.n < n) pl->coo_items.alloc(n);
+    if (pl->coo_vals.n < n) pl->coo_vals.alloc(n);
+    pl->coo_users.upload(su, n, s);
+    pl->coo_items.upload(si, n, s);
+    pl->coo_vals.upload(sv, n, s);
+    const size_t pn = static_cast<size_t>(std::max(1, pl->n_users)) * pl->ld, qn = static_cast<size_t>(std::max(1, pl->n_items)) * pl->ld;
+    (void)buffer_bytes32(qn, sizeof(float), "item factor matrix");
+    if (pl->P.n != pn) {
+        pl->P.alloc(pn);
+        RS_HIP(hipMemsetAsync(pl->P.p, 0, pn * sizeof(float), s));
+    }
+    if (pl->Q.n != qn) {
+        pl->Q.alloc(qn);
+        RS_HIP(hipMemsetAsync(pl->Q.p, 0, qn * sizeof(float), s));
+    }
+    pl->n_qrows = pl->n_items;
+    if (!pl->gb.p) pl->gb.alloc(1);
+    RS_HIP(hipMemsetAsync(pl->gb.p, 0, sizeof(double), s));
+    if (!pl->ev0) RS_HIP(hipEventCreate(&pl->ev0));
+    if (!pl->ev1) RS_HIP(hipEventCreate(&pl->ev1));
+    static const bool trace = std::getenv("RSGPU_FIT_TRACE") != nullptr;
+    auto t0 = std::chrono::steady_clock::now();
+    tile_build(pl);  // syncs the stream (the staging buffer is free again)
+    if (trace)
+        std::fprintf(stderr, "fit-trace   schedule %8.3f ms (%s)\n",
+                     std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count(),
+                     pl->tile_rule == RS_TILE_RULE_SNAKE_DEVICE ? "device" : "host fallback");
+}
+
+// A new one-shot Fit plan takes over the previous one's device buffers (hipMalloc / hipFree cost tens of us
+// each and hipFree waits for the device): the COO, the schedule and its workspace by capacity, P and Q when
+// their shapes match, the flag, GlobalBias and the events.
+static void plan_recycle(rs_svd_plan* pl, rs_svd_plan* old, int32_t n_users, int32_t n_items, int32_t k) {
+    plan_sync_last(old);
+    pl->coo_users = std::move(old->coo_users);
+    pl->coo_items = std::move(old->coo_items);
+    pl->coo_vals = std::move(old->coo_vals);
+    pl->sched_ws = std::move(old->sched_ws);
+    pl->t_tiles = std::move(old->t_tiles);
+    pl->t_users = std::move(old->t_users);
+    pl->t_streams = std::move(old->t_streams);
+    pl->t_runs = std::move(old->t_runs);
+    pl->t_recs = std::move(old->t_recs);
+    pl->t_split_rows = std::move(old->t_split_rows);
+    pl->partial = std::move(old->partial);
+    pl->numflag = std::move(old->numflag);  // (zero: a raised flag is cleared when it is reported)
+    pl->gb = std::move(old->gb);
+    if (old->ld == fast_ld(k) && old->n_users == n_users) pl->P = std::move(old->P);
+    if (old->ld == fast_ld(k) && old->n_items == n_items && old->n_qrows == old->n_items) pl->Q = std::move(old->Q);
+    std::swap(pl->ev0, old->ev0);
+    std::swap(pl->ev1, old->ev1);
+}
+
+// rs_svd_fit's factor transfers: f64 <-> the f32 row layout [p, b] on the host threads through pinned
+// staging slot 1 (one DMA per matrix, no intermediate vectors); past 256 MiB of rows the plan_upload /
+// plan_download path (pageable) is taken instead.
+constexpr size_t kFitStageMax = size_t{256} << 20;
+static bool plan_upload_fit(rs_svd_plan* pl, const double* P, const double* Q, const double* bu, const double* bi,
+                            const double* gb) {
+    const size_t pn = static_cast<size_t>(std::max(1, pl->n_users)) * pl->ld, qn = static_cast<size_t>(std::max(1, pl->n_items)) * pl->ld;
+    if ((pn + qn) * 4 > kFitStageMax) return false;
+    plan_sync_last(pl);
+    hipStream_t s = pl->ctx->stream;
+    float* st = static_cast<float*>(pinned_staging((pn + qn) * 4, 1));
+    const int32_t k = pl->k, ld = pl->ld;
+    auto pack = [&](float* dst, const double* F, const double* bias, int64_t rows) {
+        parallel_ranges(rows, 16, [&](int64_t r0, int64_t r1) {
+            for (int64_t r = r0; r < r1; ++r) {
+                float* d = dst + r * ld;
+                for (int32_t f = 0; f < k; ++f) d[f] = static_cast<float>(F[r * k + f]);
+                d[k] = static_cast<float>(bias[r]);
+                for (int32_t f = k + 1; f < ld; ++f) d[f] = 0.f;
+            }
+        });
+    };
+    pack(st, P, bu, pl->n_users);
+    pack(st + pn, Q, bi, pl->n_items);
+    pl->P.upload(st, static_cast<size_t>(pl->n_users) * ld, s);
+    pl->Q.upload(st + pn, static_cast<size_t>(pl->n_items) * ld, s);
+    sync_item_copies(pl, s, 1);
+    pl->gb.upload(gb, 1, s);  // (8 bytes from pageable memory: the runtime copies it before returning)
+    return true;
+}
+
+static bool plan_download_fit(rs_svd_plan* pl, double* P, double* Q, double* bu, double* bi, double* gb) {
+    const size_t pn = static_cast<size_t>(std::max(1, pl->n_users)) * pl->ld, qn = static_cast<size_t>(std::max(1, pl->n_items)) * pl->ld;
+    if ((pn + qn) * 4 > kFitStageMax) return false;
+    plan_sync_last(pl);
+    hipStream_t s = pl->ctx->stream;
+    float* st = static_cast<float*>(pinned_staging((pn + qn) * 4, 1));
+    pl->P.download(st, static_cast<size_t>(pl->n_users) * pl->ld, s);
+    pl->Q.download(st + pn, static_cast<size_t>(pl->n_items) * pl->ld, s);
+    pl->gb.download(gb, 1, s);
+    int32_t flag = 0;
+    if (pl->numflag.p) pl->numflag.download(&flag, 1, s);
+    RS_HIP(hipStreamSynchronize(s));
+    const int32_t k = pl->k, ld = pl->ld;
+    auto unpack = [&](const float* src, double* F, double* bias, int64_t rows) {
+        parallel_ranges(rows, 16, [&](int64_t r0, int64_t r1) {
+            for (int64_t r = r0; r < r1; ++r) {
+                const float* a = src + r * ld;
+                for (int32_t f = 0; f < k; ++f) F[r * k + f] = a[f];
+                bias[r] = a[k];
+            }
+        });
+    };
+    unpack(st, P, bu, pl->n_users);
+    unpack(st + pn, Q, bi, pl->n_items);
+    if (flag) {
+        RS_HIP(hipMemsetAsync(pl->numflag.p, 0, sizeof(int32_t), s));
+        RS_HIP(hipStreamSynchronize(s));
+        throw NumericError{"item factors left the fixed-point range (non-finite or |q| >= 128) during "
+                           "an epoch; the returned model is not trustworthy"};
+    }
+    return true;
 }
 
 static void plan_build(rs_ctx* ctx, const rs_ratings* r, int32_t k, rs_svd_plan* pl) {
@@ -1763,6 +1909,69 @@ extern "C" int rs_svd_plan_set_tile_claim(rs_svd_plan* pl, int32_t runs_per_clai
     });
 }
 
+extern "C" int rs_svd_plan_set_tile_rule(rs_svd_plan* pl, int32_t rule) {
+    if (!pl) return rs::set_error(nullptr, RS_ERR_INVALID, "plan is NULL");
+    if (rule < RS_TILE_RULE_LPT || rule > RS_TILE_RULE_SNAKE_DEVICE)
+        return rs::set_error(pl->ctx, RS_ERR_INVALID, "tile rule must be RS_TILE_RULE_LPT, _SNAKE or _SNAKE_DEVICE");
+    return rs_guard(pl->ctx, [&]() -> int {
+        rs::plan_sync_last(pl);
+        if (rule == RS_TILE_RULE_SNAKE) {  // the host snake: whole users only
+            rs::ensure_host_csr(pl);
+            const int64_t rec_cap = static_cast<int64_t>((rs::kTileLdsBudget - 16 - static_cast<size_t>(rs::tile_lds_row(pl)) * 4) / 16);
+            for (int32_t u = 0; u < pl->n_users; ++u)
+                if (pl->h_rowptr[u + 1] - pl->h_rowptr[u] > rec_cap)
+                    return rs::set_error(pl->ctx, RS_ERR_UNSUPPORTED, "snake tile rule: a user above the LDS bound");
+        }
+        const int32_t old = pl->tile_rule;
+        pl->tile_rule = rule;
+        try {
+            rs::tile_build(pl);
+        } catch (...) {
+            pl->tile_rule = old;
+            throw;
+        }
+        if (pl->write_back == RS_SGD_WB_TILE) pl->n_blocks = rs::tile_partials(pl);
+        return RS_OK;
+    });
+}
+
+extern "C" int rs_svd_plan_tile_rule(const rs_svd_plan* pl, int32_t* rule) {
+    if (!pl || !rule) return rs::set_error(pl ? pl->ctx : nullptr, RS_ERR_INVALID, "bad arguments");
+    *rule = pl->tile_rule;
+    return RS_OK;
+}
+
+extern "C" int rs_svd_plan_schedule_digest(rs_svd_plan* pl, uint64_t* digest) {
+    if (!pl || !digest) return rs::set_error(pl ? pl->ctx : nullptr, RS_ERR_INVALID, "bad arguments");
+    return rs_guard(pl->ctx, [&]() -> int {
+        rs::plan_sync_last(pl);
+        if (!pl->tiles_built) rs::tile_build(pl);
+        uint64_t h = 1469598103934665603ULL;  // FNV-1a 64
+        auto mix = [&](const void* p, size_t n) {
+            const unsigned char* b = static_cast<const unsigned char*>(p);
+            for (size_t x = 0; x < n; ++x) h = (h ^ b[x]) * 1099511628211ULL;
+        };
+        const int64_t nt = pl->n_tiles, lds = static_cast<int64_t>(pl->tile_lds);
+        mix(&nt, 8);
+        mix(&lds, 8);
+        hipStream_t s = pl->ctx->stream;
+        auto add = [&](const auto& buf, size_t count) {
+            using T = std::remove_reference_t<decltype(*buf.p)>;
+            std::vector<T> v(count);
+            buf.download(v.data(), count, s);
+            RS_HIP(hipStreamSynchronize(s));
+            mix(v.data(), count * sizeof(T));
+        };
+        add(pl->t_tiles, static_cast<size_t>(nt));
+        add(pl->t_users, static_cast<size_t>(pl->t_n_users));
+        add(pl->t_streams, static_cast<size_t>(nt) * (pl->tile_waves + 1));
+        add(pl->t_runs, static_cast<size_t>(pl->t_n_runs));
+        add(pl->t_recs, static_cast<size_t>(pl->nnz));
+        *digest = h;
+        return RS_OK;
+    });
+}
+
 extern "C" int rs_svd_plan_tile_clocks(rs_svd_plan* pl, int64_t* out, int64_t n) {
     if (!pl || !out || n < 0) return rs::set_error(pl ? pl->ctx : nullptr, RS_ERR_INVALID, "bad arguments");
     return rs_guard(pl->ctx, [&]() -> int {
@@ -1952,6 +2161,11 @@ struct SvdFitCache {
     }
 };
 
+// RSGPU_FIT_DEVICE_BUILD=0: one-shot Fit builds its schedule on the host (LPT rule) -- experiments only
+static bool fit_device_build_on() {
+    static const bool on = !(std::getenv("RSGPU_FIT_DEVICE_BUILD") && std::atoi(std::getenv("RSGPU_FIT_DEVICE_BUILD")) == 0);
+    return on;
+}
 static bool fit_cache_on() {
     static const bool on = !(std::getenv("RSGPU_FIT_CACHE") && std::atoi(std::getenv("RSGPU_FIT_CACHE")) == 0);
     return on;
@@ -1965,6 +2179,15 @@ extern "C" int rs_fit_refits(const rs_ctx* ctx, int32_t* n) {
     if (!ctx || !n) return rs::set_error(nullptr, RS_ERR_INVALID, "bad arguments");
     *n = ctx->fit_refits;
     return RS_OK;
+}
+
+extern "C" int rs_fit_schedule_digest(rs_ctx* ctx, uint64_t* digest, int32_t* rule) {
+    if (!ctx || !digest || !rule) return rs::set_error(ctx, RS_ERR_INVALID, "bad arguments");
+    auto cache = std::static_pointer_cast<rs::SvdFitCache>(ctx->svd_fit_cache);
+    if (!cache || !cache->plan || cache->plan->write_back != RS_SGD_WB_TILE)
+        return rs::set_error(ctx, RS_ERR_INVALID, "no cached FAST tile plan (no rs_svd_fit ran on this ctx)");
+    *rule = cache->plan->tile_rule;
+    return rs_svd_plan_schedule_digest(cache->plan.get(), digest);
 }
 
 extern "C" int rs_svd_fit(rs_ctx* ctx, const rs_ratings* r, const rs_sgd_params* p, double* P,
@@ -1994,34 +2217,49 @@ extern "C" int rs_svd_fit(rs_ctx* ctx, const rs_ratings* r, const rs_sgd_params*
             const bool hit = rs::fit_cache_on() && cache && cache->matches(r, p->n_factors, wb);
             mark(hit ? "cache-hit" : "cache-miss");
             if (!hit) {
-                ctx->svd_fit_cache.reset();  // free the old plan's device buffers first
+                const bool dev = wb == RS_SGD_WB_TILE && r->nnz > 0 && r->nnz <= rs::kDeviceBuildMaxNnz && rs::fit_device_build_on();
+                auto old = dev ? cache : nullptr;  // the device path recycles the old plan's buffers
+                ctx->svd_fit_cache.reset();          // (otherwise they are freed first)
                 cache = std::make_shared<rs::SvdFitCache>();
                 cache->plan = std::make_unique<rs_svd_plan>();
                 cache->plan->write_back = wb;
-                rs::UserCSR csr;
-                rs::build_csr(r->nnz, r->n_users, r->users, r->items, r->ratings, csr);
-                mark("csr");
-                rs::plan_build_csr(ctx, r->n_users, r->n_items, std::move(csr), p->n_factors, cache->plan.get());
-                mark("plan");
-                if (rs::fit_cache_on() && r->nnz <= rs::kFitCacheMaxNnz) {
-                    const size_t n = static_cast<size_t>(r->nnz);
-                    cache->nnz = r->nnz;
-                    cache->n_users = r->n_users;
-                    cache->n_items = r->n_items;
-                    cache->k = p->n_factors;
-                    cache->write_back = wb;
-                    cache->users.resize(n);
-                    cache->items.resize(n);
-                    cache->ratings.resize(n);
-                    rs::parallel_ranges(r->nnz, 16, [&](int64_t b, int64_t e) {  // the COO copy, pooled threads
-                        const size_t o = static_cast<size_t>(b), m = static_cast<size_t>(e - b);
-                        std::memcpy(cache->users.data() + o, r->users + o, m * 4);
-                        std::memcpy(cache->items.data() + o, r->items + o, m * 4);
-                        std::memcpy(cache->ratings.data() + o, r->ratings + o, m * 8);
-                    });
-                    ctx->svd_fit_cache = cache;
+                if (dev) {
+                    if (old && old->plan) rs::plan_recycle(cache->plan.get(), old->plan.get(), r->n_users, r->n_items, p->n_factors);
+                    if (old) {  // and the host COO copy's memory
+                        cache->users = std::move(old->users);
+                        cache->items = std::move(old->items);
+                        cache->ratings = std::move(old->ratings);
+                    }
+                    old.reset();
+                    rs::plan_build_coo_device(ctx, r, p->n_factors, cache->plan.get());
+                } else {
+                    rs::UserCSR csr;
+                    rs::build_csr(r->nnz, r->n_users, r->users, r->items, r->ratings, csr);
+                    mark("csr");
+                    rs::plan_build_csr(ctx, r->n_users, r->n_items, std::move(csr), p->n_factors, cache->plan.get());
                 }
+                mark("plan");
             }
+            // the cache's copy of the COO (compared by the next call) is made while the first epochs run
+            auto keep_coo = [&] {
+                if (hit || !rs::fit_cache_on() || r->nnz > rs::kFitCacheMaxNnz) return;
+                const size_t n = static_cast<size_t>(r->nnz);
+                cache->nnz = r->nnz;
+                cache->n_users = r->n_users;
+                cache->n_items = r->n_items;
+                cache->k = p->n_factors;
+                cache->write_back = wb;
+                cache->users.resize(n);
+                cache->items.resize(n);
+                cache->ratings.resize(n);
+                rs::parallel_ranges(r->nnz, 16, [&](int64_t b, int64_t e) {  // the COO copy, pooled threads
+                    const size_t o = static_cast<size_t>(b), m = static_cast<size_t>(e - b);
+                    std::memcpy(cache->users.data() + o, r->users + o, m * 4);
+                    std::memcpy(cache->items.data() + o, r->items + o, m * 4);
+                    std::memcpy(cache->ratings.data() + o, r->ratings + o, m * 8);
+                });
+                ctx->svd_fit_cache = cache;
+            };
             rs_svd_plan& pl = *cache->plan;
             ctx->fit_refits = 0;
             // Divergence guard (tile schedule): a fit that leaves the fixed-point range or goes non-finite is
@@ -2035,12 +2273,18 @@ extern "C" int rs_svd_fit(rs_ctx* ctx, const rs_ratings* r, const rs_sgd_params*
             for (int attempt = 0;; ++attempt) {
                 if (p->n_epochs > 0) *gb = rs::gb_warm_start(r, bu, bi);
                 mark("warm");
-                rs::plan_upload(&pl, P, Q, bu, bi, gb);
+                if (!rs::plan_upload_fit(&pl, P, Q, bu, bi, gb)) rs::plan_upload(&pl, P, Q, bu, bi, gb);
                 mark("upload");
                 rs::kernel_span_begin(ctx);
                 rs::plan_epochs(&pl, p->n_epochs, lr, reg, ctx->stream);
-                rs::kernel_span_end(ctx);
+                rs::kernel_span_record(ctx);
+                if (attempt == 0 && !trace) keep_coo();  // host work under the epochs
+                rs::kernel_span_wait(ctx);
                 mark("epochs");
+                if (attempt == 0 && trace) {
+                    keep_coo();
+                    mark("cache-copy");
+                }
                 if (wb != RS_SGD_WB_TILE || attempt == 3 || !rs::plan_diverged(&pl)) break;
                 if (pl.tile_grid <= 1) break;
                 pl.tile_wg = std::max(1, pl.tile_grid / 2);
@@ -2049,7 +2293,7 @@ extern "C" int rs_svd_fit(rs_ctx* ctx, const rs_ratings* r, const rs_sgd_params*
                 ++ctx->fit_refits;
                 if (trace) std::fprintf(stderr, "fit-trace diverged: refit on %d workgroups\n", pl.tile_wg);
             }
-            rs::plan_download(&pl, P, Q, bu, bi, gb);
+            if (!rs::plan_download_fit(&pl, P, Q, bu, bi, gb)) rs::plan_download(&pl, P, Q, bu, bi, gb);
             mark("download");
             return RS_OK;
         }

@@ -92,6 +92,7 @@ struct rs_svd_plan {
     rs::DevBuf<int2> t_recs;    // {user (tile-local), rating bits}
     rs::DevBuf<int32_t> t_split_rows;  // users cut into pieces over several tiles
     int32_t t_n_split = 0;
+    int64_t t_n_runs = 0, t_n_users = 0;  // entries of t_runs / t_users in use (the buffers may be larger)
     // user blocks: consecutive user ranges of near-equal ratings, each with its own tiles (tiles
     // [t_block_tile[b], t_block_tile[b+1]) hold users [t_block_user[b], t_block_user[b+1])); the
     // item-sharded multi-GPU epoch all-reduces a block's user deltas while the next block computes
@@ -119,6 +120,13 @@ struct rs_svd_plan {
     std::shared_ptr<rs::ShardComm> shard;  // item-sharded multi-GPU state (multi.hip), or empty
     int32_t exchange = RS_EXCHANGE_ROTATE;  // the multi-GPU exchange a join sets up
     int32_t fault_sub_epoch = -1;  // test hook (rs_svd_plan_inject_fault): the next sharded call throws there
+    // how tiles are formed (rs_svd_plan_set_tile_rule): RS_TILE_RULE_LPT (host: LPT by ratings + cost
+    // refinement), RS_TILE_RULE_SNAKE (host: users by degree dealt boustrophedon), RS_TILE_RULE_SNAKE_DEVICE
+    // (the same rule built on the device from coo_*; one-shot rs_svd_fit's default)
+    int32_t tile_rule = RS_TILE_RULE_LPT;
+    rs::DevBuf<int32_t> coo_users, coo_items;  // device COO of a device-built schedule (any rating order)
+    rs::DevBuf<float> coo_vals;
+    rs::DevBuf<char> sched_ws;                 // its build workspace (kept for refits)
     ~rs_svd_plan() {
         if (ev0) (void)hipEventDestroy(ev0);
         if (ev1) (void)hipEventDestroy(ev1);
@@ -208,7 +216,31 @@ void ordered_epochs(const int32_t* users, const int32_t* items, const float* rat
                     hipStream_t s);
 
 // sgd_tile.hip
-void tile_build(rs_svd_plan* pl);  // (re)builds the tile schedule from the host CSR
+constexpr size_t kTileLdsBudget = 160 * 1024 - 512;  // gfx950: 160 KiB of LDS per workgroup
+// LDS ints per tile user (k factors + two bias columns, or the caller's tile_user_lds)
+inline int32_t tile_lds_row(const rs_svd_plan* pl) {
+    return pl->tile_user_lds > 0 ? pl->tile_user_lds : 64 * ((pl->k + 2 + 63) / 64);
+}
+// LDS bytes of a tile: P rows, records, run headers + sentinel (ld: the LDS row)
+inline size_t tile_bytes(int64_t users, int64_t recs, int64_t runs, int32_t ld) {
+    return static_cast<size_t>(users) * ld * 4 + static_cast<size_t>(recs) * 8 + static_cast<size_t>(runs + 1) * 8;
+}
+// Queue key of item `item`'s run in tile `tile`: runs are queued in key order, a per-tile pseudo-random
+// item order.  fmix32 (murmur3's finaliser) of item ^ salt(tile) is a bijection of the item id, so no two
+// items of a tile share a key and the order needs no tie rule (host and device builds agree by construction).
+__host__ __device__ inline uint32_t run_key(int32_t item, int32_t tile) {
+    uint32_t x = static_cast<uint32_t>(item) ^ (static_cast<uint32_t>(tile) * 0x9E3779B1u);
+    x ^= x >> 16;
+    x *= 0x85EBCA6Bu;
+    x ^= x >> 13;
+    x *= 0xC2B2AE35u;
+    x ^= x >> 16;
+    return x;
+}
+int32_t device_cus(const rs_ctx* ctx);
+// the run cap the library picks (see auto_run_cap, sgd_tile.hip) from the item degree maximum
+int32_t run_cap_rule(int64_t nnz, int64_t dmax_item, int32_t grid, int32_t waves);
+void tile_build(rs_svd_plan* pl);  // (re)builds the tile schedule (host CSR, or the device for RS_TILE_RULE_SNAKE_DEVICE)
 std::vector<int32_t> user_block_bounds(const int64_t* cum, int32_t n_users, int32_t nb);
 void tile_launch(rs_svd_plan* pl, float lr, float reg, hipStream_t s, float* dP);  // one epoch (Q int32)
 // tiles [t0, t1) only (one user block), delta mode into dP (row stride ldd); returns the number of
@@ -220,4 +252,13 @@ int32_t tile_cap_in_use(const rs_svd_plan* pl);  // the run cap the schedule is 
 // visit order of the tile schedule (user-CSR positions, nnz entries) and its GlobalBias work items
 // (one per tile and wave: n_works + 1 offsets into pos); any pointer may be NULL
 void tile_order(rs_svd_plan* pl, int64_t* pos, int64_t* work_off, int32_t* n_works);
+
+// sched_dev.hip: the snake-rule tile schedule built on the device from the plan's device COO (coo_*).
+// Returns false, with nothing of the plan changed, where the rule does not apply (a user above the LDS
+// bound, keys past 64 bits, a tile past the LDS): the caller builds on the host instead.
+bool tile_build_device(rs_svd_plan* pl);
+// the device COO of a plan built from the host CSR (rows expanded), for tile_build_device
+void upload_coo_from_csr(rs_svd_plan* pl);
+// the host CSR of a plan built on the device (downloaded COO, stable CSR build) -- for the host builders
+void ensure_host_csr(rs_svd_plan* pl);
 }  // namespace rs

@@ -56,7 +56,6 @@
 
 namespace rs {
 
-constexpr size_t kTileLdsBudget = 160 * 1024 - 512;  // gfx950: 160 KiB of LDS per workgroup
 
 // Wave sum ending in lane 63 (GFX9 DPP row broadcasts): the in-row tree gives every lane its row's
 // sum, row_bcast:15 adds row 0 / 2's sum into rows 1 / 3, row_bcast:31 adds rows 0-1 into rows 2-3.
@@ -435,17 +434,6 @@ struct TileHost {
     size_t lds = 0;
 };
 
-int32_t device_cus(const rs_ctx* ctx) {
-    int cus = 0;
-    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, ctx->device) != hipSuccess || cus <= 0)
-        cus = 256;
-    return cus;
-}
-
-size_t tile_bytes(int64_t users, int64_t recs, int64_t runs, int32_t ld) {  // ld: the LDS row
-    return static_cast<size_t>(users) * ld * 4 + static_cast<size_t>(recs) * 8 + static_cast<size_t>(runs + 1) * 8;
-}
-
 // Tiles from the host user-CSR.  Entries (user pieces) are consecutive users; a tile closes when the
 // next entry would pass the rating target or the LDS bound (runs <= records).  A user whose ratings
 // do not fit one tile's LDS is cut into near-equal pieces (count-weighted merge after the epoch).
@@ -453,8 +441,7 @@ void build_tile_host(const rs_svd_plan* pl, int32_t u_begin, int32_t u_end, int3
                      int32_t run_cap, bool want_pos, TileHost& th) {
     const bool claim = pl->tile_claim > 0;  // one run queue per tile, claimed by the waves
     const std::vector<int64_t>& rp = pl->h_rowptr;
-    const int32_t ld = pl->tile_user_lds > 0 ? pl->tile_user_lds
-                                             : 64 * ((pl->k + 2 + 63) / 64);  // LDS per user: k factors + two bias columns
+    const int32_t ld = tile_lds_row(pl);
     // one entry alone must fit: ld*4 + d*16 + 8 <= budget
     const int64_t rec_cap = static_cast<int64_t>((kTileLdsBudget - 16 - static_cast<size_t>(ld) * 4) / 16);
     if (rec_cap < 64) throw std::invalid_argument("n_factors too large for the tile schedule's LDS");
@@ -494,7 +481,30 @@ void build_tile_host(const rs_svd_plan* pl, int32_t u_begin, int32_t u_end, int3
         const int64_t n_target = (total + target - 1) / std::max<int64_t>(target, 1);
         const int64_t n_lds = static_cast<int64_t>(std::ceil(bytes / (0.85 * static_cast<double>(kTileLdsBudget))));
         const int64_t n0 = std::max<int64_t>({1, n_target, n_lds});
-        if (n_lds > 64 && n_lds >= 4 * n_target) {
+        if (pl->tile_rule != RS_TILE_RULE_LPT) {
+            // snake rule (the device build, sched_dev.hip, restates it): entries by ratings, descending (ties by
+            // user id), dealt boustrophedon over min(n0, entries) tiles; a tile's entries in user order
+            if (!th.split.empty()) throw std::invalid_argument("snake tile rule: a user above the LDS bound");
+            const size_t ne = ents.size(), ntl = std::min(static_cast<size_t>(n0), ne);
+            std::vector<size_t> order(ne);
+            std::iota(order.begin(), order.end(), size_t{0});
+            std::stable_sort(order.begin(), order.end(), [&](size_t a, size_t b) {
+                return ents[a].e - ents[a].b > ents[b].e - ents[b].b;
+            });
+            std::vector<std::vector<size_t>> bins(ntl);
+            for (size_t p = 0; p < ne; ++p) {
+                const size_t r = p / ntl, i = p % ntl;
+                bins[(r & 1) ? ntl - 1 - i : i].push_back(order[p]);
+            }
+            std::vector<Ent> sorted;
+            sorted.reserve(ne);
+            for (std::vector<size_t>& bn : bins) {
+                std::sort(bn.begin(), bn.end());
+                for (size_t x : bn) sorted.push_back(ents[x]);
+                tb.push_back(sorted.size());
+            }
+            ents.swap(sorted);
+        } else if (n_lds > 64 && n_lds >= 4 * n_target) {
             // LDS-bound (many tiles per workgroup, e.g. a ROTATE_Q stratum of 10M users' ratings): the launch
             // balances itself over the tiles, so fill tiles in user order to the LDS instead of LPT (which took
             // ~1 s per configs[4] stratum for nothing)
@@ -552,9 +562,12 @@ void build_tile_host(const rs_svd_plan* pl, int32_t u_begin, int32_t u_end, int3
         // tiles of many light users -- more shared items -- are cheaper than tiles of one heavy user).
         // Move users from the costliest tile to the cheapest while that lowers the maximum.
         const size_t nb = bins.size();
-        static const bool no_refine = std::getenv("RSGPU_TILE_NO_REFINE") != nullptr;  // (experiment, round 4)
-        if (!no_refine && nb > 1 && nb <= 8192 && static_cast<double>(nb) * std::max(1, pl->n_items) <= 6.4e7) {
+        // (round 4 A/B on the bench shape: 176 us per epoch with it, 186 us without; profiles/r04_refine.txt)
+        if (nb > 1 && nb <= 8192 && static_cast<double>(nb) * std::max(1, pl->n_items) <= 6.4e7) {
+            // (round 4 sweep with claims: run cost 1 / 2 / 3 / 4 / 6 -> 181 / 180 / 177 / 176 / 177 us; 16 nb moves
+            // instead of 4 nb: no change -- the moves have converged; profiles/r04_refine.txt)
             constexpr int64_t kRunCost = 3;
+            constexpr size_t kIt = 4;
             std::vector<int32_t> cnt(nb * static_cast<size_t>(std::max(1, pl->n_items)), 0);
             std::vector<int64_t> runs(nb, 0), cost(nb, 0);
             auto row = [&](size_t b) { return cnt.data() + b * static_cast<size_t>(pl->n_items); };
@@ -568,7 +581,7 @@ void build_tile_host(const rs_svd_plan* pl, int32_t u_begin, int32_t u_end, int3
                     cost[b] = bins[b].recs + kRunCost * runs[b];
                 }
             });
-            for (size_t it = 0; it < 4 * nb; ++it) {
+            for (size_t it = 0; it < kIt * nb; ++it) {
                 const size_t hi = static_cast<size_t>(std::max_element(cost.begin(), cost.end()) - cost.begin());
                 const size_t lo = static_cast<size_t>(std::min_element(cost.begin(), cost.end()) - cost.begin());
                 if (hi == lo || bins[hi].ents.size() < 2) break;
@@ -656,7 +669,7 @@ void build_tile_host(const rs_svd_plan* pl, int32_t u_begin, int32_t u_end, int3
         const size_t nd = ditem.size();
         std::vector<uint32_t> key(nd), ord(nd), tmp(nd);
         for (size_t d = 0; d < nd; ++d) {
-            key[d] = mix32((static_cast<uint64_t>(ditem[d]) << 20) ^ (t * 0x9E3779B1ULL));
+            key[d] = run_key(ditem[d], static_cast<int32_t>(t));
             ord[d] = static_cast<uint32_t>(d);
         }
         for (int sh = 0; sh < 32; sh += 8) {  // LSD radix by key (ties: first appearance)
@@ -698,7 +711,9 @@ void build_tile_host(const rs_svd_plan* pl, int32_t u_begin, int32_t u_end, int3
             // scripts/experiments/exp_stability.py): pieces spread evenly over the queue instead -- each
             // tile then holds one of the item's runs in flight most of the time -- diverged at epoch 3-4 with
             // chunks of 4 and of 8; adjacent pieces train as the host deal does (10-epoch held-out 0.683 /
-            // 0.683 against 0.686 for the reference order), at the same ML-1M epoch time.
+            // 0.683 against 0.686 for the reference order), at the same ML-1M epoch time.  The key order itself
+            // matters: single-rating runs last, longest runs first or shortest first gave 197 / 252 / 257 us
+            // per ML-1M epoch against 177 us (profiles/r04_refine.txt).
             struct QE { uint64_t at; int32_t sl, pc, pieces; };
             std::vector<QE> qv;
             qv.reserve(nd);
@@ -838,12 +853,26 @@ int32_t auto_run_cap(const rs_svd_plan* pl, int32_t grid, int32_t waves) {
     if (waves <= 1 || pl->nnz == 0) return 0;
     std::vector<int64_t> deg(std::max(1, pl->n_items), 0);
     for (int32_t c : pl->h_cols) deg[c]++;
-    const int64_t dmax = *std::max_element(deg.begin(), deg.end());
-    const double c = 2.0 * kStaleTarget * static_cast<double>(pl->nnz) /
-                     (static_cast<double>(dmax) * grid * waves);
-    const int64_t c_hot = pl->nnz >= kHotFloorMinNnz ? (dmax * 256 + pl->nnz - 1) / pl->nnz : 0;
+    return run_cap_rule(pl->nnz, *std::max_element(deg.begin(), deg.end()), grid, waves);
+}
+
+}  // namespace
+
+int32_t run_cap_rule(int64_t nnz, int64_t dmax, int32_t grid, int32_t waves) {
+    if (waves <= 1 || nnz == 0) return 0;
+    const double c = 2.0 * kStaleTarget * static_cast<double>(nnz) / (static_cast<double>(dmax) * grid * waves);
+    const int64_t c_hot = nnz >= kHotFloorMinNnz ? (dmax * 256 + nnz - 1) / nnz : 0;
     return c >= 1e6 ? 0 : static_cast<int32_t>(std::max<int64_t>({2, static_cast<int64_t>(c), c_hot}));
 }
+
+int32_t device_cus(const rs_ctx* ctx) {
+    int cus = 0;
+    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, ctx->device) != hipSuccess || cus <= 0)
+        cus = 256;
+    return cus;
+}
+
+namespace {
 
 // Ratings per tile: nnz / workgroups, but at least the heaviest user's ratings (cutting users into
 // pieces costs accuracy -- their rows are averaged after the epoch -- so small sets get fewer tiles).
@@ -1003,6 +1032,7 @@ void build_tile_blocks(const rs_svd_plan* pl, int32_t grid0, bool want_pos, Tile
 int32_t tile_partials(const rs_svd_plan* pl) { return std::max(1, pl->tile_grid) * pl->tile_waves; }
 
 int32_t tile_cap_in_use(const rs_svd_plan* pl) {
+    ensure_host_csr(const_cast<rs_svd_plan*>(pl));
     if (pl->tile_run_cap > 0) return pl->tile_run_cap;
     const int32_t grid0 = pl->tile_wg > 0 ? pl->tile_wg : device_cus(pl->ctx);
     const int32_t c = auto_run_cap(pl, grid0, pl->tile_waves);
@@ -1013,6 +1043,13 @@ int32_t tile_cap_in_use(const rs_svd_plan* pl) {
 }
 
 void tile_build(rs_svd_plan* pl) {
+    if (pl->tile_rule == RS_TILE_RULE_SNAKE_DEVICE) {
+        plan_sync_last(pl);
+        if (!pl->coo_users.p) upload_coo_from_csr(pl);
+        if (tile_build_device(pl)) return;
+        pl->tile_rule = RS_TILE_RULE_LPT;  // the rule does not apply to this set: the host's default build
+    }
+    ensure_host_csr(pl);
     hipStream_t s = pl->ctx->stream;
     const int32_t cus = device_cus(pl->ctx);
     const int32_t grid0 = pl->tile_wg > 0 ? pl->tile_wg : cus;
@@ -1020,6 +1057,8 @@ void tile_build(rs_svd_plan* pl) {
     build_tile_blocks(pl, grid0, false, th, pl->t_block_tile, pl->t_block_user, &pl->t_block_split);
     plan_sync_last(pl);
     pl->n_tiles = static_cast<int32_t>(th.tiles.size());
+    pl->t_n_runs = static_cast<int64_t>(th.runs.size());
+    pl->t_n_users = static_cast<int64_t>(th.users.size());
     pl->tile_grid = std::max(1, std::min(grid0, pl->n_tiles));
     pl->tile_lds = std::max<size_t>(th.lds, 16);
     pl->t_tiles.alloc(std::max<size_t>(1, th.tiles.size()));
@@ -1064,6 +1103,7 @@ void tile_build(rs_svd_plan* pl) {
 }
 
 void tile_order(rs_svd_plan* pl, int64_t* pos, int64_t* work_off, int32_t* n_works) {
+    ensure_host_csr(pl);
     const int32_t cus = device_cus(pl->ctx);
     const int32_t grid0 = pl->tile_wg > 0 ? pl->tile_wg : cus;
     TileHost th;

@@ -24,6 +24,7 @@ SIM_COSINE, SIM_MSD, SIM_PEARSON = 0, 1, 2
 TIE_GO_SORT, TIE_STABLE = 0, 1  # KNN.Predict tie order (rs_knn_plan_set_tie_order)
 DEV_SLOPE_ONE = 3  # rs_knn_sims kind: SlopeOne deviation matrix (slope_one.go:64-92)
 EXCHANGE_ROTATE, EXCHANGE_AVERAGE, EXCHANGE_ROTATE_Q = 0, 1, 2  # multi-GPU exchange of the sharded fit (rsgpu.h)
+TILE_RULE_LPT, TILE_RULE_SNAKE, TILE_RULE_SNAKE_DEVICE = 0, 1, 2  # how users are cut into tiles (rsgpu.h)
 
 HEADER_SYMBOLS = (
     "rs_version", "rs_device_count", "rs_open", "rs_close", "rs_last_error", "rs_synchronize",
@@ -42,6 +43,7 @@ HEADER_SYMBOLS = (
     "rs_svd_plan_set_item_weights", "rs_svd_plan_epoch_qdelta", "rs_svd_plan_apply_qdelta",
     "rs_svd_plan_set_hot_replicas", "rs_svd_plan_set_fixed_q", "rs_svd_plan_set_tiles",
     "rs_svd_plan_set_tile_claim", "rs_svd_plan_tile_order", "rs_svd_plan_tile_clocks",
+    "rs_svd_plan_set_tile_rule", "rs_svd_plan_tile_rule", "rs_svd_plan_schedule_digest", "rs_fit_schedule_digest",
     "rs_comm_unique_id", "rs_svd_plan_join", "rs_svd_plan_epochs_sharded", "rs_svd_plan_leave",
     "rs_svd_plan_set_user_blocks", "rs_svd_group_create", "rs_svd_group_epochs", "rs_svd_group_destroy",
     "rs_item_shards", "rs_svd_fit_multi", "rs_tile_schedule_host", "rs_svd_plan_set_exchange",
@@ -145,6 +147,10 @@ def lib():
             "rs_svd_plan_set_fixed_q": (C.c_int, [_vp, _i32]),
             "rs_svd_plan_set_tiles": (C.c_int, [_vp, _i32, _i32, _i32, _i32, _i32]),
             "rs_svd_plan_set_tile_claim": (C.c_int, [_vp, _i32]),
+            "rs_svd_plan_set_tile_rule": (C.c_int, [_vp, _i32]),
+            "rs_svd_plan_tile_rule": (C.c_int, [_vp, C.POINTER(_i32)]),
+            "rs_svd_plan_schedule_digest": (C.c_int, [_vp, C.POINTER(C.c_uint64)]),
+            "rs_fit_schedule_digest": (C.c_int, [_vp, C.POINTER(C.c_uint64), C.POINTER(_i32)]),
             "rs_svd_plan_tile_order": (C.c_int, [_vp, _vp, _vp, C.POINTER(_i32)]),
             "rs_svd_plan_tile_clocks": (C.c_int, [_vp, _vp, _i64]),
             "rs_svd_plan_epoch_qdelta": (C.c_int, [_vp, _flt, _flt, _vp, _vp, _vp]),
@@ -332,6 +338,12 @@ class Context:
         self.check(lib().rs_fit_refits(self.h, C.byref(n)))
         return n.value
 
+    def fit_schedule_digest(self):
+        """(digest, tile rule) of the tile schedule the last FAST svd_fit built (rs_fit_schedule_digest)."""
+        d, rule = C.c_uint64(0), _i32(0)
+        self.check(lib().rs_fit_schedule_digest(self.h, C.byref(d), C.byref(rule)))
+        return d.value, rule.value
+
     def svd_fit(self, r: Ratings, P, Q, bu=None, bi=None, gb=0.0, n_epochs=20, lr=0.005,
                 reg=0.02, mode=SGD_FAST, write_back=WB_TILE):
         P = np.array(P, dtype=np.float64, order="C")
@@ -512,6 +524,21 @@ class SvdPlan:
     def set_tiles(self, workgroups=0, waves=16, target=0, run_cap=0, ring=0):
         """WB_TILE schedule parameters (rs_svd_plan_set_tiles); rebuilds the tiles."""
         self.ctx.check(lib().rs_svd_plan_set_tiles(self.h, workgroups, waves, target, run_cap, ring))
+
+    def set_tile_rule(self, rule):
+        """TILE_RULE_LPT / _SNAKE / _SNAKE_DEVICE (rs_svd_plan_set_tile_rule); rebuilds the tiles."""
+        self.ctx.check(lib().rs_svd_plan_set_tile_rule(self.h, rule))
+
+    def tile_rule(self):
+        v = _i32(0)
+        self.ctx.check(lib().rs_svd_plan_tile_rule(self.h, C.byref(v)))
+        return v.value
+
+    def schedule_digest(self):
+        """64-bit digest of the tile schedule in HBM (rs_svd_plan_schedule_digest)."""
+        v = C.c_uint64(0)
+        self.ctx.check(lib().rs_svd_plan_schedule_digest(self.h, C.byref(v)))
+        return v.value
 
     def set_tile_claim(self, runs_per_claim=4):
         """Runs per claim from a tile's run queue (4, 8), or 0: runs dealt on the host
