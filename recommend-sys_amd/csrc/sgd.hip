@@ -1356,12 +1356,10 @@ static void plan_recycle(rs_svd_plan* pl, rs_svd_plan* old, int32_t n_users, int
 // staging slot 1 (one DMA per matrix, no intermediate vectors); past 256 MiB of rows the plan_upload /
 // plan_download path (pageable) is taken instead.
 constexpr size_t kFitStageMax = size_t{256} << 20;
-static bool plan_upload_fit(rs_svd_plan* pl, const double* P, const double* Q, const double* bu, const double* bi,
-                            const double* gb) {
+// host half: the rows packed into staging slot 1 (false: too large, nothing done)
+static bool plan_pack_fit(rs_svd_plan* pl, const double* P, const double* Q, const double* bu, const double* bi) {
     const size_t pn = static_cast<size_t>(std::max(1, pl->n_users)) * pl->ld, qn = static_cast<size_t>(std::max(1, pl->n_items)) * pl->ld;
     if ((pn + qn) * 4 > kFitStageMax) return false;
-    plan_sync_last(pl);
-    hipStream_t s = pl->ctx->stream;
     float* st = static_cast<float*>(pinned_staging((pn + qn) * 4, 1));
     const int32_t k = pl->k, ld = pl->ld;
     auto pack = [&](float* dst, const double* F, const double* bias, int64_t rows) {
@@ -1376,14 +1374,30 @@ static bool plan_upload_fit(rs_svd_plan* pl, const double* P, const double* Q, c
     };
     pack(st, P, bu, pl->n_users);
     pack(st + pn, Q, bi, pl->n_items);
-    pl->P.upload(st, static_cast<size_t>(pl->n_users) * ld, s);
-    pl->Q.upload(st + pn, static_cast<size_t>(pl->n_items) * ld, s);
-    sync_item_copies(pl, s, 1);
-    pl->gb.upload(gb, 1, s);  // (8 bytes from pageable memory: the runtime copies it before returning)
     return true;
 }
 
-static bool plan_download_fit(rs_svd_plan* pl, double* P, double* Q, double* bu, double* bi, double* gb) {
+// device half: the DMAs of the packed rows and GlobalBias (after plan_pack_fit)
+static void plan_dma_fit(rs_svd_plan* pl, const double* gb) {
+    const size_t pn = static_cast<size_t>(std::max(1, pl->n_users)) * pl->ld, qn = static_cast<size_t>(std::max(1, pl->n_items)) * pl->ld;
+    plan_sync_last(pl);
+    hipStream_t s = pl->ctx->stream;
+    float* st = static_cast<float*>(pinned_staging((pn + qn) * 4, 1));
+    pl->P.upload(st, static_cast<size_t>(pl->n_users) * pl->ld, s);
+    pl->Q.upload(st + pn, static_cast<size_t>(pl->n_items) * pl->ld, s);
+    sync_item_copies(pl, s, 1);
+    pl->gb.upload(gb, 1, s);  // (8 bytes from pageable memory: the runtime copies it before returning)
+}
+
+static bool plan_upload_fit(rs_svd_plan* pl, const double* P, const double* Q, const double* bu, const double* bi,
+                            const double* gb) {
+    if (!plan_pack_fit(pl, P, Q, bu, bi)) return false;
+    plan_dma_fit(pl, gb);
+    return true;
+}
+
+// D2H of P and Q (staging slot 1), GlobalBias and the numeric flag, one wait (false: too large for staging)
+static bool plan_fetch_fit(rs_svd_plan* pl, double* gb, int32_t* flag) {
     const size_t pn = static_cast<size_t>(std::max(1, pl->n_users)) * pl->ld, qn = static_cast<size_t>(std::max(1, pl->n_items)) * pl->ld;
     if ((pn + qn) * 4 > kFitStageMax) return false;
     plan_sync_last(pl);
@@ -1392,9 +1406,21 @@ static bool plan_download_fit(rs_svd_plan* pl, double* P, double* Q, double* bu,
     pl->P.download(st, static_cast<size_t>(pl->n_users) * pl->ld, s);
     pl->Q.download(st + pn, static_cast<size_t>(pl->n_items) * pl->ld, s);
     pl->gb.download(gb, 1, s);
-    int32_t flag = 0;
-    if (pl->numflag.p) pl->numflag.download(&flag, 1, s);
+    *flag = 0;
+    if (pl->numflag.p) pl->numflag.download(flag, 1, s);
     RS_HIP(hipStreamSynchronize(s));
+    return true;
+}
+
+static void plan_clear_flag(rs_svd_plan* pl) {
+    RS_HIP(hipMemsetAsync(pl->numflag.p, 0, sizeof(int32_t), pl->ctx->stream));
+    RS_HIP(hipStreamSynchronize(pl->ctx->stream));
+}
+
+// after plan_fetch_fit: the f64 rows; a raised flag is cleared and reported (values already written)
+static void plan_finish_fit(rs_svd_plan* pl, double* P, double* Q, double* bu, double* bi, int32_t flag) {
+    const size_t pn = static_cast<size_t>(std::max(1, pl->n_users)) * pl->ld;
+    const float* st = static_cast<const float*>(pinned_staging(0, 1));
     const int32_t k = pl->k, ld = pl->ld;
     auto unpack = [&](const float* src, double* F, double* bias, int64_t rows) {
         parallel_ranges(rows, 16, [&](int64_t r0, int64_t r1) {
@@ -1408,11 +1434,16 @@ static bool plan_download_fit(rs_svd_plan* pl, double* P, double* Q, double* bu,
     unpack(st, P, bu, pl->n_users);
     unpack(st + pn, Q, bi, pl->n_items);
     if (flag) {
-        RS_HIP(hipMemsetAsync(pl->numflag.p, 0, sizeof(int32_t), s));
-        RS_HIP(hipStreamSynchronize(s));
+        plan_clear_flag(pl);
         throw NumericError{"item factors left the fixed-point range (non-finite or |q| >= 128) during "
                            "an epoch; the returned model is not trustworthy"};
     }
+}
+
+static bool plan_download_fit(rs_svd_plan* pl, double* P, double* Q, double* bu, double* bi, double* gb) {
+    int32_t flag = 0;
+    if (!plan_fetch_fit(pl, gb, &flag)) return false;
+    plan_finish_fit(pl, P, Q, bu, bi, flag);
     return true;
 }
 
@@ -2216,6 +2247,7 @@ extern "C" int rs_svd_fit(rs_ctx* ctx, const rs_ratings* r, const rs_sgd_params*
             auto cache = std::static_pointer_cast<rs::SvdFitCache>(ctx->svd_fit_cache);
             const bool hit = rs::fit_cache_on() && cache && cache->matches(r, p->n_factors, wb);
             mark(hit ? "cache-hit" : "cache-miss");
+            bool prepared = false;  // warm start done and factors packed during the device build
             if (!hit) {
                 const bool dev = wb == RS_SGD_WB_TILE && r->nnz > 0 && r->nnz <= rs::kDeviceBuildMaxNnz && rs::fit_device_build_on();
                 auto old = dev ? cache : nullptr;  // the device path recycles the old plan's buffers
@@ -2231,7 +2263,13 @@ extern "C" int rs_svd_fit(rs_ctx* ctx, const rs_ratings* r, const rs_sgd_params*
                         cache->ratings = std::move(old->ratings);
                     }
                     old.reset();
-                    rs::plan_build_coo_device(ctx, r, p->n_factors, cache->plan.get());
+                    rs_svd_plan* np = cache->plan.get();
+                    np->build_overlap = [&, np] {  // under the device build's kernels
+                        if (p->n_epochs > 0) *gb = rs::gb_warm_start(r, bu, bi);
+                        prepared = rs::plan_pack_fit(np, P, Q, bu, bi);
+                    };
+                    rs::plan_build_coo_device(ctx, r, p->n_factors, np);
+                    np->build_overlap = nullptr;
                 } else {
                     rs::UserCSR csr;
                     rs::build_csr(r->nnz, r->n_users, r->users, r->items, r->ratings, csr);
@@ -2270,10 +2308,16 @@ extern "C" int rs_svd_fit(rs_ctx* ctx, const rs_ratings* r, const rs_sgd_params*
             // and halving them halves that staleness.  The plan keeps the smaller grid for later fits of the
             // same ratings.  Only then does the caller see RS_ERR_NUMERIC (a Go Fit that panics on an error
             // never gets a NaN model first).
+            bool fetched = false;  // the results are in staging (fetched with the divergence check)
+            int32_t flag = 0;
             for (int attempt = 0;; ++attempt) {
-                if (p->n_epochs > 0) *gb = rs::gb_warm_start(r, bu, bi);
-                mark("warm");
-                if (!rs::plan_upload_fit(&pl, P, Q, bu, bi, gb)) rs::plan_upload(&pl, P, Q, bu, bi, gb);
+                if (attempt == 0 && prepared) {
+                    rs::plan_dma_fit(&pl, gb);
+                } else {
+                    if (p->n_epochs > 0) *gb = rs::gb_warm_start(r, bu, bi);
+                    mark("warm");
+                    if (!rs::plan_upload_fit(&pl, P, Q, bu, bi, gb)) rs::plan_upload(&pl, P, Q, bu, bi, gb);
+                }
                 mark("upload");
                 rs::kernel_span_begin(ctx);
                 rs::plan_epochs(&pl, p->n_epochs, lr, reg, ctx->stream);
@@ -2285,15 +2329,22 @@ extern "C" int rs_svd_fit(rs_ctx* ctx, const rs_ratings* r, const rs_sgd_params*
                     keep_coo();
                     mark("cache-copy");
                 }
-                if (wb != RS_SGD_WB_TILE || attempt == 3 || !rs::plan_diverged(&pl)) break;
-                if (pl.tile_grid <= 1) break;
+                if (wb != RS_SGD_WB_TILE || attempt == 3 || pl.tile_grid <= 1) break;
+                // the divergence check rides on the results' download (one wait instead of two)
+                bool diverged;
+                if ((fetched = rs::plan_fetch_fit(&pl, gb, &flag))) diverged = flag != 0 || !std::isfinite(*gb);
+                else diverged = rs::plan_diverged(&pl);
+                if (!diverged) break;
+                if (fetched && flag) rs::plan_clear_flag(&pl);
+                fetched = false;
                 pl.tile_wg = std::max(1, pl.tile_grid / 2);
                 rs::tile_build(&pl);
                 pl.n_blocks = rs::tile_partials(&pl);
                 ++ctx->fit_refits;
                 if (trace) std::fprintf(stderr, "fit-trace diverged: refit on %d workgroups\n", pl.tile_wg);
             }
-            if (!rs::plan_download_fit(&pl, P, Q, bu, bi, gb)) rs::plan_download(&pl, P, Q, bu, bi, gb);
+            if (fetched) rs::plan_finish_fit(&pl, P, Q, bu, bi, flag);
+            else if (!rs::plan_download_fit(&pl, P, Q, bu, bi, gb)) rs::plan_download(&pl, P, Q, bu, bi, gb);
             mark("download");
             return RS_OK;
         }

@@ -5,6 +5,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
+#include <functional>
 #include <stdexcept>
 #include <string>
 #include <memory>
@@ -127,6 +128,7 @@ struct rs_svd_plan {
     rs::DevBuf<int32_t> coo_users, coo_items;  // device COO of a device-built schedule (any rating order)
     rs::DevBuf<float> coo_vals;
     rs::DevBuf<char> sched_ws;                 // its build workspace (kept for refits)
+    std::function<void()> build_overlap;       // host work run (once) while the device build's kernels execute
     ~rs_svd_plan() {
         if (ev0) (void)hipEventDestroy(ev0);
         if (ev1) (void)hipEventDestroy(ev1);

@@ -345,11 +345,17 @@ class Context:
         return d.value, rule.value
 
     def svd_fit(self, r: Ratings, P, Q, bu=None, bi=None, gb=0.0, n_epochs=20, lr=0.005,
-                reg=0.02, mode=SGD_FAST, write_back=WB_TILE):
-        P = np.array(P, dtype=np.float64, order="C")
-        Q = np.array(Q, dtype=np.float64, order="C")
-        bu = np.zeros(r.n_users) if bu is None else np.array(bu, dtype=np.float64)
-        bi = np.zeros(r.n_items) if bi is None else np.array(bi, dtype=np.float64)
+                reg=0.02, mode=SGD_FAST, write_back=WB_TILE, inplace=False):
+        """core/svd.go:63-132 through rs_svd_fit.  inplace=True: P, Q, bu, bi (float64, C order) are trained in
+        place, as the Go binding's slices are (no copies); otherwise copies are trained and returned."""
+        if inplace:
+            for a in (P, Q, bu, bi):
+                assert isinstance(a, np.ndarray) and a.dtype == np.float64 and a.flags.c_contiguous and a.flags.writeable
+        else:
+            P = np.array(P, dtype=np.float64, order="C")
+            Q = np.array(Q, dtype=np.float64, order="C")
+            bu = np.zeros(r.n_users) if bu is None else np.array(bu, dtype=np.float64)
+            bi = np.zeros(r.n_items) if bi is None else np.array(bi, dtype=np.float64)
         g = np.array([gb], dtype=np.float64)
         assert P.shape == (r.n_users, P.shape[1]) and Q.shape == (r.n_items, P.shape[1])
         prm = _SgdParams(P.shape[1], n_epochs, lr, reg, mode, write_back)

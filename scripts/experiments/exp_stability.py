@@ -75,10 +75,13 @@ def run(ctx, name, claim, cap, log, wg=0):
     except rsgpu.RsError as e:
         numeric = f"RS_ERR {e.code}"
     plan.close()
+    out = {"nnz": nnz, "hot_share": hot / nnz, "k": k, "rmse0": r0, "curve": curve, "ref_curve": ref_curve,
+           "numeric": numeric, "epoch_ms": ms / ep}
     log(f"{name:12s} claim {claim} cap {cap or 'auto'} wg {wg or 'all'}: nnz {nnz} hottest {hot} ({100.0 * hot / nnz:.2f} %) k {k} "
         f"epoch {ms / ep:.2f} ms  held-out {r0:.4f} -> " + " ".join(f"{x:.4f}" for x in curve) +
         (("  | reference " + " ".join(f"{x:.4f}" for x in ref_curve)) if ref_curve else "") +
         f"  [{numeric}, {time.time() - t0:.0f} s]")
+    return out
 
 
 def run_fit(ctx, name, log):
@@ -100,8 +103,10 @@ def run_fit(ctx, name, log):
         e = float(np.sqrt(np.mean((O.svd_predict(hu, hi, *got) - hr) ** 2)))
         res = f"held-out RMSE after {ep} epochs {e:.4f}"
     except rsgpu.RsError as x:
+        e = None
         res = f"RS_ERR {x.code}"
     log(f"{name:12s} rs_svd_fit: {res}, refits {ctx.fit_refits()} ({time.time() - t0:.1f} s)")
+    return {"rmse": e, "refits": ctx.fit_refits()}
 
 
 def main():
