@@ -286,6 +286,14 @@ int rs_svd_plan_set_tile_claim(rs_svd_plan* plan, int32_t runs_per_claim);
  * Both snake builds give byte-identical schedules (rs_svd_plan_schedule_digest); where the rule does not
  * apply (a user above the LDS bound, a tile past the LDS) the device build falls back to RS_TILE_RULE_LPT
  * and RS_TILE_RULE_SNAKE fails with RS_ERR_UNSUPPORTED.  Rebuilds the schedule. */
+/* Divergence guard of the tile schedule (default on): rs_svd_plan_epochs checks a call's epochs once at the
+ * end (fixed-point range of P and Q, a finite GlobalBias; one small readback, so the call waits for its
+ * epochs) and redoes a failed call from its start state -- P, Q and GlobalBias copied on the device first --
+ * on half the workgroups, up to three times; the plan keeps the smaller grid.  A call still failing leaves
+ * the flag for the download (RS_ERR_NUMERIC).  rs_svd_fit always runs guarded.  off: no snapshot, no wait. */
+int rs_svd_plan_set_guard(rs_svd_plan* plan, int32_t on);
+/* Calls the guard has redone on this plan so far. */
+int rs_svd_plan_refits(const rs_svd_plan* plan, int32_t* n);
 #define RS_TILE_RULE_LPT 0
 #define RS_TILE_RULE_SNAKE 1
 #define RS_TILE_RULE_SNAKE_DEVICE 2

@@ -39,6 +39,7 @@
 
 #include <algorithm>
 #include <atomic>
+#include <functional>
 #include <cstring>
 #include <memory>
 #include <chrono>
@@ -1571,6 +1572,14 @@ static void plan_download(rs_svd_plan* pl, double* P, double* Q, double* bu, dou
     }
 }
 
+// P rows out of the fixed-point range of the tile kernel's LDS (|p| >= 127.5, or non-finite): flag
+__global__ __launch_bounds__(256) void p_range_kernel(const float* __restrict__ P, int64_t n, int32_t* __restrict__ flag) {
+    bool bad = false;
+    for (int64_t t = static_cast<int64_t>(blockIdx.x) * 256 + threadIdx.x; t < n; t += static_cast<int64_t>(gridDim.x) * 256)
+        bad |= !(fabsf(P[t]) < 127.5f);
+    if (bad) flag[0] = 1;
+}
+
 // After a call's epochs: did the model leave the fixed-point range or go non-finite (the Q conversion's flag,
 // a non-finite GlobalBias)?  Waits for the stream; clears the flag when it is raised.
 static bool plan_diverged(rs_svd_plan* pl) {
@@ -1588,7 +1597,7 @@ static bool plan_diverged(rs_svd_plan* pl) {
     return f != 0 || !std::isfinite(g);
 }
 
-static void plan_epochs(rs_svd_plan* pl, int32_t epochs, float lr, float reg, hipStream_t s) {
+static void plan_epochs_once(rs_svd_plan* pl, int32_t epochs, float lr, float reg, hipStream_t s) {
     const double inv_nnz = pl->nnz > 0 ? 1.0 / static_cast<double>(pl->nnz) : 0.0;
     if (pl->timing) {
         while (static_cast<int32_t>(pl->tev.size()) < 2 * epochs) {
@@ -1654,6 +1663,62 @@ static void plan_epochs(rs_svd_plan* pl, int32_t epochs, float lr, float reg, hi
     pl->last_launches = pl->timing ? epochs : (2 + (pl->n_split > 0) + (pl->n_isplit > 0)) * epochs;
     pl->last_stream = s;
     pl->last_ms = -1.0;  // resolved lazily by rs_svd_plan_last_kernel_ms
+}
+
+// The divergence guard (tile schedule).  What diverges under the FAST schedule is a hot item's
+// q_i / b_i: the updates other runs apply between a run's read of the row and its write grow with the
+// chip-wide update rate, i.e. with the workgroups in flight, and halving them halves
+// that staleness.  So a call's epochs are checked once, at the end (the Q conversion's range flag, a P range
+// scan, a finite GlobalBias: one small readback), and a call that failed is redone from its start state --
+// P, Q and GlobalBias copied on the device before the first epoch -- on half the workgroups, up to three
+// times; the plan keeps the smaller grid.  Only then does the caller see the flag (RS_ERR_NUMERIC at
+// download).  `under` is host work run while the first attempt's kernels execute.
+static void plan_epochs(rs_svd_plan* pl, int32_t epochs, float lr, float reg, hipStream_t s,
+                        const std::function<void()>& under = nullptr) {
+    const bool guarded = pl->guard && pl->write_back == RS_SGD_WB_TILE && epochs > 0 && pl->tiles_built;
+    if (!guarded) {
+        plan_epochs_once(pl, epochs, lr, reg, s);
+        if (under) under();
+        return;
+    }
+    if (pl->P_snap.n != pl->P.n) pl->P_snap.alloc(pl->P.n);
+    if (pl->Q_snap.n != pl->Q.n) pl->Q_snap.alloc(pl->Q.n);
+    if (!pl->gb_snap.p) pl->gb_snap.alloc(1);
+    RS_HIP(hipMemcpyAsync(pl->P_snap.p, pl->P.p, pl->P.n * sizeof(float), hipMemcpyDeviceToDevice, s));
+    RS_HIP(hipMemcpyAsync(pl->Q_snap.p, pl->Q.p, pl->Q.n * sizeof(float), hipMemcpyDeviceToDevice, s));
+    RS_HIP(hipMemcpyAsync(pl->gb_snap.p, pl->gb.p, sizeof(double), hipMemcpyDeviceToDevice, s));
+    struct Check {  // pinned readback slot, per thread
+        int64_t* p = nullptr;
+        Check() { RS_HIP(hipHostMalloc(reinterpret_cast<void**>(&p), 16, hipHostMallocPortable)); }
+    };
+    thread_local Check ck;
+    int32_t* flag = numflag(pl);
+    for (int attempt = 0;; ++attempt) {
+        plan_epochs_once(pl, epochs, lr, reg, s);
+        const int64_t pn = static_cast<int64_t>(pl->P.n);
+        hipLaunchKernelGGL(p_range_kernel, dim3(static_cast<int>(std::min<int64_t>(1024, (pn + 255) / 256))), dim3(256), 0, s,
+                           pl->P.p, pn, flag);
+        RS_HIP(hipGetLastError());
+        RS_HIP(hipMemcpyAsync(ck.p, pl->gb.p, sizeof(double), hipMemcpyDeviceToHost, s));
+        RS_HIP(hipMemcpyAsync(ck.p + 1, flag, sizeof(int32_t), hipMemcpyDeviceToHost, s));
+        if (attempt == 0 && under) under();
+        RS_HIP(hipStreamSynchronize(s));
+        double g;
+        std::memcpy(&g, ck.p, 8);
+        const bool bad = static_cast<int32_t>(ck.p[1]) != 0 || !std::isfinite(g);
+        if (!bad || attempt == 3 || pl->tile_grid <= 1) return;  // (a flag still raised reaches the download)
+        RS_HIP(hipMemsetAsync(flag, 0, sizeof(int32_t), s));
+        RS_HIP(hipMemcpyAsync(pl->P.p, pl->P_snap.p, pl->P.n * sizeof(float), hipMemcpyDeviceToDevice, s));
+        RS_HIP(hipMemcpyAsync(pl->Q.p, pl->Q_snap.p, pl->Q.n * sizeof(float), hipMemcpyDeviceToDevice, s));
+        RS_HIP(hipMemcpyAsync(pl->gb.p, pl->gb_snap.p, sizeof(double), hipMemcpyDeviceToDevice, s));
+        RS_HIP(hipStreamSynchronize(s));
+        pl->tile_wg = std::max(1, pl->tile_grid / 2);
+        tile_build(pl);
+        pl->n_blocks = tile_partials(pl);
+        ++pl->refits;
+        static const bool trace = std::getenv("RSGPU_FIT_TRACE") != nullptr;
+        if (trace) std::fprintf(stderr, "fit-trace diverged: redone on %d workgroups\n", pl->tile_wg);
+    }
 }
 
 static int check_sgd(rs_ctx* ctx, const rs_ratings* r, const rs_sgd_params* p) {
@@ -1964,6 +2029,21 @@ extern "C" int rs_svd_plan_set_tile_rule(rs_svd_plan* pl, int32_t rule) {
         if (pl->write_back == RS_SGD_WB_TILE) pl->n_blocks = rs::tile_partials(pl);
         return RS_OK;
     });
+}
+
+extern "C" int rs_svd_plan_set_guard(rs_svd_plan* pl, int32_t on) {
+    if (!pl) return rs::set_error(nullptr, RS_ERR_INVALID, "plan is NULL");
+    return rs_guard(pl->ctx, [&]() -> int {
+        rs::plan_sync_last(pl);
+        pl->guard = on != 0;
+        return RS_OK;
+    });
+}
+
+extern "C" int rs_svd_plan_refits(const rs_svd_plan* pl, int32_t* n) {
+    if (!pl || !n) return rs::set_error(pl ? pl->ctx : nullptr, RS_ERR_INVALID, "bad arguments");
+    *n = pl->refits;
+    return RS_OK;
 }
 
 extern "C" int rs_svd_plan_tile_rule(const rs_svd_plan* pl, int32_t* rule) {
@@ -2299,50 +2379,30 @@ extern "C" int rs_svd_fit(rs_ctx* ctx, const rs_ratings* r, const rs_sgd_params*
                 ctx->svd_fit_cache = cache;
             };
             rs_svd_plan& pl = *cache->plan;
-            ctx->fit_refits = 0;
-            // Divergence guard (tile schedule): a fit that leaves the fixed-point range or goes non-finite is
-            // redone from the caller's inputs (still intact: nothing is written back before the check) on half
-            // the workgroups, up to three times.  What diverges is a hot item's q_i / b_i under Hogwild
-            // staleness: the updates other workgroups apply between a run's read of the row and its write
-            // grow with the chip-wide update rate, i.e. with the workgroups in flight,
-            // and halving them halves that staleness.  The plan keeps the smaller grid for later fits of the
-            // same ratings.  Only then does the caller see RS_ERR_NUMERIC (a Go Fit that panics on an error
-            // never gets a NaN model first).
-            bool fetched = false;  // the results are in staging (fetched with the divergence check)
-            int32_t flag = 0;
-            for (int attempt = 0;; ++attempt) {
-                if (attempt == 0 && prepared) {
-                    rs::plan_dma_fit(&pl, gb);
-                } else {
-                    if (p->n_epochs > 0) *gb = rs::gb_warm_start(r, bu, bi);
-                    mark("warm");
-                    if (!rs::plan_upload_fit(&pl, P, Q, bu, bi, gb)) rs::plan_upload(&pl, P, Q, bu, bi, gb);
-                }
-                mark("upload");
-                rs::kernel_span_begin(ctx);
-                rs::plan_epochs(&pl, p->n_epochs, lr, reg, ctx->stream);
-                rs::kernel_span_record(ctx);
-                if (attempt == 0 && !trace) keep_coo();  // host work under the epochs
-                rs::kernel_span_wait(ctx);
-                mark("epochs");
-                if (attempt == 0 && trace) {
-                    keep_coo();
-                    mark("cache-copy");
-                }
-                if (wb != RS_SGD_WB_TILE || attempt == 3 || pl.tile_grid <= 1) break;
-                // the divergence check rides on the results' download (one wait instead of two)
-                bool diverged;
-                if ((fetched = rs::plan_fetch_fit(&pl, gb, &flag))) diverged = flag != 0 || !std::isfinite(*gb);
-                else diverged = rs::plan_diverged(&pl);
-                if (!diverged) break;
-                if (fetched && flag) rs::plan_clear_flag(&pl);
-                fetched = false;
-                pl.tile_wg = std::max(1, pl.tile_grid / 2);
-                rs::tile_build(&pl);
-                pl.n_blocks = rs::tile_partials(&pl);
-                ++ctx->fit_refits;
-                if (trace) std::fprintf(stderr, "fit-trace diverged: refit on %d workgroups\n", pl.tile_wg);
+            // Divergence guard: plan_epochs redoes a call that left the fixed-point range or went non-finite on
+            // half the workgroups (up to three times; the plan keeps the smaller grid), so a Go Fit that panics on
+            // an error never gets a NaN model first; RS_ERR_NUMERIC only when every attempt failed.
+            const int32_t refits0 = pl.refits;
+            if (prepared) {
+                rs::plan_dma_fit(&pl, gb);
+            } else {
+                if (p->n_epochs > 0) *gb = rs::gb_warm_start(r, bu, bi);
+                mark("warm");
+                if (!rs::plan_upload_fit(&pl, P, Q, bu, bi, gb)) rs::plan_upload(&pl, P, Q, bu, bi, gb);
             }
+            mark("upload");
+            rs::kernel_span_begin(ctx);
+            rs::plan_epochs(&pl, p->n_epochs, lr, reg, ctx->stream, trace ? std::function<void()>() : std::function<void()>(keep_coo));
+            rs::kernel_span_end(ctx);
+            ctx->fit_refits = pl.refits - refits0;
+            mark("epochs");
+            if (trace) {
+                keep_coo();
+                mark("cache-copy");
+            }
+            bool fetched = false;
+            int32_t flag = 0;
+            fetched = rs::plan_fetch_fit(&pl, gb, &flag);
             if (fetched) rs::plan_finish_fit(&pl, P, Q, bu, bi, flag);
             else if (!rs::plan_download_fit(&pl, P, Q, bu, bi, gb)) rs::plan_download(&pl, P, Q, bu, bi, gb);
             mark("download");

@@ -129,6 +129,12 @@ struct rs_svd_plan {
     rs::DevBuf<float> coo_vals;
     rs::DevBuf<char> sched_ws;                 // its build workspace (kept for refits)
     std::function<void()> build_overlap;       // host work run (once) while the device build's kernels execute
+    // divergence guard of the tile schedule (rs_svd_plan_set_guard, default on): a call's epochs that leave the
+    // fixed-point range or go non-finite are redone from the call-start state on half the workgroups
+    int32_t guard = 1;
+    int32_t refits = 0;                        // redone calls so far (rs_svd_plan_refits)
+    rs::DevBuf<float> P_snap, Q_snap;          // the call-start state (allocated on first use)
+    rs::DevBuf<double> gb_snap;
     ~rs_svd_plan() {
         if (ev0) (void)hipEventDestroy(ev0);
         if (ev1) (void)hipEventDestroy(ev1);

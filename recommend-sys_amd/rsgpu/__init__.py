@@ -43,7 +43,7 @@ HEADER_SYMBOLS = (
     "rs_svd_plan_set_item_weights", "rs_svd_plan_epoch_qdelta", "rs_svd_plan_apply_qdelta",
     "rs_svd_plan_set_hot_replicas", "rs_svd_plan_set_fixed_q", "rs_svd_plan_set_tiles",
     "rs_svd_plan_set_tile_claim", "rs_svd_plan_tile_order", "rs_svd_plan_tile_clocks",
-    "rs_svd_plan_set_tile_rule", "rs_svd_plan_tile_rule", "rs_svd_plan_schedule_digest", "rs_fit_schedule_digest",
+    "rs_svd_plan_set_tile_rule", "rs_svd_plan_tile_rule", "rs_svd_plan_set_guard", "rs_svd_plan_refits", "rs_svd_plan_schedule_digest", "rs_fit_schedule_digest",
     "rs_comm_unique_id", "rs_svd_plan_join", "rs_svd_plan_epochs_sharded", "rs_svd_plan_leave",
     "rs_svd_plan_set_user_blocks", "rs_svd_group_create", "rs_svd_group_epochs", "rs_svd_group_destroy",
     "rs_item_shards", "rs_svd_fit_multi", "rs_tile_schedule_host", "rs_svd_plan_set_exchange",
@@ -148,6 +148,8 @@ def lib():
             "rs_svd_plan_set_tiles": (C.c_int, [_vp, _i32, _i32, _i32, _i32, _i32]),
             "rs_svd_plan_set_tile_claim": (C.c_int, [_vp, _i32]),
             "rs_svd_plan_set_tile_rule": (C.c_int, [_vp, _i32]),
+            "rs_svd_plan_set_guard": (C.c_int, [_vp, _i32]),
+            "rs_svd_plan_refits": (C.c_int, [_vp, C.POINTER(_i32)]),
             "rs_svd_plan_tile_rule": (C.c_int, [_vp, C.POINTER(_i32)]),
             "rs_svd_plan_schedule_digest": (C.c_int, [_vp, C.POINTER(C.c_uint64)]),
             "rs_fit_schedule_digest": (C.c_int, [_vp, C.POINTER(C.c_uint64), C.POINTER(_i32)]),
@@ -534,6 +536,15 @@ class SvdPlan:
     def set_tile_rule(self, rule):
         """TILE_RULE_LPT / _SNAKE / _SNAKE_DEVICE (rs_svd_plan_set_tile_rule); rebuilds the tiles."""
         self.ctx.check(lib().rs_svd_plan_set_tile_rule(self.h, rule))
+
+    def set_guard(self, on=True):
+        """Divergence guard of the tile schedule (rs_svd_plan_set_guard; default on)."""
+        self.ctx.check(lib().rs_svd_plan_set_guard(self.h, int(bool(on))))
+
+    def refits(self):
+        v = _i32(0)
+        self.ctx.check(lib().rs_svd_plan_refits(self.h, C.byref(v)))
+        return v.value
 
     def tile_rule(self):
         v = _i32(0)

@@ -74,13 +74,14 @@ def run(ctx, name, claim, cap, log, wg=0):
         numeric = "ok"
     except rsgpu.RsError as e:
         numeric = f"RS_ERR {e.code}"
+    refits = plan.refits()
     plan.close()
     out = {"nnz": nnz, "hot_share": hot / nnz, "k": k, "rmse0": r0, "curve": curve, "ref_curve": ref_curve,
-           "numeric": numeric, "epoch_ms": ms / ep}
+           "numeric": numeric, "epoch_ms": ms / ep, "refits": refits}
     log(f"{name:12s} claim {claim} cap {cap or 'auto'} wg {wg or 'all'}: nnz {nnz} hottest {hot} ({100.0 * hot / nnz:.2f} %) k {k} "
         f"epoch {ms / ep:.2f} ms  held-out {r0:.4f} -> " + " ".join(f"{x:.4f}" for x in curve) +
         (("  | reference " + " ".join(f"{x:.4f}" for x in ref_curve)) if ref_curve else "") +
-        f"  [{numeric}, {time.time() - t0:.0f} s]")
+        f"  [{numeric}, refits {refits}, {time.time() - t0:.0f} s]")
     return out
 
 

@@ -44,3 +44,29 @@ def test_stable_and_falling(ctx, S, name):
     assert out["numeric"] == "ok" and all(np.isfinite(c))
     assert all(b < a for a, b in zip(c, c[1:])), c
     assert c[-1] < c[0] - 0.1
+
+
+def test_guard_redoes_a_diverging_call(ctx):
+    """lr = 2 diverges on any grid: the guard redoes the call three times on half the workgroups each, then
+    leaves RS_ERR_NUMERIC for the download; a sane call afterwards is not redone; guard off: no redo."""
+    import rsgpu
+    from rsgpu import synth
+    u, i, r, nu, ni = synth.ml1m_like(seed=3)
+    plan = ctx.svd_plan(rsgpu.Ratings(u, i, r, nu, ni), 64)
+    plan.init_normal(0.0, 0.1, seed=1)
+    plan.upload(gb=float(np.mean(r)))
+    plan.epochs(2, lr=2.0)
+    assert plan.refits() == 3
+    with pytest.raises(rsgpu.RsError) as e:
+        plan.download()
+    assert e.value.code == -6
+    plan.init_normal(0.0, 0.1, seed=1)
+    plan.upload(gb=float(np.mean(r)))
+    plan.epochs(3)
+    assert plan.refits() == 3
+    P, Q, bu, bi, gb = plan.download()
+    assert np.isfinite(P).all() and np.isfinite(Q).all()
+    plan.set_guard(False)
+    plan.epochs(1, lr=2.0)
+    assert plan.refits() == 3
+    plan.close()
