@@ -309,6 +309,11 @@ bool tile_build_device(rs_svd_plan* pl) {
                        w.deg_i, ni, w.stats);
     RS_HIP(hipGetLastError());
     RS_HIP(hipMemcpyAsync(h, w.stats, 4 * sizeof(int32_t), hipMemcpyDeviceToHost, s));
+    if (pl->build_overlap) {  // the caller's host work (rs_svd_fit: GlobalBias warm start, factor packing) runs
+        auto f = std::move(pl->build_overlap);  // under the COO upload and the degree kernels
+        pl->build_overlap = nullptr;
+        f();
+    }
     RS_HIP(hipStreamSynchronize(s));
     const int32_t n_active = h[0], dmax_u = h[1], dmax_i = h[2];
     tmark("degrees");
@@ -374,11 +379,6 @@ bool tile_build_device(rs_svd_plan* pl) {
                        w.head, w.rid, w.pscan, n, T, nw, ld, pl->t_tiles.p, pl->t_runs.p, pl->t_streams.p, w.stats);
     RS_HIP(hipGetLastError());
     RS_HIP(hipMemcpyAsync(h + 3, w.stats + 3, 2 * sizeof(int32_t), hipMemcpyDeviceToHost, s));
-    if (pl->build_overlap) {  // the caller's host work (rs_svd_fit: GlobalBias warm start, factor packing)
-        auto f = std::move(pl->build_overlap);
-        pl->build_overlap = nullptr;
-        f();
-    }
     RS_HIP(hipStreamSynchronize(s));
     const size_t lds = static_cast<size_t>(h[3]);
     tmark("emit");

@@ -1346,6 +1346,9 @@ static void plan_recycle(rs_svd_plan* pl, rs_svd_plan* old, int32_t n_users, int
     pl->t_split_rows = std::move(old->t_split_rows);
     pl->partial = std::move(old->partial);
     pl->numflag = std::move(old->numflag);  // (zero: a raised flag is cleared when it is reported)
+    if (old->P_snap.n == static_cast<size_t>(std::max(1, n_users)) * fast_ld(k)) pl->P_snap = std::move(old->P_snap);
+    if (old->Q_snap.n == static_cast<size_t>(std::max(1, n_items)) * fast_ld(k)) pl->Q_snap = std::move(old->Q_snap);
+    pl->gb_snap = std::move(old->gb_snap);
     pl->gb = std::move(old->gb);
     if (old->ld == fast_ld(k) && old->n_users == n_users) pl->P = std::move(old->P);
     if (old->ld == fast_ld(k) && old->n_items == n_items && old->n_qrows == old->n_items) pl->Q = std::move(old->Q);
@@ -1357,24 +1360,35 @@ static void plan_recycle(rs_svd_plan* pl, rs_svd_plan* old, int32_t n_users, int
 // staging slot 1 (one DMA per matrix, no intermediate vectors); past 256 MiB of rows the plan_upload /
 // plan_download path (pageable) is taken instead.
 constexpr size_t kFitStageMax = size_t{256} << 20;
+// pinned scalars of rs_svd_fit's copies (a copy to or from pageable memory waits for the stream's earlier work,
+// which would serialise the host work meant to run under the epochs)
+struct FitScalars {
+    double* p = nullptr;  // [0] GlobalBias in, [1] GlobalBias out, [2] flag out (int32)
+    FitScalars() { RS_HIP(hipHostMalloc(reinterpret_cast<void**>(&p), 32, hipHostMallocPortable)); }
+};
+static FitScalars& fit_scalars() {
+    thread_local FitScalars f;
+    return f;
+}
+
 // host half: the rows packed into staging slot 1 (false: too large, nothing done)
 static bool plan_pack_fit(rs_svd_plan* pl, const double* P, const double* Q, const double* bu, const double* bi) {
     const size_t pn = static_cast<size_t>(std::max(1, pl->n_users)) * pl->ld, qn = static_cast<size_t>(std::max(1, pl->n_items)) * pl->ld;
     if ((pn + qn) * 4 > kFitStageMax) return false;
     float* st = static_cast<float*>(pinned_staging((pn + qn) * 4, 1));
     const int32_t k = pl->k, ld = pl->ld;
-    auto pack = [&](float* dst, const double* F, const double* bias, int64_t rows) {
-        parallel_ranges(rows, 16, [&](int64_t r0, int64_t r1) {
-            for (int64_t r = r0; r < r1; ++r) {
-                float* d = dst + r * ld;
-                for (int32_t f = 0; f < k; ++f) d[f] = static_cast<float>(F[r * k + f]);
-                d[k] = static_cast<float>(bias[r]);
-                for (int32_t f = k + 1; f < ld; ++f) d[f] = 0.f;
-            }
-        });
-    };
-    pack(st, P, bu, pl->n_users);
-    pack(st + pn, Q, bi, pl->n_items);
+    const int64_t nu = pl->n_users, ni = pl->n_items;
+    parallel_ranges(nu + ni, 16, [&](int64_t r0, int64_t r1) {  // P rows then Q rows, one pass
+        for (int64_t r = r0; r < r1; ++r) {
+            const bool u = r < nu;
+            const int64_t x = u ? r : r - nu;
+            float* d = (u ? st : st + pn) + x * ld;
+            const double* F = (u ? P : Q) + x * k;
+            for (int32_t f = 0; f < k; ++f) d[f] = static_cast<float>(F[f]);
+            d[k] = static_cast<float>((u ? bu : bi)[x]);
+            for (int32_t f = k + 1; f < ld; ++f) d[f] = 0.f;
+        }
+    });
     return true;
 }
 
@@ -1387,7 +1401,9 @@ static void plan_dma_fit(rs_svd_plan* pl, const double* gb) {
     pl->P.upload(st, static_cast<size_t>(pl->n_users) * pl->ld, s);
     pl->Q.upload(st + pn, static_cast<size_t>(pl->n_items) * pl->ld, s);
     sync_item_copies(pl, s, 1);
-    pl->gb.upload(gb, 1, s);  // (8 bytes from pageable memory: the runtime copies it before returning)
+    double* sc = fit_scalars().p;
+    sc[0] = *gb;
+    pl->gb.upload(sc, 1, s);
 }
 
 static bool plan_upload_fit(rs_svd_plan* pl, const double* P, const double* Q, const double* bu, const double* bi,
@@ -1397,43 +1413,53 @@ static bool plan_upload_fit(rs_svd_plan* pl, const double* P, const double* Q, c
     return true;
 }
 
-// D2H of P and Q (staging slot 1), GlobalBias and the numeric flag, one wait (false: too large for staging)
-static bool plan_fetch_fit(rs_svd_plan* pl, double* gb, int32_t* flag) {
+static bool fit_fits_staging(const rs_svd_plan* pl) {
     const size_t pn = static_cast<size_t>(std::max(1, pl->n_users)) * pl->ld, qn = static_cast<size_t>(std::max(1, pl->n_items)) * pl->ld;
-    if ((pn + qn) * 4 > kFitStageMax) return false;
-    plan_sync_last(pl);
+    return (pn + qn) * 4 <= kFitStageMax;
+}
+
+// enqueues the D2H of P and Q (staging slot 1), GlobalBias and the numeric flag (pinned scalars) on the ctx
+// stream; plan_fetch_result reads the scalars after the wait
+static void plan_fetch_enqueue(rs_svd_plan* pl) {
+    const size_t pn = static_cast<size_t>(std::max(1, pl->n_users)) * pl->ld, qn = static_cast<size_t>(std::max(1, pl->n_items)) * pl->ld;
     hipStream_t s = pl->ctx->stream;
     float* st = static_cast<float*>(pinned_staging((pn + qn) * 4, 1));
+    double* sc = fit_scalars().p;
     pl->P.download(st, static_cast<size_t>(pl->n_users) * pl->ld, s);
     pl->Q.download(st + pn, static_cast<size_t>(pl->n_items) * pl->ld, s);
-    pl->gb.download(gb, 1, s);
-    *flag = 0;
-    if (pl->numflag.p) pl->numflag.download(flag, 1, s);
-    RS_HIP(hipStreamSynchronize(s));
-    return true;
+    pl->gb.download(sc + 1, 1, s);
+    int32_t* f = reinterpret_cast<int32_t*>(sc + 2);
+    *f = 0;
+    if (pl->numflag.p) RS_HIP(hipMemcpyAsync(f, pl->numflag.p, sizeof(int32_t), hipMemcpyDeviceToHost, s));
 }
+static void plan_fetch_result(double* gb, int32_t* flag) {
+    const double* sc = fit_scalars().p;
+    *gb = sc[1];
+    *flag = *reinterpret_cast<const int32_t*>(sc + 2);
+}
+
 
 static void plan_clear_flag(rs_svd_plan* pl) {
     RS_HIP(hipMemsetAsync(pl->numflag.p, 0, sizeof(int32_t), pl->ctx->stream));
     RS_HIP(hipStreamSynchronize(pl->ctx->stream));
 }
 
-// after plan_fetch_fit: the f64 rows; a raised flag is cleared and reported (values already written)
+// after plan_fetch_enqueue and a wait: the f64 rows; a raised flag is cleared and reported (values already written)
 static void plan_finish_fit(rs_svd_plan* pl, double* P, double* Q, double* bu, double* bi, int32_t flag) {
     const size_t pn = static_cast<size_t>(std::max(1, pl->n_users)) * pl->ld;
     const float* st = static_cast<const float*>(pinned_staging(0, 1));
     const int32_t k = pl->k, ld = pl->ld;
-    auto unpack = [&](const float* src, double* F, double* bias, int64_t rows) {
-        parallel_ranges(rows, 16, [&](int64_t r0, int64_t r1) {
-            for (int64_t r = r0; r < r1; ++r) {
-                const float* a = src + r * ld;
-                for (int32_t f = 0; f < k; ++f) F[r * k + f] = a[f];
-                bias[r] = a[k];
-            }
-        });
-    };
-    unpack(st, P, bu, pl->n_users);
-    unpack(st + pn, Q, bi, pl->n_items);
+    const int64_t nu = pl->n_users, ni = pl->n_items;
+    parallel_ranges(nu + ni, 16, [&](int64_t r0, int64_t r1) {  // P rows then Q rows, one pass
+        for (int64_t r = r0; r < r1; ++r) {
+            const bool u = r < nu;
+            const int64_t x = u ? r : r - nu;
+            const float* a = (u ? st : st + pn) + x * ld;
+            double* F = (u ? P : Q) + x * k;
+            for (int32_t f = 0; f < k; ++f) F[f] = a[f];
+            (u ? bu : bi)[x] = a[k];
+        }
+    });
     if (flag) {
         plan_clear_flag(pl);
         throw NumericError{"item factors left the fixed-point range (non-finite or |q| >= 128) during "
@@ -1441,12 +1467,6 @@ static void plan_finish_fit(rs_svd_plan* pl, double* P, double* Q, double* bu, d
     }
 }
 
-static bool plan_download_fit(rs_svd_plan* pl, double* P, double* Q, double* bu, double* bi, double* gb) {
-    int32_t flag = 0;
-    if (!plan_fetch_fit(pl, gb, &flag)) return false;
-    plan_finish_fit(pl, P, Q, bu, bi, flag);
-    return true;
-}
 
 static void plan_build(rs_ctx* ctx, const rs_ratings* r, int32_t k, rs_svd_plan* pl) {
     UserCSR csr;
@@ -1580,22 +1600,6 @@ __global__ __launch_bounds__(256) void p_range_kernel(const float* __restrict__ 
     if (bad) flag[0] = 1;
 }
 
-// After a call's epochs: did the model leave the fixed-point range or go non-finite (the Q conversion's flag,
-// a non-finite GlobalBias)?  Waits for the stream; clears the flag when it is raised.
-static bool plan_diverged(rs_svd_plan* pl) {
-    plan_sync_last(pl);
-    hipStream_t s = pl->ctx->stream;
-    double g = 0.0;
-    pl->gb.download(&g, 1, s);
-    int32_t f = 0;
-    if (pl->numflag.p) pl->numflag.download(&f, 1, s);
-    RS_HIP(hipStreamSynchronize(s));
-    if (f) {
-        RS_HIP(hipMemsetAsync(pl->numflag.p, 0, sizeof(int32_t), s));
-        RS_HIP(hipStreamSynchronize(s));
-    }
-    return f != 0 || !std::isfinite(g);
-}
 
 static void plan_epochs_once(rs_svd_plan* pl, int32_t epochs, float lr, float reg, hipStream_t s) {
     const double inv_nnz = pl->nnz > 0 ? 1.0 / static_cast<double>(pl->nnz) : 0.0;
@@ -1667,17 +1671,19 @@ static void plan_epochs_once(rs_svd_plan* pl, int32_t epochs, float lr, float re
 
 // The divergence guard (tile schedule).  What diverges under the FAST schedule is a hot item's
 // q_i / b_i: the updates other runs apply between a run's read of the row and its write grow with the
-// chip-wide update rate, i.e. with the workgroups in flight, and halving them halves
-// that staleness.  So a call's epochs are checked once, at the end (the Q conversion's range flag, a P range
+// chip-wide update rate, i.e. with the workgroups in flight, and halving them (and
+// the run cap: the automatic cap would grow as the grid shrinks) halves that staleness.  So a call's epochs are checked once, at the end (the Q conversion's range flag, a P range
 // scan, a finite GlobalBias: one small readback), and a call that failed is redone from its start state --
 // P, Q and GlobalBias copied on the device before the first epoch -- on half the workgroups, up to three
-// times; the plan keeps the smaller grid.  Only then does the caller see the flag (RS_ERR_NUMERIC at
+// times; the plan keeps the smaller grid and cap.  Only then does the caller see the flag (RS_ERR_NUMERIC at
 // download).  `under` is host work run while the first attempt's kernels execute.
 static void plan_epochs(rs_svd_plan* pl, int32_t epochs, float lr, float reg, hipStream_t s,
-                        const std::function<void()>& under = nullptr) {
+                        const std::function<void()>& under = nullptr, const std::function<void()>& after = nullptr) {
+    // `after` enqueues the caller's follow-up copies (rs_svd_fit: the results' download) before the guard's wait
     const bool guarded = pl->guard && pl->write_back == RS_SGD_WB_TILE && epochs > 0 && pl->tiles_built;
     if (!guarded) {
         plan_epochs_once(pl, epochs, lr, reg, s);
+        if (after) after();
         if (under) under();
         return;
     }
@@ -1701,6 +1707,7 @@ static void plan_epochs(rs_svd_plan* pl, int32_t epochs, float lr, float reg, hi
         RS_HIP(hipGetLastError());
         RS_HIP(hipMemcpyAsync(ck.p, pl->gb.p, sizeof(double), hipMemcpyDeviceToHost, s));
         RS_HIP(hipMemcpyAsync(ck.p + 1, flag, sizeof(int32_t), hipMemcpyDeviceToHost, s));
+        if (after) after();
         if (attempt == 0 && under) under();
         RS_HIP(hipStreamSynchronize(s));
         double g;
@@ -1712,7 +1719,9 @@ static void plan_epochs(rs_svd_plan* pl, int32_t epochs, float lr, float reg, hi
         RS_HIP(hipMemcpyAsync(pl->Q.p, pl->Q_snap.p, pl->Q.n * sizeof(float), hipMemcpyDeviceToDevice, s));
         RS_HIP(hipMemcpyAsync(pl->gb.p, pl->gb_snap.p, sizeof(double), hipMemcpyDeviceToDevice, s));
         RS_HIP(hipStreamSynchronize(s));
+        const int32_t cap = tile_cap_in_use(pl);  // (before the grid changes: the automatic cap depends on it)
         pl->tile_wg = std::max(1, pl->tile_grid / 2);
+        pl->tile_run_cap = std::max(2, cap / 2);
         tile_build(pl);
         pl->n_blocks = tile_partials(pl);
         ++pl->refits;
@@ -2391,20 +2400,30 @@ extern "C" int rs_svd_fit(rs_ctx* ctx, const rs_ratings* r, const rs_sgd_params*
                 if (!rs::plan_upload_fit(&pl, P, Q, bu, bi, gb)) rs::plan_upload(&pl, P, Q, bu, bi, gb);
             }
             mark("upload");
+            // the results' download is enqueued behind the epochs (and the guard's check), so one wait covers both
+            const bool staged = rs::fit_fits_staging(&pl);
+            int32_t flag = 0;
+            auto fetch = [&] {
+                rs::kernel_span_record(ctx);  // the kernel span ends before the copies
+                if (staged) rs::plan_fetch_enqueue(&pl);
+            };
             rs::kernel_span_begin(ctx);
-            rs::plan_epochs(&pl, p->n_epochs, lr, reg, ctx->stream, trace ? std::function<void()>() : std::function<void()>(keep_coo));
-            rs::kernel_span_end(ctx);
+            rs::plan_epochs(&pl, p->n_epochs, lr, reg, ctx->stream, trace ? std::function<void()>() : std::function<void()>(keep_coo),
+                            fetch);
+            rs::kernel_span_wait(ctx);
             ctx->fit_refits = pl.refits - refits0;
             mark("epochs");
             if (trace) {
                 keep_coo();
                 mark("cache-copy");
             }
-            bool fetched = false;
-            int32_t flag = 0;
-            fetched = rs::plan_fetch_fit(&pl, gb, &flag);
-            if (fetched) rs::plan_finish_fit(&pl, P, Q, bu, bi, flag);
-            else if (!rs::plan_download_fit(&pl, P, Q, bu, bi, gb)) rs::plan_download(&pl, P, Q, bu, bi, gb);
+            if (staged) {
+                RS_HIP(hipStreamSynchronize(ctx->stream));
+                rs::plan_fetch_result(gb, &flag);
+                rs::plan_finish_fit(&pl, P, Q, bu, bi, flag);
+            } else {
+                rs::plan_download(&pl, P, Q, bu, bi, gb);
+            }
             mark("download");
             return RS_OK;
         }

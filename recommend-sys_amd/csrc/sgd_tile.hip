@@ -842,13 +842,20 @@ void build_tile_host(const rs_svd_plan* pl, int32_t u_begin, int32_t u_end, int3
 // hottest item 3.4M of 126M ratings) the staleness model alone gives 2 and the hottest row's 1.7M
 // atomic rows bound the epoch at 143 ms; caps 4 / 6 / 8 / 10 / 12 give 92 / 80 / 76 / 74 / 75 ms at the
 // same held-out RMSE after five epochs (0.8815-0.8818; profiles/r03_experiments/cfg4_ring.log), and 7
-// is what this rule picks.  On ML-1M (dmax 3428) it is 1 and changes nothing.  The floor applies from
-// 2^25 ratings on: below that it buys little time and its staleness can diverge -- the 1.13M-rating,
-// k = 64 set of tests/test_csr_plan_gpu.py (hottest item 16271 ratings) trains at the model's cap 3
-// (held-out 1.005 -> 0.729 in 10 epochs) and goes NaN at the floor's 4 within 1-3 epochs
-// (scripts/experiments/exp_synth_cap.py, profiles/r03_experiments/synth_cap.log).
+// is what this rule picks.  On ML-1M (dmax 3428) it is 1 and changes nothing.
+// The floor applies where the serialised atomics of the hottest row would outlast the rest of the epoch
+// (round 4; it replaces round 3's 2^25-rating threshold): at the model's cap c the row takes d / c run-end
+// atomics of L line requests each, ~4.9 ns per line (the 1.7M k = 256 rows of 17 lines in 143 ms above),
+// while the epoch's other work is ~0.176 ns per rating per 7 lines (the ML-1M k = 100 epoch, 176 us per
+// 1M ratings); L cancels.  The floor is taken when those atomics would take twice the rest of the epoch,
+// d / (c nnz) > 2 x 0.0251 / 4.9 = 1.02 %: configs[4]'s shard, 3.4M / (2 x 126M) = 1.35 %, floor 7; the
+// 1.13M-rating k = 64 sets (hottest item 1.4-1.6 %, model cap 3): 0.48-0.54 %, no floor -- the floor's
+// caps 4-5 diverge there (round 3, profiles/r03_experiments/synth_cap.log; round 4, a first criterion at
+// 1x took the floor at 0.54 % and diverged on every grid) --; ML-1M: 0.02 %.  What the model does not
+// foresee, the divergence guard (plan_epochs, sgd.hip) catches: a call that leaves the fixed-point range is
+// redone on half the workgroups with half the run cap.
 constexpr double kStaleTarget = 100.0;
-constexpr int64_t kHotFloorMinNnz = int64_t{1} << 25;
+constexpr double kHotRowBoundShare = 2.0 * 0.0251 / 4.9;
 int32_t auto_run_cap(const rs_svd_plan* pl, int32_t grid, int32_t waves) {
     if (waves <= 1 || pl->nnz == 0) return 0;
     std::vector<int64_t> deg(std::max(1, pl->n_items), 0);
@@ -861,7 +868,9 @@ int32_t auto_run_cap(const rs_svd_plan* pl, int32_t grid, int32_t waves) {
 int32_t run_cap_rule(int64_t nnz, int64_t dmax, int32_t grid, int32_t waves) {
     if (waves <= 1 || nnz == 0) return 0;
     const double c = 2.0 * kStaleTarget * static_cast<double>(nnz) / (static_cast<double>(dmax) * grid * waves);
-    const int64_t c_hot = nnz >= kHotFloorMinNnz ? (dmax * 256 + nnz - 1) / nnz : 0;
+    const int64_t c_model = std::max<int64_t>(2, static_cast<int64_t>(c));
+    const bool row_bound = static_cast<double>(dmax) / (static_cast<double>(c_model) * static_cast<double>(nnz)) > kHotRowBoundShare;
+    const int64_t c_hot = row_bound ? (dmax * 256 + nnz - 1) / nnz : 0;
     return c >= 1e6 ? 0 : static_cast<int32_t>(std::max<int64_t>({2, static_cast<int64_t>(c), c_hot}));
 }
 
