@@ -658,7 +658,8 @@ __global__ __launch_bounds__(256) void svd_epoch_epilogue_kernel(
     int32_t* __restrict__ Q, const int4* __restrict__ meta, int32_t* __restrict__ qlast, int32_t n_live,
     float* __restrict__ P, float* __restrict__ dP, const int32_t* __restrict__ rows, int32_t n_split,
     int32_t ld, const double* __restrict__ partial, int64_t n_partial, double* __restrict__ gb,
-    double inv_nnz, int32_t* __restrict__ done) {
+    double inv_nnz, int32_t* __restrict__ done, const float* __restrict__ loss_part, double* __restrict__ loss_state,
+    int32_t* __restrict__ flag, double inv_lr2) {
     const int b = static_cast<int>(blockIdx.x);
     const int tid = static_cast<int>(threadIdx.x);
     if (b < n_live) {
@@ -682,18 +683,32 @@ __global__ __launch_bounds__(256) void svd_epoch_epilogue_kernel(
         }
         return;
     }
-    __shared__ double sh[256];
-    double t = 0.0;
-    for (int64_t x = tid; x < n_partial; x += 256) t += partial[x];
+    __shared__ double sh[256], sl[256];
+    double t = 0.0, l = 0.0;
+    for (int64_t x = tid; x < n_partial; x += 256) {
+        t += partial[x];
+        if (loss_part) l += static_cast<double>(loss_part[x]);
+    }
     sh[tid] = t;
+    sl[tid] = l;
     __syncthreads();
     for (int w = 128; w > 0; w >>= 1) {
-        if (tid < w) sh[tid] += sh[tid + w];
+        if (tid < w) {
+            sh[tid] += sh[tid + w];
+            sl[tid] += sl[tid + w];
+        }
         __syncthreads();
     }
     if (tid == 0) {
         gb[0] += sh[0] * inv_nnz;
         if (done) *done = 0;
+        if (loss_part && loss_state) {
+            // the divergence guard's second signal: this epoch's training MSE (at the ratings' pre-update
+            // residuals) more than 1.2x the previous epoch's -- SGD at a stable rate does not raise it
+            const double mse = sl[0] * inv_nnz * inv_lr2, prev = loss_state[0];
+            if (!(mse < 1e30) || (prev > 0.0 && mse > 1.2 * prev)) flag[0] = 1;
+            loss_state[0] = mse;
+        }
     }
 }
 
@@ -1014,6 +1029,12 @@ int32_t* numflag(rs_svd_plan* pl) {
 void plan_sync_last(rs_svd_plan* pl) {
     if (pl->last_stream) RS_HIP(hipStreamSynchronize(pl->last_stream));
 }
+
+// new factors: the guard's loss history starts over
+static void reset_loss(rs_svd_plan* pl, hipStream_t s) {
+    if (pl->loss_state.p) RS_HIP(hipMemsetAsync(pl->loss_state.p, 0, sizeof(double), s));
+}
+
 
 // Item row copies from the host CSR: an item with deg > cap gets R = ceil(deg / cap) rows (its own
 // plus R - 1 appended after n_items); its ratings are dealt in user-CSR order, the s-th rating of the
@@ -1404,6 +1425,7 @@ static void plan_dma_fit(rs_svd_plan* pl, const double* gb) {
     double* sc = fit_scalars().p;
     sc[0] = *gb;
     pl->gb.upload(sc, 1, s);
+    reset_loss(pl, s);
 }
 
 static bool plan_upload_fit(rs_svd_plan* pl, const double* P, const double* Q, const double* bu, const double* bi,
@@ -1533,6 +1555,7 @@ static void pack_with_bias(const double* F, const double* bias, int64_t rows, in
 static void plan_upload(rs_svd_plan* pl, const double* P, const double* Q, const double* bu,
                         const double* bi, const double* gb) {
     plan_sync_last(pl);
+    reset_loss(pl, pl->ctx->stream);
     hipStream_t s = pl->ctx->stream;
     std::vector<float> old, tmp;
     auto put = [&](DevBuf<float>& d, int64_t rows, const double* F, const double* bias) {
@@ -1626,6 +1649,8 @@ static void plan_epochs_once(rs_svd_plan* pl, int32_t epochs, float lr, float re
                                pl->qlast.p, pl->ld, 0);
             RS_HIP(hipMemsetAsync(pl->done.p, 0, sizeof(int32_t), s));
         }
+        // the guard's loss check: tile epochs of a guarded plan (loss partials written by the kernel)
+        const bool loss_on = tile && pl->guard && lr > 0.f && pl->loss_state.p && pl->loss_part.n >= pl->partial.n;
         struct HoistScope {  // launch_fast sees the hoisted state only inside this loop, even on a throw
             rs_svd_plan* p;
             ~HoistScope() { p->hoisted = false; }
@@ -1641,7 +1666,9 @@ static void plan_epochs_once(rs_svd_plan* pl, int32_t epochs, float lr, float re
                                reinterpret_cast<int32_t*>(pl->qlast.p), n_live, pl->P.p, pl->dPs.p,
                                tile ? pl->t_split_rows.p : pl->split_rows.p, n_split, pl->ld, pl->partial.p,
                                static_cast<int64_t>(pl->n_blocks), pl->gb.p, inv_nnz,
-                               n_live > 0 ? pl->done.p : nullptr);
+                               n_live > 0 ? pl->done.p : nullptr, loss_on ? pl->loss_part.p : nullptr,
+                               loss_on ? pl->loss_state.p : nullptr, loss_on ? numflag(pl) : nullptr,
+                               1.0 / (static_cast<double>(lr) * static_cast<double>(lr)));
             RS_HIP(hipGetLastError());
         }
         pl->hoisted = false;
@@ -1689,10 +1716,16 @@ static void plan_epochs(rs_svd_plan* pl, int32_t epochs, float lr, float reg, hi
     }
     if (pl->P_snap.n != pl->P.n) pl->P_snap.alloc(pl->P.n);
     if (pl->Q_snap.n != pl->Q.n) pl->Q_snap.alloc(pl->Q.n);
-    if (!pl->gb_snap.p) pl->gb_snap.alloc(1);
+    if (!pl->gb_snap.p) pl->gb_snap.alloc(2);
+    if (pl->loss_part.n < pl->partial.n) pl->loss_part.alloc(pl->partial.n);
+    if (!pl->loss_state.p) {
+        pl->loss_state.alloc(1);
+        RS_HIP(hipMemsetAsync(pl->loss_state.p, 0, sizeof(double), s));
+    }
     RS_HIP(hipMemcpyAsync(pl->P_snap.p, pl->P.p, pl->P.n * sizeof(float), hipMemcpyDeviceToDevice, s));
     RS_HIP(hipMemcpyAsync(pl->Q_snap.p, pl->Q.p, pl->Q.n * sizeof(float), hipMemcpyDeviceToDevice, s));
     RS_HIP(hipMemcpyAsync(pl->gb_snap.p, pl->gb.p, sizeof(double), hipMemcpyDeviceToDevice, s));
+    RS_HIP(hipMemcpyAsync(pl->gb_snap.p + 1, pl->loss_state.p, sizeof(double), hipMemcpyDeviceToDevice, s));
     struct Check {  // pinned readback slot, per thread
         int64_t* p = nullptr;
         Check() { RS_HIP(hipHostMalloc(reinterpret_cast<void**>(&p), 16, hipHostMallocPortable)); }
@@ -1718,6 +1751,7 @@ static void plan_epochs(rs_svd_plan* pl, int32_t epochs, float lr, float reg, hi
         RS_HIP(hipMemcpyAsync(pl->P.p, pl->P_snap.p, pl->P.n * sizeof(float), hipMemcpyDeviceToDevice, s));
         RS_HIP(hipMemcpyAsync(pl->Q.p, pl->Q_snap.p, pl->Q.n * sizeof(float), hipMemcpyDeviceToDevice, s));
         RS_HIP(hipMemcpyAsync(pl->gb.p, pl->gb_snap.p, sizeof(double), hipMemcpyDeviceToDevice, s));
+        RS_HIP(hipMemcpyAsync(pl->loss_state.p, pl->gb_snap.p + 1, sizeof(double), hipMemcpyDeviceToDevice, s));
         RS_HIP(hipStreamSynchronize(s));
         const int32_t cap = tile_cap_in_use(pl);  // (before the grid changes: the automatic cap depends on it)
         pl->tile_wg = std::max(1, pl->tile_grid / 2);
@@ -1807,6 +1841,7 @@ extern "C" int rs_svd_plan_init_normal(rs_svd_plan* pl, double mean, double std_
     if (!pl) return rs::set_error(nullptr, RS_ERR_INVALID, "plan is NULL");
     return rs_guard(pl->ctx, [&]() -> int {
         rs::plan_init_normal(pl, mean, std_dev, seed);
+        rs::reset_loss(pl, pl->ctx->stream);
         return RS_OK;
     });
 }

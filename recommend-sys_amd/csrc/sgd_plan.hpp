@@ -134,7 +134,9 @@ struct rs_svd_plan {
     int32_t guard = 1;
     int32_t refits = 0;                        // redone calls so far (rs_svd_plan_refits)
     rs::DevBuf<float> P_snap, Q_snap;          // the call-start state (allocated on first use)
-    rs::DevBuf<double> gb_snap;
+    rs::DevBuf<double> gb_snap;                // {GlobalBias, loss state} at the call start
+    rs::DevBuf<float> loss_part;               // per (workgroup, wave): sum of (lr diff)^2 of the last epoch
+    rs::DevBuf<double> loss_state;             // last epoch's training MSE (0: none since the factors were set)
     ~rs_svd_plan() {
         if (ev0) (void)hipEventDestroy(ev0);
         if (ev1) (void)hipEventDestroy(ev1);

@@ -96,7 +96,7 @@ __global__ __launch_bounds__(NW * 64) void svd_epoch_tile_kernel(
     const int4* __restrict__ tiles, int32_t n_tiles, const int2* __restrict__ tile_users,
     const int32_t* __restrict__ streams, const int2* __restrict__ runs, const int2* __restrict__ recs,
     float* __restrict__ P, int32_t* Q, int32_t q_bytes, const double* __restrict__ gb_in,
-    double* __restrict__ gb_partial, float lr, float reg, float* __restrict__ dP,
+    double* __restrict__ gb_partial, float* __restrict__ loss_partial, float lr, float reg, float* __restrict__ dP,
     const float* __restrict__ uw, float* __restrict__ dPs, int32_t kf, int32_t ldm, int32_t ldd,
     int64_t* __restrict__ dbg) {
 #pragma clang fp contract(fast)
@@ -127,6 +127,7 @@ __global__ __launch_bounds__(NW * 64) void svd_epoch_tile_kernel(
     }
     auto qaddr = [&](int32_t row, int x) { return (row >= 0 && qoff[x] >= 0) ? row + qoff[x] : kOutOfRange; };
     double contrib = 0.0;
+    float se = 0.f;  // sum of c^2 = (lr diff)^2 over this wave's ratings: the epoch's training loss (the guard)
     const int64_t t_begin = SPAN ? clk() : 0;
     const int64_t rt_begin = SPAN ? static_cast<int64_t>(__builtin_amdgcn_s_memrealtime()) : 0;  // 100 MHz, chip-wide
 
@@ -255,6 +256,7 @@ __global__ __launch_bounds__(NW * 64) void svd_epoch_tile_kernel(
                 // p <- a p - c q ; q <- a q - c p_new (Q1) ; gb <- gb - c
                 const float c = __builtin_fmaf(sd, klr, lr * ((gbf - cs) - rt));
                 cs += c;
+                se = __builtin_fmaf(c, c, se);
 
                 float pn[E];
 #pragma unroll
@@ -392,6 +394,7 @@ __global__ __launch_bounds__(NW * 64) void svd_epoch_tile_kernel(
         if constexpr (TIMED) tm_tail += clk() - tm_c;
     }
     if (lane == 0) gb_partial[static_cast<int64_t>(blockIdx.x) * NW + w] = contrib;
+    if (lane == 0 && loss_partial) loss_partial[static_cast<int64_t>(blockIdx.x) * NW + w] = se;
     if constexpr (SPAN) {
         const int64_t t_end = clk();
         if (lane == 0) {
@@ -1149,7 +1152,7 @@ static void tile_launch_t(rs_svd_plan* pl, float lr, float reg, hipStream_t s, f
     hipLaunchKernelGGL(kern, dim3(tr.grid), dim3(NW * 64), pl->tile_lds, s, pl->t_tiles.p + tr.t0, tr.t1 - tr.t0,
                        pl->t_users.p, pl->t_streams.p + static_cast<int64_t>(tr.t0) * (NW + 1), pl->t_runs.p,
                        pl->t_recs.p, pl->P.p, reinterpret_cast<int32_t*>(pl->Q.p), q_bytes, pl->gb.p, pl->partial.p,
-                       lr, reg, dP, dP ? pl->uw.p : nullptr, pl->dPs.p, pl->k, pl->ld, tr.ldd, pl->trace.p);
+                       pl->loss_part.n >= pl->partial.n ? pl->loss_part.p : nullptr, lr, reg, dP, dP ? pl->uw.p : nullptr, pl->dPs.p, pl->k, pl->ld, tr.ldd, pl->trace.p);
 }
 
 // q_i rows in flight per wave (runs ahead): the ring's loads and the runs' atomics share the wave's
