@@ -286,9 +286,10 @@ int rs_svd_plan_set_tile_claim(rs_svd_plan* plan, int32_t runs_per_claim);
  * Both snake builds give byte-identical schedules (rs_svd_plan_schedule_digest); where the rule does not
  * apply (a user above the LDS bound, a tile past the LDS) the device build falls back to RS_TILE_RULE_LPT
  * and RS_TILE_RULE_SNAKE fails with RS_ERR_UNSUPPORTED.  Rebuilds the schedule. */
-/* Divergence guard of the tile schedule (default on): rs_svd_plan_epochs checks a call's epochs once at the
- * end (fixed-point range of P and Q, a finite GlobalBias; one small readback, so the call waits for its
- * epochs) and redoes a failed call from its start state -- P, Q and GlobalBias copied on the device first --
+/* Divergence guard of the tile schedule (default on): every epoch measures its training MSE and flags one
+ * that rises more than 1.2x over the previous epoch's (the history starts over on upload / init);
+ * rs_svd_plan_epochs checks a call's epochs once at the end (that flag, fixed-point range of P and Q, a
+ * finite GlobalBias; one small readback, so the call waits for its epochs) and redoes a failed call from its start state -- P, Q and GlobalBias copied on the device first --
  * on half the workgroups and half the run cap, up to three times; the plan keeps them.  A call still failing leaves
  * the flag for the download (RS_ERR_NUMERIC).  rs_svd_fit always runs guarded.  off: no snapshot, no wait. */
 int rs_svd_plan_set_guard(rs_svd_plan* plan, int32_t on);
@@ -491,8 +492,9 @@ int rs_item_shards(int64_t nnz, const int32_t* items, int32_t n_items, int32_t n
 /* core/svd.go:63-132 (FAST tile schedule) on n_devices GPUs of this process: with n_items >= n_users the
  * items are sharded by rs_item_shards and P rank-blocks rotate (RS_EXCHANGE_ROTATE); with fewer items than
  * users the users are cut into ranges of near-equal ratings and Q item blocks rotate
- * (RS_EXCHANGE_ROTATE_Q).  As rs_svd_fit otherwise (GlobalBias warm start, host buffers in / out;
- * RS_ERR_NUMERIC after every shard's values are written). */
+ * (RS_EXCHANGE_ROTATE_Q).  As rs_svd_fit otherwise (GlobalBias warm start, host buffers in / out; a fit
+ * whose shards leave the fixed-point range is rebuilt and redone from the inputs on half the workgroups and
+ * run cap 2, up to three times; RS_ERR_NUMERIC after every shard's values are written). */
 int rs_svd_fit_multi(const int32_t* devices, int32_t n_devices, const rs_ratings* r, const rs_sgd_params* p,
                      int32_t n_blocks, double* P, double* Q, double* bu, double* bi, double* gb);
 /* ---- user-sharded multi-GPU (the dual partition, SURVEY §8e "measured alternative") ---------- *

@@ -1164,10 +1164,22 @@ extern "C" int rs_svd_fit_multi(const int32_t* devices, int32_t n_devices, const
         for (rs_svd_plan* pl : plans) rs_svd_plan_destroy(pl);
         for (rs_ctx* c : ctxs) rs_close(c);
     };
+    // Divergence guard (as rs_svd_fit's): a fit whose shards leave the fixed-point range
+    // or go non-finite is rebuilt and redone from the caller's inputs -- untouched until the final download --
+    // on half the workgroups and the smallest run cap (2), up to three times.
+    int32_t refits = 0;
     int st = rs_guard(nullptr, [&]() -> int {
-        *gb = p->n_epochs > 0 ? rs::gb_warm_start(r, bu, bi) : *gb;  // as rs_svd_fit (FAST)
+      const double gb_in = *gb;
+      for (int attempt = 0;; ++attempt) {
+        if (g) rs_svd_group_destroy(g);
+        g = nullptr;
+        for (rs_svd_plan*& pl : plans) {
+            rs_svd_plan_destroy(pl);
+            pl = nullptr;
+        }
+        *gb = p->n_epochs > 0 ? rs::gb_warm_start(r, bu, bi) : gb_in;  // as rs_svd_fit (FAST)
         for (int32_t s = 0; s < n; ++s) {
-            int e = rs_open(devices[s], &ctxs[s]);
+            int e = ctxs[s] ? RS_OK : rs_open(devices[s], &ctxs[s]);
             if (e != RS_OK) return e;
             const int32_t lo = bounds[s], hi = bounds[s + 1];
             std::vector<int32_t> su, si;
@@ -1184,6 +1196,10 @@ extern "C" int rs_svd_fit_multi(const int32_t* devices, int32_t n_devices, const
                           sr.data()};
             e = rs_svd_plan_create(ctxs[s], &sh, k, &plans[s]);
             if (e != RS_OK) return e;
+            if (attempt > 0) {
+                e = rs_svd_plan_set_tiles(plans[s], std::max(1, rs::device_cus(ctxs[s]) >> attempt), 16, 0, 2, 0);
+                if (e != RS_OK) return e;
+            }
             if (rq) {
                 e = rs_svd_plan_set_exchange(plans[s], RS_EXCHANGE_ROTATE_Q);
                 if (e != RS_OK) return e;
@@ -1197,6 +1213,20 @@ extern "C" int rs_svd_fit_multi(const int32_t* devices, int32_t n_devices, const
         if (e != RS_OK) return e;
         e = rs_svd_group_epochs(g, p->n_epochs, static_cast<float>(p->lr), static_cast<float>(p->reg));
         if (e != RS_OK) return e;
+        bool diverged = false;  // any shard's range flag or a non-finite GlobalBias (before anything is returned)
+        for (int32_t s = 0; s < n; ++s) {
+            rs_svd_plan* pl = plans[s];
+            double gv = 0.0;
+            int32_t f = 0;
+            pl->gb.download(&gv, 1, pl->ctx->stream);
+            if (pl->numflag.p) pl->numflag.download(&f, 1, pl->ctx->stream);
+            RS_HIP(hipStreamSynchronize(pl->ctx->stream));
+            diverged = diverged || f != 0 || !std::isfinite(gv);
+        }
+        if (diverged && attempt < 3 && p->n_epochs > 0) {
+            ++refits;
+            continue;
+        }
         int numeric = RS_OK;  // every shard's values are returned before RS_ERR_NUMERIC is
         for (int32_t s = 0; s < n; ++s) {  // P, b_u, GlobalBias (ROTATE_Q: everything) identical on every shard
             if (rq && s > 0) break;
@@ -1207,7 +1237,9 @@ extern "C" int rs_svd_fit_multi(const int32_t* devices, int32_t n_devices, const
             else if (e != RS_OK && e != RS_ERR_NUMERIC) return e;
         }
         return numeric;
+      }
     });
+    (void)refits;
     std::string err = st != RS_OK ? std::string(rs_last_error(nullptr)) : std::string();
     for (int32_t s = 0; s < n && st != RS_OK && err.empty(); ++s)
         if (ctxs[s]) err = rs_last_error(ctxs[s]);

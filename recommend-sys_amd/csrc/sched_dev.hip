@@ -324,7 +324,7 @@ bool tile_build_device(rs_svd_plan* pl) {
     const double bytes = static_cast<double>(n_active) * (static_cast<double>(ld) * 4) + 16.0 * static_cast<double>(n);
     const int64_t n_lds = static_cast<int64_t>(std::ceil(bytes / (0.85 * static_cast<double>(kTileLdsBudget))));
     const int32_t T = static_cast<int32_t>(std::min<int64_t>(std::max<int64_t>({1, n_target, n_lds}), n_active));
-    const int32_t cap = (pl->tile_run_cap > 0 ? pl->tile_run_cap : run_cap_rule(n, dmax_i, grid0, nw));
+    const int32_t cap = (pl->tile_run_cap > 0 ? pl->tile_run_cap : run_cap_rule(n, dmax_i, grid0, nw, pl->k));
     const int32_t cap_eff = (cap > 0 && nw > 1) ? cap : 0;
     const int ulb = bit_len(static_cast<uint64_t>((n_active + T - 1) / T - 1));
     const int tb = bit_len(static_cast<uint64_t>(T));  // tile ids 0..T (T: inactive users' sort key)

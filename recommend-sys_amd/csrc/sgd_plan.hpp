@@ -249,7 +249,7 @@ __host__ __device__ inline uint32_t run_key(int32_t item, int32_t tile) {
 }
 int32_t device_cus(const rs_ctx* ctx);
 // the run cap the library picks (see auto_run_cap, sgd_tile.hip) from the item degree maximum
-int32_t run_cap_rule(int64_t nnz, int64_t dmax_item, int32_t grid, int32_t waves);
+int32_t run_cap_rule(int64_t nnz, int64_t dmax_item, int32_t grid, int32_t waves, int32_t k);
 void tile_build(rs_svd_plan* pl);  // (re)builds the tile schedule (host CSR, or the device for RS_TILE_RULE_SNAKE_DEVICE)
 std::vector<int32_t> user_block_bounds(const int64_t* cum, int32_t n_users, int32_t nb);
 void tile_launch(rs_svd_plan* pl, float lr, float reg, hipStream_t s, float* dP);  // one epoch (Q int32)

@@ -850,29 +850,34 @@ void build_tile_host(const rs_svd_plan* pl, int32_t u_begin, int32_t u_end, int3
 // (round 4; it replaces round 3's 2^25-rating threshold): at the model's cap c the row takes d / c run-end
 // atomics of L line requests each, ~4.9 ns per line (the 1.7M k = 256 rows of 17 lines in 143 ms above),
 // while the epoch's other work is ~0.176 ns per rating per 7 lines (the ML-1M k = 100 epoch, 176 us per
-// 1M ratings); L cancels.  The floor is taken when those atomics would take twice the rest of the epoch,
-// d / (c nnz) > 2 x 0.0251 / 4.9 = 1.02 %: configs[4]'s shard, 3.4M / (2 x 126M) = 1.35 %, floor 7; the
-// 1.13M-rating k = 64 sets (hottest item 1.4-1.6 %, model cap 3): 0.48-0.54 %, no floor -- the floor's
-// caps 4-5 diverge there (round 3, profiles/r03_experiments/synth_cap.log; round 4, a first criterion at
-// 1x took the floor at 0.54 % and diverged on every grid) --; ML-1M: 0.02 %.  What the model does not
-// foresee, the divergence guard (plan_epochs, sgd.hip) catches: a call that leaves the fixed-point range is
-// redone on half the workgroups with half the run cap.
+// 1M ratings) plus ~20 us that no launch goes below.  The floor is taken when those atomics would take twice
+// the rest of the epoch: configs[4]'s shard (1.7M x 17 lines = 142 ms against 2 x 54 ms): floor 7; the
+// 1.13M-rating k = 64 sets (hottest item 1.4-1.6 %, model cap 3: 0.13 ms against 2 x 0.16 ms): no floor --
+// caps 4-5 diverge there (round 3, profiles/r03_experiments/synth_cap.log; round 4, a first form of this
+// criterion without the factor 2 took the floor on such a set and diverged on every grid) --; an ML-1M
+// stratum of an 8-shard ROTATE_Q fit (14k ratings, the hottest item 428 of them: 7 us against 2 x 22 us):
+// no floor -- cap 8 diverged there --; ML-1M: no floor.  What the model does not foresee, the divergence
+// guard (plan_epochs, sgd.hip) catches: an epoch whose training loss rises, or a call that leaves the
+// fixed-point range, is redone on half the workgroups with half the run cap.
 constexpr double kStaleTarget = 100.0;
-constexpr double kHotRowBoundShare = 2.0 * 0.0251 / 4.9;
+constexpr double kAtomicLineNs = 4.9, kRatingLineNs = 0.176 / 7.0, kLaunchFloorNs = 20000.0;
 int32_t auto_run_cap(const rs_svd_plan* pl, int32_t grid, int32_t waves) {
     if (waves <= 1 || pl->nnz == 0) return 0;
     std::vector<int64_t> deg(std::max(1, pl->n_items), 0);
     for (int32_t c : pl->h_cols) deg[c]++;
-    return run_cap_rule(pl->nnz, *std::max_element(deg.begin(), deg.end()), grid, waves);
+    return run_cap_rule(pl->nnz, *std::max_element(deg.begin(), deg.end()), grid, waves, pl->k);
 }
 
 }  // namespace
 
-int32_t run_cap_rule(int64_t nnz, int64_t dmax, int32_t grid, int32_t waves) {
+int32_t run_cap_rule(int64_t nnz, int64_t dmax, int32_t grid, int32_t waves, int32_t k) {
     if (waves <= 1 || nnz == 0) return 0;
     const double c = 2.0 * kStaleTarget * static_cast<double>(nnz) / (static_cast<double>(dmax) * grid * waves);
     const int64_t c_model = std::max<int64_t>(2, static_cast<int64_t>(c));
-    const bool row_bound = static_cast<double>(dmax) / (static_cast<double>(c_model) * static_cast<double>(nnz)) > kHotRowBoundShare;
+    const double lines = std::ceil((k + 1) / 16.0);  // 64-B line requests of a row (factors + bias)
+    const double t_hot = static_cast<double>(dmax) / static_cast<double>(c_model) * lines * kAtomicLineNs;
+    const double t_rest = static_cast<double>(nnz) * lines * kRatingLineNs + kLaunchFloorNs;
+    const bool row_bound = t_hot > 2.0 * t_rest;
     const int64_t c_hot = row_bound ? (dmax * 256 + nnz - 1) / nnz : 0;
     return c >= 1e6 ? 0 : static_cast<int32_t>(std::max<int64_t>({2, static_cast<int64_t>(c), c_hot}));
 }

@@ -33,7 +33,7 @@ if [ "${SKIP_PROF:-0}" != "1" ]; then
   echo "== rocprofv3 kernel trace" >> "$OUT/session.log"
   cd /tmp
   timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof" -o run -- \
-      python3 "$ROOT/bench.py" --steps $STEPS --warmup 3 --no-cpu-baseline > "$OUT/bench_prof.log" 2>&1
+      python3 "$ROOT/bench.py" --steps $STEPS --warmup 3 --no-cpu-baseline --no-strong > "$OUT/bench_prof.log" 2>&1
   c=$?; echo "rocprof exit $c" >> "$OUT/session.log"; [ $c -eq 0 ] || exit 14
 fi
 echo "== done" >> "$OUT/session.log"
