@@ -278,14 +278,15 @@ int rs_svd_plan_set_tile_claim(rs_svd_plan* plan, int32_t runs_per_claim);
 /* How the users are cut into tiles (round 4):
  *   RS_TILE_RULE_LPT          (plans' default) host build: users dealt largest first to the least-loaded
  *                             tile, then moved between tiles by a per-run cost model;
- *   RS_TILE_RULE_SNAKE        host build: users by degree (descending, ties by id) dealt boustrophedon over
- *                             min(tiles, active users) tiles, no refinement;
- *   RS_TILE_RULE_SNAKE_DEVICE the same rule built on the device (radix sorts of the users by degree and of the
- *                             ratings by (tile, run key, user)) -- rs_svd_fit's default for sets of at most
- *                             2^24 ratings: the one-shot Fit's schedule then costs no host time.
- * Both snake builds give byte-identical schedules (rs_svd_plan_schedule_digest); where the rule does not
+ *   RS_TILE_RULE_FILL         host build: users by degree (descending, ties by id) over T = min(tiles,
+ *                             active users) tiles; the first 4T dealt boustrophedon, the rest laid by prefix
+ *                             sums on the line of the tiles' deficits against the mean load (midpoint rule);
+ *                             no refinement;
+ *   RS_TILE_RULE_FILL_DEVICE  the same rule built on the device (radix sorts and scans) -- rs_svd_fit's default
+ *                             for sets of at most 2^24 ratings: the one-shot Fit's schedule costs no host time.
+ * Both fill builds give byte-identical schedules (rs_svd_plan_schedule_digest); where the rule does not
  * apply (a user above the LDS bound, a tile past the LDS) the device build falls back to RS_TILE_RULE_LPT
- * and RS_TILE_RULE_SNAKE fails with RS_ERR_UNSUPPORTED.  Rebuilds the schedule. */
+ * and RS_TILE_RULE_FILL fails with RS_ERR_UNSUPPORTED.  Rebuilds the schedule. */
 /* Divergence guard of the tile schedule (default on): every epoch measures its training MSE and flags one
  * that rises more than 1.2x over the previous epoch's (the history starts over on upload / init);
  * rs_svd_plan_epochs checks a call's epochs once at the end (that flag, fixed-point range of P and Q, a
@@ -296,8 +297,8 @@ int rs_svd_plan_set_guard(rs_svd_plan* plan, int32_t on);
 /* Calls the guard has redone on this plan so far. */
 int rs_svd_plan_refits(const rs_svd_plan* plan, int32_t* n);
 #define RS_TILE_RULE_LPT 0
-#define RS_TILE_RULE_SNAKE 1
-#define RS_TILE_RULE_SNAKE_DEVICE 2
+#define RS_TILE_RULE_FILL 1
+#define RS_TILE_RULE_FILL_DEVICE 2
 int rs_svd_plan_set_tile_rule(rs_svd_plan* plan, int32_t rule);
 /* The rule the plan's current schedule was built with (a device build that fell back reports LPT). */
 int rs_svd_plan_tile_rule(const rs_svd_plan* plan, int32_t* rule);
@@ -305,8 +306,8 @@ int rs_svd_plan_tile_rule(const rs_svd_plan* plan, int32_t* rule);
  * tiles, tile users, streams, run headers, records). */
 int rs_svd_plan_schedule_digest(rs_svd_plan* plan, uint64_t* digest);
 /* The same digest, and the tile rule, of the plan the last FAST rs_svd_fit on ctx built and cached (a
- * one-shot Fit builds with RS_TILE_RULE_SNAKE_DEVICE from the caller's COO; tests compare it with a
- * plan's host RS_TILE_RULE_SNAKE build).  RS_ERR_INVALID when no such plan is cached. */
+ * one-shot Fit builds with RS_TILE_RULE_FILL_DEVICE from the caller's COO; tests compare it with a
+ * plan's host RS_TILE_RULE_FILL build).  RS_ERR_INVALID when no such plan is cached. */
 int rs_fit_schedule_digest(rs_ctx* ctx, uint64_t* digest, int32_t* rule);
 /* Visit order of the tile schedule: pos[n] = user-CSR position (rowptr order, data order inside a row)
  * of the n-th rating (nnz entries) as the kernel's streams walk it -- tile by tile, a tile's waves in

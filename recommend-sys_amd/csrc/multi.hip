@@ -1141,8 +1141,12 @@ extern "C" int rs_svd_fit_multi(const int32_t* devices, int32_t n_devices, const
     if (r->nnz < 0 || r->n_users < 0 || r->n_items < 0 || (r->nnz > 0 && (!r->users || !r->items || !r->ratings)))
         return rs::set_error(nullptr, RS_ERR_INVALID, "bad ratings");
     const int32_t n = n_devices, k = p->n_factors;
-    // the smaller factor matrix travels: item shards + P rotation, or user ranges + Q rotation
-    const bool rq = r->n_items < r->n_users;
+    // the smaller factor matrix travels -- item shards + P rotation, or user ranges + Q rotation -- where the
+    // bytes matter: a P rank-block of 16 MiB or more (configs[4] at 8 GPUs: 1.6 GB against 160 MB of Q).  Below
+    // that the item shards of north_star stay (ML-1M at 8 shards: 386 KB per rank-block; its Q rotation's
+    // 7k-rating strata hold 5 % of one item each and trained less reliably, DESIGN.md Multi-GPU round 4)
+    const size_t p_block = static_cast<size_t>(r->n_users) / static_cast<size_t>(n) * static_cast<size_t>(rs::fast_ld(p->n_factors)) * 4;
+    const bool rq = r->n_items < r->n_users && p_block >= (size_t{16} << 20);
     std::vector<int32_t> bounds(static_cast<size_t>(n) + 1);
     if (rq) {
         std::vector<int64_t> cum(static_cast<size_t>(r->n_users) + 1, 0);

@@ -1,12 +1,14 @@
-// sched_dev.hip -- the tile schedule of sgd_tile.hip built on the device (RS_TILE_RULE_SNAKE_DEVICE), so that
+// sched_dev.hip -- the tile schedule of sgd_tile.hip built on the device (RS_TILE_RULE_FILL_DEVICE), so that
 // a one-shot rs_svd_fit (the Go Fit, reference core/svd.go:63-132) spends no host time on it.
 //
-// The rule is the host build's RS_TILE_RULE_SNAKE (build_tile_host), restated with radix sorts:
+// The rule is the host build's RS_TILE_RULE_FILL (build_tile_host), restated with radix sorts:
 //   1. degrees: histogram of the COO's users and items; one readback {active users, max user degree,
 //      max item degree} fixes the tile count, the run cap and the key widths on the host;
-//   2. tiles: the users sorted by degree (descending; a stable sort keeps ties in id order) are dealt
-//      boustrophedon -- position p, round r = p / T, tile r even ? p % T : T - 1 - p % T --; a second
-//      stable sort of the users by tile gives every tile its entries in user order;
+//   2. tiles: the users sorted by degree (descending; a stable sort keeps ties in id order); the first
+//      kFillSnakeRounds * T are dealt boustrophedon -- position p, round r = p / T, tile r even ? p % T :
+//      T - 1 - p % T --; the tiles' deficits against the mean load, sorted (descending, ties by tile), are laid
+//      end to end and the remaining users, heaviest first, go to the tile whose stretch holds the midpoint of
+//      their prefix sums; a second stable sort of the users by tile gives every tile its entries in user order;
 //   3. runs: the ratings sorted by (tile, run_key(item, tile), tile-local user) -- one stable LSD sort, so a
 //      run's ratings come in user order and a user's repeated item in COO order, as the host's CSR scan
 //      gives them -- are cut where (tile, key) changes; a run longer than the cap is cut into
@@ -77,17 +79,62 @@ __global__ __launch_bounds__(kB) void degree_keys_kernel(const int32_t* __restri
     iota[u] = u;
 }
 
-// boustrophedon deal of the degree order over T tiles (inactive users: tile T, sorted past every tile)
-__global__ __launch_bounds__(kB) void snake_kernel(const int32_t* __restrict__ by_deg, int32_t nu, int32_t n_active,
-                                                   int32_t T, uint32_t* __restrict__ tile_of) {
+// boustrophedon deal of the first ns users of the degree order over T tiles, with the tiles' loads; the rest
+// of the active users are placed by fill_kernel (inactive users: tile T, sorted past every tile)
+// (weights: the LDS bytes w0 + w1 d of a user, w0 = 4 ld, w1 = 16)
+__global__ __launch_bounds__(kB) void snake_kernel(const int32_t* __restrict__ by_deg, const int32_t* __restrict__ deg_u,
+                                                   int32_t nu, int32_t n_active, int32_t ns, int32_t T, int32_t w0,
+                                                   int32_t w1, uint32_t* __restrict__ tile_of,
+                                                   unsigned long long* __restrict__ load, int64_t* __restrict__ rem_w) {
     const int32_t p = blockIdx.x * kB + threadIdx.x;
     if (p >= nu) return;
-    int32_t t = T;
-    if (p < n_active) {
+    const int32_t u = by_deg[p];
+    const int64_t wu = w0 + static_cast<int64_t>(w1) * deg_u[u];
+    if (p < ns) {
         const int32_t r = p / T, i = p - r * T;
-        t = (r & 1) ? T - 1 - i : i;
+        const int32_t t = (r & 1) ? T - 1 - i : i;
+        tile_of[u] = static_cast<uint32_t>(t);
+        atomicAdd(load + t, static_cast<unsigned long long>(wu));
+    } else if (p < n_active) {
+        rem_w[p - ns] = wu;
+    } else {
+        tile_of[u] = static_cast<uint32_t>(T);
     }
-    tile_of[by_deg[p]] = static_cast<uint32_t>(t);
+}
+
+// deficit keys of the line: ascending key = descending deficit (a stable sort keeps ties in tile order)
+__global__ __launch_bounds__(kB) void deficit_kernel(const unsigned long long* __restrict__ load, int32_t T, int64_t mean,
+                                                     uint64_t* __restrict__ key, int32_t* __restrict__ iota) {
+    const int32_t t = blockIdx.x * kB + threadIdx.x;
+    if (t >= T) return;
+    const int64_t d = max<int64_t>(0, mean - static_cast<int64_t>(load[t]));
+    key[t] = static_cast<uint64_t>(INT64_MAX - d);
+    iota[t] = t;
+}
+
+__global__ __launch_bounds__(kB) void line_kernel(const unsigned long long* __restrict__ load, const int32_t* __restrict__ lt,
+                                                  int32_t T, int64_t mean, int64_t* __restrict__ dl) {
+    const int32_t j = blockIdx.x * kB + threadIdx.x;
+    if (j < T) dl[j] = max<int64_t>(0, mean - static_cast<int64_t>(load[lt[j]]));
+    if (j == T) dl[T] = 0;
+}
+
+// the remaining users: the tile whose stretch of the line (exclusive prefix E, T + 1 entries) holds the
+// midpoint of their prefix sum R: first j with 2 E[j + 1] > 2 R + d
+__global__ __launch_bounds__(kB) void fill_kernel(const int32_t* __restrict__ by_deg, int32_t ns, int32_t n_rem,
+                                                  const int64_t* __restrict__ rem_d, const int64_t* __restrict__ R,
+                                                  const int64_t* __restrict__ E, const int32_t* __restrict__ lt,
+                                                  int32_t T, uint32_t* __restrict__ tile_of) {
+    const int32_t q = blockIdx.x * kB + threadIdx.x;
+    if (q >= n_rem) return;
+    const int64_t m2 = 2 * R[q] + rem_d[q];
+    int32_t lo = 0, hi = T;  // over j in [0, T): predicate 2 E[j + 1] > m2 is monotone
+    while (lo < hi) {
+        const int32_t mid = (lo + hi) >> 1;
+        if (2 * E[mid + 1] > m2) hi = mid;
+        else lo = mid + 1;
+    }
+    tile_of[by_deg[ns + q]] = static_cast<uint32_t>(lt[min(lo, T - 1)]);
 }
 
 // entries (users in tile order): per tile its first entry, users and ratings; per user its tile-local index
@@ -250,6 +297,10 @@ bool tile_build_device(rs_svd_plan* pl) {
             uint32_t *dkey, *dkey_o, *tile_of, *tkey_o;
             uint64_t *key, *key_o;
             int32_t *idx, *perm, *head, *rid, *run_start, *pieces, *pscan;
+            int32_t* lt;
+            unsigned long long* load;
+            uint64_t *lkey, *lkey_o;
+            int64_t *rem_w, *R, *dl, *E;
             void* temp;
         } w;
         const size_t U = static_cast<size_t>(std::max(1, nu)), N = static_cast<size_t>(n);
@@ -277,6 +328,14 @@ bool tile_build_device(rs_svd_plan* pl) {
         w.run_start = c.take<int32_t>(N);
         w.pieces = c.take<int32_t>(N + 1);
         w.pscan = c.take<int32_t>(N + 1);
+        w.load = c.take<unsigned long long>(U + 1);
+        w.lkey = c.take<uint64_t>(U + 1);
+        w.lkey_o = c.take<uint64_t>(U + 1);
+        w.lt = c.take<int32_t>(U + 1);
+        w.rem_w = c.take<int64_t>(U + 1);
+        w.R = c.take<int64_t>(U + 1);
+        w.dl = c.take<int64_t>(U + 1);
+        w.E = c.take<int64_t>(U + 1);
         w.temp = nullptr;
         return w;
     };
@@ -289,6 +348,12 @@ bool tile_build_device(rs_svd_plan* pl) {
                                               static_cast<const int32_t*>(nullptr), static_cast<int32_t*>(nullptr), n, 0, 64, s));
     tmp = std::max(tmp, t1);
     RS_HIP(hipcub::DeviceScan::ExclusiveSum(nullptr, t1, static_cast<const int32_t*>(nullptr), static_cast<int32_t*>(nullptr), n + 1, s));
+    tmp = std::max(tmp, t1);
+    RS_HIP(hipcub::DeviceScan::ExclusiveSum(nullptr, t1, static_cast<const int64_t*>(nullptr), static_cast<int64_t*>(nullptr),
+                                            static_cast<int64_t>(std::max(1, nu)) + 1, s));
+    tmp = std::max(tmp, t1);
+    RS_HIP(hipcub::DeviceRadixSort::SortPairs(nullptr, t1, static_cast<const uint64_t*>(nullptr), static_cast<uint64_t*>(nullptr),
+                                              static_cast<const int32_t*>(nullptr), static_cast<int32_t*>(nullptr), std::max(1, nu), 0, 64, s));
     tmp = std::max(tmp, t1);
     Carve probe{nullptr};
     (void)carve(probe);
@@ -317,7 +382,11 @@ bool tile_build_device(rs_svd_plan* pl) {
     RS_HIP(hipStreamSynchronize(s));
     const int32_t n_active = h[0], dmax_u = h[1], dmax_i = h[2];
     tmark("degrees");
-    if (n_active <= 0 || dmax_u > rec_cap) return false;  // users cut into pieces: the host builds
+    if (n_active <= 0 || dmax_u > rec_cap) {  // users cut into pieces: the host builds
+        if (trace) std::fprintf(stderr, "sched-dev fallback: active %d, max degree %d, LDS record cap %lld\n", n_active, dmax_u,
+                                static_cast<long long>(rec_cap));
+        return false;
+    }
     const int64_t target = pl->tile_target > 0 ? pl->tile_target
                                                : std::max<int64_t>({64, dmax_u, (n + grid0 - 1) / std::max(1, grid0)});
     const int64_t n_target = (n + target - 1) / std::max<int64_t>(target, 1);
@@ -326,17 +395,45 @@ bool tile_build_device(rs_svd_plan* pl) {
     const int32_t T = static_cast<int32_t>(std::min<int64_t>(std::max<int64_t>({1, n_target, n_lds}), n_active));
     const int32_t cap = (pl->tile_run_cap > 0 ? pl->tile_run_cap : run_cap_rule(n, dmax_i, grid0, nw, pl->k));
     const int32_t cap_eff = (cap > 0 && nw > 1) ? cap : 0;
-    const int ulb = bit_len(static_cast<uint64_t>((n_active + T - 1) / T - 1));
+    // tile-local user index width: a tile holds at most kFillSnakeRounds dealt users plus the users whose
+    // midpoints fall in its stretch of the line, at most its deficit + 1 <= mean + 1 (every user spans >= 1)
+    // (the weights are LDS bytes: a user weighs >= 4 ld + 16, so a stretch holds at most mean / that + 1 users)
+    const int64_t wmin = int64_t{4} * ld + 16;
+    const int64_t mean_w = (int64_t{4} * ld * n_active + 16 * n + T - 1) / T;
+    const int ulb = bit_len(static_cast<uint64_t>(std::min<int64_t>(n_active - 1, kFillSnakeRounds + mean_w / wmin + 1)));
     const int tb = bit_len(static_cast<uint64_t>(T));  // tile ids 0..T (T: inactive users' sort key)
-    if (tb + 32 + ulb > 64) return false;
+    if (tb + 32 + ulb > 64) {
+        if (trace) std::fprintf(stderr, "sched-dev fallback: key bits %d + 32 + %d\n", tb, ulb);
+        return false;
+    }
 
-    // 2. tiles: degree order, snake deal, entries in tile order
+    // 2. tiles: degree order, boustrophedon deal of the heaviest, deficit fill of the rest, entries in tile order
     const int ub = blocks_for(nu);
     hipLaunchKernelGGL(degree_keys_kernel, dim3(ub), dim3(kB), 0, s, w.deg_u, nu, dmax_u, w.dkey, w.iota);
     size_t tb_bytes = tmp;
     RS_HIP(hipcub::DeviceRadixSort::SortPairs(w.temp, tb_bytes, w.dkey, w.dkey_o, w.iota, w.by_deg, nu, 0,
                                               std::max(1, bit_len(static_cast<uint64_t>(dmax_u))), s));
-    hipLaunchKernelGGL(snake_kernel, dim3(ub), dim3(kB), 0, s, w.by_deg, nu, n_active, T, w.tile_of);
+    const int32_t ns = static_cast<int32_t>(std::min<int64_t>(n_active, static_cast<int64_t>(kFillSnakeRounds) * T));
+    const int32_t n_rem = n_active - ns;
+    // loads in LDS bytes, as build_tile_host
+    const int32_t w0 = 4 * ld, w1 = 16;
+    const int64_t wsum = static_cast<int64_t>(w0) * n_active + static_cast<int64_t>(w1) * n;
+    const int64_t mean = (wsum + T - 1) / T;
+    RS_HIP(hipMemsetAsync(w.load, 0, sizeof(unsigned long long) * (T + 1), s));
+    hipLaunchKernelGGL(snake_kernel, dim3(ub), dim3(kB), 0, s, w.by_deg, w.deg_u, nu, n_active, ns, T, w0, w1, w.tile_of,
+                       w.load, w.rem_w);
+    if (n_rem > 0) {  // the deficit line and the fill
+        hipLaunchKernelGGL(deficit_kernel, dim3(blocks_for(T)), dim3(kB), 0, s, w.load, T, mean, w.lkey, w.iota);  // (iota[t] = t: unchanged)
+        tb_bytes = tmp;
+        RS_HIP(hipcub::DeviceRadixSort::SortPairs(w.temp, tb_bytes, w.lkey, w.lkey_o, w.iota, w.lt, T, 0, 64, s));
+        hipLaunchKernelGGL(line_kernel, dim3(blocks_for(T + 1)), dim3(kB), 0, s, w.load, w.lt, T, mean, w.dl);
+        tb_bytes = tmp;
+        RS_HIP(hipcub::DeviceScan::ExclusiveSum(w.temp, tb_bytes, w.dl, w.E, T + 1, s));
+        tb_bytes = tmp;
+        RS_HIP(hipcub::DeviceScan::ExclusiveSum(w.temp, tb_bytes, w.rem_w, w.R, n_rem, s));
+        hipLaunchKernelGGL(fill_kernel, dim3(blocks_for(n_rem)), dim3(kB), 0, s, w.by_deg, ns, n_rem, w.rem_w, w.R, w.E,
+                           w.lt, T, w.tile_of);
+    }
     tb_bytes = tmp;
     RS_HIP(hipcub::DeviceRadixSort::SortPairs(w.temp, tb_bytes, w.tile_of, w.tkey_o, w.iota, w.entry_user, nu, 0, tb, s));
     RS_HIP(hipMemsetAsync(w.users_t, 0, sizeof(int32_t) * (T + 1), s));
@@ -382,7 +479,10 @@ bool tile_build_device(rs_svd_plan* pl) {
     RS_HIP(hipStreamSynchronize(s));
     const size_t lds = static_cast<size_t>(h[3]);
     tmark("emit");
-    if (lds > kTileLdsBudget) return false;  // (the t_* buffers are rebuilt by the host build)
+    if (lds > kTileLdsBudget) {  // (the t_* buffers are rebuilt by the host build)
+        if (trace) std::fprintf(stderr, "sched-dev fallback: largest tile %zu B of LDS\n", lds);
+        return false;
+    }
 
     pl->n_tiles = T;
     pl->tile_grid = std::max(1, std::min(grid0, T));

@@ -1296,7 +1296,7 @@ static void plan_build_csr(rs_ctx* ctx, int32_t n_users, int32_t n_items, UserCS
 
 // One-shot Fit's plan (RS_SGD_WB_TILE, at most kDeviceBuildMaxNnz ratings): the COO goes to the device as it
 // is (ratings rounded to f32 on the host threads, one pinned staging buffer, three DMAs) and the tile
-// schedule is built there (RS_TILE_RULE_SNAKE_DEVICE, sched_dev.hip): no host CSR, no host schedule.  Where
+// schedule is built there (RS_TILE_RULE_FILL_DEVICE, sched_dev.hip): no host CSR, no host schedule.  Where
 // the rule does not apply, tile_build falls back to the host CSR (downloaded COO) and the LPT build.
 constexpr int64_t kDeviceBuildMaxNnz = int64_t{1} << 24;
 static void plan_build_coo_device(rs_ctx* ctx, const rs_ratings* r, int32_t k, rs_svd_plan* pl) {
@@ -1308,7 +1308,7 @@ static void plan_build_coo_device(rs_ctx* ctx, const rs_ratings* r, int32_t k, r
     pl->k = k;
     pl->ld = fast_ld(k);
     pl->nnz = r->nnz;
-    pl->tile_rule = RS_TILE_RULE_SNAKE_DEVICE;
+    pl->tile_rule = RS_TILE_RULE_FILL_DEVICE;
     const size_t n = static_cast<size_t>(r->nnz);
     char* st = static_cast<char*>(pinned_staging(12 * n));
     int32_t* su = reinterpret_cast<int32_t*>(st);
@@ -1347,7 +1347,7 @@ static void plan_build_coo_device(rs_ctx* ctx, const rs_ratings* r, int32_t k, r
     if (trace)
         std::fprintf(stderr, "fit-trace   schedule %8.3f ms (%s)\n",
                      std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count(),
-                     pl->tile_rule == RS_TILE_RULE_SNAKE_DEVICE ? "device" : "host fallback");
+                     pl->tile_rule == RS_TILE_RULE_FILL_DEVICE ? "device" : "host fallback");
 }
 
 // A new one-shot Fit plan takes over the previous one's device buffers (hipMalloc / hipFree cost tens of us
@@ -2051,16 +2051,16 @@ extern "C" int rs_svd_plan_set_tile_claim(rs_svd_plan* pl, int32_t runs_per_clai
 
 extern "C" int rs_svd_plan_set_tile_rule(rs_svd_plan* pl, int32_t rule) {
     if (!pl) return rs::set_error(nullptr, RS_ERR_INVALID, "plan is NULL");
-    if (rule < RS_TILE_RULE_LPT || rule > RS_TILE_RULE_SNAKE_DEVICE)
+    if (rule < RS_TILE_RULE_LPT || rule > RS_TILE_RULE_FILL_DEVICE)
         return rs::set_error(pl->ctx, RS_ERR_INVALID, "tile rule must be RS_TILE_RULE_LPT, _SNAKE or _SNAKE_DEVICE");
     return rs_guard(pl->ctx, [&]() -> int {
         rs::plan_sync_last(pl);
-        if (rule == RS_TILE_RULE_SNAKE) {  // the host snake: whole users only
+        if (rule == RS_TILE_RULE_FILL) {  // the host fill rule: whole users only
             rs::ensure_host_csr(pl);
             const int64_t rec_cap = static_cast<int64_t>((rs::kTileLdsBudget - 16 - static_cast<size_t>(rs::tile_lds_row(pl)) * 4) / 16);
             for (int32_t u = 0; u < pl->n_users; ++u)
                 if (pl->h_rowptr[u + 1] - pl->h_rowptr[u] > rec_cap)
-                    return rs::set_error(pl->ctx, RS_ERR_UNSUPPORTED, "snake tile rule: a user above the LDS bound");
+                    return rs::set_error(pl->ctx, RS_ERR_UNSUPPORTED, "fill tile rule: a user above the LDS bound");
         }
         const int32_t old = pl->tile_rule;
         pl->tile_rule = rule;

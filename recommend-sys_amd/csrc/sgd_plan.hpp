@@ -122,7 +122,7 @@ struct rs_svd_plan {
     int32_t exchange = RS_EXCHANGE_ROTATE;  // the multi-GPU exchange a join sets up
     int32_t fault_sub_epoch = -1;  // test hook (rs_svd_plan_inject_fault): the next sharded call throws there
     // how tiles are formed (rs_svd_plan_set_tile_rule): RS_TILE_RULE_LPT (host: LPT by ratings + cost
-    // refinement), RS_TILE_RULE_SNAKE (host: users by degree dealt boustrophedon), RS_TILE_RULE_SNAKE_DEVICE
+    // refinement), RS_TILE_RULE_FILL (host: users by degree dealt boustrophedon), RS_TILE_RULE_FILL_DEVICE
     // (the same rule built on the device from coo_*; one-shot rs_svd_fit's default)
     int32_t tile_rule = RS_TILE_RULE_LPT;
     rs::DevBuf<int32_t> coo_users, coo_items;  // device COO of a device-built schedule (any rating order)
@@ -200,6 +200,7 @@ inline int32_t buffer_bytes32(size_t elems, size_t elem_size, const char* what) 
 }
 
 // sgd.hip
+int32_t fast_ld(int32_t k);            // row stride of the FAST plans (k factors + bias, 64-float lines)
 void plan_sync_last(rs_svd_plan* pl);  // waits for the stream of the last enqueued epochs
 int32_t* numflag(rs_svd_plan* pl);  // the RS_ERR_NUMERIC device flag (allocated on first use)
 void q_convert(rs_svd_plan* pl, hipStream_t s, int32_t to_fixed);  // Q <-> int32 fixed point in place
@@ -247,10 +248,11 @@ __host__ __device__ inline uint32_t run_key(int32_t item, int32_t tile) {
     x ^= x >> 16;
     return x;
 }
+constexpr int32_t kFillSnakeRounds = 4;  // RS_TILE_RULE_FILL: boustrophedon rounds before the deficit fill
 int32_t device_cus(const rs_ctx* ctx);
 // the run cap the library picks (see auto_run_cap, sgd_tile.hip) from the item degree maximum
 int32_t run_cap_rule(int64_t nnz, int64_t dmax_item, int32_t grid, int32_t waves, int32_t k);
-void tile_build(rs_svd_plan* pl);  // (re)builds the tile schedule (host CSR, or the device for RS_TILE_RULE_SNAKE_DEVICE)
+void tile_build(rs_svd_plan* pl);  // (re)builds the tile schedule (host CSR, or the device for RS_TILE_RULE_FILL_DEVICE)
 std::vector<int32_t> user_block_bounds(const int64_t* cum, int32_t n_users, int32_t nb);
 void tile_launch(rs_svd_plan* pl, float lr, float reg, hipStream_t s, float* dP);  // one epoch (Q int32)
 // tiles [t0, t1) only (one user block), delta mode into dP (row stride ldd); returns the number of
@@ -263,7 +265,7 @@ int32_t tile_cap_in_use(const rs_svd_plan* pl);  // the run cap the schedule is 
 // (one per tile and wave: n_works + 1 offsets into pos); any pointer may be NULL
 void tile_order(rs_svd_plan* pl, int64_t* pos, int64_t* work_off, int32_t* n_works);
 
-// sched_dev.hip: the snake-rule tile schedule built on the device from the plan's device COO (coo_*).
+// sched_dev.hip: the fill-rule tile schedule built on the device from the plan's device COO (coo_*).
 // Returns false, with nothing of the plan changed, where the rule does not apply (a user above the LDS
 // bound, keys past 64 bits, a tile past the LDS): the caller builds on the host instead.
 bool tile_build_device(rs_svd_plan* pl);

@@ -24,7 +24,7 @@ SIM_COSINE, SIM_MSD, SIM_PEARSON = 0, 1, 2
 TIE_GO_SORT, TIE_STABLE = 0, 1  # KNN.Predict tie order (rs_knn_plan_set_tie_order)
 DEV_SLOPE_ONE = 3  # rs_knn_sims kind: SlopeOne deviation matrix (slope_one.go:64-92)
 EXCHANGE_ROTATE, EXCHANGE_AVERAGE, EXCHANGE_ROTATE_Q = 0, 1, 2  # multi-GPU exchange of the sharded fit (rsgpu.h)
-TILE_RULE_LPT, TILE_RULE_SNAKE, TILE_RULE_SNAKE_DEVICE = 0, 1, 2  # how users are cut into tiles (rsgpu.h)
+TILE_RULE_LPT, TILE_RULE_FILL, TILE_RULE_FILL_DEVICE = 0, 1, 2  # how users are cut into tiles (rsgpu.h)
 
 HEADER_SYMBOLS = (
     "rs_version", "rs_device_count", "rs_open", "rs_close", "rs_last_error", "rs_synchronize",

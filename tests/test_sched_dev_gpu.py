@@ -1,5 +1,5 @@
-"""The tile schedule built on the device (RS_TILE_RULE_SNAKE_DEVICE, csrc/sched_dev.hip) -- one-shot Fit's
-schedule -- against the host build of the same rule (RS_TILE_RULE_SNAKE, build_tile_host):
+"""The tile schedule built on the device (RS_TILE_RULE_FILL_DEVICE, csrc/sched_dev.hip) -- one-shot Fit's
+schedule -- against the host build of the same rule (RS_TILE_RULE_FILL, build_tile_host):
 byte-identical schedules (rs_svd_plan_schedule_digest over every array the kernel reads), on real ML-100K
 data, hot-item sets whose runs are cut into pieces, repeated (user, item) ratings, empty users, several
 workgroup / wave counts and k; the kernel on a device-built schedule is the sequential SGD of
@@ -20,10 +20,10 @@ def _digests(ctx, R, k, wg=0, waves=16, run_cap=0):
     plan = ctx.svd_plan(R, k)
     if wg or waves != 16 or run_cap:
         plan.set_tiles(workgroups=wg, waves=waves, run_cap=run_cap)
-    plan.set_tile_rule(rsgpu.TILE_RULE_SNAKE)
+    plan.set_tile_rule(rsgpu.TILE_RULE_FILL)
     host = plan.schedule_digest()
-    plan.set_tile_rule(rsgpu.TILE_RULE_SNAKE_DEVICE)
-    assert plan.tile_rule() == rsgpu.TILE_RULE_SNAKE_DEVICE
+    plan.set_tile_rule(rsgpu.TILE_RULE_FILL_DEVICE)
+    assert plan.tile_rule() == rsgpu.TILE_RULE_FILL_DEVICE
     dev = plan.schedule_digest()
     plan.set_tile_rule(rsgpu.TILE_RULE_LPT)
     lpt = plan.schedule_digest()
@@ -67,7 +67,7 @@ def test_device_schedule_equals_host_ml1m_shape(ctx):
 
 def test_one_shot_fit_builds_on_device(ctx):
     """rs_svd_fit (the Go Fit) on a shuffled COO: its cached schedule is the device rule and equals the host
-    snake build of a plan over the same ratings; the fit trains (held-out RMSE falls, finite)."""
+    fill build of a plan over the same ratings; the fit trains (held-out RMSE falls, finite)."""
     u, i, r, nu, ni = synth.ml1m_like(seed=12)
     p = np.random.default_rng(0).permutation(len(r))
     hold = p[:20000]
@@ -77,9 +77,9 @@ def test_one_shot_fit_builds_on_device(ctx):
     P0, Q0 = rng.normal(0, 0.1, (nu, 100)), rng.normal(0, 0.1, (ni, 100))
     P, Q, bu, bi, gb = ctx.svd_fit(R, P0, Q0, n_epochs=10)
     digest, rule = ctx.fit_schedule_digest()
-    assert rule == rsgpu.TILE_RULE_SNAKE_DEVICE
+    assert rule == rsgpu.TILE_RULE_FILL_DEVICE
     plan = ctx.svd_plan(R, 100)
-    plan.set_tile_rule(rsgpu.TILE_RULE_SNAKE)
+    plan.set_tile_rule(rsgpu.TILE_RULE_FILL)
     assert plan.schedule_digest() == digest
     plan.close()
     pred = O.svd_predict(u[hold], i[hold], P, Q, bu, bi, gb)
@@ -90,7 +90,7 @@ def test_one_shot_fit_builds_on_device(ctx):
 @pytest.mark.parametrize("epochs,target,run_cap", [(1, 3000, 0), (2, 2000, 3)])
 def test_one_wave_on_device_schedule_is_sequential_sgd(ctx, ml100k, epochs, target, run_cap):
     """One workgroup of one wave on the device-built schedule: svd.go:93-129 in the visit order the host's
-    snake build exports (rs_svd_plan_tile_order), to 1e-5."""
+    fill build exports (rs_svd_plan_tile_order), to 1e-5."""
     f = folds(*ml100k)[0]
     n, k = 20000, 64
     u, i, r, nu, ni = f.iu[:n], f.ii[:n], f.r[:n], f.nu, f.ni
@@ -99,8 +99,8 @@ def test_one_wave_on_device_schedule_is_sequential_sgd(ctx, ml100k, epochs, targ
     bu0, bi0 = rng.normal(0, 0.1, nu), rng.normal(0, 0.1, ni)
     plan = ctx.svd_plan(rsgpu.Ratings(u, i, r, nu, ni), k)
     plan.set_tiles(workgroups=1, waves=1, target=target, run_cap=run_cap)
-    plan.set_tile_rule(rsgpu.TILE_RULE_SNAKE_DEVICE)
-    assert plan.tile_rule() == rsgpu.TILE_RULE_SNAKE_DEVICE
+    plan.set_tile_rule(rsgpu.TILE_RULE_FILL_DEVICE)
+    assert plan.tile_rule() == rsgpu.TILE_RULE_FILL_DEVICE
     plan.upload(P0, Q0, bu0, bi0, 3.2)
     plan.epochs(epochs)
     got = plan.download()
@@ -116,16 +116,16 @@ def test_one_wave_on_device_schedule_is_sequential_sgd(ctx, ml100k, epochs, targ
 
 def test_device_build_falls_back_above_lds_bound(ctx):
     """k = 256: a user of 12000 ratings exceeds one tile's LDS (pieces needed): the device rule does not
-    apply -- the build falls back to LPT and the host snake is RS_ERR_UNSUPPORTED."""
+    apply -- the build falls back to LPT and the host fill rule is RS_ERR_UNSUPPORTED."""
     rng = np.random.default_rng(3)
     u = np.concatenate([np.zeros(12000, np.int32), rng.integers(1, 500, 30000).astype(np.int32)])
     i = rng.integers(0, 20000, len(u)).astype(np.int32)
     R = rsgpu.Ratings(u, i, rng.integers(1, 6, len(u)).astype(np.float64), 500, 20000)
     plan = ctx.svd_plan(R, 256)
-    plan.set_tile_rule(rsgpu.TILE_RULE_SNAKE_DEVICE)
+    plan.set_tile_rule(rsgpu.TILE_RULE_FILL_DEVICE)
     assert plan.tile_rule() == rsgpu.TILE_RULE_LPT
     with pytest.raises(rsgpu.RsError) as e:
-        plan.set_tile_rule(rsgpu.TILE_RULE_SNAKE)
+        plan.set_tile_rule(rsgpu.TILE_RULE_FILL)
     assert e.value.code == -4
     plan.epochs(1)
     plan.download()
