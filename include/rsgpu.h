@@ -490,9 +490,9 @@ int rs_svd_group_epochs(rs_svd_group* group, int32_t n_epochs, float lr, float r
 void rs_svd_group_destroy(rs_svd_group* group);
 /* Item shards of near-equal ratings over contiguous inner item ids: bounds (n_shards + 1 entries). */
 int rs_item_shards(int64_t nnz, const int32_t* items, int32_t n_items, int32_t n_shards, int32_t* bounds);
-/* core/svd.go:63-132 (FAST tile schedule) on n_devices GPUs of this process: with n_items >= n_users the
- * items are sharded by rs_item_shards and P rank-blocks rotate (RS_EXCHANGE_ROTATE); with fewer items than
- * users the users are cut into ranges of near-equal ratings and Q item blocks rotate
+/* core/svd.go:63-132 (FAST tile schedule) on n_devices GPUs of this process: the items are sharded by
+ * rs_item_shards and P rank-blocks rotate (RS_EXCHANGE_ROTATE); with fewer items than users and P rank-blocks
+ * of 16 MiB or more the users are cut into ranges of near-equal ratings and Q item blocks rotate
  * (RS_EXCHANGE_ROTATE_Q).  As rs_svd_fit otherwise (GlobalBias warm start, host buffers in / out; a fit
  * whose shards leave the fixed-point range is rebuilt and redone from the inputs on half the workgroups and
  * run cap 2, up to three times; RS_ERR_NUMERIC after every shard's values are written). */
