@@ -153,7 +153,7 @@ int rs_last_kernel_ms(const rs_ctx* ctx, double* ms);
 int rs_svd_fit(rs_ctx* ctx, const rs_ratings* r, const rs_sgd_params* p, double* P, double* Q,
                double* bu, double* bi, double* gb);
 /* Divergence refits of the last rs_svd_fit on this ctx (FAST tile schedule): a fit whose model left the
- * fixed-point range or went non-finite is redone from the caller's inputs on half the workgroups and half the run cap (less
+ * fixed-point range or went non-finite is redone from the caller's inputs on a quarter of the workgroups and half the run cap (less
  * Hogwild staleness on the hot item rows), up to three times, before RS_ERR_NUMERIC is returned. */
 int rs_fit_refits(const rs_ctx* ctx, int32_t* n);
 
@@ -288,10 +288,10 @@ int rs_svd_plan_set_tile_claim(rs_svd_plan* plan, int32_t runs_per_claim);
  * apply (a user above the LDS bound, a tile past the LDS) the device build falls back to RS_TILE_RULE_LPT
  * and RS_TILE_RULE_FILL fails with RS_ERR_UNSUPPORTED.  Rebuilds the schedule. */
 /* Divergence guard of the tile schedule (default on): every epoch measures its training MSE and flags one
- * that rises more than 1.2x over the previous epoch's (the history starts over on upload / init);
+ * that rises more than 1.03x over the previous epoch's (the history starts over on upload / init);
  * rs_svd_plan_epochs checks a call's epochs once at the end (that flag, fixed-point range of P and Q, a
  * finite GlobalBias; one small readback, so the call waits for its epochs) and redoes a failed call from its start state -- P, Q and GlobalBias copied on the device first --
- * on half the workgroups and half the run cap, up to three times; the plan keeps them.  A call still failing leaves
+ * on a quarter of the workgroups and half the run cap, up to three times; the plan keeps them.  A call still failing leaves
  * the flag for the download (RS_ERR_NUMERIC).  rs_svd_fit always runs guarded.  off: no snapshot, no wait. */
 int rs_svd_plan_set_guard(rs_svd_plan* plan, int32_t on);
 /* Calls the guard has redone on this plan so far. */

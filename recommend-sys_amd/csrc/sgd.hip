@@ -704,9 +704,9 @@ __global__ __launch_bounds__(256) void svd_epoch_epilogue_kernel(
         if (done) *done = 0;
         if (loss_part && loss_state) {
             // the divergence guard's second signal: this epoch's training MSE (at the ratings' pre-update
-            // residuals) more than 1.2x the previous epoch's -- SGD at a stable rate does not raise it
+            // residuals) more than 1.03x the previous epoch's -- SGD at a stable rate does not raise it
             const double mse = sl[0] * inv_nnz * inv_lr2, prev = loss_state[0];
-            if (!(mse < 1e30) || (prev > 0.0 && mse > 1.2 * prev)) flag[0] = 1;
+            if (!(mse < 1e30) || (prev > 0.0 && mse > 1.03 * prev)) flag[0] = 1;
             loss_state[0] = mse;
         }
     }
@@ -1615,11 +1615,13 @@ static void plan_download(rs_svd_plan* pl, double* P, double* Q, double* bu, dou
     }
 }
 
-// P rows out of the fixed-point range of the tile kernel's LDS (|p| >= 127.5, or non-finite): flag
-__global__ __launch_bounds__(256) void p_range_kernel(const float* __restrict__ P, int64_t n, int32_t* __restrict__ flag) {
+// rows with an entry at or past `bound` (or non-finite): flag.  The guard scans P and Q at 32 -- a quarter of
+// the fixed-point range, far past any trained factor or bias on star ratings -- so a run-away row is caught
+// while the call can still be redone from a sane start
+__global__ __launch_bounds__(256) void range_kernel(const float* __restrict__ P, int64_t n, float bound, int32_t* __restrict__ flag) {
     bool bad = false;
     for (int64_t t = static_cast<int64_t>(blockIdx.x) * 256 + threadIdx.x; t < n; t += static_cast<int64_t>(gridDim.x) * 256)
-        bad |= !(fabsf(P[t]) < 127.5f);
+        bad |= !(fabsf(P[t]) < bound);
     if (bad) flag[0] = 1;
 }
 
@@ -1650,7 +1652,8 @@ static void plan_epochs_once(rs_svd_plan* pl, int32_t epochs, float lr, float re
             RS_HIP(hipMemsetAsync(pl->done.p, 0, sizeof(int32_t), s));
         }
         // the guard's loss check: tile epochs of a guarded plan (loss partials written by the kernel)
-        const bool loss_on = tile && pl->guard && lr > 0.f && pl->loss_state.p && pl->loss_part.n >= pl->partial.n;
+        const bool loss_on = tile && pl->guard && lr > 0.f && pl->loss_state.p && pl->guard_flag.p &&
+                             pl->loss_part.n >= pl->partial.n;
         struct HoistScope {  // launch_fast sees the hoisted state only inside this loop, even on a throw
             rs_svd_plan* p;
             ~HoistScope() { p->hoisted = false; }
@@ -1667,7 +1670,7 @@ static void plan_epochs_once(rs_svd_plan* pl, int32_t epochs, float lr, float re
                                tile ? pl->t_split_rows.p : pl->split_rows.p, n_split, pl->ld, pl->partial.p,
                                static_cast<int64_t>(pl->n_blocks), pl->gb.p, inv_nnz,
                                n_live > 0 ? pl->done.p : nullptr, loss_on ? pl->loss_part.p : nullptr,
-                               loss_on ? pl->loss_state.p : nullptr, loss_on ? numflag(pl) : nullptr,
+                               loss_on ? pl->loss_state.p : nullptr, loss_on ? pl->guard_flag.p : nullptr,
                                1.0 / (static_cast<double>(lr) * static_cast<double>(lr)));
             RS_HIP(hipGetLastError());
         }
@@ -1701,7 +1704,7 @@ static void plan_epochs_once(rs_svd_plan* pl, int32_t epochs, float lr, float re
 // chip-wide update rate, i.e. with the workgroups in flight, and halving them (and
 // the run cap: the automatic cap would grow as the grid shrinks) halves that staleness.  So a call's epochs are checked once, at the end (the Q conversion's range flag, a P range
 // scan, a finite GlobalBias: one small readback), and a call that failed is redone from its start state --
-// P, Q and GlobalBias copied on the device before the first epoch -- on half the workgroups, up to three
+// P, Q and GlobalBias copied on the device before the first epoch -- on a quarter of the workgroups, up to three
 // times; the plan keeps the smaller grid and cap.  Only then does the caller see the flag (RS_ERR_NUMERIC at
 // download).  `under` is host work run while the first attempt's kernels execute.
 static void plan_epochs(rs_svd_plan* pl, int32_t epochs, float lr, float reg, hipStream_t s,
@@ -1722,6 +1725,8 @@ static void plan_epochs(rs_svd_plan* pl, int32_t epochs, float lr, float reg, hi
         pl->loss_state.alloc(1);
         RS_HIP(hipMemsetAsync(pl->loss_state.p, 0, sizeof(double), s));
     }
+    if (!pl->guard_flag.p) pl->guard_flag.alloc(1);
+    RS_HIP(hipMemsetAsync(pl->guard_flag.p, 0, sizeof(int32_t), s));
     RS_HIP(hipMemcpyAsync(pl->P_snap.p, pl->P.p, pl->P.n * sizeof(float), hipMemcpyDeviceToDevice, s));
     RS_HIP(hipMemcpyAsync(pl->Q_snap.p, pl->Q.p, pl->Q.n * sizeof(float), hipMemcpyDeviceToDevice, s));
     RS_HIP(hipMemcpyAsync(pl->gb_snap.p, pl->gb.p, sizeof(double), hipMemcpyDeviceToDevice, s));
@@ -1734,19 +1739,25 @@ static void plan_epochs(rs_svd_plan* pl, int32_t epochs, float lr, float reg, hi
     int32_t* flag = numflag(pl);
     for (int attempt = 0;; ++attempt) {
         plan_epochs_once(pl, epochs, lr, reg, s);
-        const int64_t pn = static_cast<int64_t>(pl->P.n);
-        hipLaunchKernelGGL(p_range_kernel, dim3(static_cast<int>(std::min<int64_t>(1024, (pn + 255) / 256))), dim3(256), 0, s,
-                           pl->P.p, pn, flag);
+        const int64_t pn = static_cast<int64_t>(pl->P.n), qn = static_cast<int64_t>(pl->Q.n);
+        hipLaunchKernelGGL(range_kernel, dim3(static_cast<int>(std::min<int64_t>(1024, (pn + 255) / 256))), dim3(256), 0, s,
+                           pl->P.p, pn, 32.0f, pl->guard_flag.p);
+        hipLaunchKernelGGL(range_kernel, dim3(static_cast<int>(std::min<int64_t>(1024, (qn + 255) / 256))), dim3(256), 0, s,
+                           pl->Q.p, qn, 32.0f, pl->guard_flag.p);
         RS_HIP(hipGetLastError());
         RS_HIP(hipMemcpyAsync(ck.p, pl->gb.p, sizeof(double), hipMemcpyDeviceToHost, s));
         RS_HIP(hipMemcpyAsync(ck.p + 1, flag, sizeof(int32_t), hipMemcpyDeviceToHost, s));
+        RS_HIP(hipMemcpyAsync(reinterpret_cast<int32_t*>(ck.p + 1) + 1, pl->guard_flag.p, sizeof(int32_t),
+                              hipMemcpyDeviceToHost, s));
         if (after) after();
         if (attempt == 0 && under) under();
         RS_HIP(hipStreamSynchronize(s));
         double g;
         std::memcpy(&g, ck.p, 8);
-        const bool bad = static_cast<int32_t>(ck.p[1]) != 0 || !std::isfinite(g);
-        if (!bad || attempt == 3 || pl->tile_grid <= 1) return;  // (a flag still raised reaches the download)
+        const int32_t* fl = reinterpret_cast<const int32_t*>(ck.p + 1);
+        const bool bad = fl[0] != 0 || fl[1] != 0 || !std::isfinite(g);
+        RS_HIP(hipMemsetAsync(pl->guard_flag.p, 0, sizeof(int32_t), s));  // (the guard's own signal is never an error)
+        if (!bad || attempt == 3 || pl->tile_grid <= 1) return;  // (a range flag still raised reaches the download)
         RS_HIP(hipMemsetAsync(flag, 0, sizeof(int32_t), s));
         RS_HIP(hipMemcpyAsync(pl->P.p, pl->P_snap.p, pl->P.n * sizeof(float), hipMemcpyDeviceToDevice, s));
         RS_HIP(hipMemcpyAsync(pl->Q.p, pl->Q_snap.p, pl->Q.n * sizeof(float), hipMemcpyDeviceToDevice, s));
@@ -1754,7 +1765,7 @@ static void plan_epochs(rs_svd_plan* pl, int32_t epochs, float lr, float reg, hi
         RS_HIP(hipMemcpyAsync(pl->loss_state.p, pl->gb_snap.p + 1, sizeof(double), hipMemcpyDeviceToDevice, s));
         RS_HIP(hipStreamSynchronize(s));
         const int32_t cap = tile_cap_in_use(pl);  // (before the grid changes: the automatic cap depends on it)
-        pl->tile_wg = std::max(1, pl->tile_grid / 2);
+        pl->tile_wg = std::max(1, pl->tile_grid / 4);
         pl->tile_run_cap = std::max(2, cap / 2);
         tile_build(pl);
         pl->n_blocks = tile_partials(pl);
@@ -2424,7 +2435,7 @@ extern "C" int rs_svd_fit(rs_ctx* ctx, const rs_ratings* r, const rs_sgd_params*
             };
             rs_svd_plan& pl = *cache->plan;
             // Divergence guard: plan_epochs redoes a call that left the fixed-point range or went non-finite on
-            // half the workgroups (up to three times; the plan keeps the smaller grid), so a Go Fit that panics on
+            // a quarter of the workgroups (up to three times; the plan keeps the smaller grid), so a Go Fit that panics on
             // an error never gets a NaN model first; RS_ERR_NUMERIC only when every attempt failed.
             const int32_t refits0 = pl.refits;
             if (prepared) {

@@ -137,6 +137,7 @@ struct rs_svd_plan {
     rs::DevBuf<double> gb_snap;                // {GlobalBias, loss state} at the call start
     rs::DevBuf<float> loss_part;               // per (workgroup, wave): sum of (lr diff)^2 of the last epoch
     rs::DevBuf<double> loss_state;             // last epoch's training MSE (0: none since the factors were set)
+    rs::DevBuf<int32_t> guard_flag;            // the guard's own signals (a rising loss, |p| or |q| >= 32): redo, not an error
     ~rs_svd_plan() {
         if (ev0) (void)hipEventDestroy(ev0);
         if (ev1) (void)hipEventDestroy(ev1);

@@ -22,6 +22,8 @@ CASES = {
     "1m_k64": (20000, 4000, 60.0, 0.9, 64, 10, True),
     "1m_k64_hot": (20000, 4000, 60.0, 1.1, 64, 10, True),
     "1m_k100_hot": (20000, 2000, 50.0, 1.2, 100, 10, True),
+    "1m_k100_flat": (20000, 8000, 50.0, 0.6, 100, 10, True),
+    "1m_k64_3pct": (20000, 2000, 50.0, 1.4, 64, 10, True),
     "8m_k100": (100000, 20000, 80.0, 0.9, 100, 8, False),
     "8m_k256_hot": (200000, 10000, 40.0, 1.1, 256, 5, False),
     "32m_k100": (400000, 50000, 80.0, 1.0, 100, 5, False),

@@ -1,5 +1,5 @@
 """FAST default stability at library defaults: rs_synth sets of 1M / 8M / 32M / 128M ratings,
-hottest item 0.85-2.3 % of the ratings, k 64 / 100 / 256 (scripts/experiments/exp_stability.py CASES), 5 %
+hottest item 0.3-3 % of the ratings, k 64 / 100 / 256 (scripts/experiments/exp_stability.py CASES), 5 %
 held out.  Where the sequential reference (or_svd_fit, core/svd.go:92-130 in user-major order, the same
 init) is affordable (the 1M sets) the held-out RMSE after 10 epochs may not be worse than the reference's
 by more than 0.003 -- lower is allowed: FAST's GlobalBias warm start and its concurrent epochs reach the
@@ -16,7 +16,7 @@ pytestmark = pytest.mark.gpu
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(REPO, "scripts", "experiments"))
 
-SMALL = ["1m_k64", "1m_k64_hot", "1m_k100_hot"]
+SMALL = ["1m_k64", "1m_k64_hot", "1m_k100_hot", "1m_k100_flat", "1m_k64_3pct"]
 LARGE = ["8m_k100", "8m_k256_hot", "32m_k100", "128m_k256"]
 
 
