@@ -1370,6 +1370,9 @@ static void plan_recycle(rs_svd_plan* pl, rs_svd_plan* old, int32_t n_users, int
     if (old->P_snap.n == static_cast<size_t>(std::max(1, n_users)) * fast_ld(k)) pl->P_snap = std::move(old->P_snap);
     if (old->Q_snap.n == static_cast<size_t>(std::max(1, n_items)) * fast_ld(k)) pl->Q_snap = std::move(old->Q_snap);
     pl->gb_snap = std::move(old->gb_snap);
+    pl->loss_part = std::move(old->loss_part);    // (the loss history is reset by the upload)
+    pl->loss_state = std::move(old->loss_state);
+    pl->guard_flag = std::move(old->guard_flag);  // (zero: cleared after every check)
     pl->gb = std::move(old->gb);
     if (old->ld == fast_ld(k) && old->n_users == n_users) pl->P = std::move(old->P);
     if (old->ld == fast_ld(k) && old->n_items == n_items && old->n_qrows == old->n_items) pl->Q = std::move(old->Q);
@@ -1618,10 +1621,11 @@ static void plan_download(rs_svd_plan* pl, double* P, double* Q, double* bu, dou
 // rows with an entry at or past `bound` (or non-finite): flag.  The guard scans P and Q at 32 -- a quarter of
 // the fixed-point range, far past any trained factor or bias on star ratings -- so a run-away row is caught
 // while the call can still be redone from a sane start
-__global__ __launch_bounds__(256) void range_kernel(const float* __restrict__ P, int64_t n, float bound, int32_t* __restrict__ flag) {
+__global__ __launch_bounds__(256) void range_kernel(const float* __restrict__ P, int64_t np, const float* __restrict__ Q,
+                                                   int64_t nq, float bound, int32_t* __restrict__ flag) {
     bool bad = false;
-    for (int64_t t = static_cast<int64_t>(blockIdx.x) * 256 + threadIdx.x; t < n; t += static_cast<int64_t>(gridDim.x) * 256)
-        bad |= !(fabsf(P[t]) < bound);
+    for (int64_t t = static_cast<int64_t>(blockIdx.x) * 256 + threadIdx.x; t < np + nq; t += static_cast<int64_t>(gridDim.x) * 256)
+        bad |= !(fabsf(t < np ? P[t] : Q[t - np]) < bound);
     if (bad) flag[0] = 1;
 }
 
@@ -1725,8 +1729,10 @@ static void plan_epochs(rs_svd_plan* pl, int32_t epochs, float lr, float reg, hi
         pl->loss_state.alloc(1);
         RS_HIP(hipMemsetAsync(pl->loss_state.p, 0, sizeof(double), s));
     }
-    if (!pl->guard_flag.p) pl->guard_flag.alloc(1);
-    RS_HIP(hipMemsetAsync(pl->guard_flag.p, 0, sizeof(int32_t), s));
+    if (!pl->guard_flag.p) {  // (zero between calls: cleared after every check)
+        pl->guard_flag.alloc(1);
+        RS_HIP(hipMemsetAsync(pl->guard_flag.p, 0, sizeof(int32_t), s));
+    }
     RS_HIP(hipMemcpyAsync(pl->P_snap.p, pl->P.p, pl->P.n * sizeof(float), hipMemcpyDeviceToDevice, s));
     RS_HIP(hipMemcpyAsync(pl->Q_snap.p, pl->Q.p, pl->Q.n * sizeof(float), hipMemcpyDeviceToDevice, s));
     RS_HIP(hipMemcpyAsync(pl->gb_snap.p, pl->gb.p, sizeof(double), hipMemcpyDeviceToDevice, s));
@@ -1740,10 +1746,8 @@ static void plan_epochs(rs_svd_plan* pl, int32_t epochs, float lr, float reg, hi
     for (int attempt = 0;; ++attempt) {
         plan_epochs_once(pl, epochs, lr, reg, s);
         const int64_t pn = static_cast<int64_t>(pl->P.n), qn = static_cast<int64_t>(pl->Q.n);
-        hipLaunchKernelGGL(range_kernel, dim3(static_cast<int>(std::min<int64_t>(1024, (pn + 255) / 256))), dim3(256), 0, s,
-                           pl->P.p, pn, 32.0f, pl->guard_flag.p);
-        hipLaunchKernelGGL(range_kernel, dim3(static_cast<int>(std::min<int64_t>(1024, (qn + 255) / 256))), dim3(256), 0, s,
-                           pl->Q.p, qn, 32.0f, pl->guard_flag.p);
+        hipLaunchKernelGGL(range_kernel, dim3(static_cast<int>(std::min<int64_t>(1024, (pn + qn + 255) / 256))), dim3(256), 0, s,
+                           pl->P.p, pn, pl->Q.p, qn, 32.0f, pl->guard_flag.p);
         RS_HIP(hipGetLastError());
         RS_HIP(hipMemcpyAsync(ck.p, pl->gb.p, sizeof(double), hipMemcpyDeviceToHost, s));
         RS_HIP(hipMemcpyAsync(ck.p + 1, flag, sizeof(int32_t), hipMemcpyDeviceToHost, s));
