@@ -14,10 +14,15 @@
 //
 // (likewise in SVDPP.Fit, NMF.Fit and, for the pair loop of knn.go:188-216, KNN.Fit).
 //
-// This file is not compiled in the build's own CI: neither the container nor the MI355X boxes this
-// repository is tested on have a Go toolchain (DESIGN.md §1).  Every entry point it calls is exercised
-// through the same C-ABI by the Python ctypes binding (tests/) and by the C++ mirror of this API
-// (recommend-sys_amd/host/, tests/test_host_cpp.py).
+// cgo pointer rules: no memory handed to C holds a Go pointer.  The rs_ratings struct and its arrays are
+// C.malloc'd and freed after the call (newCRatings); outputs are []float64 backing arrays (no pointers
+// inside); the rs_ctx is closed before Fit returns.  The library keeps no caller pointer after a call.
+//
+// This file is unverified by a Go build: neither the container nor the MI355X boxes this repository is
+// tested on have a Go toolchain (DESIGN.md §1).  Every entry point it calls is exercised through the same
+// C-ABI by the Python ctypes binding (tests/) and by the C++ mirror of this API (recommend-sys_amd/host/,
+// tests/test_host_cpp.py), whose TestCgoRatingsShape drives rs_svd_fit with rs_ratings allocated and
+// freed exactly as newCRatings does.
 package core
 
 // #cgo CFLAGS: -I${SRCDIR}/../third_party/rsgpu/include
@@ -28,13 +33,14 @@ import "C"
 
 import (
 	"fmt"
-	"runtime"
 	"unsafe"
 )
 
 // gpuCtx is one rs_ctx: one device and one HIP stream, not thread-safe.  CrossValidate (eval.go:28-35)
-// fits every fold's own estimator copy in its own goroutine, so each Fit opens its own ctx; the
-// library's entry points re-bind their device, so goroutine migration between OS threads is harmless.
+// fits every fold's own estimator copy in its own goroutine, so each Fit opens its own ctx and closes it
+// before returning (`defer g.close()`): the ctx holds a HIP stream and pinned staging, which a finalizer
+// would keep alive until some later GC.  The library's entry points re-bind their device, so goroutine
+// migration between OS threads is harmless.
 type gpuCtx struct{ p *C.rs_ctx }
 
 func openGPU(device int) *gpuCtx {
@@ -42,9 +48,14 @@ func openGPU(device int) *gpuCtx {
 	if rc := C.rs_open(C.int32_t(device), &p); rc != C.RS_OK {
 		panic(fmt.Sprintf("rs_open: %s", C.GoString(C.rs_last_error(nil))))
 	}
-	g := &gpuCtx{p}
-	runtime.SetFinalizer(g, func(g *gpuCtx) { C.rs_close(g.p) })
-	return g
+	return &gpuCtx{p}
+}
+
+func (g *gpuCtx) close() {
+	if g.p != nil {
+		C.rs_close(g.p)
+		g.p = nil
+	}
 }
 
 // check panics like the reference does on bad input: its Fit has no error return.  RS_ERR_NUMERIC means
@@ -55,22 +66,42 @@ func (g *gpuCtx) check(rc C.int, what string) {
 	}
 }
 
-// ratingsView: the TrainSet's triples in train-set order with inner ids (data.go:131-154).  The slices
-// hold no Go pointers, so cgo may pass them; the library copies them during the call and keeps nothing.
-func ratingsView(t *TrainSet) (C.rs_ratings, []int32, []int32) {
+// cRatings: the TrainSet's triples in train-set order with inner ids (data.go:131-154), copied into C
+// memory.  cgo's pointer-passing rule forbids handing C a Go struct that holds Go pointers (the default
+// GODEBUG=cgocheck=1 panics with "cgo argument has Go pointer to unpinned Go pointer"), so the
+// rs_ratings struct and its three arrays are all C.malloc'd; the caller frees them once the call has
+// returned (`defer cr.free()`).  The library copies what it needs during the call and keeps no pointer.
+// (tests: host/tests/core_test.cpp TestCgoRatingsShape builds and frees rs_ratings exactly this way.)
+type cRatings struct{ r *C.rs_ratings }
+
+func newCRatings(t *TrainSet) cRatings {
 	n := t.Length()
-	u := make([]int32, n+1) // +1: a valid &u[0] for an empty set
-	i := make([]int32, n+1)
+	m := n
+	if m == 0 {
+		m = 1 // a valid pointer for an empty set
+	}
+	r := (*C.rs_ratings)(C.malloc(C.size_t(unsafe.Sizeof(C.rs_ratings{}))))
+	users := (*C.int32_t)(C.malloc(C.size_t(m) * 4))
+	items := (*C.int32_t)(C.malloc(C.size_t(m) * 4))
+	vals := (*C.double)(C.malloc(C.size_t(m) * 8))
+	u, i, v := unsafe.Slice(users, m), unsafe.Slice(items, m), unsafe.Slice(vals, m)
 	for k := 0; k < n; k++ {
-		u[k] = int32(t.ConvertUserID(t.Users[k]))
-		i[k] = int32(t.ConvertItemID(t.Items[k]))
+		u[k] = C.int32_t(t.ConvertUserID(t.Users[k]))
+		i[k] = C.int32_t(t.ConvertItemID(t.Items[k]))
+		v[k] = C.double(t.Ratings[k])
 	}
-	r := C.rs_ratings{nnz: C.int64_t(n), n_users: C.int32_t(t.UserCount), n_items: C.int32_t(t.ItemCount),
-		users: (*C.int32_t)(unsafe.Pointer(&u[0])), items: (*C.int32_t)(unsafe.Pointer(&i[0]))}
-	if n > 0 {
-		r.ratings = (*C.double)(unsafe.Pointer(&t.Ratings[0]))
-	}
-	return r, u, i
+	r.nnz = C.int64_t(n)
+	r.n_users = C.int32_t(t.UserCount)
+	r.n_items = C.int32_t(t.ItemCount)
+	r.users, r.items, r.ratings = users, items, vals
+	return cRatings{r}
+}
+
+func (c cRatings) free() {
+	C.free(unsafe.Pointer(c.r.users))
+	C.free(unsafe.Pointer(c.r.items))
+	C.free(unsafe.Pointer(c.r.ratings))
+	C.free(unsafe.Pointer(c.r))
 }
 
 // flat: one contiguous []float64 with the [][]float64 rows sliced out of it (the rows alias the buffer
@@ -84,6 +115,9 @@ func flat(rows, k int) ([]float64, [][]float64) {
 	return buf, m
 }
 
+// f64: an output buffer.  Passing a pointer into a []float64 is legal cgo: the backing array holds no Go
+// pointers, and the library writes it before returning and keeps nothing.  (rs_sgd_params, passed as &p,
+// holds no pointers either.)
 func f64(b []float64) *C.double { return (*C.double)(unsafe.Pointer(&b[0])) }
 
 func sgdMode(p Parameters) C.int32_t {
@@ -115,7 +149,8 @@ func (s *SVD) fitGPU(trainData TrainSet) {
 	s.UserBias = make([]float64, trainData.UserCount+1)[:trainData.UserCount]
 	s.ItemBias = make([]float64, trainData.ItemCount+1)[:trainData.ItemCount]
 	s.GlobalBias = 0
-	r, u, i := ratingsView(&trainData)
+	cr := newCRatings(&trainData)
+	defer cr.free()
 	p := C.rs_sgd_params{n_factors: C.int32_t(nFactors), n_epochs: C.int32_t(nEpochs),
 		lr: C.double(lr), reg: C.double(reg), mode: sgdMode(s.Params), write_back: C.RS_SGD_WB_TILE}
 	bu := (*C.double)(unsafe.Pointer(&s.UserBias[:1][0]))
@@ -126,19 +161,16 @@ func (s *SVD) fitGPU(trainData TrainSet) {
 		for k := range d {
 			d[k] = int32(k)
 		}
-		rc := C.rs_svd_fit_multi((*C.int32_t)(unsafe.Pointer(&d[0])), C.int32_t(len(d)), &r, &p, 0,
+		rc := C.rs_svd_fit_multi((*C.int32_t)(unsafe.Pointer(&d[0])), C.int32_t(len(d)), cr.r, &p, 0,
 			f64(pBuf), f64(qBuf), bu, bi, gb)
-		runtime.KeepAlive(u)
-		runtime.KeepAlive(i)
 		if rc != C.RS_OK {
 			panic(fmt.Sprintf("SVD.Fit (%d GPUs): %s", nGPUs, C.GoString(C.rs_last_error(nil))))
 		}
 		return
 	}
 	g := openGPU(s.Params.GetInt("deviceID", 0))
-	g.check(C.rs_svd_fit(g.p, &r, &p, f64(pBuf), f64(qBuf), bu, bi, gb), "SVD.Fit")
-	runtime.KeepAlive(u)
-	runtime.KeepAlive(i)
+	defer g.close()
+	g.check(C.rs_svd_fit(g.p, cr.r, &p, f64(pBuf), f64(qBuf), bu, bi, gb), "SVD.Fit")
 }
 
 // fitGPU is (*SVDPP).Fit (svd.go:316-427): the same shape with the implicit factors Y.
@@ -165,15 +197,15 @@ func (pp *SVDPP) fitGPU(trainData TrainSet) {
 	pp.UserFactor, pp.ItemFactor, pp.ImplFactor = P, Q, Y
 	pp.GlobalBias = 0
 	pp.UserRatings = trainData.UserRatings() // Predict still needs N(u) (svd.go:271-282)
-	r, u, i := ratingsView(&trainData)
+	cr := newCRatings(&trainData)
+	defer cr.free()
 	p := C.rs_sgd_params{n_factors: C.int32_t(nFactors), n_epochs: C.int32_t(nEpochs),
 		lr: C.double(lr), reg: C.double(reg), mode: sgdMode(pp.Params), write_back: C.RS_SGD_WB_TILE}
 	g := openGPU(pp.Params.GetInt("deviceID", 0))
-	g.check(C.rs_svdpp_fit(g.p, &r, &p, f64(pBuf), f64(qBuf), f64(yBuf),
+	defer g.close()
+	g.check(C.rs_svdpp_fit(g.p, cr.r, &p, f64(pBuf), f64(qBuf), f64(yBuf),
 		(*C.double)(unsafe.Pointer(&pp.UserBias[:1][0])), (*C.double)(unsafe.Pointer(&pp.ItemBias[:1][0])),
 		(*C.double)(unsafe.Pointer(&pp.GlobalBias))), "SVDPP.Fit")
-	runtime.KeepAlive(u)
-	runtime.KeepAlive(i)
 }
 
 // fitGPU is (*NMF).Fit (svd.go:158-251).  "nmfAsWritten" (default true) keeps svd.go:243-249's item
@@ -200,12 +232,12 @@ func (N *NMF) fitGPU(trainSet TrainSet) {
 	if !N.Params.GetBool("nmfAsWritten", true) {
 		asWritten = 0
 	}
-	r, u, i := ratingsView(&trainSet)
+	cr := newCRatings(&trainSet)
+	defer cr.free()
 	g := openGPU(N.Params.GetInt("deviceID", 0))
-	g.check(C.rs_nmf_fit(g.p, &r, C.int32_t(nFactors), C.int32_t(nEpochs), C.double(reg), asWritten,
+	defer g.close()
+	g.check(C.rs_nmf_fit(g.p, cr.r, C.int32_t(nFactors), C.int32_t(nEpochs), C.double(reg), asWritten,
 		f64(pBuf), f64(qBuf)), "NMF.Fit")
-	runtime.KeepAlive(u)
-	runtime.KeepAlive(i)
 }
 
 // simsGPU replaces the sorts() + nJobs pair loop of (*KNN).Fit (knn.go:188-216): everything before
@@ -226,6 +258,7 @@ func (K *KNN) simsGPU(sim Sim) {
 	ids, vals = append(ids, 0), append(vals, 0) // valid &x[0] for an empty set
 	buf, S := flat(L, L)
 	g := openGPU(K.Params.GetInt("deviceID", 0))
+	defer g.close()
 	g.check(C.rs_knn_sims(g.p, simKind(sim), C.int32_t(L), C.int32_t(R),
 		(*C.int64_t)(unsafe.Pointer(&rowptr[0])), (*C.int32_t)(unsafe.Pointer(&ids[0])),
 		f64(vals), f64(buf)), "KNN.Fit")
@@ -254,11 +287,11 @@ func (baseLine *BaseLine) fitGPU(trainSet TrainSet) {
 	baseLine.userBias = make([]float64, trainSet.UserCount+1)[:trainSet.UserCount]
 	baseLine.itemBias = make([]float64, trainSet.ItemCount+1)[:trainSet.ItemCount]
 	baseLine.globalBias = 0 // base.go:135-163 starts it at zero (the loop learns it)
-	r, u, i := ratingsView(&trainSet)
+	cr := newCRatings(&trainSet)
+	defer cr.free()
 	g := openGPU(baseLine.Params.GetInt("deviceID", 0))
-	g.check(C.rs_baseline_fit(g.p, &r, C.int32_t(nEpochs), C.double(lr), C.double(reg),
+	defer g.close()
+	g.check(C.rs_baseline_fit(g.p, cr.r, C.int32_t(nEpochs), C.double(lr), C.double(reg),
 		(*C.double)(unsafe.Pointer(&baseLine.userBias[:1][0])), (*C.double)(unsafe.Pointer(&baseLine.itemBias[:1][0])),
 		(*C.double)(unsafe.Pointer(&baseLine.globalBias))), "BaseLine.Fit")
-	runtime.KeepAlive(u)
-	runtime.KeepAlive(i)
 }

@@ -48,7 +48,8 @@ extern "C" {
 #define RS_ERR_NOMEM (-3)       /* host or device allocation failed                               */
 #define RS_ERR_UNSUPPORTED (-4) /* valid request this build does not implement                    */
 #define RS_ERR_NO_DEVICE (-5)   /* no gfx950 device visible                                       */
-#define RS_ERR_NUMERIC (-6)     /* the model left its number format (non-finite or |q| >= 128);
+#define RS_ERR_NUMERIC (-6)     /* the model left its number format (non-finite, or |q| past the fixed-point
+                                   range: 128 on star ratings, wider for wider rating scales);
                                    the values are still returned                                   */
 
 /* SGD visit schedule (SURVEY §8a parity contract P1/P2) */
@@ -265,7 +266,8 @@ int rs_svd_plan_set_mode(rs_svd_plan* plan, int32_t write_back, int32_t ring_dep
  * (an item's run in a tile longer than this is cut into pieces on different waves; 0 = auto: hot items
  * cut so that ~100 of an item's updates are in flight; a huge value = never; ignored with
  * one wave), ring (q_i rows each wave loads ahead, in runs: 0 = auto = 2; with claimed runs (the default,
- * rs_svd_plan_set_tile_claim) 2, or 3 for k <= 126; with host-dealt runs 2 or 4, and 3, 6, 8, 12 for
+ * rs_svd_plan_set_tile_claim) 2, or for k <= 126 a ring of 3 or more becomes 4 on chunks of 8 runs (the
+ * ring must divide the chunk); with host-dealt runs 2 or 4, and 3, 6, 8, 12 for
  * k <= 126; other values round down; deeper rings read hot rows earlier, i.e. staler).  Rebuilds the
  * schedule. */
 int rs_svd_plan_set_tiles(rs_svd_plan* plan, int32_t workgroups, int32_t waves, int32_t target,
@@ -291,8 +293,13 @@ int rs_svd_plan_set_tile_claim(rs_svd_plan* plan, int32_t runs_per_claim);
  * that rises more than 1.03x over the previous epoch's (the history starts over on upload / init);
  * rs_svd_plan_epochs checks a call's epochs once at the end (that flag, fixed-point range of P and Q, a
  * finite GlobalBias; one small readback, so the call waits for its epochs) and redoes a failed call from its start state -- P, Q and GlobalBias copied on the device first --
- * on a quarter of the workgroups and half the run cap, up to three times; the plan keeps them.  A call still failing leaves
- * the flag for the download (RS_ERR_NUMERIC).  rs_svd_fit always runs guarded.  off: no snapshot, no wait. */
+ * on a quarter of the workgroups and half the run cap, up to three times.  The plan keeps the smaller grid after a hard
+ * signal (the range flag, a non-finite GlobalBias); after redos that only the loss rule or the guard bound asked for
+ * it returns to the caller's grid for the next call (until such redos have come three times).  The guard bound is a
+ * quarter of the fixed-point range, which follows the ratings' spread (|v| < 32 on star scales, 512 for 1-100
+ * ratings).  A call still failing leaves the flag for the download (RS_ERR_NUMERIC).  rs_svd_fit always runs
+ * guarded.  Cost: a second resident copy of P and Q on the device (the call-start snapshot) and one host wait per
+ * call.  off: no snapshot, no wait. */
 int rs_svd_plan_set_guard(rs_svd_plan* plan, int32_t on);
 /* Calls the guard has redone on this plan so far. */
 int rs_svd_plan_refits(const rs_svd_plan* plan, int32_t* n);
@@ -494,10 +501,13 @@ int rs_item_shards(int64_t nnz, const int32_t* items, int32_t n_items, int32_t n
  * rs_item_shards and P rank-blocks rotate (RS_EXCHANGE_ROTATE); with fewer items than users and P rank-blocks
  * of 16 MiB or more the users are cut into ranges of near-equal ratings and Q item blocks rotate
  * (RS_EXCHANGE_ROTATE_Q).  As rs_svd_fit otherwise (GlobalBias warm start, host buffers in / out; a fit
- * whose shards leave the fixed-point range is rebuilt and redone from the inputs on half the workgroups and
- * run cap 2, up to three times; RS_ERR_NUMERIC after every shard's values are written). */
+ * whose shards leave the fixed-point range, go non-finite or hold a factor past the guard bound is rebuilt and
+ * redone from the inputs on half the workgroups and run cap 2, up to three times -- rs_fit_multi_refits counts
+ * them; RS_ERR_NUMERIC after every shard's values are written). */
 int rs_svd_fit_multi(const int32_t* devices, int32_t n_devices, const rs_ratings* r, const rs_sgd_params* p,
                      int32_t n_blocks, double* P, double* Q, double* bu, double* bi, double* gb);
+/* Refits of the calling thread's last rs_svd_fit_multi (0, 1, 2 or 3). */
+int rs_fit_multi_refits(int32_t* n);
 /* ---- user-sharded multi-GPU (the dual partition, SURVEY §8e "measured alternative") ---------- *
  * Each rank builds a plan over its user range (local user ids) with ALL items; Q and b_i are
  * replicated, P and b_u are exclusive to the rank.  Per epoch: rs_svd_plan_epoch_qdelta runs the

@@ -221,7 +221,7 @@ __device__ __host__ inline bool hot_copy_used(int32_t b, int32_t nb, int2 meta) 
 __global__ __launch_bounds__(256) void hot_partial_kernel(const int32_t* __restrict__ Q, const int32_t* __restrict__ hot,
                                                           const int2* __restrict__ meta, int32_t H, int32_t nb,
                                                           int32_t n_items, int32_t ld, int32_t b0, int32_t b1,
-                                                          float* __restrict__ out) {
+                                                          float* __restrict__ out, float fx_inv) {
     const int64_t n = static_cast<int64_t>(H) * ld;
     for (int64_t t = static_cast<int64_t>(blockIdx.x) * 256 + threadIdx.x; t < n; t += static_cast<int64_t>(gridDim.x) * 256) {
         const int64_t h = t / ld;
@@ -231,19 +231,19 @@ __global__ __launch_bounds__(256) void hot_partial_kernel(const int32_t* __restr
         float acc = 0.f;
         for (int32_t b = b0; b < b1; ++b)
             if (hot_copy_used(b, nb, m)) acc += static_cast<float>(Q[(n_items + static_cast<int64_t>(b) * H + h) * ld + c] - base);
-        out[t] = acc * kFxInv;
+        out[t] = acc * fx_inv;
     }
 }
 // every copy of blocks [b0, b1) and the item's row take the merged value, last + w_h x the summed moves (back to
 // the fixed point)
 __global__ __launch_bounds__(256) void hot_write_kernel(int32_t* __restrict__ Q, const int32_t* __restrict__ hot,
                                                         int32_t H, int32_t n_items, int32_t ld, int32_t b0, int32_t b1,
-                                                        const float* __restrict__ w, const float* __restrict__ moves) {
+                                                        const float* __restrict__ w, const float* __restrict__ moves, float fx) {
     const int64_t n = static_cast<int64_t>(H) * ld;
     for (int64_t t = static_cast<int64_t>(blockIdx.x) * 256 + threadIdx.x; t < n; t += static_cast<int64_t>(gridDim.x) * 256) {
         const int64_t h = t / ld;
         const int32_t c = static_cast<int32_t>(t - h * ld);
-        const int32_t v = __float2int_rn(w[h] * moves[t] * kFx) + Q[static_cast<int64_t>(hot[h]) * ld + c];
+        const int32_t v = __float2int_rn(w[h] * moves[t] * fx) + Q[static_cast<int64_t>(hot[h]) * ld + c];
         Q[static_cast<int64_t>(hot[h]) * ld + c] = v;
         for (int32_t b = b0; b < b1; ++b) Q[(n_items + static_cast<int64_t>(b) * H + h) * ld + c] = v;
     }
@@ -607,7 +607,7 @@ void epochs_rotate(rs_svd_plan* pl, int32_t n_epochs, float lr, float reg, hipSt
                     c.pending[b] = 0;
                 }
             hipLaunchKernelGGL(hot_partial_kernel, dim3(grid_for(hn)), dim3(256), 0, s, Qi, pl->hot_rows.p, pl->hot_meta.p,
-                               H, nb, pl->n_items, pl->ld, b0, b1, c.hot_part.p);
+                               H, nb, pl->n_items, pl->ld, b0, b1, c.hot_part.p, pl->fx_inv());
             RS_HIP(hipGetLastError());
             const float* avg = c.hot_part.p;
             if (c.nccl && N > 1) {
@@ -631,7 +631,7 @@ void epochs_rotate(rs_svd_plan* pl, int32_t n_epochs, float lr, float reg, hipSt
                 avg = c.hot_avg.p;
             }
             hipLaunchKernelGGL(hot_write_kernel, dim3(grid_for(hn)), dim3(256), 0, s, Qi, pl->hot_rows.p, H, pl->n_items,
-                               pl->ld, b0, b1, c.hot_w.p, avg);
+                               pl->ld, b0, b1, c.hot_w.p, avg, pl->fx());
             RS_HIP(hipGetLastError());
         }
         // GlobalBias: every stratum's partial, folded once per epoch on every rank
@@ -746,6 +746,9 @@ void group_join(rs_svd_group* g, int32_t n_blocks) {
     std::vector<double> tot(static_cast<size_t>(std::max(1, rq ? ni : nu)), 0.0);
     std::vector<int64_t> first(n), end(n);
     double total = 0.0;
+    int32_t shift = 31;  // the group's fixed-point shift: the smallest of its shards' (Q rows move between them)
+    for (rs_svd_plan* pl : g->plans) shift = std::min(shift, pl->fx_shift);
+    for (rs_svd_plan* pl : g->plans) pl->fx_shift = shift;
     for (int r = 0; r < n; ++r) {
         const rs_svd_plan* pl = g->plans[r];
         if (pl->n_users != nu || pl->k != g->plans[0]->k)
@@ -999,6 +1002,9 @@ extern "C" int rs_svd_plan_join(rs_svd_plan* pl, const void* id, int32_t rank, i
             cnt[span_at + 2 * rank] = static_cast<double>(sp.first + 1);
             cnt[span_at + 2 * rank + 1] = static_cast<double>(sp.second);
         }
+        const size_t shift_at = cnt.size();  // every rank's fixed-point shift: the group runs at the smallest
+        cnt.resize(shift_at + static_cast<size_t>(n_ranks), 0.0);
+        cnt[shift_at + rank] = static_cast<double>(pl->fx_shift);
         cnt.push_back(static_cast<double>(pl->nnz));
         rs::DevBuf<double> d(cnt.size());
         d.upload(cnt.data(), cnt.size(), s);
@@ -1006,6 +1012,8 @@ extern "C" int rs_svd_plan_join(rs_svd_plan* pl, const void* id, int32_t rank, i
         d.download(cnt.data(), cnt.size(), s);
         RS_HIP(hipStreamSynchronize(s));
         c->total_nnz = cnt.back();
+        for (int32_t r = 0; r < n_ranks; ++r)  // (Q rows travel between ranks as fixed-point words)
+            pl->fx_shift = std::min(pl->fx_shift, static_cast<int32_t>(cnt[shift_at + r]));
         if (rq) {
             std::vector<int64_t> first(n_ranks), end(n_ranks);
             for (int32_t r = 0; r < n_ranks; ++r) {
@@ -1131,6 +1139,15 @@ extern "C" int rs_item_shards(int64_t nnz, const int32_t* items, int32_t n_items
     return RS_OK;
 }
 
+namespace rs {
+thread_local int32_t g_multi_refits = 0;  // refits of this thread's last rs_svd_fit_multi
+}
+extern "C" int rs_fit_multi_refits(int32_t* n) {
+    if (!n) return rs::set_error(nullptr, RS_ERR_INVALID, "n is NULL");
+    *n = rs::g_multi_refits;
+    return RS_OK;
+}
+
 extern "C" int rs_svd_fit_multi(const int32_t* devices, int32_t n_devices, const rs_ratings* r,
                                 const rs_sgd_params* p, int32_t n_blocks, double* P, double* Q, double* bu,
                                 double* bi, double* gb) {
@@ -1168,9 +1185,10 @@ extern "C" int rs_svd_fit_multi(const int32_t* devices, int32_t n_devices, const
         for (rs_svd_plan* pl : plans) rs_svd_plan_destroy(pl);
         for (rs_ctx* c : ctxs) rs_close(c);
     };
-    // Divergence guard (as rs_svd_fit's): a fit whose shards leave the fixed-point range
-    // or go non-finite is rebuilt and redone from the caller's inputs -- untouched until the final download --
-    // on half the workgroups and the smallest run cap (2), up to three times.
+    // Divergence guard (as rs_svd_fit's): a fit whose shards leave the fixed-point range,
+    // go non-finite or hold a row past the guard bound is rebuilt and redone from the caller's inputs -- untouched
+    // until the final download -- on half the workgroups and the smallest run cap (2), up to three times
+    // (rs_fit_multi_refits counts them).
     int32_t refits = 0;
     int st = rs_guard(nullptr, [&]() -> int {
       const double gb_in = *gb;
@@ -1217,7 +1235,7 @@ extern "C" int rs_svd_fit_multi(const int32_t* devices, int32_t n_devices, const
         if (e != RS_OK) return e;
         e = rs_svd_group_epochs(g, p->n_epochs, static_cast<float>(p->lr), static_cast<float>(p->reg));
         if (e != RS_OK) return e;
-        bool diverged = false;  // any shard's range flag or a non-finite GlobalBias (before anything is returned)
+        bool diverged = false;  // any shard's range flag, a non-finite GlobalBias or a row past the guard bound
         for (int32_t s = 0; s < n; ++s) {
             rs_svd_plan* pl = plans[s];
             double gv = 0.0;
@@ -1225,7 +1243,8 @@ extern "C" int rs_svd_fit_multi(const int32_t* devices, int32_t n_devices, const
             pl->gb.download(&gv, 1, pl->ctx->stream);
             if (pl->numflag.p) pl->numflag.download(&f, 1, pl->ctx->stream);
             RS_HIP(hipStreamSynchronize(pl->ctx->stream));
-            diverged = diverged || f != 0 || !std::isfinite(gv);
+            // (and, as the single-GPU guard, a factor or bias past the guard bound: a run-away row)
+            diverged = diverged || f != 0 || !std::isfinite(gv) || !rs::plan_range_ok(pl);
         }
         if (diverged && attempt < 3 && p->n_epochs > 0) {
             ++refits;
@@ -1243,7 +1262,7 @@ extern "C" int rs_svd_fit_multi(const int32_t* devices, int32_t n_devices, const
         return numeric;
       }
     });
-    (void)refits;
+    rs::g_multi_refits = refits;
     std::string err = st != RS_OK ? std::string(rs_last_error(nullptr)) : std::string();
     for (int32_t s = 0; s < n && st != RS_OK && err.empty(); ++s)
         if (ctxs[s]) err = rs_last_error(ctxs[s]);

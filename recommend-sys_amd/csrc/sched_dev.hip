@@ -19,7 +19,8 @@
 // Keys are distinct within a tile (run_key is a bijection of the item), so no tie rule is needed and the
 // two builds are byte-identical (tests/test_sched_dev_gpu.py compares rs_svd_plan_schedule_digest).
 #include <hip/hip_runtime.h>
-#include <hipcub/hipcub.hpp>
+#include <rocprim/device/device_radix_sort.hpp>
+#include <rocprim/device/device_scan.hpp>
 
 #include <algorithm>
 #include <chrono>
@@ -39,6 +40,12 @@ namespace {
 constexpr int kB = 256;
 inline int blocks_for(int64_t n) { return static_cast<int>(std::max<int64_t>(1, std::min<int64_t>((n + kB - 1) / kB, 1 << 20))); }
 inline int bit_len(uint64_t x) { int b = 0; while (x) { ++b; x >>= 1; } return b; }
+
+// exclusive prefix sum on the stream (rocPRIM's device scan; a null temp pointer queries its bytes)
+template <class T>
+hipError_t excl_sum(void* temp, size_t& bytes, const T* in, T* out, int64_t n, hipStream_t s) {
+    return rocprim::exclusive_scan(temp, bytes, in, out, T{0}, static_cast<size_t>(n), rocprim::plus<T>(), s);
+}
 
 // stats: [0] active users, [1] max user degree, [2] max item degree, [3] LDS bytes of the largest tile,
 // [4] run-header entries (pieces + one sentinel per tile)
@@ -339,20 +346,20 @@ bool tile_build_device(rs_svd_plan* pl) {
         w.temp = nullptr;
         return w;
     };
-    // cub temp storage: the largest of the five sorts / scans, queried with null pointers
+    // rocPRIM temp storage: the largest of the five sorts / scans, queried with null pointers
     size_t tmp = 0, t1 = 0;
-    RS_HIP(hipcub::DeviceRadixSort::SortPairs(nullptr, t1, static_cast<const uint32_t*>(nullptr), static_cast<uint32_t*>(nullptr),
+    RS_HIP(rocprim::radix_sort_pairs(nullptr, t1, static_cast<const uint32_t*>(nullptr), static_cast<uint32_t*>(nullptr),
                                               static_cast<const int32_t*>(nullptr), static_cast<int32_t*>(nullptr), std::max(1, nu), 0, 32, s));
     tmp = std::max(tmp, t1);
-    RS_HIP(hipcub::DeviceRadixSort::SortPairs(nullptr, t1, static_cast<const uint64_t*>(nullptr), static_cast<uint64_t*>(nullptr),
+    RS_HIP(rocprim::radix_sort_pairs(nullptr, t1, static_cast<const uint64_t*>(nullptr), static_cast<uint64_t*>(nullptr),
                                               static_cast<const int32_t*>(nullptr), static_cast<int32_t*>(nullptr), n, 0, 64, s));
     tmp = std::max(tmp, t1);
-    RS_HIP(hipcub::DeviceScan::ExclusiveSum(nullptr, t1, static_cast<const int32_t*>(nullptr), static_cast<int32_t*>(nullptr), n + 1, s));
+    RS_HIP(excl_sum(nullptr, t1, static_cast<const int32_t*>(nullptr), static_cast<int32_t*>(nullptr), n + 1, s));
     tmp = std::max(tmp, t1);
-    RS_HIP(hipcub::DeviceScan::ExclusiveSum(nullptr, t1, static_cast<const int64_t*>(nullptr), static_cast<int64_t*>(nullptr),
+    RS_HIP(excl_sum(nullptr, t1, static_cast<const int64_t*>(nullptr), static_cast<int64_t*>(nullptr),
                                             static_cast<int64_t>(std::max(1, nu)) + 1, s));
     tmp = std::max(tmp, t1);
-    RS_HIP(hipcub::DeviceRadixSort::SortPairs(nullptr, t1, static_cast<const uint64_t*>(nullptr), static_cast<uint64_t*>(nullptr),
+    RS_HIP(rocprim::radix_sort_pairs(nullptr, t1, static_cast<const uint64_t*>(nullptr), static_cast<uint64_t*>(nullptr),
                                               static_cast<const int32_t*>(nullptr), static_cast<int32_t*>(nullptr), std::max(1, nu), 0, 64, s));
     tmp = std::max(tmp, t1);
     Carve probe{nullptr};
@@ -411,7 +418,7 @@ bool tile_build_device(rs_svd_plan* pl) {
     const int ub = blocks_for(nu);
     hipLaunchKernelGGL(degree_keys_kernel, dim3(ub), dim3(kB), 0, s, w.deg_u, nu, dmax_u, w.dkey, w.iota);
     size_t tb_bytes = tmp;
-    RS_HIP(hipcub::DeviceRadixSort::SortPairs(w.temp, tb_bytes, w.dkey, w.dkey_o, w.iota, w.by_deg, nu, 0,
+    RS_HIP(rocprim::radix_sort_pairs(w.temp, tb_bytes, w.dkey, w.dkey_o, w.iota, w.by_deg, nu, 0,
                                               std::max(1, bit_len(static_cast<uint64_t>(dmax_u))), s));
     const int32_t ns = static_cast<int32_t>(std::min<int64_t>(n_active, static_cast<int64_t>(kFillSnakeRounds) * T));
     const int32_t n_rem = n_active - ns;
@@ -425,23 +432,23 @@ bool tile_build_device(rs_svd_plan* pl) {
     if (n_rem > 0) {  // the deficit line and the fill
         hipLaunchKernelGGL(deficit_kernel, dim3(blocks_for(T)), dim3(kB), 0, s, w.load, T, mean, w.lkey, w.iota);  // (iota[t] = t: unchanged)
         tb_bytes = tmp;
-        RS_HIP(hipcub::DeviceRadixSort::SortPairs(w.temp, tb_bytes, w.lkey, w.lkey_o, w.iota, w.lt, T, 0, 64, s));
+        RS_HIP(rocprim::radix_sort_pairs(w.temp, tb_bytes, w.lkey, w.lkey_o, w.iota, w.lt, T, 0, 64, s));
         hipLaunchKernelGGL(line_kernel, dim3(blocks_for(T + 1)), dim3(kB), 0, s, w.load, w.lt, T, mean, w.dl);
         tb_bytes = tmp;
-        RS_HIP(hipcub::DeviceScan::ExclusiveSum(w.temp, tb_bytes, w.dl, w.E, T + 1, s));
+        RS_HIP(excl_sum(w.temp, tb_bytes, w.dl, w.E, T + 1, s));
         tb_bytes = tmp;
-        RS_HIP(hipcub::DeviceScan::ExclusiveSum(w.temp, tb_bytes, w.rem_w, w.R, n_rem, s));
+        RS_HIP(excl_sum(w.temp, tb_bytes, w.rem_w, w.R, n_rem, s));
         hipLaunchKernelGGL(fill_kernel, dim3(blocks_for(n_rem)), dim3(kB), 0, s, w.by_deg, ns, n_rem, w.rem_w, w.R, w.E,
                            w.lt, T, w.tile_of);
     }
     tb_bytes = tmp;
-    RS_HIP(hipcub::DeviceRadixSort::SortPairs(w.temp, tb_bytes, w.tile_of, w.tkey_o, w.iota, w.entry_user, nu, 0, tb, s));
+    RS_HIP(rocprim::radix_sort_pairs(w.temp, tb_bytes, w.tile_of, w.tkey_o, w.iota, w.entry_user, nu, 0, tb, s));
     RS_HIP(hipMemsetAsync(w.users_t, 0, sizeof(int32_t) * (T + 1), s));
     RS_HIP(hipMemsetAsync(w.recs_t, 0, sizeof(int32_t) * (T + 1), s));
     hipLaunchKernelGGL(entries_kernel, dim3(blocks_for(n_active)), dim3(kB), 0, s, w.entry_user, n_active, w.tile_of,
                        w.deg_u, w.first_entry, w.users_t, w.recs_t);
     tb_bytes = tmp;
-    RS_HIP(hipcub::DeviceScan::ExclusiveSum(w.temp, tb_bytes, w.recs_t, w.rec_at, T + 1, s));
+    RS_HIP(excl_sum(w.temp, tb_bytes, w.recs_t, w.rec_at, T + 1, s));
     // outputs (upper bounds: pieces <= ratings)
     const size_t runs_cap = static_cast<size_t>(n) + static_cast<size_t>(T);
     if (pl->t_tiles.n < static_cast<size_t>(T)) pl->t_tiles.alloc(static_cast<size_t>(T));
@@ -458,15 +465,15 @@ bool tile_build_device(rs_svd_plan* pl) {
     hipLaunchKernelGGL(rating_keys_kernel, dim3(nb), dim3(kB), 0, s, pl->coo_users.p, pl->coo_items.p, n, w.tile_of, w.ul_of,
                        ulb, w.key, w.idx);
     tb_bytes = tmp;
-    RS_HIP(hipcub::DeviceRadixSort::SortPairs(w.temp, tb_bytes, w.key, w.key_o, w.idx, w.perm, n, 0, tb + 32 + ulb, s));
+    RS_HIP(rocprim::radix_sort_pairs(w.temp, tb_bytes, w.key, w.key_o, w.idx, w.perm, n, 0, tb + 32 + ulb, s));
     hipLaunchKernelGGL(heads_kernel, dim3(nb), dim3(kB), 0, s, w.key_o, w.perm, pl->coo_vals.p, n, ulb, w.head, pl->t_recs.p);
     tb_bytes = tmp;
-    RS_HIP(hipcub::DeviceScan::ExclusiveSum(w.temp, tb_bytes, w.head, w.rid, n, s));
+    RS_HIP(excl_sum(w.temp, tb_bytes, w.head, w.rid, n, s));
     hipLaunchKernelGGL(run_start_kernel, dim3(nb), dim3(kB), 0, s, w.head, w.rid, n, w.run_start);
     RS_HIP(hipMemsetAsync(w.pieces, 0, sizeof(int32_t) * (n + 1), s));
     hipLaunchKernelGGL(pieces_kernel, dim3(nb), dim3(kB), 0, s, w.head, w.rid, w.run_start, n, cap_eff, nw, w.pieces);
     tb_bytes = tmp;
-    RS_HIP(hipcub::DeviceScan::ExclusiveSum(w.temp, tb_bytes, w.pieces, w.pscan, n + 1, s));
+    RS_HIP(excl_sum(w.temp, tb_bytes, w.pieces, w.pscan, n + 1, s));
 
     // 4. emit
     tmark("runs");

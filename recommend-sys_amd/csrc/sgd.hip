@@ -50,6 +50,7 @@
 #include <thread>
 #include <stdexcept>
 #include <type_traits>
+#include <mutex>
 #include <vector>
 
 #include "common.hpp"
@@ -78,14 +79,14 @@ __device__ __forceinline__ double sgd_work_item(
     const float* __restrict__ wk_frac, const int32_t* __restrict__ items,
     const float* __restrict__ ratings, float* __restrict__ P, __amdgpu_buffer_rsrc_t rq, float gb0,
     float lr, float reg, float* __restrict__ dP, const float* __restrict__ uw, int32_t whole_direct,
-    int32_t lc, Emit&& emit) {
+    int32_t lc, float fx, Emit&& emit) {
 #pragma clang fp contract(fast)
     constexpr int LD = 64 * E, B = 32;  // ratings per chunk (one unrolled loop body)
     static_assert(B % D == 0 && D <= B, "ring depth must divide the 32-rating chunk");
     const int lane = threadIdx.x & 63;
     const int32_t lane4 = lane * 4;
     const bool bias_lane = lane == 63;
-    const float a = 1.f - lr * reg;
+    const float a = 1.f - lr * reg, fx_inv = 1.f / fx;
     const int32_t u = wk_user[w];
     const int64_t b = wk_rng[2 * w], e = wk_rng[2 * w + 1];
     const float frac = wk_frac[w];
@@ -101,7 +102,7 @@ __device__ __forceinline__ double sgd_work_item(
 #pragma unroll
         for (int x = 0; x < E; ++x) {
             const uint32_t v = __builtin_amdgcn_raw_buffer_load_b32(rq, roff<E>(row, x, lane4, lc), 0, kSgdAux);
-            q[x] = FX ? fx_to_f(v) : __uint_as_float(v);
+            q[x] = FX ? fx_to_f(v, fx_inv) : __uint_as_float(v);
         }
     };
 
@@ -254,7 +255,7 @@ __global__ __launch_bounds__(256) void svd_epoch_fast_kernel(
     if (w < n_work) {
         contrib = sgd_work_item<E, D>(
             w, wk_user, wk_rng, wk_frac, items, ratings, P, rq, static_cast<float>(gb_in[0]), lr, reg,
-            dP, uw, whole_direct, lc, [&](int32_t row, const float (&qn)[E], const float (&q)[E]) {
+            dP, uw, whole_direct, lc, 1.f, [&](int32_t row, const float (&qn)[E], const float (&q)[E]) {
 #pragma unroll
                 for (int x = 0; x < E; ++x) {
                     if constexpr (WB == 1)
@@ -322,7 +323,7 @@ __global__ __launch_bounds__(256) void svd_epoch_hybrid_kernel(
     float* Q, int32_t q_bytes, const double* __restrict__ gb_in, double* __restrict__ gb_partial,
     float lr, float reg, float* __restrict__ dP, const float* __restrict__ uw, int32_t whole_direct,
     int64_t* __restrict__ trace, const int4* __restrict__ live_meta, int32_t n_live,
-    float* __restrict__ qlast, int32_t* __restrict__ done, int32_t kf) {
+    float* __restrict__ qlast, int32_t* __restrict__ done, int32_t kf, float fx) {
     constexpr int R = HeavyRing<E>::kRing, NB = HeavyRing<E>::kBatch, LD = 64 * E, NW = 3;
     // the producer's vmcnt holds only its q_i loads: prefetch as deep as the 63-op counter allows
     constexpr int DH = E == 1 ? 32 : (E == 2 ? 32 : (E <= 4 ? 16 : 8));
@@ -430,13 +431,13 @@ __global__ __launch_bounds__(256) void svd_epoch_hybrid_kernel(
         for (int w = n_heavy + (blk - n_heavy) * 4 + wib; w < n_work; w += stride) {
             const int64_t t0 = trace ? static_cast<int64_t>(__builtin_amdgcn_s_memrealtime()) : 0;
             contrib += sgd_work_item<E, D, FX>(
-                w, wk_user, wk_rng, wk_frac, items, ratings, P, rq, gb0, lr, reg, dP, uw, whole_direct, lc,
+                w, wk_user, wk_rng, wk_frac, items, ratings, P, rq, gb0, lr, reg, dP, uw, whole_direct, lc, fx,
                 [&](int32_t row, const float (&qn)[E], const float (&q)[E]) {
 #pragma unroll
                     for (int x = 0; x < E; ++x) {
                         if constexpr (DROP) {
                         } else if constexpr (FX) {
-                            __builtin_amdgcn_raw_ptr_buffer_atomic_add_i32(fx_delta(qn[x], q[x]), rq, roff<E>(row, x, lane4, lc), 0, 0);
+                            __builtin_amdgcn_raw_ptr_buffer_atomic_add_i32(fx_delta(qn[x], q[x], fx), rq, roff<E>(row, x, lane4, lc), 0, 0);
                         } else {
                             __builtin_amdgcn_raw_ptr_buffer_atomic_fadd_f32(qn[x] - q[x], rq, roff<E>(row, x, lane4, lc), 0, 0);
                         }
@@ -468,7 +469,7 @@ __global__ __launch_bounds__(256) void svd_epoch_hybrid_kernel(
     if (wib == 0) {
         int32_t tail = 0, free_end = R;  // entries [tail, free_end) may be written
         contrib = sgd_work_item<E, DH, FX, false>(
-            blk, wk_user, wk_rng, wk_frac, items, ratings, P, rq, gb0, lr, reg, dP, uw, whole_direct, lc,
+            blk, wk_user, wk_rng, wk_frac, items, ratings, P, rq, gb0, lr, reg, dP, uw, whole_direct, lc, fx,
             [&](int32_t row, const float (&qn)[E], const float (&q)[E]) {
                 if (tail >= free_end) {  // ring full: every entry below min(head) has been drained
                     for (;;) {
@@ -482,7 +483,7 @@ __global__ __launch_bounds__(256) void svd_epoch_hybrid_kernel(
                 const int slot = tail & (R - 1);
 #pragma unroll
                 for (int x = 0; x < E; ++x)
-                    s_q[slot][lane + 64 * x] = FX ? __int_as_float(fx_delta(qn[x], q[x])) : qn[x] - q[x];
+                    s_q[slot][lane + 64 * x] = FX ? __int_as_float(fx_delta(qn[x], q[x], fx)) : qn[x] - q[x];
                 if (lane == 0) s_row[slot] = row;
                 __atomic_signal_fence(__ATOMIC_SEQ_CST);  // entry before tail, in issue order
                 ++tail;
@@ -611,22 +612,24 @@ __global__ __launch_bounds__(64) void svd_live_merge_kernel(float* __restrict__ 
 }
 
 // Fixed-point item rows around a call (tile schedule; hybrid with rs_svd_plan_set_fixed_q), in place
-// over Q's n words: to == 1: q -> round(q * 2^24) (saturating), to == 0: back to fp32.  A value that
-// is non-finite or |q| >= 128 going in, or within 2^-1 of the int32 range coming back (integer
-// atomics wrap), raises *flag (plan_download reports RS_ERR_NUMERIC).
+// over Q's n words: to == 1: q -> round(q * 2^shift) (saturating), to == 0: back to fp32.  A value that
+// is non-finite or |q| >= 2^(31 - shift) going in (128 at the star-scale shift 24), or within 1/2 of the
+// int32 range coming back (integer atomics wrap), raises *flag (plan_download reports RS_ERR_NUMERIC).
 __global__ __launch_bounds__(256) void svd_q_fixed_kernel(float* __restrict__ Q, int64_t n, int32_t to,
-                                                          int32_t* __restrict__ flag) {
+                                                          int32_t* __restrict__ flag, int32_t shift) {
+    const float fx = static_cast<float>(1u << shift), range = static_cast<float>(1u << (31 - shift));
+    const int32_t lim = static_cast<int32_t>(0x80000000u - (1u << (shift - 1)));  // within 1/2 of the int32 range
     bool bad = false;
     for (int64_t t = static_cast<int64_t>(blockIdx.x) * 256 + threadIdx.x; t < n;
          t += static_cast<int64_t>(gridDim.x) * 256) {
         if (to) {
             const float v = Q[t];
-            bad |= !(fabsf(v) < 128.0f);
-            Q[t] = __int_as_float(__float2int_rn(v * kFx));
+            bad |= !(fabsf(v) < range);
+            Q[t] = __int_as_float(__float2int_rn(v * fx));
         } else {
             const int32_t v = __float_as_int(Q[t]);
-            bad |= v >= (127 << 24) + (1 << 23) || v <= -((127 << 24) + (1 << 23));
-            Q[t] = fx_to_f(static_cast<uint32_t>(v));
+            bad |= v >= lim || v <= -lim;
+            Q[t] = fx_to_f(static_cast<uint32_t>(v), 1.f / fx);
         }
     }
     if (bad) flag[0] = 1;
@@ -884,7 +887,7 @@ static void launch_fast_t(rs_svd_plan* pl, float lr, float reg, hipStream_t s, f
                                pl->partial.p, lr, reg, d, multi ? pl->uw.p : nullptr, multi ? 0 : 1,
                                pl->trace.n ? pl->trace.p : nullptr, pl->n_live > 0 ? pl->live_meta.p : nullptr,
                                pl->n_live, pl->n_live > 0 ? pl->qlast.p : nullptr, pl->n_live > 0 ? pl->done.p : nullptr,
-                               pl->k);
+                               pl->k, pl->fx());
         } else if (pl->n_live > 0) {
             RS_HIP(hipMemsetAsync(pl->done.p, 0, sizeof(int32_t), s));
             hipLaunchKernelGGL((svd_epoch_hybrid_kernel<E, D, WB == 5, true>), dim3(pl->n_blocks), dim3(256), 0, s,
@@ -892,13 +895,13 @@ static void launch_fast_t(rs_svd_plan* pl, float lr, float reg, hipStream_t s, f
                                pl->items.p, pl->ratings.p, pl->P.p, pl->Q.p, q_bytes, pl->gb.p,
                                pl->partial.p, lr, reg, d, multi ? pl->uw.p : nullptr, multi ? 0 : 1,
                                pl->trace.n ? pl->trace.p : nullptr, pl->live_meta.p, pl->n_live, pl->qlast.p,
-                               pl->done.p, pl->k);
+                               pl->done.p, pl->k, 1.f);
         } else {
             hipLaunchKernelGGL((svd_epoch_hybrid_kernel<E, D, WB == 5, false>), dim3(pl->n_blocks), dim3(256), 0, s,
                                pl->wk_user.p, pl->wk_rng.p, pl->wk_frac.p, pl->n_work, pl->n_heavy,
                                pl->items.p, pl->ratings.p, pl->P.p, pl->Q.p, q_bytes, pl->gb.p,
                                pl->partial.p, lr, reg, d, multi ? pl->uw.p : nullptr, multi ? 0 : 1,
-                               pl->trace.n ? pl->trace.p : nullptr, nullptr, 0, nullptr, nullptr, pl->k);
+                               pl->trace.n ? pl->trace.p : nullptr, nullptr, 0, nullptr, nullptr, pl->k, 1.f);
         }
     } else {
         hipLaunchKernelGGL((svd_epoch_fast_kernel<E, D, WB>), dim3(pl->n_blocks), dim3(256), 0, s,
@@ -939,9 +942,9 @@ static void launch_fast(rs_svd_plan* pl, float lr, float reg, hipStream_t s, flo
         }
         const int64_t qn = static_cast<int64_t>(pl->Q.n);
         const int fx_blocks = static_cast<int>(std::min<int64_t>(2048, (qn + 255) / 256));
-        hipLaunchKernelGGL(svd_q_fixed_kernel, dim3(fx_blocks), dim3(256), 0, s, pl->Q.p, qn, 1, numflag(pl));
+        hipLaunchKernelGGL(svd_q_fixed_kernel, dim3(fx_blocks), dim3(256), 0, s, pl->Q.p, qn, 1, numflag(pl), pl->fx_shift);
         tile_launch(pl, lr, reg, s, dP);
-        hipLaunchKernelGGL(svd_q_fixed_kernel, dim3(fx_blocks), dim3(256), 0, s, pl->Q.p, qn, 0, numflag(pl));
+        hipLaunchKernelGGL(svd_q_fixed_kernel, dim3(fx_blocks), dim3(256), 0, s, pl->Q.p, qn, 0, numflag(pl), pl->fx_shift);
         RS_HIP(hipGetLastError());
         return;
     }
@@ -953,7 +956,7 @@ static void launch_fast(rs_svd_plan* pl, float lr, float reg, hipStream_t s, flo
     const bool fx = pl->fixed_q && pl->write_back == RS_SGD_WB_ATOMIC;
     const int64_t qn = static_cast<int64_t>(pl->Q.n);
     const int fx_blocks = static_cast<int>(std::min<int64_t>(2048, (qn + 255) / 256));
-    if (fx) hipLaunchKernelGGL(svd_q_fixed_kernel, dim3(fx_blocks), dim3(256), 0, s, pl->Q.p, qn, 1, numflag(pl));
+    if (fx) hipLaunchKernelGGL(svd_q_fixed_kernel, dim3(fx_blocks), dim3(256), 0, s, pl->Q.p, qn, 1, numflag(pl), pl->fx_shift);
     if (pl->n_live > 0)  // L = the live items' rows at the epoch start (a bit copy: int32 rows too)
         hipLaunchKernelGGL(svd_live_merge_kernel, dim3(pl->n_live), dim3(64), 0, s, pl->Q.p, pl->live_meta.p,
                            pl->qlast.p, pl->ld, 0);
@@ -969,7 +972,7 @@ static void launch_fast(rs_svd_plan* pl, float lr, float reg, hipStream_t s, flo
                                reinterpret_cast<int32_t*>(pl->qlast.p), pl->ld);
             pl->live_merged = true;
         }
-        hipLaunchKernelGGL(svd_q_fixed_kernel, dim3(fx_blocks), dim3(256), 0, s, pl->Q.p, qn, 0, numflag(pl));
+        hipLaunchKernelGGL(svd_q_fixed_kernel, dim3(fx_blocks), dim3(256), 0, s, pl->Q.p, qn, 0, numflag(pl), pl->fx_shift);
     }
     RS_HIP(hipGetLastError());
 }
@@ -1001,7 +1004,7 @@ void q_convert(rs_svd_plan* pl, hipStream_t s, int32_t to_fixed) {
     const int64_t qn = static_cast<int64_t>(pl->Q.n);
     if (qn == 0) return;
     const int fx_blocks = static_cast<int>(std::min<int64_t>(2048, (qn + 255) / 256));
-    hipLaunchKernelGGL(svd_q_fixed_kernel, dim3(fx_blocks), dim3(256), 0, s, pl->Q.p, qn, to_fixed, numflag(pl));
+    hipLaunchKernelGGL(svd_q_fixed_kernel, dim3(fx_blocks), dim3(256), 0, s, pl->Q.p, qn, to_fixed, numflag(pl), pl->fx_shift);
     RS_HIP(hipGetLastError());
 }
 
@@ -1267,9 +1270,15 @@ static void plan_build_csr(rs_ctx* ctx, int32_t n_users, int32_t n_items, UserCS
     pl->ld = fast_ld(k);
     pl->nnz = static_cast<int64_t>(csr.cols.size());
     {
-        double sum = 0.0;
-        for (float v : csr.vals) sum += v;
+        double sum = 0.0, lo = 0.0, hi = 0.0;
+        for (size_t t = 0; t < csr.vals.size(); ++t) {
+            const double v = csr.vals[t];
+            sum += v;
+            lo = t == 0 ? v : std::min(lo, v);
+            hi = t == 0 ? v : std::max(hi, v);
+        }
         pl->mean_rating = pl->nnz > 0 ? sum / static_cast<double>(pl->nnz) : 0.0;
+        pl->fx_shift = fx_shift_for(lo, hi, pl->mean_rating);  // the fixed-point scale follows the ratings
     }
     pl->h_rowptr = std::move(csr.rowptr);
     pl->h_cols = std::move(csr.cols);
@@ -1314,11 +1323,30 @@ static void plan_build_coo_device(rs_ctx* ctx, const rs_ratings* r, int32_t k, r
     int32_t* su = reinterpret_cast<int32_t*>(st);
     int32_t* si = su + n;
     float* sv = reinterpret_cast<float*>(si + n);
+    std::mutex mx;
+    double lo = 0.0, hi = 0.0, sum = 0.0;
+    bool any = false;
     parallel_ranges(r->nnz, 16, [&](int64_t b, int64_t e) {
         std::memcpy(su + b, r->users + b, static_cast<size_t>(e - b) * 4);
         std::memcpy(si + b, r->items + b, static_cast<size_t>(e - b) * 4);
-        for (int64_t t = b; t < e; ++t) sv[t] = static_cast<float>(r->ratings[t]);
+        double l = 0.0, h = 0.0, sm = 0.0;
+        for (int64_t t = b; t < e; ++t) {
+            const double v = r->ratings[t];
+            sv[t] = static_cast<float>(v);
+            l = t == b ? v : std::min(l, v);
+            h = t == b ? v : std::max(h, v);
+            sm += v;
+        }
+        if (e > b) {
+            std::lock_guard<std::mutex> g(mx);
+            lo = any ? std::min(lo, l) : l;
+            hi = any ? std::max(hi, h) : h;
+            sum += sm;
+            any = true;
+        }
     });
+    // the fixed-point scale follows the ratings' spread (fx_shift_for); the mean only places the range
+    pl->fx_shift = fx_shift_for(lo, hi, r->nnz > 0 ? sum / static_cast<double>(r->nnz) : 0.0);
     // (buffers recycled from the previous Fit's plan are kept where large enough; P and Q must fit exactly)
     if (pl->coo_users.n < n) pl->coo_users.alloc(n);
     if (pl->coo_items.n < n) pl->coo_items.alloc(n);
@@ -1487,7 +1515,7 @@ static void plan_finish_fit(rs_svd_plan* pl, double* P, double* Q, double* bu, d
     });
     if (flag) {
         plan_clear_flag(pl);
-        throw NumericError{"item factors left the fixed-point range (non-finite or |q| >= 128) during "
+        throw NumericError{"item factors left the fixed-point range (non-finite or |q| >= 2^(31 - shift)) during "
                            "an epoch; the returned model is not trustworthy"};
     }
 }
@@ -1612,15 +1640,15 @@ static void plan_download(rs_svd_plan* pl, double* P, double* Q, double* bu, dou
         if (f) {
             RS_HIP(hipMemsetAsync(pl->numflag.p, 0, sizeof(int32_t), s));
             RS_HIP(hipStreamSynchronize(s));
-            throw NumericError{"item factors left the fixed-point range (non-finite or |q| >= 128) during "
+            throw NumericError{"item factors left the fixed-point range (non-finite or |q| >= 2^(31 - shift)) during "
                                "an epoch; the returned model is not trustworthy"};
         }
     }
 }
 
-// rows with an entry at or past `bound` (or non-finite): flag.  The guard scans P and Q at 32 -- a quarter of
-// the fixed-point range, far past any trained factor or bias on star ratings -- so a run-away row is caught
-// while the call can still be redone from a sane start
+// rows with an entry at or past `bound` (or non-finite): flag.  The guard scans P and Q at a quarter of the
+// plan's fixed-point range (32 on star ratings; the range follows the ratings' spread, fx_shift_for), far past
+// any trained factor or bias, so a run-away row is caught while the call can still be redone from a sane start
 __global__ __launch_bounds__(256) void range_kernel(const float* __restrict__ P, int64_t np, const float* __restrict__ Q,
                                                    int64_t nq, float bound, int32_t* __restrict__ flag) {
     bool bad = false;
@@ -1629,6 +1657,25 @@ __global__ __launch_bounds__(256) void range_kernel(const float* __restrict__ P,
     if (bad) flag[0] = 1;
 }
 
+// every P and Q entry finite and below the plan's guard bound (one launch, one readback; the stream is synced)
+bool plan_range_ok(rs_svd_plan* pl) {
+    plan_sync_last(pl);
+    hipStream_t s = pl->ctx->stream;
+    if (!pl->guard_flag.p) pl->guard_flag.alloc(1);
+    RS_HIP(hipMemsetAsync(pl->guard_flag.p, 0, sizeof(int32_t), s));
+    const int64_t pn = static_cast<int64_t>(pl->P.n), qn = static_cast<int64_t>(pl->Q.n);
+    hipLaunchKernelGGL(range_kernel, dim3(static_cast<int>(std::max<int64_t>(1, std::min<int64_t>(1024, (pn + qn + 255) / 256)))),
+                       dim3(256), 0, s, pl->P.p, pn, pl->Q.p, qn, pl->guard_bound(), pl->guard_flag.p);
+    RS_HIP(hipGetLastError());
+    int32_t f = 0;
+    pl->guard_flag.download(&f, 1, s);
+    RS_HIP(hipStreamSynchronize(s));
+    if (f) {
+        RS_HIP(hipMemsetAsync(pl->guard_flag.p, 0, sizeof(int32_t), s));
+        RS_HIP(hipStreamSynchronize(s));
+    }
+    return f == 0;
+}
 
 static void plan_epochs_once(rs_svd_plan* pl, int32_t epochs, float lr, float reg, hipStream_t s) {
     const double inv_nnz = pl->nnz > 0 ? 1.0 / static_cast<double>(pl->nnz) : 0.0;
@@ -1649,7 +1696,7 @@ static void plan_epochs_once(rs_svd_plan* pl, int32_t epochs, float lr, float re
     const int64_t qn = static_cast<int64_t>(pl->Q.n);
     const int fx_blocks = static_cast<int>(std::min<int64_t>(2048, (qn + 255) / 256));
     if (hoist) {
-        hipLaunchKernelGGL(svd_q_fixed_kernel, dim3(fx_blocks), dim3(256), 0, s, pl->Q.p, qn, 1, numflag(pl));
+        hipLaunchKernelGGL(svd_q_fixed_kernel, dim3(fx_blocks), dim3(256), 0, s, pl->Q.p, qn, 1, numflag(pl), pl->fx_shift);
         if (!tile && pl->n_live > 0) {
             hipLaunchKernelGGL(svd_live_merge_kernel, dim3(pl->n_live), dim3(64), 0, s, pl->Q.p, pl->live_meta.p,
                                pl->qlast.p, pl->ld, 0);
@@ -1679,7 +1726,7 @@ static void plan_epochs_once(rs_svd_plan* pl, int32_t epochs, float lr, float re
             RS_HIP(hipGetLastError());
         }
         pl->hoisted = false;
-        hipLaunchKernelGGL(svd_q_fixed_kernel, dim3(fx_blocks), dim3(256), 0, s, pl->Q.p, qn, 0, numflag(pl));
+        hipLaunchKernelGGL(svd_q_fixed_kernel, dim3(fx_blocks), dim3(256), 0, s, pl->Q.p, qn, 0, numflag(pl), pl->fx_shift);
         RS_HIP(hipGetLastError());
         RS_HIP(hipEventRecord(pl->ev1, s));
         pl->last_launches = pl->timing ? epochs : 2 * epochs;  // SGD + epilogue (conversions in the span)
@@ -1709,8 +1756,9 @@ static void plan_epochs_once(rs_svd_plan* pl, int32_t epochs, float lr, float re
 // the run cap: the automatic cap would grow as the grid shrinks) halves that staleness.  So a call's epochs are checked once, at the end (the Q conversion's range flag, a P range
 // scan, a finite GlobalBias: one small readback), and a call that failed is redone from its start state --
 // P, Q and GlobalBias copied on the device before the first epoch -- on a quarter of the workgroups, up to three
-// times; the plan keeps the smaller grid and cap.  Only then does the caller see the flag (RS_ERR_NUMERIC at
-// download).  `under` is host work run while the first attempt's kernels execute.
+// times; the plan keeps the smaller grid and cap where a hard signal (range flag, non-finite) fired or soft redos
+// keep coming (see the end of the loop).  Only then does the caller see the flag (RS_ERR_NUMERIC at download).
+// `under` is host work run while the first attempt's kernels execute.
 static void plan_epochs(rs_svd_plan* pl, int32_t epochs, float lr, float reg, hipStream_t s,
                         const std::function<void()>& under = nullptr, const std::function<void()>& after = nullptr) {
     // `after` enqueues the caller's follow-up copies (rs_svd_fit: the results' download) before the guard's wait
@@ -1743,11 +1791,13 @@ static void plan_epochs(rs_svd_plan* pl, int32_t epochs, float lr, float reg, hi
     };
     thread_local Check ck;
     int32_t* flag = numflag(pl);
+    bool hard = false;  // a hard signal (the fixed-point range flag, a non-finite GlobalBias) in this call
+    const int32_t wg0 = pl->tile_wg, cap0 = pl->tile_run_cap;
     for (int attempt = 0;; ++attempt) {
         plan_epochs_once(pl, epochs, lr, reg, s);
         const int64_t pn = static_cast<int64_t>(pl->P.n), qn = static_cast<int64_t>(pl->Q.n);
         hipLaunchKernelGGL(range_kernel, dim3(static_cast<int>(std::min<int64_t>(1024, (pn + qn + 255) / 256))), dim3(256), 0, s,
-                           pl->P.p, pn, pl->Q.p, qn, 32.0f, pl->guard_flag.p);
+                           pl->P.p, pn, pl->Q.p, qn, pl->guard_bound(), pl->guard_flag.p);
         RS_HIP(hipGetLastError());
         RS_HIP(hipMemcpyAsync(ck.p, pl->gb.p, sizeof(double), hipMemcpyDeviceToHost, s));
         RS_HIP(hipMemcpyAsync(ck.p + 1, flag, sizeof(int32_t), hipMemcpyDeviceToHost, s));
@@ -1759,9 +1809,23 @@ static void plan_epochs(rs_svd_plan* pl, int32_t epochs, float lr, float reg, hi
         double g;
         std::memcpy(&g, ck.p, 8);
         const int32_t* fl = reinterpret_cast<const int32_t*>(ck.p + 1);
-        const bool bad = fl[0] != 0 || fl[1] != 0 || !std::isfinite(g);
+        const bool bad_hard = fl[0] != 0 || !std::isfinite(g), bad = bad_hard || fl[1] != 0;
+        hard = hard || bad_hard;
         RS_HIP(hipMemsetAsync(pl->guard_flag.p, 0, sizeof(int32_t), s));  // (the guard's own signal is never an error)
-        if (!bad || attempt == 3 || pl->tile_grid <= 1) return;  // (a range flag still raised reaches the download)
+        if (!bad || attempt == 3 || pl->tile_grid <= 1) {  // (a range flag still raised reaches the download)
+            // Redos that only the guard's own signals asked for (a rising loss, a factor past the guard bound) may
+            // be false positives: the plan returns to the caller's grid and cap for its next call (rebuilt here)
+            // instead of keeping a quarter of the workgroups for good -- until such redos have come three times,
+            // or a hard signal (range flag, non-finite) came in this call, when the smaller grid stays.
+            if (attempt > 0 && !bad && !hard && ++pl->soft_refits < 3 &&
+                (pl->tile_wg != wg0 || pl->tile_run_cap != cap0)) {
+                pl->tile_wg = wg0;
+                pl->tile_run_cap = cap0;
+                tile_build(pl);
+                pl->n_blocks = tile_partials(pl);
+            }
+            return;
+        }
         RS_HIP(hipMemsetAsync(flag, 0, sizeof(int32_t), s));
         RS_HIP(hipMemcpyAsync(pl->P.p, pl->P_snap.p, pl->P.n * sizeof(float), hipMemcpyDeviceToDevice, s));
         RS_HIP(hipMemcpyAsync(pl->Q.p, pl->Q_snap.p, pl->Q.n * sizeof(float), hipMemcpyDeviceToDevice, s));

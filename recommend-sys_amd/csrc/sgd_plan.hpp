@@ -4,6 +4,7 @@
 
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cstdint>
 #include <functional>
 #include <stdexcept>
@@ -130,14 +131,27 @@ struct rs_svd_plan {
     rs::DevBuf<char> sched_ws;                 // its build workspace (kept for refits)
     std::function<void()> build_overlap;       // host work run (once) while the device build's kernels execute
     // divergence guard of the tile schedule (rs_svd_plan_set_guard, default on): a call's epochs that leave the
-    // fixed-point range or go non-finite are redone from the call-start state on half the workgroups
+    // fixed-point range, go non-finite, raise the training loss or pass the guard bound are redone from the
+    // call-start state on a quarter of the workgroups and half the run cap (sgd.hip plan_epochs).  Memory: the
+    // snapshot is a second resident copy of P and Q (allocated on a guarded plan's first call), and every
+    // guarded call ends in one small readback the host waits for.
     int32_t guard = 1;
     int32_t refits = 0;                        // redone calls so far (rs_svd_plan_refits)
     rs::DevBuf<float> P_snap, Q_snap;          // the call-start state (allocated on first use)
     rs::DevBuf<double> gb_snap;                // {GlobalBias, loss state} at the call start
     rs::DevBuf<float> loss_part;               // per (workgroup, wave): sum of (lr diff)^2 of the last epoch
     rs::DevBuf<double> loss_state;             // last epoch's training MSE (0: none since the factors were set)
-    rs::DevBuf<int32_t> guard_flag;            // the guard's own signals (a rising loss, |p| or |q| >= 32): redo, not an error
+    rs::DevBuf<int32_t> guard_flag;            // the guard's own signals (a rising loss, |p| or |q| >= guard bound): redo, not an error
+    int32_t soft_refits = 0;                   // redos the guard's own signals alone asked for (the grid is restored after them)
+    int32_t grid_wg0 = -1, grid_cap0 = -1;     // the caller's tile_wg / tile_run_cap before a soft redo shrank them
+    // Fixed-point scale of the FAST schedules: P / Q values are held as int32 round(v * 2^fx_shift)
+    // while a call runs, so |v| < 2^(31 - fx_shift).  The shift follows the ratings (fx_shift_for): 24 (|v| < 128)
+    // on star scales, fewer bits of fraction where the biases must reach further (1-100 ratings: 20, |v| < 2048).
+    int32_t fx_shift = 24;
+    float fx() const { return static_cast<float>(1u << fx_shift); }
+    float fx_inv() const { return 1.f / fx(); }
+    float fx_range() const { return static_cast<float>(1u << (31 - fx_shift)); }  // |v| must stay below
+    float guard_bound() const { return fx_range() / 4.f; }                        // the guard's range scan
     ~rs_svd_plan() {
         if (ev0) (void)hipEventDestroy(ev0);
         if (ev1) (void)hipEventDestroy(ev1);
@@ -148,8 +162,18 @@ struct rs_svd_plan {
 namespace rs {
 constexpr int32_t kOutOfRange = 0x7FFFFFF0;  // buffer offset past num_records: load 0 / drop store
 constexpr int kSgdAux = 16;                  // sc1
-// Fixed-point rows (2^-24 resolution, |v| < 128): see sgd.hip
-constexpr float kFx = 16777216.f, kFxInv = 1.f / 16777216.f;
+// Fixed-point rows: 2^-fx_shift resolution, |v| < 2^(31 - fx_shift); fx_shift from the ratings (below)
+// The plan's fixed-point shift for ratings in [lo, hi] with mean m: a bias moves a rating by at most about
+// d = max(hi - m, m - lo) and a factor product by less, so the range is 32 U with U = 2^ceil(log2(max(d, 4))):
+// 2^-24 resolution and |v| < 128 on star scales (d <= 4, as before round 5), 2^-20 / 2048 for 1-100 ratings.
+// The guard's range scan sits at a quarter of that (8 U: 32 on stars).
+inline int32_t fx_shift_for(double lo, double hi, double mean) {
+    const double d = std::max({hi - mean, mean - lo, 4.0});
+    if (!(d < 1e30)) return 8;
+    int32_t lg = 0;
+    while (lg < 16 && static_cast<double>(int64_t{1} << lg) < d) ++lg;
+    return std::max(8, std::min(24, 26 - lg));
+}
 
 // Sum over the 64 lanes of a wave: DPP inside each 16-lane row, then the gfx950 permlane swaps
 // across rows.  Every lane ends with the bitwise-identical total.
@@ -162,13 +186,13 @@ __device__ __forceinline__ float wave_sum(float x) {
 }
 
 // Fixed-point item rows (rs_svd_plan_set_fixed_q): during a hybrid FAST epoch Q holds
-// round(q * 2^24) as int32 and the q_i deltas are integer atomics.  Measured on gfx950
+// round(q * 2^s) as int32 (s = the plan's fx_shift) and the q_i deltas are integer atomics.  Measured on gfx950
 // (scripts/experiments/exp_atomics.hip, exp_atomics2.hip): memory-side u32 atomic adds sustain 1.69 TB/s of
-// added bytes against 1.32 TB/s for f32 -- and the epoch is bound by that rate.  The resolution
-// 2^-24 is the fp32 ulp at |q| in [0.5, 1); the range is |q| < 128 (v_cvt_i32_f32 saturates).
+// added bytes against 1.32 TB/s for f32 -- and the epoch is bound by that rate.  At s = 24 (star ratings) the
+// resolution 2^-24 is the fp32 ulp at |q| in [0.5, 1); the range is |q| < 2^(31-s) (v_cvt_i32_f32 saturates).
 // Integer adds are exact and associative, so the sum of the deltas no longer depends on their order.
-__device__ __forceinline__ float fx_to_f(uint32_t bits) { return static_cast<float>(static_cast<int32_t>(bits)) * kFxInv; }
-__device__ __forceinline__ int32_t fx_delta(float qn, float q) { return __float2int_rn((qn - q) * kFx); }
+__device__ __forceinline__ float fx_to_f(uint32_t bits, float fx_inv) { return static_cast<float>(static_cast<int32_t>(bits)) * fx_inv; }
+__device__ __forceinline__ int32_t fx_delta(float qn, float q, float fx) { return __float2int_rn((qn - q) * fx); }
 
 // Row layout of the FAST plan: lane l's register x holds column l + 64 x, except lane 63's last
 // register, which holds the bias in column kf (right after the kf factors).  The other lanes of the
@@ -203,6 +227,7 @@ inline int32_t buffer_bytes32(size_t elems, size_t elem_size, const char* what) 
 // sgd.hip
 int32_t fast_ld(int32_t k);            // row stride of the FAST plans (k factors + bias, 64-float lines)
 void plan_sync_last(rs_svd_plan* pl);  // waits for the stream of the last enqueued epochs
+bool plan_range_ok(rs_svd_plan* pl);   // P and Q finite and below the guard bound (syncs the stream)
 int32_t* numflag(rs_svd_plan* pl);  // the RS_ERR_NUMERIC device flag (allocated on first use)
 void q_convert(rs_svd_plan* pl, hipStream_t s, int32_t to_fixed);  // Q <-> int32 fixed point in place
 void gb_sum(const double* partial, int64_t n, double* out, hipStream_t s);  // fixed-order sum

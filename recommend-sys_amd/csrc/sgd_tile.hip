@@ -11,7 +11,7 @@
 //
 //   * Users are cut into TILES (consecutive users, about nnz / #CUs ratings each, bounded by the
 //     LDS).  One workgroup of NW waves owns a tile at a time: its P rows are staged into LDS as
-//     int32 fixed point round(p * 2^24) and every p_u update is a ds_add_u32 of the rounded delta --
+//     int32 fixed point round(p * 2^S) and every p_u update is a ds_add_u32 of the rounded delta --
 //     exact and order-free, so the NW waves share the rows without locks (Hogwild inside the CU, no
 //     update lost).  Tiles hold disjoint users, so P needs no cross-CU coherence at all.
 //   * The tile's ratings are grouped into RUNS, one per item (the item's ratings by the tile's
@@ -96,7 +96,7 @@ __global__ __launch_bounds__(NW * 64) void svd_epoch_tile_kernel(
     const int4* __restrict__ tiles, int32_t n_tiles, const int2* __restrict__ tile_users,
     const int32_t* __restrict__ streams, const int2* __restrict__ runs, const int2* __restrict__ recs,
     float* __restrict__ P, int32_t* Q, int32_t q_bytes, const double* __restrict__ gb_in,
-    double* __restrict__ gb_partial, float* __restrict__ loss_partial, float lr, float reg, float* __restrict__ dP,
+    double* __restrict__ gb_partial, float* __restrict__ loss_partial, float lr, float reg, float fx, float* __restrict__ dP,
     const float* __restrict__ uw, float* __restrict__ dPs, int32_t kf, int32_t ldm, int32_t ldd,
     int64_t* __restrict__ dbg) {
 #pragma clang fp contract(fast)
@@ -104,6 +104,9 @@ __global__ __launch_bounds__(NW * 64) void svd_epoch_tile_kernel(
     constexpr bool TIMED = (DIAG & 16) != 0;  // per-wave phase clocks into dbg (experiments)
     constexpr bool SPAN = (DIAG & 32) != 0;   // per-wave start / end clocks only (no extra waits)
     static_assert(CH == 0 || (CH > RQ && CH >= 2 && CH < 64), "a claimed chunk must outlast the ring");
+    // the chunk loop steps the ring RQ runs at a time: a ring that does not divide the chunk would train
+    // runs of the next chunk here (the wave that claims it trains them again) and misalign the slots
+    static_assert(CH == 0 || CH % RQ == 0, "a claimed chunk must be a whole number of ring turns");
     int64_t tm_stage = 0, tm_ring = 0, tm_loop = 0, tm_tail = 0, tm_c = 0;
     auto clk = [] { return static_cast<int64_t>(__builtin_amdgcn_s_memtime()); };
     static_assert(2 * E * RQ <= 60, "ring loads and atomics must fit the 63-op vmcnt");
@@ -114,7 +117,7 @@ __global__ __launch_bounds__(NW * 64) void svd_epoch_tile_kernel(
     const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
     const __amdgpu_buffer_rsrc_t rq = __builtin_amdgcn_make_buffer_rsrc(Q, 0, q_bytes, 0x00020000);
     const double gb0 = gb_in[0];
-    const float a = 1.f - lr * reg, am1 = -lr * reg;
+    const float a = 1.f - lr * reg, am1 = -lr * reg, fx_inv = 1.f / fx;
     // per register: global byte offset of this lane's Q element in a row (-1: none), constant lanes
     int32_t qoff[E];
     bool qone[E], pone[E];
@@ -176,8 +179,8 @@ __global__ __launch_bounds__(NW * 64) void svd_epoch_tile_kernel(
         for (int32_t x = tid; x < nu * LD; x += NT) {
             const int32_t ul = x / LD, c = x - ul * LD;
             int32_t v = 0;
-            if (c <= kf) v = __float2int_rn(P[static_cast<int64_t>(tile_users[tm.x + ul].x) * ldm + c] * kFx);
-            else if (c == kf + 1) v = 1 << 24;
+            if (c <= kf) v = __float2int_rn(P[static_cast<int64_t>(tile_users[tm.x + ul].x) * ldm + c] * fx);
+            else if (c == kf + 1) v = static_cast<int32_t>(fx);
             Pl[x] = v;
         }
         for (int32_t x = tid; x < n_rec; x += NT) Rl[x] = recs[tm.w + x];
@@ -200,7 +203,7 @@ __global__ __launch_bounds__(NW * 64) void svd_epoch_tile_kernel(
             rw1 = Rl[min(rb + 64 + lane, n_rec - 1)];
         };
         double gb = gb0;
-        const float klr = lr * kFxInv * kFxInv;  // c = lr (s 2^-48 + gb - r): p and q in 2^-24 units
+        const float klr = lr * fx_inv * fx_inv;  // c = lr (s 2^-2S + gb - r): p and q in 2^-S units (S: the plan's shift)
         // One run: its q_i row comes out of ring slot `slot`, which is refilled with the row of `next`;
         // records [j, e) are trained in order with q_i in registers, then the run's delta goes to memory.
         auto run = [&](int32_t (&slot)[E], int32_t item, int32_t e, int32_t next) {
@@ -214,7 +217,7 @@ __global__ __launch_bounds__(NW * 64) void svd_epoch_tile_kernel(
                 // coalesced copy would keep both live and the compiler would rotate the ring with
                 // moves at the loop back edge, waiting for every load in flight there)
                 asm volatile("v_mov_b32 %0, %1" : "=v"(q0[x]) : "v"(slot[x]));
-                q[x] = qone[x] ? kFx : static_cast<float>(q0[x]);  // q in 2^-24 units too
+                q[x] = qone[x] ? fx : static_cast<float>(q0[x]);  // q in 2^-S units too
             }
             if constexpr (TIMED) {
                 asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // (timed variant only) honest split
@@ -235,7 +238,7 @@ __global__ __launch_bounds__(NW * 64) void svd_epoch_tile_kernel(
                 const int32_t ul = __builtin_amdgcn_readlane(rw0.x, o);
                 const float rt = __int_as_float(__builtin_amdgcn_readlane(rw0.y, o));
                 int32_t* prow = Pl + ul * LD + lane;
-                float pu[E];  // p in 2^-24 units
+                float pu[E];  // p in 2^-S units
 #pragma unroll
                 for (int x = 0; x < E; ++x)
                     pu[x] = (DIAG & 8) ? 1e5f * ul : static_cast<float>(prow[64 * x]);
@@ -261,7 +264,7 @@ __global__ __launch_bounds__(NW * 64) void svd_epoch_tile_kernel(
                 float pn[E];
 #pragma unroll
                 for (int x = 0; x + 1 < E + 1; x += 2) {
-                    if (x + 1 < E) {  // d = (a - 1) p - c q in 2^-24 units; p_new = p + d
+                    if (x + 1 < E) {  // d = (a - 1) p - c q in 2^-S units; p_new = p + d
                         const f2 pv = {pu[x], pu[x + 1]}, qv = {q[x], q[x + 1]};
                         f2 d = __builtin_elementwise_fma(qv, f2{-c, -c}, pv * f2{am1, am1});
                         if (pone[x]) d.x = 0.f;  // P's constant column stays 1 (b_i's partner)
@@ -280,7 +283,7 @@ __global__ __launch_bounds__(NW * 64) void svd_epoch_tile_kernel(
                 }
 #pragma unroll
                 for (int x = 0; x < E; ++x) {
-                    if (qone[x]) q[x] = kFx;
+                    if (qone[x]) q[x] = fx;
                     const int32_t di = cvt_rpi(pn[x]);
                     if (!(DIAG & 4))
                         __hip_atomic_fetch_add(prow + 64 * x, di, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
@@ -378,7 +381,7 @@ __global__ __launch_bounds__(NW * 64) void svd_epoch_tile_kernel(
             const int2 te = tile_users[tm.x + ul];  // {user, frac bits}
             const float frac = __int_as_float(te.y);
             const int64_t g = static_cast<int64_t>(te.x) * ldm + c;
-            const float v = fx_to_f(static_cast<uint32_t>(Pl[x]));
+            const float v = fx_to_f(static_cast<uint32_t>(Pl[x]), fx_inv);
             if (dP) {  // multi-GPU delta mode: dP rows of stride ldd
                 const float d = uw[te.x] * frac * (v - P[g]);
                 const int64_t gd = static_cast<int64_t>(te.x) * ldd + c;
@@ -1189,7 +1192,7 @@ static void tile_launch_t(rs_svd_plan* pl, float lr, float reg, hipStream_t s, f
     hipLaunchKernelGGL(kern, dim3(tr.grid), dim3(NW * 64), pl->tile_lds, s, pl->t_tiles.p + tr.t0, tr.t1 - tr.t0,
                        pl->t_users.p, pl->t_streams.p + static_cast<int64_t>(tr.t0) * (NW + 1), pl->t_runs.p,
                        pl->t_recs.p, pl->P.p, reinterpret_cast<int32_t*>(pl->Q.p), q_bytes, pl->gb.p, pl->partial.p,
-                       pl->loss_part.n >= pl->partial.n ? pl->loss_part.p : nullptr, lr, reg, dP, dP ? pl->uw.p : nullptr, pl->dPs.p, pl->k, pl->ld, tr.ldd, pl->trace.p);
+                       pl->loss_part.n >= pl->partial.n ? pl->loss_part.p : nullptr, lr, reg, pl->fx(), dP, dP ? pl->uw.p : nullptr, pl->dPs.p, pl->k, pl->ld, tr.ldd, pl->trace.p);
 }
 
 // q_i rows in flight per wave (runs ahead): the ring's loads and the runs' atomics share the wave's
@@ -1220,12 +1223,13 @@ static void tile_launch_r(rs_svd_plan* pl, float lr, float reg, hipStream_t s, f
             default: break;
         }
     }
-    if (claim) {  // chunks of 8 runs and rings of 3 are instantiated for the bench's rows (E <= 2) only
+    if (claim) {  // chunks of 8 runs and the 4-deep ring are instantiated for the bench's rows (E <= 2) only
         if constexpr (E <= 2) {
-            const bool big = pl->tile_claim >= 8;
-            if (want <= 2) return big ? tile_launch_t<E, NW, 2, 8>(pl, lr, reg, s, dP, tr)
-                                      : tile_launch_t<E, NW, 2, 4>(pl, lr, reg, s, dP, tr);
-            return big ? tile_launch_t<E, NW, 3, 8>(pl, lr, reg, s, dP, tr) : tile_launch_t<E, NW, 3, 4>(pl, lr, reg, s, dP, tr);
+            // the ring must divide the chunk (static_assert in the kernel): a ring of 3 or more runs with
+            // claims takes the 4-deep ring on chunks of 8
+            if (want >= 3) return tile_launch_t<E, NW, 4, 8>(pl, lr, reg, s, dP, tr);
+            return pl->tile_claim >= 8 ? tile_launch_t<E, NW, 2, 8>(pl, lr, reg, s, dP, tr)
+                                       : tile_launch_t<E, NW, 2, 4>(pl, lr, reg, s, dP, tr);
         } else {
             return tile_launch_t<E, NW, 2, 4>(pl, lr, reg, s, dP, tr);
         }

@@ -59,17 +59,17 @@ __device__ __forceinline__ int32_t pp_roff(int32_t row, int x, int32_t lane4, in
 }
 
 // Fixed-point Q and Y (FX, the default; RSGPU_PP_FX=0 keeps fp32): the FAST fit packs Q and Y as
-// int32 round(v * 2^24) on the host and unpacks them after the last epoch; loads convert to fp32 and
+// int32 round(v * 2^S) on the host and unpacks them after the last epoch; loads convert to fp32 and
 // the q_i / y_j deltas become integer atomics (memory-side u32 adds at 1.69 TB/s against 1.32 for
-// f32, K1).  Resolution 2^-24 (the fp32 ulp at |v| in [0.5, 1)), |v| < 128.
-constexpr float kPPFx = 16777216.f, kPPFxInv = 1.f / 16777216.f;
-__device__ __forceinline__ float pp_ld(uint32_t bits, bool fx) {
-    return fx ? static_cast<float>(static_cast<int32_t>(bits)) * kPPFxInv : __uint_as_float(bits);
+// f32, K1).  S follows the ratings (fx_shift_for, sgd_plan.hpp): 24 on star scales (resolution 2^-24,
+// the fp32 ulp at |v| in [0.5, 1), |v| < 128), fewer where the biases reach further (|v| < 2^(31-S)).
+__device__ __forceinline__ float pp_ld(uint32_t bits, bool fx, float fx_inv) {
+    return fx ? static_cast<float>(static_cast<int32_t>(bits)) * fx_inv : __uint_as_float(bits);
 }
 template <bool FX>
-__device__ __forceinline__ void pp_atomic_add(float d, __amdgpu_buffer_rsrc_t r, int32_t off) {
+__device__ __forceinline__ void pp_atomic_add(float d, __amdgpu_buffer_rsrc_t r, int32_t off, float fx) {
     if constexpr (FX)
-        __builtin_amdgcn_raw_ptr_buffer_atomic_add_i32(__float2int_rn(d * kPPFx), r, off, 0, 0);
+        __builtin_amdgcn_raw_ptr_buffer_atomic_add_i32(__float2int_rn(d * fx), r, off, 0, 0);
     else
         __builtin_amdgcn_raw_ptr_buffer_atomic_fadd_f32(d, r, off, 0, 0);
 }
@@ -86,7 +86,7 @@ __device__ __forceinline__ float pp_lane63(float x) {
 template <int E, int YB, bool FX>
 __device__ __forceinline__ void pp_sum_y(__amdgpu_buffer_rsrc_t ry, const int32_t* __restrict__ items,
                                          int64_t b, int64_t e, int32_t first, int32_t step, int32_t lane4,
-                                         int32_t lcy, float (&S0)[E]) {
+                                         int32_t lcy, float (&S0)[E], float fx) {
     constexpr int LD = 64 * E;
 #pragma unroll
     for (int x = 0; x < E; ++x) S0[x] = 0.f;
@@ -98,7 +98,7 @@ __device__ __forceinline__ void pp_sum_y(__amdgpu_buffer_rsrc_t ry, const int32_
             const int32_t row = j < rem ? items[base + j] * (LD * 4) : kPPOut;
 #pragma unroll
             for (int x = 0; x < E; ++x)
-                yv[j][x] = pp_ld(__builtin_amdgcn_raw_buffer_load_b32(ry, pp_roff<E>(row, x, lane4, lcy), 0, kPPAux), FX);
+                yv[j][x] = pp_ld(__builtin_amdgcn_raw_buffer_load_b32(ry, pp_roff<E>(row, x, lane4, lcy), 0, kPPAux), FX, 1.f / fx);
         }
 #pragma unroll
         for (int j = 0; j < YB; ++j)
@@ -111,7 +111,7 @@ __device__ __forceinline__ void pp_sum_y(__amdgpu_buffer_rsrc_t ry, const int32_
 template <int E, int YB, bool FX>
 __device__ __forceinline__ void pp_update_y(__amdgpu_buffer_rsrc_t ry, const int32_t* __restrict__ items,
                                             int64_t b, int64_t e, int32_t first, int32_t step,
-                                            int32_t lane4, int32_t lcy, float am1, const float (&Cv)[E]) {
+                                            int32_t lane4, int32_t lcy, float am1, const float (&Cv)[E], float fx) {
     constexpr int LD = 64 * E;
     for (int64_t base = b + first; base < e; base += step) {
         const int32_t rem = static_cast<int32_t>(e - base);
@@ -122,13 +122,13 @@ __device__ __forceinline__ void pp_update_y(__amdgpu_buffer_rsrc_t ry, const int
             rows[j] = j < rem ? items[base + j] * (LD * 4) : kPPOut;
 #pragma unroll
             for (int x = 0; x < E; ++x)
-                yv[j][x] = pp_ld(__builtin_amdgcn_raw_buffer_load_b32(ry, pp_roff<E>(rows[j], x, lane4, lcy), 0, kPPAux), FX);
+                yv[j][x] = pp_ld(__builtin_amdgcn_raw_buffer_load_b32(ry, pp_roff<E>(rows[j], x, lane4, lcy), 0, kPPAux), FX, 1.f / fx);
         }
 #pragma unroll
         for (int j = 0; j < YB; ++j)
 #pragma unroll
             for (int x = 0; x < E; ++x)
-                pp_atomic_add<FX>(__builtin_fmaf(am1, yv[j][x], -Cv[x]), ry, pp_roff<E>(rows[j], x, lane4, lcy));
+                pp_atomic_add<FX>(__builtin_fmaf(am1, yv[j][x], -Cv[x]), ry, pp_roff<E>(rows[j], x, lane4, lcy), fx);
     }
 }
 
@@ -139,7 +139,7 @@ template <int E, int D, bool FX, class Emit>
 __device__ __forceinline__ void pp_chain(__amdgpu_buffer_rsrc_t rq, const int32_t* __restrict__ items,
                                          const float* __restrict__ ratings, int64_t b, int64_t e,
                                          int32_t lane, int32_t lcq, float lr, float a, const float (&S0)[E], float (&p)[E],
-                                         float& ub, float& gb, float& A, float (&Cv)[E], Emit&& emit) {
+                                         float& ub, float& gb, float& A, float (&Cv)[E], float fx, Emit&& emit) {
 #pragma clang fp contract(fast)
     constexpr int LD = 64 * E, B = 16;
     static_assert(B % D == 0, "ring depth must divide the 16-rating batch");
@@ -148,11 +148,12 @@ __device__ __forceinline__ void pp_chain(__amdgpu_buffer_rsrc_t rq, const int32_
     const int32_t deg = static_cast<int32_t>(e - b);
     const float nf = static_cast<float>(deg);
     const float rsq = 1.f / sqrtf(nf);  // the chain multiplies by 1/sqrt|N(u)| (no divide per rating)
+    const float fx_inv = 1.f / fx;
     auto load_rowq = [&](float (&q)[E], int32_t valid, int32_t item) {
         const int32_t row = valid ? item * (LD * 4) : kPPOut;
 #pragma unroll
         for (int x = 0; x < E; ++x)
-            q[x] = pp_ld(__builtin_amdgcn_raw_buffer_load_b32(rq, pp_roff<E>(row, x, lane4, lcq), 0, kPPAux), FX);
+            q[x] = pp_ld(__builtin_amdgcn_raw_buffer_load_b32(rq, pp_roff<E>(row, x, lane4, lcq), 0, kPPAux), FX, fx_inv);
     };
     int32_t it_cur[B], it_nxt[B];
 #pragma unroll
@@ -237,7 +238,7 @@ __global__ __launch_bounds__(256) void svdpp_epoch_fast_kernel(
     const int64_t* __restrict__ rowptr,
     const int32_t* __restrict__ items, const float* __restrict__ ratings, float* __restrict__ P,
     float* Q, float* Y, int32_t row_bytes_q, int32_t row_bytes_y, const double* __restrict__ gb_in,
-    double* __restrict__ gb_partial, float lr, float reg, int32_t kf) {
+    double* __restrict__ gb_partial, float lr, float reg, int32_t kf, float fx) {
 #pragma clang fp contract(fast)
     constexpr int LD = 64 * E;
     constexpr int YB = 8;  // y rows per pass-1/3 batch (24 was measured to break the FAST RMSE on ML-100K)
@@ -273,16 +274,16 @@ __global__ __launch_bounds__(256) void svdpp_epoch_fast_kernel(
             float ub = pp_lane63(p[E - 1]);
             float gb = gb0, A = 1.f;
             float S0[E], Cv[E];
-            pp_sum_y<E, YB, FX>(ry, items, b, e, 0, YB, lane4, lcy, S0);
+            pp_sum_y<E, YB, FX>(ry, items, b, e, 0, YB, lane4, lcy, S0, fx);
 #pragma unroll
             for (int x = 0; x < E; ++x) Cv[x] = 0.f;
-            pp_chain<E, D, FX>(rq, items, ratings, b, e, lane, lcq, lr, a, S0, p, ub, gb, A, Cv,
+            pp_chain<E, D, FX>(rq, items, ratings, b, e, lane, lcq, lr, a, S0, p, ub, gb, A, Cv, fx,
                                [&](int32_t row, const float (&qw)[E], const float (&q)[E]) {
 #pragma unroll
                                    for (int x = 0; x < E; ++x)
-                                       pp_atomic_add<FX>(qw[x] - q[x], rq, pp_roff<E>(row, x, lane4, lcq));
+                                       pp_atomic_add<FX>(qw[x] - q[x], rq, pp_roff<E>(row, x, lane4, lcq), fx);
                                });
-            pp_update_y<E, YB, FX>(ry, items, b, e, 0, YB, lane4, lcy, A - 1.f, Cv);
+            pp_update_y<E, YB, FX>(ry, items, b, e, 0, YB, lane4, lcy, A - 1.f, Cv, fx);
 #pragma unroll
             for (int x = 0; x < E; ++x)
                 if (pcol(x) >= 0) prow[pcol(x)] = p[x];
@@ -307,7 +308,7 @@ __global__ __launch_bounds__(256) void svdpp_epoch_fast_kernel(
         // pass 1 split over the four waves, the partial sums added in wave order (identical everywhere)
         {
             float S0w[E];
-            pp_sum_y<E, YB, FX>(ry, items, b, e, wib * YB, 4 * YB, lane4, lcy, S0w);
+            pp_sum_y<E, YB, FX>(ry, items, b, e, wib * YB, 4 * YB, lane4, lcy, S0w, fx);
 #pragma unroll
             for (int x = 0; x < E; ++x) s_red[wib][lane + 64 * x] = S0w[x];
         }
@@ -327,7 +328,7 @@ __global__ __launch_bounds__(256) void svdpp_epoch_fast_kernel(
             float ub = pp_lane63(p[E - 1]);
             float gb = gb0, A = 1.f;
             int32_t tail = 0, free_end = R;
-            pp_chain<E, DH, FX>(rq, items, ratings, b, e, lane, lcq, lr, a, S0, p, ub, gb, A, Cv,
+            pp_chain<E, DH, FX>(rq, items, ratings, b, e, lane, lcq, lr, a, S0, p, ub, gb, A, Cv, fx,
                             [&](int32_t row, const float (&qw)[E], const float (&q)[E]) {
                                 if (tail >= free_end) {  // ring full: wait for the writers
                                     for (;;) {
@@ -378,7 +379,7 @@ __global__ __launch_bounds__(256) void svdpp_epoch_fast_kernel(
                                 const int32_t row = __builtin_amdgcn_readlane(myrow, j);
 #pragma unroll
                                 for (int x = 0; x < E; ++x)
-                                    pp_atomic_add<FX>(v[j][x], rq, pp_roff<E>(row, x, lane4, lcq));
+                                    pp_atomic_add<FX>(v[j][x], rq, pp_roff<E>(row, x, lane4, lcq), fx);
                             }
                         }
                         next += NW * n;
@@ -397,7 +398,7 @@ __global__ __launch_bounds__(256) void svdpp_epoch_fast_kernel(
             float C[E];
 #pragma unroll
             for (int x = 0; x < E; ++x) C[x] = s_red[0][lane + 64 * x];
-            pp_update_y<E, YB, FX>(ry, items, b, e, wib * YB, 4 * YB, lane4, lcy, s_A - 1.f, C);
+            pp_update_y<E, YB, FX>(ry, items, b, e, wib * YB, 4 * YB, lane4, lcy, s_A - 1.f, C, fx);
         }
         __syncthreads();  // s_red, s_A and the ring are reset by the next user
     }
@@ -492,34 +493,48 @@ __global__ __launch_bounds__(NT) void svdpp_ordered_kernel(
     if (f == 0) gb_io[0] = gb;
 }
 
-// fixed point (FX): the fp32 value v stored as int32 round(v * 2^24), saturating like v_cvt_i32_f32
-static float pp_host_fx(float v) {
-    const double t = std::nearbyint(static_cast<double>(v) * 16777216.0);
+// fixed point (FX): the fp32 value v stored as int32 round(v * 2^shift), saturating like v_cvt_i32_f32
+static float pp_host_fx(float v, int32_t shift) {
+    const double t = std::nearbyint(static_cast<double>(v) * std::ldexp(1.0, shift));
     const int32_t i = t >= 2147483647.0 ? INT32_MAX : (t <= -2147483648.0 ? INT32_MIN : static_cast<int32_t>(t));
     float out;
     std::memcpy(&out, &i, 4);
     return out;
 }
-static float pp_host_unfx(float bits) {
+static float pp_host_unfx(float bits, int32_t shift) {
     int32_t i;
     std::memcpy(&i, &bits, 4);
-    return static_cast<float>(i) * (1.f / 16777216.f);
+    return static_cast<float>(i) * std::ldexp(1.f, -shift);
+}
+// a fixed-point word within 1/2 of the int32 range (integer atomics may have wrapped), or a non-finite float
+static bool pp_out_of_range(const std::vector<float>& v, bool fx, int32_t shift) {
+    const int32_t lim = static_cast<int32_t>(0x80000000u - (1u << (shift - 1)));
+    for (float x : v) {
+        if (fx) {
+            int32_t i;
+            std::memcpy(&i, &x, 4);
+            if (i >= lim || i <= -lim) return true;
+        } else if (!std::isfinite(x)) {
+            return true;
+        }
+    }
+    return false;
 }
 
 static void pack_bias_rows(const double* F, const double* bias, int64_t rows, int32_t k, int32_t ld,
-                           std::vector<float>& dst, bool fx = false) {
+                           std::vector<float>& dst, bool fx = false, int32_t shift = 24) {
     dst.assign(static_cast<size_t>(rows) * ld, 0.f);
     for (int64_t r = 0; r < rows; ++r) {
         for (int32_t f = 0; f < k; ++f) dst[r * ld + f] = static_cast<float>(F[r * k + f]);
         if (bias) dst[r * ld + k] = static_cast<float>(bias[r]);  // bias column k
     }
     if (fx)
-        for (float& v : dst) v = pp_host_fx(v);
+        for (float& v : dst) v = pp_host_fx(v, shift);
 }
 
 static void unpack_bias_rows(const std::vector<float>& src, int64_t rows, int32_t k, int32_t ld,
-                             double* F, double* bias, bool fx = false) {
-    auto v = [&](int64_t x) { return fx ? pp_host_unfx(src[x]) : src[x]; };
+                             double* F, double* bias, bool fx = false, int32_t shift = 24) {
+    auto v = [&](int64_t x) { return fx ? pp_host_unfx(src[x], shift) : src[x]; };
     for (int64_t r = 0; r < rows; ++r) {
         for (int32_t f = 0; f < k; ++f) F[r * k + f] = v(r * ld + f);
         if (bias) bias[r] = v(r * ld + k);
@@ -531,13 +546,13 @@ static void launch_pp_fast(int32_t n_blocks, const DevBuf<int32_t>& work, int32_
                            const DevBuf<int64_t>& rowptr, const DevBuf<int32_t>& items,
                            const DevBuf<float>& ratings, DevBuf<float>& P, DevBuf<float>& Q,
                            DevBuf<float>& Y, DevBuf<double>& gb, DevBuf<double>& partial, float lr,
-                           float reg, int32_t kf, bool fx, hipStream_t s) {
+                           float reg, int32_t kf, bool fx, int32_t shift, hipStream_t s) {
     // light ring depth 8: 16 and 32 measured slower (1.33 / 1.34 against 1.28 ms per ML-1M epoch, k = 128)
     auto kern = fx ? svdpp_epoch_fast_kernel<E, 8, true> : svdpp_epoch_fast_kernel<E, 8, false>;
     hipLaunchKernelGGL(kern, dim3(n_blocks), dim3(256), 0, s, work.p,
                        n_work, n_heavy, n_hblocks, rowptr.p, items.p, ratings.p, P.p, Q.p, Y.p,
                        rs::buffer_bytes32(Q.n, 4, "item factor matrix"), rs::buffer_bytes32(Y.n, 4, "implicit factor matrix"), gb.p,
-                       partial.p, lr, reg, kf);
+                       partial.p, lr, reg, kf, std::ldexp(1.f, shift));
 }
 
 }  // namespace rs
@@ -661,9 +676,18 @@ extern "C" int rs_svdpp_fit(rs_ctx* ctx, const rs_ratings* r, const rs_sgd_param
         std::vector<float> hP, hQ, hY;
         bool fx = true;  // fixed-point Q and Y (see pp_ld); RSGPU_PP_FX=0: fp32 float atomics
         if (const char* env = std::getenv("RSGPU_PP_FX")) fx = std::atoi(env) != 0;
+        // the fixed-point scale from the ratings' spread (fx_shift_for, sgd_plan.hpp: 2^-24 on star scales)
+        double lo = 0.0, hi = 0.0, sum = 0.0;
+        for (int64_t t = 0; t < r->nnz; ++t) {
+            const double v = r->ratings[t];
+            lo = t == 0 ? v : std::min(lo, v);
+            hi = t == 0 ? v : std::max(hi, v);
+            sum += v;
+        }
+        const int32_t shift = rs::fx_shift_for(lo, hi, r->nnz > 0 ? sum / static_cast<double>(r->nnz) : 0.0);
         rs::pack_bias_rows(P, bu, r->n_users, k, ld, hP);
-        rs::pack_bias_rows(Q, bi, r->n_items, k, ld, hQ, fx);
-        rs::pack_bias_rows(Y, nullptr, r->n_items, k, ld, hY, fx);
+        rs::pack_bias_rows(Q, bi, r->n_items, k, ld, hQ, fx, shift);
+        rs::pack_bias_rows(Y, nullptr, r->n_items, k, ld, hY, fx, shift);
         rs::DevBuf<float> dP(std::max<size_t>(1, hP.size())), dQ(std::max<size_t>(1, hQ.size())),
             dY(std::max<size_t>(1, hY.size()));
         rs::DevBuf<double> dpart(n_blocks);
@@ -675,14 +699,14 @@ extern "C" int rs_svdpp_fit(rs_ctx* ctx, const rs_ratings* r, const rs_sgd_param
         rs::kernel_span_begin(ctx);
         for (int32_t ep = 0; ep < p->n_epochs; ++ep) {
             switch (E) {
-                case 1: rs::launch_pp_fast<1>(n_blocks, dwork, n_work, n_heavy, n_hblocks, drow, dcol, dval, dP, dQ, dY, dgb, dpart, lr, reg, k, fx, s); break;
-                case 2: rs::launch_pp_fast<2>(n_blocks, dwork, n_work, n_heavy, n_hblocks, drow, dcol, dval, dP, dQ, dY, dgb, dpart, lr, reg, k, fx, s); break;
-                case 3: rs::launch_pp_fast<3>(n_blocks, dwork, n_work, n_heavy, n_hblocks, drow, dcol, dval, dP, dQ, dY, dgb, dpart, lr, reg, k, fx, s); break;
-                case 4: rs::launch_pp_fast<4>(n_blocks, dwork, n_work, n_heavy, n_hblocks, drow, dcol, dval, dP, dQ, dY, dgb, dpart, lr, reg, k, fx, s); break;
-                case 5: rs::launch_pp_fast<5>(n_blocks, dwork, n_work, n_heavy, n_hblocks, drow, dcol, dval, dP, dQ, dY, dgb, dpart, lr, reg, k, fx, s); break;
-                case 6: rs::launch_pp_fast<6>(n_blocks, dwork, n_work, n_heavy, n_hblocks, drow, dcol, dval, dP, dQ, dY, dgb, dpart, lr, reg, k, fx, s); break;
-                case 7: rs::launch_pp_fast<7>(n_blocks, dwork, n_work, n_heavy, n_hblocks, drow, dcol, dval, dP, dQ, dY, dgb, dpart, lr, reg, k, fx, s); break;
-                default: rs::launch_pp_fast<8>(n_blocks, dwork, n_work, n_heavy, n_hblocks, drow, dcol, dval, dP, dQ, dY, dgb, dpart, lr, reg, k, fx, s); break;
+                case 1: rs::launch_pp_fast<1>(n_blocks, dwork, n_work, n_heavy, n_hblocks, drow, dcol, dval, dP, dQ, dY, dgb, dpart, lr, reg, k, fx, shift, s); break;
+                case 2: rs::launch_pp_fast<2>(n_blocks, dwork, n_work, n_heavy, n_hblocks, drow, dcol, dval, dP, dQ, dY, dgb, dpart, lr, reg, k, fx, shift, s); break;
+                case 3: rs::launch_pp_fast<3>(n_blocks, dwork, n_work, n_heavy, n_hblocks, drow, dcol, dval, dP, dQ, dY, dgb, dpart, lr, reg, k, fx, shift, s); break;
+                case 4: rs::launch_pp_fast<4>(n_blocks, dwork, n_work, n_heavy, n_hblocks, drow, dcol, dval, dP, dQ, dY, dgb, dpart, lr, reg, k, fx, shift, s); break;
+                case 5: rs::launch_pp_fast<5>(n_blocks, dwork, n_work, n_heavy, n_hblocks, drow, dcol, dval, dP, dQ, dY, dgb, dpart, lr, reg, k, fx, shift, s); break;
+                case 6: rs::launch_pp_fast<6>(n_blocks, dwork, n_work, n_heavy, n_hblocks, drow, dcol, dval, dP, dQ, dY, dgb, dpart, lr, reg, k, fx, shift, s); break;
+                case 7: rs::launch_pp_fast<7>(n_blocks, dwork, n_work, n_heavy, n_hblocks, drow, dcol, dval, dP, dQ, dY, dgb, dpart, lr, reg, k, fx, shift, s); break;
+                default: rs::launch_pp_fast<8>(n_blocks, dwork, n_work, n_heavy, n_hblocks, drow, dcol, dval, dP, dQ, dY, dgb, dpart, lr, reg, k, fx, shift, s); break;
             }
             RS_HIP(hipGetLastError());
             hipLaunchKernelGGL(rs::pp_gb_fold_kernel, dim3(1), dim3(256), 0, s, dpart.p,
@@ -696,8 +720,12 @@ extern "C" int rs_svdpp_fit(rs_ctx* ctx, const rs_ratings* r, const rs_sgd_param
         dgb.download(gb, 1, s);
         RS_HIP(hipStreamSynchronize(s));
         rs::unpack_bias_rows(hP, r->n_users, k, ld, P, bu);
-        rs::unpack_bias_rows(hQ, r->n_items, k, ld, Q, bi, fx);
-        rs::unpack_bias_rows(hY, r->n_items, k, ld, Y, nullptr, fx);
+        rs::unpack_bias_rows(hQ, r->n_items, k, ld, Q, bi, fx, shift);
+        rs::unpack_bias_rows(hY, r->n_items, k, ld, Y, nullptr, fx, shift);
+        if (rs::pp_out_of_range(hQ, fx, shift) || rs::pp_out_of_range(hY, fx, shift) || rs::pp_out_of_range(hP, false, shift) ||
+            !std::isfinite(*gb))
+            return rs::set_error(ctx, RS_ERR_NUMERIC, "SVD++ factors left the fixed-point range (or went non-finite) "
+                                                      "during the fit; the returned model is not trustworthy");
         return RS_OK;
     });
 }

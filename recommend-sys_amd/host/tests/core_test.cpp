@@ -9,9 +9,12 @@
 //
 // usage: core_test [--cpu-only] <ml-100k u.data path>
 //   --cpu-only runs only the host tests (no device is opened).
+#include <algorithm>
 #include <cmath>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
+#include <random>
 #include <functional>
 #include <numeric>
 #include <set>
@@ -168,6 +171,80 @@ int main(int argc, char** argv) {
         for (int f = 0; f < 8; ++f) dotpq += s->UserFactor[0][f] * s->ItemFactor[0][f];
         const double want = s->GlobalBias + s->UserBias[0] + s->ItemBias[0] + dotpq;
         CHECK(p == want && s->Predict(-5, data.Items[0]) == s->GlobalBias + s->ItemBias[0]);
+    });
+    run("TestCgoRatingsShape", [&] {
+        // go/core/gpu.go newCRatings / cr.free(): the rs_ratings struct and its three arrays are malloc'd
+        // separately, filled from the TrainSet (train-set order, inner ids, data.go:131-154) and freed once
+        // the call has returned; the ctx is opened per Fit and closed before it returns.  The library must
+        // not keep a pointer into them: after the first fit the arrays are poisoned and freed, and a second
+        // fit on the same ctx (its plan cache compares the ratings) from fresh copies gives the same ORDERED
+        // model bit for bit.  A FAST fit from a third copy trains.
+        std::vector<int64_t> idx(20000);
+        std::iota(idx.begin(), idx.end(), 0);
+        const TrainSet t = NewTrainSet(data.SubSet(idx));
+        auto c_ratings = [&t]() {
+            const int64_t n = t.Length(), m = std::max<int64_t>(n, 1);
+            auto* r = static_cast<rs_ratings*>(std::malloc(sizeof(rs_ratings)));
+            auto* users = static_cast<int32_t*>(std::malloc(static_cast<size_t>(m) * 4));
+            auto* items = static_cast<int32_t*>(std::malloc(static_cast<size_t>(m) * 4));
+            auto* vals = static_cast<double*>(std::malloc(static_cast<size_t>(m) * 8));
+            CHECK(r && users && items && vals);
+            for (int64_t k = 0; k < n; ++k) {
+                users[k] = t.ConvertUserID(t.Users[k]);
+                items[k] = t.ConvertItemID(t.Items[k]);
+                vals[k] = t.Ratings[k];
+            }
+            r->nnz = n;
+            r->n_users = t.UserCount;
+            r->n_items = t.ItemCount;
+            r->users = users;
+            r->items = items;
+            r->ratings = vals;
+            return r;
+        };
+        auto c_free = [&t](rs_ratings* r) {  // poisoned first: a retained pointer would read garbage
+            const size_t m = static_cast<size_t>(std::max<int64_t>(t.Length(), 1));
+            std::memset(const_cast<int32_t*>(r->users), 0xff, m * 4);
+            std::memset(const_cast<int32_t*>(r->items), 0x7f, m * 4);
+            std::memset(const_cast<double*>(r->ratings), 0xff, m * 8);
+            std::free(const_cast<int32_t*>(r->users));
+            std::free(const_cast<int32_t*>(r->items));
+            std::free(const_cast<double*>(r->ratings));
+            std::free(r);
+        };
+        const int k = 16;
+        std::mt19937_64 g(11);
+        std::normal_distribution<double> nd(0.0, 0.1);
+        std::vector<double> P0(static_cast<size_t>(t.UserCount) * k), Q0(static_cast<size_t>(t.ItemCount) * k);
+        for (double& v : P0) v = nd(g);
+        for (double& v : Q0) v = nd(g);
+        struct Model { std::vector<double> P, Q, bu, bi; double gb = 0; };
+        auto fit = [&](rs_ctx* ctx, int32_t mode, int32_t epochs) {
+            Model m{P0, Q0, std::vector<double>(t.UserCount), std::vector<double>(t.ItemCount), 0.0};
+            rs_sgd_params p{k, epochs, 0.005, 0.02, mode, RS_SGD_WB_TILE};
+            rs_ratings* r = c_ratings();
+            const int rc = rs_svd_fit(ctx, r, &p, m.P.data(), m.Q.data(), m.bu.data(), m.bi.data(), &m.gb);
+            c_free(r);
+            if (rc != RS_OK) throw std::runtime_error(std::string("rs_svd_fit: ") + rs_last_error(ctx));
+            return m;
+        };
+        rs_ctx* ctx = nullptr;
+        CHECK(rs_open(0, &ctx) == RS_OK);
+        Model a, b, f;
+        try {
+            a = fit(ctx, RS_SGD_ORDERED, 2);
+            b = fit(ctx, RS_SGD_ORDERED, 2);
+            f = fit(ctx, RS_SGD_FAST, 5);
+        } catch (...) {
+            rs_close(ctx);
+            throw;
+        }
+        rs_close(ctx);
+        CHECK(a.P == b.P && a.Q == b.Q && a.bu == b.bu && a.bi == b.bi && a.gb == b.gb);
+        bool finite = std::isfinite(f.gb);
+        for (const auto* v : {&f.P, &f.Q, &f.bu, &f.bi})
+            for (double x : *v) finite = finite && std::isfinite(x);
+        CHECK(finite && f.P != P0);
     });
     std::printf("%d/%d passed\n", g_run - g_failed, g_run);
     return g_failed ? 1 : 0;

@@ -48,7 +48,7 @@ HEADER_SYMBOLS = (
     "rs_svd_plan_set_user_blocks", "rs_svd_group_create", "rs_svd_group_epochs", "rs_svd_group_destroy",
     "rs_item_shards", "rs_svd_fit_multi", "rs_tile_schedule_host", "rs_svd_plan_set_exchange",
     "rs_comm_info", "rs_rotation_step", "rs_svd_plan_shard_info", "rs_svd_plan_inject_fault",
-    "rs_svd_plan_time_blocks", "rs_knn_plan_set_tie_order", "rs_fit_refits",
+    "rs_svd_plan_time_blocks", "rs_knn_plan_set_tie_order", "rs_fit_refits", "rs_fit_multi_refits",
     "rs_svd_plan_set_hot_split",
 )
 COMM_ID_BYTES = 128
@@ -178,6 +178,7 @@ def lib():
             "rs_svd_plan_time_blocks": (C.c_int, [_vp, _flt, _flt, _vp, _i32]),
             "rs_knn_plan_set_tie_order": (C.c_int, [_vp, _i32]),
             "rs_fit_refits": (C.c_int, [_vp, C.POINTER(_i32)]),
+            "rs_fit_multi_refits": (C.c_int, [C.POINTER(_i32)]),
             "rs_svd_plan_set_hot_split": (C.c_int, [_vp, _dbl, _i64, _i32]),
             "rs_comm_info": (C.c_int, [C.POINTER(_i32), _vp, _i32]),
             "rs_rotation_step": (C.c_int, [_i32, _i32, _i32, _vp]),
@@ -335,7 +336,7 @@ class Context:
     # ---- estimators --------------------------------------------------------------------------
 
     def fit_refits(self):
-        """Divergence refits (half the workgroups each) the last svd_fit made (rs_fit_refits)."""
+        """Divergence refits (a quarter of the workgroups each) the last svd_fit made (rs_fit_refits)."""
         n = _i32(0)
         self.check(lib().rs_fit_refits(self.h, C.byref(n)))
         return n.value
@@ -774,6 +775,13 @@ def svd_fit_multi(devices, r: "Ratings", P, Q, bu=None, bi=None, gb=0.0, n_epoch
     _check(lib().rs_svd_fit_multi(_ptr(dev), len(dev), C.byref(rc), C.byref(prm), n_blocks, _ptr(P), _ptr(Q),
                                   _ptr(bu), _ptr(bi), _ptr(g)))
     return P, Q, bu, bi, float(g[0])
+
+
+def fit_multi_refits():
+    """Refits of this thread's last svd_fit_multi (rs_fit_multi_refits)."""
+    n = _i32(0)
+    _check(lib().rs_fit_multi_refits(C.byref(n)))
+    return n.value
 
 
 def svd_predict(users, items, P, Q, bu, bi, gb):

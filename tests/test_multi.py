@@ -431,3 +431,134 @@ def test_rs_item_shards_balanced_ranges():
         cum = np.concatenate([[0], np.cumsum(np.bincount(items, minlength=ni))])
         for r in range(1, n):
             assert b[r] == np.searchsorted(cum, len(items) * r // n, side="left")
+
+
+# ---- ROTATE_Q (the exchange rs_svd_fit_multi picks at configs[4]): user ranges stay, item blocks rotate -------
+# Host model of epochs_rotate(RS_EXCHANGE_ROTATE_Q) (csrc/multi.hip; rules restated in tests/rotq_model.py) on
+# world_size 2 and 3 over gloo: the library's rs_rotation_step schedule, Q item blocks plus their hot copies by
+# isend/irecv, the hot copies' summed moves all-reduced and merged with RS_HOT_SCALED's weights, the GlobalBias
+# partials all-reduced, the item rank-blocks and P ranges broadcast at the end.  Checked against the
+# single-process sequential run over the strata (rotq_model.sequential).  tests/test_multi_gpu.py checks the
+# same sequential model against the library's in-process group on one GPU (1e-5).
+
+RQ_PIECES, RQ_HOT = 2, 0.05
+
+
+def _rq_data():
+    rng = np.random.default_rng(11)
+    nu, ni, nnz = 60, 50, 1400
+    pop = 1.0 / np.arange(1, ni + 1) ** 1.1  # a Zipf head, so that hot items exist
+    pairs = set()
+    while len(pairs) < nnz:
+        pairs.add((int(rng.integers(0, nu)), int(rng.choice(ni, p=pop / pop.sum()))))
+    pairs = sorted(pairs, key=lambda _: rng.random())
+    u = np.array([a for a, _ in pairs], np.int32)
+    i = np.array([b for _, b in pairs], np.int32)
+    return u, i, rng.integers(1, 6, nnz).astype(float), nu, ni
+
+
+def _rq_setup(world):
+    import rotq_model as RQ
+    u, i, r, nu, ni = _rq_data()
+    rng = np.random.default_rng(6)
+    P0, Q0 = rng.normal(0, 0.1, (nu, K)), rng.normal(0, 0.1, (ni, K))
+    lay = RQ.Layout(u, i, ni, world, RQ_PIECES, hot_share=RQ_HOT, min_stratum=0)
+    ub = RQ.block_bounds(u, nu, world)  # the ranks' user ranges (rs_svd_fit_multi's user_block_bounds)
+    return RQ, u, i, r, nu, ni, P0, Q0, lay, ub
+
+
+def _rq_works(RQ, lay, u, i, r, ub):
+    def works(g, b):
+        m = (u >= ub[g]) & (u < ub[g + 1])
+        return [RQ.stratum_csr(lay, u[m], i[m], r[m], b)]
+    return works
+
+
+def _rq_worker(rank, world, port, out):
+    import rsgpu
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    RQ, u, i, r, nu, ni, P0, Q0, lay, ub = _rq_setup(world)
+    works = _rq_works(RQ, lay, u, i, r, ub)
+    h, nb, H = lay.h, lay.nb, lay.H
+    P, bu = P0.copy(), np.zeros(nu)
+    Q = np.zeros((lay.rows(), K))
+    Q[:ni] = Q0
+    bi = np.zeros(lay.rows())
+    lay.seed(Q, bi)
+    gb = 3.0
+
+    def block_rows(rb):  # item rows of rank-block rb, then its blocks' copy rows
+        a, z = lay.ib[rb * h], lay.ib[rb * h + h]
+        rows = list(range(a, z)) + [lay.copy_row(b, x) for b in range(rb * h, rb * h + h) for x in range(H)]
+        return np.array(rows, np.int64)
+
+    for _ in range(EPOCHS):
+        part = 0.0
+        for st in range(world):
+            train, send_to, recv, recv_from = rsgpu.rotation_step(rank, world, st)
+            for j in range(h):
+                P, Q, bu, bi, p = RQ.train_works(P, Q, bu, bi, gb, works(rank, train * h + j))
+                part += p
+            out_rows, in_rows = block_rows(train), block_rows(recv)
+            blk = torch.from_numpy(np.concatenate([Q[out_rows], bi[out_rows, None]], 1).copy())
+            inc = torch.zeros((len(in_rows), K + 1), dtype=torch.float64)
+            for q in [dist.isend(blk, send_to), dist.irecv(inc, recv_from)]:
+                q.wait()
+            Q[in_rows], bi[in_rows] = inc[:, :K].numpy(), inc[:, K].numpy()
+        if H:  # rank g holds item rank-block g again: its copies' moves, summed over the ranks
+            t = torch.from_numpy(lay.partial(Q, bi, rank * h, rank * h + h))
+            dist.all_reduce(t)
+            lay.write(Q, bi, t.numpy(), rank * h, rank * h + h)
+        t = torch.tensor([part], dtype=torch.float64)
+        dist.all_reduce(t)
+        gb += float(t.item()) / len(r)
+    for g in range(world):  # item rank-block g is current on rank g, P range g too
+        a, z = lay.ib[g * h], lay.ib[g * h + h]
+        blk = torch.from_numpy(np.concatenate([Q[a:z], bi[a:z, None]], 1).copy())
+        dist.broadcast(blk, g)
+        Q[a:z], bi[a:z] = blk[:, :K].numpy(), blk[:, K].numpy()
+        pr = torch.from_numpy(np.concatenate([P[ub[g]:ub[g + 1]], bu[ub[g]:ub[g + 1], None]], 1).copy())
+        dist.broadcast(pr, g)
+        P[ub[g]:ub[g + 1]], bu[ub[g]:ub[g + 1]] = pr[:, :K].numpy(), pr[:, K].numpy()
+    out[rank] = (P, Q[:ni], bu, bi[:ni], gb, H)
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_gloo_rotation_q_matches_single_process(world):
+    port = _free_port()
+    with mp.Manager() as m:
+        out = m.dict()
+        mp.spawn(_rq_worker, args=(world, port, out), nprocs=world, join=True)
+        res = dict(out)
+    RQ, u, i, r, nu, ni, P0, Q0, lay, ub = _rq_setup(world)
+    assert lay.H >= 2 and any(c > 1 for _, c in lay.meta)  # the hot split is exercised
+    P, Q, bu, bi, gb = RQ.sequential(lay, u, i, r, nu, P0, Q0, 3.0, EPOCHS, ub, _rq_works(RQ, lay, u, i, r, ub))
+    for rank in range(world):
+        rP, rQ, rbu, rbi, rgb, H = res[rank]
+        assert H == lay.H
+        np.testing.assert_allclose(rP, P, atol=1e-12)
+        np.testing.assert_allclose(rbu, bu, atol=1e-12)
+        np.testing.assert_allclose(rQ, Q, atol=1e-12)
+        np.testing.assert_allclose(rbi, bi, atol=1e-12)
+        assert abs(rgb - gb) < 1e-12
+        for x in range(4):  # replicated bit for bit after the broadcasts
+            np.testing.assert_array_equal(res[0][x], res[rank][x])
+
+
+def test_rotation_q_layout_rules():
+    """The restated hot rules: every hot item's copies sit nb // copies blocks apart from its natural block,
+    every rating of a hot item lands on a used copy, and a copy's block is a function of the user only."""
+    import rotq_model as RQ
+    u, i, r, nu, ni = _rq_data()
+    lay = RQ.Layout(u, i, ni, 3, RQ_PIECES, hot_share=RQ_HOT, min_stratum=0)
+    assert lay.H > 0
+    for h, x in enumerate(lay.hot):
+        nat, c = lay.meta[h]
+        assert lay.ib[nat] <= x < lay.ib[nat + 1]
+        assert sum(lay.copy_used(b, h) for b in range(lay.nb)) == c
+        for a in np.unique(u[i == x]):
+            b = lay.block_of(a, x)
+            assert lay.copy_used(b, h) and b == lay.block_of(a, x)
+    assert RQ.mix32(0) == (0xE220A8397B1DCDAF >> 16) & 0xFFFFFFFF  # splitmix64(0)'s published first output

@@ -193,6 +193,59 @@ def test_rotation_q_one_wave_equals_oracle(ctx, ml100k, n_shards, pieces):
         assert all(np.array_equal(b[0][x], y[x]) for x in range(4)) and b[0][4] == y[4]
 
 
+@pytest.mark.parametrize("n_shards,pieces", [(2, 2), (3, 1)])
+def test_rotation_q_hot_copies_equal_host_model(ctx, ml100k, n_shards, pieces):
+    """ROTATE_Q with a forced hot split (share 1 %, no stratum minimum: ML-100K's head items get per-block
+    copies), in-process exchange, one wave per shard: equal (1e-5) to tests/rotq_model.py's sequential
+    model -- the same model the world-size 2 / 3 gloo run of tests/test_multi.py matches -- with every
+    stratum's ratings in the tile order the shard exports, the copies' moves merged once per epoch with
+    RS_HOT_SCALED's weights, and the replicated state bitwise identical on every shard."""
+    import rotq_model as RQ
+    f = folds(*ml100k)[2]
+    n = 30000
+    u, i, r, nu, ni = f.iu[:n], f.ii[:n], f.r[:n], f.nu, f.ni
+    k = 24
+    rng = np.random.default_rng(70 + n_shards)
+    P0, Q0 = rng.normal(0, 0.1, (nu, k)), rng.normal(0, 0.1, (ni, k))
+    ub = _block_bounds(u, nu, n_shards)
+    sh = _user_shards(u, i, r, nu, n_shards)
+    lay = RQ.Layout(u, i, ni, n_shards, pieces, hot_share=0.01, min_stratum=0)
+    assert lay.H >= 4 and any(c > 1 for _, c in lay.meta)
+    plans = []
+    for su, si, sr in sh:
+        pl = ctx.svd_plan(rsgpu.Ratings(su, si, sr, nu, ni), k)
+        pl.set_tiles(workgroups=1, waves=1)
+        pl.set_exchange(rsgpu.EXCHANGE_ROTATE_Q)
+        pl.set_hot_split(0.01, 0, 0)
+        pl.upload(P0, Q0, np.zeros(nu), np.zeros(ni), 3.5)
+        plans.append(pl)
+    g = rsgpu.SvdGroup(plans, n_blocks=n_shards * pieces)
+    g.epochs(2)
+    strata = {}  # (shard, block) -> works in the shard's visit order
+    for gi, (pl, (su, si, sr)) in enumerate(zip(plans, sh)):
+        rowptr, items, rr = O.csr_by(su, nu, si, sr)
+        cu = np.repeat(np.arange(nu, dtype=np.int32), np.diff(rowptr))
+        pos, off = pl.tile_order()
+        uu, ii, r_ = cu[pos], np.asarray(items, np.int32)[pos], np.asarray(rr)[pos]
+        for w in range(len(off) - 1):
+            a, z = off[w], off[w + 1]
+            if z == a:
+                continue
+            blk = {lay.block_of(x, y) for x, y in zip(uu[a:z], ii[a:z])}
+            assert len(blk) == 1  # a work lies in one stratum
+            b = blk.pop()
+            rows = np.array([lay.row_of(b, y) for y in ii[a:z]], np.int32)
+            strata.setdefault((gi, b), []).append((uu[a:z], rows, r_[a:z]))
+    ref = RQ.sequential(lay, u, i, r, nu, P0, Q0, 3.5, 2, ub, lambda gi, b: strata.get((gi, b), []))
+    g.close()
+    got = [pl.download() for pl in plans]
+    for pl in plans:
+        pl.close()
+    assert _maxdiff(ref[:4], got[0][:4]) <= TOL and abs(ref[4] - got[0][4]) <= TOL
+    for y in got[1:]:
+        assert all(np.array_equal(got[0][x], y[x]) for x in range(4)) and got[0][4] == y[4]
+
+
 def test_rotation_fewer_users_than_blocks(ctx):
     """ROTATE with more user blocks than users (4 shards x 2 pieces, 5 users): empty blocks send and
     receive nothing and the fit still equals a single plan's users trained (finite, every rating seen)."""

@@ -62,6 +62,30 @@ def test_one_wave_is_sequential_sgd(ctx, ml100k, k, epochs, target, run_cap):
     assert _maxdiff(ref[:4], got[:4]) <= TOL and abs(ref[4] - got[4]) <= TOL
 
 
+@pytest.mark.parametrize("claim,ring", [(4, 3), (8, 3), (8, 2), (4, 2)])
+def test_one_wave_claims_any_ring(ctx, ml100k, claim, ring):
+    """Claimed runs with every ring the API accepts (a ring of 3 runs on 4- or 8-run claims is taken
+    as the 4-deep ring on chunks of 8, which the ring divides): one wave equals the oracle in the
+    exported order (1e-5).  A ring that did not divide the chunk trained the next chunk's runs twice
+    and added q deltas to the wrong rows (advisor round 4)."""
+    f = folds(*ml100k)[0]
+    n = 12000
+    u, i, r, nu, ni = f.iu[:n], f.ii[:n], f.r[:n], f.nu, f.ni
+    k = 40
+    rng = np.random.default_rng(claim * 10 + ring)
+    P0, Q0 = rng.normal(0, 0.1, (nu, k)), rng.normal(0, 0.1, (ni, k))
+    bu0, bi0 = rng.normal(0, 0.1, nu), rng.normal(0, 0.1, ni)
+    plan = ctx.svd_plan(rsgpu.Ratings(u, i, r, nu, ni), k)
+    plan.set_tile_claim(claim)
+    plan.set_tiles(workgroups=1, waves=1, target=2500, ring=ring)
+    plan.upload(P0, Q0, bu0, bi0, 3.4)
+    plan.epochs(2)
+    got = plan.download()
+    ref = _oracle_in_tile_order(plan, u, i, r, nu, P0, Q0, bu0, bi0, 3.4, 2)
+    plan.close()
+    assert _maxdiff(ref[:4], got[:4]) <= TOL and abs(ref[4] - got[4]) <= TOL
+
+
 def _private_items(n_users=300, per_user=25, seed=4):
     rng = np.random.default_rng(seed)
     deg = rng.integers(1, 2 * per_user, n_users)
