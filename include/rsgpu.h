@@ -437,6 +437,16 @@ int rs_svd_plan_apply_delta(rs_svd_plan* plan, const void* dP, const void* gbsum
  * on every rank.  n_blocks = item blocks in all (rounded up to a multiple of n_ranks; 0 = automatic: 2..16
  * pieces of ~64 MiB of Q per rank-block).  rs_svd_fit_multi picks it when n_items < n_users. */
 #define RS_EXCHANGE_ROTATE_Q 2
+/* RS_EXCHANGE_QDELTA -- north_star's once-per-epoch all-reduce, on the smaller factor matrix (round 5; for
+ * U > I, configs[4]).  As ROTATE_Q the ranks hold user ranges (contiguous, ascending by rank) and every item;
+ * an epoch is one plain tile epoch of the rank's users against the whole Q (P in place), then ONE all-reduce
+ * of the item moves in the int32 fixed point (n_items x (k + 1); exact integer sums, identical on every rank):
+ * q_i <- q_i,start + sum over ranks of w_i (q_i,end - q_i,start), with w_i = kappa_i / c_i over the c_i ranks
+ * that rate item i, kappa_i = (1 - a^(c_i n_i)) / (1 - a^n_i), n_i = its ratings per rank, a = 1 - lr (the
+ * moves of a unit-curvature coordinate that c_i ranks each close by 1 - a^n_i, scaled to the sequential
+ * 1 - a^(c_i n_i)): exact for items of one rank, the mean of converged moves.  GlobalBias: the ranks' partials,
+ * one f64 all-reduce.  After the call the ranks' P ranges are broadcast. */
+#define RS_EXCHANGE_QDELTA 3
 int rs_svd_plan_set_exchange(rs_svd_plan* plan, int32_t mode);
 /* RS_EXCHANGE_ROTATE_Q on Zipf-headed sets: a stratum (one rank's users x one item block) holds an item's
  * ratings n_blocks-fold concentrated, so the head's rows get many concurrent runs in flight (Hogwild staleness

@@ -25,6 +25,17 @@
 // item rows per sub-epoch instead of 10M / 8 user rows).  After the call the item rank-blocks and the ranks'
 // user ranges are broadcast.
 //
+// QDELTA (round 5; north_star's once-per-epoch all-reduce, on the smaller matrix).  The ranks hold user ranges
+// (as ROTATE_Q) and every item.  An epoch is one plain tile epoch of the rank's users against the whole Q (P
+// in place: the users are exclusive), then the ranks' item moves are merged with one all-reduce: dQ_i =
+// w_i (q_i,end - q_i,start) in the int32 fixed point (an exact, order-free integer sum), every rank applies
+// q_i,start + sum.  w_i interpolates between a sum and a mean of the moves (the RS_HOT_SCALED rule over the
+// c_i ranks that rated item i: kappa / c_i, kappa = (1 - a^(c n)) / (1 - a^n), n = the item's ratings per
+// rank, a = 1 - lr): an item on one rank moves exactly as in its epoch, an item whose rank moves each
+// converged moves by their mean.  One collective per epoch of n_items x (k + 1) int32 (configs[4]: 1.03 GB)
+// instead of N transfers of 1/N of Q; the ranks' epochs are whole-set-shaped (no strata).  After the call
+// the ranks' P ranges are broadcast.
+//
 // AVERAGE (round 2's protocol, kept selectable).  Every rank trains all users against its shard in
 // delta mode from the same P; the count-weighted average of the shards' user deltas is all-reduced
 // per user block and applied.  It under-trains users split over shards (5-fold ML-100K held-out RMSE
@@ -72,6 +83,7 @@ struct LocalGroup {  // host-barrier exchange between the shards of one process
     std::vector<float*> P;    // ROTATE: every shard's P (rank-blocks are pulled from the neighbour)
     std::vector<float*> Q;    // ROTATE_Q: every shard's Q
     std::vector<float*> hot;  // ROTATE_Q: every shard's partial hot-copy averages
+    std::vector<int32_t*> dq; // QDELTA: every shard's item moves
     std::vector<int> dev;
     void barrier() {
         std::unique_lock<std::mutex> l(m);
@@ -100,6 +112,10 @@ struct ShardComm {
     std::vector<int32_t> owner;  // ROTATE_Q: the ranks' user ranges [owner[r], owner[r + 1])
     DevBuf<float> hot_part, hot_avg;  // ROTATE_Q hot copies: this rank's summed moves, over all ranks (H x ld)
     DevBuf<float> hot_w;              // merge weight per hot item
+    DevBuf<float> item_c, item_n;     // QDELTA: per item the ranks that rate it and its ratings over all ranks
+    DevBuf<int32_t> q0, dq, dq_sum;   // QDELTA: Q at the epoch start (int32 rows of ld), the moves (k + 1 wide), their sum
+    DevBuf<float> qw;                 // QDELTA: merge weight per item (for the call's lr)
+    float qw_lr = -1.f;
     ncclComm_t nccl = nullptr;
     bool own_nccl = true;
     std::atomic<bool> aborted{false};
@@ -257,6 +273,40 @@ __global__ __launch_bounds__(256) void hot_sum_kernel(Srcs src, int32_t n_src, i
     }
 }
 
+// QDELTA, after a rank's epoch: dq[i][c] = round(w_i (Q[i][c] - Q0[i][c])) for the k + 1 columns (int32 fixed
+// point rows of ld; the moves k + 1 wide), and Q back to its epoch-start value
+__global__ __launch_bounds__(256) void qdelta_moves_kernel(int32_t* __restrict__ Q, const int32_t* __restrict__ Q0,
+                                                           const float* __restrict__ w, int32_t* __restrict__ dq,
+                                                           int32_t n_items, int32_t ld, int32_t kw) {
+    const int64_t n = static_cast<int64_t>(n_items) * kw;
+    for (int64_t t = static_cast<int64_t>(blockIdx.x) * 256 + threadIdx.x; t < n; t += static_cast<int64_t>(gridDim.x) * 256) {
+        const int64_t i = t / kw;
+        const int32_t c = static_cast<int32_t>(t - i * kw);
+        const int64_t g = i * ld + c;
+        const int32_t q0 = Q0[g];
+        dq[t] = __float2int_rn(w[i] * static_cast<float>(Q[g] - q0));
+        Q[g] = q0;
+    }
+}
+// QDELTA: Q += the summed moves (int32, exact)
+__global__ __launch_bounds__(256) void qdelta_apply_kernel(int32_t* __restrict__ Q, const int32_t* __restrict__ dq,
+                                                           int32_t n_items, int32_t ld, int32_t kw) {
+    const int64_t n = static_cast<int64_t>(n_items) * kw;
+    for (int64_t t = static_cast<int64_t>(blockIdx.x) * 256 + threadIdx.x; t < n; t += static_cast<int64_t>(gridDim.x) * 256) {
+        const int64_t i = t / kw;
+        const int32_t c = static_cast<int32_t>(t - i * kw);
+        Q[i * ld + c] += dq[t];
+    }
+}
+// QDELTA, in-process exchange: out = the sum over the shards (shard order; integer, so any order) of their moves
+__global__ __launch_bounds__(256) void qdelta_sum_kernel(Srcs src, int32_t n_src, int64_t n, int32_t* __restrict__ out) {
+    for (int64_t t = static_cast<int64_t>(blockIdx.x) * 256 + threadIdx.x; t < n; t += static_cast<int64_t>(gridDim.x) * 256) {
+        int32_t a = reinterpret_cast<const int32_t*>(src.p[0])[t];
+        for (int32_t r = 1; r < n_src; ++r) a += reinterpret_cast<const int32_t*>(src.p[r])[t];
+        out[t] = a;
+    }
+}
+
 int grid_for(int64_t n) { return static_cast<int>(std::max<int64_t>(1, std::min<int64_t>(4096, (n + 255) / 256))); }
 
 int32_t auto_blocks(const rs_svd_plan* pl, int32_t nranks, int32_t ldd) {
@@ -332,13 +382,48 @@ std::pair<int64_t, int64_t> user_span(const rs_svd_plan* pl) {
 // buffers, blocks and (RCCL) the comm stream of a shard whose comm / local group is set; tot: every
 // user's ratings over all shards (ROTATE, AVERAGE: the user blocks must be the same on every shard) or
 // every item's (ROTATE_Q: the item blocks)
-void shard_setup(rs_svd_plan* pl, ShardComm& c, int32_t n_blocks, const std::vector<double>& tot) {
+void shard_setup(rs_svd_plan* pl, ShardComm& c, int32_t n_blocks, const std::vector<double>& tot,
+                 const std::vector<double>* item_ranks = nullptr) {
     if (pl->write_back != RS_SGD_WB_TILE)
         throw std::invalid_argument("the item-sharded epoch runs the tile schedule (RS_SGD_WB_TILE)");
     c.device = pl->ctx->device;
     c.ldd = round_up4(pl->k + 1);
     c.mode = pl->exchange;
     const bool rq = c.mode == RS_EXCHANGE_ROTATE_Q;
+    if (c.mode == RS_EXCHANGE_QDELTA) {  // the rank's users against every item: one plain tile schedule
+        if (!item_ranks) throw std::logic_error("QDELTA: the items' rank counts are missing");
+        // n_blocks: merges per epoch (the rank's users cut into that many blocks of near-equal ratings, the item
+        // moves all-reduced after each; 0 = 1)
+        pl->tile_ublocks = std::max(1, n_blocks);
+        pl->ublock_bounds.clear();
+        pl->iblock_bounds.clear();
+        pl->hot_items.clear();
+        const size_t ni = static_cast<size_t>(std::max(1, pl->n_items));
+        std::vector<float> cn(ni, 0.f), cc(ni, 0.f);
+        for (size_t x = 0; x < static_cast<size_t>(pl->n_items); ++x) {
+            cn[x] = static_cast<float>(tot[x]);
+            cc[x] = static_cast<float>((*item_ranks)[x]);
+        }
+        c.item_n.alloc(ni);
+        c.item_c.alloc(ni);
+        c.item_n.upload(cn.data(), ni, pl->ctx->stream);
+        c.item_c.upload(cc.data(), ni, pl->ctx->stream);
+        tile_build(pl);
+        c.pieces = static_cast<int32_t>(pl->t_block_tile.size()) - 1;  // merges per epoch
+        c.gbs.alloc(1);
+        if (c.local) c.gbs_sum.alloc(1);
+        if (c.nccl) {
+            RS_HIP(hipStreamCreateWithFlags(&c.cs, hipStreamNonBlocking));
+            RS_HIP(hipEventCreateWithFlags(&c.ev_epoch, hipEventDisableTiming));
+            RS_HIP(hipEventCreateWithFlags(&c.ev_gb, hipEventDisableTiming));
+        }
+        const size_t kw = static_cast<size_t>(pl->k) + 1;
+        c.q0.alloc(ni * static_cast<size_t>(pl->ld));
+        c.dq.alloc(ni * kw);
+        if (c.local) c.dq_sum.alloc(ni * kw);
+        RS_HIP(hipStreamSynchronize(pl->ctx->stream));
+        return;
+    }
     int32_t nbk = 0;  // blocks of the rows `tot` counts
     if (c.mode != RS_EXCHANGE_AVERAGE) {  // n_blocks: blocks in all, rounded up to whole rank-blocks
         c.pieces = n_blocks > 0 ? (n_blocks + c.nranks - 1) / c.nranks : auto_pieces(pl, c.nranks, rq);
@@ -703,15 +788,122 @@ void epochs_rotate(rs_svd_plan* pl, int32_t n_epochs, float lr, float reg, hipSt
     q_convert(pl, s, 0);
 }
 
+// QDELTA: n_epochs of the user-range epochs with one all-reduce of the item moves per epoch, on stream s
+void epochs_qdelta(rs_svd_plan* pl, int32_t n_epochs, float lr, float reg, hipStream_t s) {
+    ShardComm& c = *pl->shard;
+    const int32_t N = c.nranks, ni = pl->n_items, ld = pl->ld, kw = pl->k + 1;
+    const int64_t nq = static_cast<int64_t>(ni) * kw;
+    const double inv_total = c.total_nnz > 0 ? 1.0 / c.total_nnz : 0.0;
+    if (c.qw_lr != lr) {  // the merge weights for this lr (module header: kappa / c per item)
+        const size_t n1 = static_cast<size_t>(std::max(1, ni));
+        std::vector<float> cn(n1), cc(n1), w(n1, 1.f);
+        c.item_n.download(cn.data(), n1, s);
+        c.item_c.download(cc.data(), n1, s);
+        RS_HIP(hipStreamSynchronize(s));
+        const double a = std::max(1e-12, 1.0 - static_cast<double>(lr));
+        const double merges = static_cast<double>(std::max(1, c.pieces));  // the moves of 1 / merges of an epoch
+        for (size_t x = 0; x < static_cast<size_t>(ni); ++x) {
+            const double cp = std::max(1.0, static_cast<double>(cc[x])), n = static_cast<double>(cn[x]) / cp / merges;
+            if (cp <= 1.0 || n <= 0.0) continue;
+            const double kappa = (1.0 - std::pow(a, cp * n)) / std::max(1e-300, 1.0 - std::pow(a, n));
+            w[x] = static_cast<float>(kappa / cp);
+        }
+        if (c.qw.n < n1) c.qw.alloc(n1);
+        c.qw.upload(w.data(), n1, s);
+        RS_HIP(hipStreamSynchronize(s));  // w dies with this scope
+        c.qw_lr = lr;
+    }
+    int32_t* const Qi = reinterpret_cast<int32_t*>(pl->Q.p);
+    const int32_t nb = static_cast<int32_t>(pl->t_block_tile.size()) - 1;  // merges per epoch
+    q_convert(pl, s, 1);
+    for (int32_t e = 0; e < n_epochs * nb; ++e) {
+        const int32_t b = e % nb;
+        if (ni > 0) RS_HIP(hipMemcpyAsync(c.q0.p, Qi, static_cast<size_t>(ni) * ld * sizeof(int32_t), hipMemcpyDeviceToDevice, s));
+        const int32_t parts = tile_launch_range(pl, lr, reg, s, nullptr, 0, pl->t_block_tile[b], pl->t_block_tile[b + 1]);
+        merge_tile_split_rows(pl, pl->t_block_split[b], pl->t_block_split[b + 1], s);
+        gb_sum(pl->partial.p, parts, c.gbs.p, s);
+        if (pl->fault_sub_epoch == 0) {  // test hook (rs_svd_plan_inject_fault), once
+            pl->fault_sub_epoch = -1;
+            throw std::runtime_error("injected shard fault (rs_svd_plan_inject_fault)");
+        }
+        if (nq > 0)
+            hipLaunchKernelGGL(qdelta_moves_kernel, dim3(grid_for(nq)), dim3(256), 0, s, Qi, c.q0.p, c.qw.p, c.dq.p, ni, ld, kw);
+        RS_HIP(hipGetLastError());
+        if (c.nccl && N > 1) {
+            RS_HIP(hipEventRecord(c.ev_gb, s));
+            RS_HIP(hipStreamWaitEvent(c.cs, c.ev_gb, 0));
+            check_nccl(ncclGroupStart(), "ncclGroupStart");
+            if (nq > 0)
+                check_nccl(ncclAllReduce(c.dq.p, c.dq.p, static_cast<size_t>(nq), ncclInt32, ncclSum, c.nccl, c.cs),
+                           "ncclAllReduce(item moves)");
+            check_nccl(ncclAllReduce(c.gbs.p, c.gbs.p, 1, ncclFloat64, ncclSum, c.nccl, c.cs), "ncclAllReduce(GlobalBias)");
+            check_nccl(ncclGroupEnd(), "ncclGroupEnd");
+            if (nq > 0) hipLaunchKernelGGL(qdelta_apply_kernel, dim3(grid_for(nq)), dim3(256), 0, c.cs, Qi, c.dq.p, ni, ld, kw);
+            hipLaunchKernelGGL(gb_fold_blocks_kernel, dim3(1), dim3(64), 0, c.cs, pl->gb.p, c.gbs.p, 1, inv_total);
+            RS_HIP(hipGetLastError());
+            RS_HIP(hipEventRecord(c.ev_epoch, c.cs));
+            RS_HIP(hipStreamWaitEvent(s, c.ev_epoch, 0));  // the next epoch reads Q and the new GlobalBias
+        } else if (c.local && N > 1) {
+            LocalGroup& lg = *c.local;
+            RS_HIP(hipStreamSynchronize(s));
+            lg.barrier();  // every shard's moves and partial are in place
+            Srcs src{};
+            for (int r = 0; r < lg.n; ++r) {
+                src.p[r] = reinterpret_cast<const float4*>(lg.dq[r]);
+                src.g[r] = lg.gbs[r];
+            }
+            if (nq > 0) hipLaunchKernelGGL(qdelta_sum_kernel, dim3(grid_for(nq)), dim3(256), 0, s, src, lg.n, nq, c.dq_sum.p);
+            hipLaunchKernelGGL(local_gb_fold_kernel, dim3(1), dim3(64), 0, s, src, lg.n, 1, pl->gb.p, inv_total);
+            RS_HIP(hipGetLastError());
+            RS_HIP(hipStreamSynchronize(s));
+            lg.barrier();  // every shard has read every shard's moves: the next epoch may overwrite them
+            if (nq > 0) hipLaunchKernelGGL(qdelta_apply_kernel, dim3(grid_for(nq)), dim3(256), 0, s, Qi, c.dq_sum.p, ni, ld, kw);
+        } else {
+            if (nq > 0) hipLaunchKernelGGL(qdelta_apply_kernel, dim3(grid_for(nq)), dim3(256), 0, s, Qi, c.dq.p, ni, ld, kw);
+            hipLaunchKernelGGL(gb_fold_blocks_kernel, dim3(1), dim3(64), 0, s, pl->gb.p, c.gbs.p, 1, inv_total);
+        }
+        RS_HIP(hipGetLastError());
+    }
+    // every rank's P range is current on that rank only: broadcast them so P is replicated again
+    if (n_epochs > 0 && N > 1) {
+        if (c.nccl) {
+            RS_HIP(hipEventRecord(c.ev_gb, s));
+            RS_HIP(hipStreamWaitEvent(c.cs, c.ev_gb, 0));
+            check_nccl(ncclGroupStart(), "ncclGroupStart");
+            for (int32_t r = 0; r < N; ++r) {
+                const RowRange u = rows_of(pl, pl->P.p, c.owner[r], c.owner[r + 1]);
+                if (u.n) check_nccl(ncclBroadcast(u.p, u.p, u.n, ncclFloat32, r, c.nccl, c.cs), "ncclBroadcast(P range)");
+            }
+            check_nccl(ncclGroupEnd(), "ncclGroupEnd");
+            RS_HIP(hipEventRecord(c.ev_epoch, c.cs));
+            RS_HIP(hipStreamWaitEvent(s, c.ev_epoch, 0));
+        } else {
+            LocalGroup& lg = *c.local;
+            for (int32_t r = 0; r < N; ++r) {
+                if (r == c.rank) continue;
+                const RowRange u = rows_of(pl, pl->P.p, c.owner[r], c.owner[r + 1]);
+                if (u.n)
+                    RS_HIP(hipMemcpyPeerAsync(u.p, lg.dev[c.rank], lg.P[r] + (u.p - pl->P.p), lg.dev[r], u.n * sizeof(float), s));
+            }
+            RS_HIP(hipStreamSynchronize(s));
+            lg.barrier();  // nobody trains on (or is read from) before every shard has its copy
+        }
+    }
+    q_convert(pl, s, 0);
+}
+
 }  // namespace
 
 // n_epochs of the item-sharded schedule on stream s (every rank calls it with the same arguments)
 void epochs_sharded(rs_svd_plan* pl, int32_t n_epochs, float lr, float reg, hipStream_t s) {
     if (!pl->tiles_built) tile_build(pl);
-    if (static_cast<int32_t>(pl->shard->gbs.n) != static_cast<int32_t>(pl->t_block_tile.size()) - 1)
+    const int32_t want_gbs = pl->shard->mode == RS_EXCHANGE_QDELTA ? 1 : static_cast<int32_t>(pl->t_block_tile.size()) - 1;
+    if (static_cast<int32_t>(pl->shard->gbs.n) != want_gbs || (pl->shard->mode == RS_EXCHANGE_QDELTA &&
+                                                              static_cast<int32_t>(pl->t_block_tile.size()) - 1 != pl->shard->pieces))
         throw std::logic_error("user blocks changed after the join");
     RS_HIP(hipEventRecord(pl->ev0, s));
     if (pl->shard->mode == RS_EXCHANGE_AVERAGE) epochs_average(pl, n_epochs, lr, reg, s);
+    else if (pl->shard->mode == RS_EXCHANGE_QDELTA) epochs_qdelta(pl, n_epochs, lr, reg, s);
     else epochs_rotate(pl, n_epochs, lr, reg, s);
     RS_HIP(hipEventRecord(pl->ev1, s));
     pl->last_launches = n_epochs;  // rs_svd_plan_last_kernel_ms: the call's device span per epoch
@@ -742,8 +934,10 @@ void group_join(rs_svd_group* g, int32_t n_blocks) {
     // user (ROTATE_Q: item) totals, the user ranges and the total from the shards' host CSRs (no
     // collective needed in one process)
     const int32_t nu = g->plans[0]->n_users, ni = g->plans[0]->n_items;
-    const bool rq = g->plans[0]->exchange == RS_EXCHANGE_ROTATE_Q;
+    const bool qd = g->plans[0]->exchange == RS_EXCHANGE_QDELTA;
+    const bool rq = g->plans[0]->exchange == RS_EXCHANGE_ROTATE_Q || qd;  // user ranges, per-item counts
     std::vector<double> tot(static_cast<size_t>(std::max(1, rq ? ni : nu)), 0.0);
+    std::vector<double> ranks(qd ? tot.size() : 0, 0.0);  // QDELTA: the shards that rate each item
     std::vector<int64_t> first(n), end(n);
     double total = 0.0;
     int32_t shift = 31;  // the group's fixed-point shift: the smallest of its shards' (Q rows move between them)
@@ -755,8 +949,13 @@ void group_join(rs_svd_group* g, int32_t n_blocks) {
             throw std::invalid_argument("shards must have the same users and n_factors");
         if (pl->exchange != g->plans[0]->exchange) throw std::invalid_argument("shards must use the same exchange");
         if (rq) {
-            if (pl->n_items != ni) throw std::invalid_argument("RS_EXCHANGE_ROTATE_Q shards must have the same items");
+            if (pl->n_items != ni) throw std::invalid_argument("RS_EXCHANGE_ROTATE_Q / QDELTA shards must have the same items");
             for (int32_t c : pl->h_cols) tot[c] += 1.0;
+            if (qd) {
+                std::vector<uint8_t> seen(static_cast<size_t>(std::max(1, ni)), 0);
+                for (int32_t c : pl->h_cols) seen[c] = 1;
+                for (int32_t x = 0; x < ni; ++x) ranks[x] += seen[x];
+            }
             std::tie(first[r], end[r]) = rs::user_span(pl);
         } else {
             for (int32_t u = 0; u < nu; ++u) tot[u] += static_cast<double>(pl->h_rowptr[u + 1] - pl->h_rowptr[u]);
@@ -800,7 +999,7 @@ void group_join(rs_svd_group* g, int32_t n_blocks) {
         c->total_nnz = total;
         c->owner = owner;
         if (pl->exchange == RS_EXCHANGE_AVERAGE) rs::set_weights(pl, tot);
-        rs::shard_setup(pl, *c, n_blocks, tot);
+        rs::shard_setup(pl, *c, n_blocks, tot, qd ? &ranks : nullptr);
         pl->shard = std::move(c);
     }
     if (g->local) {
@@ -810,6 +1009,7 @@ void group_join(rs_svd_group* g, int32_t n_blocks) {
             g->local->P.push_back(pl->P.p);
             g->local->Q.push_back(pl->Q.p);
             g->local->hot.push_back(pl->shard->hot_part.p);
+            g->local->dq.push_back(pl->shard->dq.p);
             g->local->dev.push_back(pl->ctx->device);
         }
     }
@@ -904,7 +1104,7 @@ extern "C" int rs_svd_plan_set_user_blocks(rs_svd_plan* pl, int32_t n_blocks, co
 
 extern "C" int rs_svd_plan_set_exchange(rs_svd_plan* pl, int32_t mode) {
     if (!pl) return rs::set_error(nullptr, RS_ERR_INVALID, "plan is NULL");
-    if (mode != RS_EXCHANGE_ROTATE && mode != RS_EXCHANGE_AVERAGE && mode != RS_EXCHANGE_ROTATE_Q)
+    if (mode != RS_EXCHANGE_ROTATE && mode != RS_EXCHANGE_AVERAGE && mode != RS_EXCHANGE_ROTATE_Q && mode != RS_EXCHANGE_QDELTA)
         return rs::set_error(pl->ctx, RS_ERR_INVALID, "unknown exchange");
     if (pl->shard) return rs::set_error(pl->ctx, RS_ERR_INVALID, "plan is joined to a group (leave first)");
     pl->exchange = mode;
@@ -987,7 +1187,8 @@ extern "C" int rs_svd_plan_join(rs_svd_plan* pl, const void* id, int32_t rank, i
         // user span, in one all-reduce
         hipStream_t s = pl->ctx->stream;
         const int32_t nu = pl->n_users;
-        const bool rq = pl->exchange == RS_EXCHANGE_ROTATE_Q;
+        const bool qd = pl->exchange == RS_EXCHANGE_QDELTA;
+        const bool rq = pl->exchange == RS_EXCHANGE_ROTATE_Q || qd;  // user ranges, per-item counts
         const int32_t n_rows = rq ? pl->n_items : nu;
         std::vector<double> cnt(static_cast<size_t>(std::max(1, n_rows)), 0.0);
         if (rq) {
@@ -1001,6 +1202,11 @@ extern "C" int rs_svd_plan_join(rs_svd_plan* pl, const void* id, int32_t rank, i
             const std::pair<int64_t, int64_t> sp = rs::user_span(pl);
             cnt[span_at + 2 * rank] = static_cast<double>(sp.first + 1);
             cnt[span_at + 2 * rank + 1] = static_cast<double>(sp.second);
+        }
+        const size_t ranks_at = cnt.size();  // QDELTA: 1 per item this rank rates (summed: the ranks per item)
+        if (qd) {
+            cnt.resize(ranks_at + static_cast<size_t>(std::max(1, pl->n_items)), 0.0);
+            for (int32_t c2 : pl->h_cols) cnt[ranks_at + c2] = 1.0;
         }
         const size_t shift_at = cnt.size();  // every rank's fixed-point shift: the group runs at the smallest
         cnt.resize(shift_at + static_cast<size_t>(n_ranks), 0.0);
@@ -1022,9 +1228,12 @@ extern "C" int rs_svd_plan_join(rs_svd_plan* pl, const void* id, int32_t rank, i
             }
             c->owner = rs::owner_ranges(first, end, nu);
         }
+        std::vector<double> ranks;
+        if (qd) ranks.assign(cnt.begin() + static_cast<std::ptrdiff_t>(ranks_at),
+                             cnt.begin() + static_cast<std::ptrdiff_t>(ranks_at) + std::max(1, pl->n_items));
         cnt.resize(span_at);
         if (pl->exchange == RS_EXCHANGE_AVERAGE) rs::set_weights(pl, cnt);
-        rs::shard_setup(pl, *c, n_blocks, cnt);
+        rs::shard_setup(pl, *c, n_blocks, cnt, qd ? &ranks : nullptr);
         pl->shard = std::move(c);
         return RS_OK;
     });

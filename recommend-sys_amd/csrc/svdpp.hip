@@ -667,9 +667,18 @@ extern "C" int rs_svdpp_fit(rs_ctx* ctx, const rs_ratings* r, const rs_sgd_param
             ++n_heavy;
         // one block per heavy user: fewer blocks striding over them (or every user on the block path,
         // heavy_min = 1) measured slower at equal or worse RMSE (profiles/r03_experiments/pp_accuracy.log)
+        // Users in flight set the Hogwild error, so a set with few users gets fewer light blocks: at least
+        // kPPUsersPerWave light users per wave (round 5).  ML-100K (943 users) on 256 blocks of 4 waves had every
+        // user in flight at once: 5-fold-0 held-out 4.75 / 4.70 on the -10..10 rescaled ratings against 4.54 /
+        // 4.58 for the sequential restatement (0.922 against 0.920 on stars); 32 blocks: 4.54 / 4.57
+        // (profiles/r05/svdpp_blocks_scales.log).  ML-1M (6040 users) keeps about one block per CU (250).
+        constexpr int32_t kPPUsersPerWave = 6;
+        const int32_t light_cap = std::max<int32_t>(1, (n_work - n_heavy + 4 * kPPUsersPerWave - 1) / (4 * kPPUsersPerWave));
         const int32_t n_hblocks = n_heavy;
         const int32_t n_light_blocks =
-            n_work > n_heavy || n_hblocks == 0 ? std::max<int32_t>(1, std::min<int32_t>((n_work - n_heavy + 3) / 4, cap)) : 0;
+            n_work > n_heavy || n_hblocks == 0
+                ? std::max<int32_t>(1, std::min<int32_t>({(n_work - n_heavy + 3) / 4, cap, light_cap}))
+                : 0;
         const int32_t n_blocks = n_hblocks + n_light_blocks;
         rs::DevBuf<int32_t> dwork(std::max<size_t>(1, order.size()));
         dwork.upload(order.data(), order.size(), s);

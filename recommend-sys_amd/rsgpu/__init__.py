@@ -23,7 +23,7 @@ WB_TILE, WB_STORE, WB_ATOMIC_DIRECT, WB_ATOMIC = 0, 1, 2, 3  # WB_TILE: the defa
 SIM_COSINE, SIM_MSD, SIM_PEARSON = 0, 1, 2
 TIE_GO_SORT, TIE_STABLE = 0, 1  # KNN.Predict tie order (rs_knn_plan_set_tie_order)
 DEV_SLOPE_ONE = 3  # rs_knn_sims kind: SlopeOne deviation matrix (slope_one.go:64-92)
-EXCHANGE_ROTATE, EXCHANGE_AVERAGE, EXCHANGE_ROTATE_Q = 0, 1, 2  # multi-GPU exchange of the sharded fit (rsgpu.h)
+EXCHANGE_ROTATE, EXCHANGE_AVERAGE, EXCHANGE_ROTATE_Q, EXCHANGE_QDELTA = 0, 1, 2, 3  # multi-GPU exchange (rsgpu.h)
 TILE_RULE_LPT, TILE_RULE_FILL, TILE_RULE_FILL_DEVICE = 0, 1, 2  # how users are cut into tiles (rsgpu.h)
 
 HEADER_SYMBOLS = (
@@ -459,6 +459,7 @@ class SvdPlan:
             ctx.check(lib().rs_svd_plan_create_csr(ctx.h, nu, ni, _ptr(rowptr), _ptr(cols), _ptr(vals),
                                                    n_factors, C.byref(h)))
         self.h = h
+        self._groups = weakref.WeakSet()  # SvdGroups over this plan: destroyed before it
         ctx._plans.add(self)
 
     def init_normal(self, mean=0.0, std=0.1, seed=1):
@@ -679,6 +680,8 @@ class SvdPlan:
 
     def close(self):
         if self.h:
+            for g in list(self._groups):  # a group holds the plan's shard state: it goes first
+                g.close()
             lib().rs_svd_plan_destroy(self.h)
             self.h = None
 
@@ -743,8 +746,11 @@ class SvdGroup:
         self.plans = list(plans)
         arr = (C.c_void_p * len(self.plans))(*[p.h for p in self.plans])
         h = C.c_void_p()
+        self.h = None
         _check(lib().rs_svd_group_create(arr, len(self.plans), n_blocks, C.byref(h)))
         self.h = h
+        for p in self.plans:
+            p._groups.add(self)
 
     def epochs(self, n, lr=0.005, reg=0.02):
         _check(lib().rs_svd_group_epochs(self.h, n, lr, reg))

@@ -81,6 +81,8 @@ def parse(argv=None):
     ap.add_argument("--hot-share", type=float, default=None, help="rs_svd_plan_set_hot_split share (default: library)")
     ap.add_argument("--hot-min", type=int, default=None, help="rs_svd_plan_set_hot_split min stratum ratings")
     ap.add_argument("--hot-merge", type=int, default=None, help="0 scaled (default), 1 average, 2 sum")
+    ap.add_argument("--exchange", choices=["rotq", "qdelta"], default="rotq",
+                    help="RS_EXCHANGE_ROTATE_Q (Q item blocks rotate) or RS_EXCHANGE_QDELTA (one all-reduce of item moves)")
     return ap.parse_args(argv)
 
 
@@ -134,7 +136,7 @@ def run(args, say=log):
     plans = []
     for p in parts:
         pl = ctx.svd_plan_csr(U, I, padded_rowptr(p, U), p["cols"], p["vals"], k)
-        pl.set_exchange(rsgpu.EXCHANGE_ROTATE_Q)
+        pl.set_exchange(rsgpu.EXCHANGE_QDELTA if args.exchange == "qdelta" else rsgpu.EXCHANGE_ROTATE_Q)
         if args.wg:
             pl.set_tiles(workgroups=args.wg)
         if args.hot_share is not None or args.hot_min is not None or args.hot_merge is not None:
@@ -155,12 +157,21 @@ def run(args, say=log):
         ep_s.append(time.perf_counter() - t)
         curve.append(plans[0].evaluate(hu, hi_, hr)[0])
         log(f"sharded epoch {e + 1}: {ep_s[-1]:.3f} s, held-out RMSE {curve[-1]:.4f}")
-    sh = {"n_shards": n, "exchange": "RS_EXCHANGE_ROTATE_Q", "item_blocks": nblk, "setup_s": t_join,
+    sh = {"n_shards": n, "exchange": "RS_EXCHANGE_QDELTA" if args.exchange == "qdelta" else "RS_EXCHANGE_ROTATE_Q",
+          "item_blocks": nblk, "setup_s": t_join,
           "rmse_init": r0, "rmse_per_epoch": curve, "epoch_s_one_gpu": ep_s}
     if whole:
         sh["rmse_diff_vs_whole"] = curve[-1] - whole["rmse_per_epoch"][-1]
     g.close()
-    if args.strata:  # per-stratum kernel times: shard g trains item rank-block (g + s) mod n in sub-epoch s
+    if args.strata and args.exchange == "qdelta":  # one epoch of each shard alone: what an 8-GPU epoch waits on
+        t = np.array([pl.time_blocks(nblk, LR, REG) for pl in plans]).sum(1)  # the shard's user blocks, summed
+        sh["shard_epoch_ms"] = t.tolist()
+        sh["shard_epoch_max_ms"] = float(t.max())
+        sh["imbalance_max_over_mean"] = float(t.max() / t.mean())
+        sh["allreduce_bytes"] = int(I * (k + 1) * 4)
+        log(f"shard epochs {t.min():.1f}-{t.max():.1f} ms (max/mean {sh['imbalance_max_over_mean']:.3f}); "
+            f"all-reduce of {sh['allreduce_bytes'] / 1e9:.2f} GB per epoch")
+    elif args.strata:  # per-stratum kernel times: shard g trains item rank-block (g + s) mod n in sub-epoch s
         pieces = nblk // n
         t = np.array([pl.time_blocks(nblk, LR, REG) for pl in plans])  # [shard, item block] ms
         rb = t.reshape(n, n, pieces).sum(2)  # [shard, item rank-block]

@@ -562,3 +562,100 @@ def test_rotation_q_layout_rules():
             b = lay.block_of(a, x)
             assert lay.copy_used(b, h) and b == lay.block_of(a, x)
     assert RQ.mix32(0) == (0xE220A8397B1DCDAF >> 16) & 0xFFFFFFFF  # splitmix64(0)'s published first output
+
+
+# ---- QDELTA (round 5): user ranges, every item, one all-reduce of the weighted item moves per merge ---------
+# Host model of epochs_qdelta (csrc/multi.hip) on world_size 2 and 3 over gloo: every rank trains its user
+# range (the oracle's sequential SGD in user-CSR order, work-local GlobalBias) from the same Q, the item moves
+# w_i (q_end - q_start) with w_i = kappa_i / c_i are summed by one all-reduce (with the GlobalBias partials),
+# every rank applies the same sum; `merges` user blocks per epoch each end in a merge; the P ranges are
+# broadcast at the end.  Checked against the single-process run of the same rule.
+
+QD_MERGES = 2
+
+
+def _qd_weights(i, shard_items, ni, lr, merges):
+    cnt = np.bincount(i, minlength=ni).astype(np.float64)
+    c = np.sum([np.bincount(si, minlength=ni) > 0 for si in shard_items], 0).astype(np.float64)
+    a = 1.0 - float(np.float32(lr))
+    w = np.ones(ni)
+    m = (c > 1) & (cnt > 0)
+    n = cnt[m] / c[m] / merges
+    w[m] = (1.0 - a ** (c[m] * n)) / (1.0 - a ** n) / c[m]
+    return w
+
+
+def _qd_setup(world):
+    import rotq_model as RQ
+    u, i, r, nu, ni = _rq_data()
+    rng = np.random.default_rng(8)
+    P0, Q0 = rng.normal(0, 0.1, (nu, K)), rng.normal(0, 0.1, (ni, K))
+    ub = RQ.block_bounds(u, nu, world)
+    shards = [((u >= ub[g]) & (u < ub[g + 1])) for g in range(world)]
+    w = _qd_weights(i, [i[m] for m in shards], ni, 0.005, QD_MERGES)
+    blocks = []  # per rank: its merges' user blocks (user_block_bounds over the rank's own ratings)
+    for g, m in enumerate(shards):
+        bb = RQ.block_bounds(u[m], nu, QD_MERGES)
+        blocks.append([_stratum_rows(u[m], i[m], r[m], bb[b], bb[b + 1]) for b in range(QD_MERGES)])
+    return RQ, u, i, r, nu, ni, P0, Q0, ub, w, blocks
+
+
+def _stratum_rows(u, i, r, lo, hi):
+    m = (u >= lo) & (u < hi)
+    o = np.argsort(u[m], kind="stable")
+    return u[m][o].astype(np.int32), i[m][o].astype(np.int32), r[m][o]
+
+
+def _qd_train(RQ, P, Q, bu, bi, gb, blk):
+    P, Qn, bu, bin_, part = RQ.train_works(P, Q.copy(), bu, bi.copy(), gb, [blk])
+    return P, bu, Qn - Q, bin_ - bi, part
+
+
+def _qd_worker(rank, world, port, out):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    RQ, u, i, r, nu, ni, P0, Q0, ub, w, blocks = _qd_setup(world)
+    P, Q, bu, bi, gb = P0.copy(), Q0.copy(), np.zeros(nu), np.zeros(ni), 3.0
+    for _ in range(EPOCHS):
+        for b in range(QD_MERGES):
+            P, bu, mQ, mb, part = _qd_train(RQ, P, Q, bu, bi, gb, blocks[rank][b])
+            t = torch.from_numpy(np.concatenate([w[:, None] * mQ, (w * mb)[:, None]], 1).copy())
+            g = torch.tensor([part], dtype=torch.float64)
+            dist.all_reduce(t)
+            dist.all_reduce(g)
+            Q, bi = Q + t[:, :K].numpy(), bi + t[:, K].numpy()
+            gb += float(g.item()) / len(r)
+    for g in range(world):  # P range g is current on rank g
+        pr = torch.from_numpy(np.concatenate([P[ub[g]:ub[g + 1]], bu[ub[g]:ub[g + 1], None]], 1).copy())
+        dist.broadcast(pr, g)
+        P[ub[g]:ub[g + 1]], bu[ub[g]:ub[g + 1]] = pr[:, :K].numpy(), pr[:, K].numpy()
+    out[rank] = (P, Q, bu, bi, gb)
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_gloo_qdelta_matches_single_process(world):
+    port = _free_port()
+    with mp.Manager() as m:
+        out = m.dict()
+        mp.spawn(_qd_worker, args=(world, port, out), nprocs=world, join=True)
+        res = dict(out)
+    RQ, u, i, r, nu, ni, P0, Q0, ub, w, blocks = _qd_setup(world)
+    P, Q, bu, bi, gb = P0.copy(), Q0.copy(), np.zeros(nu), np.zeros(ni), 3.0
+    for _ in range(EPOCHS):
+        for b in range(QD_MERGES):
+            mQ, mb, part = np.zeros_like(Q), np.zeros_like(bi), 0.0
+            for g in range(world):
+                P, bu, dq, db, p = _qd_train(RQ, P, Q, bu, bi, gb, blocks[g][b])
+                mQ, mb, part = mQ + w[:, None] * dq, mb + w * db, part + p
+            Q, bi, gb = Q + mQ, bi + mb, gb + part / len(r)
+    assert any(0.0 < x < 1.0 for x in w)  # items on several ranks: weighted merges are exercised
+    for rank in range(world):
+        rP, rQ, rbu, rbi, rgb = res[rank]
+        np.testing.assert_allclose(rP, P, atol=1e-12)
+        np.testing.assert_allclose(rbu, bu, atol=1e-12)
+        np.testing.assert_allclose(rQ, Q, atol=1e-12)
+        np.testing.assert_allclose(rbi, bi, atol=1e-12)
+        assert abs(rgb - gb) < 1e-12
+        for x in range(4):
+            np.testing.assert_array_equal(res[0][x], res[rank][x])

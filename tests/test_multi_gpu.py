@@ -246,6 +246,83 @@ def test_rotation_q_hot_copies_equal_host_model(ctx, ml100k, n_shards, pieces):
         assert all(np.array_equal(got[0][x], y[x]) for x in range(4)) and got[0][4] == y[4]
 
 
+def _qdelta_weights(i, shard_items, ni, lr, merges=1):
+    """RS_EXCHANGE_QDELTA's merge weight per item (rsgpu.h): kappa / c over the c shards that rate it."""
+    cnt = np.bincount(i, minlength=ni).astype(np.float64)
+    c = np.sum([np.bincount(si, minlength=ni) > 0 for si in shard_items], 0).astype(np.float64)
+    a = 1.0 - float(np.float32(lr))
+    w = np.ones(ni)
+    m = (c > 1) & (cnt > 0)
+    n = cnt[m] / c[m] / merges
+    w[m] = (1.0 - a ** (c[m] * n)) / (1.0 - a ** n) / c[m]
+    return w.astype(np.float32).astype(np.float64)
+
+
+@pytest.mark.parametrize("n_shards,merges", [(2, 1), (3, 1), (8, 1), (2, 3), (4, 2)])
+def test_qdelta_one_wave_equals_host_model(ctx, ml100k, n_shards, merges):
+    """RS_EXCHANGE_QDELTA through the in-process exchange, one wave per shard: every epoch each shard trains
+    its user range against the same start Q (the oracle's sequential SGD in the shard's exported tile order,
+    P in place), the item moves merge with the kappa / c weights, GlobalBias folds the shards' partials --
+    equal to that host model to 1e-5, and P, Q, the biases and GlobalBias identical on every shard after the
+    call (the P-range broadcast; Q and GlobalBias are the same integer sums everywhere)."""
+    f = folds(*ml100k)[2]
+    n = 30000
+    u, i, r, nu, ni = f.iu[:n], f.ii[:n], f.r[:n], f.nu, f.ni
+    k, lr, epochs = 24, 0.005, 2
+    rng = np.random.default_rng(90 + n_shards)
+    P0, Q0 = rng.normal(0, 0.1, (nu, k)), rng.normal(0, 0.1, (ni, k))
+    sh = _user_shards(u, i, r, nu, n_shards)
+    plans = []
+    for su, si, sr in sh:
+        pl = ctx.svd_plan(rsgpu.Ratings(su, si, sr, nu, ni), k)
+        pl.set_tiles(workgroups=1, waves=1)
+        pl.set_exchange(rsgpu.EXCHANGE_QDELTA)
+        pl.upload(P0, Q0, np.zeros(nu), np.zeros(ni), 3.5)
+        plans.append(pl)
+    g = rsgpu.SvdGroup(plans, n_blocks=merges if merges > 1 else 0)
+    assert all(pl.shard_info()[2] == rsgpu.EXCHANGE_QDELTA for pl in plans)
+    g.epochs(epochs, lr=lr)
+    works = []  # per shard and merge: (users, items, ratings, work offsets) in the shard's visit order
+    for pl, (su, si, sr) in zip(plans, sh):
+        rowptr, items, rr = O.csr_by(su, nu, si, sr)
+        cu = np.repeat(np.arange(nu, dtype=np.int32), np.diff(rowptr))
+        pos, off = pl.tile_order()
+        uu, ii, r_ = cu[pos], np.asarray(items, np.int32)[pos], np.asarray(rr)[pos]
+        ub = _block_bounds(su, nu, merges)  # the merges' user blocks (user_block_bounds of the shard's ratings)
+        per = [[] for _ in range(merges)]
+        for x in range(len(off) - 1):
+            if off[x + 1] > off[x]:
+                per[int(np.searchsorted(ub, uu[off[x]], side="right") - 1)].append((off[x], off[x + 1]))
+        for b in range(merges):
+            seg = per[b]
+            sel = np.concatenate([np.arange(a, z) for a, z in seg]) if seg else np.zeros(0, np.int64)
+            wo = np.concatenate([[0], np.cumsum([z - a for a, z in seg])]).astype(np.int64)
+            per[b] = (uu[sel], ii[sel], r_[sel], wo)
+        works.append(per)
+    w = _qdelta_weights(i, [x[1] for x in sh], ni, lr, merges)
+    P, Q, bu, bi, gb = P0.copy(), Q0.copy(), np.zeros(nu), np.zeros(ni), 3.5
+    for _ in range(epochs):
+        for b in range(merges):
+            mQ, mb, part = np.zeros_like(Q), np.zeros_like(bi), 0.0
+            for per in works:
+                uu, ii, r_, off = per[b]
+                if len(r_) == 0:
+                    continue
+                P, Qg, bu, big, gg = O.svd_fit_works(uu, ii, r_, off, P, Q, bu, bi, gb, epochs=1, lr=lr)
+                mQ += Qg - Q
+                mb += big - bi
+                part += (gg - gb) * len(r_)
+            Q, bi = Q + w[:, None] * mQ, bi + w * mb
+            gb += part / len(r)
+    g.close()
+    got = [pl.download() for pl in plans]
+    for pl in plans:
+        pl.close()
+    assert _maxdiff((P, Q, bu, bi), got[0][:4]) <= TOL and abs(gb - got[0][4]) <= TOL
+    for y in got[1:]:
+        assert all(np.array_equal(got[0][x], y[x]) for x in range(4)) and got[0][4] == y[4]
+
+
 def test_rotation_fewer_users_than_blocks(ctx):
     """ROTATE with more user blocks than users (4 shards x 2 pieces, 5 users): empty blocks send and
     receive nothing and the fit still equals a single plan's users trained (finite, every rating seen)."""

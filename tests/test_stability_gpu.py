@@ -1,11 +1,11 @@
 """FAST default stability at library defaults: rs_synth sets of 1M / 8M / 32M / 128M ratings,
 hottest item 0.3-3 % of the ratings, k 64 / 100 / 256 (scripts/experiments/exp_stability.py CASES), 5 %
-held out.  Where the sequential reference (or_svd_fit, core/svd.go:92-130 in user-major order, the same
-init) is affordable (the 1M sets) the held-out RMSE after 10 epochs may not be worse than the reference's
-by more than 0.003 -- lower is allowed: FAST's GlobalBias warm start and its concurrent epochs reach the
-same curve a little sooner on these still-falling curves --; elsewhere the factors stay finite and the
-held-out RMSE falls every epoch.  Both the plan path (rs_svd_plan_epochs) and the Go drop-in (rs_svd_fit,
-with its divergence guard) run every oracle case."""
+held out.  Where the sequential reference (or_svd_fit, core/svd.go:92-130 over the ratings in a shuffled
+TrainSet order -- KFold's data order, data.go:49-70 --, the same init) is affordable (the 1M sets) the
+held-out RMSE after 10 epochs is within 0.003 of the reference's (P2, both sides); elsewhere the factors
+stay finite and the held-out RMSE falls every epoch.  Both the plan path (rs_svd_plan_epochs) and the Go
+drop-in (rs_svd_fit, with its divergence guard) run every oracle case; the divergence guard's redos are
+reported (profiles/r05/stability.log)."""
 import os
 import sys
 
@@ -30,10 +30,10 @@ def S():
 def test_stable_within_reference(ctx, S, name):
     out = S.run(ctx, name, claim=4, cap=0, log=print)
     assert out["numeric"] == "ok" and all(np.isfinite(out["curve"]))
-    assert out["curve"][-1] <= out["ref_curve"][-1] + 0.003, (out["curve"][-1], out["ref_curve"][-1])
+    assert abs(out["curve"][-1] - out["ref_curve"][-1]) <= 0.003, (out["curve"][-1], out["ref_curve"][-1])
     fit = S.run_fit(ctx, name, log=print)
     assert fit["rmse"] is not None and np.isfinite(fit["rmse"])
-    assert fit["rmse"] <= out["ref_curve"][-1] + 0.003, (fit["rmse"], out["ref_curve"][-1])
+    assert abs(fit["rmse"] - out["ref_curve"][-1]) <= 0.003, (fit["rmse"], out["ref_curve"][-1])
 
 
 @pytest.mark.timeout(600)
