@@ -14,9 +14,10 @@ fails when fewer than N GPUs are visible.
 
 Extra fields of the same line:
   strong_scaling  BASELINE configs[4] at full size (10M users x 1M items x ~1e9 ratings, k = 256), user
-                  ranges over the N ranks with the Q item rank-blocks rotating (RS_EXCHANGE_ROTATE_Q) --
-                  the north_star scaling question; the driver's N = 1, 2, 4, 8 lines give its curve.
-                  About a minute at N = 1 (generation ~35 s, plan ~10-30 s, 4 epochs of ~0.6 s).
+                  ranges over the N ranks, the ranks' item moves all-reduced 16 times per epoch (RS_EXCHANGE_QDELTA,
+                  fp16 moves, each all-reduce behind the next block's kernel) -- the north_star scaling question;
+                  the driver's N = 1, 2, 4, 8 lines give its curve.  One timed call of 20 epochs (a default Fit,
+                  core/svd.go:66).  About a minute at N = 1 (generation ~35 s, plan ~10-30 s, 21 epochs of ~0.6 s).
   ordered         N = 1: throughput of the ORDERED mode (the reference visit order, the mode that
                   meets north_star's 1e-5 factor contract) on the same ML-1M-shaped set.
 
@@ -39,6 +40,8 @@ METRIC = "SGD updates/sec, SVD k=100 MovieLens-1M, 1/2/4/8 GPU; % HBM roofline"
 K = 100
 LR, REG = 0.005, 0.02
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md chip table: 8.0 TB/s spec
+EXCHANGE_NAMES = {0: "RS_EXCHANGE_ROTATE (stratum rotation)", 1: "RS_EXCHANGE_AVERAGE", 2: "RS_EXCHANGE_ROTATE_Q",
+                  3: "RS_EXCHANGE_QDELTA"}
 
 
 def algorithmic_bytes(nnz, n_users, k):
@@ -65,12 +68,14 @@ def cpu_baseline(u, i, r, n_users, n_items, budget_s=10.0):
                       f"of core/svd.go:92-130 (oracle/), single thread, {t_total:.1f} s"}
 
 
-def strong_scaling(ctx, rank, world, dist, dev, stream, epochs=3, warmup=1):
+def strong_scaling(ctx, rank, world, dist, dev, stream, epochs=20, warmup=1):
     """BASELINE configs[4] at its own size: SVD nFactors=256 on the synthetic 10M users x 1M items x ~1e9
     ratings set (rs_synth, seed 20250826 -- the set tests/test_config4_gpu.py fits), library defaults.  Rank r
     generates and holds users [U r / N, U (r + 1) / N) (global ids, every item); with N > 1 the library's RCCL
-    communicator runs RS_EXCHANGE_ROTATE_Q (user ranges stay, the Q item rank-blocks rotate, N sub-epochs per
-    epoch; the Zipf head's items split into per-block copies merged once per epoch, csrc/multi.hip)."""
+    communicator runs RS_EXCHANGE_QDELTA (each rank trains its users against the whole Q in 16 blocks; after each
+    block the ranks' weighted item moves are all-reduced as fp16 while the next block trains, csrc/multi.hip).
+    One timed call of `epochs` epochs: a default Fit is 20 (core/svd.go:66), and P's ranges are broadcast once
+    per call."""
     import torch
     import rsgpu
     n_users, n_items, k = 10_000_000, 1_000_000, 256
@@ -95,7 +100,7 @@ def strong_scaling(ctx, rank, world, dist, dev, stream, epochs=3, warmup=1):
         dist.all_reduce(tot)
     plan.upload(gb=float(tot[1] / tot[0]))  # the training mean: the same GlobalBias on every rank
     if dist:
-        plan.set_exchange(rsgpu.EXCHANGE_ROTATE_Q)
+        plan.set_exchange(rsgpu.EXCHANGE_QDELTA)
         uid = [rsgpu.comm_unique_id() if rank == 0 else None]
         dist.broadcast_object_list(uid, src=0)
         plan.join(uid[0], rank, world)
@@ -133,8 +138,9 @@ def strong_scaling(ctx, rank, world, dist, dev, stream, epochs=3, warmup=1):
             "scaling": "strong", "n_gpus": world, "epochs": epochs, "warmup": warmup,
             "value": total * epochs / dt, "unit": "updates/s", "ms_per_epoch": dt / epochs * 1e3,
             "gen_s_rank0": gen_s, "setup_s_rank0": setup_s, "finite": finite, "item_blocks": n_blocks,
-            "exchange": "rs_svd_plan_join + rs_svd_plan_epochs_sharded, RS_EXCHANGE_ROTATE_Q (RCCL send/recv of "
-                        "Q item rank-blocks, piece by piece; hot-copy merge by one all-reduce per epoch)"
+            "exchange": f"rs_svd_plan_join + rs_svd_plan_epochs_sharded, RS_EXCHANGE_QDELTA ({n_blocks} merges per "
+                        "epoch: RCCL all-reduce of the ranks' weighted item moves as fp16, each behind the next "
+                        "block's kernel; P ranges broadcast once per call)"
                         if world > 1 else "none (one GPU, one plan over the whole set)"}
 
 
@@ -259,10 +265,10 @@ def main():
         uid = [rsgpu.comm_unique_id() if rank == 0 else None]
         dist.broadcast_object_list(uid, src=0)
         plan.join(uid[0], rank, world)
-        comm_rank, comm_ranks, _, comm_blocks = plan.shard_info()
+        comm_rank, comm_ranks, comm_exchange, comm_blocks = plan.shard_info()
         run = lambda n: plan.epochs_sharded(n, LR, REG, stream)
     else:
-        comm_ranks, comm_blocks = 1, 1
+        comm_ranks, comm_blocks, comm_exchange = 1, 1, None
         run = lambda n: plan.epochs(n, LR, REG, stream)
     rccl_version, rccl_path = rsgpu.comm_info()
 
@@ -324,9 +330,9 @@ def main():
                                    "per step (BASELINE configs[1])",
                        "n_users": n_users, "n_items_per_rank": n_items, "nnz_per_rank": nnz,
                        "n_factors": K, "lr": LR, "reg": REG,
-                       "parallelism": f"item-sharded x{world}: stratum rotation, {comm_blocks} user blocks "
-                                      "(RCCL send/recv of P rank-blocks per sub-epoch)" if world > 1
-                                      else "single GPU"},
+                       "parallelism": (f"item-sharded x{world}: {EXCHANGE_NAMES.get(comm_exchange, comm_exchange)}, "
+                                       f"{comm_blocks} user blocks (RCCL send/recv of P rank-blocks per sub-epoch)")
+                                      if world > 1 else "single GPU"},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
                          "traffic": traffic,

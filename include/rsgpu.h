@@ -435,19 +435,29 @@ int rs_svd_plan_apply_delta(rs_svd_plan* plan, const void* dP, const void* gbsum
  * 1M / 8 Q rows (160 MB at k = 256) instead of 10M / 8 P rows (1.6 GB).  After the call the item
  * rank-blocks and every rank's user range are broadcast, so P, Q, the biases and GlobalBias are identical
  * on every rank.  n_blocks = item blocks in all (rounded up to a multiple of n_ranks; 0 = automatic: 2..16
- * pieces of ~64 MiB of Q per rank-block).  rs_svd_fit_multi picks it when n_items < n_users. */
+ * pieces of ~64 MiB of Q per rank-block). */
 #define RS_EXCHANGE_ROTATE_Q 2
 /* RS_EXCHANGE_QDELTA -- north_star's once-per-epoch all-reduce, on the smaller factor matrix (round 5; for
  * U > I, configs[4]).  As ROTATE_Q the ranks hold user ranges (contiguous, ascending by rank) and every item;
- * an epoch is one plain tile epoch of the rank's users against the whole Q (P in place), then ONE all-reduce
- * of the item moves in the int32 fixed point (n_items x (k + 1); exact integer sums, identical on every rank):
+ * the rank's users are cut into n_blocks merges per epoch (user blocks of near-equal ratings; 0 = 16, the fewest
+ * that keep configs[4]'s held-out RMSE within 0.01 of the whole-set fit after 10 epochs) and each
+ * block is one plain tile launch of those users against the whole Q (P in place), after which the rank's item
+ * moves are all-reduced (n_items rows of the plan's row stride):
  * q_i <- q_i,start + sum over ranks of w_i (q_i,end - q_i,start), with w_i = kappa_i / c_i over the c_i ranks
- * that rate item i, kappa_i = (1 - a^(c_i n_i)) / (1 - a^n_i), n_i = its ratings per rank, a = 1 - lr (the
- * moves of a unit-curvature coordinate that c_i ranks each close by 1 - a^n_i, scaled to the sequential
- * 1 - a^(c_i n_i)): exact for items of one rank, the mean of converged moves.  GlobalBias: the ranks' partials,
- * one f64 all-reduce.  After the call the ranks' P ranges are broadcast. */
+ * that rate item i, kappa_i = (1 - a^(c_i n_i)) / (1 - a^n_i), n_i = its ratings per rank and merge, a = 1 - lr
+ * (the moves of a unit-curvature coordinate that c_i ranks each close by 1 - a^n_i, scaled to the sequential
+ * 1 - a^(c_i n_i)): exact for items of one rank, the mean of converged moves.  Pipelined: a rank applies its
+ * own weighted moves at once and the other ranks' (sum - own) after its next block, so merge m's all-reduce
+ * runs behind block m + 1's kernel; after the call's last merge every rank holds the same Q.  The moves travel
+ * as fp16 factor units (rs_svd_plan_set_qdelta_wire 16, the default: half the bytes) or int32 fixed point (32:
+ * exact integer sums); either way every rank applies the same rounded values.  GlobalBias: the ranks'
+ * partials, one f64 all-reduce per merge (applied with the same one-merge delay).  After the call the ranks'
+ * P ranges are broadcast. */
 #define RS_EXCHANGE_QDELTA 3
 int rs_svd_plan_set_exchange(rs_svd_plan* plan, int32_t mode);
+/* RS_EXCHANGE_QDELTA's wire width: 16 (fp16 moves, default) or 32 (int32 fixed point).  Set before the join;
+ * every rank of a group must use the same width (the join checks). */
+int rs_svd_plan_set_qdelta_wire(rs_svd_plan* plan, int32_t bits);
 /* RS_EXCHANGE_ROTATE_Q on Zipf-headed sets: a stratum (one rank's users x one item block) holds an item's
  * ratings n_blocks-fold concentrated, so the head's rows get many concurrent runs in flight (Hogwild staleness
  * that diverges at lr 0.005; configs[4]: the hottest item is 0.8 % of the set but 12.7 % of its stratum).  An
@@ -509,8 +519,8 @@ void rs_svd_group_destroy(rs_svd_group* group);
 int rs_item_shards(int64_t nnz, const int32_t* items, int32_t n_items, int32_t n_shards, int32_t* bounds);
 /* core/svd.go:63-132 (FAST tile schedule) on n_devices GPUs of this process: the items are sharded by
  * rs_item_shards and P rank-blocks rotate (RS_EXCHANGE_ROTATE); with fewer items than users and P rank-blocks
- * of 16 MiB or more the users are cut into ranges of near-equal ratings and Q item blocks rotate
- * (RS_EXCHANGE_ROTATE_Q).  As rs_svd_fit otherwise (GlobalBias warm start, host buffers in / out; a fit
+ * of 16 MiB or more the users are cut into ranges of near-equal ratings and the ranks' item moves are
+ * all-reduced (RS_EXCHANGE_QDELTA, fp16 wire; n_blocks = merges per epoch, 0 = 16).  As rs_svd_fit otherwise (GlobalBias warm start, host buffers in / out; a fit
  * whose shards leave the fixed-point range, go non-finite or hold a factor past the guard bound is rebuilt and
  * redone from the inputs on half the workgroups and run cap 2, up to three times -- rs_fit_multi_refits counts
  * them; RS_ERR_NUMERIC after every shard's values are written). */

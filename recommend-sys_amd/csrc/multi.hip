@@ -44,6 +44,7 @@
 // Both exchanges run over RCCL (ncclComm per rank: rs_svd_plan_join for one process per GPU,
 // rs_svd_group_create for one process driving several GPUs) or, for shards that share a device
 // (tests), over an in-process host-barrier exchange (no overlap).
+#include <hip/hip_fp16.h>
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
 #include <dlfcn.h>
@@ -113,7 +114,11 @@ struct ShardComm {
     DevBuf<float> hot_part, hot_avg;  // ROTATE_Q hot copies: this rank's summed moves, over all ranks (H x ld)
     DevBuf<float> hot_w;              // merge weight per hot item
     DevBuf<float> item_c, item_n;     // QDELTA: per item the ranks that rate it and its ratings over all ranks
-    DevBuf<int32_t> q0, dq, dq_sum;   // QDELTA: Q at the epoch start (int32 rows of ld), the moves (k + 1 wide), their sum
+    DevBuf<int32_t> q0;               // QDELTA: Q at the block's start (int32 rows of ld)
+    DevBuf<int32_t> dq, dq_sum;       // QDELTA: the weighted moves and their sum (rows of ld, `wire` bits each), two
+                                      // merges' worth (parity m % 2: merge m's all-reduce overlaps block m + 1)
+    int32_t wire = 32;
+    hipEvent_t ev_ar[2] = {nullptr, nullptr};  // QDELTA: merge m's all-reduce ended (comm stream)
     DevBuf<float> qw;                 // QDELTA: merge weight per item (for the call's lr)
     float qw_lr = -1.f;
     ncclComm_t nccl = nullptr;
@@ -142,6 +147,8 @@ struct ShardComm {
         for (hipEvent_t e : ev_recv) (void)hipEventDestroy(e);
         if (ev_epoch) (void)hipEventDestroy(ev_epoch);
         if (ev_gb) (void)hipEventDestroy(ev_gb);
+        for (hipEvent_t e : ev_ar)
+            if (e) (void)hipEventDestroy(e);
         if (cs) (void)hipStreamDestroy(cs);
     }
 };
@@ -151,6 +158,11 @@ namespace {
 void check_nccl(ncclResult_t r, const char* what) {
     if (r != ncclSuccess) throw std::runtime_error(std::string(what) + ": " + ncclGetErrorString(r));
 }
+
+// QDELTA merges per epoch when the caller leaves them to the library (n_blocks = 0).  configs[4], 8 ranks, held-out
+// RMSE after 10 epochs against 0.6079 for the whole-set fit: 1 merge 0.6522, 4 merges 0.6239, 8 0.6202, 12
+// 0.6184, 16 0.6167 (pipelined; profiles/r05/config4_qdelta_*.log) -- 16 is the fewest within 0.01.
+constexpr int32_t kQdeltaMerges = 16;
 
 int32_t comm_ctas() {
     static const int v = std::getenv("RSGPU_COMM_CTAS") ? std::atoi(std::getenv("RSGPU_COMM_CTAS")) : 32;
@@ -273,37 +285,130 @@ __global__ __launch_bounds__(256) void hot_sum_kernel(Srcs src, int32_t n_src, i
     }
 }
 
-// QDELTA, after a rank's epoch: dq[i][c] = round(w_i (Q[i][c] - Q0[i][c])) for the k + 1 columns (int32 fixed
-// point rows of ld; the moves k + 1 wide), and Q back to its epoch-start value
-__global__ __launch_bounds__(256) void qdelta_moves_kernel(int32_t* __restrict__ Q, const int32_t* __restrict__ Q0,
-                                                           const float* __restrict__ w, int32_t* __restrict__ dq,
-                                                           int32_t n_items, int32_t ld, int32_t kw) {
-    const int64_t n = static_cast<int64_t>(n_items) * kw;
-    for (int64_t t = static_cast<int64_t>(blockIdx.x) * 256 + threadIdx.x; t < n; t += static_cast<int64_t>(gridDim.x) * 256) {
-        const int64_t i = t / kw;
-        const int32_t c = static_cast<int32_t>(t - i * kw);
-        const int64_t g = i * ld + c;
-        const int32_t q0 = Q0[g];
-        dq[t] = __float2int_rn(w[i] * static_cast<float>(Q[g] - q0));
-        Q[g] = q0;
+// QDELTA moves on the wire: B = 32, int32 in the plan's fixed point (exact sums); B = 16, fp16 in factor units
+// (half the bytes; every rank applies the same rounded values, so the ranks still agree bit for bit).  Four
+// columns of one row per thread (rows of ld, a multiple of 4).
+template <int B> struct Wire4;
+template <> struct Wire4<32> {
+    using T = int4;
+    __device__ static int4 fixed(T v, float) { return v; }
+    // the weighted moves of raw fixed-point moves r: on the wire and (own) as applied here
+    __device__ static T make(const int4& r, float w, float, float, int4& own) {
+        own = make_int4(__float2int_rn(w * static_cast<float>(r.x)), __float2int_rn(w * static_cast<float>(r.y)),
+                        __float2int_rn(w * static_cast<float>(r.z)), __float2int_rn(w * static_cast<float>(r.w)));
+        return own;
+    }
+};
+// IEEE binary16 bits -> float, decoded with integer operations: the value a rank applies as its own move and
+// the value it later subtracts (read back from the wire buffer) come from the same bits by construction, with
+// no float conversion the compiler could fold against the rounding that made them (exact: every half is a float)
+__device__ inline float half_bits_to_float(uint32_t h) {
+    const uint32_t e = (h >> 10) & 0x1fu, m = h & 0x3ffu, sign = (h & 0x8000u) << 16;
+    uint32_t bits;
+    if (e == 0) bits = __float_as_uint(static_cast<float>(m) * 5.9604644775390625e-8f);  // m 2^-24 (subnormal)
+    else if (e == 31) bits = 0x7f800000u | (m << 13);                                    // inf / nan
+    else bits = ((e + 112u) << 23) | (m << 13);
+    return __uint_as_float(bits | sign);
+}
+template <> struct Wire4<16> {
+    using T = uint2;  // four halves
+    __device__ static float4 f(T v) {
+        return make_float4(half_bits_to_float(v.x & 0xffffu), half_bits_to_float(v.x >> 16),
+                           half_bits_to_float(v.y & 0xffffu), half_bits_to_float(v.y >> 16));
+    }
+    __device__ static T h(float4 x) {
+        const __half2 a = __floats2half2_rn(x.x, x.y), b = __floats2half2_rn(x.z, x.w);
+        return make_uint2(__builtin_bit_cast(uint32_t, a), __builtin_bit_cast(uint32_t, b));
+    }
+    __device__ static int4 fixed(T v, float fx) {
+        const float4 x = f(v);
+        return make_int4(__float2int_rn(x.x * fx), __float2int_rn(x.y * fx), __float2int_rn(x.z * fx), __float2int_rn(x.w * fx));
+    }
+    __device__ static T make(const int4& r, float w, float fx, float fx_inv, int4& own) {
+        const float s = w * fx_inv;
+        const T v = h(make_float4(s * static_cast<float>(r.x), s * static_cast<float>(r.y), s * static_cast<float>(r.z),
+                                  s * static_cast<float>(r.w)));
+        own = fixed(v, fx);
+        return v;
+    }
+};
+__device__ inline int4 add4(int4 a, int4 b) { return make_int4(a.x + b.x, a.y + b.y, a.z + b.z, a.w + b.w); }
+__device__ inline int4 sub4(int4 a, int4 b) { return make_int4(a.x - b.x, a.y - b.y, a.z - b.z, a.w - b.w); }
+
+// QDELTA, after a rank's block m, one pass over the items' rows: the raw moves Q - Q0 become weighted moves
+// w_i (Q - Q0) -- what merge m all-reduces --, Q keeps Q0 + its own share plus, when merge m - 1's all-reduce
+// has come in (prev_sum), the other ranks' moves of that merge, prev_sum - prev_dq (exact in int32); Q0 = Q
+// for block m + 1.  Q0 and the wire buffers hold the k + 1 live columns of each row, rounded up to 4 (l4 int4
+// vectors per row; Q's rows are ld4 vectors: the tile kernel pads them to whole 64-column chunks, 320 at
+// k = 256), n4 = n_items x l4.  One vector per thread (grid qdelta_grid: a grid-stride loop over these five
+// streams runs at 4.5-4.7 TB/s, one vector per thread at 5.4-5.5, profiles/r05/qdelta_merge_bench.log).
+template <int B>
+__global__ __launch_bounds__(256) void qdelta_merge_kernel(int32_t* __restrict__ Q, int32_t* __restrict__ Q0,
+                                                           const float* __restrict__ w, void* __restrict__ dq,
+                                                           const void* __restrict__ prev_sum,
+                                                           const void* __restrict__ prev_dq, uint32_t n4, uint32_t l4,
+                                                           uint32_t ld4, float fx, float fx_inv) {
+    using W = Wire4<B>;
+    using T = typename W::T;
+    int4* const z4 = reinterpret_cast<int4*>(Q0);
+    const uint32_t t = blockIdx.x * 256u + threadIdx.x;
+    if (t < n4) {
+        const uint32_t i = t / l4;
+        int4& qv = reinterpret_cast<int4*>(Q)[static_cast<size_t>(i) * ld4 + (t - i * l4)];  // the same vector in Q
+        const int4 q = qv, q0 = z4[t];
+        int4 own;
+        reinterpret_cast<T*>(dq)[t] = W::make(sub4(q, q0), w[i], fx, fx_inv, own);
+        int4 v = add4(q0, own);
+        if (prev_sum)
+            v = add4(v, sub4(W::fixed(reinterpret_cast<const T*>(prev_sum)[t], fx),
+                             W::fixed(reinterpret_cast<const T*>(prev_dq)[t], fx)));
+        qv = v;
+        z4[t] = v;
     }
 }
-// QDELTA: Q += the summed moves (int32, exact)
-__global__ __launch_bounds__(256) void qdelta_apply_kernel(int32_t* __restrict__ Q, const int32_t* __restrict__ dq,
-                                                           int32_t n_items, int32_t ld, int32_t kw) {
-    const int64_t n = static_cast<int64_t>(n_items) * kw;
-    for (int64_t t = static_cast<int64_t>(blockIdx.x) * 256 + threadIdx.x; t < n; t += static_cast<int64_t>(gridDim.x) * 256) {
-        const int64_t i = t / kw;
-        const int32_t c = static_cast<int32_t>(t - i * kw);
-        Q[i * ld + c] += dq[t];
+inline dim3 qdelta_grid(int64_t n4) { return dim3(static_cast<uint32_t>(std::max<int64_t>(1, (n4 + 255) / 256))); }
+// QDELTA, the call's last merge when its all-reduce has come in: Q += sum - dq (the other ranks' weighted moves;
+// the rank's own are in Q already), exact in int32.  sum == nullptr: only Q0 = Q (the call's start).
+template <int B>
+__global__ __launch_bounds__(256) void qdelta_correct_kernel(int32_t* __restrict__ Q, const void* __restrict__ sum,
+                                                             const void* __restrict__ dq, int32_t* __restrict__ Q0,
+                                                             uint32_t n4, uint32_t l4, uint32_t ld4, float fx) {
+    using W = Wire4<B>;
+    using T = typename W::T;
+    const uint32_t t = blockIdx.x * 256u + threadIdx.x;
+    if (t < n4) {
+        const uint32_t i = t / l4;
+        int4& qv = reinterpret_cast<int4*>(Q)[static_cast<size_t>(i) * ld4 + (t - i * l4)];
+        int4 v = qv;
+        if (sum) {
+            v = add4(v, sub4(W::fixed(reinterpret_cast<const T*>(sum)[t], fx), W::fixed(reinterpret_cast<const T*>(dq)[t], fx)));
+            qv = v;
+        }
+        if (Q0) reinterpret_cast<int4*>(Q0)[t] = v;
     }
 }
-// QDELTA, in-process exchange: out = the sum over the shards (shard order; integer, so any order) of their moves
-__global__ __launch_bounds__(256) void qdelta_sum_kernel(Srcs src, int32_t n_src, int64_t n, int32_t* __restrict__ out) {
-    for (int64_t t = static_cast<int64_t>(blockIdx.x) * 256 + threadIdx.x; t < n; t += static_cast<int64_t>(gridDim.x) * 256) {
-        int32_t a = reinterpret_cast<const int32_t*>(src.p[0])[t];
-        for (int32_t r = 1; r < n_src; ++r) a += reinterpret_cast<const int32_t*>(src.p[r])[t];
-        out[t] = a;
+// QDELTA, in-process exchange: out = the sum over the shards of their weighted moves (int32: exact; fp16: summed
+// in fp32 in shard order, rounded once)
+struct WireSrcs {
+    const void* p[kMaxLocal];
+};
+template <int B>
+__global__ __launch_bounds__(256) void qdelta_sum_kernel(WireSrcs src, int32_t n_src, uint32_t n4, void* __restrict__ out) {
+    using T = typename Wire4<B>::T;
+    const uint32_t t = blockIdx.x * 256u + threadIdx.x;
+    if (t < n4) {
+        if constexpr (B == 32) {
+            int4 a = reinterpret_cast<const int4*>(src.p[0])[t];
+            for (int32_t r = 1; r < n_src; ++r) a = add4(a, reinterpret_cast<const int4*>(src.p[r])[t]);
+            reinterpret_cast<int4*>(out)[t] = a;
+        } else {
+            float4 a = Wire4<16>::f(reinterpret_cast<const T*>(src.p[0])[t]);
+            for (int32_t r = 1; r < n_src; ++r) {
+                const float4 b = Wire4<16>::f(reinterpret_cast<const T*>(src.p[r])[t]);
+                a.x += b.x; a.y += b.y; a.z += b.z; a.w += b.w;
+            }
+            reinterpret_cast<T*>(out)[t] = Wire4<16>::h(a);
+        }
     }
 }
 
@@ -393,8 +498,8 @@ void shard_setup(rs_svd_plan* pl, ShardComm& c, int32_t n_blocks, const std::vec
     if (c.mode == RS_EXCHANGE_QDELTA) {  // the rank's users against every item: one plain tile schedule
         if (!item_ranks) throw std::logic_error("QDELTA: the items' rank counts are missing");
         // n_blocks: merges per epoch (the rank's users cut into that many blocks of near-equal ratings, the item
-        // moves all-reduced after each; 0 = 1)
-        pl->tile_ublocks = std::max(1, n_blocks);
+        // moves all-reduced after each; 0 = kQdeltaMerges)
+        pl->tile_ublocks = n_blocks > 0 ? n_blocks : kQdeltaMerges;
         pl->ublock_bounds.clear();
         pl->iblock_bounds.clear();
         pl->hot_items.clear();
@@ -408,19 +513,29 @@ void shard_setup(rs_svd_plan* pl, ShardComm& c, int32_t n_blocks, const std::vec
         c.item_c.alloc(ni);
         c.item_n.upload(cn.data(), ni, pl->ctx->stream);
         c.item_c.upload(cc.data(), ni, pl->ctx->stream);
+        // CUs for the all-reduce that runs behind each block.  Free at configs[4]: the shard epoch is 74.8-76.1 ms
+        // on 224 workgroups, 74.7-77.6 on 192 and 73.4-77.5 on 256 -- the memory-side atomic unit bounds it, not
+        // the CUs (profiles/r05/config4_qdelta_wg.log).
+        if (c.nccl && c.nranks > 1 && pl->tile_wg == 0) {
+            int cus = 0;
+            RS_HIP(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, c.device));
+            pl->tile_wg = std::max(1, cus - comm_ctas());
+        }
         tile_build(pl);
         c.pieces = static_cast<int32_t>(pl->t_block_tile.size()) - 1;  // merges per epoch
-        c.gbs.alloc(1);
-        if (c.local) c.gbs_sum.alloc(1);
+        c.gbs.alloc(2);
+        if (c.local) c.gbs_sum.alloc(2);
         if (c.nccl) {
             RS_HIP(hipStreamCreateWithFlags(&c.cs, hipStreamNonBlocking));
             RS_HIP(hipEventCreateWithFlags(&c.ev_epoch, hipEventDisableTiming));
             RS_HIP(hipEventCreateWithFlags(&c.ev_gb, hipEventDisableTiming));
+            for (hipEvent_t& e : c.ev_ar) RS_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
         }
-        const size_t kw = static_cast<size_t>(pl->k) + 1;
-        c.q0.alloc(ni * static_cast<size_t>(pl->ld));
-        c.dq.alloc(ni * kw);
-        if (c.local) c.dq_sum.alloc(ni * kw);
+        const size_t nq = ni * static_cast<size_t>(round_up4(pl->k + 1));  // the live columns, whole int4 vectors
+        c.wire = pl->qdelta_wire;
+        c.q0.alloc(nq);
+        c.dq.alloc(2 * nq * c.wire / 32);
+        c.dq_sum.alloc(2 * nq * c.wire / 32);
         RS_HIP(hipStreamSynchronize(pl->ctx->stream));
         return;
     }
@@ -791,8 +906,13 @@ void epochs_rotate(rs_svd_plan* pl, int32_t n_epochs, float lr, float reg, hipSt
 // QDELTA: n_epochs of the user-range epochs with one all-reduce of the item moves per epoch, on stream s
 void epochs_qdelta(rs_svd_plan* pl, int32_t n_epochs, float lr, float reg, hipStream_t s) {
     ShardComm& c = *pl->shard;
-    const int32_t N = c.nranks, ni = pl->n_items, ld = pl->ld, kw = pl->k + 1;
-    const int64_t nq = static_cast<int64_t>(ni) * kw;
+    const int32_t N = c.nranks, ni = pl->n_items, ld = pl->ld, kc = round_up4(pl->k + 1);
+    const int64_t nq = static_cast<int64_t>(ni) * kc, n4 = nq / 4;  // wire values per merge (k + 1 live columns), vectors
+    const size_t wb = static_cast<size_t>(nq) * (c.wire / 8);        // wire bytes per merge
+    const bool h16 = c.wire == 16;
+    const float fx = pl->fx(), fx_inv = pl->fx_inv();
+    char* const dq = reinterpret_cast<char*>(c.dq.p);
+    char* const dsum = reinterpret_cast<char*>(c.dq_sum.p);
     const double inv_total = c.total_nnz > 0 ? 1.0 / c.total_nnz : 0.0;
     if (c.qw_lr != lr) {  // the merge weights for this lr (module header: kappa / c per item)
         const size_t n1 = static_cast<size_t>(std::max(1, ni));
@@ -815,53 +935,82 @@ void epochs_qdelta(rs_svd_plan* pl, int32_t n_epochs, float lr, float reg, hipSt
     }
     int32_t* const Qi = reinterpret_cast<int32_t*>(pl->Q.p);
     const int32_t nb = static_cast<int32_t>(pl->t_block_tile.size()) - 1;  // merges per epoch
+    const bool ex = N > 1 && (c.nccl || c.local);
+    if (n4 >= (int64_t{1} << 32)) throw std::invalid_argument("QDELTA: n_items x row stride must stay below 2^34");
+    const dim3 gq = qdelta_grid(n4);
+    const uint32_t u4 = static_cast<uint32_t>(n4), l4 = static_cast<uint32_t>(kc / 4), ld4 = static_cast<uint32_t>(ld / 4);
+    // merge m's all-reduce has come in (on the compute stream after ev_ar) and the GlobalBias fold of its partials
+    auto arrived = [&](int32_t m) {
+        const int32_t par = m & 1;
+        if (c.nccl) RS_HIP(hipStreamWaitEvent(s, c.ev_ar[par], 0));
+        hipLaunchKernelGGL(gb_fold_blocks_kernel, dim3(1), dim3(64), 0, s, pl->gb.p,
+                           (c.nccl ? c.gbs.p : c.gbs_sum.p) + par, 1, inv_total);
+        RS_HIP(hipGetLastError());
+    };
     q_convert(pl, s, 1);
-    for (int32_t e = 0; e < n_epochs * nb; ++e) {
-        const int32_t b = e % nb;
-        if (ni > 0) RS_HIP(hipMemcpyAsync(c.q0.p, Qi, static_cast<size_t>(ni) * ld * sizeof(int32_t), hipMemcpyDeviceToDevice, s));
+    if (ex && nq > 0)  // Q0 = Q (no correction pending)
+        hipLaunchKernelGGL(qdelta_correct_kernel<32>, gq, dim3(256), 0, s, Qi, nullptr, nullptr, c.q0.p, u4, l4, ld4, fx);
+    const int32_t n_merges = n_epochs * nb;
+    for (int32_t m = 0; m < n_merges; ++m) {
+        const int32_t b = m % nb, par = m & 1;
         const int32_t parts = tile_launch_range(pl, lr, reg, s, nullptr, 0, pl->t_block_tile[b], pl->t_block_tile[b + 1]);
         merge_tile_split_rows(pl, pl->t_block_split[b], pl->t_block_split[b + 1], s);
-        gb_sum(pl->partial.p, parts, c.gbs.p, s);
+        gb_sum(pl->partial.p, parts, c.gbs.p + par, s);
         if (pl->fault_sub_epoch == 0) {  // test hook (rs_svd_plan_inject_fault), once
             pl->fault_sub_epoch = -1;
             throw std::runtime_error("injected shard fault (rs_svd_plan_inject_fault)");
         }
+        if (!ex) {
+            hipLaunchKernelGGL(gb_fold_blocks_kernel, dim3(1), dim3(64), 0, s, pl->gb.p, c.gbs.p + par, 1, inv_total);
+            RS_HIP(hipGetLastError());
+            continue;
+        }
+        // this block's moves and the previous merge's correction (its all-reduce ran behind this block)
+        if (m > 0) arrived(m - 1);
+        const int32_t pp = par ^ 1;
         if (nq > 0)
-            hipLaunchKernelGGL(qdelta_moves_kernel, dim3(grid_for(nq)), dim3(256), 0, s, Qi, c.q0.p, c.qw.p, c.dq.p, ni, ld, kw);
+            hipLaunchKernelGGL(h16 ? qdelta_merge_kernel<16> : qdelta_merge_kernel<32>, gq, dim3(256), 0, s, Qi, c.q0.p, c.qw.p,
+                               static_cast<void*>(dq + par * wb), m > 0 ? static_cast<const void*>(dsum + pp * wb) : nullptr,
+                               m > 0 ? static_cast<const void*>(dq + pp * wb) : nullptr, u4, l4, ld4, fx, fx_inv);
         RS_HIP(hipGetLastError());
-        if (c.nccl && N > 1) {
+        if (c.nccl) {  // merge m's all-reduce on the comm stream, behind block m + 1's kernel
             RS_HIP(hipEventRecord(c.ev_gb, s));
             RS_HIP(hipStreamWaitEvent(c.cs, c.ev_gb, 0));
             check_nccl(ncclGroupStart(), "ncclGroupStart");
             if (nq > 0)
-                check_nccl(ncclAllReduce(c.dq.p, c.dq.p, static_cast<size_t>(nq), ncclInt32, ncclSum, c.nccl, c.cs),
-                           "ncclAllReduce(item moves)");
-            check_nccl(ncclAllReduce(c.gbs.p, c.gbs.p, 1, ncclFloat64, ncclSum, c.nccl, c.cs), "ncclAllReduce(GlobalBias)");
+                check_nccl(ncclAllReduce(dq + par * wb, dsum + par * wb, static_cast<size_t>(nq), h16 ? ncclFloat16 : ncclInt32,
+                                         ncclSum, c.nccl, c.cs), "ncclAllReduce(item moves)");
+            check_nccl(ncclAllReduce(c.gbs.p + par, c.gbs.p + par, 1, ncclFloat64, ncclSum, c.nccl, c.cs),
+                       "ncclAllReduce(GlobalBias)");
             check_nccl(ncclGroupEnd(), "ncclGroupEnd");
-            if (nq > 0) hipLaunchKernelGGL(qdelta_apply_kernel, dim3(grid_for(nq)), dim3(256), 0, c.cs, Qi, c.dq.p, ni, ld, kw);
-            hipLaunchKernelGGL(gb_fold_blocks_kernel, dim3(1), dim3(64), 0, c.cs, pl->gb.p, c.gbs.p, 1, inv_total);
-            RS_HIP(hipGetLastError());
-            RS_HIP(hipEventRecord(c.ev_epoch, c.cs));
-            RS_HIP(hipStreamWaitEvent(s, c.ev_epoch, 0));  // the next epoch reads Q and the new GlobalBias
-        } else if (c.local && N > 1) {
+            RS_HIP(hipEventRecord(c.ev_ar[par], c.cs));
+        } else {  // in-process: the sum now (no overlap), applied on the same deferred schedule
             LocalGroup& lg = *c.local;
             RS_HIP(hipStreamSynchronize(s));
             lg.barrier();  // every shard's moves and partial are in place
             Srcs src{};
+            WireSrcs ws{};
             for (int r = 0; r < lg.n; ++r) {
-                src.p[r] = reinterpret_cast<const float4*>(lg.dq[r]);
+                ws.p[r] = reinterpret_cast<const char*>(lg.dq[r]) + par * wb;
                 src.g[r] = lg.gbs[r];
             }
-            if (nq > 0) hipLaunchKernelGGL(qdelta_sum_kernel, dim3(grid_for(nq)), dim3(256), 0, s, src, lg.n, nq, c.dq_sum.p);
-            hipLaunchKernelGGL(local_gb_fold_kernel, dim3(1), dim3(64), 0, s, src, lg.n, 1, pl->gb.p, inv_total);
+            if (nq > 0)
+                hipLaunchKernelGGL(h16 ? qdelta_sum_kernel<16> : qdelta_sum_kernel<32>, gq, dim3(256), 0, s, ws, lg.n, u4,
+                                   static_cast<void*>(dsum + par * wb));
+            hipLaunchKernelGGL(local_sum_kernel, dim3(1), dim3(64), 0, s, src, lg.n, int64_t{0}, int64_t{0},
+                               static_cast<float4*>(nullptr), par, c.gbs_sum.p);
             RS_HIP(hipGetLastError());
             RS_HIP(hipStreamSynchronize(s));
-            lg.barrier();  // every shard has read every shard's moves: the next epoch may overwrite them
-            if (nq > 0) hipLaunchKernelGGL(qdelta_apply_kernel, dim3(grid_for(nq)), dim3(256), 0, s, Qi, c.dq_sum.p, ni, ld, kw);
-        } else {
-            if (nq > 0) hipLaunchKernelGGL(qdelta_apply_kernel, dim3(grid_for(nq)), dim3(256), 0, s, Qi, c.dq.p, ni, ld, kw);
-            hipLaunchKernelGGL(gb_fold_blocks_kernel, dim3(1), dim3(64), 0, s, pl->gb.p, c.gbs.p, 1, inv_total);
+            lg.barrier();  // every shard has read every shard's moves of this parity
         }
+    }
+    if (ex && n_merges > 0) {  // the last merge: every rank's Q is the same again
+        const int32_t par = (n_merges - 1) & 1;
+        arrived(n_merges - 1);
+        if (nq > 0)
+            hipLaunchKernelGGL(h16 ? qdelta_correct_kernel<16> : qdelta_correct_kernel<32>, gq, dim3(256), 0, s, Qi,
+                               static_cast<const void*>(dsum + par * wb), static_cast<const void*>(dq + par * wb),
+                               static_cast<int32_t*>(nullptr), u4, l4, ld4, fx);
         RS_HIP(hipGetLastError());
     }
     // every rank's P range is current on that rank only: broadcast them so P is replicated again
@@ -897,7 +1046,7 @@ void epochs_qdelta(rs_svd_plan* pl, int32_t n_epochs, float lr, float reg, hipSt
 // n_epochs of the item-sharded schedule on stream s (every rank calls it with the same arguments)
 void epochs_sharded(rs_svd_plan* pl, int32_t n_epochs, float lr, float reg, hipStream_t s) {
     if (!pl->tiles_built) tile_build(pl);
-    const int32_t want_gbs = pl->shard->mode == RS_EXCHANGE_QDELTA ? 1 : static_cast<int32_t>(pl->t_block_tile.size()) - 1;
+    const int32_t want_gbs = pl->shard->mode == RS_EXCHANGE_QDELTA ? 2 : static_cast<int32_t>(pl->t_block_tile.size()) - 1;
     if (static_cast<int32_t>(pl->shard->gbs.n) != want_gbs || (pl->shard->mode == RS_EXCHANGE_QDELTA &&
                                                               static_cast<int32_t>(pl->t_block_tile.size()) - 1 != pl->shard->pieces))
         throw std::logic_error("user blocks changed after the join");
@@ -948,6 +1097,8 @@ void group_join(rs_svd_group* g, int32_t n_blocks) {
         if (pl->n_users != nu || pl->k != g->plans[0]->k)
             throw std::invalid_argument("shards must have the same users and n_factors");
         if (pl->exchange != g->plans[0]->exchange) throw std::invalid_argument("shards must use the same exchange");
+        if (qd && pl->qdelta_wire != g->plans[0]->qdelta_wire)
+            throw std::invalid_argument("shards must use the same QDELTA wire width");
         if (rq) {
             if (pl->n_items != ni) throw std::invalid_argument("RS_EXCHANGE_ROTATE_Q / QDELTA shards must have the same items");
             for (int32_t c : pl->h_cols) tot[c] += 1.0;
@@ -1111,6 +1262,14 @@ extern "C" int rs_svd_plan_set_exchange(rs_svd_plan* pl, int32_t mode) {
     return RS_OK;
 }
 
+extern "C" int rs_svd_plan_set_qdelta_wire(rs_svd_plan* pl, int32_t bits) {
+    if (!pl) return rs::set_error(nullptr, RS_ERR_INVALID, "plan is NULL");
+    if (bits != 16 && bits != 32) return rs::set_error(pl->ctx, RS_ERR_INVALID, "QDELTA wire: 16 or 32 bits");
+    if (pl->shard) return rs::set_error(pl->ctx, RS_ERR_INVALID, "plan is joined to a group (leave first)");
+    pl->qdelta_wire = bits;
+    return RS_OK;
+}
+
 // Diagnostic (DESIGN.md Multi-GPU, configs[4]): one epoch of this plan with each user block / stratum of its
 // tile schedule launched on its own and timed (HIP events on the ctx stream) -- the per-stratum kernel
 // times a sharded run's sub-epochs wait on.  Trains the model like an epoch (blocks in order).
@@ -1211,6 +1370,9 @@ extern "C" int rs_svd_plan_join(rs_svd_plan* pl, const void* id, int32_t rank, i
         const size_t shift_at = cnt.size();  // every rank's fixed-point shift: the group runs at the smallest
         cnt.resize(shift_at + static_cast<size_t>(n_ranks), 0.0);
         cnt[shift_at + rank] = static_cast<double>(pl->fx_shift);
+        const size_t wire_at = cnt.size();  // every rank's QDELTA wire width (must agree)
+        cnt.resize(wire_at + static_cast<size_t>(n_ranks), 0.0);
+        cnt[wire_at + rank] = static_cast<double>(pl->qdelta_wire);
         cnt.push_back(static_cast<double>(pl->nnz));
         rs::DevBuf<double> d(cnt.size());
         d.upload(cnt.data(), cnt.size(), s);
@@ -1218,6 +1380,9 @@ extern "C" int rs_svd_plan_join(rs_svd_plan* pl, const void* id, int32_t rank, i
         d.download(cnt.data(), cnt.size(), s);
         RS_HIP(hipStreamSynchronize(s));
         c->total_nnz = cnt.back();
+        for (int32_t r = 0; qd && r < n_ranks; ++r)
+            if (cnt[wire_at + r] != static_cast<double>(pl->qdelta_wire))
+                throw std::invalid_argument("ranks must use the same QDELTA wire width (rs_svd_plan_set_qdelta_wire)");
         for (int32_t r = 0; r < n_ranks; ++r)  // (Q rows travel between ranks as fixed-point words)
             pl->fx_shift = std::min(pl->fx_shift, static_cast<int32_t>(cnt[shift_at + r]));
         if (rq) {
@@ -1367,10 +1532,10 @@ extern "C" int rs_svd_fit_multi(const int32_t* devices, int32_t n_devices, const
     if (r->nnz < 0 || r->n_users < 0 || r->n_items < 0 || (r->nnz > 0 && (!r->users || !r->items || !r->ratings)))
         return rs::set_error(nullptr, RS_ERR_INVALID, "bad ratings");
     const int32_t n = n_devices, k = p->n_factors;
-    // the smaller factor matrix travels -- item shards + P rotation, or user ranges + Q rotation -- where the
-    // bytes matter: a P rank-block of 16 MiB or more (configs[4] at 8 GPUs: 1.6 GB against 160 MB of Q).  Below
-    // that the item shards of north_star stay (ML-1M at 8 shards: 386 KB per rank-block; its Q rotation's
-    // 7k-rating strata hold 5 % of one item each and trained less reliably, DESIGN.md Multi-GPU round 4)
+    // the smaller factor matrix travels -- item shards + P rotation, or user ranges + the item moves' all-reduce
+    // (QDELTA, 16 merges per epoch) -- where the bytes matter: a P rank-block of 16 MiB or more (configs[4] at 8
+    // GPUs: 1.6 GB of P per rotation step against 0.52 GB of fp16 item moves per merge).  Below that the item
+    // shards of north_star stay (ML-1M at 8 shards: 386 KB per rank-block, DESIGN.md Multi-GPU rounds 4-5)
     const size_t p_block = static_cast<size_t>(r->n_users) / static_cast<size_t>(n) * static_cast<size_t>(rs::fast_ld(p->n_factors)) * 4;
     const bool rq = r->n_items < r->n_users && p_block >= (size_t{16} << 20);
     std::vector<int32_t> bounds(static_cast<size_t>(n) + 1);
@@ -1432,7 +1597,7 @@ extern "C" int rs_svd_fit_multi(const int32_t* devices, int32_t n_devices, const
                 if (e != RS_OK) return e;
             }
             if (rq) {
-                e = rs_svd_plan_set_exchange(plans[s], RS_EXCHANGE_ROTATE_Q);
+                e = rs_svd_plan_set_exchange(plans[s], RS_EXCHANGE_QDELTA);
                 if (e != RS_OK) return e;
                 e = rs_svd_plan_upload(plans[s], P, Q, bu, bi, gb);
             } else {

@@ -291,7 +291,7 @@ bool tile_build_device(rs_svd_plan* pl) {
     if (n <= 0 || n >= (int64_t{1} << 31) || !pl->coo_users.p) return false;
     hipStream_t s = pl->ctx->stream;
     const int32_t nu = pl->n_users, ni = std::max(1, pl->n_items), nw = pl->tile_waves;
-    const int32_t grid0 = pl->tile_wg > 0 ? pl->tile_wg : device_cus(pl->ctx);
+    const int32_t grid0 = tile_grid0(pl);  // (the host build's own function: the two builds agree)
     const int32_t ld = tile_lds_row(pl);
     const int64_t rec_cap = static_cast<int64_t>((kTileLdsBudget - 16 - static_cast<size_t>(ld) * 4) / 16);
     thread_local Pinned4 rb;

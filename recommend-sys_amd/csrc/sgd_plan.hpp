@@ -121,6 +121,7 @@ struct rs_svd_plan {
     std::vector<int32_t> t_block_split;  // block b's split users: t_split_rows[t_block_split[b], t_block_split[b+1])
     std::shared_ptr<rs::ShardComm> shard;  // item-sharded multi-GPU state (multi.hip), or empty
     int32_t exchange = RS_EXCHANGE_ROTATE;  // the multi-GPU exchange a join sets up
+    int32_t qdelta_wire = 16;               // QDELTA: bits per item move on the wire (16: fp16, 32: int32 fixed point)
     int32_t fault_sub_epoch = -1;  // test hook (rs_svd_plan_inject_fault): the next sharded call throws there
     // how tiles are formed (rs_svd_plan_set_tile_rule): RS_TILE_RULE_LPT (host: LPT by ratings + cost
     // refinement), RS_TILE_RULE_FILL (host: users by degree dealt boustrophedon), RS_TILE_RULE_FILL_DEVICE
@@ -276,6 +277,7 @@ __host__ __device__ inline uint32_t run_key(int32_t item, int32_t tile) {
 }
 constexpr int32_t kFillSnakeRounds = 4;  // RS_TILE_RULE_FILL: boustrophedon rounds before the deficit fill
 int32_t device_cus(const rs_ctx* ctx);
+int32_t tile_grid0(const rs_svd_plan* pl);  // the tile launch's workgroups (tile_wg, or the library's choice)
 // the run cap the library picks (see auto_run_cap, sgd_tile.hip) from the item degree maximum
 int32_t run_cap_rule(int64_t nnz, int64_t dmax_item, int32_t grid, int32_t waves, int32_t k);
 void tile_build(rs_svd_plan* pl);  // (re)builds the tile schedule (host CSR, or the device for RS_TILE_RULE_FILL_DEVICE)

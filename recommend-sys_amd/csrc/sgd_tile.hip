@@ -924,6 +924,22 @@ int32_t device_cus(const rs_ctx* ctx) {
     return cus;
 }
 
+// Workgroups of the tile launch when the caller leaves them to the library (tile_wg = 0).  The epoch is bound by
+// the memory-side atomic unit -- one row atomic per (item, tile) run, DESIGN.md K1 round 5 -- and fewer tiles mean
+// fewer runs, so a schedule whose tiles are set by the ratings target (they fit the LDS at nnz / grid ratings
+// each) runs on 11/16 of the CUs: ML-1M shape, k = 100 (profiles/r05/k1_workgroups_sweep2.log): 256 / 192 / 176
+// / 160 / 144 workgroups -> 176.5 / 154.0 / 146.8 / 147.1 / 158.5 us per epoch, held-out RMSE 0.6683-0.6686
+// throughout; 128 and fewer run two tiles per workgroup (the LDS) and take 292-298 us.  A schedule whose tiles
+// the LDS sets (configs[4]: 10M users) keeps every CU: its run count does not depend on the grid.  The host and
+// the device builds use this same function of (n_users, nnz, k).
+int32_t tile_grid0(const rs_svd_plan* pl) {
+    if (pl->tile_wg > 0) return pl->tile_wg;
+    const int32_t cus = device_cus(pl->ctx);
+    const int32_t g = std::max(1, cus * 11 / 16);
+    const double bytes = static_cast<double>(pl->n_users) * tile_lds_row(pl) * 4.0 + 16.0 * static_cast<double>(pl->nnz);
+    return bytes / (0.85 * static_cast<double>(kTileLdsBudget)) <= static_cast<double>(g) ? g : cus;
+}
+
 namespace {
 
 // Ratings per tile: nnz / workgroups, but at least the heaviest user's ratings (cutting users into
@@ -1086,7 +1102,7 @@ int32_t tile_partials(const rs_svd_plan* pl) { return std::max(1, pl->tile_grid)
 int32_t tile_cap_in_use(const rs_svd_plan* pl) {
     ensure_host_csr(const_cast<rs_svd_plan*>(pl));
     if (pl->tile_run_cap > 0) return pl->tile_run_cap;
-    const int32_t grid0 = pl->tile_wg > 0 ? pl->tile_wg : device_cus(pl->ctx);
+    const int32_t grid0 = tile_grid0(pl);
     const int32_t c = auto_run_cap(pl, grid0, pl->tile_waves);
     if (c > 0) return c;
     std::vector<int64_t> deg(std::max(1, pl->n_items), 0);  // uncut: the longest run is at most an item's degree
@@ -1103,8 +1119,7 @@ void tile_build(rs_svd_plan* pl) {
     }
     ensure_host_csr(pl);
     hipStream_t s = pl->ctx->stream;
-    const int32_t cus = device_cus(pl->ctx);
-    const int32_t grid0 = pl->tile_wg > 0 ? pl->tile_wg : cus;
+    const int32_t grid0 = tile_grid0(pl);
     TileHost th;
     build_tile_blocks(pl, grid0, false, th, pl->t_block_tile, pl->t_block_user, &pl->t_block_split);
     plan_sync_last(pl);
@@ -1156,8 +1171,7 @@ void tile_build(rs_svd_plan* pl) {
 
 void tile_order(rs_svd_plan* pl, int64_t* pos, int64_t* work_off, int32_t* n_works) {
     ensure_host_csr(pl);
-    const int32_t cus = device_cus(pl->ctx);
-    const int32_t grid0 = pl->tile_wg > 0 ? pl->tile_wg : cus;
+    const int32_t grid0 = tile_grid0(pl);
     TileHost th;
     std::vector<int32_t> bt, bu;
     build_tile_blocks(pl, grid0, true, th, bt, bu);

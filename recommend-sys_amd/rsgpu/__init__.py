@@ -46,7 +46,7 @@ HEADER_SYMBOLS = (
     "rs_svd_plan_set_tile_rule", "rs_svd_plan_tile_rule", "rs_svd_plan_set_guard", "rs_svd_plan_refits", "rs_svd_plan_schedule_digest", "rs_fit_schedule_digest",
     "rs_comm_unique_id", "rs_svd_plan_join", "rs_svd_plan_epochs_sharded", "rs_svd_plan_leave",
     "rs_svd_plan_set_user_blocks", "rs_svd_group_create", "rs_svd_group_epochs", "rs_svd_group_destroy",
-    "rs_item_shards", "rs_svd_fit_multi", "rs_tile_schedule_host", "rs_svd_plan_set_exchange",
+    "rs_item_shards", "rs_svd_fit_multi", "rs_tile_schedule_host", "rs_svd_plan_set_exchange", "rs_svd_plan_set_qdelta_wire",
     "rs_comm_info", "rs_rotation_step", "rs_svd_plan_shard_info", "rs_svd_plan_inject_fault",
     "rs_svd_plan_time_blocks", "rs_knn_plan_set_tie_order", "rs_fit_refits", "rs_fit_multi_refits",
     "rs_svd_plan_set_hot_split",
@@ -174,6 +174,7 @@ def lib():
             "rs_svd_fit_multi": (C.c_int, [_vp, _i32, C.POINTER(_Ratings), C.POINTER(_SgdParams), _i32,
                                            _vp, _vp, _vp, _vp, _vp]),
             "rs_svd_plan_set_exchange": (C.c_int, [_vp, _i32]),
+            "rs_svd_plan_set_qdelta_wire": (C.c_int, [_vp, _i32]),
             "rs_svd_plan_inject_fault": (C.c_int, [_vp, _i32]),
             "rs_svd_plan_time_blocks": (C.c_int, [_vp, _flt, _flt, _vp, _i32]),
             "rs_knn_plan_set_tie_order": (C.c_int, [_vp, _i32]),
@@ -495,6 +496,10 @@ class SvdPlan:
     def set_exchange(self, mode=EXCHANGE_ROTATE):
         """Multi-GPU exchange a later join / group sets up (rs_svd_plan_set_exchange)."""
         self.ctx.check(lib().rs_svd_plan_set_exchange(self.h, mode))
+
+    def set_qdelta_wire(self, bits):
+        """RS_EXCHANGE_QDELTA's moves on the wire: 16 (fp16, default) or 32 (int32 fixed point; exact sums)."""
+        self.ctx.check(lib().rs_svd_plan_set_qdelta_wire(self.h, bits))
 
     def time_blocks(self, n_blocks, lr=0.005, reg=0.02):
         """One epoch with every user block / stratum launched alone and timed: ms per block

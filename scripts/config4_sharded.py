@@ -83,6 +83,7 @@ def parse(argv=None):
     ap.add_argument("--hot-merge", type=int, default=None, help="0 scaled (default), 1 average, 2 sum")
     ap.add_argument("--exchange", choices=["rotq", "qdelta"], default="rotq",
                     help="RS_EXCHANGE_ROTATE_Q (Q item blocks rotate) or RS_EXCHANGE_QDELTA (one all-reduce of item moves)")
+    ap.add_argument("--wire", type=int, default=16, choices=[16, 32], help="QDELTA moves on the wire: fp16 or int32")
     return ap.parse_args(argv)
 
 
@@ -137,6 +138,8 @@ def run(args, say=log):
     for p in parts:
         pl = ctx.svd_plan_csr(U, I, padded_rowptr(p, U), p["cols"], p["vals"], k)
         pl.set_exchange(rsgpu.EXCHANGE_QDELTA if args.exchange == "qdelta" else rsgpu.EXCHANGE_ROTATE_Q)
+        if args.exchange == "qdelta":
+            pl.set_qdelta_wire(args.wire)
         if args.wg:
             pl.set_tiles(workgroups=args.wg)
         if args.hot_share is not None or args.hot_min is not None or args.hot_merge is not None:
@@ -157,7 +160,8 @@ def run(args, say=log):
         ep_s.append(time.perf_counter() - t)
         curve.append(plans[0].evaluate(hu, hi_, hr)[0])
         log(f"sharded epoch {e + 1}: {ep_s[-1]:.3f} s, held-out RMSE {curve[-1]:.4f}")
-    sh = {"n_shards": n, "exchange": "RS_EXCHANGE_QDELTA" if args.exchange == "qdelta" else "RS_EXCHANGE_ROTATE_Q",
+    sh = {"n_shards": n, "exchange": f"RS_EXCHANGE_QDELTA (wire {args.wire} bits)" if args.exchange == "qdelta"
+          else "RS_EXCHANGE_ROTATE_Q",
           "item_blocks": nblk, "setup_s": t_join,
           "rmse_init": r0, "rmse_per_epoch": curve, "epoch_s_one_gpu": ep_s}
     if whole:
@@ -168,9 +172,10 @@ def run(args, say=log):
         sh["shard_epoch_ms"] = t.tolist()
         sh["shard_epoch_max_ms"] = float(t.max())
         sh["imbalance_max_over_mean"] = float(t.max() / t.mean())
-        sh["allreduce_bytes"] = int(I * (k + 1) * 4)
+        sh["allreduce_bytes_per_merge"] = int(I * ((k + 1 + 3) // 4 * 4) * args.wire // 8)
+        sh["merges_per_epoch"] = nblk
         log(f"shard epochs {t.min():.1f}-{t.max():.1f} ms (max/mean {sh['imbalance_max_over_mean']:.3f}); "
-            f"all-reduce of {sh['allreduce_bytes'] / 1e9:.2f} GB per epoch")
+            f"{nblk} all-reduces of {sh['allreduce_bytes_per_merge'] / 1e9:.2f} GB per epoch")
     elif args.strata:  # per-stratum kernel times: shard g trains item rank-block (g + s) mod n in sub-epoch s
         pieces = nblk // n
         t = np.array([pl.time_blocks(nblk, LR, REG) for pl in plans])  # [shard, item block] ms

@@ -1,8 +1,8 @@
 """BASELINE configs[4] as a sharded fit at its own size, on one MI355X: SVD nFactors=256 on
 the synthetic 10M users x 1M items x ~1e9 ratings set (rs_synth, seed 20250826), library defaults, 8 shards
-through the in-process group (RS_EXCHANGE_ROTATE_Q: user ranges stay, Q item rank-blocks rotate; the Zipf
-head's items split into per-block copies), beside the whole set fitted by one plan from the same factors.
-Reference loop: core/svd.go:92-130.
+through the in-process group with the exchange bench.py's strong_scaling and rs_svd_fit_multi run there
+(RS_EXCHANGE_QDELTA: user ranges, 16 merges per epoch of the ranks' weighted item moves, fp16 wire), beside
+the whole set fitted by one plan from the same factors.  Reference loop: core/svd.go:92-130.
 
 About three minutes on the box (generation ~35 s, the two plans ~55 s, 2 x 10 epochs); progress lines go to
 the terminal so the run never looks silent.
@@ -24,7 +24,7 @@ def test_config4_sharded_full_size(request):
     import config4_sharded as C
     tr = request.config.pluginmanager.get_plugin("terminalreporter")
     say = (lambda *a: tr.write_line("  [configs[4]] " + " ".join(str(x) for x in a))) if tr else (lambda *a: None)
-    out = C.run(C.parse(["--epochs", "10"]), say=say)
+    out = C.run(C.parse(["--epochs", "10", "--exchange", "qdelta"]), say=say)
     whole, sh = out["whole"], out["sharded"]
     assert out["nnz_train"] > 9.9e8 and out["n_users"] == 10_000_000 and out["n_items"] == 1_000_000
     assert sh["finite"] and all(np.isfinite(x) for x in sh["rmse_per_epoch"])

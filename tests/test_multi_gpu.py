@@ -277,9 +277,10 @@ def test_qdelta_one_wave_equals_host_model(ctx, ml100k, n_shards, merges):
         pl = ctx.svd_plan(rsgpu.Ratings(su, si, sr, nu, ni), k)
         pl.set_tiles(workgroups=1, waves=1)
         pl.set_exchange(rsgpu.EXCHANGE_QDELTA)
+        pl.set_qdelta_wire(32)  # exact integer sums (the fp16 wire: test_qdelta_fp16_wire_tracks_int32)
         pl.upload(P0, Q0, np.zeros(nu), np.zeros(ni), 3.5)
         plans.append(pl)
-    g = rsgpu.SvdGroup(plans, n_blocks=merges if merges > 1 else 0)
+    g = rsgpu.SvdGroup(plans, n_blocks=merges)
     assert all(pl.shard_info()[2] == rsgpu.EXCHANGE_QDELTA for pl in plans)
     g.epochs(epochs, lr=lr)
     works = []  # per shard and merge: (users, items, ratings, work offsets) in the shard's visit order
@@ -300,20 +301,32 @@ def test_qdelta_one_wave_equals_host_model(ctx, ml100k, n_shards, merges):
             per[b] = (uu[sel], ii[sel], r_[sel], wo)
         works.append(per)
     w = _qdelta_weights(i, [x[1] for x in sh], ni, lr, merges)
-    P, Q, bu, bi, gb = P0.copy(), Q0.copy(), np.zeros(nu), np.zeros(ni), 3.5
-    for _ in range(epochs):
-        for b in range(merges):
-            mQ, mb, part = np.zeros_like(Q), np.zeros_like(bi), 0.0
-            for per in works:
-                uu, ii, r_, off = per[b]
-                if len(r_) == 0:
-                    continue
-                P, Qg, bu, big, gg = O.svd_fit_works(uu, ii, r_, off, P, Q, bu, bi, gb, epochs=1, lr=lr)
-                mQ += Qg - Q
-                mb += big - bi
-                part += (gg - gb) * len(r_)
-            Q, bi = Q + w[:, None] * mQ, bi + w * mb
-            gb += part / len(r)
+    # pipelined merges (csrc/multi.hip epochs_qdelta): each shard keeps its own weighted moves at once and adds
+    # the other shards' (and the GlobalBias fold) of merge m - 1 after its block m -- the all-reduce overlaps it
+    P, bu, gb = P0.copy(), np.zeros(nu), 3.5
+    Qs, bis = [Q0.copy() for _ in sh], [np.zeros(ni) for _ in sh]
+    prev = None
+    for m in range(epochs * merges):
+        b = m % merges
+        dQ, dB, part = [], [], 0.0
+        for x, per in enumerate(works):
+            uu, ii, r_, off = per[b]
+            if len(r_) == 0:
+                dQ.append(np.zeros_like(Q0))
+                dB.append(np.zeros(ni))
+                continue
+            P, Qg, bu, big, gg = O.svd_fit_works(uu, ii, r_, off, P, Qs[x], bu, bis[x], gb, epochs=1, lr=lr)
+            dQ.append(w[:, None] * (Qg - Qs[x]))
+            dB.append(w * (big - bis[x]))
+            Qs[x], bis[x] = Qs[x] + dQ[x], bis[x] + dB[x]
+            part += (gg - gb) * len(r_)
+        cur = (dQ, dB, sum(dQ), sum(dB), part)
+        for c_ in ([prev] if prev else []) + ([cur] if m == epochs * merges - 1 else []):
+            for x in range(len(sh)):
+                Qs[x], bis[x] = Qs[x] + c_[2] - c_[0][x], bis[x] + c_[3] - c_[1][x]
+            gb += c_[4] / len(r)
+        prev = cur
+    Q, bi = Qs[0], bis[0]
     g.close()
     got = [pl.download() for pl in plans]
     for pl in plans:
@@ -321,6 +334,42 @@ def test_qdelta_one_wave_equals_host_model(ctx, ml100k, n_shards, merges):
     assert _maxdiff((P, Q, bu, bi), got[0][:4]) <= TOL and abs(gb - got[0][4]) <= TOL
     for y in got[1:]:
         assert all(np.array_equal(got[0][x], y[x]) for x in range(4)) and got[0][4] == y[4]
+
+
+@pytest.mark.parametrize("n_shards,merges", [(2, 1), (4, 3)])
+def test_qdelta_fp16_wire_tracks_int32(ctx, ml100k, n_shards, merges):
+    """The default fp16 wire (rs_svd_plan_set_qdelta_wire 16): every shard ends with the same bits (each applies
+    the same rounded moves), and the fit stays within 2e-3 of the exact int32-wire fit (fp16 keeps 11 bits of
+    each merge's move) with held-out RMSE within 1e-3 of it."""
+    f = folds(*ml100k)[1]
+    u, i, r, nu, ni = f.iu, f.ii, f.r, f.nu, f.ni
+    k, lr, epochs = 32, 0.005, 5
+    rng = np.random.default_rng(7)
+    P0, Q0 = rng.normal(0, 0.1, (nu, k)), rng.normal(0, 0.1, (ni, k))
+    sh = _user_shards(u, i, r, nu, n_shards)
+    res = {}
+    for bits in (32, 16):
+        plans = []
+        for su, si, sr in sh:
+            pl = ctx.svd_plan(rsgpu.Ratings(su, si, sr, nu, ni), k)
+            pl.set_tiles(workgroups=1, waves=1)  # deterministic: the two runs differ only by the wire
+            pl.set_exchange(rsgpu.EXCHANGE_QDELTA)
+            pl.set_qdelta_wire(bits)
+            pl.upload(P0, Q0, np.zeros(nu), np.zeros(ni), float(np.mean(r)))
+            plans.append(pl)
+        g = rsgpu.SvdGroup(plans, n_blocks=merges)
+        g.epochs(epochs, lr=lr)
+        g.close()
+        got = [pl.download() for pl in plans]
+        for y in got[1:]:
+            bad = [(x, float(np.max(np.abs(got[0][x] - y[x]))), int(np.sum(got[0][x] != y[x]))) for x in range(4)
+                   if not np.array_equal(got[0][x], y[x])]
+            assert not bad and got[0][4] == y[4], (bits, bad, got[0][4], y[4])
+        res[bits] = (got[0], rmse(O.svd_predict(f.tu, f.ti, *got[0]), f.te_r))
+        for pl in plans:
+            pl.close()
+    assert _maxdiff(res[16][0][:4], res[32][0][:4]) <= 2e-3
+    assert abs(res[16][1] - res[32][1]) <= 1e-3, (res[16][1], res[32][1])
 
 
 def test_rotation_fewer_users_than_blocks(ctx):
