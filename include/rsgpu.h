@@ -446,9 +446,12 @@ int rs_svd_plan_apply_delta(rs_svd_plan* plan, const void* dP, const void* gbsum
  * q_i <- q_i,start + sum over ranks of w_i (q_i,end - q_i,start), with w_i = kappa_i / c_i over the c_i ranks
  * that rate item i, kappa_i = (1 - a^(c_i n_i)) / (1 - a^n_i), n_i = its ratings per rank and merge, a = 1 - lr
  * (the moves of a unit-curvature coordinate that c_i ranks each close by 1 - a^n_i, scaled to the sequential
- * 1 - a^(c_i n_i)): exact for items of one rank, the mean of converged moves.  Pipelined: a rank applies its
- * own weighted moves at once and the other ranks' (sum - own) after its next block, so merge m's all-reduce
- * runs behind block m + 1's kernel; after the call's last merge every rank holds the same Q.  The moves travel
+ * 1 - a^(c_i n_i)): exact for items of one rank, the mean of converged moves.  Hot items -- rated on several
+ * ranks, at least 4 ratings per rank and block -- are merged after every block; the others (cold) only after
+ * every cold_every-th block (the largest divisor of the merges per epoch up to 2; rs_svd_plan_set_qdelta_split),
+ * where every item is merged (a full merge), their n_i counted over those blocks.  Pipelined: a rank applies its own weighted moves at
+ * once and the other ranks' (sum - own) at the row's next merge, so merge m's all-reduce runs behind block
+ * m + 1's kernel; the call's last merge is a full one, after which every rank holds the same Q.  The moves travel
  * as fp16 factor units (rs_svd_plan_set_qdelta_wire 16, the default: half the bytes) or int32 fixed point (32:
  * exact integer sums); either way every rank applies the same rounded values.  GlobalBias: the ranks'
  * partials, one f64 all-reduce per merge (applied with the same one-merge delay).  After the call the ranks'
@@ -458,6 +461,11 @@ int rs_svd_plan_set_exchange(rs_svd_plan* plan, int32_t mode);
 /* RS_EXCHANGE_QDELTA's wire width: 16 (fp16 moves, default) or 32 (int32 fixed point).  Set before the join;
  * every rank of a group must use the same width (the join checks). */
 int rs_svd_plan_set_qdelta_wire(rs_svd_plan* plan, int32_t bits);
+/* RS_EXCHANGE_QDELTA's hot / cold split: items rated on several ranks with at least hot_ratings ratings per rank
+ * and block are hot (merged after every block; hot_ratings <= 0: every such item); the others are merged after
+ * every cold_every-th block (the largest divisor of the merges per epoch up to cold_every; 1: every merge is a
+ * full one).  Set before the join, the same on every rank. */
+int rs_svd_plan_set_qdelta_split(rs_svd_plan* plan, double hot_ratings, int32_t cold_every);
 /* RS_EXCHANGE_ROTATE_Q on Zipf-headed sets: a stratum (one rank's users x one item block) holds an item's
  * ratings n_blocks-fold concentrated, so the head's rows get many concurrent runs in flight (Hogwild staleness
  * that diverges at lr 0.005; configs[4]: the hottest item is 0.8 % of the set but 12.7 % of its stratum).  An
@@ -492,6 +500,9 @@ int rs_comm_info(int32_t* version, char* path, int32_t path_len);
  * its user blocks in all (any pointer may be NULL). */
 int rs_svd_plan_shard_info(rs_svd_plan* plan, int32_t* rank, int32_t* n_ranks, int32_t* exchange,
                            int32_t* n_blocks);
+/* RS_EXCHANGE_QDELTA's item split of a joined plan: the hot items (merged after every block) and the blocks
+ * between full merges (either pointer may be NULL). */
+int rs_svd_plan_qdelta_info(rs_svd_plan* plan, int32_t* n_hot, int32_t* cold_every);
 #define RS_COMM_ID_BYTES 128
 int rs_comm_unique_id(void* id /* RS_COMM_ID_BYTES */);
 int rs_svd_plan_join(rs_svd_plan* plan, const void* id, int32_t rank, int32_t n_ranks, int32_t n_blocks);

@@ -84,7 +84,8 @@ struct LocalGroup {  // host-barrier exchange between the shards of one process
     std::vector<float*> P;    // ROTATE: every shard's P (rank-blocks are pulled from the neighbour)
     std::vector<float*> Q;    // ROTATE_Q: every shard's Q
     std::vector<float*> hot;  // ROTATE_Q: every shard's partial hot-copy averages
-    std::vector<int32_t*> dq; // QDELTA: every shard's item moves
+    std::vector<int32_t*> dq; // QDELTA: every shard's item moves (full merges)
+    std::vector<int32_t*> hdq;  // QDELTA: every shard's hot-item moves (hot merges)
     std::vector<int> dev;
     void barrier() {
         std::unique_lock<std::mutex> l(m);
@@ -115,8 +116,11 @@ struct ShardComm {
     DevBuf<float> hot_w;              // merge weight per hot item
     DevBuf<float> item_c, item_n;     // QDELTA: per item the ranks that rate it and its ratings over all ranks
     DevBuf<int32_t> q0;               // QDELTA: Q at the block's start (int32 rows of ld)
-    DevBuf<int32_t> dq, dq_sum;       // QDELTA: the weighted moves and their sum (rows of ld, `wire` bits each), two
-                                      // merges' worth (parity m % 2: merge m's all-reduce overlaps block m + 1)
+    DevBuf<int32_t> dq, dq_sum;       // QDELTA full merges: the weighted moves and their sum (`wire` bits each), two
+                                      // merges' worth (parity of the full merge: its all-reduce overlaps the next block)
+    DevBuf<int32_t> hdq, hdq_sum;     // QDELTA hot merges: the same over the hot items' rows
+    DevBuf<int32_t> hot_ids, hot_pos; // QDELTA: the hot items (ascending) and every item's position among them or -1
+    int32_t n_hot = 0, cold_every = 1;  // QDELTA: hot items; a full merge after every cold_every-th block
     int32_t wire = 32;
     hipEvent_t ev_ar[2] = {nullptr, nullptr};  // QDELTA: merge m's all-reduce ended (comm stream)
     DevBuf<float> qw;                 // QDELTA: merge weight per item (for the call's lr)
@@ -163,6 +167,19 @@ void check_nccl(ncclResult_t r, const char* what) {
 // RMSE after 10 epochs against 0.6079 for the whole-set fit: 1 merge 0.6522, 4 merges 0.6239, 8 0.6202, 12
 // 0.6184, 16 0.6167 (pipelined; profiles/r05/config4_qdelta_*.log) -- 16 is the fewest within 0.01.
 constexpr int32_t kQdeltaMerges = 16;
+// QDELTA hot and cold items (rs_svd_plan_set_qdelta_split).  An item rated on several ranks with at least
+// plan->qdelta_hot ratings per rank and block is hot and merged after every block; the others only at the full
+// merges, after every cold_every-th block (the largest divisor of the merges per epoch up to
+// plan->qdelta_cold_every): a cold item's few ratings per block move it little, and a hot merge moves only the
+// hot rows.  configs[4], 8 ranks, 16 merges, held-out RMSE after 10 epochs (whole set 0.6079; every merge full
+// 0.6166, 19.6 ms of merge passes per epoch): hot >= 16 / cold every 4 blocks 0.6198 (52k hot items, 5.6 ms),
+// 16 / 2 0.6177 (10.3 ms), 4 / 4 0.6181 (244k hot, 8.5 ms), 4 / 2 0.6171 (12.2 ms) -- the default --, 1 / 4
+// 0.6166 (996k hot); profiles/r05/config4_qdelta_split_*.log.
+int32_t qdelta_cold_every(int32_t merges, int32_t most) {
+    for (int32_t f = std::min(std::max(1, most), std::max(1, merges)); f > 1; --f)
+        if (merges % f == 0) return f;
+    return 1;
+}
 
 int32_t comm_ctas() {
     static const int v = std::getenv("RSGPU_COMM_CTAS") ? std::atoi(std::getenv("RSGPU_COMM_CTAS")) : 32;
@@ -335,35 +352,47 @@ template <> struct Wire4<16> {
 __device__ inline int4 add4(int4 a, int4 b) { return make_int4(a.x + b.x, a.y + b.y, a.z + b.z, a.w + b.w); }
 __device__ inline int4 sub4(int4 a, int4 b) { return make_int4(a.x - b.x, a.y - b.y, a.z - b.z, a.w - b.w); }
 
-// QDELTA, after a rank's block m, one pass over the items' rows: the raw moves Q - Q0 become weighted moves
-// w_i (Q - Q0) -- what merge m all-reduces --, Q keeps Q0 + its own share plus, when merge m - 1's all-reduce
-// has come in (prev_sum), the other ranks' moves of that merge, prev_sum - prev_dq (exact in int32); Q0 = Q
-// for block m + 1.  Q0 and the wire buffers hold the k + 1 live columns of each row, rounded up to 4 (l4 int4
-// vectors per row; Q's rows are ld4 vectors: the tile kernel pads them to whole 64-column chunks, 320 at
-// k = 256), n4 = n_items x l4.  One vector per thread (grid qdelta_grid: a grid-stride loop over these five
-// streams runs at 4.5-4.7 TB/s, one vector per thread at 5.4-5.5, profiles/r05/qdelta_merge_bench.log).
+// QDELTA, after a rank's block m, one pass over the rows merged at m (every item at a full merge, the hot items at
+// a hot merge; module header): the raw moves Q - Q0 become weighted moves w_i (Q - Q0) -- what merge m
+// all-reduces --, Q keeps Q0 + its own share plus the correction still pending from the row's previous merge
+// (that merge's all-reduced sum - the rank's own moves; exact in int32): for a hot row merge m - 1's (ph: the
+// full buffers, item-indexed, or the hot buffers, hot-position-indexed), for a cold row the previous full
+// merge's (pc, item-indexed); Q0 = Q for the row's next merge.  Q0 and the wire buffers hold the k + 1 live
+// columns of each row rounded up to 4 (l4 int4 vectors per row; Q's rows are ld4 vectors: the tile kernel pads
+// them to whole 64-column chunks, 320 at k = 256).  rows: the hot items (n4 = n_hot x l4, dq hot-indexed) or
+// nullptr (every item, n4 = n_items x l4, dq item-indexed); hpos: every item's hot position or -1.  One vector
+// per thread (a grid-stride loop over these five streams runs at 4.5-4.7 TB/s, one vector per thread at 5.4-5.5,
+// profiles/r05/qdelta_merge_bench.log).
 template <int B>
 __global__ __launch_bounds__(256) void qdelta_merge_kernel(int32_t* __restrict__ Q, int32_t* __restrict__ Q0,
                                                            const float* __restrict__ w, void* __restrict__ dq,
-                                                           const void* __restrict__ prev_sum,
-                                                           const void* __restrict__ prev_dq, uint32_t n4, uint32_t l4,
+                                                           const int32_t* __restrict__ rows, const int32_t* __restrict__ hpos,
+                                                           const void* __restrict__ ph_sum, const void* __restrict__ ph_dq,
+                                                           int32_t ph_full, const void* __restrict__ pc_sum,
+                                                           const void* __restrict__ pc_dq, uint32_t n4, uint32_t l4,
                                                            uint32_t ld4, float fx, float fx_inv) {
     using W = Wire4<B>;
     using T = typename W::T;
-    int4* const z4 = reinterpret_cast<int4*>(Q0);
     const uint32_t t = blockIdx.x * 256u + threadIdx.x;
     if (t < n4) {
-        const uint32_t i = t / l4;
-        int4& qv = reinterpret_cast<int4*>(Q)[static_cast<size_t>(i) * ld4 + (t - i * l4)];  // the same vector in Q
-        const int4 q = qv, q0 = z4[t];
+        const uint32_t r = t / l4, c4 = t - r * l4;
+        const uint32_t i = rows ? static_cast<uint32_t>(rows[r]) : r;
+        const size_t ti = static_cast<size_t>(i) * l4 + c4;  // the row's vector in the item-indexed buffers
+        int4& qv = reinterpret_cast<int4*>(Q)[static_cast<size_t>(i) * ld4 + c4];
+        int4& zv = reinterpret_cast<int4*>(Q0)[ti];
+        const int4 q = qv, q0 = zv;
         int4 own;
         reinterpret_cast<T*>(dq)[t] = W::make(sub4(q, q0), w[i], fx, fx_inv, own);
         int4 v = add4(q0, own);
-        if (prev_sum)
-            v = add4(v, sub4(W::fixed(reinterpret_cast<const T*>(prev_sum)[t], fx),
-                             W::fixed(reinterpret_cast<const T*>(prev_dq)[t], fx)));
+        const int32_t hp = rows ? static_cast<int32_t>(r) : (hpos ? hpos[i] : -1);
+        const void* ps = hp >= 0 ? ph_sum : pc_sum;
+        const void* pd = hp >= 0 ? ph_dq : pc_dq;
+        if (ps) {
+            const size_t pi = (hp >= 0 && !ph_full) ? static_cast<size_t>(hp) * l4 + c4 : ti;
+            v = add4(v, sub4(W::fixed(reinterpret_cast<const T*>(ps)[pi], fx), W::fixed(reinterpret_cast<const T*>(pd)[pi], fx)));
+        }
         qv = v;
-        z4[t] = v;
+        zv = v;
     }
 }
 inline dim3 qdelta_grid(int64_t n4) { return dim3(static_cast<uint32_t>(std::max<int64_t>(1, (n4 + 255) / 256))); }
@@ -523,6 +552,18 @@ void shard_setup(rs_svd_plan* pl, ShardComm& c, int32_t n_blocks, const std::vec
         }
         tile_build(pl);
         c.pieces = static_cast<int32_t>(pl->t_block_tile.size()) - 1;  // merges per epoch
+        c.cold_every = qdelta_cold_every(c.pieces, pl->qdelta_cold_every);
+        std::vector<int32_t> hot, hpos(ni, -1);
+        for (int32_t x = 0; c.cold_every > 1 && x < pl->n_items; ++x)
+            if (cc[x] > 1.f && static_cast<double>(cn[x]) / (static_cast<double>(cc[x]) * c.pieces) >= pl->qdelta_hot) {
+                hpos[x] = static_cast<int32_t>(hot.size());
+                hot.push_back(x);
+            }
+        c.n_hot = static_cast<int32_t>(hot.size());
+        c.hot_pos.alloc(ni);
+        c.hot_pos.upload(hpos.data(), ni, pl->ctx->stream);
+        c.hot_ids.alloc(std::max<size_t>(1, hot.size()));
+        if (!hot.empty()) c.hot_ids.upload(hot.data(), hot.size(), pl->ctx->stream);
         c.gbs.alloc(2);
         if (c.local) c.gbs_sum.alloc(2);
         if (c.nccl) {
@@ -533,9 +574,12 @@ void shard_setup(rs_svd_plan* pl, ShardComm& c, int32_t n_blocks, const std::vec
         }
         const size_t nq = ni * static_cast<size_t>(round_up4(pl->k + 1));  // the live columns, whole int4 vectors
         c.wire = pl->qdelta_wire;
+        const size_t nh = static_cast<size_t>(std::max(1, c.n_hot)) * static_cast<size_t>(round_up4(pl->k + 1));
         c.q0.alloc(nq);
         c.dq.alloc(2 * nq * c.wire / 32);
         c.dq_sum.alloc(2 * nq * c.wire / 32);
+        c.hdq.alloc(2 * nh * c.wire / 32);
+        c.hdq_sum.alloc(2 * nh * c.wire / 32);
         RS_HIP(hipStreamSynchronize(pl->ctx->stream));
         return;
     }
@@ -903,26 +947,35 @@ void epochs_rotate(rs_svd_plan* pl, int32_t n_epochs, float lr, float reg, hipSt
     q_convert(pl, s, 0);
 }
 
-// QDELTA: n_epochs of the user-range epochs with one all-reduce of the item moves per epoch, on stream s
+// QDELTA: n_epochs of the user-range epochs, the item moves all-reduced after every block (hot items) or every
+// cold_every-th block (every item), each all-reduce behind the next block's kernel; on stream s
 void epochs_qdelta(rs_svd_plan* pl, int32_t n_epochs, float lr, float reg, hipStream_t s) {
     ShardComm& c = *pl->shard;
     const int32_t N = c.nranks, ni = pl->n_items, ld = pl->ld, kc = round_up4(pl->k + 1);
-    const int64_t nq = static_cast<int64_t>(ni) * kc, n4 = nq / 4;  // wire values per merge (k + 1 live columns), vectors
-    const size_t wb = static_cast<size_t>(nq) * (c.wire / 8);        // wire bytes per merge
+    const int64_t nq = static_cast<int64_t>(ni) * kc, n4 = nq / 4;  // wire values of a full merge, vectors
+    const int64_t nqh = static_cast<int64_t>(c.n_hot) * kc, n4h = nqh / 4;  // of a hot merge
+    const size_t wb = static_cast<size_t>(nq) * (c.wire / 8), wbh = static_cast<size_t>(nqh) * (c.wire / 8);
     const bool h16 = c.wire == 16;
     const float fx = pl->fx(), fx_inv = pl->fx_inv();
     char* const dq = reinterpret_cast<char*>(c.dq.p);
     char* const dsum = reinterpret_cast<char*>(c.dq_sum.p);
+    char* const hdq = reinterpret_cast<char*>(c.hdq.p);
+    char* const hsum = reinterpret_cast<char*>(c.hdq_sum.p);
     const double inv_total = c.total_nnz > 0 ? 1.0 / c.total_nnz : 0.0;
+    const int32_t nb = static_cast<int32_t>(pl->t_block_tile.size()) - 1;  // blocks per epoch
+    const int32_t F = c.cold_every;
     if (c.qw_lr != lr) {  // the merge weights for this lr (module header: kappa / c per item)
         const size_t n1 = static_cast<size_t>(std::max(1, ni));
         std::vector<float> cn(n1), cc(n1), w(n1, 1.f);
+        std::vector<int32_t> hp(n1);
         c.item_n.download(cn.data(), n1, s);
         c.item_c.download(cc.data(), n1, s);
+        c.hot_pos.download(hp.data(), n1, s);
         RS_HIP(hipStreamSynchronize(s));
         const double a = std::max(1e-12, 1.0 - static_cast<double>(lr));
-        const double merges = static_cast<double>(std::max(1, c.pieces));  // the moves of 1 / merges of an epoch
         for (size_t x = 0; x < static_cast<size_t>(ni); ++x) {
+            // the moves of 1 / merges of an epoch: every block's for a hot item, cold_every blocks' for a cold one
+            const double merges = static_cast<double>(std::max(1, hp[x] >= 0 ? nb : nb / F));
             const double cp = std::max(1.0, static_cast<double>(cc[x])), n = static_cast<double>(cn[x]) / cp / merges;
             if (cp <= 1.0 || n <= 0.0) continue;
             const double kappa = (1.0 - std::pow(a, cp * n)) / std::max(1e-300, 1.0 - std::pow(a, n));
@@ -934,12 +987,11 @@ void epochs_qdelta(rs_svd_plan* pl, int32_t n_epochs, float lr, float reg, hipSt
         c.qw_lr = lr;
     }
     int32_t* const Qi = reinterpret_cast<int32_t*>(pl->Q.p);
-    const int32_t nb = static_cast<int32_t>(pl->t_block_tile.size()) - 1;  // merges per epoch
     const bool ex = N > 1 && (c.nccl || c.local);
-    if (n4 >= (int64_t{1} << 32)) throw std::invalid_argument("QDELTA: n_items x row stride must stay below 2^34");
-    const dim3 gq = qdelta_grid(n4);
-    const uint32_t u4 = static_cast<uint32_t>(n4), l4 = static_cast<uint32_t>(kc / 4), ld4 = static_cast<uint32_t>(ld / 4);
-    // merge m's all-reduce has come in (on the compute stream after ev_ar) and the GlobalBias fold of its partials
+    if (n4 >= (int64_t{1} << 32)) throw std::invalid_argument("QDELTA: n_items x (k + 1) must stay below 2^34");
+    const uint32_t l4 = static_cast<uint32_t>(kc / 4), ld4 = static_cast<uint32_t>(ld / 4);
+    // merge m's all-reduce has come in (on the compute stream after ev_ar; the comm stream is in order, so every
+    // earlier one too) and the GlobalBias fold of its partials
     auto arrived = [&](int32_t m) {
         const int32_t par = m & 1;
         if (c.nccl) RS_HIP(hipStreamWaitEvent(s, c.ev_ar[par], 0));
@@ -949,10 +1001,14 @@ void epochs_qdelta(rs_svd_plan* pl, int32_t n_epochs, float lr, float reg, hipSt
     };
     q_convert(pl, s, 1);
     if (ex && nq > 0)  // Q0 = Q (no correction pending)
-        hipLaunchKernelGGL(qdelta_correct_kernel<32>, gq, dim3(256), 0, s, Qi, nullptr, nullptr, c.q0.p, u4, l4, ld4, fx);
+        hipLaunchKernelGGL(qdelta_correct_kernel<32>, qdelta_grid(n4), dim3(256), 0, s, Qi, nullptr, nullptr, c.q0.p,
+                           static_cast<uint32_t>(n4), l4, ld4, fx);
     const int32_t n_merges = n_epochs * nb;
+    int32_t f = 0, h = 0;         // full and hot merges so far (buffer parities)
+    bool prev_full = false;       // merge m - 1 was a full merge
     for (int32_t m = 0; m < n_merges; ++m) {
         const int32_t b = m % nb, par = m & 1;
+        const bool full = b % F == F - 1;  // (nb is a multiple of F: every call ends with a full merge)
         const int32_t parts = tile_launch_range(pl, lr, reg, s, nullptr, 0, pl->t_block_tile[b], pl->t_block_tile[b + 1]);
         merge_tile_split_rows(pl, pl->t_block_split[b], pl->t_block_split[b + 1], s);
         gb_sum(pl->partial.p, parts, c.gbs.p + par, s);
@@ -965,21 +1021,41 @@ void epochs_qdelta(rs_svd_plan* pl, int32_t n_epochs, float lr, float reg, hipSt
             RS_HIP(hipGetLastError());
             continue;
         }
-        // this block's moves and the previous merge's correction (its all-reduce ran behind this block)
+        // this merge's rows: their moves and the corrections pending from their previous merges (whose all-reduces
+        // ran behind this block): a hot row's from merge m - 1, a cold row's from the last full merge
         if (m > 0) arrived(m - 1);
-        const int32_t pp = par ^ 1;
-        if (nq > 0)
-            hipLaunchKernelGGL(h16 ? qdelta_merge_kernel<16> : qdelta_merge_kernel<32>, gq, dim3(256), 0, s, Qi, c.q0.p, c.qw.p,
-                               static_cast<void*>(dq + par * wb), m > 0 ? static_cast<const void*>(dsum + pp * wb) : nullptr,
-                               m > 0 ? static_cast<const void*>(dq + pp * wb) : nullptr, u4, l4, ld4, fx, fx_inv);
+        const void* ph_sum = nullptr;
+        const void* ph_dq = nullptr;
+        if (m > 0) {
+            if (prev_full) {
+                ph_sum = dsum + ((f - 1) & 1) * wb;
+                ph_dq = dq + ((f - 1) & 1) * wb;
+            } else {
+                ph_sum = hsum + ((h - 1) & 1) * wbh;
+                ph_dq = hdq + ((h - 1) & 1) * wbh;
+            }
+        }
+        const int64_t m4 = full ? n4 : n4h;
+        char* const out = full ? dq + (f & 1) * wb : hdq + (h & 1) * wbh;
+        if (m4 > 0) {
+            const bool pc = full && f > 0;  // a cold row's pending correction: the previous full merge's
+            hipLaunchKernelGGL(h16 ? qdelta_merge_kernel<16> : qdelta_merge_kernel<32>, qdelta_grid(m4), dim3(256), 0, s, Qi,
+                               c.q0.p, c.qw.p, static_cast<void*>(out), full ? nullptr : c.hot_ids.p,
+                               c.n_hot > 0 ? c.hot_pos.p : nullptr, ph_sum, ph_dq, static_cast<int32_t>(prev_full),
+                               pc ? static_cast<const void*>(dsum + ((f - 1) & 1) * wb) : nullptr,
+                               pc ? static_cast<const void*>(dq + ((f - 1) & 1) * wb) : nullptr, static_cast<uint32_t>(m4),
+                               l4, ld4, fx, fx_inv);
+        }
         RS_HIP(hipGetLastError());
+        char* const sum_out = full ? dsum + (f & 1) * wb : hsum + (h & 1) * wbh;
+        const int64_t mq = full ? nq : nqh;
         if (c.nccl) {  // merge m's all-reduce on the comm stream, behind block m + 1's kernel
             RS_HIP(hipEventRecord(c.ev_gb, s));
             RS_HIP(hipStreamWaitEvent(c.cs, c.ev_gb, 0));
             check_nccl(ncclGroupStart(), "ncclGroupStart");
-            if (nq > 0)
-                check_nccl(ncclAllReduce(dq + par * wb, dsum + par * wb, static_cast<size_t>(nq), h16 ? ncclFloat16 : ncclInt32,
-                                         ncclSum, c.nccl, c.cs), "ncclAllReduce(item moves)");
+            if (mq > 0)
+                check_nccl(ncclAllReduce(out, sum_out, static_cast<size_t>(mq), h16 ? ncclFloat16 : ncclInt32, ncclSum, c.nccl,
+                                         c.cs), "ncclAllReduce(item moves)");
             check_nccl(ncclAllReduce(c.gbs.p + par, c.gbs.p + par, 1, ncclFloat64, ncclSum, c.nccl, c.cs),
                        "ncclAllReduce(GlobalBias)");
             check_nccl(ncclGroupEnd(), "ncclGroupEnd");
@@ -991,26 +1067,30 @@ void epochs_qdelta(rs_svd_plan* pl, int32_t n_epochs, float lr, float reg, hipSt
             Srcs src{};
             WireSrcs ws{};
             for (int r = 0; r < lg.n; ++r) {
-                ws.p[r] = reinterpret_cast<const char*>(lg.dq[r]) + par * wb;
+                ws.p[r] = full ? reinterpret_cast<const char*>(lg.dq[r]) + (f & 1) * wb
+                               : reinterpret_cast<const char*>(lg.hdq[r]) + (h & 1) * wbh;
                 src.g[r] = lg.gbs[r];
             }
-            if (nq > 0)
-                hipLaunchKernelGGL(h16 ? qdelta_sum_kernel<16> : qdelta_sum_kernel<32>, gq, dim3(256), 0, s, ws, lg.n, u4,
-                                   static_cast<void*>(dsum + par * wb));
+            if (m4 > 0)
+                hipLaunchKernelGGL(h16 ? qdelta_sum_kernel<16> : qdelta_sum_kernel<32>, qdelta_grid(m4), dim3(256), 0, s, ws,
+                                   lg.n, static_cast<uint32_t>(m4), static_cast<void*>(sum_out));
             hipLaunchKernelGGL(local_sum_kernel, dim3(1), dim3(64), 0, s, src, lg.n, int64_t{0}, int64_t{0},
                                static_cast<float4*>(nullptr), par, c.gbs_sum.p);
             RS_HIP(hipGetLastError());
             RS_HIP(hipStreamSynchronize(s));
-            lg.barrier();  // every shard has read every shard's moves of this parity
+            lg.barrier();  // every shard has read every shard's moves of this merge
         }
+        if (full) ++f;
+        else ++h;
+        prev_full = full;
     }
-    if (ex && n_merges > 0) {  // the last merge: every rank's Q is the same again
-        const int32_t par = (n_merges - 1) & 1;
+    if (ex && n_merges > 0) {  // the last merge (a full one): every rank's Q is the same again
+        const int32_t fp = (f - 1) & 1;
         arrived(n_merges - 1);
         if (nq > 0)
-            hipLaunchKernelGGL(h16 ? qdelta_correct_kernel<16> : qdelta_correct_kernel<32>, gq, dim3(256), 0, s, Qi,
-                               static_cast<const void*>(dsum + par * wb), static_cast<const void*>(dq + par * wb),
-                               static_cast<int32_t*>(nullptr), u4, l4, ld4, fx);
+            hipLaunchKernelGGL(h16 ? qdelta_correct_kernel<16> : qdelta_correct_kernel<32>, qdelta_grid(n4), dim3(256), 0, s, Qi,
+                               static_cast<const void*>(dsum + fp * wb), static_cast<const void*>(dq + fp * wb),
+                               static_cast<int32_t*>(nullptr), static_cast<uint32_t>(n4), l4, ld4, fx);
         RS_HIP(hipGetLastError());
     }
     // every rank's P range is current on that rank only: broadcast them so P is replicated again
@@ -1097,8 +1177,9 @@ void group_join(rs_svd_group* g, int32_t n_blocks) {
         if (pl->n_users != nu || pl->k != g->plans[0]->k)
             throw std::invalid_argument("shards must have the same users and n_factors");
         if (pl->exchange != g->plans[0]->exchange) throw std::invalid_argument("shards must use the same exchange");
-        if (qd && pl->qdelta_wire != g->plans[0]->qdelta_wire)
-            throw std::invalid_argument("shards must use the same QDELTA wire width");
+        if (qd && (pl->qdelta_wire != g->plans[0]->qdelta_wire || pl->qdelta_hot != g->plans[0]->qdelta_hot ||
+                   pl->qdelta_cold_every != g->plans[0]->qdelta_cold_every))
+            throw std::invalid_argument("shards must use the same QDELTA wire width and split");
         if (rq) {
             if (pl->n_items != ni) throw std::invalid_argument("RS_EXCHANGE_ROTATE_Q / QDELTA shards must have the same items");
             for (int32_t c : pl->h_cols) tot[c] += 1.0;
@@ -1161,6 +1242,7 @@ void group_join(rs_svd_group* g, int32_t n_blocks) {
             g->local->Q.push_back(pl->Q.p);
             g->local->hot.push_back(pl->shard->hot_part.p);
             g->local->dq.push_back(pl->shard->dq.p);
+            g->local->hdq.push_back(pl->shard->hdq.p);
             g->local->dev.push_back(pl->ctx->device);
         }
     }
@@ -1187,6 +1269,15 @@ extern "C" int rs_rotation_step(int32_t rank, int32_t n_ranks, int32_t sub_epoch
     out[1] = r.send_to;
     out[2] = r.recv;
     out[3] = r.recv_from;
+    return RS_OK;
+}
+
+extern "C" int rs_svd_plan_qdelta_info(rs_svd_plan* pl, int32_t* n_hot, int32_t* cold_every) {
+    if (!pl) return rs::set_error(nullptr, RS_ERR_INVALID, "plan is NULL");
+    if (!pl->shard || pl->shard->mode != RS_EXCHANGE_QDELTA)
+        return rs::set_error(pl->ctx, RS_ERR_INVALID, "plan is not joined with RS_EXCHANGE_QDELTA");
+    if (n_hot) *n_hot = pl->shard->n_hot;
+    if (cold_every) *cold_every = pl->shard->cold_every;
     return RS_OK;
 }
 
@@ -1259,6 +1350,15 @@ extern "C" int rs_svd_plan_set_exchange(rs_svd_plan* pl, int32_t mode) {
         return rs::set_error(pl->ctx, RS_ERR_INVALID, "unknown exchange");
     if (pl->shard) return rs::set_error(pl->ctx, RS_ERR_INVALID, "plan is joined to a group (leave first)");
     pl->exchange = mode;
+    return RS_OK;
+}
+
+extern "C" int rs_svd_plan_set_qdelta_split(rs_svd_plan* pl, double hot_ratings, int32_t cold_every) {
+    if (!pl) return rs::set_error(nullptr, RS_ERR_INVALID, "plan is NULL");
+    if (cold_every < 1 || !std::isfinite(hot_ratings)) return rs::set_error(pl->ctx, RS_ERR_INVALID, "bad QDELTA split");
+    if (pl->shard) return rs::set_error(pl->ctx, RS_ERR_INVALID, "plan is joined to a group (leave first)");
+    pl->qdelta_hot = hot_ratings;
+    pl->qdelta_cold_every = cold_every;
     return RS_OK;
 }
 
@@ -1370,9 +1470,11 @@ extern "C" int rs_svd_plan_join(rs_svd_plan* pl, const void* id, int32_t rank, i
         const size_t shift_at = cnt.size();  // every rank's fixed-point shift: the group runs at the smallest
         cnt.resize(shift_at + static_cast<size_t>(n_ranks), 0.0);
         cnt[shift_at + rank] = static_cast<double>(pl->fx_shift);
-        const size_t wire_at = cnt.size();  // every rank's QDELTA wire width (must agree)
-        cnt.resize(wire_at + static_cast<size_t>(n_ranks), 0.0);
-        cnt[wire_at + rank] = static_cast<double>(pl->qdelta_wire);
+        const size_t wire_at = cnt.size();  // every rank's QDELTA settings (must agree): wire, split
+        cnt.resize(wire_at + 3 * static_cast<size_t>(n_ranks), 0.0);
+        cnt[wire_at + 3 * rank] = static_cast<double>(pl->qdelta_wire);
+        cnt[wire_at + 3 * rank + 1] = pl->qdelta_hot;
+        cnt[wire_at + 3 * rank + 2] = static_cast<double>(pl->qdelta_cold_every);
         cnt.push_back(static_cast<double>(pl->nnz));
         rs::DevBuf<double> d(cnt.size());
         d.upload(cnt.data(), cnt.size(), s);
@@ -1381,8 +1483,10 @@ extern "C" int rs_svd_plan_join(rs_svd_plan* pl, const void* id, int32_t rank, i
         RS_HIP(hipStreamSynchronize(s));
         c->total_nnz = cnt.back();
         for (int32_t r = 0; qd && r < n_ranks; ++r)
-            if (cnt[wire_at + r] != static_cast<double>(pl->qdelta_wire))
-                throw std::invalid_argument("ranks must use the same QDELTA wire width (rs_svd_plan_set_qdelta_wire)");
+            if (cnt[wire_at + 3 * r] != static_cast<double>(pl->qdelta_wire) || cnt[wire_at + 3 * r + 1] != pl->qdelta_hot ||
+                cnt[wire_at + 3 * r + 2] != static_cast<double>(pl->qdelta_cold_every))
+                throw std::invalid_argument("ranks must use the same QDELTA wire width and split "
+                                            "(rs_svd_plan_set_qdelta_wire / _split)");
         for (int32_t r = 0; r < n_ranks; ++r)  // (Q rows travel between ranks as fixed-point words)
             pl->fx_shift = std::min(pl->fx_shift, static_cast<int32_t>(cnt[shift_at + r]));
         if (rq) {

@@ -122,6 +122,8 @@ struct rs_svd_plan {
     std::shared_ptr<rs::ShardComm> shard;  // item-sharded multi-GPU state (multi.hip), or empty
     int32_t exchange = RS_EXCHANGE_ROTATE;  // the multi-GPU exchange a join sets up
     int32_t qdelta_wire = 16;               // QDELTA: bits per item move on the wire (16: fp16, 32: int32 fixed point)
+    double qdelta_hot = 4.0;                // QDELTA: ratings per rank and block that make an item hot (<= 0: all hot)
+    int32_t qdelta_cold_every = 2;          // QDELTA: most blocks between a cold item's merges (multi.hip kQdelta*)
     int32_t fault_sub_epoch = -1;  // test hook (rs_svd_plan_inject_fault): the next sharded call throws there
     // how tiles are formed (rs_svd_plan_set_tile_rule): RS_TILE_RULE_LPT (host: LPT by ratings + cost
     // refinement), RS_TILE_RULE_FILL (host: users by degree dealt boustrophedon), RS_TILE_RULE_FILL_DEVICE

@@ -46,8 +46,8 @@ HEADER_SYMBOLS = (
     "rs_svd_plan_set_tile_rule", "rs_svd_plan_tile_rule", "rs_svd_plan_set_guard", "rs_svd_plan_refits", "rs_svd_plan_schedule_digest", "rs_fit_schedule_digest",
     "rs_comm_unique_id", "rs_svd_plan_join", "rs_svd_plan_epochs_sharded", "rs_svd_plan_leave",
     "rs_svd_plan_set_user_blocks", "rs_svd_group_create", "rs_svd_group_epochs", "rs_svd_group_destroy",
-    "rs_item_shards", "rs_svd_fit_multi", "rs_tile_schedule_host", "rs_svd_plan_set_exchange", "rs_svd_plan_set_qdelta_wire",
-    "rs_comm_info", "rs_rotation_step", "rs_svd_plan_shard_info", "rs_svd_plan_inject_fault",
+    "rs_item_shards", "rs_svd_fit_multi", "rs_tile_schedule_host", "rs_svd_plan_set_exchange", "rs_svd_plan_set_qdelta_wire", "rs_svd_plan_set_qdelta_split",
+    "rs_comm_info", "rs_rotation_step", "rs_svd_plan_shard_info", "rs_svd_plan_qdelta_info", "rs_svd_plan_inject_fault",
     "rs_svd_plan_time_blocks", "rs_knn_plan_set_tie_order", "rs_fit_refits", "rs_fit_multi_refits",
     "rs_svd_plan_set_hot_split",
 )
@@ -175,6 +175,7 @@ def lib():
                                            _vp, _vp, _vp, _vp, _vp]),
             "rs_svd_plan_set_exchange": (C.c_int, [_vp, _i32]),
             "rs_svd_plan_set_qdelta_wire": (C.c_int, [_vp, _i32]),
+            "rs_svd_plan_set_qdelta_split": (C.c_int, [_vp, C.c_double, _i32]),
             "rs_svd_plan_inject_fault": (C.c_int, [_vp, _i32]),
             "rs_svd_plan_time_blocks": (C.c_int, [_vp, _flt, _flt, _vp, _i32]),
             "rs_knn_plan_set_tie_order": (C.c_int, [_vp, _i32]),
@@ -185,6 +186,7 @@ def lib():
             "rs_rotation_step": (C.c_int, [_i32, _i32, _i32, _vp]),
             "rs_svd_plan_shard_info": (C.c_int, [_vp, C.POINTER(_i32), C.POINTER(_i32), C.POINTER(_i32),
                                                  C.POINTER(_i32)]),
+            "rs_svd_plan_qdelta_info": (C.c_int, [_vp, C.POINTER(_i32), C.POINTER(_i32)]),
         }
         for name, (res, args) in sig.items():
             f = getattr(L, name)
@@ -497,6 +499,10 @@ class SvdPlan:
         """Multi-GPU exchange a later join / group sets up (rs_svd_plan_set_exchange)."""
         self.ctx.check(lib().rs_svd_plan_set_exchange(self.h, mode))
 
+    def set_qdelta_split(self, hot_ratings, cold_every):
+        """RS_EXCHANGE_QDELTA's hot / cold split (rs_svd_plan_set_qdelta_split)."""
+        self.ctx.check(lib().rs_svd_plan_set_qdelta_split(self.h, float(hot_ratings), int(cold_every)))
+
     def set_qdelta_wire(self, bits):
         """RS_EXCHANGE_QDELTA's moves on the wire: 16 (fp16, default) or 32 (int32 fixed point; exact sums)."""
         self.ctx.check(lib().rs_svd_plan_set_qdelta_wire(self.h, bits))
@@ -528,6 +534,12 @@ class SvdPlan:
         """(rank, n_ranks, exchange, user blocks) of a joined plan; ranks from the RCCL communicator."""
         v = [_i32(0) for _ in range(4)]
         self.ctx.check(lib().rs_svd_plan_shard_info(self.h, *[C.byref(x) for x in v]))
+        return tuple(x.value for x in v)
+
+    def qdelta_info(self):
+        """(hot items, blocks between full merges) of a plan joined with EXCHANGE_QDELTA."""
+        v = [_i32(0) for _ in range(2)]
+        self.ctx.check(lib().rs_svd_plan_qdelta_info(self.h, *[C.byref(x) for x in v]))
         return tuple(x.value for x in v)
 
     def epochs_sharded(self, n, lr=0.005, reg=0.02, stream=None):

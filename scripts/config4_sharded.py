@@ -84,6 +84,8 @@ def parse(argv=None):
     ap.add_argument("--exchange", choices=["rotq", "qdelta"], default="rotq",
                     help="RS_EXCHANGE_ROTATE_Q (Q item blocks rotate) or RS_EXCHANGE_QDELTA (one all-reduce of item moves)")
     ap.add_argument("--wire", type=int, default=16, choices=[16, 32], help="QDELTA moves on the wire: fp16 or int32")
+    ap.add_argument("--hot", type=float, default=None, help="QDELTA hot threshold, ratings per rank and block")
+    ap.add_argument("--cold-every", type=int, default=None, help="QDELTA most blocks between a cold item's merges")
     return ap.parse_args(argv)
 
 
@@ -140,6 +142,8 @@ def run(args, say=log):
         pl.set_exchange(rsgpu.EXCHANGE_QDELTA if args.exchange == "qdelta" else rsgpu.EXCHANGE_ROTATE_Q)
         if args.exchange == "qdelta":
             pl.set_qdelta_wire(args.wire)
+            if args.hot is not None or args.cold_every is not None:
+                pl.set_qdelta_split(16.0 if args.hot is None else args.hot, 4 if args.cold_every is None else args.cold_every)
         if args.wg:
             pl.set_tiles(workgroups=args.wg)
         if args.hot_share is not None or args.hot_min is not None or args.hot_merge is not None:
@@ -151,7 +155,9 @@ def run(args, say=log):
     g = rsgpu.SvdGroup(plans, n_blocks=args.blocks)
     t_join = time.perf_counter() - t0
     _, _, exch, nblk = plans[0].shard_info()
-    log(f"{n} shard plans + group in {t_join:.1f} s: exchange {exch}, {nblk} item blocks")
+    qinfo = plans[0].qdelta_info() if args.exchange == "qdelta" else None
+    log(f"{n} shard plans + group in {t_join:.1f} s: exchange {exch}, {nblk} blocks"
+        + (f", {qinfo[0]} hot items, a full merge every {qinfo[1]} blocks" if qinfo else ""))
     r0 = plans[0].evaluate(hu, hi_, hr)[0]
     curve, ep_s = [], []
     for e in range(args.epochs):
@@ -162,7 +168,8 @@ def run(args, say=log):
         log(f"sharded epoch {e + 1}: {ep_s[-1]:.3f} s, held-out RMSE {curve[-1]:.4f}")
     sh = {"n_shards": n, "exchange": f"RS_EXCHANGE_QDELTA (wire {args.wire} bits)" if args.exchange == "qdelta"
           else "RS_EXCHANGE_ROTATE_Q",
-          "item_blocks": nblk, "setup_s": t_join,
+          "item_blocks": nblk, "setup_s": t_join, "qdelta_hot_items": qinfo[0] if qinfo else None,
+          "qdelta_cold_every": qinfo[1] if qinfo else None,
           "rmse_init": r0, "rmse_per_epoch": curve, "epoch_s_one_gpu": ep_s}
     if whole:
         sh["rmse_diff_vs_whole"] = curve[-1] - whole["rmse_per_epoch"][-1]

@@ -575,30 +575,38 @@ def test_rotation_q_layout_rules():
 QD_MERGES = 2
 
 
-def _qd_weights(i, shard_items, ni, lr, merges):
-    cnt = np.bincount(i, minlength=ni).astype(np.float64)
-    c = np.sum([np.bincount(si, minlength=ni) > 0 for si in shard_items], 0).astype(np.float64)
-    a = 1.0 - float(np.float32(lr))
-    w = np.ones(ni)
-    m = (c > 1) & (cnt > 0)
-    n = cnt[m] / c[m] / merges
-    w[m] = (1.0 - a ** (c[m] * n)) / (1.0 - a ** n) / c[m]
-    return w
+def _qd_data():
+    """A Zipf head over 200 items and 400 users (unique pairs), so that some items pass the hot threshold (4
+    ratings per rank and block) and the tail stays cold."""
+    rng = np.random.default_rng(12)
+    nu, ni, nnz = 400, 200, 4000
+    pop = 1.0 / np.arange(1, ni + 1) ** 1.1
+    pairs = set()
+    while len(pairs) < nnz:
+        pairs.add((int(rng.integers(0, nu)), int(rng.choice(ni, p=pop / pop.sum()))))
+    pairs = sorted(pairs, key=lambda _: rng.random())
+    u = np.array([a for a, _ in pairs], np.int32)
+    i = np.array([b for _, b in pairs], np.int32)
+    return u, i, rng.integers(1, 6, nnz).astype(float), nu, ni
 
 
 def _qd_setup(world):
     import rotq_model as RQ
-    u, i, r, nu, ni = _rq_data()
+    import qdelta_model as QM
+    u, i, r, nu, ni = _qd_data()
     rng = np.random.default_rng(8)
     P0, Q0 = rng.normal(0, 0.1, (nu, K)), rng.normal(0, 0.1, (ni, K))
     ub = RQ.block_bounds(u, nu, world)
     shards = [((u >= ub[g]) & (u < ub[g + 1])) for g in range(world)]
-    w = _qd_weights(i, [i[m] for m in shards], ni, 0.005, QD_MERGES)
+    cnt = np.bincount(i, minlength=ni).astype(np.float64)
+    c = np.sum([np.bincount(i[m], minlength=ni) > 0 for m in shards], 0).astype(np.float64)
+    hot = QM.hot_items(cnt, c, QD_MERGES)
+    w = QM.weights(cnt, c, 0.005, QD_MERGES, hot)
     blocks = []  # per rank: its merges' user blocks (user_block_bounds over the rank's own ratings)
     for g, m in enumerate(shards):
         bb = RQ.block_bounds(u[m], nu, QD_MERGES)
         blocks.append([_stratum_rows(u[m], i[m], r[m], bb[b], bb[b + 1]) for b in range(QD_MERGES)])
-    return RQ, u, i, r, nu, ni, P0, Q0, ub, w, blocks
+    return RQ, QM, u, i, r, nu, ni, P0, Q0, ub, w, hot, blocks
 
 
 def _stratum_rows(u, i, r, lo, hi):
@@ -607,35 +615,40 @@ def _stratum_rows(u, i, r, lo, hi):
     return u[m][o].astype(np.int32), i[m][o].astype(np.int32), r[m][o]
 
 
-def _qd_train(RQ, P, Q, bu, bi, gb, blk):
-    P, Qn, bu, bin_, part = RQ.train_works(P, Q.copy(), bu, bi.copy(), gb, [blk])
-    return P, bu, Qn - Q, bin_ - bi, part
+def _qd_train(RQ, P, rows, bu, gb, blk):
+    """One block of a rank: (P, b_u, the rank's [Q | b_i] after it, its GlobalBias partial)."""
+    P, Qn, bu, bin_, part = RQ.train_works(P, rows[:, :K].copy(), bu, rows[:, K].copy(), gb, [blk])
+    return P, bu, np.concatenate([Qn, bin_[:, None]], 1), part
 
 
 def _qd_worker(rank, world, port, out):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
-    RQ, u, i, r, nu, ni, P0, Q0, ub, w, blocks = _qd_setup(world)
-    P, Q, bu, bi, gb = P0.copy(), Q0.copy(), np.zeros(nu), np.zeros(ni), 3.0
-    pend = None  # merge m - 1: (own weighted moves, their all-reduced sum, GlobalBias partials), applied after block m
+    RQ, QM, u, i, r, nu, ni, P0, Q0, ub, w, hot, blocks = _qd_setup(world)
+    P, bu, gb = P0.copy(), np.zeros(nu), 3.0
+    rows = np.concatenate([Q0, np.zeros((ni, 1))], 1)
+    st = QM.Rank(rows)
+    pend_gb = None  # merge m - 1's GlobalBias partials, folded after block m
     n_merges = EPOCHS * QD_MERGES
     for m in range(n_merges):
-        P, bu, mQ, mb, part = _qd_train(RQ, P, Q, bu, bi, gb, blocks[rank][m % QD_MERGES])
-        own = np.concatenate([w[:, None] * mQ, (w * mb)[:, None]], 1)
-        Q, bi = Q + own[:, :K], bi + own[:, K]
-        t = torch.from_numpy(own.copy())
+        X, _ = QM.merge_set(m, QD_MERGES, hot)
+        P, bu, rows, part = _qd_train(RQ, P, rows, bu, gb, blocks[rank][m % QD_MERGES])
+        rows = st.merge(rows, X, w)
+        t = torch.from_numpy(st.own.copy())
         g = torch.tensor([part], dtype=torch.float64)
-        dist.all_reduce(t)
+        dist.all_reduce(t)  # (the library all-reduces only the rows of X; the others' moves are zero here)
         dist.all_reduce(g)
-        for o, sm, gg in ([pend] if pend else []) + ([(own, t.numpy(), float(g.item()))] if m == n_merges - 1 else []):
-            Q, bi = Q + sm[:, :K] - o[:, :K], bi + sm[:, K] - o[:, K]
-            gb += gg / len(r)
-        pend = (own, t.numpy(), float(g.item()))
+        st.settle(t.numpy(), X)
+        if pend_gb is not None:
+            gb += pend_gb / len(r)
+        pend_gb = float(g.item())
+    rows = st.flush(rows)
+    gb += pend_gb / len(r)
     for g in range(world):  # P range g is current on rank g
         pr = torch.from_numpy(np.concatenate([P[ub[g]:ub[g + 1]], bu[ub[g]:ub[g + 1], None]], 1).copy())
         dist.broadcast(pr, g)
         P[ub[g]:ub[g + 1]], bu[ub[g]:ub[g + 1]] = pr[:, :K].numpy(), pr[:, K].numpy()
-    out[rank] = (P, Q, bu, bi, gb)
+    out[rank] = (P, rows[:, :K], bu, rows[:, K], gb)
     dist.destroy_process_group()
 
 
@@ -646,25 +659,30 @@ def test_gloo_qdelta_matches_single_process(world):
         out = m.dict()
         mp.spawn(_qd_worker, args=(world, port, out), nprocs=world, join=True)
         res = dict(out)
-    RQ, u, i, r, nu, ni, P0, Q0, ub, w, blocks = _qd_setup(world)
-    # the single-process run of the same rule: every rank's Q misses the others' moves of merge m - 1 during
-    # block m, and after the call every rank holds the start Q plus every merge's summed moves
+    RQ, QM, u, i, r, nu, ni, P0, Q0, ub, w, hot, blocks = _qd_setup(world)
+    # the single-process run of the same rules: the ranks train one after another (disjoint users), each from
+    # its own rows, and the merges' sums are formed here
     P, bu, gb = P0.copy(), np.zeros(nu), 3.0
-    Qs, bis = [Q0.copy() for _ in range(world)], [np.zeros(ni) for _ in range(world)]
-    pend, n_merges = None, EPOCHS * QD_MERGES
+    rows = [np.concatenate([Q0, np.zeros((ni, 1))], 1) for _ in range(world)]
+    st = [QM.Rank(x) for x in rows]
+    pend_gb, n_merges = None, EPOCHS * QD_MERGES
+    assert hot.any() and not hot.all()  # both hot merges and full merges move rows
     for m in range(n_merges):
-        own, part = [], 0.0
+        X, _ = QM.merge_set(m, QD_MERGES, hot)
+        part = 0.0
         for g in range(world):
-            P, bu, dq, db, p = _qd_train(RQ, P, Qs[g], bu, bis[g], gb, blocks[g][m % QD_MERGES])
-            own.append((w[:, None] * dq, w * db))
-            Qs[g], bis[g], part = Qs[g] + own[g][0], bis[g] + own[g][1], part + p
-        cur = (own, sum(o[0] for o in own), sum(o[1] for o in own), part)
-        for o, sq, sb, pp in ([pend] if pend else []) + ([cur] if m == n_merges - 1 else []):
-            for g in range(world):
-                Qs[g], bis[g] = Qs[g] + sq - o[g][0], bis[g] + sb - o[g][1]
-            gb += pp / len(r)
-        pend = cur
-    Q, bi = Qs[0], bis[0]
+            P, bu, rows[g], p = _qd_train(RQ, P, rows[g], bu, gb, blocks[g][m % QD_MERGES])
+            rows[g] = st[g].merge(rows[g], X, w)
+            part += p
+        total = sum(x.own for x in st)
+        for x in st:
+            x.settle(total, X)
+        if pend_gb is not None:
+            gb += pend_gb / len(r)
+        pend_gb = part
+    rows = [x.flush(y) for x, y in zip(st, rows)]
+    gb += pend_gb / len(r)
+    Q, bi = rows[0][:, :K], rows[0][:, K]
     assert any(0.0 < x < 1.0 for x in w)  # items on several ranks: weighted merges are exercised
     for rank in range(world):
         rP, rQ, rbu, rbi, rgb = res[rank]

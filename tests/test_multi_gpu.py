@@ -22,6 +22,7 @@ import numpy as np
 import pytest
 
 import oracle as O
+import qdelta_model as QM
 import rsgpu
 from helpers import folds, rmse
 from rsgpu import synth
@@ -246,24 +247,13 @@ def test_rotation_q_hot_copies_equal_host_model(ctx, ml100k, n_shards, pieces):
         assert all(np.array_equal(got[0][x], y[x]) for x in range(4)) and got[0][4] == y[4]
 
 
-def _qdelta_weights(i, shard_items, ni, lr, merges=1):
-    """RS_EXCHANGE_QDELTA's merge weight per item (rsgpu.h): kappa / c over the c shards that rate it."""
-    cnt = np.bincount(i, minlength=ni).astype(np.float64)
-    c = np.sum([np.bincount(si, minlength=ni) > 0 for si in shard_items], 0).astype(np.float64)
-    a = 1.0 - float(np.float32(lr))
-    w = np.ones(ni)
-    m = (c > 1) & (cnt > 0)
-    n = cnt[m] / c[m] / merges
-    w[m] = (1.0 - a ** (c[m] * n)) / (1.0 - a ** n) / c[m]
-    return w.astype(np.float32).astype(np.float64)
-
-
-@pytest.mark.parametrize("n_shards,merges", [(2, 1), (3, 1), (8, 1), (2, 3), (4, 2)])
+@pytest.mark.parametrize("n_shards,merges", [(2, 1), (3, 1), (8, 1), (2, 3), (4, 2), (2, 8)])
 def test_qdelta_one_wave_equals_host_model(ctx, ml100k, n_shards, merges):
-    """RS_EXCHANGE_QDELTA through the in-process exchange, one wave per shard: every epoch each shard trains
-    its user range against the same start Q (the oracle's sequential SGD in the shard's exported tile order,
-    P in place), the item moves merge with the kappa / c weights, GlobalBias folds the shards' partials --
-    equal to that host model to 1e-5, and P, Q, the biases and GlobalBias identical on every shard after the
+    """RS_EXCHANGE_QDELTA through the in-process exchange (int32 wire), one wave per shard: each shard trains
+    its user range block by block (the oracle's sequential SGD in the shard's exported tile order, P in place)
+    and merges the hot items after every block and every item after every cold_every-th block, with the
+    kappa / c weights and pipelined corrections (tests/qdelta_model.py) -- equal to that host model to 1e-5,
+    with the library's hot-item count, and P, Q, the biases and GlobalBias identical on every shard after the
     call (the P-range broadcast; Q and GlobalBias are the same integer sums everywhere)."""
     f = folds(*ml100k)[2]
     n = 30000
@@ -300,33 +290,41 @@ def test_qdelta_one_wave_equals_host_model(ctx, ml100k, n_shards, merges):
             wo = np.concatenate([[0], np.cumsum([z - a for a, z in seg])]).astype(np.int64)
             per[b] = (uu[sel], ii[sel], r_[sel], wo)
         works.append(per)
-    w = _qdelta_weights(i, [x[1] for x in sh], ni, lr, merges)
-    # pipelined merges (csrc/multi.hip epochs_qdelta): each shard keeps its own weighted moves at once and adds
-    # the other shards' (and the GlobalBias fold) of merge m - 1 after its block m -- the all-reduce overlaps it
+    cnt = np.bincount(i, minlength=ni).astype(np.float64)
+    c = np.sum([np.bincount(x[1], minlength=ni) > 0 for x in sh], 0).astype(np.float64)
+    hot = QM.hot_items(cnt, c, merges)
+    w = QM.weights(cnt, c, lr, merges, hot).astype(np.float32).astype(np.float64)
+    assert all(pl.qdelta_info() == (int(hot.sum()), QM.cold_every(merges)) for pl in plans)
+    if merges in (2, 8):  # hot merges and full merges both move rows
+        assert 0 < hot.sum() < ni
+    # the merge rules of tests/qdelta_model.py: each shard trains its block from its own rows, merges the hot
+    # rows (or every row, at a full merge) with its own weighted moves and the corrections pending from the
+    # rows' previous merges; GlobalBias folds merge m's partials after block m + 1
     P, bu, gb = P0.copy(), np.zeros(nu), 3.5
-    Qs, bis = [Q0.copy() for _ in sh], [np.zeros(ni) for _ in sh]
-    prev = None
+    rows = [np.concatenate([Q0, np.zeros((ni, 1))], 1) for _ in sh]
+    st = [QM.Rank(x) for x in rows]
+    pend_gb = None
     for m in range(epochs * merges):
         b = m % merges
-        dQ, dB, part = [], [], 0.0
+        X, _ = QM.merge_set(m, merges, hot)
+        part = 0.0
         for x, per in enumerate(works):
             uu, ii, r_, off = per[b]
-            if len(r_) == 0:
-                dQ.append(np.zeros_like(Q0))
-                dB.append(np.zeros(ni))
-                continue
-            P, Qg, bu, big, gg = O.svd_fit_works(uu, ii, r_, off, P, Qs[x], bu, bis[x], gb, epochs=1, lr=lr)
-            dQ.append(w[:, None] * (Qg - Qs[x]))
-            dB.append(w * (big - bis[x]))
-            Qs[x], bis[x] = Qs[x] + dQ[x], bis[x] + dB[x]
-            part += (gg - gb) * len(r_)
-        cur = (dQ, dB, sum(dQ), sum(dB), part)
-        for c_ in ([prev] if prev else []) + ([cur] if m == epochs * merges - 1 else []):
-            for x in range(len(sh)):
-                Qs[x], bis[x] = Qs[x] + c_[2] - c_[0][x], bis[x] + c_[3] - c_[1][x]
-            gb += c_[4] / len(r)
-        prev = cur
-    Q, bi = Qs[0], bis[0]
+            if len(r_):
+                P, Qg, bu, big, gg = O.svd_fit_works(uu, ii, r_, off, P, rows[x][:, :k], bu, rows[x][:, k], gb, epochs=1,
+                                                     lr=lr)
+                rows[x] = np.concatenate([Qg, big[:, None]], 1)
+                part += (gg - gb) * len(r_)
+            rows[x] = st[x].merge(rows[x], X, w)
+        total = sum(y.own for y in st)
+        for y in st:
+            y.settle(total, X)
+        if pend_gb is not None:
+            gb += pend_gb / len(r)
+        pend_gb = part
+    rows = [y.flush(z) for y, z in zip(st, rows)]
+    gb += pend_gb / len(r)
+    Q, bi = rows[0][:, :k], rows[0][:, k]
     g.close()
     got = [pl.download() for pl in plans]
     for pl in plans:
