@@ -501,6 +501,9 @@ bool tile_build_device(rs_svd_plan* pl) {
     pl->t_block_tile = {0, T};
     pl->t_block_user = {0, pl->n_users};
     pl->t_block_split = {0, 0};
+    pl->t_item_deg.alloc(static_cast<size_t>(std::max(1, ni)));  // the hot-run damping's degrees (sgd_tile.hip)
+    RS_HIP(hipMemcpyAsync(pl->t_item_deg.p, w.deg_i, sizeof(int32_t) * ni, hipMemcpyDeviceToDevice, s));
+    pl->tile_damp = tile_damp_rule(dmax_i, pl->tile_grid, pl->tile_waves, n);
     const size_t parts = static_cast<size_t>(tile_partials(pl));
     if (pl->partial.n < parts) pl->partial.alloc(parts);
     pl->tiles_built = true;

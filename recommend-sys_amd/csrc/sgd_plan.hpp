@@ -93,6 +93,8 @@ struct rs_svd_plan {
     rs::DevBuf<int2> t_runs;    // {item, first record (tile-local)}, a sentinel after each tile
     rs::DevBuf<int2> t_recs;    // {user (tile-local), rating bits}
     rs::DevBuf<int32_t> t_split_rows;  // users cut into pieces over several tiles
+    rs::DevBuf<int32_t> t_item_deg;    // every item's ratings in the schedule (the hot-run damping, sgd_tile.hip)
+    bool tile_damp = false;            // the schedule's hottest item has >= kTileDampRuns runs in flight: damped kernel
     int32_t t_n_split = 0;
     int64_t t_n_runs = 0, t_n_users = 0;  // entries of t_runs / t_users in use (the buffers may be larger)
     // user blocks: consecutive user ranges of near-equal ratings, each with its own tiles (tiles
@@ -279,7 +281,13 @@ __host__ __device__ inline uint32_t run_key(int32_t item, int32_t tile) {
 }
 constexpr int32_t kFillSnakeRounds = 4;  // RS_TILE_RULE_FILL: boustrophedon rounds before the deficit fill
 int32_t device_cus(const rs_ctx* ctx);
-int32_t tile_grid0(const rs_svd_plan* pl);  // the tile launch's workgroups (tile_wg, or the library's choice)
+int32_t tile_grid0(const rs_svd_plan* pl);
+// Hot-run damping (sgd_tile.hip) where the hottest item's runs in flight -- deg x workgroups x waves / nnz --
+// reach this many
+constexpr double kTileDampRuns = 40.0;
+inline bool tile_damp_rule(int64_t dmax, int32_t grid, int32_t waves, int64_t nnz) {
+    return nnz > 0 && static_cast<double>(dmax) * grid * waves / static_cast<double>(nnz) >= kTileDampRuns;
+}  // the tile launch's workgroups (tile_wg, or the library's choice)
 // the run cap the library picks (see auto_run_cap, sgd_tile.hip) from the item degree maximum
 int32_t run_cap_rule(int64_t nnz, int64_t dmax_item, int32_t grid, int32_t waves, int32_t k);
 void tile_build(rs_svd_plan* pl);  // (re)builds the tile schedule (host CSR, or the device for RS_TILE_RULE_FILL_DEVICE)

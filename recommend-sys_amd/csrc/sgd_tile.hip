@@ -91,14 +91,14 @@ __device__ __forceinline__ int32_t cvt_rpi(float x) {
 // headers / first record window are read after the chunk's first / second run, so no LDS round trip
 // waits on the critical path.  With one wave the claims come in queue order: the visit order is the
 // queue, as rs_svd_plan_tile_order exports it.
-template <int E, int NW, int RQ, int CH, int DIAG = 0>
+template <int E, int NW, int RQ, int CH, int DIAG = 0, bool DAMP = false>
 __global__ __launch_bounds__(NW * 64) void svd_epoch_tile_kernel(
     const int4* __restrict__ tiles, int32_t n_tiles, const int2* __restrict__ tile_users,
     const int32_t* __restrict__ streams, const int2* __restrict__ runs, const int2* __restrict__ recs,
     float* __restrict__ P, int32_t* Q, int32_t q_bytes, const double* __restrict__ gb_in,
     double* __restrict__ gb_partial, float* __restrict__ loss_partial, float lr, float reg, float fx, float* __restrict__ dP,
     const float* __restrict__ uw, float* __restrict__ dPs, int32_t kf, int32_t ldm, int32_t ldd,
-    int64_t* __restrict__ dbg) {
+    int64_t* __restrict__ dbg, const int32_t* __restrict__ item_deg, int32_t deg_bytes, float kconc) {
 #pragma clang fp contract(fast)
     constexpr int LD = 64 * E, NT = NW * 64;  // LD: LDS row (k + 2 columns fit); ldm: the rows in HBM
     constexpr bool TIMED = (DIAG & 16) != 0;  // per-wave phase clocks into dbg (experiments)
@@ -109,24 +109,28 @@ __global__ __launch_bounds__(NW * 64) void svd_epoch_tile_kernel(
     static_assert(CH == 0 || CH % RQ == 0, "a claimed chunk must be a whole number of ring turns");
     int64_t tm_stage = 0, tm_ring = 0, tm_loop = 0, tm_tail = 0, tm_c = 0;
     auto clk = [] { return static_cast<int64_t>(__builtin_amdgcn_s_memtime()); };
-    static_assert(2 * E * RQ <= 60, "ring loads and atomics must fit the 63-op vmcnt");
+    static_assert((2 * E + (DAMP ? 1 : 0)) * RQ <= 60, "ring loads and atomics must fit the 63-op vmcnt");
     typedef float f2 __attribute__((ext_vector_type(2)));
     extern __shared__ __align__(16) int32_t lds[];
     __shared__ int32_t s_claim;  // CH > 0: next unclaimed chunk of the tile's run queue
     const int tid = static_cast<int>(threadIdx.x), lane = tid & 63;
     const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
     const __amdgpu_buffer_rsrc_t rq = __builtin_amdgcn_make_buffer_rsrc(Q, 0, q_bytes, 0x00020000);
+    // the items' degrees (hot-run damping): loaded with each run's q_i row, in order on the same vmcnt
+    const __amdgpu_buffer_rsrc_t rdeg =
+        __builtin_amdgcn_make_buffer_rsrc(const_cast<int32_t*>(item_deg), 0, item_deg ? deg_bytes : 0, 0x00020000);
     const double gb0 = gb_in[0];
     const float a = 1.f - lr * reg, am1 = -lr * reg, fx_inv = 1.f / fx;
     // per register: global byte offset of this lane's Q element in a row (-1: none), constant lanes
     int32_t qoff[E];
-    bool qone[E], pone[E];
+    bool qone[E], pone[E], pfac[E];
 #pragma unroll
     for (int x = 0; x < E; ++x) {
         const int32_t c = lane + 64 * x;
         qoff[x] = c < kf ? 4 * c : (c == kf + 1 ? 4 * kf : -1);
         qone[x] = c == kf;      // Q's constant 1 (partner of b_u)
-        pone[x] = c == kf + 1;  // P's constant 1 (partner of b_i)
+        pone[x] = c == kf + 1;  // P's constant 1 (partner of b_i); Q's b_i
+        pfac[x] = c < kf;       // a factor column
     }
     auto qaddr = [&](int32_t row, int x) { return (row >= 0 && qoff[x] >= 0) ? row + qoff[x] : kOutOfRange; };
     double contrib = 0.0;
@@ -145,18 +149,22 @@ __global__ __launch_bounds__(NW * 64) void svd_epoch_tile_kernel(
         int32_t* Pl = lds;
         int2* Rl = reinterpret_cast<int2*>(Pl + nu * LD);
         int2* Ul = Rl + n_rec;
-        auto load_q = [&](int32_t (&q)[E], int32_t item) {
+        auto load_q = [&](int32_t (&q)[E], int32_t& dg, int32_t item) {
             const int32_t row = item >= 0 ? item * (ldm * 4) : -1;  // SGPR arithmetic
 #pragma unroll
             for (int x = 0; x < E; ++x)
                 q[x] = (DIAG & 2) ? 0
                                   : static_cast<int32_t>(__builtin_amdgcn_raw_buffer_load_b32(rq, qaddr(row, x), 0, kSgdAux));
+            if constexpr (DAMP)
+                dg = static_cast<int32_t>(__builtin_amdgcn_raw_buffer_load_b32(rdeg, item >= 0 ? item * 4 : kOutOfRange, 0, 0));
+            else
+                dg = 0;
         };
-        int32_t ring[RQ][E];
+        int32_t ring[RQ][E], ringd[RQ];
         auto prefill = [&](auto&& item_at) {
 #pragma unroll
             for (int s = 0; s < RQ; ++s) {
-                load_q(ring[s], item_at(s));
+                load_q(ring[s], ringd[s], item_at(s));
                 // dropped atomics (out-of-range offsets): the loop is entered with the same pattern of
                 // loads and atomics in flight as its back edge carries, so the compiler's vmcnt waits
                 // keep the whole ring in flight instead of draining to the prologue's count
@@ -206,9 +214,20 @@ __global__ __launch_bounds__(NW * 64) void svd_epoch_tile_kernel(
         const float klr = lr * fx_inv * fx_inv;  // c = lr (s 2^-2S + gb - r): p and q in 2^-S units (S: the plan's shift)
         // One run: its q_i row comes out of ring slot `slot`, which is refilled with the row of `next`;
         // records [j, e) are trained in order with q_i in registers, then the run's delta goes to memory.
-        auto run = [&](int32_t (&slot)[E], int32_t item, int32_t e, int32_t next) {
+        auto run = [&](int32_t (&slot)[E], int32_t& slotd, int32_t item, int32_t e, int32_t next) {
             int64_t c0 = 0;
             if constexpr (TIMED) c0 = clk();
+            // Hot-run damping (round 5).  About R = deg_i x workgroups x waves / nnz runs of item i are in flight
+            // at any time (the item's share of the ratings the chip's waves hold), each from a q_i read before the
+            // others' deltas land.  Where their summed step would pass the gap sequential SGD closes -- R times
+            // this run's own closing fraction f = 1 - prod(1 - lr (|p_u|^2 + reg)) over its ratings, beyond 1 --
+            // the run's delta is scaled by 1 / (R f) (the bias column: f from 1 - lr (1 + reg) per rating).
+            // Only runs with R >= 4 measure |p_u|^2 (an extra wave sum per rating); with one wave per tile, or
+            // the runs of an ML-1M epoch (R <= 10, R f < 1), nothing changes.  DESIGN.md K1 round 5.
+            const float R = DAMP ? static_cast<float>(__builtin_amdgcn_readfirstlane(slotd)) * kconc : 0.f;
+            const bool hot = DAMP && R >= 4.f;
+            const int32_t n_run = e - j;
+            float hp = 0.f;  // this lane's columns of the run's sum of |p_u|^2, in 2^-2S units
             int32_t q0[E];
             float q[E];
 #pragma unroll
@@ -225,7 +244,7 @@ __global__ __launch_bounds__(NW * 64) void svd_epoch_tile_kernel(
                 tm_ring += c1 - c0;
                 c0 = c1;
             }
-            load_q(slot, next);  // refill: every slot issues E loads + E atomics
+            load_q(slot, slotd, next);  // refill: every slot issues E + 1 loads + E atomics
             const float gbf = static_cast<float>(gb);
             float cs = 0.f;  // sum of this run's c: GlobalBias moves by -cs (folded in double)
             for (; j < e; ++j) {
@@ -255,6 +274,11 @@ __global__ __launch_bounds__(NW * 64) void svd_epoch_tile_kernel(
                     if constexpr (E & 1) sd = __builtin_fmaf(pu[E - 1], q[E - 1], sd);
                 }
                 sd = wave_sum_l63(sd);
+                if (hot) {  // per lane; summed over the wave once, at the run's end
+#pragma unroll
+                    for (int x = 0; x < E; ++x)
+                        if (pfac[x]) hp = __builtin_fmaf(pu[x], pu[x], hp);
+                }
                 // svd.go:102-128: diff = (gb + b_u + b_i + p.q) - r, c = lr diff;
                 // p <- a p - c q ; q <- a q - c p_new (Q1) ; gb <- gb - c
                 const float c = __builtin_fmaf(sd, klr, lr * ((gbf - cs) - rt));
@@ -292,13 +316,35 @@ __global__ __launch_bounds__(NW * 64) void svd_epoch_tile_kernel(
             gb -= static_cast<double>(cs);
             if constexpr (TIMED) tm_loop += clk() - c0;
             const int32_t row = item >= 0 ? item * (ldm * 4) : -1;
+            bool damp = false;  // wave-uniform: the common path keeps its exact integer delta and no extra work
+            float wq = 1.f, wb = 1.f;
+            if (hot) {
+                hp = wave_sum_l63(hp);
+                const float fq = 1.f - __expf(-lr * (hp * fx_inv * fx_inv + static_cast<float>(n_run) * reg));
+                const float fb = 1.f - __expf(static_cast<float>(n_run) * __logf(1.f - lr * (1.f + reg)));
+                wq = fminf(1.f, 1.f / (R * fq));
+                wb = fminf(1.f, 1.f / (R * fb));
+                damp = wq < 1.f || wb < 1.f;
+            }
+            if (damp) {
 #pragma unroll
-            for (int x = 0; x < E; ++x) {
-                const int32_t dq = cvt_rpi(q[x]) - q0[x];
-                if constexpr (DIAG & 1)  // diagnostic: the atomic goes nowhere (same issue count)
-                    __builtin_amdgcn_raw_ptr_buffer_atomic_add_i32(dq, rq, kOutOfRange + lane * 4 + 256 * x, 0, 0);
-                else
-                    __builtin_amdgcn_raw_ptr_buffer_atomic_add_i32(dq, rq, qaddr(row, x), 0, 0);
+                for (int x = 0; x < E; ++x) {
+                    const float wx = pone[x] ? wb : wq;
+                    const int32_t dq = cvt_rpi(wx * (q[x] - static_cast<float>(q0[x])));
+                    if constexpr (DIAG & 1)
+                        __builtin_amdgcn_raw_ptr_buffer_atomic_add_i32(dq, rq, kOutOfRange + lane * 4 + 256 * x, 0, 0);
+                    else
+                        __builtin_amdgcn_raw_ptr_buffer_atomic_add_i32(dq, rq, qaddr(row, x), 0, 0);
+                }
+            } else {
+#pragma unroll
+                for (int x = 0; x < E; ++x) {
+                    const int32_t dq = cvt_rpi(q[x]) - q0[x];
+                    if constexpr (DIAG & 1)  // diagnostic: the atomic goes nowhere (same issue count)
+                        __builtin_amdgcn_raw_ptr_buffer_atomic_add_i32(dq, rq, kOutOfRange + lane * 4 + 256 * x, 0, 0);
+                    else
+                        __builtin_amdgcn_raw_ptr_buffer_atomic_add_i32(dq, rq, qaddr(row, x), 0, 0);
+                }
             }
         };
 
@@ -330,7 +376,7 @@ __global__ __launch_bounds__(NW * 64) void svd_epoch_tile_kernel(
                     }
                     const int32_t item = live ? run_hdr(rr, false) : -1;
                     const int32_t e = live ? run_hdr(rr + 1, true) : j;
-                    run(ring[s], item, e, item_of(rr + RQ));
+                    run(ring[s], ringd[s], item, e, item_of(rr + RQ));
                 }
             }
             nr = s_end - s_begin;
@@ -359,7 +405,7 @@ __global__ __launch_bounds__(NW * 64) void svd_epoch_tile_kernel(
                     for (int s = 0; s < RQ; ++s) {
                         const int p = p0 + s;
                         const int32_t nxt = p + RQ < CH ? hx(hc, p + RQ) : hx(hn, p + RQ - CH);
-                        run(ring[s], hx(hc, p), hy(hc, p + 1), nxt);
+                        run(ring[s], ringd[s], hx(hc, p), hy(hc, p + 1), nxt);
                         if (p == 0) {  // the claim has landed behind this run's LDS traffic
                             cn = __builtin_amdgcn_readfirstlane(claim);
                             hn = hdr(cn);
@@ -1159,6 +1205,11 @@ void tile_build(rs_svd_plan* pl) {
     pl->t_n_split = static_cast<int32_t>(th.split.size());
     pl->t_split_rows.alloc(std::max<size_t>(1, th.split.size()));
     pl->t_split_rows.upload(th.split.data(), th.split.size(), s);
+    std::vector<int32_t> deg(static_cast<size_t>(std::max(1, pl->n_items)), 0);  // the hot-run damping's degrees
+    for (int32_t c : pl->h_cols) deg[c]++;
+    pl->t_item_deg.alloc(deg.size());
+    pl->t_item_deg.upload(deg.data(), deg.size(), s);
+    pl->tile_damp = tile_damp_rule(*std::max_element(deg.begin(), deg.end()), pl->tile_grid, pl->tile_waves, pl->nnz);
     if (pl->t_n_split > 0 && pl->dPs.n != static_cast<size_t>(std::max(1, pl->n_users)) * pl->ld) {
         pl->dPs.alloc(static_cast<size_t>(std::max(1, pl->n_users)) * pl->ld);
         RS_HIP(hipMemsetAsync(pl->dPs.p, 0, pl->dPs.n * sizeof(float), s));
@@ -1193,9 +1244,9 @@ struct TileRange {  // tiles [t0, t1) into dP rows of stride ldd (delta mode), g
     int32_t t0, t1, ldd, grid;
 };
 
-template <int E, int NW, int RQ, int CH, int DIAG = 0>
+template <int E, int NW, int RQ, int CH, int DIAG = 0, bool DAMP = false>
 static void tile_launch_t(rs_svd_plan* pl, float lr, float reg, hipStream_t s, float* dP, const TileRange& tr) {
-    auto kern = svd_epoch_tile_kernel<E, NW, RQ, CH, DIAG>;
+    auto kern = svd_epoch_tile_kernel<E, NW, RQ, CH, DIAG, DAMP>;
     static bool attr = false;  // per instantiation
     if (!attr) {
         RS_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(kern),
@@ -1206,7 +1257,8 @@ static void tile_launch_t(rs_svd_plan* pl, float lr, float reg, hipStream_t s, f
     hipLaunchKernelGGL(kern, dim3(tr.grid), dim3(NW * 64), pl->tile_lds, s, pl->t_tiles.p + tr.t0, tr.t1 - tr.t0,
                        pl->t_users.p, pl->t_streams.p + static_cast<int64_t>(tr.t0) * (NW + 1), pl->t_runs.p,
                        pl->t_recs.p, pl->P.p, reinterpret_cast<int32_t*>(pl->Q.p), q_bytes, pl->gb.p, pl->partial.p,
-                       pl->loss_part.n >= pl->partial.n ? pl->loss_part.p : nullptr, lr, reg, pl->fx(), dP, dP ? pl->uw.p : nullptr, pl->dPs.p, pl->k, pl->ld, tr.ldd, pl->trace.p);
+                       pl->loss_part.n >= pl->partial.n ? pl->loss_part.p : nullptr, lr, reg, pl->fx(), dP, dP ? pl->uw.p : nullptr, pl->dPs.p, pl->k, pl->ld, tr.ldd, pl->trace.p,
+                       pl->t_item_deg.p, buffer_bytes32(pl->t_item_deg.n, sizeof(int32_t), "item degrees"), pl->nnz > 0 ? static_cast<float>(static_cast<double>(tr.grid) * NW / static_cast<double>(pl->nnz)) : 0.f);
 }
 
 // q_i rows in flight per wave (runs ahead): the ring's loads and the runs' atomics share the wave's
@@ -1242,11 +1294,11 @@ static void tile_launch_r(rs_svd_plan* pl, float lr, float reg, hipStream_t s, f
             // the ring must divide the chunk (static_assert in the kernel): a ring of 3 or more runs with
             // claims takes the 4-deep ring on chunks of 8
             if (want >= 3) return tile_launch_t<E, NW, 4, 8>(pl, lr, reg, s, dP, tr);
-            return pl->tile_claim >= 8 ? tile_launch_t<E, NW, 2, 8>(pl, lr, reg, s, dP, tr)
-                                       : tile_launch_t<E, NW, 2, 4>(pl, lr, reg, s, dP, tr);
-        } else {
-            return tile_launch_t<E, NW, 2, 4>(pl, lr, reg, s, dP, tr);
+            if (pl->tile_claim >= 8) return tile_launch_t<E, NW, 2, 8>(pl, lr, reg, s, dP, tr);
         }
+        // the default claims (4 runs, ring 2), with the hot-run damping where the schedule asks for it
+        return pl->tile_damp ? tile_launch_t<E, NW, 2, 4, 0, true>(pl, lr, reg, s, dP, tr)
+                             : tile_launch_t<E, NW, 2, 4>(pl, lr, reg, s, dP, tr);
     }
     // the host-dealt schedule (round 3; tile_claim = 0): rings 2 and 4, and 3 / 6 / 8 / 12 for E = 2
     if constexpr (E == 2) {

@@ -116,6 +116,45 @@ def run_fit(ctx, name, log):
     return {"rmse": e, "refits": ctx.fit_refits()}
 
 
+def run_diag(ctx, name, wg=0, epochs=None, log=print):
+    """Guard off: per epoch the held-out RMSE, the largest |factor| / |bias| and where (item's rating rank),
+    to find the rows that run away without the guard's redo."""
+    U, I, deg, zs, k, ep, _ = CASES[name]
+    ep = epochs or ep
+    s = rsgpu.Synth(U, I, mean_deg=deg, zipf_s=zs, seed=20250901, n_threads=16)
+    d = np.diff(s.rowptr)
+    users = np.repeat(np.arange(U, dtype=np.int32), d)
+    hold = np.random.default_rng(0).random(s.nnz) < 0.05
+    keep = ~hold
+    rp = np.concatenate([[0], np.cumsum(np.bincount(users[keep], minlength=U))]).astype(np.int64)
+    cols, vals = s.cols[keep].copy(), s.vals[keep].copy()
+    hu, hi, hr = users[hold], s.cols[hold].copy(), s.vals[hold].astype(np.float64)
+    s.close()
+    cnt = np.bincount(cols, minlength=I)
+    rank = np.empty(I, np.int64)
+    rank[np.argsort(-cnt, kind="stable")] = np.arange(I)
+    plan = ctx.svd_plan_csr(U, I, rp, cols, vals, k)
+    plan.set_guard(False)
+    if wg:
+        plan.set_tiles(workgroups=wg)
+    plan.init_normal(0.0, 0.1, seed=1)
+    plan.upload(gb=float(np.mean(vals, dtype=np.float64)))
+    for e in range(ep):
+        plan.epochs(1)
+        try:
+            P, Q, bu, bi, g = plan.download()
+        except rsgpu.RsError as x:
+            log(f"{name} wg {wg or 'auto'} epoch {e + 1}: download RS_ERR {x.code}")
+            break
+        qa = np.abs(Q).max(1)
+        top = np.argsort(-qa)[:3]
+        rm = plan.evaluate(hu, hi, hr)[0]
+        log(f"{name} wg {wg or 'auto'} epoch {e + 1}: held-out {rm:.4f} gb {g:.3f} max|P| {np.abs(P).max():.3f} "
+            f"max|bu| {np.abs(bu).max():.3f} max|bi| {np.abs(bi).max():.3f} (item rank {rank[int(np.argmax(np.abs(bi)))]}) "
+            f"max|Q| rows " + ", ".join(f"{qa[t]:.3f}@rank{rank[t]}({cnt[t]})" for t in top))
+    plan.close()
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("cases", nargs="*", default=list(CASES))
@@ -123,10 +162,13 @@ def main():
     ap.add_argument("--cap", type=int, default=0)
     ap.add_argument("--wg", type=int, default=0, help="workgroups (0: one per CU)")
     ap.add_argument("--fit", action="store_true", help="through rs_svd_fit (the guarded Go drop-in)")
+    ap.add_argument("--diag", action="store_true", help="guard off, per-epoch extremes (run_diag)")
     args = ap.parse_args()
     ctx = rsgpu.Context(0)
     for c in args.cases:
-        if args.fit:
+        if args.diag:
+            run_diag(ctx, c, args.wg)
+        elif args.fit:
             run_fit(ctx, c, lambda m: print(m, flush=True))
         else:
             run(ctx, c, args.claim, args.cap, lambda m: print(m, flush=True), args.wg)
