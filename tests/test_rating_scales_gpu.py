@@ -39,8 +39,8 @@ def scaled(ml100k):
 
 @pytest.mark.parametrize("scale", sorted(SCALES))
 def test_svd_fast_on_rating_scale(ctx, scaled, scale):
-    """5-fold, k = 100, 20 epochs: no refit, no error, within the base_test.go:34-36 bound in star units,
-    and within 0.003 x scale of a sequential SGD restatement of the reference -- the closer of the
+    """5-fold, k = 100, 20 epochs: no refit, no error, within the base_test.go:34-36 bound in star units where
+    the restatement meets it, and within 0.003 x scale of a sequential SGD restatement of the reference -- the closer of the
     reference visit order (or_svd_fit) and the user-major order with FAST's GlobalBias warm start
     (or_svd_fit_chunked).  At x20 / lr 0.0005 the visit order alone moves the result: reference order
     18.649, user-major 18.711 (0.062 = 0.0031 in star units), so the tile schedule (yet another order) is
@@ -62,7 +62,10 @@ def test_svd_fast_on_rating_scale(ctx, scaled, scale):
     ref_m, um_m, gpu_m = float(np.mean(ref_r)), float(np.mean(um_r)), float(np.mean(gpu_r))
     assert refits == [0] * len(refits), refits
     assert min(abs(gpu_m - ref_m), abs(gpu_m - um_m)) <= 0.003 * mult, (gpu_m, ref_m, um_m)
-    assert gpu_m / mult <= 0.934 + 0.008, gpu_m
+    # base_test.go:34-36's bound in star units, where the sequential restatement itself meets it: on the -10..10
+    # scale at lr 0.005 the reference order lands at 5.18-5.25 (1.04 in star units) on its own
+    if min(ref_m, um_m) / mult <= 0.934:
+        assert gpu_m / mult <= 0.934 + 0.008, gpu_m
 
 
 def test_svd_fast_one_wave_exact_on_1_100(ctx, scaled):
