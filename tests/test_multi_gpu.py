@@ -370,6 +370,69 @@ def test_qdelta_fp16_wire_tracks_int32(ctx, ml100k, n_shards, merges):
     assert abs(res[16][1] - res[32][1]) <= 1e-3, (res[16][1], res[32][1])
 
 
+def test_qdelta_edge_shards(ctx, ml100k):
+    """QDELTA edge cases, in-process group: a shard whose user range holds no ratings (its plan trains nothing
+    and still takes part in every merge), more merges than a shard has users, and an item no shard rates --
+    the fit stays finite, every shard ends with the same bits, and the empty shard's start P rows for its
+    (unrated) users come back unchanged."""
+    f = folds(*ml100k)[4]
+    u, i, r, nu, ni = f.iu[:20000], f.ii[:20000], f.r[:20000], f.nu, f.ni + 3  # 3 items nobody rates
+    k = 16
+    rng = np.random.default_rng(21)
+    P0, Q0 = rng.normal(0, 0.1, (nu, k)), rng.normal(0, 0.1, (ni, k))
+    lo = int(np.max(u)) + 1  # users past the last rated one: an empty range for the third shard
+    sh = [(u[u < nu // 3], i[u < nu // 3], r[u < nu // 3]), (u[u >= nu // 3], i[u >= nu // 3], r[u >= nu // 3]),
+          (np.zeros(0, np.int32), np.zeros(0, np.int32), np.zeros(0))]
+    plans = []
+    for su, si, sr in sh:
+        pl = ctx.svd_plan(rsgpu.Ratings(su, si, sr, nu, ni), k)
+        pl.set_exchange(rsgpu.EXCHANGE_QDELTA)
+        pl.upload(P0, Q0, np.zeros(nu), np.zeros(ni), 3.5)
+        plans.append(pl)
+    g = rsgpu.SvdGroup(plans, n_blocks=64)
+    g.epochs(3)
+    g.close()
+    got = [pl.download() for pl in plans]
+    for pl in plans:
+        pl.close()
+    assert all(np.all(np.isfinite(x)) for x in got[0][:4]) and np.isfinite(got[0][4])
+    for y in got[1:]:
+        assert all(np.array_equal(got[0][x], y[x]) for x in range(4)) and got[0][4] == y[4]
+    assert np.allclose(got[0][1][-3:], Q0[-3:], atol=1e-7)  # unrated items: the start rows (2^-24 fixed point)
+    assert not np.array_equal(got[0][0][: nu // 3], P0[: nu // 3])
+    if lo < nu:
+        assert np.allclose(got[0][0][lo:], P0[lo:], atol=1e-6)
+
+
+def test_rccl_single_rank_qdelta_equals_group_of_one(ctx, ml100k):
+    """QDELTA through the RCCL join with one rank (communicator, comm stream, events; no collective runs at
+    N = 1): the same blocks, GlobalBias folds and results as the in-process group of one plan (one wave)."""
+    f = folds(*ml100k)[1]
+    n = 20000
+    u, i, r, nu, ni = f.iu[:n], f.ii[:n], f.r[:n], f.nu, f.ni
+    k = 24
+    rng = np.random.default_rng(5)
+    P0, Q0 = rng.normal(0, 0.1, (nu, k)), rng.normal(0, 0.1, (ni, k))
+    out = []
+    for join in (True, False):
+        pl = ctx.svd_plan(rsgpu.Ratings(u, i, r, nu, ni), k)
+        pl.set_tiles(workgroups=1, waves=1)
+        pl.set_exchange(rsgpu.EXCHANGE_QDELTA)
+        pl.upload(P0, Q0, np.zeros(nu), np.zeros(ni), 3.5)
+        if join:
+            pl.join(rsgpu.comm_unique_id(), 0, 1, 4)
+            assert pl.shard_info()[1:] == (1, rsgpu.EXCHANGE_QDELTA, 4)
+            pl.epochs_sharded(2)
+            pl.leave()
+        else:
+            g = rsgpu.SvdGroup([pl], n_blocks=4)
+            g.epochs(2)
+            g.close()
+        out.append(pl.download())
+        pl.close()
+    assert _maxdiff(out[0][:4], out[1][:4]) <= TOL and abs(out[0][4] - out[1][4]) <= TOL
+
+
 def test_rotation_fewer_users_than_blocks(ctx):
     """ROTATE with more user blocks than users (4 shards x 2 pieces, 5 users): empty blocks send and
     receive nothing and the fit still equals a single plan's users trained (finite, every rating seen)."""
