@@ -657,7 +657,11 @@ __global__ __launch_bounds__(64) void svd_live_merge_fx_kernel(int32_t* __restri
 // [n_live, n_live + n_split) the split users' row merges (as svd_merge_rows_kernel), and the last
 // block the GlobalBias fold (as gb_fold_kernel, the same 256-thread tree) plus re-arming the
 // merger's done counter for the next epoch.  Columns are independent, so the arithmetic is theirs.
-__global__ __launch_bounds__(256) void svd_epoch_epilogue_kernel(
+// 1024 threads: the fold's partials (workgroups x waves of the SGD launch, 2816 on ML-1M) are three loads per
+// thread and a wave-shuffle sum -- 8.1 us per epoch with 256 threads and an LDS tree
+// (profiles/r05/final/bench_kernel_stats.csv), the whole epilogue of an ML-1M epoch.
+constexpr int kEpilogueThreads = 1024;
+__global__ __launch_bounds__(kEpilogueThreads) void svd_epoch_epilogue_kernel(
     int32_t* __restrict__ Q, const int4* __restrict__ meta, int32_t* __restrict__ qlast, int32_t n_live,
     float* __restrict__ P, float* __restrict__ dP, const int32_t* __restrict__ rows, int32_t n_split,
     int32_t ld, const double* __restrict__ partial, int64_t n_partial, double* __restrict__ gb,
@@ -669,7 +673,7 @@ __global__ __launch_bounds__(256) void svd_epoch_epilogue_kernel(
         const int4 m = meta[b];
         auto row = [&](int32_t c) { return static_cast<int64_t>(c == 0 ? m.x : m.y + c - 1) * ld; };
         int32_t* L = qlast + static_cast<int64_t>(b) * ld;
-        for (int32_t col = tid; col < ld; col += 256) {
+        for (int32_t col = tid; col < ld; col += kEpilogueThreads) {
             const uint32_t l = static_cast<uint32_t>(L[col]);
             uint32_t v = l;
             for (int32_t c = 0; c < m.z; ++c) v += static_cast<uint32_t>(Q[row(c) + col]) - l;
@@ -680,29 +684,33 @@ __global__ __launch_bounds__(256) void svd_epoch_epilogue_kernel(
     }
     if (b < n_live + n_split) {
         const int64_t r = static_cast<int64_t>(rows[b - n_live]) * ld;
-        for (int32_t c = tid; c < ld; c += 256) {
+        for (int32_t c = tid; c < ld; c += kEpilogueThreads) {
             P[r + c] += dP[r + c];
             dP[r + c] = 0.f;
         }
         return;
     }
-    __shared__ double sh[256], sl[256];
+    constexpr int NWV = kEpilogueThreads / 64;
+    __shared__ double sh[NWV], sl[NWV];
     double t = 0.0, l = 0.0;
-    for (int64_t x = tid; x < n_partial; x += 256) {
+    for (int64_t x = tid; x < n_partial; x += kEpilogueThreads) {
         t += partial[x];
         if (loss_part) l += static_cast<double>(loss_part[x]);
     }
-    sh[tid] = t;
-    sl[tid] = l;
-    __syncthreads();
-    for (int w = 128; w > 0; w >>= 1) {
-        if (tid < w) {
-            sh[tid] += sh[tid + w];
-            sl[tid] += sl[tid + w];
-        }
-        __syncthreads();
+    for (int o = 32; o > 0; o >>= 1) {  // fixed order: the same bits on every run
+        t += __shfl_xor(t, o);
+        l += __shfl_xor(l, o);
     }
+    if ((tid & 63) == 0) {
+        sh[tid >> 6] = t;
+        sl[tid >> 6] = l;
+    }
+    __syncthreads();
     if (tid == 0) {
+        for (int w = 1; w < NWV; ++w) {
+            sh[0] += sh[w];
+            sl[0] += sl[w];
+        }
         gb[0] += sh[0] * inv_nnz;
         if (done) *done = 0;
         if (loss_part && loss_state) {
@@ -1715,7 +1723,7 @@ static void plan_epochs_once(rs_svd_plan* pl, int32_t epochs, float lr, float re
             launch_fast(pl, lr, reg, s);
             if (pl->timing) RS_HIP(hipEventRecord(pl->tev[2 * e + 1], s));
             const int32_t n_live = tile ? 0 : pl->n_live, n_split = tile ? pl->t_n_split : pl->n_split;
-            hipLaunchKernelGGL(svd_epoch_epilogue_kernel, dim3(n_live + n_split + 1), dim3(256), 0, s,
+            hipLaunchKernelGGL(svd_epoch_epilogue_kernel, dim3(n_live + n_split + 1), dim3(kEpilogueThreads), 0, s,
                                reinterpret_cast<int32_t*>(pl->Q.p), pl->live_meta.p,
                                reinterpret_cast<int32_t*>(pl->qlast.p), n_live, pl->P.p, pl->dPs.p,
                                tile ? pl->t_split_rows.p : pl->split_rows.p, n_split, pl->ld, pl->partial.p,
