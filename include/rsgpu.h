@@ -169,25 +169,6 @@ int rs_svd_predict(rs_ctx* ctx, int64_t n, const int32_t* users, const int32_t* 
 int rs_svdpp_fit(rs_ctx* ctx, const rs_ratings* r, const rs_sgd_params* p, double* P, double* Q,
                  double* Y, double* bu, double* bi, double* gb);
 
-/* The RS_SGD_FAST schedule of rs_svdpp_fit on this ctx.  RS_PP_SCHED_TILE: K1's user tiles with three LDS rows
- * per user (p_u, the implicit sum S_u of the epoch-start y_j, the lazy offset C~_u), one q_i atomic row per
- * (item, tile) run, and every y_j moved once per epoch by the composed affine maps of its runs (svdpp_tile.hip);
- * it applies where every user's row fits one tile (else the user-major kernel runs).  RS_PP_SCHED_USER: the
- * user-major kernel (one wave per user, q_i and y_j deltas as memory-side atomics).  RS_PP_SCHED_AUTO (default):
- * the tile schedule where it applies.  workgroups (0 = the library's choice) and waves (1, 16) shape the tile
- * launch.  rs_svdpp_schedule_used: the schedule the last rs_svdpp_fit ran (-1: none yet). */
-#define RS_PP_SCHED_AUTO 0
-#define RS_PP_SCHED_TILE 1
-#define RS_PP_SCHED_USER 2
-int rs_svdpp_set_schedule(rs_ctx* ctx, int32_t schedule, int32_t workgroups, int32_t waves);
-int rs_svdpp_schedule_used(const rs_ctx* ctx, int32_t* schedule);
-/* The tile schedule's visit order for these ratings (test oracle hook): pos (nnz) = user-CSR positions (stable
- * CSR of the data order) in the order one wave per workgroup trains them (tiles in order, a tile's runs, a run's
- * ratings); run_off (n_runs + 1) = each run's first entry of pos; tile_off (n_tiles + 1) = each tile's first run.
- * With any output NULL only the counts are returned.  RS_ERR_UNSUPPORTED where the schedule does not apply. */
-int rs_svdpp_tile_order(rs_ctx* ctx, const rs_ratings* r, int32_t n_factors, int32_t workgroups, int32_t waves,
-                        int64_t* pos, int64_t* run_off, int32_t* tile_off, int64_t* n_runs, int32_t* n_tiles);
-
 /* core/svd.go:158-251.  as_written=1 reproduces svd.go:243-249 (Q5), 0 the intended update. */
 int rs_nmf_fit(rs_ctx* ctx, const rs_ratings* r, int32_t n_factors, int32_t n_epochs, double reg,
                int32_t as_written, double* P, double* Q);

@@ -1107,83 +1107,6 @@ void or_svdpp_fit_lazy(int32_t n_users, const int64_t* rowptr, const int32_t* it
     free(e);
 }
 
-/* The tile schedule of svdpp_tile.hip in one wave's order (oracle.h).  Follows svd.go:352-424 per rating in
- * or_svdpp_fit_lazy's affine form; the y rows are read only through S (epoch start) and moved after each tile. */
-void or_svdpp_fit_tiles(int32_t n_users, const int64_t* rowptr, const int32_t* items, const double* r,
-                        int32_t n_tiles, const int32_t* tile_off, const int64_t* run_off, const int64_t* pos,
-                        int32_t k, int32_t epochs, double lr, double reg, double* P, double* Q, double* Y,
-                        double* bu, double* bi, double* gb) {
-    const int64_t nnz = rowptr[n_users];
-    const size_t nu = (size_t)(n_users > 0 ? n_users : 1);
-    int32_t* uu = (int32_t*)malloc((size_t)(nnz > 0 ? nnz : 1) * sizeof(int32_t));
-    double* S = (double*)malloc(nu * (size_t)k * sizeof(double));
-    double* Cv = (double*)malloc(nu * (size_t)k * sizeof(double));
-    double* A = (double*)malloc(nu * sizeof(double));
-    double* e = (double*)malloc((size_t)k * sizeof(double));
-    for (int32_t x = 0; x < n_users; x++)
-        for (int64_t t = rowptr[x]; t < rowptr[x + 1]; t++) uu[t] = x;
-    const double al = 1.0 - lr * reg;
-    double GB = *gb;
-    for (int32_t epoch = 0; epoch < epochs; epoch++) {
-        for (int32_t x = 0; x < n_users; x++) {
-            A[x] = 1.0;
-            for (int32_t f = 0; f < k; f++) {
-                S[(int64_t)x * k + f] = 0.0;
-                Cv[(int64_t)x * k + f] = 0.0;
-            }
-            for (int64_t t = rowptr[x]; t < rowptr[x + 1]; t++)
-                for (int32_t f = 0; f < k; f++) S[(int64_t)x * k + f] += Y[(int64_t)items[t] * k + f];
-        }
-        double gsum = 0.0;
-        for (int32_t tl = 0; tl < n_tiles; tl++) {
-            const int64_t b = run_off[tile_off[tl]], en = run_off[tile_off[tl + 1]];
-            double g = GB;
-            for (int64_t v = b; v < en; v++) {
-                const int64_t t = pos[v];
-                const int32_t x = uu[t], ii = items[t];
-                const double n = (double)(rowptr[x + 1] - rowptr[x]), sq = sqrt(n);
-                double* pu = P + (int64_t)x * k;
-                double* qi = Q + (int64_t)ii * k;
-                const double* Sx = S + (int64_t)x * k;
-                double* Cx = Cv + (int64_t)x * k;
-                const double userBias = bu[x], itemBias = bi[ii];
-                double pred = g;
-                pred += bu[x];
-                pred += bi[ii];
-                double s = 0.0;
-                for (int32_t f = 0; f < k; f++) {
-                    e[f] = (A[x] * Sx[f] - n * Cx[f]) / sq;
-                    s += (pu[f] + e[f]) * qi[f];
-                }
-                pred += s;
-                const double diff = pred - r[t];
-                g -= lr * diff;
-                bu[x] -= lr * (diff + reg * userBias);
-                bi[ii] -= lr * (diff + reg * itemBias);
-                for (int32_t f = 0; f < k; f++) pu[f] = pu[f] - (qi[f] * diff + pu[f] * reg) * lr;
-                for (int32_t f = 0; f < k; f++) qi[f] = qi[f] - ((pu[f] + e[f]) * diff + qi[f] * reg) * lr;
-                const double bt = lr * diff / sq;
-                for (int32_t f = 0; f < k; f++) Cx[f] = al * Cx[f] + bt * qi[f];
-                A[x] *= al;
-            }
-            gsum += (double)(en - b) * (g - GB);
-            for (int64_t v = b; v < en; v++) {  /* the y moves, run by run in the tile's order */
-                const int64_t t = pos[v];
-                const int32_t x = uu[t];
-                double* y = Y + (int64_t)items[t] * k;
-                for (int32_t f = 0; f < k; f++) y[f] = A[x] * y[f] - Cv[(int64_t)x * k + f];
-            }
-        }
-        if (nnz > 0) GB += gsum / (double)nnz;
-    }
-    *gb = GB;
-    free(uu);
-    free(S);
-    free(Cv);
-    free(A);
-    free(e);
-}
-
 double or_gb_warm_start(int32_t n_users, const int64_t* rowptr, const int32_t* items,
                         const double* r, const double* bu, const double* bi) {
     const int64_t nnz = rowptr[n_users];

@@ -146,15 +146,6 @@ void or_svdpp_fit_lazy(int32_t n_users, const int64_t* rowptr, const int32_t* it
 void or_svdpp_fit_userwise(int32_t n_users, const int64_t* rowptr, const int32_t* items,
                            const double* r, int32_t k, int32_t epochs, double lr, double reg,
                            double* P, double* Q, double* Y, double* bu, double* bi, double* gb);
-/* Restatement of the SVD++ tile schedule (svdpp_tile.hip) run by one wave: per epoch the implicit sums
- * S_u = sum_{j in N(u)} y_j of the epoch-start Y; then the ratings in visit order (pos: user-CSR positions,
- * run_off: runs into pos, tile_off: tiles into runs) with the lazy per-user state of or_svdpp_fit_lazy
- * (e = (A S_u - n C) / sqrt n), a tile-local GlobalBias copy; after a tile's ratings every y_j of a run moves by
- * y <- A_u y - C_u for the run's users in order (A_u = a^n: all of u's ratings are in its tile). */
-void or_svdpp_fit_tiles(int32_t n_users, const int64_t* rowptr, const int32_t* items, const double* r,
-                        int32_t n_tiles, const int32_t* tile_off, const int64_t* run_off, const int64_t* pos,
-                        int32_t k, int32_t epochs, double lr, double reg, double* P, double* Q, double* Y,
-                        double* bu, double* bi, double* gb);
 
 /* CPU baselines with the reference's own goroutine fan-out, restated with OpenMP (bench only). */
 void or_svdpp_fit_jobs(int64_t n, const int32_t* u, const int32_t* i, const double* r,

@@ -68,10 +68,7 @@ def lib():
                                             _f64p, _dp]
         L.or_svdpp_fit_lazy.argtypes = [C.c_int32, _i64p, _i32p, _f64p, C.c_int32, C.c_int32, C.c_double,
                                         C.c_double, _f64p, _f64p, _f64p, _f64p, _f64p, _dp]
-        L.or_svdpp_fit_tiles.argtypes = [C.c_int32, _i64p, _i32p, _f64p, C.c_int32, _i32p, _i64p, _i64p,
-                                         C.c_int32, C.c_int32, C.c_double, C.c_double, _f64p, _f64p, _f64p,
-                                         _f64p, _f64p, _dp]
-        L.or_svd_fit_works.argtypes =[C.c_int64, _i32p, _i32p, _f64p, C.c_int64, _i64p, C.c_int32,
+        L.or_svd_fit_works.argtypes = [C.c_int64, _i32p, _i32p, _f64p, C.c_int64, _i64p, C.c_int32,
                                        C.c_int32, C.c_double, C.c_double, _f64p, _f64p, _f64p, _f64p, _dp]
         L.or_svd_fit_chunked.argtypes = [C.c_int32, _i64p, _i32p, _f64p, C.c_int32, C.c_int32,
                                          C.c_int32, C.c_double, C.c_double, _f64p, _f64p, _f64p,
@@ -225,17 +222,6 @@ def svdpp_fit_lazy(rowptr, items, r, P, Q, Y, epochs=20, lr=0.007, reg=0.02, war
     g = C.c_double(gb_warm_start(rowptr, items, r, bu, bi) if warm and epochs > 0 else 0.0)
     lib().or_svdpp_fit_lazy(P.shape[0], _i64(rowptr), _i32(items), _f64(r), P.shape[1], epochs, lr, reg,
                             P, Q, Y, bu, bi, C.byref(g))
-    return P, Q, Y, bu, bi, g.value
-
-
-def svdpp_fit_tiles(rowptr, items, r, pos, run_off, tile_off, P, Q, Y, epochs=1, lr=0.007, reg=0.02, warm=True):
-    """The SVD++ tile schedule (svdpp_tile.hip) in one wave's visit order (or_svdpp_fit_tiles)."""
-    P, Q, Y = _f64(P).copy(), _f64(Q).copy(), _f64(Y).copy()
-    bu, bi = np.zeros(P.shape[0]), np.zeros(Q.shape[0])
-    g = C.c_double(gb_warm_start(rowptr, items, r, bu, bi) if warm and epochs > 0 else 0.0)
-    lib().or_svdpp_fit_tiles(P.shape[0], _i64(rowptr), _i32(items), _f64(r), len(tile_off) - 1,
-                             np.ascontiguousarray(tile_off, dtype=np.int32), _i64(run_off), _i64(pos), P.shape[1],
-                             epochs, lr, reg, P, Q, Y, bu, bi, C.byref(g))
     return P, Q, Y, bu, bi, g.value
 
 

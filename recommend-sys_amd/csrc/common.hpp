@@ -24,9 +24,6 @@ struct rs_ctx {
     std::shared_ptr<void> svd_fit_cache;  // rs_svd_fit: the last FAST plan and the COO it was built from
     std::shared_ptr<void> staging;        // pinned host ring of the streamed Sims download (sim.hip)
     int32_t fit_refits = 0;               // divergence refits of the last rs_svd_fit (rs_fit_refits)
-    // SVD++ FAST schedule (rs_svdpp_set_schedule): RS_PP_SCHED_*, the tile launch's workgroups / waves, and what
-    // the last rs_svdpp_fit ran
-    int32_t pp_schedule = RS_PP_SCHED_AUTO, pp_tile_wg = 0, pp_tile_waves = 16, pp_used = -1;
 };
 
 namespace rs {

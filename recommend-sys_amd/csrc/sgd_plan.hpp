@@ -292,24 +292,6 @@ inline bool tile_damp_rule(int64_t dmax, int32_t grid, int32_t waves, int64_t nn
 int32_t run_cap_rule(int64_t nnz, int64_t dmax_item, int32_t grid, int32_t waves, int32_t k);
 void tile_build(rs_svd_plan* pl);  // (re)builds the tile schedule (host CSR, or the device for RS_TILE_RULE_FILL_DEVICE)
 std::vector<int32_t> user_block_bounds(const int64_t* cum, int32_t n_users, int32_t nb);
-// the host tile schedule (sgd_tile.hip): tiles, entries, per-wave streams, run headers, records
-struct TileHost {
-    std::vector<int4> tiles;
-    std::vector<int2> users;      // {user, frac bits}
-    std::vector<int32_t> streams; // per tile NW + 1
-    std::vector<int2> runs, recs;
-    std::vector<int64_t> pos;     // CSR position of every record (want_pos only)
-    std::vector<int32_t> split;   // users cut into pieces
-    size_t lds = 0;
-};
-void build_tile_blocks(const rs_svd_plan* pl, int32_t grid0, bool want_pos, TileHost& th,
-                       std::vector<int32_t>& block_tile, std::vector<int32_t>& block_user,
-                       std::vector<int32_t>* block_split = nullptr);
-// svdpp_tile.hip: SVD++ FAST on the tile schedule; *applied false (nothing done) where a user's row does not fit
-// one tile.  shift: the fixed-point scale of Q (fx_shift_for)
-int svdpp_fit_tile(rs_ctx* ctx, const rs_ratings* r, const rs_sgd_params* p, const UserCSR& csr, int32_t shift,
-                   int32_t workgroups, int32_t waves, double* P, double* Q, double* Y, double* bu, double* bi, double* gb,
-                   bool* applied);
 void tile_launch(rs_svd_plan* pl, float lr, float reg, hipStream_t s, float* dP);  // one epoch (Q int32)
 // tiles [t0, t1) only (one user block), delta mode into dP (row stride ldd); returns the number of
 // GlobalBias partials written to pl->partial

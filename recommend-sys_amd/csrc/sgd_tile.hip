@@ -57,6 +57,23 @@
 namespace rs {
 
 
+// Wave sum ending in lane 63 (GFX9 DPP row broadcasts): the in-row tree gives every lane its row's
+// sum, row_bcast:15 adds row 0 / 2's sum into rows 1 / 3, row_bcast:31 adds rows 0-1 into rows 2-3.
+// Six VALU ops and a v_readlane, against ten for the all-lanes form (the value is needed as a scalar).
+__device__ __forceinline__ float wave_sum_l63(float x) {
+    x = group_sum<16>(x);
+    x += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(x), 0x142, 0xA, 0xF, false));  // row_bcast:15
+    x += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(x), 0x143, 0xC, 0xF, false));  // row_bcast:31
+    return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(x), 63));
+}
+
+// floor(x + 0.5) as int32 in one VALU op (v_cvt_rpi_i32_f32; __float2int_rn is rndne + cvt)
+__device__ __forceinline__ int32_t cvt_rpi(float x) {
+    int32_t r;
+    asm("v_cvt_rpi_i32_f32 %0, %1" : "=v"(r) : "v"(x));
+    return r;
+}
+
 // Register layout of the tile kernel: lane l's register x holds logical column c = l + 64 x.  Columns
 // [0, k) are the factors; the biases fold into the dot product with a constant partner column:
 //   P row: [p_0 .. p_{k-1}, b_u, 1]     Q row: [q_0 .. q_{k-1}, 1, b_i]
@@ -459,6 +476,15 @@ uint32_t mix32(uint64_t x) {
     return static_cast<uint32_t>((x ^ (x >> 31)) >> 16);
 }
 
+struct TileHost {
+    std::vector<int4> tiles;
+    std::vector<int2> users;      // {user, frac bits}
+    std::vector<int32_t> streams; // per tile NW + 1
+    std::vector<int2> runs, recs;
+    std::vector<int64_t> pos;     // CSR position of every record (want_pos only)
+    std::vector<int32_t> split;   // users cut into pieces
+    size_t lds = 0;
+};
 
 // Tiles from the host user-CSR.  Entries (user pieces) are consecutive users; a tile closes when the
 // next entry would pass the rating target or the LDS bound (runs <= records).  A user whose ratings
@@ -1087,11 +1113,9 @@ void build_tile_strata(const rs_svd_plan* pl, int32_t grid0, bool want_pos, Tile
     }
 }
 
-}  // namespace
-
 void build_tile_blocks(const rs_svd_plan* pl, int32_t grid0, bool want_pos, TileHost& th,
                        std::vector<int32_t>& block_tile, std::vector<int32_t>& block_user,
-                       std::vector<int32_t>* block_split) {
+                       std::vector<int32_t>* block_split = nullptr) {
     const std::vector<int64_t>& rp = pl->h_rowptr;
     if (!pl->iblock_bounds.empty()) {  // strata of a Q-rotation shard
         block_user = {0, pl->n_users};
@@ -1116,6 +1140,8 @@ void build_tile_blocks(const rs_svd_plan* pl, int32_t grid0, bool want_pos, Tile
         if (block_split) block_split->push_back(static_cast<int32_t>(th.split.size()));  // users ascend by block
     }
 }
+
+}  // namespace
 
 int32_t tile_partials(const rs_svd_plan* pl) { return std::max(1, pl->tile_grid) * pl->tile_waves; }
 

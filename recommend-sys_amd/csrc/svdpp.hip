@@ -34,7 +34,6 @@
 
 namespace rs {
 
-constexpr bool kPPTileDefault = false;  // RS_PP_SCHED_AUTO runs the tile schedule (svdpp_tile.hip)
 constexpr int32_t kPPOut = 0x7FFFFFF0;
 constexpr int kPPAux = 16;  // sc1
 
@@ -630,26 +629,7 @@ extern "C" int rs_svdpp_fit(rs_ctx* ctx, const rs_ratings* r, const rs_sgd_param
             rs::unpack_rows_f64(hbi, r->n_items, 1, 1, bi);
             return RS_OK;
         }
-        // the fixed-point scale from the ratings' spread (fx_shift_for, sgd_plan.hpp: 2^-24 on star scales)
-        double lo = 0.0, hi = 0.0, sum = 0.0;
-        for (int64_t t = 0; t < r->nnz; ++t) {
-            const double v = r->ratings[t];
-            lo = t == 0 ? v : std::min(lo, v);
-            hi = t == 0 ? v : std::max(hi, v);
-            sum += v;
-        }
-        const int32_t shift = rs::fx_shift_for(lo, hi, r->nnz > 0 ? sum / static_cast<double>(r->nnz) : 0.0);
-        ctx->pp_used = RS_PP_SCHED_USER;
-        if (ctx->pp_schedule == RS_PP_SCHED_TILE || (ctx->pp_schedule == RS_PP_SCHED_AUTO && rs::kPPTileDefault)) {
-            bool applied = false;
-            const int st2 = rs::svdpp_fit_tile(ctx, r, p, csr, shift, ctx->pp_tile_wg, ctx->pp_tile_waves, P, Q, Y, bu, bi,
-                                               gb, &applied);
-            if (applied) {
-                ctx->pp_used = RS_PP_SCHED_TILE;
-                return st2;
-            }
-        }
-        // FAST user-major: heaviest user first; GlobalBias warm start (common.hpp)
+        // FAST: heaviest user first; GlobalBias warm start (common.hpp)
         if (p->n_epochs > 0) {
             *gb = rs::gb_warm_start(r, bu, bi);
             dgb.upload(gb, 1, s);
@@ -705,6 +685,15 @@ extern "C" int rs_svdpp_fit(rs_ctx* ctx, const rs_ratings* r, const rs_sgd_param
         std::vector<float> hP, hQ, hY;
         bool fx = true;  // fixed-point Q and Y (see pp_ld); RSGPU_PP_FX=0: fp32 float atomics
         if (const char* env = std::getenv("RSGPU_PP_FX")) fx = std::atoi(env) != 0;
+        // the fixed-point scale from the ratings' spread (fx_shift_for, sgd_plan.hpp: 2^-24 on star scales)
+        double lo = 0.0, hi = 0.0, sum = 0.0;
+        for (int64_t t = 0; t < r->nnz; ++t) {
+            const double v = r->ratings[t];
+            lo = t == 0 ? v : std::min(lo, v);
+            hi = t == 0 ? v : std::max(hi, v);
+            sum += v;
+        }
+        const int32_t shift = rs::fx_shift_for(lo, hi, r->nnz > 0 ? sum / static_cast<double>(r->nnz) : 0.0);
         rs::pack_bias_rows(P, bu, r->n_users, k, ld, hP);
         rs::pack_bias_rows(Q, bi, r->n_items, k, ld, hQ, fx, shift);
         rs::pack_bias_rows(Y, nullptr, r->n_items, k, ld, hY, fx, shift);

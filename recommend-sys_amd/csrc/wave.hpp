@@ -32,21 +32,4 @@ __device__ __forceinline__ float dot4(const float4& a, const float4& b) {
     return a.x * b.x + a.y * b.y + a.z * b.z + a.w * b.w;
 }
 
-// Wave sum ending in lane 63 (GFX9 DPP row broadcasts): the in-row tree gives every lane its row's
-// sum, row_bcast:15 adds row 0 / 2's sum into rows 1 / 3, row_bcast:31 adds rows 0-1 into rows 2-3.
-// Six VALU ops and a v_readlane, against ten for the all-lanes form (the value is needed as a scalar).
-__device__ __forceinline__ float wave_sum_l63(float x) {
-    x = group_sum<16>(x);
-    x += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(x), 0x142, 0xA, 0xF, false));  // row_bcast:15
-    x += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(x), 0x143, 0xC, 0xF, false));  // row_bcast:31
-    return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(x), 63));
-}
-
-// floor(x + 0.5) as int32 in one VALU op (v_cvt_rpi_i32_f32; __float2int_rn is rndne + cvt)
-__device__ __forceinline__ int32_t cvt_rpi(float x) {
-    int32_t r;
-    asm("v_cvt_rpi_i32_f32 %0, %1" : "=v"(r) : "v"(x));
-    return r;
-}
-
 }  // namespace rs

@@ -25,7 +25,6 @@ TIE_GO_SORT, TIE_STABLE = 0, 1  # KNN.Predict tie order (rs_knn_plan_set_tie_ord
 DEV_SLOPE_ONE = 3  # rs_knn_sims kind: SlopeOne deviation matrix (slope_one.go:64-92)
 EXCHANGE_ROTATE, EXCHANGE_AVERAGE, EXCHANGE_ROTATE_Q, EXCHANGE_QDELTA = 0, 1, 2, 3  # multi-GPU exchange (rsgpu.h)
 TILE_RULE_LPT, TILE_RULE_FILL, TILE_RULE_FILL_DEVICE = 0, 1, 2  # how users are cut into tiles (rsgpu.h)
-PP_SCHED_AUTO, PP_SCHED_TILE, PP_SCHED_USER = 0, 1, 2  # rs_svdpp_set_schedule (rsgpu.h)
 
 HEADER_SYMBOLS = (
     "rs_version", "rs_device_count", "rs_open", "rs_close", "rs_last_error", "rs_synchronize",
@@ -50,7 +49,7 @@ HEADER_SYMBOLS = (
     "rs_item_shards", "rs_svd_fit_multi", "rs_tile_schedule_host", "rs_svd_plan_set_exchange", "rs_svd_plan_set_qdelta_wire", "rs_svd_plan_set_qdelta_split",
     "rs_comm_info", "rs_rotation_step", "rs_svd_plan_shard_info", "rs_svd_plan_qdelta_info", "rs_svd_plan_inject_fault",
     "rs_svd_plan_time_blocks", "rs_knn_plan_set_tie_order", "rs_fit_refits", "rs_fit_multi_refits",
-    "rs_svd_plan_set_hot_split", "rs_svdpp_set_schedule", "rs_svdpp_schedule_used", "rs_svdpp_tile_order",
+    "rs_svd_plan_set_hot_split",
 )
 COMM_ID_BYTES = 128
 
@@ -104,10 +103,6 @@ def lib():
                                          _vp, _dbl, _vp]),
             "rs_svdpp_fit": (C.c_int, [_vp, C.POINTER(_Ratings), C.POINTER(_SgdParams), _vp, _vp,
                                        _vp, _vp, _vp, _vp]),
-            "rs_svdpp_set_schedule": (C.c_int, [_vp, _i32, _i32, _i32]),
-            "rs_svdpp_schedule_used": (C.c_int, [_vp, C.POINTER(_i32)]),
-            "rs_svdpp_tile_order": (C.c_int, [_vp, C.POINTER(_Ratings), _i32, _i32, _i32, _vp, _vp, _vp,
-                                              C.POINTER(_i64), C.POINTER(_i32)]),
             "rs_nmf_fit": (C.c_int, [_vp, C.POINTER(_Ratings), _i32, _i32, _dbl, _i32, _vp, _vp]),
             "rs_baseline_fit": (C.c_int, [_vp, C.POINTER(_Ratings), _i32, _dbl, _dbl, _vp, _vp,
                                           _vp]),
@@ -390,32 +385,6 @@ class Context:
         self.check(lib().rs_svdpp_fit(self.h, C.byref(rc), C.byref(prm), _ptr(P), _ptr(Q), _ptr(Y),
                                       _ptr(bu), _ptr(bi), _ptr(g)))
         return P, Q, Y, bu, bi, float(g[0])
-
-    def svdpp_set_schedule(self, schedule=PP_SCHED_AUTO, workgroups=0, waves=16):
-        """The FAST schedule of svdpp_fit on this context (rs_svdpp_set_schedule: PP_SCHED_AUTO / _TILE / _USER)."""
-        self.check(lib().rs_svdpp_set_schedule(self.h, schedule, workgroups, waves))
-
-    def svdpp_schedule_used(self):
-        """PP_SCHED_TILE or PP_SCHED_USER: what the last svdpp_fit ran (-1: none yet)."""
-        s = _i32(0)
-        self.check(lib().rs_svdpp_schedule_used(self.h, C.byref(s)))
-        return s.value
-
-    def svdpp_tile_order(self, r: Ratings, n_factors, workgroups=1, waves=1):
-        """(pos, run_off, tile_off) of the SVD++ tile schedule (rs_svdpp_tile_order): user-CSR positions in visit
-        order, each run's first entry of pos, each tile's first run."""
-        rc = r.c()
-        nr, nt = _i64(0), _i32(0)
-        L = lib()
-        self.check(L.rs_svdpp_tile_order(self.h, C.byref(rc), n_factors, workgroups, waves, None, None, None,
-                                         C.byref(nr), C.byref(nt)))
-        nnz = len(r.ratings)
-        pos = np.zeros(max(1, nnz), dtype=np.int64)
-        run_off = np.zeros(nr.value + 1, dtype=np.int64)
-        tile_off = np.zeros(nt.value + 1, dtype=np.int32)
-        self.check(L.rs_svdpp_tile_order(self.h, C.byref(rc), n_factors, workgroups, waves, _ptr(pos), _ptr(run_off),
-                                         _ptr(tile_off), C.byref(nr), C.byref(nt)))
-        return pos[:nnz], run_off, tile_off
 
     def nmf_fit(self, r: Ratings, P, Q, n_epochs=50, reg=0.06, as_written=True):
         """core/svd.go:158-251 (as_written reproduces svd.go:243-249, Q5)."""

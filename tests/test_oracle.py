@@ -100,38 +100,6 @@ def test_svdpp_lazy_equals_userwise_literal():
     assert abs(a[5] - b[5]) < 1e-12
 
 
-def test_svdpp_tiles_equals_lazy_on_user_tiles():
-    """or_svdpp_fit_tiles (the SVD++ tile schedule: S from the epoch-start Y, y moved after each tile) with
-    one user per tile, its ratings in row order, is or_svdpp_fit_lazy's schedule exactly where no two users
-    share an item (then nobody else moves a user's y_j within the epoch); with shared items the two differ
-    only in which y_j a user's S reads (epoch start vs. the users before it)."""
-    rng = np.random.default_rng(8)
-    nu, k = 30, 10
-    deg = rng.integers(1, 25, nu)
-    u = np.repeat(np.arange(nu), deg)
-    i = rng.permutation(len(u))  # every item rated once: disjoint rows
-    r = rng.integers(1, 6, len(u)).astype(float)
-    ni = len(u)
-    rowptr, items, rr = O.csr_by(u, nu, i, r)
-    pos = np.arange(len(u), dtype=np.int64)
-    run_off = np.arange(len(u) + 1, dtype=np.int64)  # one rating per run
-    tile_off = rowptr.astype(np.int32)               # one user per tile
-    P0, Q0, Y0 = rng.normal(0, 0.1, (nu, k)), rng.normal(0, 0.1, (ni, k)), rng.normal(0, 0.1, (ni, k))
-    a = O.svdpp_fit_lazy(rowptr, items, rr, P0, Q0, Y0, epochs=3)
-    b = O.svdpp_fit_tiles(rowptr, items, rr, pos, run_off, tile_off, P0, Q0, Y0, epochs=3)
-    for x, y in zip(a[:5], b[:5]):
-        np.testing.assert_allclose(x, y, rtol=0, atol=1e-12)
-    assert abs(a[5] - b[5]) < 1e-12
-    # shared items: S reads the epoch-start y_j, so the first epoch's first user is still identical
-    i2 = rng.integers(0, 40, len(u))
-    rowptr2, items2, rr2 = O.csr_by(u, nu, i2, r)
-    Q2, Y2 = rng.normal(0, 0.1, (40, k)), rng.normal(0, 0.1, (40, k))
-    c = O.svdpp_fit_lazy(rowptr2, items2, rr2, P0, Q2, Y2, epochs=1)
-    d = O.svdpp_fit_tiles(rowptr2, items2, rr2, pos, run_off, rowptr2.astype(np.int32), P0, Q2, Y2, epochs=1)
-    np.testing.assert_allclose(c[0][0], d[0][0], rtol=0, atol=1e-12)
-    assert np.max(np.abs(c[2] - d[2])) > 1e-9
-
-
 @pytest.fixture(scope="module")
 def ml100k_folds(ml100k):
     return folds(*ml100k)
