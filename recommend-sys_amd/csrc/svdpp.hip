@@ -35,7 +35,6 @@
 namespace rs {
 
 constexpr int32_t kPPOut = 0x7FFFFFF0;
-constexpr int32_t kPPRounds = 0;  // rs_svdpp_fit FAST: ROUNDS schedule with this many rounds per epoch (0: one launch)
 constexpr int kPPAux = 16;  // sc1
 
 __device__ __forceinline__ float pp_wave_sum(float x) {
@@ -139,15 +138,15 @@ __device__ __forceinline__ void pp_update_y(__amdgpu_buffer_rsrc_t ry, const int
 template <int E, int D, bool FX, class Emit>
 __device__ __forceinline__ void pp_chain(__amdgpu_buffer_rsrc_t rq, const int32_t* __restrict__ items,
                                          const float* __restrict__ ratings, int64_t b, int64_t e,
-                                         int64_t n_row, int32_t lane, int32_t lcq, float lr, float a, const float (&S0)[E], float (&p)[E],
+                                         int32_t lane, int32_t lcq, float lr, float a, const float (&S0)[E], float (&p)[E],
                                          float& ub, float& gb, float& A, float (&Cv)[E], float fx, Emit&& emit) {
 #pragma clang fp contract(fast)
     constexpr int LD = 64 * E, B = 16;
     static_assert(B % D == 0, "ring depth must divide the 16-rating batch");
     const int32_t lane4 = lane * 4;
     const bool bias_lane = lane == 63;
-    const int32_t deg = static_cast<int32_t>(e - b);  // ratings of this chain (a piece, or the whole row)
-    const float nf = static_cast<float>(n_row);        // |N(u)|: the whole row
+    const int32_t deg = static_cast<int32_t>(e - b);
+    const float nf = static_cast<float>(deg);
     const float rsq = 1.f / sqrtf(nf);  // the chain multiplies by 1/sqrt|N(u)| (no divide per rating)
     const float fx_inv = 1.f / fx;
     auto load_rowq = [&](float (&q)[E], int32_t valid, int32_t item) {
@@ -278,7 +277,7 @@ __global__ __launch_bounds__(256) void svdpp_epoch_fast_kernel(
             pp_sum_y<E, YB, FX>(ry, items, b, e, 0, YB, lane4, lcy, S0, fx);
 #pragma unroll
             for (int x = 0; x < E; ++x) Cv[x] = 0.f;
-            pp_chain<E, D, FX>(rq, items, ratings, b, e, e - b, lane, lcq, lr, a, S0, p, ub, gb, A, Cv, fx,
+            pp_chain<E, D, FX>(rq, items, ratings, b, e, lane, lcq, lr, a, S0, p, ub, gb, A, Cv, fx,
                                [&](int32_t row, const float (&qw)[E], const float (&q)[E]) {
 #pragma unroll
                                    for (int x = 0; x < E; ++x)
@@ -329,7 +328,7 @@ __global__ __launch_bounds__(256) void svdpp_epoch_fast_kernel(
             float ub = pp_lane63(p[E - 1]);
             float gb = gb0, A = 1.f;
             int32_t tail = 0, free_end = R;
-            pp_chain<E, DH, FX>(rq, items, ratings, b, e, e - b, lane, lcq, lr, a, S0, p, ub, gb, A, Cv, fx,
+            pp_chain<E, DH, FX>(rq, items, ratings, b, e, lane, lcq, lr, a, S0, p, ub, gb, A, Cv, fx,
                             [&](int32_t row, const float (&qw)[E], const float (&q)[E]) {
                                 if (tail >= free_end) {  // ring full: wait for the writers
                                     for (;;) {
@@ -404,119 +403,6 @@ __global__ __launch_bounds__(256) void svdpp_epoch_fast_kernel(
         __syncthreads();  // s_red, s_A and the ring are reset by the next user
     }
     if (threadIdx.x == 0) gb_partial[blk] = contrib;
-}
-
-// ROUNDS epoch (round 5): the epoch's work items -- whole user rows, and the long rows cut into pieces that sit in
-// consecutive rounds -- are dealt to rounds of near-equal ratings, run one round per launch.  A wave runs pass 1
-// (S0 from the current Y) and pass 2 (the chain, q_i atomics) of its item as the light path does, but instead of
-// pass 3's y_j atomics it stores the item's y map (C in columns [0, kf), A in column kf) to row w of `maps`; the
-// round's pp_round_ymap_kernel then moves every y_j by the maps of the round's items that hold j, in item order.
-// The y_j atomics (one row per (u, j)) become plain map stores and one pass of loads per round; a piece of a long
-// row continues in the next round from the p_u and y_j its predecessor left (sequential within the row).
-template <int E, int D, bool FX>
-__global__ __launch_bounds__(256) void svdpp_round_kernel(
-    const int32_t* __restrict__ work, const int64_t* __restrict__ wrng, int32_t w0, int32_t w1,
-    const int64_t* __restrict__ rowptr, const int32_t* __restrict__ items, const float* __restrict__ ratings,
-    float* __restrict__ P, float* Q, const float* Y, int32_t row_bytes_q, int32_t row_bytes_y,
-    float* __restrict__ maps, float* __restrict__ gb_row, const double* __restrict__ gb_in,
-    double* __restrict__ gb_partial, float lr, float reg, int32_t kf, float fx) {
-#pragma clang fp contract(fast)
-    constexpr int LD = 64 * E;
-    constexpr int YB = 8;
-    __shared__ double s_contrib[4];
-    const int lane = threadIdx.x & 63;
-    const int wib = __builtin_amdgcn_readfirstlane(static_cast<int>(threadIdx.x) >> 6);
-    const float gb0 = static_cast<float>(gb_in[0]);
-    const __amdgpu_buffer_rsrc_t rq = __builtin_amdgcn_make_buffer_rsrc(Q, 0, row_bytes_q, 0x00020000);
-    const __amdgpu_buffer_rsrc_t ry = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(Y), 0, row_bytes_y, 0x00020000);
-    const int32_t lane4 = lane * 4;
-    const int32_t lcq = pp_last_col<E>(lane, kf, true), lcy = pp_last_col<E>(lane, kf, false);
-    auto pcol = [&](int x) { return x < E - 1 ? lane + 64 * x : lcq; };
-    const float a = 1.f - lr * reg;
-    double contrib = 0.0;
-    const int stride = static_cast<int>(gridDim.x) * 4;
-    for (int w = w0 + static_cast<int>(blockIdx.x) * 4 + wib; w < w1; w += stride) {
-        const int32_t u = work[w];
-        const int64_t rb = rowptr[u], re = rowptr[u + 1];
-        const int64_t b = wrng[2 * w], e = wrng[2 * w + 1];
-        float p[E];
-        float* prow = P + static_cast<int64_t>(u) * LD;
-#pragma unroll
-        for (int x = 0; x < E; ++x) p[x] = pcol(x) >= 0 ? prow[pcol(x)] : 0.f;
-        float ub = pp_lane63(p[E - 1]);
-        // a row's GlobalBias copy runs on through its pieces (gb_row), folded once at the row's end
-        float gb = b == rb ? gb0 : gb_row[u], A = 1.f;
-        float S0[E], Cv[E];
-        pp_sum_y<E, YB, FX>(ry, items, rb, re, 0, YB, lane4, lcy, S0, fx);
-#pragma unroll
-        for (int x = 0; x < E; ++x) Cv[x] = 0.f;
-        pp_chain<E, D, FX>(rq, items, ratings, b, e, re - rb, lane, lcq, lr, a, S0, p, ub, gb, A, Cv, fx,
-                           [&](int32_t row, const float (&qw)[E], const float (&q)[E]) {
-#pragma unroll
-                               for (int x = 0; x < E; ++x)
-                                   pp_atomic_add<FX>(qw[x] - q[x], rq, pp_roff<E>(row, x, lane4, lcq), fx);
-                           });
-        float* mrow = maps + static_cast<int64_t>(w) * LD;
-#pragma unroll
-        for (int x = 0; x < E; ++x) {
-            const int32_t c = lane + 64 * x;
-            if (c < kf) mrow[c] = Cv[x];
-            if (pcol(x) >= 0) prow[pcol(x)] = p[x];
-        }
-        if (lane == 0) {
-            mrow[kf] = A;
-            if (e != re) gb_row[u] = gb;
-        }
-        if (e == re) contrib += static_cast<double>(re - rb) * (static_cast<double>(gb) - static_cast<double>(gb0));
-    }
-    if (lane == 0) s_contrib[wib] = contrib;
-    __syncthreads();
-    if (threadIdx.x == 0) gb_partial[blockIdx.x] = ((s_contrib[0] + s_contrib[1]) + s_contrib[2]) + s_contrib[3];
-}
-
-// A round's y moves: one wave per item j, y_j <- A_w y_j - C_w for the round's work items w that hold j (item
-// order), Y in the fit's format (FX: int32 fixed point)
-template <int E, bool FX>
-__global__ __launch_bounds__(256) void pp_round_ymap_kernel(float* Y, const float* __restrict__ maps,
-                                                            const int32_t* __restrict__ joff,
-                                                            const int32_t* __restrict__ jw, int32_t n_items,
-                                                            int32_t kf, float fx) {
-    constexpr int LD = 64 * E;
-    const int lane = threadIdx.x & 63;
-    const int32_t j = static_cast<int32_t>(blockIdx.x) * 4 + static_cast<int32_t>(threadIdx.x >> 6);
-    if (j >= n_items) return;
-    const int32_t b = joff[j], e = joff[j + 1];
-    if (b == e) return;
-    float* yrow = Y + static_cast<int64_t>(j) * LD;
-    float y[E];
-#pragma unroll
-    for (int x = 0; x < E; ++x) {
-        const int32_t c = lane + 64 * x;
-        y[x] = c < kf ? pp_ld(__float_as_uint(yrow[c]), FX, 1.f / fx) : 0.f;
-    }
-    for (int32_t t = b; t < e; t += 4) {
-        float A[4], C[4][E];
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-            const int32_t w = t + q < e ? jw[t + q] : -1;
-            const float* mrow = maps + static_cast<int64_t>(w < 0 ? 0 : w) * LD;
-            A[q] = w < 0 ? 1.f : mrow[kf];
-#pragma unroll
-            for (int x = 0; x < E; ++x) {
-                const int32_t c = lane + 64 * x;
-                C[q][x] = (w < 0 || c >= kf) ? 0.f : mrow[c];
-            }
-        }
-#pragma unroll
-        for (int q = 0; q < 4; ++q)
-#pragma unroll
-            for (int x = 0; x < E; ++x) y[x] = __builtin_fmaf(A[q], y[x], -C[q][x]);
-    }
-#pragma unroll
-    for (int x = 0; x < E; ++x) {
-        const int32_t c = lane + 64 * x;
-        if (c < kf) yrow[c] = FX ? __int_as_float(__float2int_rn(y[x] * fx)) : y[x];
-    }
 }
 
 __global__ __launch_bounds__(256) void pp_gb_fold_kernel(const double* __restrict__ partial,
@@ -653,90 +539,6 @@ static void unpack_bias_rows(const std::vector<float>& src, int64_t rows, int32_
         for (int32_t f = 0; f < k; ++f) F[r * k + f] = v(r * ld + f);
         if (bias) bias[r] = v(r * ld + k);
     }
-}
-
-
-// The ROUNDS schedule (svdpp_round_kernel): users in LPT order (`order`), rounds of near-equal ratings.  The
-// heaviest row is cut into `rounds` pieces (one per round); every row longer than that piece size into as many
-// pieces, in consecutive rounds starting where their window's load is least; other rows go whole to the least-loaded
-// round.  Within a round the items are longest first.  joff / jw: per round the item-CSR of (item j, work item w)
-// over j in N(u_w), w ascending -- the order the round's y pass applies the maps.
-struct PPRounds {
-    std::vector<int32_t> wuser, roff, joff, jw;
-    std::vector<int64_t> wr;
-};
-PPRounds pp_rounds(const std::vector<int32_t>& order, const UserCSR& csr, int32_t n_items, int32_t rounds) {
-    PPRounds o;
-    const int32_t B = std::max(1, rounds);
-    const int64_t dmax = order.empty() ? 1 : csr.rowptr[order[0] + 1] - csr.rowptr[order[0]];
-    const int64_t pcap = std::max<int64_t>(1, (dmax + B - 1) / B);
-    std::vector<int64_t> load(B, 0);
-    struct It { int32_t u; int64_t b, e; };
-    std::vector<std::vector<It>> per(B);
-    for (int32_t u : order) {
-        const int64_t b0 = csr.rowptr[u], d = csr.rowptr[u + 1] - b0;
-        const int32_t pieces = static_cast<int32_t>(std::min<int64_t>(B, (d + pcap - 1) / pcap));
-        int32_t s0 = 0;
-        int64_t best = -1;
-        for (int32_t st = 0; st + pieces <= B; ++st) {
-            int64_t m = 0;
-            for (int32_t q = 0; q < pieces; ++q) m = std::max(m, load[st + q]);
-            if (best < 0 || m < best) {
-                best = m;
-                s0 = st;
-            }
-        }
-        for (int32_t q = 0; q < pieces; ++q) {
-            const int64_t pb = b0 + d * q / pieces, pe = b0 + d * (q + 1) / pieces;
-            per[s0 + q].push_back({u, pb, pe});
-            load[s0 + q] += pe - pb;
-        }
-    }
-    o.roff.push_back(0);
-    for (int32_t t = 0; t < B; ++t) {
-        std::stable_sort(per[t].begin(), per[t].end(), [](const It& x, const It& y) { return x.e - x.b > y.e - y.b; });
-        for (const It& x : per[t]) {
-            o.wuser.push_back(x.u);
-            o.wr.push_back(x.b);
-            o.wr.push_back(x.e);
-        }
-        o.roff.push_back(static_cast<int32_t>(o.wuser.size()));
-    }
-    // per round: item-CSR of the work items over their whole rows
-    const size_t ni1 = static_cast<size_t>(n_items) + 1;
-    o.joff.assign(ni1 * B, 0);
-    int32_t base = 0;
-    for (int32_t t = 0; t < B; ++t) {
-        int32_t* off = o.joff.data() + ni1 * t;
-        for (int32_t w = o.roff[t]; w < o.roff[t + 1]; ++w) {
-            const int32_t u = o.wuser[w];
-            for (int64_t x = csr.rowptr[u]; x < csr.rowptr[u + 1]; ++x) off[csr.cols[x] + 1]++;
-        }
-        off[0] = base;
-        for (int32_t j = 0; j < n_items; ++j) off[j + 1] += off[j];
-        std::vector<int32_t> at(off, off + n_items);
-        o.jw.resize(off[n_items]);
-        for (int32_t w = o.roff[t]; w < o.roff[t + 1]; ++w) {
-            const int32_t u = o.wuser[w];
-            for (int64_t x = csr.rowptr[u]; x < csr.rowptr[u + 1]; ++x) o.jw[at[csr.cols[x]]++] = w;
-        }
-        base = off[n_items];
-    }
-    return o;
-}
-
-template <int E>
-static void launch_pp_round(int32_t blocks, int32_t w0, int32_t w1, const DevBuf<int32_t>& work, const DevBuf<int64_t>& wrng,
-                            const DevBuf<int64_t>& rowptr, const DevBuf<int32_t>& items, const DevBuf<float>& ratings,
-                            DevBuf<float>& P, DevBuf<float>& Q, DevBuf<float>& Y, DevBuf<float>& maps, DevBuf<float>& gb_row,
-                            const int32_t* joff, const DevBuf<int32_t>& jw, int32_t n_items, DevBuf<double>& gb,
-                            double* partial, float lr, float reg, int32_t kf, int32_t shift, hipStream_t s) {
-    const float fx = std::ldexp(1.f, shift);
-    hipLaunchKernelGGL((svdpp_round_kernel<E, 8, true>), dim3(blocks), dim3(256), 0, s, work.p, wrng.p, w0, w1, rowptr.p,
-                       items.p, ratings.p, P.p, Q.p, Y.p, rs::buffer_bytes32(Q.n, 4, "item factor matrix"),
-                       rs::buffer_bytes32(Y.n, 4, "implicit factor matrix"), maps.p, gb_row.p, gb.p, partial, lr, reg, kf, fx);
-    hipLaunchKernelGGL((pp_round_ymap_kernel<E, true>), dim3((n_items + 3) / 4), dim3(256), 0, s, Y.p, maps.p, joff,
-                       jw.p, n_items, kf, fx);
 }
 
 template <int E>
@@ -902,54 +704,6 @@ extern "C" int rs_svdpp_fit(rs_ctx* ctx, const rs_ratings* r, const rs_sgd_param
         dQ.upload(hQ.data(), hQ.size(), s);
         dY.upload(hY.data(), hY.size(), s);
         const double inv_nnz = r->nnz > 0 ? 1.0 / static_cast<double>(r->nnz) : 0.0;
-        int32_t rounds = rs::kPPRounds;
-        if (const char* env = std::getenv("RSGPU_PP_ROUNDS")) rounds = std::max(0, std::atoi(env));
-        if (rounds > 0 && fx && n_work > 0) {
-            const rs::PPRounds rr = rs::pp_rounds(order, csr, r->n_items, rounds);
-            const int32_t nw = static_cast<int32_t>(rr.wuser.size());
-            rs::DevBuf<int32_t> dw(nw), djoff(rr.joff.size()), djw(std::max<size_t>(1, rr.jw.size()));
-            rs::DevBuf<int64_t> dwr(rr.wr.size());
-            rs::DevBuf<float> dmaps(static_cast<size_t>(nw) * ld), dgbrow(std::max(1, r->n_users));
-            dw.upload(rr.wuser.data(), rr.wuser.size(), s);
-            dwr.upload(rr.wr.data(), rr.wr.size(), s);
-            djoff.upload(rr.joff.data(), rr.joff.size(), s);
-            djw.upload(rr.jw.data(), rr.jw.size(), s);
-            std::vector<int32_t> rblocks(rounds);
-            int32_t nparts = 0;
-            for (int32_t t = 0; t < rounds; ++t) {
-                rblocks[t] = std::max<int32_t>(1, std::min<int32_t>(cap, (rr.roff[t + 1] - rr.roff[t] + 3) / 4));
-                nparts += rblocks[t];
-            }
-            rs::DevBuf<double> dparts(nparts);
-            RS_HIP(hipStreamSynchronize(s));
-            rs::kernel_span_begin(ctx);
-            for (int32_t ep = 0; ep < p->n_epochs; ++ep) {
-                int32_t at = 0;
-                for (int32_t t = 0; t < rounds; ++t) {
-                    const int32_t* jo = djoff.p + static_cast<size_t>(r->n_items + 1) * t;
-                    auto go = [&](auto e_tag) {
-                        constexpr int EE = decltype(e_tag)::value;
-                        rs::launch_pp_round<EE>(rblocks[t], rr.roff[t], rr.roff[t + 1], dw, dwr, drow, dcol, dval, dP, dQ,
-                                                dY, dmaps, dgbrow, jo, djw, r->n_items, dgb, dparts.p + at, lr, reg, k, shift, s);
-                    };
-                    switch (E) {
-                        case 1: go(std::integral_constant<int, 1>{}); break;
-                        case 2: go(std::integral_constant<int, 2>{}); break;
-                        case 3: go(std::integral_constant<int, 3>{}); break;
-                        case 4: go(std::integral_constant<int, 4>{}); break;
-                        case 5: go(std::integral_constant<int, 5>{}); break;
-                        case 6: go(std::integral_constant<int, 6>{}); break;
-                        case 7: go(std::integral_constant<int, 7>{}); break;
-                        default: go(std::integral_constant<int, 8>{}); break;
-                    }
-                    RS_HIP(hipGetLastError());
-                    at += rblocks[t];
-                }
-                hipLaunchKernelGGL(rs::pp_gb_fold_kernel, dim3(1), dim3(256), 0, s, dparts.p, static_cast<int64_t>(nparts),
-                                   dgb.p, inv_nnz);
-                RS_HIP(hipGetLastError());
-            }
-        } else {
         RS_HIP(hipStreamSynchronize(s));
         rs::kernel_span_begin(ctx);
         for (int32_t ep = 0; ep < p->n_epochs; ++ep) {
@@ -967,7 +721,6 @@ extern "C" int rs_svdpp_fit(rs_ctx* ctx, const rs_ratings* r, const rs_sgd_param
             hipLaunchKernelGGL(rs::pp_gb_fold_kernel, dim3(1), dim3(256), 0, s, dpart.p,
                                static_cast<int64_t>(n_blocks), dgb.p, inv_nnz);
             RS_HIP(hipGetLastError());
-        }
         }
         rs::kernel_span_end(ctx);
         dP.download(hP.data(), hP.size(), s);
