@@ -42,6 +42,11 @@ LR, REG = 0.005, 0.02
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md chip table: 8.0 TB/s spec
 EXCHANGE_NAMES = {0: "RS_EXCHANGE_ROTATE (stratum rotation)", 1: "RS_EXCHANGE_AVERAGE", 2: "RS_EXCHANGE_ROTATE_Q",
                   3: "RS_EXCHANGE_QDELTA"}
+# what each exchange sends between the ranks (include/rsgpu.h)
+EXCHANGE_WIRE = {0: "RCCL send/recv of P rank-blocks per sub-epoch",
+                 1: "RCCL all-reduce of count-weighted user deltas per user block",
+                 2: "RCCL send/recv of Q rank-blocks and hot-item copies per sub-epoch",
+                 3: "RCCL all-reduce of weighted fp16 item moves per merge"}
 
 
 def algorithmic_bytes(nnz, n_users, k):
@@ -172,6 +177,44 @@ def load_traffic():
         except Exception:
             return None
     return None
+
+
+def measure_traffic():
+    """HBM bytes per SGD launch, measured now: two rocprofv3 --pmc passes (FETCH_SIZE, then WRITE_SIZE: they
+    do not fit one pass's TCC slots), kernel trace only, each a child process running the same workload
+    without torch (scripts/experiments/tile_epochs.py; PMC passes under torch's runtime hung on this image),
+    summarised with the gfx950 FETCH_SIZE x 2 correction (scripts/pmc_summary.py).  Returns (bytes, None) or
+    (None, reason).  RS_BENCH_PMC=0 skips it."""
+    import shutil
+    import subprocess
+    import tempfile
+    if os.environ.get("RS_BENCH_PMC", "1") == "0":
+        return None, "skipped (RS_BENCH_PMC=0)"
+    if any(k.startswith("ROCPROF") for k in os.environ) or "rocprof" in os.environ.get("LD_PRELOAD", ""):
+        return None, "bench.py itself runs under a profiler"
+    prof = shutil.which("rocprofv3")
+    if not prof:
+        return None, "rocprofv3 not found"
+    out = tempfile.mkdtemp(prefix="rs_pmc_", dir="/tmp")
+    env = dict(os.environ, TMPDIR="/tmp", EPOCHS="4")
+    for c in ("FETCH_SIZE", "WRITE_SIZE"):
+        cmd = [prof, "--pmc", c, "--kernel-trace", "--output-format", "csv", "-d", os.path.join(out, c), "-o", "run",
+               "--", sys.executable, os.path.join(REPO, "scripts", "experiments", "tile_epochs.py")]
+        try:
+            rc = subprocess.run(cmd, cwd="/tmp", env=env, stdout=subprocess.DEVNULL, stderr=subprocess.DEVNULL,
+                                timeout=150).returncode
+        except subprocess.TimeoutExpired:
+            return None, f"rocprofv3 --pmc {c} timed out"
+        print(f"bench: PMC pass {c} rc={rc}", file=sys.stderr, flush=True)
+        if rc != 0:
+            return None, f"rocprofv3 --pmc {c} exited {rc}"
+    try:
+        res = subprocess.run([sys.executable, os.path.join(REPO, "scripts", "pmc_summary.py"), out,
+                              "svd_epoch_tile_kernel"], capture_output=True, text=True, timeout=60)
+        b = json.loads(res.stdout.strip().splitlines()[-1]).get("hbm_bytes_per_launch")
+    except Exception as e:  # noqa: BLE001 -- any parse failure falls back to the committed figure
+        return None, f"PMC summary failed: {e}"
+    return (b, None) if b else (None, "no PMC rows for svd_epoch_tile_kernel")
 
 
 def spawn_ranks(n, argv, need_gpus=True):
@@ -306,7 +349,17 @@ def main():
         total_updates = nnz * world * args.steps
         ab = algorithmic_bytes(nnz, n_users, K)
         achieved = ab / avg_kernel_s / 1e9
-        traffic = load_traffic() if world == 1 else None
+        traffic, traffic_src = None, None
+        if world == 1:
+            traffic, why = measure_traffic()
+            if traffic:
+                traffic_src = ("measured in this run: FETCH_SIZE x 2 + WRITE_SIZE per launch of the SGD kernel, two "
+                               "rocprofv3 --pmc child passes over the same ML-1M workload (scripts/pmc_summary.py)")
+            else:
+                traffic = load_traffic()
+                traffic_src = (f"committed PMC figure ({why}): FETCH_SIZE x 2 + WRITE_SIZE per launch from separate "
+                               "rocprofv3 --pmc passes over the same workload (scripts/pmc_sgd.sh -> "
+                               "profiles/sgd_traffic.json)")
         line = {
             "metric": METRIC,
             "value": total_updates / dt,
@@ -331,14 +384,12 @@ def main():
                        "n_users": n_users, "n_items_per_rank": n_items, "nnz_per_rank": nnz,
                        "n_factors": K, "lr": LR, "reg": REG,
                        "parallelism": (f"item-sharded x{world}: {EXCHANGE_NAMES.get(comm_exchange, comm_exchange)}, "
-                                       f"{comm_blocks} user blocks (RCCL send/recv of P rank-blocks per sub-epoch)")
+                                       f"{comm_blocks} user blocks ({EXCHANGE_WIRE.get(comm_exchange, '?')})")
                                       if world > 1 else "single GPU"},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
                          "traffic": traffic,
-                         "traffic_source": "committed PMC figure, not measured in this run: FETCH_SIZE x 2 + "
-                                           "WRITE_SIZE per launch from separate rocprofv3 --pmc passes over the "
-                                           "same workload (scripts/pmc_sgd.sh -> profiles/sgd_traffic.json)",
+                         "traffic_source": traffic_src,
                          "kernel": "svd_epoch_tile_kernel<E=2,NW=16,RQ=2,CH=4> (tile schedule: user tiles in "
                                    "LDS, integer LDS atomics, one memory-side atomic per (item, tile) run, waves "
                                    "claim 4 runs at a time from the tile's run queue)",
