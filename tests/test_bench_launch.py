@@ -36,3 +36,19 @@ def test_too_few_gpus_fails_loudly():
 def test_world_size_must_match_gpus():
     r = _run(["--gpus", "2"], env={"WORLD_SIZE": "1", "RANK": "0", "LOCAL_RANK": "0"})
     assert r.returncode != 0 and "WORLD_SIZE=1" in r.stderr
+
+
+def test_pmc_traffic_fallbacks(monkeypatch):
+    """bench.py measures roofline.traffic with two rocprofv3 --pmc child passes; it falls back to the committed
+    figure, naming why, when the passes are switched off or bench.py already runs under a profiler (a nested
+    rocprofv3 would inherit the outer one's preload)."""
+    import importlib.util
+    spec = importlib.util.spec_from_file_location("bench_mod", os.path.join(REPO, "bench.py"))
+    bench = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(bench)
+    monkeypatch.setenv("RS_BENCH_PMC", "0")
+    assert bench.measure_traffic() == (None, "skipped (RS_BENCH_PMC=0)")
+    monkeypatch.delenv("RS_BENCH_PMC")
+    monkeypatch.setenv("ROCPROF_OUTPUT_PATH", "/tmp/x")
+    assert bench.measure_traffic() == (None, "bench.py itself runs under a profiler")
+    assert bench.load_traffic() > 0  # the committed summary it falls back to
