@@ -105,6 +105,13 @@ def ml100k_folds(ml100k):
     return folds(*ml100k)
 
 
+def _near(r, m, exp_r, exp_m):
+    """core/base_test.go checks ret <= expected + estimatorEpsilon (one-sided).  The restatement is held to
+    both sides: a value far below the reference's own score would be a different algorithm as surely as one
+    above it (measured: SVD +0.003, NMF +0.006, KNN +0.001..+0.004, SlopeOne -0.005 RMSE)."""
+    return abs(r - exp_r) <= EPS and abs(m - exp_m) <= EPS
+
+
 def _cv(fs, fit_predict):
     rs, ms = [], []
     for f in fs:
@@ -125,7 +132,7 @@ def test_svd_accuracy_regression(ml100k_folds):
         return O.svd_predict(f.tu, f.ti, P, Q, bu, bi, gb)
 
     r, m = _cv(ml100k_folds, fp)
-    assert r <= 0.934 + EPS and m <= 0.737 + EPS, (r, m)
+    assert _near(r, m, 0.934, 0.737), (r, m)
 
 
 def test_nmf_as_written_vs_intended(ml100k_folds):
@@ -148,7 +155,7 @@ def test_nmf_as_written_vs_intended(ml100k_folds):
         return O.nmf_predict(f.tu, f.ti, P, Q)
 
     r, m = _cv(ml100k_folds, fp)
-    assert r <= 0.963 + EPS and m <= 0.758 + EPS, (r, m)
+    assert _near(r, m, 0.963, 0.758), (r, m)
 
 
 def _knn_cv(fs, type_, kind=O.MSD, user_based=True):
@@ -181,7 +188,7 @@ def test_knn_accuracy_regression(ml100k_folds, type_, bound):
     """core/base_test.go:50-64 (KNN, KNNWithMean, KNNWithZScore, KNNBaseLine; user-based MSD,
     k=40, minK=1 defaults of knn.go:79-81, 226-227)."""
     r, m = _knn_cv(ml100k_folds[:2], type_)
-    assert r <= bound[0] + EPS and m <= bound[1] + EPS, (r, m)
+    assert _near(r, m, *bound), (r, m)
 
 
 def test_slope_one_hand_case():
@@ -216,7 +223,7 @@ def test_slope_one_accuracy_regression(ml100k_folds):
         return O.slope_one_predict(dev, up, uit, ur, float(np.mean(f.r)), f.tu, f.ti)
 
     r, m = _cv(ml100k_folds, fp)
-    assert r <= 0.946 + EPS and m <= 0.743 + EPS, (r, m)
+    assert _near(r, m, 0.946, 0.743), (r, m)
 
 
 def test_go_sort_restatement():
