@@ -200,10 +200,15 @@ def measure_traffic():
     for c in ("FETCH_SIZE", "WRITE_SIZE"):
         cmd = [prof, "--pmc", c, "--kernel-trace", "--output-format", "csv", "-d", os.path.join(out, c), "-o", "run",
                "--", sys.executable, os.path.join(REPO, "scripts", "experiments", "tile_epochs.py")]
+        # own process group: a pass that hangs is killed with everything it started (the profiled workload)
+        proc = subprocess.Popen(cmd, cwd="/tmp", env=env, stdout=subprocess.DEVNULL, stderr=subprocess.DEVNULL,
+                                start_new_session=True)
         try:
-            rc = subprocess.run(cmd, cwd="/tmp", env=env, stdout=subprocess.DEVNULL, stderr=subprocess.DEVNULL,
-                                timeout=150).returncode
+            rc = proc.wait(timeout=150)
         except subprocess.TimeoutExpired:
+            import signal
+            os.killpg(proc.pid, signal.SIGKILL)
+            proc.wait()
             return None, f"rocprofv3 --pmc {c} timed out"
         print(f"bench: PMC pass {c} rc={rc}", file=sys.stderr, flush=True)
         if rc != 0:
