@@ -692,6 +692,13 @@ __global__ __launch_bounds__(kEpilogueThreads) void svd_epoch_epilogue_kernel(
     }
     constexpr int NWV = kEpilogueThreads / 64;
     __shared__ double sh[NWV], sl[NWV];
+    // thread 0's own operands are loaded first, so their latency overlaps the partials' loads instead of
+    // following the reduction
+    double gb_old = 0.0, prev = 0.0;
+    if (tid == 0) {
+        gb_old = gb[0];
+        if (loss_part && loss_state) prev = loss_state[0];
+    }
     double t = 0.0, l = 0.0;
     for (int64_t x = tid; x < n_partial; x += kEpilogueThreads) {
         t += partial[x];
@@ -711,12 +718,12 @@ __global__ __launch_bounds__(kEpilogueThreads) void svd_epoch_epilogue_kernel(
             sh[0] += sh[w];
             sl[0] += sl[w];
         }
-        gb[0] += sh[0] * inv_nnz;
+        gb[0] = gb_old + sh[0] * inv_nnz;
         if (done) *done = 0;
         if (loss_part && loss_state) {
             // the divergence guard's second signal: this epoch's training MSE (at the ratings' pre-update
             // residuals) more than 1.03x the previous epoch's -- SGD at a stable rate does not raise it
-            const double mse = sl[0] * inv_nnz * inv_lr2, prev = loss_state[0];
+            const double mse = sl[0] * inv_nnz * inv_lr2;
             if (!(mse < 1e30) || (prev > 0.0 && mse > 1.03 * prev)) flag[0] = 1;
             loss_state[0] = mse;
         }
