@@ -466,6 +466,10 @@ int rs_svd_plan_set_qdelta_wire(rs_svd_plan* plan, int32_t bits);
  * every cold_every-th block (the largest divisor of the merges per epoch up to cold_every; 1: every merge is a
  * full one).  Set before the join, the same on every rank. */
 int rs_svd_plan_set_qdelta_split(rs_svd_plan* plan, double hot_ratings, int32_t cold_every);
+/* RS_EXCHANGE_QDELTA's merge weights: the contraction per rating a = 1 - lr x gamma in kappa_i (gamma = 1: the
+ * unit curvature above, the default; 0: w_i = 1, the plain sum of the moves).  Set before the join, the same on
+ * every rank. */
+int rs_svd_plan_set_qdelta_curvature(rs_svd_plan* plan, double gamma);
 /* RS_EXCHANGE_ROTATE_Q on Zipf-headed sets: a stratum (one rank's users x one item block) holds an item's
  * ratings n_blocks-fold concentrated, so the head's rows get many concurrent runs in flight (Hogwild staleness
  * that diverges at lr 0.005; configs[4]: the hottest item is 0.8 % of the set but 12.7 % of its stratum).  An
@@ -489,7 +493,14 @@ int rs_svd_plan_set_hot_split(rs_svd_plan* plan, double share, int64_t min_strat
 int rs_svd_plan_time_blocks(rs_svd_plan* plan, float lr, float reg, double* ms, int32_t n);
 /* Test hook (fault injection): the next rs_svd_plan_epochs_sharded / rs_svd_group_epochs call on this
  * plan throws at the start of its sub-epoch `sub_epoch` (once), so tests can check that the other ranks
- * are released.  -1 clears it.  Nothing else reads it. */
+ * are released.  RS_FAULT_DIVERGE instead changes one word of this rank's replicated factors just before
+ * the call's consistency check (below).  -1 clears it.  Nothing else reads it.
+ *
+ * Consistency check: after every sharded call (every exchange, n_ranks > 1) the ranks compare checksums of
+ * their replicated state -- P with b_u and GlobalBias, and Q with b_i under ROTATE_Q / QDELTA -- by RCCL max
+ * and min all-reduces (or the in-process group's barrier); a mismatch is RS_ERR_NUMERIC on every rank
+ * (rs_svd_fit_multi redoes the fit, as for a divergence). */
+#define RS_FAULT_DIVERGE (-2)
 int rs_svd_plan_inject_fault(rs_svd_plan* plan, int32_t sub_epoch);
 /* Host only: RS_EXCHANGE_ROTATE's sub-epoch `sub_epoch` of `rank` -- out[0] the rank-block it trains,
  * out[1] the rank its rows are sent to, out[2] the rank-block it receives, out[3] the rank that sends

@@ -50,6 +50,7 @@
 #include <dlfcn.h>
 
 #include <algorithm>
+#include <array>
 #include <cmath>
 #include <atomic>
 #include <condition_variable>
@@ -71,6 +72,7 @@
 namespace rs {
 
 constexpr int kMaxLocal = 16;  // shards of one in-process exchange
+constexpr int32_t kFaultDiverge = RS_FAULT_DIVERGE;  // rs_svd_plan_inject_fault: perturb a replica before the check
 
 struct LocalGroup {  // host-barrier exchange between the shards of one process
     int n = 0;
@@ -86,6 +88,7 @@ struct LocalGroup {  // host-barrier exchange between the shards of one process
     std::vector<float*> hot;  // ROTATE_Q: every shard's partial hot-copy averages
     std::vector<int32_t*> dq; // QDELTA: every shard's item moves (full merges)
     std::vector<int32_t*> hdq;  // QDELTA: every shard's hot-item moves (hot merges)
+    std::vector<std::array<unsigned long long, 6>> chk;  // check_replicas: every shard's checksums
     std::vector<int> dev;
     void barrier() {
         std::unique_lock<std::mutex> l(m);
@@ -124,7 +127,9 @@ struct ShardComm {
     int32_t wire = 32;
     hipEvent_t ev_ar[2] = {nullptr, nullptr};  // QDELTA: merge m's all-reduce ended (comm stream)
     DevBuf<float> qw;                 // QDELTA: merge weight per item (for the call's lr)
+    DevBuf<unsigned long long> chk;   // check_replicas: block partials and the six sums (+ their max / min)
     float qw_lr = -1.f;
+    double qw_curv = -1.0;
     ncclComm_t nccl = nullptr;
     bool own_nccl = true;
     std::atomic<bool> aborted{false};
@@ -416,8 +421,13 @@ __global__ __launch_bounds__(256) void qdelta_correct_kernel(int32_t* __restrict
         if (Q0) reinterpret_cast<int4*>(Q0)[t] = v;
     }
 }
-// QDELTA, in-process exchange: out = the sum over the shards of their weighted moves (int32: exact; fp16: summed
-// in fp32 in shard order, rounded once)
+// QDELTA, in-process exchange: out = the sum over the shards of their weighted moves.  int32: exact and
+// order-free.  fp16: the arithmetic of RCCL's ring all-reduce (its reduce-scatter), so that the one-GPU tests run
+// the numerics an 8-GPU fit runs: the values are cut into N contiguous chunks; chunk c's sum starts at rank
+// (c + 1) mod N and takes the ranks in ring order, rounded to fp16 after every add (a float add of two halves
+// rounded to half is the correctly rounded half add: the float sum is exact up to an exponent gap of 13, past
+// which the smaller term is below a quarter ulp of the half).  RCCL's own chunk-to-rank map also depends on its
+// channels and protocol; the rounding per hop and the rotated starts are what this models.
 struct WireSrcs {
     const void* p[kMaxLocal];
 };
@@ -431,14 +441,62 @@ __global__ __launch_bounds__(256) void qdelta_sum_kernel(WireSrcs src, int32_t n
             for (int32_t r = 1; r < n_src; ++r) a = add4(a, reinterpret_cast<const int4*>(src.p[r])[t]);
             reinterpret_cast<int4*>(out)[t] = a;
         } else {
-            float4 a = Wire4<16>::f(reinterpret_cast<const T*>(src.p[0])[t]);
-            for (int32_t r = 1; r < n_src; ++r) {
-                const float4 b = Wire4<16>::f(reinterpret_cast<const T*>(src.p[r])[t]);
-                a.x += b.x; a.y += b.y; a.z += b.z; a.w += b.w;
+            const int32_t chunk = static_cast<int32_t>(static_cast<uint64_t>(t) * static_cast<uint32_t>(n_src) / n4);
+            int32_t r = (chunk + 1) % n_src;
+            T a = reinterpret_cast<const T*>(src.p[r])[t];
+            for (int32_t j = 1; j < n_src; ++j) {
+                r = r + 1 == n_src ? 0 : r + 1;
+                const float4 x = Wire4<16>::f(a), y = Wire4<16>::f(reinterpret_cast<const T*>(src.p[r])[t]);
+                a = Wire4<16>::h(make_float4(x.x + y.x, x.y + y.y, x.z + y.z, x.w + y.w));
             }
-            reinterpret_cast<T*>(out)[t] = Wire4<16>::h(a);
+            reinterpret_cast<T*>(out)[t] = a;
         }
     }
+}
+
+// Replica checksum (the cross-rank consistency check after a sharded call): per block of 256 threads, two 64-bit
+// sums over the 32-bit words w_t of a matrix -- sum w_t and sum w_t (2t + 1) (mod 2^64: the second catches words
+// moved between positions) -- written to part[2 blockIdx], part[2 blockIdx + 1]; replica_fold_kernel adds the
+// blocks' partials in block order.  No atomics: the same words give the same bits.
+__global__ __launch_bounds__(256) void replica_sum_kernel(const uint32_t* __restrict__ w, int64_t n,
+                                                          unsigned long long* __restrict__ part) {
+    __shared__ unsigned long long s1[256], s2[256];
+    unsigned long long a = 0, b = 0;
+    for (int64_t t = static_cast<int64_t>(blockIdx.x) * 256 + threadIdx.x; t < n; t += static_cast<int64_t>(gridDim.x) * 256) {
+        const unsigned long long v = w[t];
+        a += v;
+        b += v * static_cast<unsigned long long>(2 * t + 1);
+    }
+    s1[threadIdx.x] = a;
+    s2[threadIdx.x] = b;
+    __syncthreads();
+    for (int h = 128; h > 0; h >>= 1) {
+        if (static_cast<int>(threadIdx.x) < h) {
+            s1[threadIdx.x] += s1[threadIdx.x + h];
+            s2[threadIdx.x] += s2[threadIdx.x + h];
+        }
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) {
+        part[2 * blockIdx.x] = s1[0];
+        part[2 * blockIdx.x + 1] = s2[0];
+    }
+}
+__global__ void replica_fold_kernel(const unsigned long long* __restrict__ part, int32_t nb,
+                                    unsigned long long* __restrict__ out) {
+    if (threadIdx.x == 0) {
+        unsigned long long a = 0, b = 0;
+        for (int32_t x = 0; x < nb; ++x) {
+            a += part[2 * x];
+            b += part[2 * x + 1];
+        }
+        out[0] = a;
+        out[1] = b;
+    }
+}
+// test hook (RS_FAULT_DIVERGE): one word of a replica changes
+__global__ void poke_kernel(uint32_t* w) {
+    if (threadIdx.x == 0) w[0] += 1u;
 }
 
 int grid_for(int64_t n) { return static_cast<int>(std::max<int64_t>(1, std::min<int64_t>(4096, (n + 255) / 256))); }
@@ -964,7 +1022,7 @@ void epochs_qdelta(rs_svd_plan* pl, int32_t n_epochs, float lr, float reg, hipSt
     const double inv_total = c.total_nnz > 0 ? 1.0 / c.total_nnz : 0.0;
     const int32_t nb = static_cast<int32_t>(pl->t_block_tile.size()) - 1;  // blocks per epoch
     const int32_t F = c.cold_every;
-    if (c.qw_lr != lr) {  // the merge weights for this lr (module header: kappa / c per item)
+    if (c.qw_lr != lr || c.qw_curv != pl->qdelta_curv) {  // the merge weights for this lr (module header: kappa / c per item)
         const size_t n1 = static_cast<size_t>(std::max(1, ni));
         std::vector<float> cn(n1), cc(n1), w(n1, 1.f);
         std::vector<int32_t> hp(n1);
@@ -972,7 +1030,7 @@ void epochs_qdelta(rs_svd_plan* pl, int32_t n_epochs, float lr, float reg, hipSt
         c.item_c.download(cc.data(), n1, s);
         c.hot_pos.download(hp.data(), n1, s);
         RS_HIP(hipStreamSynchronize(s));
-        const double a = std::max(1e-12, 1.0 - static_cast<double>(lr));
+        const double a = std::max(1e-12, 1.0 - static_cast<double>(lr) * pl->qdelta_curv);
         for (size_t x = 0; x < static_cast<size_t>(ni); ++x) {
             // the moves of 1 / merges of an epoch: every block's for a hot item, cold_every blocks' for a cold one
             const double merges = static_cast<double>(std::max(1, hp[x] >= 0 ? nb : nb / F));
@@ -985,6 +1043,7 @@ void epochs_qdelta(rs_svd_plan* pl, int32_t n_epochs, float lr, float reg, hipSt
         c.qw.upload(w.data(), n1, s);
         RS_HIP(hipStreamSynchronize(s));  // w dies with this scope
         c.qw_lr = lr;
+        c.qw_curv = pl->qdelta_curv;
     }
     int32_t* const Qi = reinterpret_cast<int32_t*>(pl->Q.p);
     const bool ex = N > 1 && (c.nccl || c.local);
@@ -1123,6 +1182,80 @@ void epochs_qdelta(rs_svd_plan* pl, int32_t n_epochs, float lr, float reg, hipSt
 
 }  // namespace
 
+namespace {
+
+// The cross-rank consistency check after a sharded call (advisor round 5): every rank must end with the same
+// replicated state -- P with b_u and GlobalBias always (ROTATE's broadcast rank-blocks, AVERAGE's summed deltas),
+// Q with b_i too for ROTATE_Q and QDELTA (user ranges, every item on every rank).  Each rank sums the words of its copies (replica_sum_kernel: two 64-bit sums per matrix),
+// and the ranks compare them: RCCL max and min all-reduces of the six sums (they agree iff max == min), or the
+// in-process group's host barrier.  A mismatch -- a transfer or a collective that delivered different bytes to
+// different ranks -- is RS_ERR_NUMERIC on every rank (rs_svd_fit_multi refits).  One pass over P and Q per call
+// (configs[4] at 8 ranks: 14 GB, under 2 ms), one 96-byte readback.
+void check_replicas(rs_svd_plan* pl, hipStream_t s) {
+    ShardComm& c = *pl->shard;
+    if (c.nranks <= 1 || !(c.nccl || c.local)) return;
+    const bool with_q = c.mode == RS_EXCHANGE_QDELTA || c.mode == RS_EXCHANGE_ROTATE_Q;
+    constexpr int kBlocks = 1024;
+    if (c.chk.n < 2 * kBlocks + 18) c.chk.alloc(2 * kBlocks + 18);
+    unsigned long long* const part = c.chk.p;
+    unsigned long long* const sums = c.chk.p + 2 * kBlocks;  // 6 sums, then 6 maxima and 6 minima
+    if (pl->fault_sub_epoch == kFaultDiverge) {  // test hook: this rank's replica differs by one word
+        pl->fault_sub_epoch = -1;
+        hipLaunchKernelGGL(poke_kernel, dim3(1), dim3(64), 0, s,
+                           reinterpret_cast<uint32_t*>(with_q ? static_cast<void*>(pl->Q.p) : static_cast<void*>(pl->P.p)));
+    }
+    struct M {
+        const void* p;
+        int64_t words;
+    } mats[3] = {{pl->P.p, static_cast<int64_t>(pl->n_users) * pl->ld},
+                 {with_q ? pl->Q.p : nullptr, with_q ? static_cast<int64_t>(pl->n_items) * pl->ld : 0},
+                 {pl->gb.p, 2}};
+    for (int x = 0; x < 3; ++x) {
+        const int nb = static_cast<int>(std::max<int64_t>(1, std::min<int64_t>(kBlocks, (mats[x].words + 255) / 256)));
+        hipLaunchKernelGGL(replica_sum_kernel, dim3(nb), dim3(256), 0, s, static_cast<const uint32_t*>(mats[x].p),
+                           mats[x].words, part);
+        hipLaunchKernelGGL(replica_fold_kernel, dim3(1), dim3(64), 0, s, part, nb, sums + 2 * x);
+    }
+    RS_HIP(hipGetLastError());
+    unsigned long long h[18] = {};
+    if (c.nccl) {
+        RS_HIP(hipEventRecord(c.ev_gb, s));
+        RS_HIP(hipStreamWaitEvent(c.cs, c.ev_gb, 0));
+        check_nccl(ncclGroupStart(), "ncclGroupStart");
+        check_nccl(ncclAllReduce(sums, sums + 6, 6, ncclUint64, ncclMax, c.nccl, c.cs), "ncclAllReduce(replica max)");
+        check_nccl(ncclAllReduce(sums, sums + 12, 6, ncclUint64, ncclMin, c.nccl, c.cs), "ncclAllReduce(replica min)");
+        check_nccl(ncclGroupEnd(), "ncclGroupEnd");
+        RS_HIP(hipMemcpyAsync(h, sums, sizeof(h), hipMemcpyDeviceToHost, c.cs));
+        RS_HIP(hipStreamSynchronize(c.cs));
+        for (int x = 0; x < 6; ++x)
+            if (h[6 + x] != h[12 + x])
+                throw NumericError{"the ranks' replicated factors disagree after the exchange (rank " + std::to_string(c.rank) +
+                                   ", " + (x < 2 ? "P" : x < 4 ? "Q" : "GlobalBias") + " checksum)"};
+        return;
+    }
+    RS_HIP(hipMemcpyAsync(h, sums, 6 * sizeof(unsigned long long), hipMemcpyDeviceToHost, s));
+    RS_HIP(hipStreamSynchronize(s));
+    LocalGroup& lg = *c.local;
+    {
+        std::lock_guard<std::mutex> l(lg.m);
+        if (lg.chk.size() != static_cast<size_t>(lg.n)) lg.chk.resize(static_cast<size_t>(lg.n));
+        std::copy(h, h + 6, lg.chk[c.rank].begin());
+    }
+    lg.barrier();  // every shard's sums are in
+    std::array<unsigned long long, 6> mine;
+    std::copy(h, h + 6, mine.begin());
+    bool same = true;
+    {
+        std::lock_guard<std::mutex> l(lg.m);
+        for (const auto& o : lg.chk) same = same && o == mine;
+    }
+    lg.barrier();  // nobody's sums are overwritten before every shard compared
+    if (!same)
+        throw NumericError{"the shards' replicated factors disagree after the exchange (shard " + std::to_string(c.rank) + ")"};
+}
+
+}  // namespace
+
 // n_epochs of the item-sharded schedule on stream s (every rank calls it with the same arguments)
 void epochs_sharded(rs_svd_plan* pl, int32_t n_epochs, float lr, float reg, hipStream_t s) {
     if (!pl->tiles_built) tile_build(pl);
@@ -1135,6 +1268,7 @@ void epochs_sharded(rs_svd_plan* pl, int32_t n_epochs, float lr, float reg, hipS
     else if (pl->shard->mode == RS_EXCHANGE_QDELTA) epochs_qdelta(pl, n_epochs, lr, reg, s);
     else epochs_rotate(pl, n_epochs, lr, reg, s);
     RS_HIP(hipEventRecord(pl->ev1, s));
+    if (n_epochs > 0) check_replicas(pl, s);
     pl->last_launches = n_epochs;  // rs_svd_plan_last_kernel_ms: the call's device span per epoch
     pl->last_stream = s;
     pl->last_ms = -1.0;
@@ -1178,7 +1312,7 @@ void group_join(rs_svd_group* g, int32_t n_blocks) {
             throw std::invalid_argument("shards must have the same users and n_factors");
         if (pl->exchange != g->plans[0]->exchange) throw std::invalid_argument("shards must use the same exchange");
         if (qd && (pl->qdelta_wire != g->plans[0]->qdelta_wire || pl->qdelta_hot != g->plans[0]->qdelta_hot ||
-                   pl->qdelta_cold_every != g->plans[0]->qdelta_cold_every))
+                   pl->qdelta_cold_every != g->plans[0]->qdelta_cold_every || pl->qdelta_curv != g->plans[0]->qdelta_curv))
             throw std::invalid_argument("shards must use the same QDELTA wire width and split");
         if (rq) {
             if (pl->n_items != ni) throw std::invalid_argument("RS_EXCHANGE_ROTATE_Q / QDELTA shards must have the same items");
@@ -1362,6 +1496,14 @@ extern "C" int rs_svd_plan_set_qdelta_split(rs_svd_plan* pl, double hot_ratings,
     return RS_OK;
 }
 
+extern "C" int rs_svd_plan_set_qdelta_curvature(rs_svd_plan* pl, double gamma) {
+    if (!pl) return rs::set_error(nullptr, RS_ERR_INVALID, "plan is NULL");
+    if (!(gamma >= 0.0) || !std::isfinite(gamma)) return rs::set_error(pl->ctx, RS_ERR_INVALID, "bad QDELTA curvature");
+    if (pl->shard) return rs::set_error(pl->ctx, RS_ERR_INVALID, "plan is joined to a group (leave first)");
+    pl->qdelta_curv = gamma;
+    return RS_OK;
+}
+
 extern "C" int rs_svd_plan_set_qdelta_wire(rs_svd_plan* pl, int32_t bits) {
     if (!pl) return rs::set_error(nullptr, RS_ERR_INVALID, "plan is NULL");
     if (bits != 16 && bits != 32) return rs::set_error(pl->ctx, RS_ERR_INVALID, "QDELTA wire: 16 or 32 bits");
@@ -1419,7 +1561,7 @@ extern "C" int rs_svd_plan_set_hot_split(rs_svd_plan* pl, double share, int64_t 
 }
 
 extern "C" int rs_svd_plan_inject_fault(rs_svd_plan* pl, int32_t sub_epoch) {
-    if (!pl || sub_epoch < -1) return rs::set_error(pl ? pl->ctx : nullptr, RS_ERR_INVALID, "bad arguments");
+    if (!pl || sub_epoch < RS_FAULT_DIVERGE) return rs::set_error(pl ? pl->ctx : nullptr, RS_ERR_INVALID, "bad arguments");
     pl->fault_sub_epoch = sub_epoch;
     return RS_OK;
 }
@@ -1470,11 +1612,12 @@ extern "C" int rs_svd_plan_join(rs_svd_plan* pl, const void* id, int32_t rank, i
         const size_t shift_at = cnt.size();  // every rank's fixed-point shift: the group runs at the smallest
         cnt.resize(shift_at + static_cast<size_t>(n_ranks), 0.0);
         cnt[shift_at + rank] = static_cast<double>(pl->fx_shift);
-        const size_t wire_at = cnt.size();  // every rank's QDELTA settings (must agree): wire, split
-        cnt.resize(wire_at + 3 * static_cast<size_t>(n_ranks), 0.0);
-        cnt[wire_at + 3 * rank] = static_cast<double>(pl->qdelta_wire);
-        cnt[wire_at + 3 * rank + 1] = pl->qdelta_hot;
-        cnt[wire_at + 3 * rank + 2] = static_cast<double>(pl->qdelta_cold_every);
+        const size_t wire_at = cnt.size();  // every rank's QDELTA settings (must agree): wire, split, curvature
+        cnt.resize(wire_at + 4 * static_cast<size_t>(n_ranks), 0.0);
+        cnt[wire_at + 4 * rank] = static_cast<double>(pl->qdelta_wire);
+        cnt[wire_at + 4 * rank + 1] = pl->qdelta_hot;
+        cnt[wire_at + 4 * rank + 2] = static_cast<double>(pl->qdelta_cold_every);
+        cnt[wire_at + 4 * rank + 3] = pl->qdelta_curv;
         cnt.push_back(static_cast<double>(pl->nnz));
         rs::DevBuf<double> d(cnt.size());
         d.upload(cnt.data(), cnt.size(), s);
@@ -1483,10 +1626,10 @@ extern "C" int rs_svd_plan_join(rs_svd_plan* pl, const void* id, int32_t rank, i
         RS_HIP(hipStreamSynchronize(s));
         c->total_nnz = cnt.back();
         for (int32_t r = 0; qd && r < n_ranks; ++r)
-            if (cnt[wire_at + 3 * r] != static_cast<double>(pl->qdelta_wire) || cnt[wire_at + 3 * r + 1] != pl->qdelta_hot ||
-                cnt[wire_at + 3 * r + 2] != static_cast<double>(pl->qdelta_cold_every))
+            if (cnt[wire_at + 4 * r] != static_cast<double>(pl->qdelta_wire) || cnt[wire_at + 4 * r + 1] != pl->qdelta_hot ||
+                cnt[wire_at + 4 * r + 2] != static_cast<double>(pl->qdelta_cold_every) || cnt[wire_at + 4 * r + 3] != pl->qdelta_curv)
                 throw std::invalid_argument("ranks must use the same QDELTA wire width and split "
-                                            "(rs_svd_plan_set_qdelta_wire / _split)");
+                                            "(rs_svd_plan_set_qdelta_wire / _split / _curvature)");
         for (int32_t r = 0; r < n_ranks; ++r)  // (Q rows travel between ranks as fixed-point words)
             pl->fx_shift = std::min(pl->fx_shift, static_cast<int32_t>(cnt[shift_at + r]));
         if (rq) {
@@ -1562,6 +1705,7 @@ extern "C" int rs_svd_group_epochs(rs_svd_group* g, int32_t n_epochs, float lr, 
     if (!g || n_epochs < 0) return rs::set_error(nullptr, RS_ERR_INVALID, "bad group arguments");
     const size_t n = g->plans.size();
     std::vector<std::string> errs(n);
+    std::vector<uint8_t> numeric(n, 0);  // the shard's check_replicas failed (every shard finished the call)
     std::vector<std::thread> th;
     for (size_t r = 0; r < n; ++r)
         th.emplace_back([&, r] {  // one host thread per shard
@@ -1572,10 +1716,13 @@ extern "C" int rs_svd_group_epochs(rs_svd_group* g, int32_t n_epochs, float lr, 
                 RS_HIP(hipStreamSynchronize(pl->ctx->stream));
             } catch (const rs::HipError& e) {
                 errs[r] = e.what;
+            } catch (const rs::NumericError& e) {
+                errs[r] = e.what;
+                numeric[r] = 1;
             } catch (const std::exception& e) {
                 errs[r] = e.what();
             }
-            if (!errs[r].empty()) {  // release the other shards: host barrier or pending collectives
+            if (!errs[r].empty() && !numeric[r]) {  // release the other shards: host barrier or pending collectives
                 if (g->local) g->local->fail();
                 for (rs_svd_plan* q : g->plans)
                     if (q->shard) q->shard->abort_comm();
@@ -1583,7 +1730,10 @@ extern "C" int rs_svd_group_epochs(rs_svd_group* g, int32_t n_epochs, float lr, 
         });
     for (std::thread& t : th) t.join();
     for (size_t r = 0; r < n; ++r)
-        if (!errs[r].empty()) return rs::set_error(g->plans[r]->ctx, RS_ERR_HIP, "shard " + std::to_string(r) + ": " + errs[r]);
+        if (!errs[r].empty() && !numeric[r])
+            return rs::set_error(g->plans[r]->ctx, RS_ERR_HIP, "shard " + std::to_string(r) + ": " + errs[r]);
+    for (size_t r = 0; r < n; ++r)
+        if (!errs[r].empty()) return rs::set_error(g->plans[r]->ctx, RS_ERR_NUMERIC, "shard " + std::to_string(r) + ": " + errs[r]);
     return RS_OK;
 }
 
@@ -1712,6 +1862,10 @@ extern "C" int rs_svd_fit_multi(const int32_t* devices, int32_t n_devices, const
         int e = rs_svd_group_create(plans.data(), n, n_blocks, &g);
         if (e != RS_OK) return e;
         e = rs_svd_group_epochs(g, p->n_epochs, static_cast<float>(p->lr), static_cast<float>(p->reg));
+        if (e == RS_ERR_NUMERIC && attempt < 3 && p->n_epochs > 0) {  // the shards' replicas disagree: redo
+            ++refits;
+            continue;
+        }
         if (e != RS_OK) return e;
         bool diverged = false;  // any shard's range flag, a non-finite GlobalBias or a row past the guard bound
         for (int32_t s = 0; s < n; ++s) {

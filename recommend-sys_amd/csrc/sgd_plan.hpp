@@ -126,6 +126,7 @@ struct rs_svd_plan {
     int32_t qdelta_wire = 16;               // QDELTA: bits per item move on the wire (16: fp16, 32: int32 fixed point)
     double qdelta_hot = 4.0;                // QDELTA: ratings per rank and block that make an item hot (<= 0: all hot)
     int32_t qdelta_cold_every = 2;          // QDELTA: most blocks between a cold item's merges (multi.hip kQdelta*)
+    double qdelta_curv = 1.0;               // QDELTA: curvature of the merge weights' contraction, a = 1 - lr x this
     int32_t fault_sub_epoch = -1;  // test hook (rs_svd_plan_inject_fault): the next sharded call throws there
     // how tiles are formed (rs_svd_plan_set_tile_rule): RS_TILE_RULE_LPT (host: LPT by ratings + cost
     // refinement), RS_TILE_RULE_FILL (host: users by degree dealt boustrophedon), RS_TILE_RULE_FILL_DEVICE

@@ -24,6 +24,7 @@ SIM_COSINE, SIM_MSD, SIM_PEARSON = 0, 1, 2
 TIE_GO_SORT, TIE_STABLE = 0, 1  # KNN.Predict tie order (rs_knn_plan_set_tie_order)
 DEV_SLOPE_ONE = 3  # rs_knn_sims kind: SlopeOne deviation matrix (slope_one.go:64-92)
 EXCHANGE_ROTATE, EXCHANGE_AVERAGE, EXCHANGE_ROTATE_Q, EXCHANGE_QDELTA = 0, 1, 2, 3  # multi-GPU exchange (rsgpu.h)
+FAULT_DIVERGE = -2  # rs_svd_plan_inject_fault: perturb a replica before the consistency check (rsgpu.h)
 TILE_RULE_LPT, TILE_RULE_FILL, TILE_RULE_FILL_DEVICE = 0, 1, 2  # how users are cut into tiles (rsgpu.h)
 
 HEADER_SYMBOLS = (
@@ -47,6 +48,7 @@ HEADER_SYMBOLS = (
     "rs_comm_unique_id", "rs_svd_plan_join", "rs_svd_plan_epochs_sharded", "rs_svd_plan_leave",
     "rs_svd_plan_set_user_blocks", "rs_svd_group_create", "rs_svd_group_epochs", "rs_svd_group_destroy",
     "rs_item_shards", "rs_svd_fit_multi", "rs_tile_schedule_host", "rs_svd_plan_set_exchange", "rs_svd_plan_set_qdelta_wire", "rs_svd_plan_set_qdelta_split",
+    "rs_svd_plan_set_qdelta_curvature",
     "rs_comm_info", "rs_rotation_step", "rs_svd_plan_shard_info", "rs_svd_plan_qdelta_info", "rs_svd_plan_inject_fault",
     "rs_svd_plan_time_blocks", "rs_knn_plan_set_tie_order", "rs_fit_refits", "rs_fit_multi_refits",
     "rs_svd_plan_set_hot_split",
@@ -176,6 +178,7 @@ def lib():
             "rs_svd_plan_set_exchange": (C.c_int, [_vp, _i32]),
             "rs_svd_plan_set_qdelta_wire": (C.c_int, [_vp, _i32]),
             "rs_svd_plan_set_qdelta_split": (C.c_int, [_vp, C.c_double, _i32]),
+            "rs_svd_plan_set_qdelta_curvature": (C.c_int, [_vp, C.c_double]),
             "rs_svd_plan_inject_fault": (C.c_int, [_vp, _i32]),
             "rs_svd_plan_time_blocks": (C.c_int, [_vp, _flt, _flt, _vp, _i32]),
             "rs_knn_plan_set_tie_order": (C.c_int, [_vp, _i32]),
@@ -502,6 +505,10 @@ class SvdPlan:
     def set_qdelta_split(self, hot_ratings, cold_every):
         """RS_EXCHANGE_QDELTA's hot / cold split (rs_svd_plan_set_qdelta_split)."""
         self.ctx.check(lib().rs_svd_plan_set_qdelta_split(self.h, float(hot_ratings), int(cold_every)))
+
+    def set_qdelta_curvature(self, gamma):
+        """RS_EXCHANGE_QDELTA's merge-weight curvature (rs_svd_plan_set_qdelta_curvature: a = 1 - lr x gamma)."""
+        self.ctx.check(lib().rs_svd_plan_set_qdelta_curvature(self.h, float(gamma)))
 
     def set_qdelta_wire(self, bits):
         """RS_EXCHANGE_QDELTA's moves on the wire: 16 (fp16, default) or 32 (int32 fixed point; exact sums)."""

@@ -86,6 +86,10 @@ def parse(argv=None):
     ap.add_argument("--wire", type=int, default=16, choices=[16, 32], help="QDELTA moves on the wire: fp16 or int32")
     ap.add_argument("--hot", type=float, default=None, help="QDELTA hot threshold, ratings per rank and block")
     ap.add_argument("--cold-every", type=int, default=None, help="QDELTA most blocks between a cold item's merges")
+    ap.add_argument("--curv", type=float, default=None, help="QDELTA merge-weight curvature (library default 1)")
+    ap.add_argument("--variants", default=None,
+                    help="JSON list of option dicts (blocks, wire, hot, cold_every, curv, epochs): several sharded "
+                         "fits of the one generated set, each after the whole-set fit")
     return ap.parse_args(argv)
 
 
@@ -108,6 +112,8 @@ def run(args, say=log):
                      f"{args.seed}), library defaults", "n_users": U, "n_items": I, "nnz_train": nnz,
            "n_holdout": int(len(hr)), "epochs": args.epochs, "lr": LR, "reg": REG, "gen_s": t_gen}
 
+    variants = json.loads(args.variants) if args.variants else [{}]
+    ep_whole = max([args.epochs] + [int(v.get("epochs", 0)) for v in variants])
     whole = None
     if not args.no_whole:  # the same set as one plan: one CSR over all users
         t0 = time.perf_counter()
@@ -122,7 +128,7 @@ def run(args, say=log):
         t_plan = time.perf_counter() - t0
         r0 = plan.evaluate(hu, hi_, hr)[0]
         curve, ep_s = [], []
-        for e in range(args.epochs):
+        for e in range(ep_whole):
             t = time.perf_counter()
             plan.epochs(1, LR, REG)
             ctx.check(rsgpu.lib().rs_synchronize(ctx.h))
@@ -134,6 +140,21 @@ def run(args, say=log):
         out["whole"] = whole
         print(json.dumps({"whole": whole}), flush=True)
 
+    out["variants"] = []
+    for vi, var in enumerate(variants):
+        a = argparse.Namespace(**{**vars(args), **var})
+        log(f"variant {vi}: {var}")
+        sh = sharded(a, ctx, parts, hu, hi_, hr, gb0, whole)
+        sh["variant"] = var
+        out["variants"].append(sh)
+        out["sharded"] = sh
+    ctx.close()
+    return out
+
+
+def sharded(args, ctx, parts, hu, hi_, hr, gb0, whole):
+    """The sharded fit of the generated set (one variant of the options)."""
+    U, I, k, n = args.users, args.items, args.k, args.shards
     # the sharded fit: n plans over user ranges (global ids, all items), Q item blocks rotate
     t0 = time.perf_counter()
     plans = []
@@ -143,7 +164,9 @@ def run(args, say=log):
         if args.exchange == "qdelta":
             pl.set_qdelta_wire(args.wire)
             if args.hot is not None or args.cold_every is not None:
-                pl.set_qdelta_split(16.0 if args.hot is None else args.hot, 4 if args.cold_every is None else args.cold_every)
+                pl.set_qdelta_split(4.0 if args.hot is None else args.hot, 2 if args.cold_every is None else args.cold_every)
+            if args.curv is not None:
+                pl.set_qdelta_curvature(args.curv)
         if args.wg:
             pl.set_tiles(workgroups=args.wg)
         if args.hot_share is not None or args.hot_min is not None or args.hot_merge is not None:
@@ -172,7 +195,9 @@ def run(args, say=log):
           "qdelta_cold_every": qinfo[1] if qinfo else None,
           "rmse_init": r0, "rmse_per_epoch": curve, "epoch_s_one_gpu": ep_s}
     if whole:
-        sh["rmse_diff_vs_whole"] = curve[-1] - whole["rmse_per_epoch"][-1]
+        wc = whole["rmse_per_epoch"]
+        sh["rmse_diff_vs_whole"] = curve[-1] - wc[len(curve) - 1] if len(wc) >= len(curve) else None
+        sh["rmse_diff_per_epoch"] = [a - b for a, b in zip(curve, wc)]
     g.close()
     if args.strata and args.exchange == "qdelta":  # one epoch of each shard alone: what an 8-GPU epoch waits on
         t = np.array([pl.time_blocks(nblk, LR, REG) for pl in plans]).sum(1)  # the shard's user blocks, summed
@@ -209,10 +234,8 @@ def run(args, say=log):
             finite = False
         pl.close()
     sh["finite"] = finite
-    out["sharded"] = sh
     print(json.dumps({"sharded": sh}), flush=True)
-    ctx.close()
-    return out
+    return sh
 
 
 if __name__ == "__main__":

@@ -334,11 +334,13 @@ def test_qdelta_one_wave_equals_host_model(ctx, ml100k, n_shards, merges):
         assert all(np.array_equal(got[0][x], y[x]) for x in range(4)) and got[0][4] == y[4]
 
 
-@pytest.mark.parametrize("n_shards,merges", [(2, 1), (4, 3)])
+@pytest.mark.parametrize("n_shards,merges", [(2, 1), (4, 3), (8, 4)])
 def test_qdelta_fp16_wire_tracks_int32(ctx, ml100k, n_shards, merges):
     """The default fp16 wire (rs_svd_plan_set_qdelta_wire 16): every shard ends with the same bits (each applies
     the same rounded moves), and the fit stays within 2e-3 of the exact int32-wire fit (fp16 keeps 11 bits of
-    each merge's move) with held-out RMSE within 1e-3 of it."""
+    each merge's move) with held-out RMSE within 1e-3 of it.  The in-process sum is the arithmetic of RCCL's ring
+    (qdelta_sum_kernel<16>): per chunk a rotated start rank, the ranks in ring order, rounded to fp16 after every
+    add -- 7 roundings per value at 8 shards, as an 8-GPU all-reduce makes them."""
     f = folds(*ml100k)[1]
     u, i, r, nu, ni = f.iu, f.ii, f.r, f.nu, f.ni
     k, lr, epochs = 32, 0.005, 5
@@ -368,6 +370,36 @@ def test_qdelta_fp16_wire_tracks_int32(ctx, ml100k, n_shards, merges):
             pl.close()
     assert _maxdiff(res[16][0][:4], res[32][0][:4]) <= 2e-3
     assert abs(res[16][1] - res[32][1]) <= 1e-3, (res[16][1], res[32][1])
+
+
+@pytest.mark.parametrize("mode", [rsgpu.EXCHANGE_QDELTA, rsgpu.EXCHANGE_ROTATE_Q, rsgpu.EXCHANGE_ROTATE])
+def test_replica_check_catches_a_diverged_shard(ctx, ml100k, mode):
+    """The consistency check after a sharded call (multi.hip check_replicas): one shard's replicated factors
+    changed by one word (test hook RS_FAULT_DIVERGE) make the call fail with RS_ERR_NUMERIC on the group; the
+    same call without the fault passes the check, and a later call on the same group is checked again."""
+    f = folds(*ml100k)[0]
+    u, i, r, nu, ni = f.iu[:20000], f.ii[:20000], f.r[:20000], f.nu, f.ni
+    k = 16
+    rng = np.random.default_rng(33)
+    P0, Q0 = rng.normal(0, 0.1, (nu, k)), rng.normal(0, 0.1, (ni, k))
+    if mode == rsgpu.EXCHANGE_ROTATE:
+        plans = _plans(ctx, _shards(u, i, r, nu, ni, 3), k, P0, Q0, 3, wg=0, waves=16, mode=mode)
+    else:
+        plans = []
+        for su, si, sr in _user_shards(u, i, r, nu, 3):
+            pl = ctx.svd_plan(rsgpu.Ratings(su, si, sr, nu, ni), k)
+            pl.set_exchange(mode)
+            pl.upload(P0, Q0, np.zeros(nu), np.zeros(ni), 3.5)
+            plans.append(pl)
+    g = rsgpu.SvdGroup(plans, n_blocks=3 if mode == rsgpu.EXCHANGE_ROTATE else 0)
+    g.epochs(1)  # clean: passes
+    plans[1].inject_fault(rsgpu.FAULT_DIVERGE)
+    with pytest.raises(rsgpu.RsError) as e:
+        g.epochs(1)
+    assert e.value.code == rsgpu.RS_ERR_NUMERIC and "disagree" in str(e.value)
+    g.close()
+    for pl in plans:
+        pl.close()
 
 
 def test_qdelta_edge_shards(ctx, ml100k):
