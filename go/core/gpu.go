@@ -38,15 +38,22 @@ import (
 
 // gpuCtx is one rs_ctx: one device and one HIP stream, not thread-safe.  CrossValidate (eval.go:28-35)
 // fits every fold's own estimator copy in its own goroutine, so each Fit opens its own ctx and closes it
-// before returning (`defer g.close()`): the ctx holds a HIP stream and pinned staging, which a finalizer
-// would keep alive until some later GC.  The library's entry points re-bind their device, so goroutine
-// migration between OS threads is harmless.
+// before returning (`defer g.close()`): the ctx holds a HIP stream and its pinned staging (owned by the ctx,
+// freed by rs_close), which a finalizer would keep alive until some later GC.
+//
+// Goroutine migration: Go may resume a goroutine on another OS thread between two cgo calls.  Every entry
+// point re-binds its ctx's device, and a ctx's error message lives in the ctx, so ctx calls are unaffected.
+// The ctx-less calls (rs_open, rs_svd_fit_multi) would leave theirs in the failing OS thread's slot, so they go
+// through the rs_report variants: the call itself writes its message (and rs_svd_fit_multi its refits) into a
+// report the caller owns -- a Go struct with no Go pointers, legal to pass (host/tests/core_test.cpp
+// TestCtxlessErrorAcrossThreads reads such a report on another thread).
 type gpuCtx struct{ p *C.rs_ctx }
 
 func openGPU(device int) *gpuCtx {
 	var p *C.rs_ctx
-	if rc := C.rs_open(C.int32_t(device), &p); rc != C.RS_OK {
-		panic(fmt.Sprintf("rs_open: %s", C.GoString(C.rs_last_error(nil))))
+	var rep C.rs_report
+	if rc := C.rs_open_r(C.int32_t(device), &p, &rep); rc != C.RS_OK {
+		panic(fmt.Sprintf("rs_open: %s", C.GoString(&rep.error[0])))
 	}
 	return &gpuCtx{p}
 }
@@ -161,10 +168,11 @@ func (s *SVD) fitGPU(trainData TrainSet) {
 		for k := range d {
 			d[k] = int32(k)
 		}
+		var rep C.rs_report
 		rc := C.rs_svd_fit_multi((*C.int32_t)(unsafe.Pointer(&d[0])), C.int32_t(len(d)), cr.r, &p, 0,
-			f64(pBuf), f64(qBuf), bu, bi, gb)
+			f64(pBuf), f64(qBuf), bu, bi, gb, &rep)
 		if rc != C.RS_OK {
-			panic(fmt.Sprintf("SVD.Fit (%d GPUs): %s", nGPUs, C.GoString(C.rs_last_error(nil))))
+			panic(fmt.Sprintf("SVD.Fit (%d GPUs, %d refits): %s", nGPUs, int(rep.refits), C.GoString(&rep.error[0])))
 		}
 		return
 	}

@@ -135,7 +135,19 @@ int32_t rs_version(void);
 int rs_device_count(int32_t* n);
 int rs_open(int32_t device, rs_ctx** out);
 void rs_close(rs_ctx* ctx);
+/* The message of the last failed call on ctx (per ctx), or with ctx == NULL of the last failed ctx-less call
+ * on the CALLING OS THREAD.  A host whose threads move between calls (Go: a goroutine may resume on another OS
+ * thread between two cgo calls) reads ctx-less errors from an rs_report instead (rs_open_r, rs_svd_fit_multi). */
 const char* rs_last_error(const rs_ctx* ctx);
+/* Per-call report of the ctx-less entry points: written by the call itself before it returns, so it needs no
+ * thread-local state.  error: the message of a failed call, NUL-terminated (truncated to fit), "" on success;
+ * refits: rs_svd_fit_multi's divergence refits (0..3). */
+typedef struct rs_report {
+    int32_t refits;
+    char error[508];
+} rs_report;
+/* rs_open with its error (if any) in *report (report may be NULL). */
+int rs_open_r(int32_t device, rs_ctx** out, rs_report* report);
 int rs_synchronize(rs_ctx* ctx);
 /* Device time (ms, HIP events on the ctx stream) of the kernels of the last estimator call on ctx
  * (rs_svd_fit, rs_svdpp_fit, rs_nmf_fit, rs_baseline_fit, rs_knn_sims): uploads, host packing and
@@ -544,12 +556,11 @@ int rs_item_shards(int64_t nnz, const int32_t* items, int32_t n_items, int32_t n
  * of 16 MiB or more the users are cut into ranges of near-equal ratings and the ranks' item moves are
  * all-reduced (RS_EXCHANGE_QDELTA, fp16 wire; n_blocks = merges per epoch, 0 = 16).  As rs_svd_fit otherwise (GlobalBias warm start, host buffers in / out; a fit
  * whose shards leave the fixed-point range, go non-finite or hold a factor past the guard bound is rebuilt and
- * redone from the inputs on half the workgroups and run cap 2, up to three times -- rs_fit_multi_refits counts
+ * redone from the inputs on half the workgroups and run cap 2, up to three times -- report->refits counts
  * them; RS_ERR_NUMERIC after every shard's values are written). */
 int rs_svd_fit_multi(const int32_t* devices, int32_t n_devices, const rs_ratings* r, const rs_sgd_params* p,
-                     int32_t n_blocks, double* P, double* Q, double* bu, double* bi, double* gb);
-/* Refits of the calling thread's last rs_svd_fit_multi (0, 1, 2 or 3). */
-int rs_fit_multi_refits(int32_t* n);
+                     int32_t n_blocks, double* P, double* Q, double* bu, double* bi, double* gb,
+                     rs_report* report /* may be NULL: the refits and the error message of this call */);
 /* ---- user-sharded multi-GPU (the dual partition, SURVEY §8e "measured alternative") ---------- *
  * Each rank builds a plan over its user range (local user ids) with ALL items; Q and b_i are
  * replicated, P and b_u are exclusive to the rank.  Per epoch: rs_svd_plan_epoch_qdelta runs the

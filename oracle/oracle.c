@@ -133,10 +133,18 @@ void or_svd_fit(int64_t n, const int32_t* u, const int32_t* i, const double* r, 
  * epoch's value, P/Q/bu/bi updated in place, works one after another; after the epoch
  * GB += sum_w n_w (gb_w - GB) / n (the fixed-order fold of sgd.hip / sgd_tile.hip).  Equal to the GPU
  * kernels when their works do not race (one wave, or works with disjoint users and items). */
-void or_svd_fit_works(int64_t n, const int32_t* u, const int32_t* i, const double* r, int64_t n_works,
-                      const int64_t* work_off, int32_t k, int32_t epochs, double lr, double reg, double* P,
-                      double* Q, double* bu, double* bi, double* gb) {
+/* The FAST schedules' GlobalBias: every work w runs svd.go:102-106's chain gb <- gb - lr (gb + e_j) from the
+ * epoch-start value GB on its own ratings, and the works are folded after the epoch.  compose = 0 (the
+ * multi-GPU exchanges): GB += sum_w n_w (g_w - GB) / n, the count-weighted mean of the works' moves.
+ * compose = 1 (the single-GPU tile schedule, round 6): the works' affine maps g -> a_w g + b_w, a_w = (1 - lr)^n_w,
+ * b_w = g_w - a_w GB, composed in work order -- GB' = A GB + sum_w c_w b_w with c_w the product of a_v over the
+ * works after w and A over all -- what the sequential chain gives when each work's e_j are its own (sgd.hip
+ * svd_epoch_epilogue_kernel evaluates the same sum). */
+void or_svd_fit_works2(int64_t n, const int32_t* u, const int32_t* i, const double* r, int64_t n_works,
+                       const int64_t* work_off, int32_t k, int32_t epochs, double lr, double reg, double* P,
+                       double* Q, double* bu, double* bi, double* gb, int32_t compose) {
     double GB = *gb;
+    double* gend = (double*)malloc((size_t)(n_works > 0 ? n_works : 1) * sizeof(double));
     for (int32_t epoch = 0; epoch < epochs; epoch++) {
         double fold = 0.0;
         for (int64_t w = 0; w < n_works; w++) {
@@ -158,10 +166,42 @@ void or_svd_fit_works(int64_t n, const int32_t* u, const int32_t* i, const doubl
                 for (int32_t f = 0; f < k; f++) qi[f] = qi[f] - (pu[f] * diff + qi[f] * reg) * lr;
             }
             fold += (double)(work_off[w + 1] - work_off[w]) * (g - GB);
+            gend[w] = g;
         }
-        if (n > 0) GB += fold / (double)n;
+        if (compose == 2) {
+            const double l1 = log1p(-lr);
+            double num = 0.0, den = 0.0, later = 0.0;
+            for (int64_t w = 0; w < n_works; w++) {
+                const double nw = (double)(work_off[w + 1] - work_off[w]);
+                const double a = exp(nw * l1);
+                num += gend[w] - a * GB;
+                den += 1.0 - a;
+                later += nw;
+            }
+            const double A = exp(later * l1);
+            if (den > 0.0) GB = A * GB + (1.0 - A) * (num / den);
+        } else if (compose) {
+            const double l1 = log1p(-lr);
+            double acc = 0.0, later = 0.0;  /* sum of c_w b_w; ratings of the works after w */
+            for (int64_t w = n_works - 1; w >= 0; w--) {
+                const double nw = (double)(work_off[w + 1] - work_off[w]);
+                const double b = gend[w] - exp(nw * l1) * GB;
+                acc += exp(later * l1) * b;
+                later += nw;
+            }
+            GB = exp(later * l1) * GB + acc;
+        } else if (n > 0) {
+            GB += fold / (double)n;
+        }
     }
+    free(gend);
     *gb = GB;
+}
+
+void or_svd_fit_works(int64_t n, const int32_t* u, const int32_t* i, const double* r, int64_t n_works,
+                      const int64_t* work_off, int32_t k, int32_t epochs, double lr, double reg, double* P,
+                      double* Q, double* bu, double* bi, double* gb) {
+    or_svd_fit_works2(n, u, i, r, n_works, work_off, k, epochs, lr, reg, P, Q, bu, bi, gb, 0);
 }
 
 void or_svd_predict(int64_t n, const int32_t* u, const int32_t* i, int32_t k, const double* P,

@@ -43,6 +43,12 @@ void or_svd_fit(int64_t n, const int32_t* u, const int32_t* i, const double* r,
 void or_svd_fit_works(int64_t n, const int32_t* u, const int32_t* i, const double* r, int64_t n_works,
                       const int64_t* work_off, int32_t k, int32_t epochs, double lr, double reg, double* P,
                       double* Q, double* bu, double* bi, double* gb);
+/* The same with the fold chosen: compose = 0 the count-weighted mean of the works' GlobalBias moves (the
+ * multi-GPU exchanges; or_svd_fit_works), 1 the works' affine chains composed in work order (the
+ * single-GPU tile schedule since round 6). */
+void or_svd_fit_works2(int64_t n, const int32_t* u, const int32_t* i, const double* r, int64_t n_works,
+                       const int64_t* work_off, int32_t k, int32_t epochs, double lr, double reg, double* P,
+                       double* Q, double* bu, double* bi, double* gb, int32_t compose);
 /* svd.go:32-51 SVD.Predict for inner ids (-1 = unknown, data.go:129 newID). */
 void or_svd_predict(int64_t n, const int32_t* u, const int32_t* i, int32_t k,
                     const double* P, const double* Q, const double* bu, const double* bi,

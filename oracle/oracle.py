@@ -70,6 +70,9 @@ def lib():
                                         C.c_double, _f64p, _f64p, _f64p, _f64p, _f64p, _dp]
         L.or_svd_fit_works.argtypes = [C.c_int64, _i32p, _i32p, _f64p, C.c_int64, _i64p, C.c_int32,
                                        C.c_int32, C.c_double, C.c_double, _f64p, _f64p, _f64p, _f64p, _dp]
+        L.or_svd_fit_works2.argtypes = [C.c_int64, _i32p, _i32p, _f64p, C.c_int64, _i64p, C.c_int32,
+                                        C.c_int32, C.c_double, C.c_double, _f64p, _f64p, _f64p, _f64p, _dp,
+                                        C.c_int32]
         L.or_svd_fit_chunked.argtypes = [C.c_int32, _i64p, _i32p, _f64p, C.c_int32, C.c_int32,
                                          C.c_int32, C.c_double, C.c_double, _f64p, _f64p, _f64p,
                                          _f64p, _dp]
@@ -157,16 +160,18 @@ def svd_fit(u, i, r, P, Q, bu=None, bi=None, gb=0.0, epochs=20, lr=0.005, reg=0.
     return P, Q, bu, bi, g.value
 
 
-def svd_fit_works(u, i, r, work_off, P, Q, bu=None, bi=None, gb=0.0, epochs=1, lr=0.005, reg=0.02):
+def svd_fit_works(u, i, r, work_off, P, Q, bu=None, bi=None, gb=0.0, epochs=1, lr=0.005, reg=0.02, compose=False):
     """The FAST schedules' own semantics: ratings (in this order) cut into works at work_off, each
-    with a work-local GlobalBias folded after the epoch (or_svd_fit_works)."""
+    with a work-local GlobalBias folded after the epoch (or_svd_fit_works2): compose=False the mean of the
+    works' moves (the multi-GPU exchanges), True their chains composed in work order (the single-GPU tile
+    schedule)."""
     P, Q = _f64(P).copy(), _f64(Q).copy()
     bu = np.zeros(P.shape[0]) if bu is None else _f64(bu).copy()
     bi = np.zeros(Q.shape[0]) if bi is None else _f64(bi).copy()
     g = C.c_double(gb)
     wo = _i64(work_off)
-    lib().or_svd_fit_works(len(r), _i32(u), _i32(i), _f64(r), len(wo) - 1, wo, P.shape[1], epochs, lr,
-                           reg, P, Q, bu, bi, C.byref(g))
+    lib().or_svd_fit_works2(len(r), _i32(u), _i32(i), _f64(r), len(wo) - 1, wo, P.shape[1], epochs, lr,
+                            reg, P, Q, bu, bi, C.byref(g), int(compose))
     return P, Q, bu, bi, g.value
 
 

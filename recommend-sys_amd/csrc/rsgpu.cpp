@@ -40,13 +40,8 @@ void build_csr(int64_t nnz, int32_t n_rows, const int32_t* rows, const int32_t* 
 }
 
 // The buffer is sized to the request rounded up to 1 MiB (callers cap requests at 256 MiB, sgd_tile.hip).
-void* pinned_staging(size_t bytes, int slot) {
-    struct Buf {
-        void* p = nullptr;
-        size_t n = 0;
-    };
-    thread_local Buf bufs[2];  // (never freed: the process may outlive the HIP runtime's teardown order)
-    Buf& b = bufs[slot & 1];
+void* pinned_staging(rs_ctx* ctx, size_t bytes, int slot) {
+    rs_ctx::Pinned& b = ctx->pinned[slot & 1];
     if (b.n < bytes) {
         if (b.p) (void)hipHostFree(b.p);
         b.p = nullptr;
@@ -56,6 +51,30 @@ void* pinned_staging(size_t bytes, int slot) {
         b.n = n;
     }
     return b.p;
+}
+
+void* pinned_small(rs_ctx* ctx, int slot) {
+    if (!ctx->pinned_small_p) RS_HIP(hipHostMalloc(&ctx->pinned_small_p, 256, hipHostMallocPortable));
+    return static_cast<char*>(ctx->pinned_small_p) + 64 * slot;
+}
+
+void release_pinned(rs_ctx* ctx) {  // (after the ctx stream is synchronised: no copy is in flight)
+    for (rs_ctx::Pinned& b : ctx->pinned) {
+        if (b.p) (void)hipHostFree(b.p);
+        b.p = nullptr;
+        b.n = 0;
+    }
+    if (ctx->pinned_small_p) (void)hipHostFree(ctx->pinned_small_p);
+    ctx->pinned_small_p = nullptr;
+}
+
+void fill_report(rs_report* rep, int status, int32_t refits) {
+    if (!rep) return;
+    rep->refits = refits;
+    const std::string& e = status == RS_OK ? std::string() : tls_error();
+    const size_t n = std::min(e.size(), sizeof(rep->error) - 1);
+    std::memcpy(rep->error, e.data(), n);
+    rep->error[n] = '\0';
 }
 
 // mean(r - b_u - b_i) over fixed 2^16-rating chunks summed in order (independent of the thread count)
@@ -166,7 +185,14 @@ extern "C" void rs_close(rs_ctx* ctx) {
     if (ctx->k1) (void)hipEventDestroy(ctx->k1);
     ctx->svd_fit_cache.reset();  // a cached plan frees its device buffers on this device
     ctx->staging.reset();
+    rs::release_pinned(ctx);
     delete ctx;
+}
+
+extern "C" int rs_open_r(int32_t device, rs_ctx** out, rs_report* report) {
+    const int st = rs_open(device, out);  // (its ctx-less error is this thread's: copied before returning)
+    rs::fill_report(report, st, 0);
+    return st;
 }
 
 extern "C" const char* rs_last_error(const rs_ctx* ctx) {

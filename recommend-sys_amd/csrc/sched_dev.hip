@@ -268,10 +268,6 @@ struct Carve {
     }
 };
 
-struct Pinned4 {  // small pinned readback slot (per thread, kept)
-    int32_t* p = nullptr;
-    Pinned4() { RS_HIP(hipHostMalloc(reinterpret_cast<void**>(&p), 8 * sizeof(int32_t), hipHostMallocPortable)); }
-};
 
 }  // namespace
 
@@ -294,8 +290,7 @@ bool tile_build_device(rs_svd_plan* pl) {
     const int32_t grid0 = tile_grid0(pl);  // (the host build's own function: the two builds agree)
     const int32_t ld = tile_lds_row(pl);
     const int64_t rec_cap = static_cast<int64_t>((kTileLdsBudget - 16 - static_cast<size_t>(ld) * 4) / 16);
-    thread_local Pinned4 rb;
-    int32_t* h = rb.p;
+    int32_t* h = static_cast<int32_t*>(pinned_small(pl->ctx, kPinSched));  // 8 ints of readback
 
     // workspace (sizes bounded by n, the users and the items; the tiles are at most the active users)
     auto carve = [&](Carve& c) {

@@ -1334,7 +1334,7 @@ static void plan_build_coo_device(rs_ctx* ctx, const rs_ratings* r, int32_t k, r
     pl->nnz = r->nnz;
     pl->tile_rule = RS_TILE_RULE_FILL_DEVICE;
     const size_t n = static_cast<size_t>(r->nnz);
-    char* st = static_cast<char*>(pinned_staging(12 * n));
+    char* st = static_cast<char*>(pinned_staging(ctx, 12 * n));
     int32_t* su = reinterpret_cast<int32_t*>(st);
     int32_t* si = su + n;
     float* sv = reinterpret_cast<float*>(si + n);
@@ -1428,21 +1428,15 @@ static void plan_recycle(rs_svd_plan* pl, rs_svd_plan* old, int32_t n_users, int
 // plan_download path (pageable) is taken instead.
 constexpr size_t kFitStageMax = size_t{256} << 20;
 // pinned scalars of rs_svd_fit's copies (a copy to or from pageable memory waits for the stream's earlier work,
-// which would serialise the host work meant to run under the epochs)
-struct FitScalars {
-    double* p = nullptr;  // [0] GlobalBias in, [1] GlobalBias out, [2] flag out (int32)
-    FitScalars() { RS_HIP(hipHostMalloc(reinterpret_cast<void**>(&p), 32, hipHostMallocPortable)); }
-};
-static FitScalars& fit_scalars() {
-    thread_local FitScalars f;
-    return f;
-}
+// which would serialise the host work meant to run under the epochs): [0] GlobalBias in, [1] GlobalBias out,
+// [2] flag out (int32) -- the ctx's kPinFit slot
+static double* fit_scalars(rs_ctx* ctx) { return static_cast<double*>(pinned_small(ctx, kPinFit)); }
 
 // host half: the rows packed into staging slot 1 (false: too large, nothing done)
 static bool plan_pack_fit(rs_svd_plan* pl, const double* P, const double* Q, const double* bu, const double* bi) {
     const size_t pn = static_cast<size_t>(std::max(1, pl->n_users)) * pl->ld, qn = static_cast<size_t>(std::max(1, pl->n_items)) * pl->ld;
     if ((pn + qn) * 4 > kFitStageMax) return false;
-    float* st = static_cast<float*>(pinned_staging((pn + qn) * 4, 1));
+    float* st = static_cast<float*>(pinned_staging(pl->ctx, (pn + qn) * 4, 1));
     const int32_t k = pl->k, ld = pl->ld;
     const int64_t nu = pl->n_users, ni = pl->n_items;
     parallel_ranges(nu + ni, 16, [&](int64_t r0, int64_t r1) {  // P rows then Q rows, one pass
@@ -1464,11 +1458,11 @@ static void plan_dma_fit(rs_svd_plan* pl, const double* gb) {
     const size_t pn = static_cast<size_t>(std::max(1, pl->n_users)) * pl->ld, qn = static_cast<size_t>(std::max(1, pl->n_items)) * pl->ld;
     plan_sync_last(pl);
     hipStream_t s = pl->ctx->stream;
-    float* st = static_cast<float*>(pinned_staging((pn + qn) * 4, 1));
+    float* st = static_cast<float*>(pinned_staging(pl->ctx, (pn + qn) * 4, 1));
     pl->P.upload(st, static_cast<size_t>(pl->n_users) * pl->ld, s);
     pl->Q.upload(st + pn, static_cast<size_t>(pl->n_items) * pl->ld, s);
     sync_item_copies(pl, s, 1);
-    double* sc = fit_scalars().p;
+    double* sc = fit_scalars(pl->ctx);
     sc[0] = *gb;
     pl->gb.upload(sc, 1, s);
     reset_loss(pl, s);
@@ -1491,8 +1485,8 @@ static bool fit_fits_staging(const rs_svd_plan* pl) {
 static void plan_fetch_enqueue(rs_svd_plan* pl) {
     const size_t pn = static_cast<size_t>(std::max(1, pl->n_users)) * pl->ld, qn = static_cast<size_t>(std::max(1, pl->n_items)) * pl->ld;
     hipStream_t s = pl->ctx->stream;
-    float* st = static_cast<float*>(pinned_staging((pn + qn) * 4, 1));
-    double* sc = fit_scalars().p;
+    float* st = static_cast<float*>(pinned_staging(pl->ctx, (pn + qn) * 4, 1));
+    double* sc = fit_scalars(pl->ctx);
     pl->P.download(st, static_cast<size_t>(pl->n_users) * pl->ld, s);
     pl->Q.download(st + pn, static_cast<size_t>(pl->n_items) * pl->ld, s);
     pl->gb.download(sc + 1, 1, s);
@@ -1500,8 +1494,8 @@ static void plan_fetch_enqueue(rs_svd_plan* pl) {
     *f = 0;
     if (pl->numflag.p) RS_HIP(hipMemcpyAsync(f, pl->numflag.p, sizeof(int32_t), hipMemcpyDeviceToHost, s));
 }
-static void plan_fetch_result(double* gb, int32_t* flag) {
-    const double* sc = fit_scalars().p;
+static void plan_fetch_result(rs_ctx* ctx, double* gb, int32_t* flag) {
+    const double* sc = fit_scalars(ctx);
     *gb = sc[1];
     *flag = *reinterpret_cast<const int32_t*>(sc + 2);
 }
@@ -1515,7 +1509,7 @@ static void plan_clear_flag(rs_svd_plan* pl) {
 // after plan_fetch_enqueue and a wait: the f64 rows; a raised flag is cleared and reported (values already written)
 static void plan_finish_fit(rs_svd_plan* pl, double* P, double* Q, double* bu, double* bi, int32_t flag) {
     const size_t pn = static_cast<size_t>(std::max(1, pl->n_users)) * pl->ld;
-    const float* st = static_cast<const float*>(pinned_staging(0, 1));
+    const float* st = static_cast<const float*>(pinned_staging(pl->ctx, 0, 1));
     const int32_t k = pl->k, ld = pl->ld;
     const int64_t nu = pl->n_users, ni = pl->n_items;
     parallel_ranges(nu + ni, 16, [&](int64_t r0, int64_t r1) {  // P rows then Q rows, one pass
@@ -1800,11 +1794,9 @@ static void plan_epochs(rs_svd_plan* pl, int32_t epochs, float lr, float reg, hi
     RS_HIP(hipMemcpyAsync(pl->Q_snap.p, pl->Q.p, pl->Q.n * sizeof(float), hipMemcpyDeviceToDevice, s));
     RS_HIP(hipMemcpyAsync(pl->gb_snap.p, pl->gb.p, sizeof(double), hipMemcpyDeviceToDevice, s));
     RS_HIP(hipMemcpyAsync(pl->gb_snap.p + 1, pl->loss_state.p, sizeof(double), hipMemcpyDeviceToDevice, s));
-    struct Check {  // pinned readback slot, per thread
-        int64_t* p = nullptr;
-        Check() { RS_HIP(hipHostMalloc(reinterpret_cast<void**>(&p), 16, hipHostMallocPortable)); }
-    };
-    thread_local Check ck;
+    struct Check {  // pinned readback slot: the ctx's kPinGuard
+        int64_t* p;
+    } ck{static_cast<int64_t*>(pinned_small(pl->ctx, kPinGuard))};
     int32_t* flag = numflag(pl);
     bool hard = false;  // a hard signal (the fixed-point range flag, a non-finite GlobalBias) in this call
     const int32_t wg0 = pl->tile_wg, cap0 = pl->tile_run_cap;
@@ -2548,7 +2540,7 @@ extern "C" int rs_svd_fit(rs_ctx* ctx, const rs_ratings* r, const rs_sgd_params*
             }
             if (staged) {
                 RS_HIP(hipStreamSynchronize(ctx->stream));
-                rs::plan_fetch_result(gb, &flag);
+                rs::plan_fetch_result(ctx, gb, &flag);
                 rs::plan_finish_fit(&pl, P, Q, bu, bi, flag);
             } else {
                 rs::plan_download(&pl, P, Q, bu, bi, gb);

@@ -1188,10 +1188,10 @@ void tile_build(rs_svd_plan* pl) {
         void* dst[5] = {pl->t_tiles.p, pl->t_users.p, pl->t_streams.p, pl->t_runs.p, pl->t_recs.p};
         size_t off[6] = {0};
         for (int a = 0; a < 5; ++a) off[a + 1] = off[a] + (sz[a] + 255) / 256 * 256;
-        // (the staging buffer lives as long as the thread: schedules past kMaxPinnedStage, e.g. configs[4]'s
-        // 1-GB shard schedule, upload from pageable memory instead of pinning that much for good)
+        // (the staging buffer lives as long as the ctx: schedules past kMaxPinnedStage, e.g. configs[4]'s
+        // 1-GB shard schedule, upload from pageable memory instead of pinning that much for the ctx's life)
         constexpr size_t kMaxPinnedStage = size_t{256} << 20;
-        char* stage = off[5] <= kMaxPinnedStage ? static_cast<char*>(pinned_staging(off[5])) : nullptr;
+        char* stage = off[5] <= kMaxPinnedStage ? static_cast<char*>(pinned_staging(pl->ctx, off[5])) : nullptr;
         for (int a = 0; a < 5 && !stage; ++a)
             if (sz[a]) RS_HIP(hipMemcpyAsync(dst[a], src[a], sz[a], hipMemcpyHostToDevice, s));
         for (int a = 0; a < 5 && stage; ++a) {

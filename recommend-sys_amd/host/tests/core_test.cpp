@@ -19,6 +19,7 @@
 #include <numeric>
 #include <set>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "core.hpp"
@@ -134,6 +135,36 @@ int main(int argc, char** argv) {
         t.Items = {0, 0, 0};
         t.Ratings = {0, 0, 0};
         CHECK(std::fabs(RMSE(e, t) - 1.63299) < 1e-5 && std::fabs(MAE(e, t) - 1.33333) < 1e-5);
+    });
+    // The Go boundary's ctx-less errors: a goroutine may resume on another OS thread between
+    // the failing cgo call and the call that fetches its message, and rs_last_error(NULL) is per OS thread.
+    // rs_report carries the message out of the call itself.  Thread A fails rs_open_r (device 2^20: out of
+    // range on a GPU box, no device here) and rs_svd_fit_multi (no devices); thread B reads both reports.
+    run("TestCtxlessErrorAcrossThreads", [] {
+        rs_report open_rep{}, multi_rep{};
+        std::string a_open, a_multi, b_tls;
+        int rc_open = 0, rc_multi = 0;
+        std::thread a([&] {
+            rs_ctx* c = nullptr;
+            rc_open = rs_open_r(1 << 20, &c, &open_rep);
+            a_open = rs_last_error(nullptr);
+            rs_sgd_params p{8, 1, 0.005, 0.02, RS_SGD_FAST, RS_SGD_WB_TILE};
+            rs_ratings r{0, 1, 1, nullptr, nullptr, nullptr};
+            double x = 0;
+            rc_multi = rs_svd_fit_multi(nullptr, 0, &r, &p, 0, &x, &x, &x, &x, &x, &multi_rep);
+            a_multi = rs_last_error(nullptr);
+        });
+        a.join();
+        std::string b_open, b_multi;
+        std::thread b([&] {
+            b_tls = rs_last_error(nullptr);  // thread B has no error of its own
+            b_open = open_rep.error;
+            b_multi = multi_rep.error;
+        });
+        b.join();
+        CHECK(rc_open != RS_OK && !a_open.empty() && b_open == a_open);
+        CHECK(rc_multi == RS_ERR_INVALID && a_multi == "bad arguments" && b_multi == a_multi && multi_rep.refits == 0);
+        CHECK(b_tls.empty());
     });
     if (cpu_only) {
         std::printf("%d/%d passed\n", g_run - g_failed, g_run);

@@ -7,6 +7,7 @@ from __future__ import annotations
 
 import ctypes as C
 import os
+import threading
 import weakref
 
 import numpy as np
@@ -50,7 +51,7 @@ HEADER_SYMBOLS = (
     "rs_item_shards", "rs_svd_fit_multi", "rs_tile_schedule_host", "rs_svd_plan_set_exchange", "rs_svd_plan_set_qdelta_wire", "rs_svd_plan_set_qdelta_split",
     "rs_svd_plan_set_qdelta_curvature",
     "rs_comm_info", "rs_rotation_step", "rs_svd_plan_shard_info", "rs_svd_plan_qdelta_info", "rs_svd_plan_inject_fault",
-    "rs_svd_plan_time_blocks", "rs_knn_plan_set_tie_order", "rs_fit_refits", "rs_fit_multi_refits",
+    "rs_svd_plan_time_blocks", "rs_knn_plan_set_tie_order", "rs_fit_refits", "rs_open_r",
     "rs_svd_plan_set_hot_split",
 )
 COMM_ID_BYTES = 128
@@ -65,6 +66,10 @@ class RsError(RuntimeError):
 class _Ratings(C.Structure):
     _fields_ = [("nnz", C.c_int64), ("n_users", C.c_int32), ("n_items", C.c_int32),
                 ("users", C.c_void_p), ("items", C.c_void_p), ("ratings", C.c_void_p)]
+
+
+class _Report(C.Structure):  # rs_report
+    _fields_ = [("refits", C.c_int32), ("error", C.c_char * 508)]
 
 
 class _SgdParams(C.Structure):
@@ -174,7 +179,7 @@ def lib():
             "rs_tile_schedule_host": (C.c_int, [_i32, _i32, _vp, _vp, _vp, _i32, _i32, _i32, _i32, _i32, _vp,
                                                 _vp, _vp, C.POINTER(_i32), C.POINTER(_dbl)]),
             "rs_svd_fit_multi": (C.c_int, [_vp, _i32, C.POINTER(_Ratings), C.POINTER(_SgdParams), _i32,
-                                           _vp, _vp, _vp, _vp, _vp]),
+                                           _vp, _vp, _vp, _vp, _vp, C.POINTER(_Report)]),
             "rs_svd_plan_set_exchange": (C.c_int, [_vp, _i32]),
             "rs_svd_plan_set_qdelta_wire": (C.c_int, [_vp, _i32]),
             "rs_svd_plan_set_qdelta_split": (C.c_int, [_vp, C.c_double, _i32]),
@@ -183,7 +188,7 @@ def lib():
             "rs_svd_plan_time_blocks": (C.c_int, [_vp, _flt, _flt, _vp, _i32]),
             "rs_knn_plan_set_tie_order": (C.c_int, [_vp, _i32]),
             "rs_fit_refits": (C.c_int, [_vp, C.POINTER(_i32)]),
-            "rs_fit_multi_refits": (C.c_int, [C.POINTER(_i32)]),
+            "rs_open_r": (C.c_int, [_i32, C.POINTER(_vp), C.POINTER(_Report)]),
             "rs_svd_plan_set_hot_split": (C.c_int, [_vp, _dbl, _i64, _i32]),
             "rs_comm_info": (C.c_int, [C.POINTER(_i32), _vp, _i32]),
             "rs_rotation_step": (C.c_int, [_i32, _i32, _i32, _vp]),
@@ -802,16 +807,21 @@ def svd_fit_multi(devices, r: "Ratings", P, Q, bu=None, bi=None, gb=0.0, n_epoch
     dev = np.ascontiguousarray(devices, np.int32)
     prm = _SgdParams(P.shape[1], n_epochs, lr, reg, SGD_FAST, WB_TILE)
     rc = r.c()
-    _check(lib().rs_svd_fit_multi(_ptr(dev), len(dev), C.byref(rc), C.byref(prm), n_blocks, _ptr(P), _ptr(Q),
-                                  _ptr(bu), _ptr(bi), _ptr(g)))
+    rep = _Report()
+    code = lib().rs_svd_fit_multi(_ptr(dev), len(dev), C.byref(rc), C.byref(prm), n_blocks, _ptr(P), _ptr(Q),
+                                  _ptr(bu), _ptr(bi), _ptr(g), C.byref(rep))
+    _last_multi.refits = rep.refits
+    if code != RS_OK:
+        raise RsError(code, rep.error.decode(errors="replace"))
     return P, Q, bu, bi, float(g[0])
 
 
+_last_multi = threading.local()
+
+
 def fit_multi_refits():
-    """Refits of this thread's last svd_fit_multi (rs_fit_multi_refits)."""
-    n = _i32(0)
-    _check(lib().rs_fit_multi_refits(C.byref(n)))
-    return n.value
+    """Refits of this thread's last svd_fit_multi (its rs_report's refits)."""
+    return getattr(_last_multi, "refits", 0)
 
 
 def svd_predict(users, items, P, Q, bu, bi, gb):

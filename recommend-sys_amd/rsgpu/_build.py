@@ -108,7 +108,7 @@ def build_host(verbose: bool = False) -> str:
     librsgpu.so, and its test binary host/tests/core_test.  rpath $ORIGIN-relative, so both run
     from the snapshot on the GPU box."""
     lib = build(verbose)
-    flags = ["-O2", "-std=c++17", "-fPIC", "-Wall", "-Wextra", f"-I{INCLUDE}", f"-I{HOST}"]
+    flags = ["-O2", "-std=c++17", "-fPIC", "-pthread", "-Wall", "-Wextra", f"-I{INCLUDE}", f"-I{HOST}"]
     steps = [
         ([os.path.join(HOST, "core.cpp")], HOST_LIB,
          ["-shared", f"-L{PKG_DIR}", "-lrsgpu", "-Wl,-rpath,$ORIGIN/../rsgpu"]),

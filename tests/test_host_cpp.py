@@ -31,7 +31,7 @@ def _run(args, timeout):
 
 def test_host_mirror_cpu(udata):
     out = _run(["--cpu-only", udata], 120)
-    assert "6/6 passed" in out, out
+    assert "7/7 passed" in out, out
 
 
 @pytest.mark.gpu
