@@ -482,6 +482,17 @@ int rs_svd_plan_set_qdelta_split(rs_svd_plan* plan, double hot_ratings, int32_t 
  * unit curvature above, the default; 0: w_i = 1, the plain sum of the moves).  Set before the join, the same on
  * every rank. */
 int rs_svd_plan_set_qdelta_curvature(rs_svd_plan* plan, double gamma);
+/* Test hook: the tile schedule's hot-run damping with the runs in flight of an item taken
+ * as R = its ratings x kconc (kconc > 0 forces the damped kernel; 0 restores the library's rule, R = ratings x
+ * workgroups x waves / nnz, damped where the hottest item reaches 40).  With one wave the runs never overlap, so
+ * the damped kernel is checked against the oracle's restatement (or_svd_fit_works_damped). */
+int rs_svd_plan_set_damp_concurrency(rs_svd_plan* plan, float kconc);
+/* Cold runs of the tile schedule (round 6): an item with so few ratings that on average fewer than
+ * `runs_in_flight` of its runs are in flight at once (ratings x workgroups x waves / nnz) ends each run with plain
+ * write-through stores of its new row instead of memory-side atomic adds -- a concurrent run of the same item
+ * then loses its update, which happens with about that probability.  0 turns it off.  With one wave per
+ * workgroup a store equals the atomic (no run overlaps).  Rebuilds the schedule. */
+int rs_svd_plan_set_cold_store(rs_svd_plan* plan, double runs_in_flight);
 /* RS_EXCHANGE_ROTATE_Q on Zipf-headed sets: a stratum (one rank's users x one item block) holds an item's
  * ratings n_blocks-fold concentrated, so the head's rows get many concurrent runs in flight (Hogwild staleness
  * that diverges at lr 0.005; configs[4]: the hottest item is 0.8 % of the set but 12.7 % of its stratum).  An

@@ -204,6 +204,83 @@ void or_svd_fit_works(int64_t n, const int32_t* u, const int32_t* i, const doubl
     or_svd_fit_works2(n, u, i, r, n_works, work_off, k, epochs, lr, reg, P, Q, bu, bi, gb, 0);
 }
 
+/* The tile schedule's hot-run damping (round 5, sgd_tile.hip; a rule of this build, not of svd.go) on top of
+ * or_svd_fit_works2: a run is a maximal stretch of one item's ratings inside a work (the kernel's (item, tile)
+ * run when runs are not cut).  The run trains as svd.go:93-128 does; at its end, where the item's runs in flight
+ * R = deg[item] x kconc reach 4, its closing fractions f_q = 1 - exp(-lr (sum |p_u|^2 + n reg)) (|p_u|^2 over the
+ * factor columns, before each rating's update) and f_b = 1 - (1 - lr (1 + reg))^n give weights
+ * w = min(1, 1 / (R f)), and the item row keeps only w of the run's move: q = q0 + w_q (q - q0),
+ * b_i = b0 + w_b (b_i - b0).  P, b_u and GlobalBias are not damped. */
+void or_svd_fit_works_damped(int64_t n, const int32_t* u, const int32_t* i, const double* r, int64_t n_works,
+                             const int64_t* work_off, const int32_t* deg, double kconc, int32_t k, int32_t epochs,
+                             double lr, double reg, double* P, double* Q, double* bu, double* bi, double* gb,
+                             int32_t compose) {
+    double GB = *gb;
+    double* gend = (double*)malloc((size_t)(n_works > 0 ? n_works : 1) * sizeof(double));
+    double* q0 = (double*)malloc((size_t)(k > 0 ? k : 1) * sizeof(double));
+    const double l1 = log1p(-lr);
+    for (int32_t epoch = 0; epoch < epochs; epoch++) {
+        double fold = 0.0;
+        for (int64_t w = 0; w < n_works; w++) {
+            double g = GB, hp = 0.0, b0 = 0.0;
+            int64_t nrun = 0;
+            for (int64_t t = work_off[w]; t < work_off[w + 1]; t++) {
+                const int32_t uu = u[t], ii = i[t];
+                double* pu = P + (int64_t)uu * k;
+                double* qi = Q + (int64_t)ii * k;
+                if (t == work_off[w] || i[t - 1] != ii) {  /* a run starts */
+                    memcpy(q0, qi, (size_t)k * sizeof(double));
+                    b0 = bi[ii];
+                    hp = 0.0;
+                    nrun = 0;
+                }
+                const double userBias = bu[uu], itemBias = bi[ii];
+                double pred = g;
+                pred += bu[uu];
+                pred += bi[ii];
+                pred += dot(pu, qi, k);
+                const double diff = pred - r[t];
+                hp += dot(pu, pu, k);
+                nrun++;
+                g -= lr * diff;
+                bu[uu] -= lr * (diff + reg * userBias);
+                bi[ii] -= lr * (diff + reg * itemBias);
+                for (int32_t f = 0; f < k; f++) pu[f] = pu[f] - (qi[f] * diff + pu[f] * reg) * lr;
+                for (int32_t f = 0; f < k; f++) qi[f] = qi[f] - (pu[f] * diff + qi[f] * reg) * lr;
+                if (t + 1 == work_off[w + 1] || i[t + 1] != ii) {  /* the run ends: its move, damped */
+                    const double R = (double)deg[ii] * kconc;
+                    if (R >= 4.0) {
+                        const double fq = 1.0 - exp(-lr * (hp + (double)nrun * reg));
+                        const double fb = 1.0 - exp((double)nrun * log(1.0 - lr * (1.0 + reg)));
+                        const double wq = fmin(1.0, 1.0 / (R * fq)), wb = fmin(1.0, 1.0 / (R * fb));
+                        for (int32_t f = 0; f < k; f++) qi[f] = q0[f] + wq * (qi[f] - q0[f]);
+                        bi[ii] = b0 + wb * (bi[ii] - b0);
+                    }
+                }
+            }
+            fold += (double)(work_off[w + 1] - work_off[w]) * (g - GB);
+            gend[w] = g;
+        }
+        if (compose == 2) {
+            double num = 0.0, den = 0.0, later = 0.0;
+            for (int64_t w = 0; w < n_works; w++) {
+                const double nw = (double)(work_off[w + 1] - work_off[w]);
+                const double a = exp(nw * l1);
+                num += gend[w] - a * GB;
+                den += 1.0 - a;
+                later += nw;
+            }
+            const double A = exp(later * l1);
+            if (den > 0.0) GB = A * GB + (1.0 - A) * (num / den);
+        } else if (n > 0) {
+            GB += fold / (double)n;
+        }
+    }
+    free(q0);
+    free(gend);
+    *gb = GB;
+}
+
 void or_svd_predict(int64_t n, const int32_t* u, const int32_t* i, int32_t k, const double* P,
                     const double* Q, const double* bu, const double* bi, double gb, double* out) {
     for (int64_t t = 0; t < n; t++) {

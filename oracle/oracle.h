@@ -49,6 +49,11 @@ void or_svd_fit_works(int64_t n, const int32_t* u, const int32_t* i, const doubl
 void or_svd_fit_works2(int64_t n, const int32_t* u, const int32_t* i, const double* r, int64_t n_works,
                        const int64_t* work_off, int32_t k, int32_t epochs, double lr, double reg, double* P,
                        double* Q, double* bu, double* bi, double* gb, int32_t compose);
+/* or_svd_fit_works2 (compose 0 or 2) with the tile schedule's hot-run damping (oracle.c). */
+void or_svd_fit_works_damped(int64_t n, const int32_t* u, const int32_t* i, const double* r, int64_t n_works,
+                             const int64_t* work_off, const int32_t* deg, double kconc, int32_t k, int32_t epochs,
+                             double lr, double reg, double* P, double* Q, double* bu, double* bi, double* gb,
+                             int32_t compose);
 /* svd.go:32-51 SVD.Predict for inner ids (-1 = unknown, data.go:129 newID). */
 void or_svd_predict(int64_t n, const int32_t* u, const int32_t* i, int32_t k,
                     const double* P, const double* Q, const double* bu, const double* bi,

@@ -70,6 +70,9 @@ def lib():
                                         C.c_double, _f64p, _f64p, _f64p, _f64p, _f64p, _dp]
         L.or_svd_fit_works.argtypes = [C.c_int64, _i32p, _i32p, _f64p, C.c_int64, _i64p, C.c_int32,
                                        C.c_int32, C.c_double, C.c_double, _f64p, _f64p, _f64p, _f64p, _dp]
+        L.or_svd_fit_works_damped.argtypes = [C.c_int64, _i32p, _i32p, _f64p, C.c_int64, _i64p, _i32p, C.c_double,
+                                              C.c_int32, C.c_int32, C.c_double, C.c_double, _f64p, _f64p, _f64p,
+                                              _f64p, _dp, C.c_int32]
         L.or_svd_fit_works2.argtypes = [C.c_int64, _i32p, _i32p, _f64p, C.c_int64, _i64p, C.c_int32,
                                         C.c_int32, C.c_double, C.c_double, _f64p, _f64p, _f64p, _f64p, _dp,
                                         C.c_int32]
@@ -172,6 +175,20 @@ def svd_fit_works(u, i, r, work_off, P, Q, bu=None, bi=None, gb=0.0, epochs=1, l
     wo = _i64(work_off)
     lib().or_svd_fit_works2(len(r), _i32(u), _i32(i), _f64(r), len(wo) - 1, wo, P.shape[1], epochs, lr,
                             reg, P, Q, bu, bi, C.byref(g), int(compose))
+    return P, Q, bu, bi, g.value
+
+
+def svd_fit_works_damped(u, i, r, work_off, deg, kconc, P, Q, bu=None, bi=None, gb=0.0, epochs=1, lr=0.005,
+                         reg=0.02, compose=2):
+    """svd_fit_works with the tile schedule's hot-run damping (or_svd_fit_works_damped): runs of an item with
+    deg[item] x kconc >= 4 runs in flight keep min(1, 1 / (R f)) of their move."""
+    P, Q = _f64(P).copy(), _f64(Q).copy()
+    bu = np.zeros(P.shape[0]) if bu is None else _f64(bu).copy()
+    bi = np.zeros(Q.shape[0]) if bi is None else _f64(bi).copy()
+    g = C.c_double(gb)
+    wo = _i64(work_off)
+    lib().or_svd_fit_works_damped(len(r), _i32(u), _i32(i), _f64(r), len(wo) - 1, wo, _i32(deg), float(kconc),
+                                  P.shape[1], epochs, lr, reg, P, Q, bu, bi, C.byref(g), int(compose))
     return P, Q, bu, bi, g.value
 
 

@@ -54,6 +54,7 @@
 #include <cmath>
 #include <atomic>
 #include <condition_variable>
+#include <cstdio>
 #include <cstdlib>
 #include <cstring>
 #include <exception>
@@ -752,13 +753,11 @@ void epochs_average(rs_svd_plan* pl, int32_t n_epochs, float lr, float reg, hipS
             if (c.nccl) {
                 RS_HIP(hipEventRecord(c.ev_done[b], s));
                 RS_HIP(hipStreamWaitEvent(c.cs, c.ev_done[b], 0));
-                check_nccl(ncclGroupStart(), "ncclGroupStart");
-                if (n > 0)
+                if (n > 0)  // (two plain collectives: see epochs_qdelta)
                     check_nccl(ncclAllReduce(c.dP.p + off, c.dP.p + off, static_cast<size_t>(n), ncclFloat32, ncclSum,
                                              c.nccl, c.cs), "ncclAllReduce(dP)");
                 check_nccl(ncclAllReduce(c.gbs.p + b, c.gbs.p + b, 1, ncclFloat64, ncclSum, c.nccl, c.cs),
                            "ncclAllReduce(GlobalBias)");
-                check_nccl(ncclGroupEnd(), "ncclGroupEnd");
                 if (n > 0)
                     hipLaunchKernelGGL(apply_rows_kernel, dim3(grid_for(n)), dim3(256), 0, c.cs, pl->P.p + static_cast<int64_t>(u0) * pl->ld,
                                        c.dP.p + off, n, pl->ld, c.ldd, pl->k);
@@ -1111,14 +1110,17 @@ void epochs_qdelta(rs_svd_plan* pl, int32_t n_epochs, float lr, float reg, hipSt
         if (c.nccl) {  // merge m's all-reduce on the comm stream, behind block m + 1's kernel
             RS_HIP(hipEventRecord(c.ev_gb, s));
             RS_HIP(hipStreamWaitEvent(c.cs, c.ev_gb, 0));
-            check_nccl(ncclGroupStart(), "ncclGroupStart");
+            // two plain collectives, not one group: a group of the two all-reduces never completed between two ranks of
+            // RCCL's network transport (tests/rccl_ranks.py), where each alone does (and costs one more launch per merge)
             if (mq > 0)
                 check_nccl(ncclAllReduce(out, sum_out, static_cast<size_t>(mq), h16 ? ncclFloat16 : ncclInt32, ncclSum, c.nccl,
                                          c.cs), "ncclAllReduce(item moves)");
             check_nccl(ncclAllReduce(c.gbs.p + par, c.gbs.p + par, 1, ncclFloat64, ncclSum, c.nccl, c.cs),
                        "ncclAllReduce(GlobalBias)");
-            check_nccl(ncclGroupEnd(), "ncclGroupEnd");
             RS_HIP(hipEventRecord(c.ev_ar[par], c.cs));
+            static const int dbg_sync = std::getenv("RSGPU_QDELTA_SYNC") ? std::atoi(std::getenv("RSGPU_QDELTA_SYNC")) : 0;
+            if (dbg_sync & 1) RS_HIP(hipStreamSynchronize(c.cs));  // (diagnostic: no overlap)
+            if (dbg_sync & 2) std::fprintf(stderr, "qdelta rank %d merge %d enqueued\n", c.rank, m);
         } else {  // in-process: the sum now (no overlap), applied on the same deferred schedule
             LocalGroup& lg = *c.local;
             RS_HIP(hipStreamSynchronize(s));
@@ -1221,10 +1223,8 @@ void check_replicas(rs_svd_plan* pl, hipStream_t s) {
     if (c.nccl) {
         RS_HIP(hipEventRecord(c.ev_gb, s));
         RS_HIP(hipStreamWaitEvent(c.cs, c.ev_gb, 0));
-        check_nccl(ncclGroupStart(), "ncclGroupStart");
         check_nccl(ncclAllReduce(sums, sums + 6, 6, ncclUint64, ncclMax, c.nccl, c.cs), "ncclAllReduce(replica max)");
         check_nccl(ncclAllReduce(sums, sums + 12, 6, ncclUint64, ncclMin, c.nccl, c.cs), "ncclAllReduce(replica min)");
-        check_nccl(ncclGroupEnd(), "ncclGroupEnd");
         RS_HIP(hipMemcpyAsync(h, sums, sizeof(h), hipMemcpyDeviceToHost, c.cs));
         RS_HIP(hipStreamSynchronize(c.cs));
         for (int x = 0; x < 6; ++x)
@@ -1244,14 +1244,17 @@ void check_replicas(rs_svd_plan* pl, hipStream_t s) {
     lg.barrier();  // every shard's sums are in
     std::array<unsigned long long, 6> mine;
     std::copy(h, h + 6, mine.begin());
-    bool same = true;
+    int bad = -1;  // the first checksum some shard disagrees on
     {
         std::lock_guard<std::mutex> l(lg.m);
-        for (const auto& o : lg.chk) same = same && o == mine;
+        for (const auto& o : lg.chk)
+            for (int x = 0; x < 6 && bad < 0; ++x)
+                if (o[x] != mine[x]) bad = x;
     }
     lg.barrier();  // nobody's sums are overwritten before every shard compared
-    if (!same)
-        throw NumericError{"the shards' replicated factors disagree after the exchange (shard " + std::to_string(c.rank) + ")"};
+    if (bad >= 0)
+        throw NumericError{"the shards' replicated factors disagree after the exchange (shard " + std::to_string(c.rank) +
+                           ", " + (bad < 2 ? "P" : bad < 4 ? "Q" : "GlobalBias") + " checksum)"};
 }
 
 }  // namespace

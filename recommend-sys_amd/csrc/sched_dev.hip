@@ -232,6 +232,15 @@ __global__ __launch_bounds__(kB) void runs_kernel(const int32_t* __restrict__ he
     }
 }
 
+// cold runs (sgd_plan.hpp kRunCold): the header bit for items with fewer than dcold ratings, as the host build sets it
+__global__ __launch_bounds__(kB) void cold_runs_kernel(int2* __restrict__ runs, int64_t n_runs, const int32_t* __restrict__ deg,
+                                                       int32_t n_items, int64_t dcold) {
+    for (int64_t r = blockIdx.x * static_cast<int64_t>(kB) + threadIdx.x; r < n_runs; r += static_cast<int64_t>(gridDim.x) * kB) {
+        const int32_t it = runs[r].x;
+        if (it >= 0 && it < n_items && deg[it] < dcold) runs[r].x = it | kRunCold;
+    }
+}
+
 // per tile: its header {first entry, entries, first run, first record}, sentinel, streams and LDS bytes
 __global__ __launch_bounds__(kB) void tiles_kernel(const int32_t* __restrict__ first_entry, const int32_t* __restrict__ users_t,
                                                    const int32_t* __restrict__ recs_t, const int32_t* __restrict__ rec_at,
@@ -488,6 +497,13 @@ bool tile_build_device(rs_svd_plan* pl) {
 
     pl->n_tiles = T;
     pl->tile_grid = std::max(1, std::min(grid0, T));
+    {
+        const int64_t dcold = ni < kRunCold ? cold_degree(pl->cold_runs, n, pl->tile_grid, nw) : 0;
+        if (dcold > 0 && h[4] > 0)
+            hipLaunchKernelGGL(cold_runs_kernel, dim3(blocks_for(h[4])), dim3(kB), 0, s, pl->t_runs.p, static_cast<int64_t>(h[4]),
+                               w.deg_i, ni, dcold);
+        RS_HIP(hipGetLastError());
+    }
     pl->tile_lds = std::max<size_t>(lds, 16);
     pl->t_n_runs = h[4];
     pl->t_n_users = n_active;

@@ -666,7 +666,7 @@ __global__ __launch_bounds__(kEpilogueThreads) void svd_epoch_epilogue_kernel(
     float* __restrict__ P, float* __restrict__ dP, const int32_t* __restrict__ rows, int32_t n_split,
     int32_t ld, const double* __restrict__ partial, int64_t n_partial, double* __restrict__ gb,
     double inv_nnz, int32_t* __restrict__ done, const float* __restrict__ loss_part, double* __restrict__ loss_state,
-    int32_t* __restrict__ flag, double inv_lr2) {
+    int32_t* __restrict__ flag, double inv_lr2, const double* __restrict__ smooth, double a_all) {
     const int b = static_cast<int>(blockIdx.x);
     const int tid = static_cast<int>(threadIdx.x);
     if (b < n_live) {
@@ -691,7 +691,7 @@ __global__ __launch_bounds__(kEpilogueThreads) void svd_epoch_epilogue_kernel(
         return;
     }
     constexpr int NWV = kEpilogueThreads / 64;
-    __shared__ double sh[NWV], sl[NWV];
+    __shared__ double sh[NWV], sl[NWV], sn[NWV], sd[NWV];
     // thread 0's own operands are loaded first, so their latency overlaps the partials' loads instead of
     // following the reduction
     double gb_old = 0.0, prev = 0.0;
@@ -699,26 +699,39 @@ __global__ __launch_bounds__(kEpilogueThreads) void svd_epoch_epilogue_kernel(
         gb_old = gb[0];
         if (loss_part && loss_state) prev = loss_state[0];
     }
-    double t = 0.0, l = 0.0;
+    double t = 0.0, l = 0.0, nm = 0.0, dn = 0.0;
     for (int64_t x = tid; x < n_partial; x += kEpilogueThreads) {
         t += partial[x];
         if (loss_part) l += static_cast<double>(loss_part[x]);
+        if (smooth) {
+            nm += smooth[2 * x];
+            dn += smooth[2 * x + 1];
+        }
     }
     for (int o = 32; o > 0; o >>= 1) {  // fixed order: the same bits on every run
         t += __shfl_xor(t, o);
         l += __shfl_xor(l, o);
+        nm += __shfl_xor(nm, o);
+        dn += __shfl_xor(dn, o);
     }
     if ((tid & 63) == 0) {
         sh[tid >> 6] = t;
         sl[tid >> 6] = l;
+        sn[tid >> 6] = nm;
+        sd[tid >> 6] = dn;
     }
     __syncthreads();
     if (tid == 0) {
         for (int w = 1; w < NWV; ++w) {
             sh[0] += sh[w];
             sl[0] += sl[w];
+            sn[0] += sn[w];
+            sd[0] += sd[w];
         }
-        gb[0] = gb_old + sh[0] * inv_nnz;
+        // the tile epoch's smoothed fold (sgd_tile.hip header): gb' = A gb + (1 - A) T, T = sum b / sum (1 - a);
+        // the other schedules: the count-weighted mean of the streams' moves
+        if (smooth) gb[0] = sd[0] > 0.0 ? a_all * gb_old + (1.0 - a_all) * (sn[0] / sd[0]) : gb_old;
+        else gb[0] = gb_old + sh[0] * inv_nnz;
         if (done) *done = 0;
         if (loss_part && loss_state) {
             // the divergence guard's second signal: this epoch's training MSE (at the ratings' pre-update
@@ -1731,7 +1744,9 @@ static void plan_epochs_once(rs_svd_plan* pl, int32_t epochs, float lr, float re
                                static_cast<int64_t>(pl->n_blocks), pl->gb.p, inv_nnz,
                                n_live > 0 ? pl->done.p : nullptr, loss_on ? pl->loss_part.p : nullptr,
                                loss_on ? pl->loss_state.p : nullptr, loss_on ? pl->guard_flag.p : nullptr,
-                               1.0 / (static_cast<double>(lr) * static_cast<double>(lr)));
+                               1.0 / (static_cast<double>(lr) * static_cast<double>(lr)),
+                               tile ? pl->gb_smooth.p : nullptr,
+                               std::exp(static_cast<double>(pl->nnz) * std::log1p(-static_cast<double>(lr))));
             RS_HIP(hipGetLastError());
         }
         pl->hoisted = false;
@@ -2116,6 +2131,32 @@ extern "C" int rs_svd_plan_set_tiles(rs_svd_plan* pl, int32_t workgroups, int32_
         pl->tile_ring = ring;
         rs::tile_build(pl);
         if (pl->write_back == RS_SGD_WB_TILE) pl->n_blocks = rs::tile_partials(pl);
+        return RS_OK;
+    });
+}
+
+// Test hook (include/rsgpu.h): the hot-run damping with a chosen concurrency, so one wave -- whose runs never
+// overlap -- runs the damped kernel on R = deg x kconc and the oracle's or_svd_fit_works_damped can check it.
+extern "C" int rs_svd_plan_set_damp_concurrency(rs_svd_plan* pl, float kconc) {
+    if (!pl) return rs::set_error(nullptr, RS_ERR_INVALID, "plan is NULL");
+    if (!(kconc >= 0.f) || !std::isfinite(kconc)) return rs::set_error(pl->ctx, RS_ERR_INVALID, "bad concurrency");
+    return rs_guard(pl->ctx, [&]() -> int {
+        rs::plan_sync_last(pl);
+        pl->damp_kconc = kconc;
+        return RS_OK;
+    });
+}
+
+// Cold runs (include/rsgpu.h, sgd_plan.hpp kRunCold): the items whose runs end in write-through stores.  Rebuilds
+// the schedule.
+extern "C" int rs_svd_plan_set_cold_store(rs_svd_plan* pl, double runs_in_flight) {
+    if (!pl) return rs::set_error(nullptr, RS_ERR_INVALID, "plan is NULL");
+    if (!(runs_in_flight >= 0.0) || !std::isfinite(runs_in_flight))
+        return rs::set_error(pl->ctx, RS_ERR_INVALID, "bad cold-run threshold");
+    return rs_guard(pl->ctx, [&]() -> int {
+        rs::plan_sync_last(pl);
+        pl->cold_runs = runs_in_flight;
+        if (pl->tiles_built) rs::tile_build(pl);
         return RS_OK;
     });
 }

@@ -5,6 +5,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cmath>
 #include <cstdint>
 #include <functional>
 #include <stdexcept>
@@ -18,6 +19,20 @@
 namespace rs {
 struct ShardComm;  // multi.hip
 }
+
+namespace rs {
+// Cold runs (sgd_tile.hip, round 6): a run header's item carries kRunCold when the item has so few ratings that
+// another run of it is rarely in flight -- R_i = deg_i x workgroups x waves / nnz below cold_runs -- and the run then
+// ends with plain write-through stores of its new row (an update of the same item landing in between is lost,
+// with probability about R_i) instead of the memory-side atomic unit, which bounds the epoch.
+constexpr int32_t kRunCold = 0x40000000, kRunItemMask = 0x3FFFFFFF;  // item ids below 2^30
+constexpr double kColdRunsDefault = 0.0;
+// items with fewer ratings than this are cold (0: none); the host and the device schedule builds both use it
+inline int64_t cold_degree(double cold_runs, int64_t nnz, int32_t grid, int32_t waves) {
+    if (!(cold_runs > 0.0) || nnz <= 0 || grid <= 0 || waves <= 0) return 0;
+    return static_cast<int64_t>(std::ceil(cold_runs * static_cast<double>(nnz) / (static_cast<double>(grid) * waves)));
+}
+}  // namespace rs
 
 struct rs_svd_plan {
     rs_ctx* ctx = nullptr;
@@ -44,6 +59,7 @@ struct rs_svd_plan {
     int32_t n_isplit = 0;
     rs::DevBuf<float> P, Q;  // bias in column k
     rs::DevBuf<double> gb, partial;
+    rs::DevBuf<double> gb_smooth;  // tile epochs: per (workgroup, wave) the smoothed GlobalBias fold's {sum b, sum (1 - a)}
     rs::DevBuf<float> uw;  // per-user share of this shard (multi-GPU delta mode)
     // hot replicas: most-rated items and copies each (0: none).  Default 256 x 8, measured on the
     // ML-1M shape (scripts/experiments/exp_replicas.py): epoch 760 -> 585 us, held-out RMSE unchanged
@@ -95,6 +111,12 @@ struct rs_svd_plan {
     rs::DevBuf<int32_t> t_split_rows;  // users cut into pieces over several tiles
     rs::DevBuf<int32_t> t_item_deg;    // every item's ratings in the schedule (the hot-run damping, sgd_tile.hip)
     bool tile_damp = false;            // the schedule's hottest item has >= kTileDampRuns runs in flight: damped kernel
+    // cold runs (round 6): items with fewer ratings than cold_degree(cold_runs, ...) -- fewer than cold_runs of their
+    // runs in flight on average -- end their runs with write-through stores of the new row instead of memory-side
+    // atomics (header bit kRunCold); 0 turns it off (rs_svd_plan_set_cold_store)
+    double cold_runs = rs::kColdRunsDefault;
+    float damp_kconc = 0.f;            // test hook (rs_svd_plan_set_damp_concurrency): > 0 forces the damped kernel with
+                                       // runs in flight R = deg x damp_kconc instead of deg x workgroups x waves / nnz
     int32_t t_n_split = 0;
     int64_t t_n_runs = 0, t_n_users = 0;  // entries of t_runs / t_users in use (the buffers may be larger)
     // user blocks: consecutive user ranges of near-equal ratings, each with its own tiles (tiles

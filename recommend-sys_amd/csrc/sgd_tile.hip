@@ -26,8 +26,12 @@
 //     of a hot q_i (updates other workgroups hold in registers while this one reads it) stays at
 //     ~ deg * run time / epoch, a few tens of ratings, like the per-rating schedules.
 //
-// GlobalBias (Q2) is a per-wave local SGD copy folded at epoch end (gb += sum n_w (gb_w - gb)/nnz,
-// fixed order), as in the other FAST schedules.  A user too heavy for one tile's LDS is cut into
+// GlobalBias (Q2) is a per-(tile, wave) local SGD copy from the epoch-start value, folded at epoch end.  The
+// single-GPU epoch folds the streams' chains smoothed (round 6; sgd.hip svd_epoch_epilogue_kernel): each stream's
+// chain gb <- (1 - lr) gb - lr e_j over its n ratings is the map gb0 -> a gb0 + b, a = (1 - lr)^n, so
+// T = sum b / sum (1 - a) is the common level the streams pull toward, and gb' = A gb0 + (1 - A) T with
+// A = (1 - lr)^nnz -- the sequential chain with its e_j at their mean.  The multi-GPU exchanges keep the mean of
+// the moves (gb += sum n_w (gb_w - gb) / nnz, fixed order), as the other FAST schedules do.  A user too heavy for one tile's LDS is cut into
 // pieces in different tiles, each from the same p_u, merged by count-weighted average after the
 // epoch (as rs_svd_plan_set_split).
 //
@@ -98,7 +102,8 @@ __global__ __launch_bounds__(NW * 64) void svd_epoch_tile_kernel(
     float* __restrict__ P, int32_t* Q, int32_t q_bytes, const double* __restrict__ gb_in,
     double* __restrict__ gb_partial, float* __restrict__ loss_partial, float lr, float reg, float fx, float* __restrict__ dP,
     const float* __restrict__ uw, float* __restrict__ dPs, int32_t kf, int32_t ldm, int32_t ldd,
-    int64_t* __restrict__ dbg, const int32_t* __restrict__ item_deg, int32_t deg_bytes, float kconc) {
+    int64_t* __restrict__ dbg, const int32_t* __restrict__ item_deg, int32_t deg_bytes, float kconc,
+    double* __restrict__ gb_smooth, double l1) {
 #pragma clang fp contract(fast)
     constexpr int LD = 64 * E, NT = NW * 64;  // LD: LDS row (k + 2 columns fit); ldm: the rows in HBM
     constexpr bool TIMED = (DIAG & 16) != 0;  // per-wave phase clocks into dbg (experiments)
@@ -134,6 +139,7 @@ __global__ __launch_bounds__(NW * 64) void svd_epoch_tile_kernel(
     }
     auto qaddr = [&](int32_t row, int x) { return (row >= 0 && qoff[x] >= 0) ? row + qoff[x] : kOutOfRange; };
     double contrib = 0.0;
+    double s_num = 0.0, s_den = 0.0;  // the smoothed GlobalBias fold's sums (gb_smooth != nullptr; sgd.hip epilogue)
     float se = 0.f;  // sum of c^2 = (lr diff)^2 over this wave's ratings: the epoch's training loss (the guard)
     const int64_t t_begin = SPAN ? clk() : 0;
     const int64_t rt_begin = SPAN ? static_cast<int64_t>(__builtin_amdgcn_s_memrealtime()) : 0;  // 100 MHz, chip-wide
@@ -150,13 +156,13 @@ __global__ __launch_bounds__(NW * 64) void svd_epoch_tile_kernel(
         int2* Rl = reinterpret_cast<int2*>(Pl + nu * LD);
         int2* Ul = Rl + n_rec;
         auto load_q = [&](int32_t (&q)[E], int32_t& dg, int32_t item) {
-            const int32_t row = item >= 0 ? item * (ldm * 4) : -1;  // SGPR arithmetic
+            const int32_t row = item >= 0 ? (item & kRunItemMask) * (ldm * 4) : -1;  // SGPR arithmetic
 #pragma unroll
             for (int x = 0; x < E; ++x)
                 q[x] = (DIAG & 2) ? 0
                                   : static_cast<int32_t>(__builtin_amdgcn_raw_buffer_load_b32(rq, qaddr(row, x), 0, kSgdAux));
             if constexpr (DAMP)
-                dg = static_cast<int32_t>(__builtin_amdgcn_raw_buffer_load_b32(rdeg, item >= 0 ? item * 4 : kOutOfRange, 0, 0));
+                dg = static_cast<int32_t>(__builtin_amdgcn_raw_buffer_load_b32(rdeg, item >= 0 ? (item & kRunItemMask) * 4 : kOutOfRange, 0, 0));
             else
                 dg = 0;
         };
@@ -315,7 +321,10 @@ __global__ __launch_bounds__(NW * 64) void svd_epoch_tile_kernel(
             }
             gb -= static_cast<double>(cs);
             if constexpr (TIMED) tm_loop += clk() - c0;
-            const int32_t row = item >= 0 ? item * (ldm * 4) : -1;
+            const int32_t row = item >= 0 ? (item & kRunItemMask) * (ldm * 4) : -1;
+            // a cold item's run (header bit kRunCold, sgd_plan.hpp): hardly any other run of the item is in flight, so
+            // the new row is written through with plain sc1 stores instead of memory-side atomics (round 6)
+            const bool cold = item >= 0 && (item & kRunCold) != 0;
             bool damp = false;  // wave-uniform: the common path keeps its exact integer delta and no extra work
             float wq = 1.f, wb = 1.f;
             if (hot) {
@@ -336,6 +345,10 @@ __global__ __launch_bounds__(NW * 64) void svd_epoch_tile_kernel(
                     else
                         __builtin_amdgcn_raw_ptr_buffer_atomic_add_i32(dq, rq, qaddr(row, x), 0, 0);
                 }
+            } else if (cold && !(DIAG & 1)) {  // the same E vector memory ops per run as the atomics (vmcnt)
+#pragma unroll
+                for (int x = 0; x < E; ++x)
+                    __builtin_amdgcn_raw_buffer_store_b32(static_cast<uint32_t>(cvt_rpi(q[x])), rq, qaddr(row, x), 0, kSgdAux);
             } else {
 #pragma unroll
                 for (int x = 0; x < E; ++x) {
@@ -418,6 +431,11 @@ __global__ __launch_bounds__(NW * 64) void svd_epoch_tile_kernel(
         }
         if constexpr (TIMED) tm_c = clk();
         contrib += static_cast<double>(nr) * (gb - gb0);
+        if (gb_smooth) {  // this stream's chain gb0 -> gb over nr ratings: gb = a gb0 + b, a = (1 - lr)^nr
+            const double an = exp(static_cast<double>(nr) * l1);
+            s_num += gb - an * gb0;
+            s_den += 1.0 - an;
+        }
         __syncthreads();
         // write the tile's P rows back: whole users stored (or their weighted delta to dP in
         // multi-GPU delta mode), pieces of split users as count-weighted deltas
@@ -443,6 +461,10 @@ __global__ __launch_bounds__(NW * 64) void svd_epoch_tile_kernel(
         if constexpr (TIMED) tm_tail += clk() - tm_c;
     }
     if (lane == 0) gb_partial[static_cast<int64_t>(blockIdx.x) * NW + w] = contrib;
+    if (lane == 0 && gb_smooth) {
+        gb_smooth[2 * (static_cast<int64_t>(blockIdx.x) * NW + w)] = s_num;
+        gb_smooth[2 * (static_cast<int64_t>(blockIdx.x) * NW + w) + 1] = s_den;
+    }
     if (lane == 0 && loss_partial) loss_partial[static_cast<int64_t>(blockIdx.x) * NW + w] = se;
     if constexpr (SPAN) {
         const int64_t t_end = clk();
@@ -1174,6 +1196,14 @@ void tile_build(rs_svd_plan* pl) {
     pl->t_n_users = static_cast<int64_t>(th.users.size());
     pl->tile_grid = std::max(1, std::min(grid0, pl->n_tiles));
     pl->tile_lds = std::max<size_t>(th.lds, 16);
+    std::vector<int32_t> deg(static_cast<size_t>(std::max(1, pl->n_items)), 0);  // the hot-run damping's degrees
+    for (int32_t c : pl->h_cols) deg[c]++;
+    {  // cold runs: the header bit (sgd_plan.hpp kRunCold; the device build marks them the same way)
+        const int64_t dcold = pl->n_items < kRunCold ? cold_degree(pl->cold_runs, pl->nnz, pl->tile_grid, pl->tile_waves) : 0;
+        if (dcold > 0)
+            for (int2& r : th.runs)
+                if (r.x >= 0 && r.x < pl->n_items && deg[r.x] < dcold) r.x |= kRunCold;
+    }
     pl->t_tiles.alloc(std::max<size_t>(1, th.tiles.size()));
     pl->t_users.alloc(std::max<size_t>(1, th.users.size()));
     pl->t_streams.alloc(std::max<size_t>(1, th.streams.size()));
@@ -1205,8 +1235,6 @@ void tile_build(rs_svd_plan* pl) {
     pl->t_n_split = static_cast<int32_t>(th.split.size());
     pl->t_split_rows.alloc(std::max<size_t>(1, th.split.size()));
     pl->t_split_rows.upload(th.split.data(), th.split.size(), s);
-    std::vector<int32_t> deg(static_cast<size_t>(std::max(1, pl->n_items)), 0);  // the hot-run damping's degrees
-    for (int32_t c : pl->h_cols) deg[c]++;
     pl->t_item_deg.alloc(deg.size());
     pl->t_item_deg.upload(deg.data(), deg.size(), s);
     pl->tile_damp = tile_damp_rule(*std::max_element(deg.begin(), deg.end()), pl->tile_grid, pl->tile_waves, pl->nnz);
@@ -1242,6 +1270,7 @@ void tile_order(rs_svd_plan* pl, int64_t* pos, int64_t* work_off, int32_t* n_wor
 
 struct TileRange {  // tiles [t0, t1) into dP rows of stride ldd (delta mode), grid workgroups
     int32_t t0, t1, ldd, grid;
+    bool smooth = false;  // write the smoothed GlobalBias fold's sums (pl->gb_smooth; single-GPU epochs)
 };
 
 template <int E, int NW, int RQ, int CH, int DIAG = 0, bool DAMP = false>
@@ -1258,7 +1287,10 @@ static void tile_launch_t(rs_svd_plan* pl, float lr, float reg, hipStream_t s, f
                        pl->t_users.p, pl->t_streams.p + static_cast<int64_t>(tr.t0) * (NW + 1), pl->t_runs.p,
                        pl->t_recs.p, pl->P.p, reinterpret_cast<int32_t*>(pl->Q.p), q_bytes, pl->gb.p, pl->partial.p,
                        pl->loss_part.n >= pl->partial.n ? pl->loss_part.p : nullptr, lr, reg, pl->fx(), dP, dP ? pl->uw.p : nullptr, pl->dPs.p, pl->k, pl->ld, tr.ldd, pl->trace.p,
-                       pl->t_item_deg.p, buffer_bytes32(pl->t_item_deg.n, sizeof(int32_t), "item degrees"), pl->nnz > 0 ? static_cast<float>(static_cast<double>(tr.grid) * NW / static_cast<double>(pl->nnz)) : 0.f);
+                       pl->t_item_deg.p, buffer_bytes32(pl->t_item_deg.n, sizeof(int32_t), "item degrees"),
+                       pl->damp_kconc > 0.f ? pl->damp_kconc
+                                            : (pl->nnz > 0 ? static_cast<float>(static_cast<double>(tr.grid) * NW / static_cast<double>(pl->nnz)) : 0.f),
+                       tr.smooth ? pl->gb_smooth.p : nullptr, std::log1p(-static_cast<double>(lr)));
 }
 
 // q_i rows in flight per wave (runs ahead): the ring's loads and the runs' atomics share the wave's
@@ -1297,7 +1329,7 @@ static void tile_launch_r(rs_svd_plan* pl, float lr, float reg, hipStream_t s, f
             if (pl->tile_claim >= 8) return tile_launch_t<E, NW, 2, 8>(pl, lr, reg, s, dP, tr);
         }
         // the default claims (4 runs, ring 2), with the hot-run damping where the schedule asks for it
-        return pl->tile_damp ? tile_launch_t<E, NW, 2, 4, 0, true>(pl, lr, reg, s, dP, tr)
+        return (pl->tile_damp || pl->damp_kconc > 0.f) ? tile_launch_t<E, NW, 2, 4, 0, true>(pl, lr, reg, s, dP, tr)
                              : tile_launch_t<E, NW, 2, 4>(pl, lr, reg, s, dP, tr);
     }
     // the host-dealt schedule (round 3; tile_claim = 0): rings 2 and 4, and 3 / 6 / 8 / 12 for E = 2
@@ -1346,6 +1378,11 @@ static void tile_partials_fit(rs_svd_plan* pl, hipStream_t s) {
         RS_HIP(hipStreamSynchronize(s));
         pl->partial.alloc(static_cast<size_t>(tile_partials(pl)));
     }
+    if (pl->gb_smooth.n < 2 * pl->partial.n) {
+        plan_sync_last(pl);
+        RS_HIP(hipStreamSynchronize(s));
+        pl->gb_smooth.alloc(2 * pl->partial.n);
+    }
 }
 
 void tile_launch(rs_svd_plan* pl, float lr, float reg, hipStream_t s, float* dP) {
@@ -1354,9 +1391,13 @@ void tile_launch(rs_svd_plan* pl, float lr, float reg, hipStream_t s, float* dP)
     tile_partials_fit(pl, s);
     if (pl->n_tiles == 0) {  // no ratings: the fold still reads its partials
         RS_HIP(hipMemsetAsync(pl->partial.p, 0, pl->partial.n * sizeof(double), s));
+        RS_HIP(hipMemsetAsync(pl->gb_smooth.p, 0, pl->gb_smooth.n * sizeof(double), s));
         return;
     }
-    tile_dispatch(pl, lr, reg, s, dP, TileRange{0, pl->n_tiles, pl->ld, pl->tile_grid});
+    // the single-GPU epoch (no dP) also writes the smoothed fold's sums; delta mode folds the mean of the moves
+    TileRange tr{0, pl->n_tiles, pl->ld, pl->tile_grid};
+    tr.smooth = dP == nullptr;
+    tile_dispatch(pl, lr, reg, s, dP, tr);
 }
 
 int32_t tile_launch_range(rs_svd_plan* pl, float lr, float reg, hipStream_t s, float* dP, int32_t ldd,

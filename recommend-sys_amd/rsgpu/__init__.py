@@ -49,7 +49,7 @@ HEADER_SYMBOLS = (
     "rs_comm_unique_id", "rs_svd_plan_join", "rs_svd_plan_epochs_sharded", "rs_svd_plan_leave",
     "rs_svd_plan_set_user_blocks", "rs_svd_group_create", "rs_svd_group_epochs", "rs_svd_group_destroy",
     "rs_item_shards", "rs_svd_fit_multi", "rs_tile_schedule_host", "rs_svd_plan_set_exchange", "rs_svd_plan_set_qdelta_wire", "rs_svd_plan_set_qdelta_split",
-    "rs_svd_plan_set_qdelta_curvature",
+    "rs_svd_plan_set_qdelta_curvature", "rs_svd_plan_set_damp_concurrency", "rs_svd_plan_set_cold_store",
     "rs_comm_info", "rs_rotation_step", "rs_svd_plan_shard_info", "rs_svd_plan_qdelta_info", "rs_svd_plan_inject_fault",
     "rs_svd_plan_time_blocks", "rs_knn_plan_set_tie_order", "rs_fit_refits", "rs_open_r",
     "rs_svd_plan_set_hot_split",
@@ -184,6 +184,8 @@ def lib():
             "rs_svd_plan_set_qdelta_wire": (C.c_int, [_vp, _i32]),
             "rs_svd_plan_set_qdelta_split": (C.c_int, [_vp, C.c_double, _i32]),
             "rs_svd_plan_set_qdelta_curvature": (C.c_int, [_vp, C.c_double]),
+            "rs_svd_plan_set_damp_concurrency": (C.c_int, [_vp, C.c_float]),
+            "rs_svd_plan_set_cold_store": (C.c_int, [_vp, C.c_double]),
             "rs_svd_plan_inject_fault": (C.c_int, [_vp, _i32]),
             "rs_svd_plan_time_blocks": (C.c_int, [_vp, _flt, _flt, _vp, _i32]),
             "rs_knn_plan_set_tie_order": (C.c_int, [_vp, _i32]),
@@ -510,6 +512,15 @@ class SvdPlan:
     def set_qdelta_split(self, hot_ratings, cold_every):
         """RS_EXCHANGE_QDELTA's hot / cold split (rs_svd_plan_set_qdelta_split)."""
         self.ctx.check(lib().rs_svd_plan_set_qdelta_split(self.h, float(hot_ratings), int(cold_every)))
+
+    def set_cold_store(self, runs_in_flight):
+        """Cold runs end in write-through stores (rs_svd_plan_set_cold_store; 0 turns it off)."""
+        self.ctx.check(lib().rs_svd_plan_set_cold_store(self.h, float(runs_in_flight)))
+
+    def set_damp_concurrency(self, kconc):
+        """Test hook: the hot-run damping with runs in flight R = deg x kconc (kconc > 0 forces the damped kernel;
+        0 restores the library's rule; rs_svd_plan_set_damp_concurrency)."""
+        self.ctx.check(lib().rs_svd_plan_set_damp_concurrency(self.h, float(kconc)))
 
     def set_qdelta_curvature(self, gamma):
         """RS_EXCHANGE_QDELTA's merge-weight curvature (rs_svd_plan_set_qdelta_curvature: a = 1 - lr x gamma)."""

@@ -5,9 +5,9 @@ import sys
 import numpy as np
 
 REPO = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
-sys.path[:0] = [os.path.join(REPO, "recommend-sys_amd"), os.path.join(REPO, "scripts")]
+sys.path[:0] = [os.path.join(REPO, "recommend-sys_amd"), os.path.join(REPO, "tests")]
 import rsgpu  # noqa: E402
-import config4_sharded as C  # noqa: E402
+import config4_fit as C  # noqa: E402  (tests/config4_fit.py)
 
 U, I, k, n = 200000, 20000, 64, 8
 ctx = rsgpu.Context(0)

@@ -102,44 +102,62 @@ def rank_env(rank):
     return env
 
 
-def launch(case, n, workdir, timeout=240):
+def launch(case, n, workdir, timeout=120, log_dir=None):
     """Starts n rank processes of `case` on device 0 and waits for them; returns every rank's download.
-    Raises on a non-zero exit or a timeout (the rank processes are killed)."""
+    Raises on a non-zero exit or a timeout (the rank processes are killed).  Each rank's output (progress lines,
+    RCCL's warnings) goes to log_dir/<case>_<n>_r<rank>.log (default: gpurun_out/rccl_ranks under the repo)."""
+    log_dir = log_dir or os.path.join(REPO, "gpurun_out", "rccl_ranks")
+    os.makedirs(log_dir, exist_ok=True)
     id_file = os.path.join(workdir, f"{case}_{n}.id")
     if os.path.exists(id_file):
         os.remove(id_file)
-    procs, outs = [], []
+    procs, outs, logs = [], [], []
     for r in range(n):
         out = os.path.join(workdir, f"{case}_{n}_r{r}.npz")
         outs.append(out)
-        procs.append(subprocess.Popen([sys.executable, "-u", os.path.abspath(__file__), case, str(r), str(n), id_file, out],
-                                      env=rank_env(r), stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True))
-    deadline, logs = time.time() + timeout, []
+        logs.append(os.path.join(log_dir, f"{case}_{n}_r{r}.log"))
+        with open(logs[-1], "w") as lf:
+            procs.append(subprocess.Popen([sys.executable, "-u", os.path.abspath(__file__), case, str(r), str(n), id_file, out],
+                                          env=rank_env(r), stdout=lf, stderr=subprocess.STDOUT))
+    deadline = time.time() + timeout
+
+    def tails():
+        return "\n".join(f"--- rank {r} ({p}):\n" + open(p, errors="replace").read()[-3000:] for r, p in enumerate(logs))
+
     for p in procs:
         try:
-            logs.append(p.communicate(timeout=max(1.0, deadline - time.time()))[0])
+            p.wait(timeout=max(1.0, deadline - time.time()))
         except subprocess.TimeoutExpired:
             for q in procs:
                 q.kill()
-            raise RuntimeError(f"{case} x{n}: rank processes timed out\n" + "\n".join(logs))
+            for q in procs:
+                q.wait()
+            raise RuntimeError(f"{case} x{n}: rank processes timed out after {timeout} s\n" + tails())
     bad = [(r, p.returncode) for r, p in enumerate(procs) if p.returncode != 0]
     if bad:
-        raise RuntimeError(f"{case} x{n}: ranks failed {bad}\n" + "\n".join(logs))
+        raise RuntimeError(f"{case} x{n}: ranks failed {bad}\n" + tails())
     res = []
     for o in outs:
         z = np.load(o)
         res.append(int(z["code"]) if "code" in z else (z["P"], z["Q"], z["bu"], z["bi"], float(z["gb"])))
-    return res, "\n".join(logs)
+    return res, tails()
 
 
 def main(case, rank, n, id_file, out):
+    t0 = time.time()
+
+    def say(m):
+        print(f"[{time.time() - t0:7.2f} s] rank {rank}/{n} {case}: {m}", flush=True)
+
     ctx = rsgpu.Context(0)
     pl = plan(ctx, case, rank, n)  # the plan first: rank 0's id must not wait for the other ranks' plans
+    say("plan built")
     if rank == 0:
         cid = rsgpu.comm_unique_id()
         with open(id_file + ".tmp", "wb") as f:
             f.write(cid)
         os.replace(id_file + ".tmp", id_file)
+        say("communicator id written")
     else:
         t0 = time.time()
         while not os.path.exists(id_file):
@@ -148,7 +166,9 @@ def main(case, rank, n, id_file, out):
             time.sleep(0.05)
         with open(id_file, "rb") as f:
             cid = f.read()
+    say("joining")
     pl.join(cid, rank, n, CASES[case][2])
+    say("joined")
     info = pl.shard_info()
     assert info[:3] == (rank, n, CASES[case][0]), info
     if case.endswith("_diverge"):  # the consistency check must fail on every rank, not only the perturbed one
@@ -166,6 +186,7 @@ def main(case, rank, n, id_file, out):
         print(f"rank {rank}/{n} {case}: call returned {code} {msg}", flush=True)
         return
     pl.epochs_sharded(EPOCHS)
+    say("epochs done")
     pl.leave()
     P, Q, bu, bi, gb = pl.download()
     pl.close()

@@ -1,10 +1,10 @@
-"""Experiment (round 4): FAST tile schedule stability at library defaults across set sizes, hot-item shares
-and k (VERDICT r3 "make the FAST default stable by rule").  rs_synth sets (lognormal user degrees, Zipf
+"""FAST tile schedule stability at library defaults across set sizes, hot-item shares and k (test
+infrastructure of tests/test_stability_gpu.py; round 4, VERDICT r3 "make the FAST default stable by rule").  rs_synth sets (lognormal user degrees, Zipf
 items), 5 % held out, device init N(0, 0.1), GlobalBias = training mean; held-out RMSE after every epoch,
 the run cap the library chose, and -- where the oracle is affordable -- the sequential reference
 (core/svd.go:92-130 in a shuffled TrainSet order, same init) beside it.
 
-    python scripts/experiments/exp_stability.py [case ...] [--claim 0|4|8] [--cap C]
+    python tests/stability_sets.py [case ...] [--claim 0|4|8] [--cap C]
 """
 import argparse
 import os
@@ -13,7 +13,7 @@ import time
 
 import numpy as np
 
-REPO = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path[:0] = [os.path.join(REPO, "recommend-sys_amd"), os.path.join(REPO, "oracle")]
 import rsgpu  # noqa: E402
 
@@ -24,6 +24,10 @@ CASES = {
     "1m_k100_hot": (20000, 2000, 50.0, 1.2, 100, 10, True),
     "1m_k100_flat": (20000, 8000, 50.0, 0.6, 100, 10, True),
     "1m_k64_3pct": (20000, 2000, 50.0, 1.4, 64, 10, True),
+    # round 6: hottest item just under the damping rule's 40 runs in flight (R = share x 176 x 16 on the library's grid):
+    # 1.03 % (R ~ 29) and 1.13 % (R ~ 32) -- the plain kernel's upper range
+    "1m_k64_r29": (20000, 4000, 60.0, 0.7, 64, 10, True),
+    "1m_k100_r32": (20000, 2000, 50.0, 0.65, 100, 10, True),
     "8m_k100": (100000, 20000, 80.0, 0.9, 100, 8, False),
     "8m_k256_hot": (200000, 10000, 40.0, 1.1, 256, 5, False),
     "32m_k100": (400000, 50000, 80.0, 1.0, 100, 5, False),

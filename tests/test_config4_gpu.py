@@ -7,21 +7,16 @@ the whole set fitted by one plan from the same factors.  Reference loop: core/sv
 About three minutes on the box (generation ~35 s, the two plans ~55 s, 2 x 10 epochs); progress lines go to
 the terminal so the run never looks silent.
 """
-import os
-import sys
-
 import numpy as np
 import pytest
 
 pytestmark = pytest.mark.gpu
 
-REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-sys.path.insert(0, os.path.join(REPO, "scripts"))
 
 
 @pytest.mark.timeout(900)
 def test_config4_sharded_full_size(request):
-    import config4_sharded as C
+    import config4_fit as C
     tr = request.config.pluginmanager.get_plugin("terminalreporter")
     say = (lambda *a: tr.write_line("  [configs[4]] " + " ".join(str(x) for x in a))) if tr else (lambda *a: None)
     out = C.run(C.parse(["--epochs", "10", "--exchange", "qdelta"]), say=say)

@@ -39,32 +39,34 @@ def scaled(ml100k):
 
 @pytest.mark.parametrize("scale", sorted(SCALES))
 def test_svd_fast_on_rating_scale(ctx, scaled, scale):
-    """5-fold, k = 100, 20 epochs: no refit, no error, within the base_test.go:34-36 bound in star units where
-    the restatement meets it, and within 0.003 x scale of a sequential SGD restatement of the reference -- the closer of the
-    reference visit order (or_svd_fit) and the user-major order with FAST's GlobalBias warm start
-    (or_svd_fit_chunked).  At x20 / lr 0.0005 the visit order alone moves the result: reference order
-    18.649, user-major 18.711 (0.062 = 0.0031 in star units), so the tile schedule (yet another order) is
-    held to the nearer of the two sequential results rather than to one of them."""
+    """5-fold, k = 100, 20 epochs: no refit, no error, and within 0.003 x scale (P2 in the scale's units) of the
+    reference visit order (or_svd_fit: svd.go:92-130 over the TrainSet in data order), and within the
+    base_test.go:34-36 bound in star units where the reference order itself meets it (on -10..10 at lr 0.005 it
+    lands at 5.20, 1.04 in star units, on its own).
+
+    Round 5 measured 18.741 at x20 against the reference order's 18.649 (0.0046 in star units).  The gap was the
+    GlobalBias fold, not the visit order: the per-stream chains folded by the mean of their moves advance
+    GlobalBias by about one stream's ~30 ratings per epoch, so at lr 0.0005 it lagged the biases; the sequential
+    chain converges within 1 / lr ratings.  The single-GPU epoch now folds the chains smoothed (sgd_tile.hip
+    header; the oracle's or_svd_fit_works2 compose = 2 restates it): on the CPU with 2816 streams in random
+    order, x20 0.93679 -> 0.93347 star units against 0.93243 for the reference, stars 0.93687 -> 0.93650
+    against 0.93675."""
     k, lr, mult = 100, SVD_LR[scale], SCALES[scale][1]
-    ref_r, um_r, gpu_r, refits = [], [], [], []
+    ref_r, gpu_r, refits = [], [], []
     for f in scaled[scale]:
         rng = np.random.default_rng(7)
         P0, Q0 = rng.normal(0, 0.1, (f.nu, k)), rng.normal(0, 0.1, (f.ni, k))
         a = O.svd_fit(f.iu, f.ii, f.r, P0, Q0, lr=lr)
         ref_r.append(rmse(O.svd_predict(f.tu, f.ti, *a), f.te_r))
-        rowptr, items, rr = O.csr_by(f.iu, f.nu, f.ii, f.r)
-        c = O.svd_fit_chunked(rowptr, items, rr, P0, Q0, 1 << 30, lr=lr)
-        um_r.append(rmse(O.svd_predict(f.tu, f.ti, *c), f.te_r))
         b = ctx.svd_fit(rsgpu.Ratings(f.iu, f.ii, f.r, f.nu, f.ni), P0, Q0, lr=lr)  # raises on RS_ERR_NUMERIC
         refits.append(ctx.fit_refits())
         assert all(np.all(np.isfinite(x)) for x in b[:4])
         gpu_r.append(rmse(rsgpu.svd_predict(f.tu, f.ti, *b), f.te_r))
-    ref_m, um_m, gpu_m = float(np.mean(ref_r)), float(np.mean(um_r)), float(np.mean(gpu_r))
+    ref_m, gpu_m = float(np.mean(ref_r)), float(np.mean(gpu_r))
+    print(f"{scale}: GPU {gpu_m:.4f}, reference order {ref_m:.4f} ({(gpu_m - ref_m) / mult:+.4f} star units)")
     assert refits == [0] * len(refits), refits
-    assert min(abs(gpu_m - ref_m), abs(gpu_m - um_m)) <= 0.003 * mult, (gpu_m, ref_m, um_m)
-    # base_test.go:34-36's bound in star units, where the sequential restatement itself meets it: on the -10..10
-    # scale at lr 0.005 the reference order lands at 5.18-5.25 (1.04 in star units) on its own
-    if min(ref_m, um_m) / mult <= 0.934:
+    assert abs(gpu_m - ref_m) <= 0.003 * mult, (gpu_m, ref_m)
+    if ref_m / mult <= 0.934:
         assert gpu_m / mult <= 0.934 + 0.008, gpu_m
 
 
@@ -86,7 +88,7 @@ def test_svd_fast_one_wave_exact_on_1_100(ctx, scaled):
     cu = np.repeat(np.arange(f.nu, dtype=np.int32), np.diff(rowptr))
     pos, off = plan.tile_order()
     ref = O.svd_fit_works(cu[pos], np.asarray(items, np.int32)[pos], np.asarray(rr)[pos], off, P0, Q0, bu0, bi0,
-                          70.0, epochs=2, lr=0.0005)
+                          70.0, epochs=2, lr=0.0005, compose=2)
     plan.close()
     d = max(float(np.max(np.abs(np.asarray(x) - np.asarray(y)))) for x, y in zip(ref[:4], got[:4]))
     assert d <= 2e-4 and abs(ref[4] - got[4]) <= 2e-4, d

@@ -16,10 +16,12 @@ from rsgpu import synth
 pytestmark = pytest.mark.gpu
 
 
-def _digests(ctx, R, k, wg=0, waves=16, run_cap=0):
+def _digests(ctx, R, k, wg=0, waves=16, run_cap=0, cold=None):
     plan = ctx.svd_plan(R, k)
     if wg or waves != 16 or run_cap:
         plan.set_tiles(workgroups=wg, waves=waves, run_cap=run_cap)
+    if cold is not None:
+        plan.set_cold_store(cold)
     plan.set_tile_rule(rsgpu.TILE_RULE_FILL)
     host = plan.schedule_digest()
     plan.set_tile_rule(rsgpu.TILE_RULE_FILL_DEVICE)
@@ -51,6 +53,18 @@ def test_device_schedule_equals_host_ml100k(ctx, ml100k, k, wg, waves, run_cap):
     host, dev, lpt = _digests(ctx, rsgpu.Ratings(f.iu, f.ii, f.r, f.nu, f.ni), k, wg, waves, run_cap)
     assert host == dev
     assert lpt != dev  # (the default build is a different rule)
+
+
+@pytest.mark.parametrize("cold", [0.0, 0.05, 1.0])
+def test_device_schedule_equals_host_cold_runs(ctx, ml100k, cold):
+    """The cold-run header bit (sgd_plan.hpp kRunCold: items below cold_degree's ratings) is set identically by the
+    host and the device builds, and changes the schedule's bytes exactly when some item is that cold."""
+    f = folds(*ml100k)[1]
+    R = rsgpu.Ratings(f.iu, f.ii, f.r, f.nu, f.ni)
+    host, dev, _ = _digests(ctx, R, 64, cold=cold)
+    base, _, _ = _digests(ctx, R, 64, cold=0.0)
+    assert host == dev
+    assert (host == base) == (cold == 0.0)
 
 
 @pytest.mark.parametrize("k,wg,waves", [(100, 0, 16), (100, 33, 16), (256, 0, 2), (8, 5, 1)])
@@ -108,7 +122,7 @@ def test_one_wave_on_device_schedule_is_sequential_sgd(ctx, ml100k, epochs, targ
     cu = np.repeat(np.arange(nu, dtype=np.int32), np.diff(rowptr))
     pos, off = plan.tile_order()
     ref = O.svd_fit_works(cu[pos], np.asarray(items, np.int32)[pos], np.asarray(rr, np.float64)[pos], off,
-                          P0, Q0, bu0, bi0, 3.2, epochs=epochs)
+                          P0, Q0, bu0, bi0, 3.2, epochs=epochs, compose=2)
     plan.close()
     d = max(float(np.max(np.abs(np.asarray(a) - np.asarray(b)))) for a, b in zip(ref[:4], got[:4]))
     assert d <= 1e-5 and abs(ref[4] - got[4]) <= 1e-5

@@ -1,5 +1,5 @@
 """FAST default stability at library defaults: rs_synth sets of 1M / 8M / 32M / 128M ratings,
-hottest item 0.3-3 % of the ratings, k 64 / 100 / 256 (scripts/experiments/exp_stability.py CASES), 5 %
+hottest item 0.3-3 % of the ratings, k 64 / 100 / 256 (tests/stability_sets.py CASES), 5 %
 held out.  Where the sequential reference (or_svd_fit, core/svd.go:92-130 over the ratings in a shuffled
 TrainSet order -- KFold's data order, data.go:49-70 --, the same init) is affordable (the 1M sets) the
 held-out RMSE after 10 epochs is at most 0.003 above the reference's (P2's margin, one-sided: the tile order
@@ -9,24 +9,19 @@ stay finite and the held-out RMSE falls every epoch.  Both the plan path (rs_svd
 drop-in (rs_svd_fit, with its divergence guard) run every oracle case; the divergence guard's redos are
 reported (profiles/r05/stability.log) and must be zero on the SMALL sets (the hot-run damping of
 sgd_tile.hip, not the redo, keeps them stable)."""
-import os
-import sys
-
 import numpy as np
 import pytest
 
 pytestmark = pytest.mark.gpu
-REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-sys.path.insert(0, os.path.join(REPO, "scripts", "experiments"))
 
-SMALL = ["1m_k64", "1m_k64_hot", "1m_k100_hot", "1m_k100_flat", "1m_k64_3pct"]
+SMALL = ["1m_k64", "1m_k64_hot", "1m_k100_hot", "1m_k100_flat", "1m_k64_3pct", "1m_k64_r29", "1m_k100_r32"]
 LARGE = ["8m_k100", "8m_k256_hot", "32m_k100", "128m_k256"]
 
 
 @pytest.fixture(scope="module")
 def S():
-    import exp_stability
-    return exp_stability
+    import stability_sets
+    return stability_sets
 
 
 @pytest.mark.parametrize("name", SMALL)

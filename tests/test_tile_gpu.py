@@ -3,8 +3,9 @@ epoch of core/svd.go:92-130.
 
 Exactness: with one wave per workgroup the tile kernel is the sequential SGD of svd.go:93-129 in the
 schedule's own visit order (rs_svd_plan_tile_order) with a work-local GlobalBias per (tile, wave)
-stream folded after the epoch.  The oracle restates exactly that (or_svd_fit_works, the reference's
-per-rating update and aliasing Q1 over explicit work segments), so:
+stream folded after the epoch (the smoothed fold of the single-GPU epoch: sgd_tile.hip header).  The oracle
+restates exactly that (or_svd_fit_works2 with compose = 2, the reference's per-rating update and aliasing Q1
+over explicit work segments), so:
   * one workgroup, one wave, real ML-100K data (users and items shared everywhere): equal to 1e-5;
   * several workgroups, one wave each, on race-free input (private items): equal to 1e-5.
 The P rows live in LDS as int32 fixed point (2^-24) and Q as int32 fixed point between calls, inside the
@@ -38,7 +39,7 @@ def _oracle_in_tile_order(plan, u, i, r, nu, P0, Q0, bu0, bi0, gb0, epochs):
     cu, ci, cr = _csr(u, i, r, nu)
     pos, off = plan.tile_order()
     assert np.array_equal(np.sort(pos), np.arange(len(r)))  # every rating exactly once
-    return O.svd_fit_works(cu[pos], ci[pos], cr[pos], off, P0, Q0, bu0, bi0, gb0, epochs=epochs)
+    return O.svd_fit_works(cu[pos], ci[pos], cr[pos], off, P0, Q0, bu0, bi0, gb0, epochs=epochs, compose=2)
 
 
 @pytest.mark.parametrize("k,epochs,target,run_cap", [(20, 1, 3000, 0), (100, 1, 5000, 0),
@@ -86,6 +87,59 @@ def test_one_wave_claims_any_ring(ctx, ml100k, claim, ring):
     assert _maxdiff(ref[:4], got[:4]) <= TOL and abs(ref[4] - got[4]) <= TOL
 
 
+@pytest.mark.parametrize("k,kconc", [(40, 1.0), (100, 0.25)])
+def test_damped_runs_one_wave_equal_oracle(ctx, ml100k, k, kconc):
+    """The hot-run damping (svd_epoch_tile_kernel<..., DAMP = true>) pinned: the test hook
+    rs_svd_plan_set_damp_concurrency makes one wave -- whose runs never overlap -- take the damped kernel with
+    R = deg x kconc runs in flight, and the result equals the oracle's restatement of the rule
+    (or_svd_fit_works_damped: each run's move scaled by min(1, 1 / (R f)) on the factors and on b_i) to 1e-5,
+    on real ML-100K ratings; the damping moved the item rows away from the undamped epoch."""
+    f = folds(*ml100k)[0]
+    n = 20000
+    u, i, r, nu, ni = f.iu[:n], f.ii[:n], f.r[:n], f.nu, f.ni
+    rng = np.random.default_rng(k)
+    P0, Q0 = rng.normal(0, 0.1, (nu, k)), rng.normal(0, 0.1, (ni, k))
+    bu0, bi0 = rng.normal(0, 0.1, nu), rng.normal(0, 0.1, ni)
+    plan = ctx.svd_plan(rsgpu.Ratings(u, i, r, nu, ni), k)
+    plan.set_tiles(workgroups=1, waves=1, target=4000)  # one wave: runs uncut (no automatic cap)
+    plan.set_damp_concurrency(kconc)
+    plan.upload(P0, Q0, bu0, bi0, 3.2)
+    plan.epochs(2)
+    got = plan.download()
+    cu, ci, cr = _csr(u, i, r, nu)
+    pos, off = plan.tile_order()
+    deg = np.bincount(i, minlength=ni).astype(np.int32)
+    ref = O.svd_fit_works_damped(cu[pos], ci[pos], cr[pos], off, deg, float(np.float32(kconc)), P0, Q0, bu0, bi0, 3.2,
+                                 epochs=2, compose=2)
+    plain = O.svd_fit_works(cu[pos], ci[pos], cr[pos], off, P0, Q0, bu0, bi0, 3.2, epochs=2, compose=2)
+    plan.set_damp_concurrency(0)
+    plan.close()
+    assert _maxdiff(ref[:4], got[:4]) <= TOL and abs(ref[4] - got[4]) <= TOL
+    assert _maxdiff(ref[1:2], plain[1:2]) > 1e-3 and _maxdiff(ref[3:4], plain[3:4]) > 1e-3  # the rule acted
+
+
+@pytest.mark.parametrize("k", [20, 100])
+def test_cold_store_one_wave_equals_oracle(ctx, ml100k, k):
+    """Cold runs (rs_svd_plan_set_cold_store: here every item cold) end in write-through stores of the new row; with
+    one wave no other run of the item is in flight, so the store is the atomic's sum and the epoch stays the
+    sequential SGD in tile order (1e-5)."""
+    f = folds(*ml100k)[3]
+    n = 20000
+    u, i, r, nu, ni = f.iu[:n], f.ii[:n], f.r[:n], f.nu, f.ni
+    rng = np.random.default_rng(k + 1)
+    P0, Q0 = rng.normal(0, 0.1, (nu, k)), rng.normal(0, 0.1, (ni, k))
+    bu0, bi0 = rng.normal(0, 0.1, nu), rng.normal(0, 0.1, ni)
+    plan = ctx.svd_plan(rsgpu.Ratings(u, i, r, nu, ni), k)
+    plan.set_tiles(workgroups=1, waves=1, target=3000)
+    plan.set_cold_store(1e9)
+    plan.upload(P0, Q0, bu0, bi0, 3.3)
+    plan.epochs(2)
+    got = plan.download()
+    ref = _oracle_in_tile_order(plan, u, i, r, nu, P0, Q0, bu0, bi0, 3.3, 2)
+    plan.close()
+    assert _maxdiff(ref[:4], got[:4]) <= TOL and abs(ref[4] - got[4]) <= TOL
+
+
 def _private_items(n_users=300, per_user=25, seed=4):
     rng = np.random.default_rng(seed)
     deg = rng.integers(1, 2 * per_user, n_users)
@@ -117,7 +171,9 @@ def test_workgroups_race_free(ctx, k, wg):
 
 def test_delta_mode_equals_direct(ctx, ml100k):
     """The item-sharded multi-GPU path with one shard holding every item (user weights 1):
-    epoch_delta + apply_delta gives the epoch of plain epochs() (one wave: deterministic)."""
+    epoch_delta + apply_delta gives the epoch of plain epochs() (one wave: deterministic) -- the same factors
+    and biases; GlobalBias is folded by the mean of the streams' moves in delta mode and smoothed in the plain
+    single-GPU epoch, each equal to the oracle's fold of that name in the exported tile order."""
     import torch
     f = folds(*ml100k)[1]
     u, i, r, nu, ni = f.iu, f.ii, f.r, f.nu, f.ni
@@ -139,9 +195,14 @@ def test_delta_mode_equals_direct(ctx, ml100k):
     plans[1].apply_delta_t(dP, g, 1.0 / len(r))
     torch.cuda.synchronize()
     a, b = plans[0].download(), plans[1].download()
+    cu, ci, cr = _csr(u, i, r, nu)
+    pos, off = plans[0].tile_order()
+    smooth = O.svd_fit_works(cu[pos], ci[pos], cr[pos], off, P0, Q0, np.zeros(nu), np.zeros(ni), 3.5, compose=2)
+    mean = O.svd_fit_works(cu[pos], ci[pos], cr[pos], off, P0, Q0, np.zeros(nu), np.zeros(ni), 3.5, compose=0)
     for pl in plans:
         pl.close()
-    assert _maxdiff(a[:4], b[:4]) <= TOL and abs(a[4] - b[4]) <= 1e-9
+    assert _maxdiff(a[:4], b[:4]) <= TOL
+    assert abs(a[4] - smooth[4]) <= TOL and abs(b[4] - mean[4]) <= TOL
 
 
 def test_heavy_user_cut_into_pieces_trains(ctx):
