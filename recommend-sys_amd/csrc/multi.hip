@@ -349,8 +349,15 @@ template <> struct Wire4<16> {
     }
     __device__ static T make(const int4& r, float w, float fx, float fx_inv, int4& own) {
         const float s = w * fx_inv;
-        const T v = h(make_float4(s * static_cast<float>(r.x), s * static_cast<float>(r.y), s * static_cast<float>(r.z),
-                                  s * static_cast<float>(r.w)));
+        float4 y = make_float4(s * static_cast<float>(r.x), s * static_cast<float>(r.y), s * static_cast<float>(r.z),
+                               s * static_cast<float>(r.w));
+        // The products are rounded to f32 here: without the barrier the compiler fuses a product with its f16
+        // conversion (v_fma_mixlo_f16, one rounding) for some lanes and not others, and the value decoded as this
+        // rank's own move left the bits on the wire by one f16 ulp on ~1e-4 of the rows (configs[4]: the 8 shards'
+        // replicated Q disagreed; check_replicas caught it, round 6).
+        asm volatile("" : "+v"(y.x), "+v"(y.y), "+v"(y.z), "+v"(y.w));
+        T v = h(y);
+        asm volatile("" : "+v"(v.x), "+v"(v.y));  // own is decoded from exactly the bits that are stored
         own = fixed(v, fx);
         return v;
     }
@@ -1118,9 +1125,6 @@ void epochs_qdelta(rs_svd_plan* pl, int32_t n_epochs, float lr, float reg, hipSt
             check_nccl(ncclAllReduce(c.gbs.p + par, c.gbs.p + par, 1, ncclFloat64, ncclSum, c.nccl, c.cs),
                        "ncclAllReduce(GlobalBias)");
             RS_HIP(hipEventRecord(c.ev_ar[par], c.cs));
-            static const int dbg_sync = std::getenv("RSGPU_QDELTA_SYNC") ? std::atoi(std::getenv("RSGPU_QDELTA_SYNC")) : 0;
-            if (dbg_sync & 1) RS_HIP(hipStreamSynchronize(c.cs));  // (diagnostic: no overlap)
-            if (dbg_sync & 2) std::fprintf(stderr, "qdelta rank %d merge %d enqueued\n", c.rank, m);
         } else {  // in-process: the sum now (no overlap), applied on the same deferred schedule
             LocalGroup& lg = *c.local;
             RS_HIP(hipStreamSynchronize(s));

@@ -193,7 +193,18 @@ def sharded(args, ctx, parts, hu, hi_, hr, gb0, whole):
     curve, ep_s = [], []
     for e in range(args.epochs):
         t = time.perf_counter()
-        g.epochs(1, LR, REG)
+        try:
+            g.epochs(1, LR, REG)
+        except rsgpu.RsError as x:  # (diagnostic: where the shards' replicas differ)
+            log(f"sharded epoch {e + 1}: {x}")
+            Qs = [pl.download()[1] for pl in plans]
+            cnt = np.bincount(np.concatenate([p_["cols"] for p_ in parts]), minlength=I)
+            for sidx in range(1, len(Qs)):
+                d = np.abs(Qs[sidx] - Qs[0]).max(1)
+                bad = np.nonzero(d > 0)[0]
+                log(f"shard {sidx} vs 0: {len(bad)} item rows differ, max {d.max():.3g}; first "
+                    + ", ".join(f"{int(b)}(deg {int(cnt[b])}, {d[b]:.3g})" for b in bad[:8]))
+            raise
         ep_s.append(time.perf_counter() - t)
         curve.append(plans[0].evaluate(hu, hi_, hr)[0])
         log(f"sharded epoch {e + 1}: {ep_s[-1]:.3f} s, held-out RMSE {curve[-1]:.4f}")
