@@ -315,6 +315,10 @@ int rs_svd_plan_set_tile_claim(rs_svd_plan* plan, int32_t runs_per_claim);
 int rs_svd_plan_set_guard(rs_svd_plan* plan, int32_t on);
 /* Calls the guard has redone on this plan so far. */
 int rs_svd_plan_refits(const rs_svd_plan* plan, int32_t* n);
+/* The plan's fixed-point shift S (FAST P / Q / Y held as int32 round(v 2^S) while a call runs; from the ratings'
+ * spread, lowered to the group's smallest while the plan is in a group or joined -- rs_svd_plan_leave /
+ * rs_svd_group_destroy restore it). */
+int rs_svd_plan_fixed_point(const rs_svd_plan* plan, int32_t* shift);
 #define RS_TILE_RULE_LPT 0
 #define RS_TILE_RULE_FILL 1
 #define RS_TILE_RULE_FILL_DEVICE 2
@@ -478,9 +482,9 @@ int rs_svd_plan_set_qdelta_wire(rs_svd_plan* plan, int32_t bits);
  * every cold_every-th block (the largest divisor of the merges per epoch up to cold_every; 1: every merge is a
  * full one).  Set before the join, the same on every rank. */
 int rs_svd_plan_set_qdelta_split(rs_svd_plan* plan, double hot_ratings, int32_t cold_every);
-/* RS_EXCHANGE_QDELTA's merge weights: the contraction per rating a = 1 - lr x gamma in kappa_i (gamma = 1: the
- * unit curvature above, the default; 0: w_i = 1, the plain sum of the moves).  Set before the join, the same on
- * every rank. */
+/* RS_EXCHANGE_QDELTA's merge weights on the factor columns: the contraction per rating a = 1 - lr x gamma in
+ * kappa_i (gamma = 1: the unit curvature above, the default; 0: w_i = 1, the plain sum of the moves).  The bias
+ * column keeps the unit curvature of its own gradient.  Set before the join, the same on every rank. */
 int rs_svd_plan_set_qdelta_curvature(rs_svd_plan* plan, double gamma);
 /* Test hook: the tile schedule's hot-run damping with the runs in flight of an item taken
  * as R = its ratings x kconc (kconc > 0 forces the damped kernel; 0 restores the library's rule, R = ratings x
@@ -493,6 +497,13 @@ int rs_svd_plan_set_damp_concurrency(rs_svd_plan* plan, float kconc);
  * then loses its update, which happens with about that probability.  0 turns it off.  With one wave per
  * workgroup a store equals the atomic (no run overlaps).  Rebuilds the schedule. */
 int rs_svd_plan_set_cold_store(rs_svd_plan* plan, double runs_in_flight);
+/* How a single-GPU tile epoch folds GlobalBias (svd.go:104-106's chain, run per (tile, wave) stream from the epoch's
+ * start value): RS_GB_FOLD_SMOOTH (default since round 6) -- the streams' chains composed with their rates at
+ * their mean, gb' = A gb + (1 - A) T (sgd_tile.hip header); RS_GB_FOLD_MEAN -- the count-weighted mean of the
+ * streams' moves (rounds 1-5; the multi-GPU exchanges always fold this way). */
+#define RS_GB_FOLD_MEAN 0
+#define RS_GB_FOLD_SMOOTH 1
+int rs_svd_plan_set_gb_fold(rs_svd_plan* plan, int32_t mode);
 /* RS_EXCHANGE_ROTATE_Q on Zipf-headed sets: a stratum (one rank's users x one item block) holds an item's
  * ratings n_blocks-fold concentrated, so the head's rows get many concurrent runs in flight (Hogwild staleness
  * that diverges at lr 0.005; configs[4]: the hottest item is 0.8 % of the set but 12.7 % of its stratum).  An

@@ -187,10 +187,7 @@ int32_t qdelta_cold_every(int32_t merges, int32_t most) {
     return 1;
 }
 
-int32_t comm_ctas() {
-    static const int v = std::getenv("RSGPU_COMM_CTAS") ? std::atoi(std::getenv("RSGPU_COMM_CTAS")) : 32;
-    return std::max(1, std::min(v, 128));
-}
+int32_t comm_ctas() { return 32; }  // workgroups of the multi-GPU piece copies
 
 // P rows [u0, u1) += the summed deltas (row stride ldd, k + 1 columns: factors and the bias)
 __global__ __launch_bounds__(256) void apply_rows_kernel(float* __restrict__ P, const float* __restrict__ D,
@@ -316,9 +313,9 @@ template <> struct Wire4<32> {
     using T = int4;
     __device__ static int4 fixed(T v, float) { return v; }
     // the weighted moves of raw fixed-point moves r: on the wire and (own) as applied here
-    __device__ static T make(const int4& r, float w, float, float, int4& own) {
-        own = make_int4(__float2int_rn(w * static_cast<float>(r.x)), __float2int_rn(w * static_cast<float>(r.y)),
-                        __float2int_rn(w * static_cast<float>(r.z)), __float2int_rn(w * static_cast<float>(r.w)));
+    __device__ static T make(const int4& r, float4 w, float, float, int4& own) {
+        own = make_int4(__float2int_rn(w.x * static_cast<float>(r.x)), __float2int_rn(w.y * static_cast<float>(r.y)),
+                        __float2int_rn(w.z * static_cast<float>(r.z)), __float2int_rn(w.w * static_cast<float>(r.w)));
         return own;
     }
 };
@@ -347,10 +344,9 @@ template <> struct Wire4<16> {
         const float4 x = f(v);
         return make_int4(__float2int_rn(x.x * fx), __float2int_rn(x.y * fx), __float2int_rn(x.z * fx), __float2int_rn(x.w * fx));
     }
-    __device__ static T make(const int4& r, float w, float fx, float fx_inv, int4& own) {
-        const float s = w * fx_inv;
-        float4 y = make_float4(s * static_cast<float>(r.x), s * static_cast<float>(r.y), s * static_cast<float>(r.z),
-                               s * static_cast<float>(r.w));
+    __device__ static T make(const int4& r, float4 w, float fx, float fx_inv, int4& own) {
+        float4 y = make_float4(w.x * fx_inv * static_cast<float>(r.x), w.y * fx_inv * static_cast<float>(r.y),
+                               w.z * fx_inv * static_cast<float>(r.z), w.w * fx_inv * static_cast<float>(r.w));
         // The products are rounded to f32 here: without the barrier the compiler fuses a product with its f16
         // conversion (v_fma_mixlo_f16, one rounding) for some lanes and not others, and the value decoded as this
         // rank's own move left the bits on the wire by one f16 ulp on ~1e-4 of the rows (configs[4]: the 8 shards'
@@ -383,7 +379,7 @@ __global__ __launch_bounds__(256) void qdelta_merge_kernel(int32_t* __restrict__
                                                            const void* __restrict__ ph_sum, const void* __restrict__ ph_dq,
                                                            int32_t ph_full, const void* __restrict__ pc_sum,
                                                            const void* __restrict__ pc_dq, uint32_t n4, uint32_t l4,
-                                                           uint32_t ld4, float fx, float fx_inv) {
+                                                           uint32_t ld4, float fx, float fx_inv, int32_t kb) {
     using W = Wire4<B>;
     using T = typename W::T;
     const uint32_t t = blockIdx.x * 256u + threadIdx.x;
@@ -395,7 +391,11 @@ __global__ __launch_bounds__(256) void qdelta_merge_kernel(int32_t* __restrict__
         int4& zv = reinterpret_cast<int4*>(Q0)[ti];
         const int4 q = qv, q0 = zv;
         int4 own;
-        reinterpret_cast<T*>(dq)[t] = W::make(sub4(q, q0), w[i], fx, fx_inv, own);
+        // the row's weights: w[2 i] on the factor columns, w[2 i + 1] on the bias (column kb)
+        const float wf = w[2 * static_cast<size_t>(i)], wb = w[2 * static_cast<size_t>(i) + 1];
+        const int32_t cb = kb - 4 * static_cast<int32_t>(c4);
+        const float4 wv = make_float4(cb == 0 ? wb : wf, cb == 1 ? wb : wf, cb == 2 ? wb : wf, cb == 3 ? wb : wf);
+        reinterpret_cast<T*>(dq)[t] = W::make(sub4(q, q0), wv, fx, fx_inv, own);
         int4 v = add4(q0, own);
         const int32_t hp = rows ? static_cast<int32_t>(r) : (hpos ? hpos[i] : -1);
         const void* ps = hp >= 0 ? ph_sum : pc_sum;
@@ -1030,23 +1030,29 @@ void epochs_qdelta(rs_svd_plan* pl, int32_t n_epochs, float lr, float reg, hipSt
     const int32_t F = c.cold_every;
     if (c.qw_lr != lr || c.qw_curv != pl->qdelta_curv) {  // the merge weights for this lr (module header: kappa / c per item)
         const size_t n1 = static_cast<size_t>(std::max(1, ni));
-        std::vector<float> cn(n1), cc(n1), w(n1, 1.f);
+        std::vector<float> cn(n1), cc(n1), w(2 * n1, 1.f);  // {factor columns, bias} per item
         std::vector<int32_t> hp(n1);
         c.item_n.download(cn.data(), n1, s);
         c.item_c.download(cc.data(), n1, s);
         c.hot_pos.download(hp.data(), n1, s);
         RS_HIP(hipStreamSynchronize(s));
-        const double a = std::max(1e-12, 1.0 - static_cast<double>(lr) * pl->qdelta_curv);
+        // the factor columns' contraction per rating a = 1 - lr x curvature (rs_svd_plan_set_qdelta_curvature); the
+        // bias column's is the unit curvature of its gradient (svd.go:112, reg aside)
+        const double af = std::max(1e-12, 1.0 - static_cast<double>(lr) * pl->qdelta_curv);
+        const double ab = std::max(1e-12, 1.0 - static_cast<double>(lr));
         for (size_t x = 0; x < static_cast<size_t>(ni); ++x) {
             // the moves of 1 / merges of an epoch: every block's for a hot item, cold_every blocks' for a cold one
             const double merges = static_cast<double>(std::max(1, hp[x] >= 0 ? nb : nb / F));
             const double cp = std::max(1.0, static_cast<double>(cc[x])), n = static_cast<double>(cn[x]) / cp / merges;
             if (cp <= 1.0 || n <= 0.0) continue;
-            const double kappa = (1.0 - std::pow(a, cp * n)) / std::max(1e-300, 1.0 - std::pow(a, n));
-            w[x] = static_cast<float>(kappa / cp);
+            for (int col = 0; col < 2; ++col) {
+                const double a = col ? ab : af;
+                const double kappa = (1.0 - std::pow(a, cp * n)) / std::max(1e-300, 1.0 - std::pow(a, n));
+                w[2 * x + col] = static_cast<float>(kappa / cp);
+            }
         }
-        if (c.qw.n < n1) c.qw.alloc(n1);
-        c.qw.upload(w.data(), n1, s);
+        if (c.qw.n < 2 * n1) c.qw.alloc(2 * n1);
+        c.qw.upload(w.data(), 2 * n1, s);
         RS_HIP(hipStreamSynchronize(s));  // w dies with this scope
         c.qw_lr = lr;
         c.qw_curv = pl->qdelta_curv;
@@ -1109,7 +1115,7 @@ void epochs_qdelta(rs_svd_plan* pl, int32_t n_epochs, float lr, float reg, hipSt
                                c.n_hot > 0 ? c.hot_pos.p : nullptr, ph_sum, ph_dq, static_cast<int32_t>(prev_full),
                                pc ? static_cast<const void*>(dsum + ((f - 1) & 1) * wb) : nullptr,
                                pc ? static_cast<const void*>(dq + ((f - 1) & 1) * wb) : nullptr, static_cast<uint32_t>(m4),
-                               l4, ld4, fx, fx_inv);
+                               l4, ld4, fx, fx_inv, pl->k);
         }
         RS_HIP(hipGetLastError());
         char* const sum_out = full ? dsum + (f & 1) * wb : hsum + (h & 1) * wbh;
@@ -1311,7 +1317,11 @@ void group_join(rs_svd_group* g, int32_t n_blocks) {
     std::vector<int64_t> first(n), end(n);
     double total = 0.0;
     int32_t shift = 31;  // the group's fixed-point shift: the smallest of its shards' (Q rows move between them)
-    for (rs_svd_plan* pl : g->plans) shift = std::min(shift, pl->fx_shift);
+    for (rs_svd_plan* pl : g->plans) {
+        pl->own_fx_shift = pl->fx_shift;
+        pl->own_tile_wg = pl->tile_wg;
+        shift = std::min(shift, pl->fx_shift);
+    }
     for (rs_svd_plan* pl : g->plans) pl->fx_shift = shift;
     for (int r = 0; r < n; ++r) {
         const rs_svd_plan* pl = g->plans[r];
@@ -1582,6 +1592,8 @@ extern "C" int rs_svd_plan_join(rs_svd_plan* pl, const void* id, int32_t rank, i
         if (pl->write_back != RS_SGD_WB_TILE)
             return rs::set_error(pl->ctx, RS_ERR_UNSUPPORTED, "the item-sharded epoch runs the tile schedule");
         rs::plan_sync_last(pl);
+        pl->own_fx_shift = pl->fx_shift;
+        pl->own_tile_wg = pl->tile_wg;
         auto c = std::make_shared<ShardComm>();
         c->rank = rank;
         c->nranks = n_ranks;
@@ -1658,11 +1670,27 @@ extern "C" int rs_svd_plan_join(rs_svd_plan* pl, const void* id, int32_t rank, i
     });
 }
 
+namespace rs {
+// A plan leaves its group: the communicator goes, and the fixed-point shift (lowered to the group's smallest) and the
+// launch grid (workgroups left to RCCL) return to the plan's own; the tiles keep the group's blocks until the next
+// rs_svd_plan_set_user_blocks.
+void plan_unjoin(rs_svd_plan* pl) {
+    pl->shard.reset();
+    if (pl->own_fx_shift >= 0) pl->fx_shift = pl->own_fx_shift;
+    if (pl->own_tile_wg >= 0 && pl->tile_wg != pl->own_tile_wg) {
+        pl->tile_wg = pl->own_tile_wg;
+        pl->tiles_built = false;  // rebuilt on the plan's own grid when it next runs
+        pl->tiles_deferred = true;
+    }
+    pl->own_fx_shift = pl->own_tile_wg = -1;
+}
+}  // namespace rs
+
 extern "C" int rs_svd_plan_leave(rs_svd_plan* pl) {
     if (!pl) return rs::set_error(nullptr, RS_ERR_INVALID, "plan is NULL");
     return rs_guard(pl->ctx, [&]() -> int {
         rs::plan_sync_last(pl);
-        pl->shard.reset();  // the tiles keep the group's blocks until the next rs_svd_plan_set_user_blocks
+        rs::plan_unjoin(pl);
         return RS_OK;
     });
 }
@@ -1699,7 +1727,7 @@ extern "C" int rs_svd_group_create(rs_svd_plan* const* plans, int32_t n, int32_t
     if (st != RS_OK) {
         for (rs_svd_plan* pl : g->plans) {
             (void)hipSetDevice(pl->ctx->device);
-            pl->shard.reset();
+            rs::plan_unjoin(pl);
         }
         delete g;
         return st;
@@ -1749,7 +1777,7 @@ extern "C" void rs_svd_group_destroy(rs_svd_group* g) {
     for (rs_svd_plan* pl : g->plans) {
         (void)hipSetDevice(pl->ctx->device);
         if (pl->last_stream) (void)hipStreamSynchronize(pl->last_stream);
-        pl->shard.reset();
+        rs::plan_unjoin(pl);
     }
     delete g;
 }

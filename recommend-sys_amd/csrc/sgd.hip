@@ -1745,7 +1745,7 @@ static void plan_epochs_once(rs_svd_plan* pl, int32_t epochs, float lr, float re
                                n_live > 0 ? pl->done.p : nullptr, loss_on ? pl->loss_part.p : nullptr,
                                loss_on ? pl->loss_state.p : nullptr, loss_on ? pl->guard_flag.p : nullptr,
                                1.0 / (static_cast<double>(lr) * static_cast<double>(lr)),
-                               tile ? pl->gb_smooth.p : nullptr,
+                               tile && pl->gb_fold == RS_GB_FOLD_SMOOTH ? pl->gb_smooth.p : nullptr,
                                std::exp(static_cast<double>(pl->nnz) * std::log1p(-static_cast<double>(lr))));
             RS_HIP(hipGetLastError());
         }
@@ -1786,6 +1786,11 @@ static void plan_epochs_once(rs_svd_plan* pl, int32_t epochs, float lr, float re
 static void plan_epochs(rs_svd_plan* pl, int32_t epochs, float lr, float reg, hipStream_t s,
                         const std::function<void()>& under = nullptr, const std::function<void()>& after = nullptr) {
     // `after` enqueues the caller's follow-up copies (rs_svd_fit: the results' download) before the guard's wait
+    if (pl->tiles_deferred && !pl->tiles_built && pl->write_back == RS_SGD_WB_TILE) {  // (after a soft redo)
+        tile_build(pl);
+        pl->n_blocks = tile_partials(pl);
+    }
+    pl->tiles_deferred = false;
     const bool guarded = pl->guard && pl->write_back == RS_SGD_WB_TILE && epochs > 0 && pl->tiles_built;
     if (!guarded) {
         plan_epochs_once(pl, epochs, lr, reg, s);
@@ -1833,18 +1838,25 @@ static void plan_epochs(rs_svd_plan* pl, int32_t epochs, float lr, float reg, hi
         const int32_t* fl = reinterpret_cast<const int32_t*>(ck.p + 1);
         const bool bad_hard = fl[0] != 0 || !std::isfinite(g), bad = bad_hard || fl[1] != 0;
         hard = hard || bad_hard;
+        static const bool trace_check = std::getenv("RSGPU_FIT_TRACE") != nullptr;
+        if (trace_check) {  // every check: the signals and this epoch's training MSE
+            double mse = 0.0;
+            RS_HIP(hipMemcpy(&mse, pl->loss_state.p, sizeof(double), hipMemcpyDeviceToHost));
+            std::fprintf(stderr, "fit-trace check: attempt %d range %d guard %d gb %.6f training mse %.6f\n", attempt, fl[0], fl[1], g, mse);
+        }
         RS_HIP(hipMemsetAsync(pl->guard_flag.p, 0, sizeof(int32_t), s));  // (the guard's own signal is never an error)
         if (!bad || attempt == 3 || pl->tile_grid <= 1) {  // (a range flag still raised reaches the download)
             // Redos that only the guard's own signals asked for (a rising loss, a factor past the guard bound) may
-            // be false positives: the plan returns to the caller's grid and cap for its next call (rebuilt here)
-            // instead of keeping a quarter of the workgroups for good -- until such redos have come three times,
-            // or a hard signal (range flag, non-finite) came in this call, when the smaller grid stays.
+            // be false positives: the plan returns to the caller's grid and cap for its next call instead of keeping
+            // a quarter of the workgroups for good -- until such redos have come three times, or a hard signal (range
+            // flag, non-finite) came in this call, when the smaller grid stays.  The schedule is rebuilt by whatever
+            // next runs or reads it (tiles_built; rs_svd_fit's plan may never run again).
             if (attempt > 0 && !bad && !hard && ++pl->soft_refits < 3 &&
                 (pl->tile_wg != wg0 || pl->tile_run_cap != cap0)) {
                 pl->tile_wg = wg0;
                 pl->tile_run_cap = cap0;
-                tile_build(pl);
-                pl->n_blocks = tile_partials(pl);
+                pl->tiles_built = false;
+                pl->tiles_deferred = true;
             }
             return;
         }
@@ -2147,6 +2159,16 @@ extern "C" int rs_svd_plan_set_damp_concurrency(rs_svd_plan* pl, float kconc) {
     });
 }
 
+extern "C" int rs_svd_plan_set_gb_fold(rs_svd_plan* pl, int32_t mode) {
+    if (!pl) return rs::set_error(nullptr, RS_ERR_INVALID, "plan is NULL");
+    if (mode != RS_GB_FOLD_MEAN && mode != RS_GB_FOLD_SMOOTH) return rs::set_error(pl->ctx, RS_ERR_INVALID, "bad GlobalBias fold");
+    return rs_guard(pl->ctx, [&]() -> int {
+        rs::plan_sync_last(pl);
+        pl->gb_fold = mode;
+        return RS_OK;
+    });
+}
+
 // Cold runs (include/rsgpu.h, sgd_plan.hpp kRunCold): the items whose runs end in write-through stores.  Rebuilds
 // the schedule.
 extern "C" int rs_svd_plan_set_cold_store(rs_svd_plan* pl, double runs_in_flight) {
@@ -2214,6 +2236,12 @@ extern "C" int rs_svd_plan_set_guard(rs_svd_plan* pl, int32_t on) {
 extern "C" int rs_svd_plan_refits(const rs_svd_plan* pl, int32_t* n) {
     if (!pl || !n) return rs::set_error(pl ? pl->ctx : nullptr, RS_ERR_INVALID, "bad arguments");
     *n = pl->refits;
+    return RS_OK;
+}
+
+extern "C" int rs_svd_plan_fixed_point(const rs_svd_plan* pl, int32_t* shift) {
+    if (!pl || !shift) return rs::set_error(pl ? pl->ctx : nullptr, RS_ERR_INVALID, "bad arguments");
+    *shift = pl->fx_shift;
     return RS_OK;
 }
 
@@ -2443,15 +2471,6 @@ struct SvdFitCache {
     }
 };
 
-// RSGPU_FIT_DEVICE_BUILD=0: one-shot Fit builds its schedule on the host (LPT rule) -- experiments only
-static bool fit_device_build_on() {
-    static const bool on = !(std::getenv("RSGPU_FIT_DEVICE_BUILD") && std::atoi(std::getenv("RSGPU_FIT_DEVICE_BUILD")) == 0);
-    return on;
-}
-static bool fit_cache_on() {
-    static const bool on = !(std::getenv("RSGPU_FIT_CACHE") && std::atoi(std::getenv("RSGPU_FIT_CACHE")) == 0);
-    return on;
-}
 // Sets larger than this are not cached (the cache holds a 16-byte-per-rating host copy of the COO and the
 // plan's device buffers): 2^26 ratings = 1 GiB of host memory at most.
 constexpr int64_t kFitCacheMaxNnz = int64_t{1} << 26;
@@ -2496,11 +2515,11 @@ extern "C" int rs_svd_fit(rs_ctx* ctx, const rs_ratings* r, const rs_sgd_params*
             };
             const int32_t wb = p->write_back >= RS_SGD_WB_TILE && p->write_back <= RS_SGD_WB_ATOMIC ? p->write_back : RS_SGD_WB_TILE;
             auto cache = std::static_pointer_cast<rs::SvdFitCache>(ctx->svd_fit_cache);
-            const bool hit = rs::fit_cache_on() && cache && cache->matches(r, p->n_factors, wb);
+            const bool hit = cache && cache->matches(r, p->n_factors, wb);
             mark(hit ? "cache-hit" : "cache-miss");
             bool prepared = false;  // warm start done and factors packed during the device build
             if (!hit) {
-                const bool dev = wb == RS_SGD_WB_TILE && r->nnz > 0 && r->nnz <= rs::kDeviceBuildMaxNnz && rs::fit_device_build_on();
+                const bool dev = wb == RS_SGD_WB_TILE && r->nnz > 0 && r->nnz <= rs::kDeviceBuildMaxNnz;
                 auto old = dev ? cache : nullptr;  // the device path recycles the old plan's buffers
                 ctx->svd_fit_cache.reset();          // (otherwise they are freed first)
                 cache = std::make_shared<rs::SvdFitCache>();
@@ -2531,7 +2550,7 @@ extern "C" int rs_svd_fit(rs_ctx* ctx, const rs_ratings* r, const rs_sgd_params*
             }
             // the cache's copy of the COO (compared by the next call) is made while the first epochs run
             auto keep_coo = [&] {
-                if (hit || !rs::fit_cache_on() || r->nnz > rs::kFitCacheMaxNnz) return;
+                if (hit || r->nnz > rs::kFitCacheMaxNnz) return;
                 const size_t n = static_cast<size_t>(r->nnz);
                 cache->nnz = r->nnz;
                 cache->n_users = r->n_users;

@@ -524,7 +524,6 @@ void ordered_epochs(const int32_t* users, const int32_t* items, const float* rat
         throw std::invalid_argument("ORDERED mode: factor matrices of 2 GiB or more");
     if (ld > 512) throw std::invalid_argument("ORDERED mode: rows of more than 512 floats");
     const int32_t pb = static_cast<int32_t>(p_floats * 4), qb = static_cast<int32_t>(q_floats * 4);
-    const int nw = [] { const char* e = std::getenv("RSGPU_ORDERED_NW"); return e ? std::atoi(e) : 16; }();
     // diagnostics: RSGPU_ORDERED_PROF=1 prints wave 0's cycles per phase of a batch
     const bool diag = [] { const char* e = std::getenv("RSGPU_ORDERED_PROF"); return e && std::atoi(e) != 0; }();
     DevBuf<uint64_t> dprof(diag ? 8 : 0);
@@ -555,8 +554,7 @@ void ordered_epochs(const int32_t* users, const int32_t* items, const float* rat
         else if (ld <= 256) go(integral_constant<int, 2>{}, nw_c);
         else go(integral_constant<int, 4>{}, nw_c);
     };
-    if (nw == 8) by_h(integral_constant<int, 8>{});
-    else by_h(integral_constant<int, 16>{});
+    by_h(integral_constant<int, 16>{});
     }
     RS_HIP(hipGetLastError());
     if (diag) {
@@ -566,7 +564,7 @@ void ordered_epochs(const int32_t* users, const int32_t* items, const float* rat
         const double nb = static_cast<double>(n_batches) * epochs;
         std::fprintf(stderr, "ordered-prof %s NW=%d batches=%.0f cycles/batch: forward+dot %.0f drain+barrier1 %.0f "
                      "prefetch+scan %.0f update+store %.0f barrier2 %.0f\n", ld <= 128 && gnw > 0 ? "group" : "wave",
-                     ld <= 128 && gnw > 0 ? gnw : nw, nb, h[0] / nb, h[1] / nb, h[2] / nb,
+                     ld <= 128 && gnw > 0 ? gnw : 16, nb, h[0] / nb, h[1] / nb, h[2] / nb,
                      h[3] / nb, h[4] / nb);
     }
 }

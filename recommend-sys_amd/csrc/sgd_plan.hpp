@@ -26,7 +26,10 @@ namespace rs {
 // ends with plain write-through stores of its new row (an update of the same item landing in between is lost,
 // with probability about R_i) instead of the memory-side atomic unit, which bounds the epoch.
 constexpr int32_t kRunCold = 0x40000000, kRunItemMask = 0x3FFFFFFF;  // item ids below 2^30
-constexpr double kColdRunsDefault = 0.0;
+// 0.05 (round 6, scripts/experiments/exp_cold_store.py, profiles/r06/): configs[4]'s whole set 0.588 -> 0.419 s per
+// epoch and its 8-shard QDELTA fit 0.954 -> 0.766 s on one GPU, held-out RMSE unchanged (0.6081 / 0.6174 after 10
+// epochs against 0.6079 / 0.6172); the ML-1M epoch unchanged (152 us, 0.6684); 0.2 costs ML-1M 0.003 of RMSE.
+constexpr double kColdRunsDefault = 0.05;
 // items with fewer ratings than this are cold (0: none); the host and the device schedule builds both use it
 inline int64_t cold_degree(double cold_runs, int64_t nnz, int32_t grid, int32_t waves) {
     if (!(cold_runs > 0.0) || nnz <= 0 || grid <= 0 || waves <= 0) return 0;
@@ -60,6 +63,7 @@ struct rs_svd_plan {
     rs::DevBuf<float> P, Q;  // bias in column k
     rs::DevBuf<double> gb, partial;
     rs::DevBuf<double> gb_smooth;  // tile epochs: per (workgroup, wave) the smoothed GlobalBias fold's {sum b, sum (1 - a)}
+    int32_t gb_fold = RS_GB_FOLD_SMOOTH;  // how a single-GPU tile epoch folds GlobalBias (rs_svd_plan_set_gb_fold)
     rs::DevBuf<float> uw;  // per-user share of this shard (multi-GPU delta mode)
     // hot replicas: most-rated items and copies each (0: none).  Default 256 x 8, measured on the
     // ML-1M shape (scripts/experiments/exp_replicas.py): epoch 760 -> 585 us, held-out RMSE unchanged
@@ -171,7 +175,8 @@ struct rs_svd_plan {
     rs::DevBuf<double> loss_state;             // last epoch's training MSE (0: none since the factors were set)
     rs::DevBuf<int32_t> guard_flag;            // the guard's own signals (a rising loss, |p| or |q| >= guard bound): redo, not an error
     int32_t soft_refits = 0;                   // redos the guard's own signals alone asked for (the grid is restored after them)
-    int32_t grid_wg0 = -1, grid_cap0 = -1;     // the caller's tile_wg / tile_run_cap before a soft redo shrank them
+    bool tiles_deferred = false;               // a soft redo restored the caller's grid: rebuilt by the next epochs call
+    int32_t own_fx_shift = -1, own_tile_wg = -1;  // while joined: the plan's own shift and grid (rs_svd_plan_leave restores them)
     // Fixed-point scale of the FAST schedules: P / Q values are held as int32 round(v * 2^fx_shift)
     // while a call runs, so |v| < 2^(31 - fx_shift).  The shift follows the ratings (fx_shift_for): 24 (|v| < 128)
     // on star scales, fewer bits of fraction where the biases must reach further (1-100 ratings: 20, |v| < 2048).

@@ -879,8 +879,8 @@ void build_tile_host(const rs_svd_plan* pl, int32_t u_begin, int32_t u_end, int3
         L.runs.push_back(make_int2(-1, rec));  // sentinel
     };
     auto parallel_tiles = [&](auto&& fn, bool with_slot) {
-        static const int want_th = std::getenv("RSGPU_TILE_THREADS") ? std::atoi(std::getenv("RSGPU_TILE_THREADS")) : 16;
-        const int nth = static_cast<int>(std::min<size_t>(static_cast<size_t>(std::max(1, want_th)), std::max<size_t>(1, nt / 8)));
+        constexpr size_t kBuildThreads = 16;
+        const int nth = static_cast<int>(std::min<size_t>(kBuildThreads, std::max<size_t>(1, nt / 8)));
         parallel_run(nth, [&](int32_t c) {  // (pooled threads, ingest.cpp)
             std::vector<int32_t> slot(with_slot ? static_cast<size_t>(std::max(1, pl->n_items)) : 0, -1);
             for (size_t t = static_cast<size_t>(c); t < nt; t += static_cast<size_t>(nth)) fn(t, slot);
@@ -962,7 +962,14 @@ void build_tile_host(const rs_svd_plan* pl, int32_t u_begin, int32_t u_end, int3
 // no floor -- cap 8 diverged there --; ML-1M: no floor.  What the model does not foresee, the divergence
 // guard (plan_epochs, sgd.hip) catches: an epoch whose training loss rises, or a call that leaves the
 // fixed-point range, is redone on half the workgroups with half the run cap.
+// Round 6: the cap is at least kRunCapFloor.  1m_k100_r32 (tests/stability_sets.py: 942k ratings, hottest item
+// 1.12 %, k = 100) takes the whole grid (its tiles need the LDS of 256 workgroups), where the model gives 4: the
+// guard redid a call in 5 of 6 runs (training MSE up 12-30 % in one epoch, NaN with the guard off), at caps 3 / 4
+// too, never on 176 / 192 workgroups (model 6 / 5).  Caps 8 and 12 took every 1M-rating stability set to 0 redos in
+// every run, 10-14 % faster per epoch (fewer run-end row atomics); 8 keeps the 10-epoch held-out RMSE within
+// 0.001 of the automatic cap's where 12 loses 0.005 on 1m_k100_hot (profiles/r06/stability_cap_floor.log).
 constexpr double kStaleTarget = 100.0;
+constexpr int64_t kRunCapFloor = 8;
 constexpr double kAtomicLineNs = 4.9, kRatingLineNs = 0.176 / 7.0, kLaunchFloorNs = 20000.0;
 int32_t auto_run_cap(const rs_svd_plan* pl, int32_t grid, int32_t waves) {
     if (waves <= 1 || pl->nnz == 0) return 0;
@@ -982,7 +989,7 @@ int32_t run_cap_rule(int64_t nnz, int64_t dmax, int32_t grid, int32_t waves, int
     const double t_rest = static_cast<double>(nnz) * lines * kRatingLineNs + kLaunchFloorNs;
     const bool row_bound = t_hot > 2.0 * t_rest;
     const int64_t c_hot = row_bound ? (dmax * 256 + nnz - 1) / nnz : 0;
-    return c >= 1e6 ? 0 : static_cast<int32_t>(std::max<int64_t>({2, static_cast<int64_t>(c), c_hot}));
+    return c >= 1e6 ? 0 : static_cast<int32_t>(std::max<int64_t>({kRunCapFloor, static_cast<int64_t>(c), c_hot}));
 }
 
 int32_t device_cus(const rs_ctx* ctx) {

@@ -651,12 +651,10 @@ extern "C" int rs_svdpp_fit(rs_ctx* ctx, const rs_ratings* r, const rs_sgd_param
         // run, 128-320 give 0.6463-0.6475 on every run against the sequential restatement's 0.6470
         // (heaviest-first order) and 0.6493 (user-id order), at the same epoch time (1.27 ms: the
         // heaviest user's chain bounds it); profiles/r03_experiments/pp_accuracy.log.
-        // RSGPU_PP_BLOCKS overrides (experiments)
         int cus = 256;
         if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, ctx->device) != hipSuccess || cus <= 0)
             cus = 256;
-        int32_t cap = cus;
-        if (const char* env = std::getenv("RSGPU_PP_BLOCKS")) cap = std::max(1, std::atoi(env));
+        const int32_t cap = cus;
         // users with >= heavy_min ratings (LPT order: the first n_heavy work items) run on the heavy
         // blocks, n_hblocks of them striding over those users
         int32_t n_heavy = 0;
@@ -683,8 +681,7 @@ extern "C" int rs_svdpp_fit(rs_ctx* ctx, const rs_ratings* r, const rs_sgd_param
         rs::DevBuf<int32_t> dwork(std::max<size_t>(1, order.size()));
         dwork.upload(order.data(), order.size(), s);
         std::vector<float> hP, hQ, hY;
-        bool fx = true;  // fixed-point Q and Y (see pp_ld); RSGPU_PP_FX=0: fp32 float atomics
-        if (const char* env = std::getenv("RSGPU_PP_FX")) fx = std::atoi(env) != 0;
+        const bool fx = true;  // fixed-point Q and Y (see pp_ld)
         // the fixed-point scale from the ratings' spread (fx_shift_for, sgd_plan.hpp: 2^-24 on star scales)
         double lo = 0.0, hi = 0.0, sum = 0.0;
         for (int64_t t = 0; t < r->nnz; ++t) {

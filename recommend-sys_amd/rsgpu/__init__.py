@@ -25,6 +25,7 @@ SIM_COSINE, SIM_MSD, SIM_PEARSON = 0, 1, 2
 TIE_GO_SORT, TIE_STABLE = 0, 1  # KNN.Predict tie order (rs_knn_plan_set_tie_order)
 DEV_SLOPE_ONE = 3  # rs_knn_sims kind: SlopeOne deviation matrix (slope_one.go:64-92)
 EXCHANGE_ROTATE, EXCHANGE_AVERAGE, EXCHANGE_ROTATE_Q, EXCHANGE_QDELTA = 0, 1, 2, 3  # multi-GPU exchange (rsgpu.h)
+GB_FOLD_MEAN, GB_FOLD_SMOOTH = 0, 1  # rs_svd_plan_set_gb_fold
 FAULT_DIVERGE = -2  # rs_svd_plan_inject_fault: perturb a replica before the consistency check (rsgpu.h)
 TILE_RULE_LPT, TILE_RULE_FILL, TILE_RULE_FILL_DEVICE = 0, 1, 2  # how users are cut into tiles (rsgpu.h)
 
@@ -45,11 +46,11 @@ HEADER_SYMBOLS = (
     "rs_svd_plan_set_item_weights", "rs_svd_plan_epoch_qdelta", "rs_svd_plan_apply_qdelta",
     "rs_svd_plan_set_hot_replicas", "rs_svd_plan_set_fixed_q", "rs_svd_plan_set_tiles",
     "rs_svd_plan_set_tile_claim", "rs_svd_plan_tile_order", "rs_svd_plan_tile_clocks",
-    "rs_svd_plan_set_tile_rule", "rs_svd_plan_tile_rule", "rs_svd_plan_set_guard", "rs_svd_plan_refits", "rs_svd_plan_schedule_digest", "rs_fit_schedule_digest",
+    "rs_svd_plan_set_tile_rule", "rs_svd_plan_tile_rule", "rs_svd_plan_set_guard", "rs_svd_plan_refits", "rs_svd_plan_fixed_point", "rs_svd_plan_schedule_digest", "rs_fit_schedule_digest",
     "rs_comm_unique_id", "rs_svd_plan_join", "rs_svd_plan_epochs_sharded", "rs_svd_plan_leave",
     "rs_svd_plan_set_user_blocks", "rs_svd_group_create", "rs_svd_group_epochs", "rs_svd_group_destroy",
     "rs_item_shards", "rs_svd_fit_multi", "rs_tile_schedule_host", "rs_svd_plan_set_exchange", "rs_svd_plan_set_qdelta_wire", "rs_svd_plan_set_qdelta_split",
-    "rs_svd_plan_set_qdelta_curvature", "rs_svd_plan_set_damp_concurrency", "rs_svd_plan_set_cold_store",
+    "rs_svd_plan_set_qdelta_curvature", "rs_svd_plan_set_damp_concurrency", "rs_svd_plan_set_cold_store", "rs_svd_plan_set_gb_fold",
     "rs_comm_info", "rs_rotation_step", "rs_svd_plan_shard_info", "rs_svd_plan_qdelta_info", "rs_svd_plan_inject_fault",
     "rs_svd_plan_time_blocks", "rs_knn_plan_set_tie_order", "rs_fit_refits", "rs_open_r",
     "rs_svd_plan_set_hot_split",
@@ -157,6 +158,7 @@ def lib():
             "rs_svd_plan_set_tile_rule": (C.c_int, [_vp, _i32]),
             "rs_svd_plan_set_guard": (C.c_int, [_vp, _i32]),
             "rs_svd_plan_refits": (C.c_int, [_vp, C.POINTER(_i32)]),
+            "rs_svd_plan_fixed_point": (C.c_int, [_vp, C.POINTER(_i32)]),
             "rs_svd_plan_tile_rule": (C.c_int, [_vp, C.POINTER(_i32)]),
             "rs_svd_plan_schedule_digest": (C.c_int, [_vp, C.POINTER(C.c_uint64)]),
             "rs_fit_schedule_digest": (C.c_int, [_vp, C.POINTER(C.c_uint64), C.POINTER(_i32)]),
@@ -186,6 +188,7 @@ def lib():
             "rs_svd_plan_set_qdelta_curvature": (C.c_int, [_vp, C.c_double]),
             "rs_svd_plan_set_damp_concurrency": (C.c_int, [_vp, C.c_float]),
             "rs_svd_plan_set_cold_store": (C.c_int, [_vp, C.c_double]),
+            "rs_svd_plan_set_gb_fold": (C.c_int, [_vp, _i32]),
             "rs_svd_plan_inject_fault": (C.c_int, [_vp, _i32]),
             "rs_svd_plan_time_blocks": (C.c_int, [_vp, _flt, _flt, _vp, _i32]),
             "rs_knn_plan_set_tie_order": (C.c_int, [_vp, _i32]),
@@ -513,6 +516,10 @@ class SvdPlan:
         """RS_EXCHANGE_QDELTA's hot / cold split (rs_svd_plan_set_qdelta_split)."""
         self.ctx.check(lib().rs_svd_plan_set_qdelta_split(self.h, float(hot_ratings), int(cold_every)))
 
+    def set_gb_fold(self, mode):
+        """GB_FOLD_SMOOTH (default) or GB_FOLD_MEAN for single-GPU tile epochs (rs_svd_plan_set_gb_fold)."""
+        self.ctx.check(lib().rs_svd_plan_set_gb_fold(self.h, int(mode)))
+
     def set_cold_store(self, runs_in_flight):
         """Cold runs end in write-through stores (rs_svd_plan_set_cold_store; 0 turns it off)."""
         self.ctx.check(lib().rs_svd_plan_set_cold_store(self.h, float(runs_in_flight)))
@@ -586,6 +593,12 @@ class SvdPlan:
     def refits(self):
         v = _i32(0)
         self.ctx.check(lib().rs_svd_plan_refits(self.h, C.byref(v)))
+        return v.value
+
+    def fixed_point(self):
+        """The fixed-point shift S of the FAST kernels (rs_svd_plan_fixed_point)."""
+        v = _i32(0)
+        self.ctx.check(lib().rs_svd_plan_fixed_point(self.h, C.byref(v)))
         return v.value
 
     def tile_rule(self):

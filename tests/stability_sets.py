@@ -35,7 +35,7 @@ CASES = {
 }
 
 
-def run(ctx, name, claim, cap, log, wg=0):
+def run(ctx, name, claim, cap, log, wg=0, damp=0.0, gb_fold=None, cold=None, ring=0):
     U, I, deg, zs, k, ep, with_oracle = CASES[name]
     t0 = time.time()
     s = rsgpu.Synth(U, I, mean_deg=deg, zipf_s=zs, seed=20250901, n_threads=16)
@@ -51,8 +51,14 @@ def run(ctx, name, claim, cap, log, wg=0):
     hot = int(np.bincount(cols, minlength=I).max())
     plan = ctx.svd_plan_csr(U, I, rp, cols, vals, k)
     plan.set_tile_claim(claim)
-    if cap or wg:
-        plan.set_tiles(workgroups=wg, run_cap=cap)
+    if cap or wg or ring:
+        plan.set_tiles(workgroups=wg, run_cap=cap, ring=ring)
+    if gb_fold is not None:
+        plan.set_gb_fold(gb_fold)
+    if cold is not None:  # (experiment) cold runs' write-through (rs_svd_plan_set_cold_store)
+        plan.set_cold_store(cold)
+    if damp:  # (experiment) the damped kernel with R = deg x damp runs in flight (rs_svd_plan_set_damp_concurrency)
+        plan.set_damp_concurrency(damp)
     plan.init_normal(0.0, 0.1, seed=1)
     gb0 = float(np.mean(vals, dtype=np.float64))
     plan.upload(gb=gb0)
@@ -159,12 +165,25 @@ def run_diag(ctx, name, wg=0, epochs=None, log=print):
     plan.close()
 
 
+def nnz_of(name):
+    """the training ratings of a case (95 % of the generated set)"""
+    U, I, deg, zs, k, ep, _ = CASES[name]
+    s = rsgpu.Synth(U, I, mean_deg=deg, zipf_s=zs, seed=20250901, n_threads=16)
+    n = s.nnz
+    s.close()
+    return 0.95 * n
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("cases", nargs="*", default=list(CASES))
     ap.add_argument("--claim", type=int, default=4)
     ap.add_argument("--cap", type=int, default=0)
     ap.add_argument("--wg", type=int, default=0, help="workgroups (0: one per CU)")
+    ap.add_argument("--gb-fold", type=int, default=None, help="0 mean, 1 smoothed (default: library)")
+    ap.add_argument("--ring", type=int, default=0, help="q rows prefetched per wave (0: library)")
+    ap.add_argument("--cold", type=float, default=None, help="cold-store runs in flight (default: library)")
+    ap.add_argument("--damp", type=float, default=0.0, help="force the damped kernel, R = deg x DAMP x nnz (natural: grid x waves)")
     ap.add_argument("--fit", action="store_true", help="through rs_svd_fit (the guarded Go drop-in)")
     ap.add_argument("--diag", action="store_true", help="guard off, per-epoch extremes (run_diag)")
     args = ap.parse_args()
@@ -175,7 +194,8 @@ def main():
         elif args.fit:
             run_fit(ctx, c, lambda m: print(m, flush=True))
         else:
-            run(ctx, c, args.claim, args.cap, lambda m: print(m, flush=True), args.wg)
+            run(ctx, c, args.claim, args.cap, lambda m: print(m, flush=True), args.wg, damp=args.damp / nnz_of(c) if args.damp else 0.0,
+                gb_fold=args.gb_fold, cold=args.cold, ring=args.ring)
     ctx.close()
 
 

@@ -660,3 +660,31 @@ def test_one_librccl_mapped(ctx):
     libs = {ln.split()[-1] for ln in maps if "librccl" in ln and ln.split()[-1].startswith("/")}
     assert len(libs) == 1, libs
     assert os.path.realpath(path) == os.path.realpath(libs.pop()) and ver > 0
+
+
+def test_group_lowers_the_shift_and_destroy_restores_it(ctx, ml100k):
+    """a group runs at its shards' smallest fixed-point shift (Q rows move between them as words); a
+    star-scale shard (2^-24) grouped with a 1-100 one (2^-20) runs at 2^-20 and gets its own 2^-24 back when the
+    group is destroyed, and then trains on its own (finite, the guard not redoing)."""
+    f = folds(*ml100k)[0]
+    n = 30000
+    u, i, r, nu, ni = f.iu[:n], f.ii[:n], f.r[:n], f.nu, f.ni
+    k = 16
+    rng = np.random.default_rng(5)
+    P0, Q0 = rng.normal(0, 0.1, (nu, k)), rng.normal(0, 0.1, (ni, k))
+    lo = i < ni // 2
+    stars = ctx.svd_plan(rsgpu.Ratings(u[lo], i[lo], r[lo], nu, ni), k)
+    wide = ctx.svd_plan(rsgpu.Ratings(u[~lo], i[~lo], 20.0 * r[~lo], nu, ni), k)
+    assert (stars.fixed_point(), wide.fixed_point()) == (24, 20)
+    for pl in (stars, wide):
+        pl.upload(P0, Q0, np.zeros(nu), np.zeros(ni), 3.5)
+    g = rsgpu.SvdGroup([stars, wide], n_blocks=2)
+    assert (stars.fixed_point(), wide.fixed_point()) == (20, 20)
+    g.close()
+    assert (stars.fixed_point(), wide.fixed_point()) == (24, 20)
+    stars.upload(P0, Q0, np.zeros(nu), np.zeros(ni), 3.5)
+    stars.epochs(2)
+    P, Q, bu, bi, gb = stars.download()
+    assert np.isfinite(P).all() and np.isfinite(Q).all() and stars.refits() == 0
+    stars.close()
+    wide.close()
