@@ -1,8 +1,9 @@
 """Host-driven multi-GPU building blocks over torch.distributed (backend "nccl" = RCCL over xGMI on ROCm).
 
 The library's own multi-GPU fit (csrc/multi.hip: rs_svd_plan_join / rs_svd_plan_epochs_sharded,
-rs_svd_fit_multi) runs the exact stratum rotation with its own RCCL communicator and is what bench.py
-and a Go host use.  This module keeps round 2's AVERAGE protocol as a host loop around the delta
+rs_svd_fit_multi) runs with its own RCCL communicator and is what bench.py and a Go host use: the exact
+stratum rotation over item shards, or -- where the user factors are the large matrix, configs[4] --
+user ranges with the item moves merged by the QDELTA all-reduce.  This module keeps round 2's AVERAGE protocol as a host loop around the delta
 C-ABI (ItemShardedStep: every rank's shard epoch in delta mode, the count-weighted user deltas and the
 global-bias sum all-reduced, the same sum applied on every rank), its user-sharded dual
 (UserShardedStep), and the KNN part split.
