@@ -498,7 +498,8 @@ bool tile_build_device(rs_svd_plan* pl) {
     pl->n_tiles = T;
     pl->tile_grid = std::max(1, std::min(grid0, T));
     {
-        const int64_t dcold = ni < kRunCold ? cold_degree(pl->cold_runs, n, pl->tile_grid, nw) : 0;
+        const int64_t dcold = cold_degree_used(pl->cold_runs, n, ni, pl->tile_grid, nw);
+        pl->tile_cold = dcold > 0;
         if (dcold > 0 && h[4] > 0)
             hipLaunchKernelGGL(cold_runs_kernel, dim3(blocks_for(h[4])), dim3(kB), 0, s, pl->t_runs.p, static_cast<int64_t>(h[4]),
                                w.deg_i, ni, dcold);

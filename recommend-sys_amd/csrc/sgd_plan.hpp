@@ -35,6 +35,14 @@ inline int64_t cold_degree(double cold_runs, int64_t nnz, int32_t grid, int32_t 
     if (!(cold_runs > 0.0) || nnz <= 0 || grid <= 0 || waves <= 0) return 0;
     return static_cast<int64_t>(std::ceil(cold_runs * static_cast<double>(nnz) / (static_cast<double>(grid) * waves)));
 }
+// The schedule marks cold runs, and the launch takes the kernel variant with the stores, only where the mean item
+// is cold (dcold >= nnz / n_items): the store path costs the ML-1M epoch 8 % even with no run marked (147 -> 159 us:
+// one more exit per run; profiles/r06/k1_cold_variant_cost.log), and there runs of cold items are few.  configs[4]
+// (whole set and QDELTA shards) is far inside the rule, ML-1M and the 1M-rating stability sets far outside it.
+inline int64_t cold_degree_used(double cold_runs, int64_t nnz, int32_t n_items, int32_t grid, int32_t waves) {
+    const int64_t d = n_items < kRunCold ? cold_degree(cold_runs, nnz, grid, waves) : 0;
+    return d > 0 && d * static_cast<int64_t>(n_items) >= nnz ? d : 0;
+}
 }  // namespace rs
 
 struct rs_svd_plan {
@@ -119,6 +127,7 @@ struct rs_svd_plan {
     // runs in flight on average -- end their runs with write-through stores of the new row instead of memory-side
     // atomics (header bit kRunCold); 0 turns it off (rs_svd_plan_set_cold_store)
     double cold_runs = rs::kColdRunsDefault;
+    bool tile_cold = false;  // the schedule marks cold runs (rs::cold_degree_used): the launch takes the store variant
     float damp_kconc = 0.f;            // test hook (rs_svd_plan_set_damp_concurrency): > 0 forces the damped kernel with
                                        // runs in flight R = deg x damp_kconc instead of deg x workgroups x waves / nnz
     int32_t t_n_split = 0;
@@ -152,7 +161,10 @@ struct rs_svd_plan {
     int32_t qdelta_wire = 16;               // QDELTA: bits per item move on the wire (16: fp16, 32: int32 fixed point)
     double qdelta_hot = 4.0;                // QDELTA: ratings per rank and block that make an item hot (<= 0: all hot)
     int32_t qdelta_cold_every = 2;          // QDELTA: most blocks between a cold item's merges (multi.hip kQdelta*)
-    double qdelta_curv = 1.0;               // QDELTA: curvature of the merge weights' contraction, a = 1 - lr x this
+    // QDELTA: curvature of the factor columns' merge weights, a = 1 - lr x this (the bias column: 1).  configs[4], 8
+    // shards, 10 / 20 epochs against the whole-set fit's 0.6081 / 0.5901 (profiles/r06/config4_qdelta_curvature*.log):
+    // 1 -> 0.6174 / 0.5918, 0.5 -> 0.6147, 0.25 -> 0.6127 / 0.5910, 0.1 left the fixed-point range
+    double qdelta_curv = 0.25;
     int32_t fault_sub_epoch = -1;  // test hook (rs_svd_plan_inject_fault): the next sharded call throws there
     // how tiles are formed (rs_svd_plan_set_tile_rule): RS_TILE_RULE_LPT (host: LPT by ratings + cost
     // refinement), RS_TILE_RULE_FILL (host: users by degree dealt boustrophedon), RS_TILE_RULE_FILL_DEVICE

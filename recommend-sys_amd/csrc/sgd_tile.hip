@@ -95,7 +95,7 @@ __device__ __forceinline__ int32_t cvt_rpi(float x) {
 // headers / first record window are read after the chunk's first / second run, so no LDS round trip
 // waits on the critical path.  With one wave the claims come in queue order: the visit order is the
 // queue, as rs_svd_plan_tile_order exports it.
-template <int E, int NW, int RQ, int CH, int DIAG = 0, bool DAMP = false>
+template <int E, int NW, int RQ, int CH, int DIAG = 0, bool DAMP = false, bool COLD = false>
 __global__ __launch_bounds__(NW * 64) void svd_epoch_tile_kernel(
     const int4* __restrict__ tiles, int32_t n_tiles, const int2* __restrict__ tile_users,
     const int32_t* __restrict__ streams, const int2* __restrict__ runs, const int2* __restrict__ recs,
@@ -324,7 +324,7 @@ __global__ __launch_bounds__(NW * 64) void svd_epoch_tile_kernel(
             const int32_t row = item >= 0 ? (item & kRunItemMask) * (ldm * 4) : -1;
             // a cold item's run (header bit kRunCold, sgd_plan.hpp): hardly any other run of the item is in flight, so
             // the new row is written through with plain sc1 stores instead of memory-side atomics (round 6)
-            const bool cold = item >= 0 && (item & kRunCold) != 0;
+            const bool cold = COLD && item >= 0 && (item & kRunCold) != 0;
             bool damp = false;  // wave-uniform: the common path keeps its exact integer delta and no extra work
             float wq = 1.f, wb = 1.f;
             if (hot) {
@@ -1206,7 +1206,8 @@ void tile_build(rs_svd_plan* pl) {
     std::vector<int32_t> deg(static_cast<size_t>(std::max(1, pl->n_items)), 0);  // the hot-run damping's degrees
     for (int32_t c : pl->h_cols) deg[c]++;
     {  // cold runs: the header bit (sgd_plan.hpp kRunCold; the device build marks them the same way)
-        const int64_t dcold = pl->n_items < kRunCold ? cold_degree(pl->cold_runs, pl->nnz, pl->tile_grid, pl->tile_waves) : 0;
+        const int64_t dcold = cold_degree_used(pl->cold_runs, pl->nnz, pl->n_items, pl->tile_grid, pl->tile_waves);
+        pl->tile_cold = dcold > 0;
         if (dcold > 0)
             for (int2& r : th.runs)
                 if (r.x >= 0 && r.x < pl->n_items && deg[r.x] < dcold) r.x |= kRunCold;
@@ -1280,9 +1281,9 @@ struct TileRange {  // tiles [t0, t1) into dP rows of stride ldd (delta mode), g
     bool smooth = false;  // write the smoothed GlobalBias fold's sums (pl->gb_smooth; single-GPU epochs)
 };
 
-template <int E, int NW, int RQ, int CH, int DIAG = 0, bool DAMP = false>
+template <int E, int NW, int RQ, int CH, int DIAG = 0, bool DAMP = false, bool COLD = false>
 static void tile_launch_t(rs_svd_plan* pl, float lr, float reg, hipStream_t s, float* dP, const TileRange& tr) {
-    auto kern = svd_epoch_tile_kernel<E, NW, RQ, CH, DIAG, DAMP>;
+    auto kern = svd_epoch_tile_kernel<E, NW, RQ, CH, DIAG, DAMP, COLD>;
     static bool attr = false;  // per instantiation
     if (!attr) {
         RS_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(kern),
@@ -1335,9 +1336,13 @@ static void tile_launch_r(rs_svd_plan* pl, float lr, float reg, hipStream_t s, f
             if (want >= 3) return tile_launch_t<E, NW, 4, 8>(pl, lr, reg, s, dP, tr);
             if (pl->tile_claim >= 8) return tile_launch_t<E, NW, 2, 8>(pl, lr, reg, s, dP, tr);
         }
-        // the default claims (4 runs, ring 2), with the hot-run damping where the schedule asks for it
-        return (pl->tile_damp || pl->damp_kconc > 0.f) ? tile_launch_t<E, NW, 2, 4, 0, true>(pl, lr, reg, s, dP, tr)
-                             : tile_launch_t<E, NW, 2, 4>(pl, lr, reg, s, dP, tr);
+        // the default claims (4 runs, ring 2), with the hot-run damping where the schedule asks for it, or the cold
+        // runs' stores where it marks them (a damped schedule's cold runs take the atomics)
+        if (pl->tile_damp || pl->damp_kconc > 0.f) return tile_launch_t<E, NW, 2, 4, 0, true>(pl, lr, reg, s, dP, tr);
+        if constexpr (NW == 16 || NW == 1) {  // (the library's waves; one wave: the exactness tests)
+            if (pl->tile_cold) return tile_launch_t<E, NW, 2, 4, 0, false, true>(pl, lr, reg, s, dP, tr);
+        }
+        return tile_launch_t<E, NW, 2, 4>(pl, lr, reg, s, dP, tr);
     }
     // the host-dealt schedule (round 3; tile_claim = 0): rings 2 and 4, and 3 / 6 / 8 / 12 for E = 2
     if constexpr (E == 2) {

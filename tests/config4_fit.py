@@ -87,7 +87,7 @@ def parse(argv=None):
     ap.add_argument("--wire", type=int, default=16, choices=[16, 32], help="QDELTA moves on the wire: fp16 or int32")
     ap.add_argument("--hot", type=float, default=None, help="QDELTA hot threshold, ratings per rank and block")
     ap.add_argument("--cold-every", type=int, default=None, help="QDELTA most blocks between a cold item's merges")
-    ap.add_argument("--curv", type=float, default=None, help="QDELTA merge-weight curvature (library default 1)")
+    ap.add_argument("--curv", type=float, default=None, help="QDELTA factor merge-weight curvature (library default 0.25)")
     ap.add_argument("--cold", type=float, default=None, help="rs_svd_plan_set_cold_store threshold (runs in flight) "
                                                              "for the shard plans (default: library)")
     ap.add_argument("--whole-cold", type=float, default=None, help="the same for the whole-set plan")

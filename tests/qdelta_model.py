@@ -14,6 +14,7 @@ import numpy as np
 
 HOT_RATINGS = 4.0  # sgd_plan.hpp qdelta_hot default: ratings per rank and block that make an item hot
 COLD_EVERY = 2     # sgd_plan.hpp qdelta_cold_every default
+CURVATURE = 0.25   # sgd_plan.hpp qdelta_curv default: the factor columns' contraction a = 1 - lr x this
 
 
 def cold_every(merges):
@@ -30,16 +31,24 @@ def hot_items(cnt, c, merges):
     return (c > 1) & (cnt / (np.maximum(c, 1) * merges) >= HOT_RATINGS) & (cold_every(merges) > 1)
 
 
-def weights(cnt, c, lr, merges, hot):
+def weights(cnt, c, lr, merges, hot, curv=None, k=None):
     """kappa / c per item (rsgpu.h RS_EXCHANGE_QDELTA), n_i over a hot item's block or a cold item's cold_every
-    blocks."""
-    a = 1.0 - float(np.float32(lr))
+    blocks.  With k: an (items, k + 1) array, the factor columns' weights at a = 1 - lr x curv (default CURVATURE)
+    and the bias column's at a = 1 - lr (multi.hip epochs_qdelta); without: one weight per item at a = 1 - lr."""
     per = np.where(hot, merges, max(1, merges // cold_every(merges))).astype(np.float64)
-    w = np.ones(len(cnt))
     m = (c > 1) & (cnt > 0)
     n = cnt[m] / c[m] / per[m]
-    w[m] = (1.0 - a ** (c[m] * n)) / (1.0 - a ** n) / c[m]
-    return w
+
+    def kc(a):
+        w = np.ones(len(cnt))
+        w[m] = (1.0 - a ** (c[m] * n)) / (1.0 - a ** n) / c[m]
+        return w
+    lr32 = float(np.float32(lr))
+    wb = kc(1.0 - lr32)
+    if k is None:
+        return wb
+    wf = kc(max(1e-12, 1.0 - lr32 * (CURVATURE if curv is None else curv)))
+    return np.concatenate([np.repeat(wf[:, None], k, 1), wb[:, None]], 1)
 
 
 def merge_set(m, merges, hot):
@@ -58,7 +67,7 @@ class Rank:
 
     def merge(self, rows, X, w):
         """rows: the rank's [Q | b] after its block; returns them after the merge of the rows X (own moves)."""
-        own = w[:, None] * (rows - self.q0)
+        own = (w[:, None] if w.ndim == 1 else w) * (rows - self.q0)
         out = rows.copy()
         out[X] = self.q0[X] + own[X] + self.pend[X]
         self.pend[X] = 0.0

@@ -4,8 +4,9 @@ through the in-process group with the exchange bench.py's strong_scaling and rs_
 (RS_EXCHANGE_QDELTA: user ranges, 16 merges per epoch of the ranks' weighted item moves, fp16 wire), beside
 the whole set fitted by one plan from the same factors.  Reference loop: core/svd.go:92-130.
 
-About three minutes on the box (generation ~35 s, the two plans ~55 s, 2 x 10 epochs); progress lines go to
-the terminal so the run never looks silent.
+About three and a half minutes on the box (generation ~35 s, the two plans ~55 s, 2 x 20 epochs); progress lines
+go to the terminal so the run never looks silent.  Bound: within 0.005 of the whole-set fit after
+10 epochs and after 20 (a default Fit, svd.go:66); round 6 measured 0.6127 / 0.5910 against 0.6081 / 0.5901.
 """
 import numpy as np
 import pytest
@@ -19,12 +20,13 @@ def test_config4_sharded_full_size(request):
     import config4_fit as C
     tr = request.config.pluginmanager.get_plugin("terminalreporter")
     say = (lambda *a: tr.write_line("  [configs[4]] " + " ".join(str(x) for x in a))) if tr else (lambda *a: None)
-    out = C.run(C.parse(["--epochs", "10", "--exchange", "qdelta"]), say=say)
+    out = C.run(C.parse(["--epochs", "20", "--exchange", "qdelta"]), say=say)
     whole, sh = out["whole"], out["sharded"]
     assert out["nnz_train"] > 9.9e8 and out["n_users"] == 10_000_000 and out["n_items"] == 1_000_000
     assert sh["finite"] and all(np.isfinite(x) for x in sh["rmse_per_epoch"])
-    e_sh, e_whole = sh["rmse_per_epoch"][-1], whole["rmse_per_epoch"][-1]
-    say(f"held-out RMSE after 10 epochs: sharded {e_sh:.4f}, whole set {e_whole:.4f}")
-    assert e_sh < 0.95
-    assert abs(e_sh - e_whole) <= 0.01, (e_sh, e_whole)
+    for ep in (10, 20):
+        e_sh, e_whole = sh["rmse_per_epoch"][ep - 1], whole["rmse_per_epoch"][ep - 1]
+        say(f"held-out RMSE after {ep} epochs: sharded {e_sh:.4f}, whole set {e_whole:.4f}")
+        assert e_sh < 0.95
+        assert abs(e_sh - e_whole) <= 0.005, (ep, e_sh, e_whole)
     assert all(b < a for a, b in zip(sh["rmse_per_epoch"], sh["rmse_per_epoch"][1:]))  # falls every epoch

@@ -601,7 +601,7 @@ def _qd_setup(world):
     cnt = np.bincount(i, minlength=ni).astype(np.float64)
     c = np.sum([np.bincount(i[m], minlength=ni) > 0 for m in shards], 0).astype(np.float64)
     hot = QM.hot_items(cnt, c, QD_MERGES)
-    w = QM.weights(cnt, c, 0.005, QD_MERGES, hot)
+    w = QM.weights(cnt, c, 0.005, QD_MERGES, hot, k=K)
     blocks = []  # per rank: its merges' user blocks (user_block_bounds over the rank's own ratings)
     for g, m in enumerate(shards):
         bb = RQ.block_bounds(u[m], nu, QD_MERGES)
@@ -683,7 +683,7 @@ def test_gloo_qdelta_matches_single_process(world):
     rows = [x.flush(y) for x, y in zip(st, rows)]
     gb += pend_gb / len(r)
     Q, bi = rows[0][:, :K], rows[0][:, K]
-    assert any(0.0 < x < 1.0 for x in w)  # items on several ranks: weighted merges are exercised
+    assert ((0.0 < w) & (w < 1.0)).any()  # items on several ranks: weighted merges are exercised
     for rank in range(world):
         rP, rQ, rbu, rbi, rgb = res[rank]
         np.testing.assert_allclose(rP, P, atol=1e-12)

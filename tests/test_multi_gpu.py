@@ -293,7 +293,7 @@ def test_qdelta_one_wave_equals_host_model(ctx, ml100k, n_shards, merges):
     cnt = np.bincount(i, minlength=ni).astype(np.float64)
     c = np.sum([np.bincount(x[1], minlength=ni) > 0 for x in sh], 0).astype(np.float64)
     hot = QM.hot_items(cnt, c, merges)
-    w = QM.weights(cnt, c, lr, merges, hot).astype(np.float32).astype(np.float64)
+    w = QM.weights(cnt, c, lr, merges, hot, k=k).astype(np.float32).astype(np.float64)  # (the library's defaults)
     assert all(pl.qdelta_info() == (int(hot.sum()), QM.cold_every(merges)) for pl in plans)
     if merges in (2, 8):  # hot merges and full merges both move rows
         assert 0 < hot.sum() < ni
