@@ -31,7 +31,8 @@ def _maxdiff(a, b):
 def test_rccl_ranks_equal_in_process_exchange(ctx, tmp_path, case, n):
     """Real RCCL ranks (one process each, one GPU, tests/rccl_ranks.py) against the in-process group of the same
     shards: bitwise at 2 ranks for every exchange. At 3 ranks the exact wires agree to 1e-6 (the f64 GlobalBias
-    partials are summed in RCCL's order); the fp16 QDELTA wire agrees to 2e-4 (7.6e-5 measured after 2 epochs,
+    partials are summed in RCCL's order); the fp16 QDELTA wire agrees to 2e-4 (7.6e-5 measured after 2 epochs;
+    GlobalBias 2.2e-7,
     profiles/r06/): the in-process sum rounds to fp16 at every hop in ring order, but which rank starts each element's
     chain follows RCCL's run-time channel and chunk sizes, which the emulation does not know (at 2 ranks the order
     does not matter: fp16 addition commutes). Every rank still holds the same bits (the replica check)."""
@@ -47,8 +48,8 @@ def test_rccl_ranks_equal_in_process_exchange(ctx, tmp_path, case, n):
             bad = [x for x in range(4) if not np.array_equal(got[r][x], ref[r][x])]
             assert not bad and got[r][4] == ref[r][4], (case, r, bad, _maxdiff(got[r][:4], ref[r][:4]), got[r][4] - ref[r][4], log)
         else:  # (the GlobalBias partials are f64 sums in RCCL's order; the fp16 wire: see below)
-            tol = 2e-4 if case == "qdelta16" else 1e-6
-            assert _maxdiff(got[r][:4], ref[r][:4]) <= tol and abs(got[r][4] - ref[r][4]) <= 1e-9, \
+            tol, tol_gb = (2e-4, 2e-6) if case == "qdelta16" else (1e-6, 1e-9)
+            assert _maxdiff(got[r][:4], ref[r][:4]) <= tol and abs(got[r][4] - ref[r][4]) <= tol_gb, \
                 (case, r, _maxdiff(got[r][:4], ref[r][:4]), got[r][4] - ref[r][4])
 
 
