@@ -96,6 +96,8 @@ def strong_scaling(ctx, rank, world, dist, dev, stream, epochs=20, warmup=1):
     probe_u = np.repeat(np.arange(lo, hi, dtype=np.int32), np.diff(s.rowptr))[:4096]
     probe_i, probe_r = s.cols[:len(probe_u)].copy(), s.vals[:len(probe_u)].astype(np.float64)
     gen_s = time.perf_counter() - t0
+    print(f"bench: strong_scaling rank {rank}/{world}: users [{lo}, {hi}), {nnz} ratings generated in {gen_s:.1f} s",
+          file=sys.stderr, flush=True)
     plan = ctx.svd_plan_csr(n_users, n_items, rp, s.cols, s.vals, k)
     s.close()
     del rp
@@ -115,6 +117,8 @@ def strong_scaling(ctx, rank, world, dist, dev, stream, epochs=20, warmup=1):
         n_blocks = 1
         run = lambda n: plan.epochs(n, LR, REG, stream)
     setup_s = time.perf_counter() - t0
+    print(f"bench: strong_scaling rank {rank}/{world}: plan ready at {setup_s:.1f} s ({n_blocks} blocks)", file=sys.stderr,
+          flush=True)
     run(warmup)
     torch.cuda.synchronize()
     if dist:
