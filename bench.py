@@ -5,8 +5,11 @@ One step = one fast-mode SGD epoch (core/svd.go:92-130) over all 1,000,209 ratin
 in HBM (user-CSR + factors uploaded before the timed region).  N>1 GPUs: one process per GPU
 (torch.distributed for the barriers and the max-over-ranks clock); each rank owns its own item-range
 shard of ML-1M size (weak scaling, the 6040 users shared) and the library's own RCCL communicator
-(rs_svd_plan_join) runs the stratum rotation: N sub-epochs per epoch, P rank-blocks sent to the
-neighbour rank after each (north_star item sharding with the exact exchange, csrc/multi.hip).
+(rs_svd_plan_join) runs north_star's protocol: one full-shard epoch per rank, then one RCCL all-reduce of the
+count-weighted user deltas (RS_EXCHANGE_AVERAGE, one user block).  The exact stratum rotation (RS_EXCHANGE_ROTATE,
+rs_svd_fit_multi's choice for item shards) trains each rank's epoch as N x 2 user-block launches; on an ML-1M-sized
+shard those cost 144 / 299 / 916 us per epoch at 1 / 2 / 8 ranks' blocks (profiles/r06/rotate_blocks_ml1m.log), a
+launch-size cost that a weak-scaling line of ML-1M shards would mostly measure.
 
 Launch: under torch.distributed.run (WORLD_SIZE set) every process is one rank.  `--gpus N` with
 N > 1 and no WORLD_SIZE starts the N rank processes itself from a parent that makes no GPU call, and
@@ -44,7 +47,7 @@ EXCHANGE_NAMES = {0: "RS_EXCHANGE_ROTATE (stratum rotation)", 1: "RS_EXCHANGE_AV
                   3: "RS_EXCHANGE_QDELTA"}
 # what each exchange sends between the ranks (include/rsgpu.h)
 EXCHANGE_WIRE = {0: "RCCL send/recv of P rank-blocks per sub-epoch",
-                 1: "RCCL all-reduce of count-weighted user deltas per user block",
+                 1: "RCCL all-reduce of count-weighted user deltas once per epoch (one user block)",
                  2: "RCCL send/recv of Q rank-blocks and hot-item copies per sub-epoch",
                  3: "RCCL all-reduce of weighted fp16 item moves per merge"}
 
@@ -316,7 +319,8 @@ def main():
     if world > 1:  # the library's own RCCL communicator (csrc/multi.hip), id sent over torch.distributed
         uid = [rsgpu.comm_unique_id() if rank == 0 else None]
         dist.broadcast_object_list(uid, src=0)
-        plan.join(uid[0], rank, world)
+        plan.set_exchange(rsgpu.EXCHANGE_AVERAGE)  # north_star's once-per-epoch all-reduce (module docstring)
+        plan.join(uid[0], rank, world, n_blocks=1)
         comm_rank, comm_ranks, comm_exchange, comm_blocks = plan.shard_info()
         run = lambda n: plan.epochs_sharded(n, LR, REG, stream)
     else:
