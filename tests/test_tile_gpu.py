@@ -140,6 +140,33 @@ def test_cold_store_one_wave_equals_oracle(ctx, ml100k, k):
     assert _maxdiff(ref[:4], got[:4]) <= TOL and abs(ref[4] - got[4]) <= TOL
 
 
+def test_gb_fold_switch_one_wave(ctx, ml100k):
+    """rs_svd_plan_set_gb_fold: with the mean fold (GB_FOLD_MEAN, rounds 1-5 and the multi-GPU exchanges) one wave
+    equals the oracle's mean-of-moves fold (or_svd_fit_works2 compose 0), with the smoothed default compose 2; the
+    factors are the same sequential SGD either way within an epoch, the folds differ in GlobalBias."""
+    f = folds(*ml100k)[1]
+    n = 20000
+    u, i, r, nu, ni = f.iu[:n], f.ii[:n], f.r[:n], f.nu, f.ni
+    rng = np.random.default_rng(11)
+    P0, Q0 = rng.normal(0, 0.1, (nu, 32)), rng.normal(0, 0.1, (ni, 32))
+    bu0, bi0 = rng.normal(0, 0.1, nu), rng.normal(0, 0.1, ni)
+    got = {}
+    for fold in (rsgpu.GB_FOLD_MEAN, rsgpu.GB_FOLD_SMOOTH):
+        plan = ctx.svd_plan(rsgpu.Ratings(u, i, r, nu, ni), 32)
+        plan.set_tiles(workgroups=1, waves=1, target=3000)
+        plan.set_gb_fold(fold)
+        plan.upload(P0, Q0, bu0, bi0, 3.3)
+        plan.epochs(2)
+        got[fold] = plan.download()
+        cu, ci, cr = _csr(u, i, r, nu)
+        pos, off = plan.tile_order()
+        ref = O.svd_fit_works(cu[pos], ci[pos], cr[pos], off, P0, Q0, bu0, bi0, 3.3, epochs=2,
+                              compose=0 if fold == rsgpu.GB_FOLD_MEAN else 2)
+        plan.close()
+        assert _maxdiff(ref[:4], got[fold][:4]) <= TOL and abs(ref[4] - got[fold][4]) <= TOL, fold
+    assert got[rsgpu.GB_FOLD_MEAN][4] != got[rsgpu.GB_FOLD_SMOOTH][4]
+
+
 def _private_items(n_users=300, per_user=25, seed=4):
     rng = np.random.default_rng(seed)
     deg = rng.integers(1, 2 * per_user, n_users)
