@@ -657,9 +657,9 @@ __global__ __launch_bounds__(64) void svd_live_merge_fx_kernel(int32_t* __restri
 // [n_live, n_live + n_split) the split users' row merges (as svd_merge_rows_kernel), and the last
 // block the GlobalBias fold (as gb_fold_kernel, the same 256-thread tree) plus re-arming the
 // merger's done counter for the next epoch.  Columns are independent, so the arithmetic is theirs.
-// 1024 threads: the fold's partials (workgroups x waves of the SGD launch, 2816 on ML-1M) are three loads per
-// thread and a wave-shuffle sum -- 8.1 us per epoch with 256 threads and an LDS tree
-// (profiles/r05/final/bench_kernel_stats.csv), the whole epilogue of an ML-1M epoch.
+// 1024 threads: the fold's partials (one per workgroup of the tile launch since round 6, 176 on ML-1M; the
+// other schedules' per-block partials) are at most a few loads per thread and a wave-shuffle sum -- round 5's
+// 2816 per-wave partials took 7-8 us per epoch (profiles/r05/final/bench_kernel_stats.csv).
 constexpr int kEpilogueThreads = 1024;
 __global__ __launch_bounds__(kEpilogueThreads) void svd_epoch_epilogue_kernel(
     int32_t* __restrict__ Q, const int4* __restrict__ meta, int32_t* __restrict__ qlast, int32_t n_live,

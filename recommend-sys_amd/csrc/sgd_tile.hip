@@ -460,12 +460,33 @@ __global__ __launch_bounds__(NW * 64) void svd_epoch_tile_kernel(
         __syncthreads();  // the next tile's staging overwrites the LDS
         if constexpr (TIMED) tm_tail += clk() - tm_c;
     }
-    if (lane == 0) gb_partial[static_cast<int64_t>(blockIdx.x) * NW + w] = contrib;
-    if (lane == 0 && gb_smooth) {
-        gb_smooth[2 * (static_cast<int64_t>(blockIdx.x) * NW + w)] = s_num;
-        gb_smooth[2 * (static_cast<int64_t>(blockIdx.x) * NW + w) + 1] = s_den;
+    // one partial per workgroup, its waves' sums in wave order: the epilogue then folds grid values instead of
+    // grid x waves (round 6: its loads were the epilogue's time, ~7 us of an ML-1M step)
+    __shared__ double s_part[3][NW];
+    __shared__ float s_loss[NW];
+    if (lane == 0) {
+        s_part[0][w] = contrib;
+        s_part[1][w] = s_num;
+        s_part[2][w] = s_den;
+        s_loss[w] = se;
     }
-    if (lane == 0 && loss_partial) loss_partial[static_cast<int64_t>(blockIdx.x) * NW + w] = se;
+    __syncthreads();
+    if (tid == 0) {
+        double c = 0.0, sn = 0.0, sd = 0.0;
+        float sl = 0.f;
+        for (int x = 0; x < NW; ++x) {
+            c += s_part[0][x];
+            sn += s_part[1][x];
+            sd += s_part[2][x];
+            sl += s_loss[x];
+        }
+        gb_partial[blockIdx.x] = c;
+        if (gb_smooth) {
+            gb_smooth[2 * static_cast<int64_t>(blockIdx.x)] = sn;
+            gb_smooth[2 * static_cast<int64_t>(blockIdx.x) + 1] = sd;
+        }
+        if (loss_partial) loss_partial[blockIdx.x] = sl;
+    }
     if constexpr (SPAN) {
         const int64_t t_end = clk();
         if (lane == 0) {
@@ -1172,7 +1193,7 @@ void build_tile_blocks(const rs_svd_plan* pl, int32_t grid0, bool want_pos, Tile
 
 }  // namespace
 
-int32_t tile_partials(const rs_svd_plan* pl) { return std::max(1, pl->tile_grid) * pl->tile_waves; }
+int32_t tile_partials(const rs_svd_plan* pl) { return std::max(1, pl->tile_grid); }  // one per workgroup
 
 int32_t tile_cap_in_use(const rs_svd_plan* pl) {
     ensure_host_csr(const_cast<rs_svd_plan*>(pl));
@@ -1417,7 +1438,7 @@ int32_t tile_launch_range(rs_svd_plan* pl, float lr, float reg, hipStream_t s, f
     if (!pl->tiles_built) tile_build(pl);
     tile_partials_fit(pl, s);
     const int32_t grid = std::max(1, std::min(pl->tile_grid, t1 - t0));
-    const int32_t parts = grid * pl->tile_waves;
+    const int32_t parts = grid;  // one partial per workgroup
     if (t1 <= t0) {
         RS_HIP(hipMemsetAsync(pl->partial.p, 0, static_cast<size_t>(parts) * sizeof(double), s));
         return parts;
