@@ -1202,7 +1202,8 @@ namespace {
 // and the ranks compare them: RCCL max and min all-reduces of the six sums (they agree iff max == min), or the
 // in-process group's host barrier.  A mismatch -- a transfer or a collective that delivered different bytes to
 // different ranks -- is RS_ERR_NUMERIC on every rank (rs_svd_fit_multi refits).  One pass over P and Q per call
-// (configs[4] at 8 ranks: 14 GB, under 2 ms), one 96-byte readback.
+// (configs[4] at 8 ranks: three passes of 2.1 ms, 6.4 ms per call -- 0.3 ms per epoch of a 20-epoch Fit;
+// profiles/r06/config4_qdelta_8shards_kernel_stats.csv), one 96-byte readback.
 void check_replicas(rs_svd_plan* pl, hipStream_t s) {
     ShardComm& c = *pl->shard;
     if (c.nranks <= 1 || !(c.nccl || c.local)) return;
