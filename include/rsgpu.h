@@ -495,8 +495,10 @@ int rs_svd_plan_set_damp_concurrency(rs_svd_plan* plan, float kconc);
 /* Cold runs of the tile schedule (round 6): an item with so few ratings that on average fewer than
  * `runs_in_flight` of its runs are in flight at once (ratings x workgroups x waves / nnz) ends each run with plain
  * write-through stores of its new row instead of memory-side atomic adds -- a concurrent run of the same item
- * then loses its update, which happens with about that probability.  0 turns it off.  With one wave per
- * workgroup a store equals the atomic (no run overlaps).  Rebuilds the schedule. */
+ * then loses its update, which happens with about that probability.  0 turns it off; default 0.05.  Runs are
+ * marked, and the kernel variant with the stores launched, only where the mean item is cold (the threshold degree
+ * reaches nnz / n_items: configs[4], not ML-1M -- the variant's extra exit costs a set of few cold runs more than the
+ * stores save).  With one wave per workgroup a store equals the atomic (no run overlaps).  Rebuilds the schedule. */
 int rs_svd_plan_set_cold_store(rs_svd_plan* plan, double runs_in_flight);
 /* How a single-GPU tile epoch folds GlobalBias (svd.go:104-106's chain, run per (tile, wave) stream from the epoch's
  * start value): RS_GB_FOLD_SMOOTH (default since round 6) -- the streams' chains composed with their rates at
